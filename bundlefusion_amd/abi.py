@@ -1,0 +1,138 @@
+"""ctypes mirror of include/bf/types.h and include/bf/bf.h.
+
+This is binding plumbing for tests and bench.py: the product is the C ABI in
+libbf_hip.so. Struct layouts are asserted against the sizes the C header
+static_asserts (HashEntry 32 B, Voxel 12 B, HashParams 224 B, ...).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_HERE, "libbf_hip.so")
+HEADER_PATH = os.path.join(REPO, "include", "bf", "bf.h")
+
+FREE_ENTRY = -2
+LOCK_ENTRY = -1
+SDF_BLOCK_SIZE = 8
+HASH_BUCKET_SIZE = 4
+
+
+class BFMat4(C.Structure):
+    _fields_ = [("m", C.c_float * 16)]
+
+
+class BFFloat3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class BFInt3(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("z", C.c_int32)]
+
+
+class BFHashParams(C.Structure):
+    _fields_ = [
+        ("rigidTransform", BFMat4),
+        ("rigidTransformInverse", BFMat4),
+        ("hashNumBuckets", C.c_uint32),
+        ("hashBucketSize", C.c_uint32),
+        ("hashMaxCollisionLinkedListSize", C.c_uint32),
+        ("numSDFBlocks", C.c_uint32),
+        ("SDFBlockSize", C.c_int32),
+        ("virtualVoxelSize", C.c_float),
+        ("numOccupiedBlocks", C.c_uint32),
+        ("maxIntegrationDistance", C.c_float),
+        ("truncScale", C.c_float),
+        ("truncation", C.c_float),
+        ("integrationWeightSample", C.c_uint32),
+        ("integrationWeightMax", C.c_uint32),
+        ("streamingVoxelExtents", BFFloat3),
+        ("streamingGridDimensions", BFInt3),
+        ("streamingMinGridPos", BFInt3),
+        ("streamingInitialChunkListSize", C.c_uint32),
+        ("dummy", C.c_uint32 * 2),
+    ]
+
+
+class BFDepthCameraParams(C.Structure):
+    _fields_ = [
+        ("fx", C.c_float), ("fy", C.c_float), ("mx", C.c_float), ("my", C.c_float),
+        ("imageWidth", C.c_uint32), ("imageHeight", C.c_uint32),
+        ("sensorDepthWorldMin", C.c_float), ("sensorDepthWorldMax", C.c_float),
+    ]
+
+
+class BFRayCastParams(C.Structure):
+    _fields_ = [
+        ("viewMatrix", BFMat4), ("viewMatrixInverse", BFMat4),
+        ("mx", C.c_float), ("my", C.c_float), ("fx", C.c_float), ("fy", C.c_float),
+        ("width", C.c_uint32), ("height", C.c_uint32),
+        ("numOccupiedSDFBlocks", C.c_uint32), ("maxNumVertices", C.c_uint32), ("splatMinimum", C.c_int32),
+        ("minDepth", C.c_float), ("maxDepth", C.c_float), ("rayIncrement", C.c_float),
+        ("thresSampleDist", C.c_float), ("thresDist", C.c_float),
+        ("useGradients", C.c_uint8), ("pad_", C.c_uint8 * 3), ("dummy0", C.c_uint32),
+    ]
+
+
+class BFTsdfStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",
+        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps")]
+
+
+class BFSceneOptions(C.Structure):
+    _fields_ = [("candidateCapacity", C.c_uint32), ("shardCount", C.c_uint32),
+                ("shardIndex", C.c_uint32), ("shardChunk", C.c_float)]
+
+
+class BFSynthScene(C.Structure):
+    _fields_ = [("seed", C.c_uint32), ("numPrimitives", C.c_uint32),
+                ("roomMin", C.c_float * 3), ("roomMax", C.c_float * 3),
+                ("prims", (C.c_float * 8) * 64)]
+
+
+# numpy views of the POD arrays
+HASH_ENTRY_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("z", "<i4"), ("ptr", "<i4"),
+                             ("offset", "<u4"), ("pad", "<i4", (3,))])
+VOXEL_DTYPE = np.dtype([("sdf", "<f4"), ("weight", "<f4"), ("color", "u1", (4,))])
+ENTRYJ_DTYPE = np.dtype([("i", "<u4"), ("j", "<u4"), ("pos_i", "<f4", (3,)), ("pos_j", "<f4", (3,))])
+
+assert C.sizeof(BFMat4) == 64
+assert C.sizeof(BFHashParams) == 224, C.sizeof(BFHashParams)
+assert C.sizeof(BFDepthCameraParams) == 32
+assert C.sizeof(BFRayCastParams) == 192, C.sizeof(BFRayCastParams)
+assert BFRayCastParams.useGradients.offset == 184
+assert HASH_ENTRY_DTYPE.itemsize == 32 and VOXEL_DTYPE.itemsize == 12 and ENTRYJ_DTYPE.itemsize == 32
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Every `bf_*` function declared in include/bf/bf.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(?:int|const char\s*\*)\s+(bf_[a-z0-9_]+)\s*\(", text)))
+
+
+def mat(T) -> C.Array:
+    a = np.ascontiguousarray(np.asarray(T, dtype=np.float32).reshape(16))
+    return (C.c_float * 16)(*a.tolist())
+
+
+def f32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def u8p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def u32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def vp(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)

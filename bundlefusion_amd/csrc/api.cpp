@@ -1,0 +1,332 @@
+// api.cpp — the C ABI (include/bf/bf.h). Catches every C++ exception at the boundary and
+// turns it into a status code + bf_last_error() message.
+#include "../../include/bf/bf.h"
+#include "bf_runtime.h"
+#include "synth.h"
+#include "tsdf.h"
+
+#include <cstring>
+#include <string>
+
+namespace bf {
+
+static thread_local std::string g_lastError;
+void set_last_error(const std::string& msg) { g_lastError = msg; }
+
+void synth_render_device(const BFSynthScene& sc, const BFMat4& T, const BFDepthCameraParams& cam, uint32_t noiseSeed,
+                         uint32_t frame, float* depth, uint8_t* color, hipStream_t stream);
+void synth_render_host(const BFSynthScene& sc, const BFMat4& T, const BFDepthCameraParams& cam, uint32_t noiseSeed,
+                       uint32_t frame, float* depth, uint8_t* color);
+void synth_scene_default(uint32_t seed, BFSynthScene* out);
+
+// General cofactor inverse, cuda_SimpleMatrixUtil.h:980-1090 (host side of setLastRigidTransform,
+// CUDASceneRepHashSDF.h:128-134).
+BFMat4 mat4_inverse(const BFMat4& M) {
+    const float* e = M.m;
+    float inv[16];
+    inv[0] = e[5] * e[10] * e[15] - e[5] * e[11] * e[14] - e[9] * e[6] * e[15] + e[9] * e[7] * e[14] + e[13] * e[6] * e[11] - e[13] * e[7] * e[10];
+    inv[4] = -e[4] * e[10] * e[15] + e[4] * e[11] * e[14] + e[8] * e[6] * e[15] - e[8] * e[7] * e[14] - e[12] * e[6] * e[11] + e[12] * e[7] * e[10];
+    inv[8] = e[4] * e[9] * e[15] - e[4] * e[11] * e[13] - e[8] * e[5] * e[15] + e[8] * e[7] * e[13] + e[12] * e[5] * e[11] - e[12] * e[7] * e[9];
+    inv[12] = -e[4] * e[9] * e[14] + e[4] * e[10] * e[13] + e[8] * e[5] * e[14] - e[8] * e[6] * e[13] - e[12] * e[5] * e[10] + e[12] * e[6] * e[9];
+    inv[1] = -e[1] * e[10] * e[15] + e[1] * e[11] * e[14] + e[9] * e[2] * e[15] - e[9] * e[3] * e[14] - e[13] * e[2] * e[11] + e[13] * e[3] * e[10];
+    inv[5] = e[0] * e[10] * e[15] - e[0] * e[11] * e[14] - e[8] * e[2] * e[15] + e[8] * e[3] * e[14] + e[12] * e[2] * e[11] - e[12] * e[3] * e[10];
+    inv[9] = -e[0] * e[9] * e[15] + e[0] * e[11] * e[13] + e[8] * e[1] * e[15] - e[8] * e[3] * e[13] - e[12] * e[1] * e[11] + e[12] * e[3] * e[9];
+    inv[13] = e[0] * e[9] * e[14] - e[0] * e[10] * e[13] - e[8] * e[1] * e[14] + e[8] * e[2] * e[13] + e[12] * e[1] * e[10] - e[12] * e[2] * e[9];
+    inv[2] = e[1] * e[6] * e[15] - e[1] * e[7] * e[14] - e[5] * e[2] * e[15] + e[5] * e[3] * e[14] + e[13] * e[2] * e[7] - e[13] * e[3] * e[6];
+    inv[6] = -e[0] * e[6] * e[15] + e[0] * e[7] * e[14] + e[4] * e[2] * e[15] - e[4] * e[3] * e[14] - e[12] * e[2] * e[7] + e[12] * e[3] * e[6];
+    inv[10] = e[0] * e[5] * e[15] - e[0] * e[7] * e[13] - e[4] * e[1] * e[15] + e[4] * e[3] * e[13] + e[12] * e[1] * e[7] - e[12] * e[3] * e[5];
+    inv[14] = -e[0] * e[5] * e[14] + e[0] * e[6] * e[13] + e[4] * e[1] * e[14] - e[4] * e[2] * e[13] - e[12] * e[1] * e[6] + e[12] * e[2] * e[5];
+    inv[3] = -e[1] * e[6] * e[11] + e[1] * e[7] * e[10] + e[5] * e[2] * e[11] - e[5] * e[3] * e[10] - e[9] * e[2] * e[7] + e[9] * e[3] * e[6];
+    inv[7] = e[0] * e[6] * e[11] - e[0] * e[7] * e[10] - e[4] * e[2] * e[11] + e[4] * e[3] * e[10] + e[8] * e[2] * e[7] - e[8] * e[3] * e[6];
+    inv[11] = -e[0] * e[5] * e[11] + e[0] * e[7] * e[9] + e[4] * e[1] * e[11] - e[4] * e[3] * e[9] - e[8] * e[1] * e[7] + e[8] * e[3] * e[5];
+    inv[15] = e[0] * e[5] * e[10] - e[0] * e[6] * e[9] - e[4] * e[1] * e[10] + e[4] * e[2] * e[9] + e[8] * e[1] * e[6] - e[8] * e[2] * e[5];
+    const float det = e[0] * inv[0] + e[1] * inv[4] + e[2] * inv[8] + e[3] * inv[12];
+    const float detr = 1.0f / det;
+    BFMat4 r;
+    for (int i = 0; i < 16; i++) r.m[i] = inv[i] * detr;
+    return r;
+}
+
+// float4x4 * float4x4 (cuda_SimpleMatrixUtil.h operator*): row i . column j, k = 0..3
+BFMat4 mat4_mul(const BFMat4& a, const BFMat4& b) {
+    BFMat4 r;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            float s = 0.0f;
+            for (int k = 0; k < 4; k++) s += a.m[i * 4 + k] * b.m[k * 4 + j];
+            r.m[i * 4 + j] = s;
+        }
+    return r;
+}
+
+static BFMat4 to_mat(const float* T) {
+    BFMat4 m;
+    std::memcpy(m.m, T, 64);
+    return m;
+}
+
+}  // namespace bf
+
+using namespace bf;
+
+#define BF_TRY try {
+#define BF_CATCH                                                      \
+    return 0;                                                         \
+    }                                                                 \
+    catch (const bf::Error& e) {                                      \
+        set_last_error(e.what());                                     \
+        return e.code;                                                \
+    }                                                                 \
+    catch (const std::bad_alloc&) {                                   \
+        set_last_error("host allocation failed");                    \
+        return BF_ERR_CAPACITY;                                       \
+    }                                                                 \
+    catch (const std::exception& e) {                                 \
+        set_last_error(e.what());                                     \
+        return BF_ERR_INTERNAL;                                       \
+    }
+
+struct bf_scene {
+    hipStream_t stream = nullptr;
+    Scene* scene = nullptr;
+};
+
+struct bf_timer {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+extern "C" {
+
+int bf_abi_version(void) { return BF_ABI_VERSION; }
+const char* bf_last_error(void) { return g_lastError.c_str(); }
+
+int bf_device_count(int* count) {
+    BF_TRY
+    BF_HIP(hipGetDeviceCount(count));
+    BF_CATCH
+}
+int bf_set_device(int device) {
+    BF_TRY
+    BF_HIP(hipSetDevice(device));
+    BF_CATCH
+}
+int bf_device_synchronize(void) {
+    BF_TRY
+    BF_HIP(hipDeviceSynchronize());
+    BF_CATCH
+}
+int bf_malloc(void** dptr, size_t bytes) {
+    BF_TRY
+    BF_REQUIRE(dptr != nullptr, BF_ERR_ARG, "dptr");
+    BF_HIP(hipMalloc(dptr, bytes ? bytes : 1));
+    BF_CATCH
+}
+int bf_free(void* dptr) {
+    BF_TRY
+    if (dptr) BF_HIP(hipFree(dptr));
+    BF_CATCH
+}
+int bf_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+    BF_TRY
+    BF_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    BF_CATCH
+}
+int bf_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+    BF_TRY
+    BF_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    BF_CATCH
+}
+int bf_memcpy_d2d(void* dst, const void* src, size_t bytes) {
+    BF_TRY
+    BF_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+    BF_CATCH
+}
+int bf_memset(void* dptr, int value, size_t bytes) {
+    BF_TRY
+    BF_HIP(hipMemset(dptr, value, bytes));
+    BF_CATCH
+}
+int bf_timer_create(bf_timer** out) {
+    BF_TRY
+    bf_timer* t = new bf_timer();
+    BF_HIP(hipEventCreate(&t->a));
+    BF_HIP(hipEventCreate(&t->b));
+    *out = t;
+    BF_CATCH
+}
+int bf_timer_destroy(bf_timer* t) {
+    BF_TRY
+    if (t) {
+        if (t->a) (void)hipEventDestroy(t->a);
+        if (t->b) (void)hipEventDestroy(t->b);
+        delete t;
+    }
+    BF_CATCH
+}
+
+// ---- scene ------------------------------------------------------------------------------
+int bf_scene_create(const BFHashParams* params, const BFSceneOptions* opts, bf_scene** out) {
+    BF_TRY
+    BF_REQUIRE(params && out, BF_ERR_ARG, "null argument");
+    SceneConfig cfg{};
+    cfg.hp = *params;
+    if (opts) {
+        cfg.candCapacity = opts->candidateCapacity;
+        cfg.shardCount = opts->shardCount;
+        cfg.shardIndex = opts->shardIndex;
+        cfg.shardChunk = opts->shardChunk;
+    }
+    bf_scene* s = new bf_scene();
+    try {
+        BF_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        s->scene = new Scene(cfg, s->stream);
+    } catch (...) {
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+        delete s;
+        throw;
+    }
+    *out = s;
+    BF_CATCH
+}
+int bf_scene_destroy(bf_scene* s) {
+    BF_TRY
+    if (s) {
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        delete s->scene;
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+        delete s;
+    }
+    BF_CATCH
+}
+int bf_scene_reset(bf_scene* s) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null scene");
+    s->scene->reset();
+    BF_CATCH
+}
+int bf_scene_integrate(bf_scene* s, const float T[16], const float* depth, const uint8_t* color,
+                       const BFDepthCameraParams* cam, const uint32_t* bitMask) {
+    BF_TRY
+    BF_REQUIRE(s && T && cam, BF_ERR_ARG, "null argument");
+    s->scene->integrate(to_mat(T), depth, color, *cam, false, bitMask);
+    BF_CATCH
+}
+int bf_scene_deintegrate(bf_scene* s, const float T[16], const float* depth, const uint8_t* color,
+                         const BFDepthCameraParams* cam, const uint32_t* bitMask) {
+    BF_TRY
+    BF_REQUIRE(s && T && cam, BF_ERR_ARG, "null argument");
+    s->scene->integrate(to_mat(T), depth, color, *cam, true, bitMask);
+    BF_CATCH
+}
+int bf_scene_garbage_collect(bf_scene* s) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null scene");
+    s->scene->garbageCollect();
+    BF_CATCH
+}
+int bf_scene_compactify(bf_scene* s, const float T[16], const BFDepthCameraParams* cam, uint32_t* nVisible) {
+    BF_TRY
+    BF_REQUIRE(s && T && cam, BF_ERR_ARG, "null argument");
+    s->scene->compactify(to_mat(T), *cam);
+    if (nVisible) *nVisible = s->scene->numVisible();
+    BF_CATCH
+}
+int bf_scene_heap_free_count(bf_scene* s, uint32_t* count) {
+    BF_TRY
+    BF_REQUIRE(s && count, BF_ERR_ARG, "null argument");
+    *count = s->scene->heapFreeCount();
+    BF_CATCH
+}
+int bf_scene_num_visible(bf_scene* s, uint32_t* count) {
+    BF_TRY
+    BF_REQUIRE(s && count, BF_ERR_ARG, "null argument");
+    *count = s->scene->numVisible();
+    BF_CATCH
+}
+int bf_scene_error_flags(bf_scene* s, uint32_t* flags) {
+    BF_TRY
+    BF_REQUIRE(s && flags, BF_ERR_ARG, "null argument");
+    *flags = s->scene->errorFlags();
+    BF_CATCH
+}
+int bf_scene_get_stats(bf_scene* s, BFTsdfStats* out) {
+    BF_TRY
+    BF_REQUIRE(s && out, BF_ERR_ARG, "null argument");
+    *out = s->scene->stats();
+    BF_CATCH
+}
+int bf_scene_reset_stats(bf_scene* s) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null scene");
+    s->scene->resetStats();
+    BF_CATCH
+}
+int bf_scene_export(bf_scene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null scene");
+    s->scene->exportState(hash, heap, heapCounter, voxels);
+    BF_CATCH
+}
+int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(s && out4 && n, BF_ERR_ARG, "null argument");
+    *n = s->scene->exportVisible(reinterpret_cast<int4*>(out4), cap);
+    BF_CATCH
+}
+int bf_scene_synchronize(bf_scene* s) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null scene");
+    BF_HIP(hipStreamSynchronize(s->stream));
+    BF_CATCH
+}
+int bf_scene_device_bytes(bf_scene* s, uint64_t* bytes) {
+    BF_TRY
+    BF_REQUIRE(s && bytes, BF_ERR_ARG, "null argument");
+    *bytes = s->scene->deviceBytes();
+    BF_CATCH
+}
+int bf_scene_timer_start(bf_scene* s, bf_timer* t) {
+    BF_TRY
+    BF_REQUIRE(s && t, BF_ERR_ARG, "null argument");
+    BF_HIP(hipEventRecord(t->a, s->stream));
+    BF_CATCH
+}
+int bf_scene_timer_stop(bf_scene* s, bf_timer* t, float* ms) {
+    BF_TRY
+    BF_REQUIRE(s && t && ms, BF_ERR_ARG, "null argument");
+    BF_HIP(hipEventRecord(t->b, s->stream));
+    BF_HIP(hipEventSynchronize(t->b));
+    BF_HIP(hipEventElapsedTime(ms, t->a, t->b));
+    BF_CATCH
+}
+
+// ---- synthetic stream ---------------------------------------------------------------------
+int bf_synth_scene_default(uint32_t seed, BFSynthScene* out) {
+    BF_TRY
+    BF_REQUIRE(out, BF_ERR_ARG, "null argument");
+    synth_scene_default(seed, out);
+    BF_CATCH
+}
+int bf_synth_pose(uint32_t frame, float T[16]) {
+    BF_TRY
+    BF_REQUIRE(T, BF_ERR_ARG, "null argument");
+    synth_pose(frame, T);
+    BF_CATCH
+}
+int bf_synth_render(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam, uint32_t noiseSeed,
+                    uint32_t frame, float* d_depth, uint8_t* d_color) {
+    BF_TRY
+    BF_REQUIRE(scene && T && cam && d_depth, BF_ERR_ARG, "null argument");
+    synth_render_device(*scene, to_mat(T), *cam, noiseSeed, frame, d_depth, d_color, nullptr);
+    BF_HIP(hipStreamSynchronize(nullptr));
+    BF_CATCH
+}
+int bf_synth_render_host(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam, uint32_t noiseSeed,
+                         uint32_t frame, float* depth, uint8_t* color) {
+    BF_TRY
+    BF_REQUIRE(scene && T && cam && depth, BF_ERR_ARG, "null argument");
+    synth_render_host(*scene, to_mat(T), *cam, noiseSeed, frame, depth, color);
+    BF_CATCH
+}
+
+}  // extern "C"

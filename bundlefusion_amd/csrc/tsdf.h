@@ -1,0 +1,103 @@
+// tsdf.h — MI355X voxel-hash TSDF scene (replaces CUDASceneRepHashSDF,
+// Source/DepthSensing/CUDASceneRepHashSDF.h:29-423).
+//
+// Device layout (one allocation per array, all resident in HBM):
+//   hash      BFHashEntry[E]      reference layout; E = 4 * numBuckets
+//   heap      uint32[B]           free-block stack, reference semantics (VoxelUtilHashSDF.h:535-546)
+//   voxels    BFVoxel[B * 512]    12-B AoS voxels, one 6 KiB run per block
+//   blockPos  int4[B]             per heap block: {x, y, z, allocated} — lets compactify stream
+//                                 only the allocated pool prefix instead of the whole hash table
+//   visible   int4[B]             compacted frustum list {x, y, z, ptr} (16 B vs 32 B HashEntry)
+//   ctrl      uint32[16]          device-resident counters (heap counter, visible count, ...)
+//   cand/candSet/candSlot/ovf     alloc scratch (per-op candidate list, global dedup set)
+//   victims                       GC scratch
+// No host round trip inside integrate / de-integrate / GC: every count a kernel needs is
+// read from `ctrl` on the device.
+#pragma once
+#include "bf_math.h"
+#include "bf_runtime.h"
+
+namespace bf {
+
+enum Ctrl {
+    C_HEAP = 0,        // heap counter (points at the last free block)
+    C_VISIBLE = 1,     // numOccupiedBlocks of the last compactify
+    C_CAND = 2,        // alloc candidates emitted
+    C_OVF = 3,         // candidates whose bucket was full (collision-list path)
+    C_HIGHWATER = 4,   // 1 + highest heap block index ever handed out
+    C_GC_SIMPLE = 5,   // GC victims deletable without touching a collision list
+    C_GC_LIST = 6,     // GC victims that touch a collision list (serial path)
+    C_ERR = 7,         // error bits (1: candidate buffer overflow, 2: heap exhausted, 4: dedup set full)
+    C_COUNT = 16
+};
+
+struct SceneConfig {
+    BFHashParams hp;
+    uint32_t candCapacity;   // max alloc candidates per integrate
+    uint32_t shardCount;     // >1: spatial ownership sharding across GPUs
+    uint32_t shardIndex;
+    float shardChunk;        // ownership chunk edge in metres (default 1 m, the streaming chunk)
+};
+
+class Scene {
+public:
+    Scene(const SceneConfig& cfg, hipStream_t stream);
+    ~Scene();
+
+    void reset();
+    // integrate (deint=false) / de-integrate (deint=true) one frame; depth/color are device
+    // pointers (float / uchar4 per pixel, W*H of cam). T is camera->world.
+    void integrate(const BFMat4& T, const float* depth, const uint8_t* color, const BFDepthCameraParams& cam,
+                   bool deint, const uint32_t* bitMask);
+    void garbageCollect();
+    void compactify(const BFMat4& T, const BFDepthCameraParams& cam);
+
+    // synchronous queries (tests, debug)
+    uint32_t heapFreeCount();
+    uint32_t numVisible();
+    uint32_t errorFlags();
+    BFTsdfStats stats();
+    void resetStats();
+    void exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
+    uint32_t exportVisible(int4* out, uint32_t cap);
+
+    const SceneConfig& config() const { return cfg_; }
+    hipStream_t stream() const { return stream_; }
+    void setStream(hipStream_t s) { stream_ = s; }
+    // raw device views for the raycaster / stream runner
+    const BFHashEntry* dHash() const { return hash_.p; }
+    const BFVoxel* dVoxels() const { return voxels_.p; }
+    const int4* dVisible() const { return visible_.p; }
+    const uint32_t* dCtrl() const { return ctrl_.p; }
+    uint32_t* dCtrlMut() { return ctrl_.p; }
+    BFTsdfStats* dStats() { return stats_.p; }
+    size_t deviceBytes() const;
+
+private:
+    void alloc(const float* depth, const BFDepthCameraParams& cam, const uint32_t* bitMask);
+    void beginOp();
+
+    SceneConfig cfg_;
+    hipStream_t stream_;
+    uint32_t E_, B_;
+    BFMat4 T_, Tinv_;
+
+    DevBuf<BFHashEntry> hash_;
+    DevBuf<uint32_t> heap_;
+    DevBuf<BFVoxel> voxels_;
+    DevBuf<int4> blockPos_;
+    DevBuf<int4> visible_;
+    DevBuf<uint32_t> ctrl_;
+    DevBuf<BFTsdfStats> stats_;
+    DevBuf<unsigned long long> cand_;
+    DevBuf<unsigned long long> candSet_;
+    DevBuf<int> candSlot_;
+    DevBuf<unsigned long long> ovf_;
+    DevBuf<int4> gcSimple_;
+    DevBuf<unsigned long long> gcList_;
+    DevBuf<uint32_t> blockCount_;
+    uint32_t candSetMask_;
+    int numCUs_;
+};
+
+}  // namespace bf

@@ -1,0 +1,830 @@
+// tsdf.hip — gfx950 kernels + host class for the voxel-hash TSDF scene.
+//
+// Replaces the reference's CUDASceneRepHashSDF.cu kernels (citations are to
+// /root/reference/FriedLiver/Source/DepthSensing/). Design points:
+//  * alloc is two-phase and lock-free: a per-pixel DDA emits absent, in-frustum blocks,
+//    de-duplicated per 16x16 tile in an LDS hash set and appended with wave-aggregated
+//    atomics; a per-candidate insert dedups globally (64-bit CAS set) and claims a bucket
+//    slot with a CAS on HashEntry.ptr. One pass replaces the reference's repeat-until-
+//    stable try-lock loop and its host round trips (CUDASceneRepHashSDF.h:335-348).
+//  * compactify streams the allocated prefix of a 16-B per-block position array instead of
+//    the whole 32-B-per-entry hash table, with wave ballot + popcount compaction.
+//  * integrate runs one wave per 8^3 block (8 z-slices of 64 voxels), touching a voxel's
+//    12 B only when it lies inside the truncation band.
+//  * GC reads a per-block count of voxels with (uint)weight != 0, maintained by the
+//    integrate kernel, instead of re-reading 512 voxels per block.
+#include "tsdf.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace bf {
+
+namespace {
+
+constexpr unsigned long long EMPTY_KEY = ~0ull;
+constexpr int ALLOC_TILE = 16;          // 16x16 pixels per workgroup
+constexpr int LDS_SET = 2048;           // per-tile candidate dedup set (16 KiB)
+constexpr uint32_t OVF_CAP = 1u << 16;  // collision-list inserts per op (serial path)
+constexpr uint32_t GC_LIST_CAP = 4096;  // collision-list deletes per GC pass (serial path)
+
+struct HashArgs {
+    BFHashEntry* hash;
+    uint32_t* heap;
+    BFVoxel* voxels;
+    int4* blockPos;
+    uint32_t* blockCount;
+    int4* visible;
+    uint32_t* ctrl;
+    BFTsdfStats* stats;
+    uint32_t numBuckets, numEntries, numBlocks, maxList;
+    float voxelSize, truncation, truncScale, maxIntegrationDistance, weightMax;
+    uint32_t shardCount, shardIndex;
+    float shardChunk;
+    // reference streaming bitmask (isSDFBlockStreamedOut, CUDASceneRepHashSDF.cu:152-163)
+    const uint32_t* bitMask;
+    BFFloat3 streamExtents;
+    BFInt3 streamGridDims;
+    BFInt3 streamMinGridPos;
+};
+
+__device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    unsigned l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+__device__ __forceinline__ void load_entry(const BFHashEntry* h, uint32_t i, int4& a, int4& b) {
+    const int4* p = reinterpret_cast<const int4*>(h + i);
+    a = p[0];
+    b = p[1];
+}
+
+// getHashEntryForSDFBlockPos, VoxelUtilHashSDF.h:440-485 -> ptr or FREE
+__device__ int lookup_ptr(const HashArgs& A, int x, int y, int z) {
+    const uint32_t h = hash_bucket(x, y, z, A.numBuckets);
+    const uint32_t hp = h * BF_HASH_BUCKET_SIZE;
+#pragma unroll
+    for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+        int4 a, b;
+        load_entry(A.hash, hp + j, a, b);
+        if (a.x == x && a.y == y && a.z == z && a.w != BF_FREE_ENTRY) return a.w;
+    }
+    const uint32_t last = hp + BF_HASH_BUCKET_SIZE - 1;
+    uint32_t i = last;
+    for (uint32_t it = 0; it < A.maxList; it++) {
+        int4 a, b;
+        load_entry(A.hash, i, a, b);
+        if (a.x == x && a.y == y && a.z == z && a.w != BF_FREE_ENTRY) return a.w;
+        if (b.x == 0) break;
+        i = (last + (uint32_t)b.x) % A.numEntries;
+    }
+    return BF_FREE_ENTRY;
+}
+
+// Spatial ownership for multi-GPU sharding: the chunk of the block's corner (worldToChunks
+// rounding, CUDASceneRepHashSDF.cu:136-150) hashed onto the shard count.
+__device__ __forceinline__ bool owned(const HashArgs& A, int bx, int by, int bz) {
+    if (A.shardCount <= 1) return true;
+    f3 w = block_to_world(bx, by, bz, A.voxelSize) / A.shardChunk;
+    int cx = f2i(w.x + (float)sgn(w.x) * 0.5f), cy = f2i(w.y + (float)sgn(w.y) * 0.5f), cz = f2i(w.z + (float)sgn(w.z) * 0.5f);
+    return hash_bucket(cx, cy, cz, A.shardCount) == A.shardIndex;
+}
+
+// isSDFBlockStreamedOut, CUDASceneRepHashSDF.cu:152-163
+__device__ __forceinline__ bool streamed_out(const HashArgs& A, int bx, int by, int bz) {
+    if (!A.bitMask) return false;
+    f3 w = block_to_world(bx, by, bz, A.voxelSize);
+    f3 p = mk3(w.x / A.streamExtents.x, w.y / A.streamExtents.y, w.z / A.streamExtents.z);
+    int cx = f2i(p.x + (float)sgn(p.x) * 0.5f) - A.streamMinGridPos.x;
+    int cy = f2i(p.y + (float)sgn(p.y) * 0.5f) - A.streamMinGridPos.y;
+    int cz = f2i(p.z + (float)sgn(p.z) * 0.5f) - A.streamMinGridPos.z;
+    uint32_t index = (uint32_t)(cz * A.streamGridDims.x * A.streamGridDims.y + cy * A.streamGridDims.x + cx);
+    return (A.bitMask[index / 32] & (1u << (index % 32))) != 0;
+}
+
+__device__ __forceinline__ uint32_t mix_hash(unsigned long long k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
+
+// ------------------------------------------------------------------------------------
+__global__ void k_reset_hash(BFHashEntry* hash, uint32_t E) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
+        int4* p = reinterpret_cast<int4*>(hash + i);
+        p[0] = make_int4(0, 0, 0, BF_FREE_ENTRY);
+        p[1] = make_int4(0, 0, 0, 0);
+    }
+}
+
+// resetHeapKernel, CUDASceneRepHashSDF.cu:27-45 (voxels are cleared by a memset)
+__global__ void k_reset_heap(uint32_t* heap, int4* blockPos, uint32_t* blockCount, uint32_t B, uint32_t* ctrl) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) {
+        heap[i] = B - i - 1;
+        blockPos[i] = make_int4(0, 0, 0, 0);
+        blockCount[i] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < C_COUNT) ctrl[threadIdx.x] = (threadIdx.x == C_HEAP) ? B - 1 : 0;
+}
+
+// Per-op counter reset (replaces the reference's memset + D2H of d_hashCompactifiedCounter).
+__global__ void k_begin_op(uint32_t* ctrl, BFTsdfStats* stats) {
+    if (threadIdx.x == 0) {
+        ctrl[C_VISIBLE] = 0;
+        ctrl[C_CAND] = 0;
+        ctrl[C_OVF] = 0;
+        stats->integrateOps++;
+    }
+}
+
+// allocKernel, CUDASceneRepHashSDF.cu:165-251: per-pixel DDA over 8^3-block cells. Emits the
+// absent, in-frustum, owned blocks (deduplicated per tile in LDS) into `cand`.
+__global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* __restrict__ depthImg,
+                                                       BFDepthCameraParams cam, BFMat4 T, BFMat4 Tinv,
+                                                       unsigned long long* __restrict__ cand, uint32_t candCap) {
+    __shared__ unsigned long long set[LDS_SET];
+    for (int k = threadIdx.x; k < LDS_SET; k += blockDim.x) set[k] = EMPTY_KEY;
+    __syncthreads();
+
+    const uint32_t x = blockIdx.x * ALLOC_TILE + (threadIdx.x % ALLOC_TILE);
+    const uint32_t y = blockIdx.y * ALLOC_TILE + (threadIdx.x / ALLOC_TILE);
+    bool active = x < cam.imageWidth && y < cam.imageHeight;
+    float d = active ? depthImg[y * cam.imageWidth + x] : 0.0f;
+    if (d == -INFINITY || d == 0.0f) active = false;
+    if (d >= A.maxIntegrationDistance) active = false;
+    const float t = A.truncation + A.truncScale * d;
+    const float minDepth = fminf(A.maxIntegrationDistance, d - t);
+    const float maxDepth = fminf(A.maxIntegrationDistance, d + t);
+    if (minDepth >= maxDepth) active = false;
+
+    i3 id = {0, 0, 0}, idBound = {0, 0, 0};
+    f3 tMax = mk3(0, 0, 0), tDelta = mk3(0, 0, 0), step = mk3(0, 0, 0);
+    if (active) {
+        const f3 rayMin = xform(T, depth_to_camera(cam, x, y, minDepth));
+        const f3 rayMax = xform(T, depth_to_camera(cam, x, y, maxDepth));
+        const f3 rayDir = normalize3(rayMax - rayMin);
+        id = world_to_block(rayMin, A.voxelSize);
+        const i3 idEnd = world_to_block(rayMax, A.voxelSize);
+        step = mk3((float)sgn(rayDir.x), (float)sgn(rayDir.y), (float)sgn(rayDir.z));
+        const f3 bp = block_to_world(id.x + f2i(fmaxf(0.0f, fminf(step.x, 1.0f))), id.y + f2i(fmaxf(0.0f, fminf(step.y, 1.0f))),
+                                     id.z + f2i(fmaxf(0.0f, fminf(step.z, 1.0f))), A.voxelSize) -
+                      mk3(1.0f, 1.0f, 1.0f) * (0.5f * A.voxelSize);
+        tMax = (bp - rayMin) / rayDir;
+        tDelta = (step * (float)BF_SDF_BLOCK_SIZE * A.voxelSize) / rayDir;
+        idBound.x = f2i((float)idEnd.x + step.x);
+        idBound.y = f2i((float)idEnd.y + step.y);
+        idBound.z = f2i((float)idEnd.z + step.z);
+        if (rayDir.x == 0.0f) { tMax.x = INFINITY; tDelta.x = INFINITY; }
+        if (bp.x - rayMin.x == 0.0f) { tMax.x = INFINITY; tDelta.x = INFINITY; }
+        if (rayDir.y == 0.0f) { tMax.y = INFINITY; tDelta.y = INFINITY; }
+        if (bp.y - rayMin.y == 0.0f) { tMax.y = INFINITY; tDelta.y = INFINITY; }
+        if (rayDir.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
+        if (bp.z - rayMin.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
+    }
+
+    unsigned long long emitted = 0;
+    for (uint32_t iter = 0; iter < 1024 && active; iter++) {
+        bool want = false;
+        unsigned long long key = 0;
+        if (block_in_frustum(cam, Tinv, id.x, id.y, id.z, A.voxelSize) && owned(A, id.x, id.y, id.z) &&
+            !streamed_out(A, id.x, id.y, id.z)) {
+            key = block_key(id.x, id.y, id.z);
+            uint32_t h = mix_hash(key) & (LDS_SET - 1);
+            want = true;  // if the tile set is congested, emit anyway (global dedup follows)
+            for (int p = 0; p < 16; p++) {
+                unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
+                if (old == EMPTY_KEY) break;
+                if (old == key) { want = false; break; }
+                h = (h + 1) & (LDS_SET - 1);
+            }
+            if (want) want = (lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY);
+        }
+        const unsigned long long m = __ballot(want);
+        if (want) {
+            const int leader = __ffsll((long long)m) - 1;
+            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+            uint32_t base = 0;
+            if ((int)lane_id() == leader) base = atomicAdd(&A.ctrl[C_CAND], (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (base + rank < candCap) cand[base + rank] = key;
+            else atomicOr(&A.ctrl[C_ERR], 1u);
+            emitted++;
+        }
+        // traverse (CUDASceneRepHashSDF.cu:231-246)
+        if (tMax.x < tMax.y && tMax.x < tMax.z) {
+            id.x = f2i((float)id.x + step.x);
+            if (id.x == idBound.x) active = false;
+            tMax.x += tDelta.x;
+        } else if (tMax.z < tMax.y) {
+            id.z = f2i((float)id.z + step.z);
+            if (id.z == idBound.z) active = false;
+            tMax.z += tDelta.z;
+        } else {
+            id.y = f2i((float)id.y + step.y);
+            if (id.y == idBound.y) active = false;
+            tMax.y += tDelta.y;
+        }
+    }
+    // stats (one atomic per wave)
+    unsigned long long tot = emitted;
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+    if (lane_id() == 0) {
+        atomicAdd((unsigned long long*)&A.stats->candidates, tot);
+        atomicAdd((unsigned long long*)&A.stats->pixels, 64ull);
+    }
+}
+
+// allocBlock, VoxelUtilHashSDF.h:549-655 (bucket path), lock-free: global dedup, CAS on the
+// slot's ptr, wave-aggregated heap pop.
+__global__ __launch_bounds__(256) void k_alloc_insert(HashArgs A, const unsigned long long* __restrict__ cand, uint32_t candCap,
+                                                      unsigned long long* candSet, uint32_t setMask, int* candSlot,
+                                                      unsigned long long* ovf) {
+    const uint32_t n = min(A.ctrl[C_CAND], candCap);
+    const uint32_t lane = lane_id();
+    const uint32_t waveStride = gridDim.x * blockDim.x;
+    unsigned long long allocated = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += waveStride) {
+        const uint32_t i = base + lane;
+        const bool valid = i < n;
+        const unsigned long long key = valid ? cand[i] : EMPTY_KEY;
+        bool owner = false;
+        if (valid) {
+            uint32_t h = mix_hash(key) & setMask;
+            int slot = -1;
+            for (int p = 0; p < 64; p++) {
+                unsigned long long old = atomicCAS(&candSet[h], EMPTY_KEY, key);
+                if (old == EMPTY_KEY) { owner = true; slot = (int)h; break; }
+                if (old == key) break;
+                h = (h + 1) & setMask;
+            }
+            if (!owner) {
+                // duplicate, unless all probes hit other keys (congested set): flag that
+                bool dup = false;
+                uint32_t h2 = mix_hash(key) & setMask;
+                for (int p = 0; p < 64 && !dup; p++) { dup = (candSet[h2] == key); h2 = (h2 + 1) & setMask; }
+                if (!dup) atomicOr(&A.ctrl[C_ERR], 4u);
+            }
+            candSlot[i] = slot;
+        }
+        int hslot = -1;
+        i3 p = key_block(key);
+        if (owner) {
+            const uint32_t b = hash_bucket(p.x, p.y, p.z, A.numBuckets);
+            for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+                int* ptrp = &A.hash[b * BF_HASH_BUCKET_SIZE + j].ptr;
+                if (atomicCAS(ptrp, BF_FREE_ENTRY, BF_LOCK_ENTRY) == BF_FREE_ENTRY) { hslot = (int)(b * BF_HASH_BUCKET_SIZE + j); break; }
+            }
+            if (hslot < 0) {
+                uint32_t o = atomicAdd(&A.ctrl[C_OVF], 1u);
+                if (o < OVF_CAP) ovf[o] = key;
+                else atomicOr(&A.ctrl[C_ERR], 1u);
+            }
+        }
+        // consumeHeap (VoxelUtilHashSDF.h:535-540), one atomic per wave
+        const bool need = hslot >= 0;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            uint32_t old = 0;
+            if ((int)lane == leader) {
+                old = atomicSub(&A.ctrl[C_HEAP], cnt);
+                if (old >= A.numBlocks) { atomicAdd(&A.ctrl[C_HEAP], cnt); atomicOr(&A.ctrl[C_ERR], 2u); }
+                else if (cnt > old + 1) { atomicAdd(&A.ctrl[C_HEAP], cnt - (old + 1)); atomicOr(&A.ctrl[C_ERR], 2u); }
+            }
+            old = __shfl(old, leader);
+            if (need) {
+                const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+                const bool ok = old < A.numBlocks && rank <= old;
+                int4* e = reinterpret_cast<int4*>(A.hash + hslot);
+                if (ok) {
+                    const uint32_t blk = A.heap[old - rank];
+                    e[1] = make_int4(0, 0, 0, 0);
+                    e[0] = make_int4(p.x, p.y, p.z, (int)(blk * BF_VOXELS_PER_BLOCK));
+                    A.blockPos[blk] = make_int4(p.x, p.y, p.z, 1);
+                    atomicMax(&A.ctrl[C_HIGHWATER], blk + 1);
+                    allocated++;
+                } else {
+                    e[0] = make_int4(0, 0, 0, BF_FREE_ENTRY);  // release the claimed slot
+                }
+            }
+        }
+    }
+    unsigned long long tot = allocated;
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+    if (lane == 0 && tot) atomicAdd((unsigned long long*)&A.stats->allocated, tot);
+}
+
+// allocBlock collision-list path (VoxelUtilHashSDF.h:573-654), serial: bucket-full candidates
+// are rare at the configured load factor; one lane replays the reference insert for each.
+__global__ void k_alloc_overflow(HashArgs A, const unsigned long long* ovf) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t n = min(A.ctrl[C_OVF], OVF_CAP);
+    for (uint32_t k = 0; k < n; k++) {
+        const i3 pos = key_block(ovf[k]);
+        const uint32_t h = hash_bucket(pos.x, pos.y, pos.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
+        int firstEmpty = -1;
+        bool present = false;
+        for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+            const BFHashEntry& c = A.hash[hp + j];
+            if (c.x == pos.x && c.y == pos.y && c.z == pos.z && c.ptr != BF_FREE_ENTRY) present = true;
+            if (firstEmpty == -1 && c.ptr == BF_FREE_ENTRY) firstEmpty = (int)(hp + j);
+        }
+        const uint32_t last = hp + BF_HASH_BUCKET_SIZE - 1;
+        uint32_t i = last;
+        for (uint32_t it = 0; it < A.maxList && !present; it++) {
+            const BFHashEntry& c = A.hash[i];
+            if (c.x == pos.x && c.y == pos.y && c.z == pos.z && c.ptr != BF_FREE_ENTRY) present = true;
+            if (c.offset == 0) break;
+            i = (last + c.offset) % A.numEntries;
+        }
+        if (present) continue;
+        uint32_t target = 0xFFFFFFFFu, newOffset = 0;
+        int offset = 0;
+        if (firstEmpty >= 0) {
+            target = (uint32_t)firstEmpty;
+        } else {
+            for (uint32_t it = 0; it < A.maxList;) {
+                offset++;
+                i = (last + (uint32_t)offset) % A.numEntries;
+                if ((offset % BF_HASH_BUCKET_SIZE) == 0) continue;
+                if (A.hash[i].ptr == BF_FREE_ENTRY) { target = i; break; }
+                it++;
+            }
+            if (target == 0xFFFFFFFFu) continue;  // no free slot within reach: not allocated (as in the reference)
+        }
+        const uint32_t old = A.ctrl[C_HEAP];
+        if (old >= A.numBlocks) { A.ctrl[C_ERR] |= 2u; continue; }
+        A.ctrl[C_HEAP] = old - 1;
+        const uint32_t blk = A.heap[old];
+        BFHashEntry& e = A.hash[target];
+        e.x = pos.x; e.y = pos.y; e.z = pos.z;
+        if (firstEmpty >= 0) {
+            e.offset = 0;
+        } else {
+            e.offset = A.hash[last].offset;
+            A.hash[last].offset = (uint32_t)offset;
+            newOffset = (uint32_t)offset;
+        }
+        (void)newOffset;
+        e.ptr = (int)(blk * BF_VOXELS_PER_BLOCK);
+        A.blockPos[blk] = make_int4(pos.x, pos.y, pos.z, 1);
+        if (blk + 1 > A.ctrl[C_HIGHWATER]) A.ctrl[C_HIGHWATER] = blk + 1;
+        A.stats->allocated++;
+    }
+}
+
+__global__ void k_alloc_cleanup(const uint32_t* ctrl, uint32_t candCap, const int* candSlot, unsigned long long* candSet) {
+    const uint32_t n = min(ctrl[C_CAND], candCap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int s = candSlot[i];
+        if (s >= 0) candSet[s] = EMPTY_KEY;
+    }
+}
+
+// compactifyHashAllInOneKernel, CUDASceneRepHashSDF.cu:324-366: stream the allocated pool
+// prefix [0, highWater), keep the in-frustum blocks; wave ballot + one atomic per wave.
+__global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraParams cam, BFMat4 Tinv) {
+    const uint32_t hw = A.ctrl[C_HIGHWATER];
+    const uint32_t lane = lane_id();
+    unsigned long long scanned = 0, vis = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < hw; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + lane;
+        int4 bp = make_int4(0, 0, 0, 0);
+        if (i < hw) bp = A.blockPos[i];
+        const bool alloc = bp.w != 0;
+        const bool keep = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
+        const unsigned long long m = __ballot(keep);
+        scanned += __popcll(__ballot(alloc));
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t b0 = 0;
+            if ((int)lane == leader) b0 = atomicAdd(&A.ctrl[C_VISIBLE], (uint32_t)__popcll(m));
+            b0 = __shfl(b0, leader);
+            if (keep) A.visible[b0 + __popcll(m & lanemask_lt())] = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
+            vis += __popcll(m);
+        }
+    }
+    if (lane == 0) {
+        atomicAdd((unsigned long long*)&A.stats->scanned, scanned);
+        atomicAdd((unsigned long long*)&A.stats->visible, vis);
+    }
+}
+
+// integrateDepthMapKernel<deIntegrate>, CUDASceneRepHashSDF.cu:420-521. One wave per block:
+// lane = (y, x) of a z-slice, 8 slices. Voxel bytes are touched only inside the band.
+template <bool DEINT>
+__global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __restrict__ depthImg,
+                                                   const uint32_t* __restrict__ colorImg, BFDepthCameraParams cam,
+                                                   BFMat4 Tinv) {
+    const uint32_t nvis = A.ctrl[C_VISIBLE];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int lx = lane & 7, ly = lane >> 3;
+    const uint32_t W = cam.imageWidth, H = cam.imageHeight;
+    const float wUpd = 1.0f;  // weightUpdate forced to 1 (:465-466)
+    unsigned long long updated = 0;
+    for (uint32_t b = wave; b < nvis; b += nwaves) {
+        const int4 e = A.visible[b];
+        const int bx = e.x * BF_SDF_BLOCK_SIZE, by = e.y * BF_SDF_BLOCK_SIZE, bz = e.z * BF_SDF_BLOCK_SIZE;
+        int dcount = 0;
+        uint32_t nupd = 0;
+#pragma unroll 2
+        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
+            const f3 pf = xform(Tinv, vvox_to_world(bx + lx, by + ly, bz + z, A.voxelSize));
+            const float sx = pf.x * cam.fx / pf.z + cam.mx;
+            const float sy = pf.y * cam.fy / pf.z + cam.my;
+            const uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
+            if (!(ux < W && uy < H)) continue;
+            if (!colorImg) continue;  // color stays MINF (:441-448)
+            const float depth = depthImg[uy * W + ux];
+            if (depth == -INFINITY) continue;
+            if (!(depth < A.maxIntegrationDistance)) continue;
+            float sdf = depth - pf.z;
+            const float tr = A.truncation + A.truncScale * depth;
+            if (!(fabsf(sdf) < tr)) continue;
+            sdf = (sdf >= 0.0f) ? fminf(tr, sdf) : fmaxf(-tr, sdf);
+            const uint32_t c = colorImg[uy * W + ux];
+            const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
+            BFVoxel* vp = A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane);
+            const float osdf = vp->sdf, ow = vp->weight;
+            const uint32_t oc = *reinterpret_cast<const uint32_t*>(vp->color);
+            const float oc0 = (float)(oc & 0xFF), oc1 = (float)((oc >> 8) & 0xFF), oc2 = (float)((oc >> 16) & 0xFF);
+            float r0, r1, r2, nsdf, nw;
+            uint32_t ncol;
+            if (!DEINT) {
+                if (ow == 0.0f) { r0 = cu0; r1 = cu1; r2 = cu2; }
+                else { r0 = 0.2f * cu0 + 0.8f * oc0; r1 = 0.2f * cu1 + 0.8f * oc1; r2 = 0.2f * cu2 + 0.8f * oc2; }
+                r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
+                r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
+                r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
+                ncol = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+                nsdf = (sdf * wUpd + osdf * ow) / (wUpd + ow);
+                nw = fminf(A.weightMax, wUpd + ow);
+            } else {
+                r0 = (oc0 * ow - cu0 * wUpd) / (ow - wUpd);
+                r1 = (oc1 * ow - cu1 * wUpd) / (ow - wUpd);
+                r2 = (oc2 * ow - cu2 * wUpd) / (ow - wUpd);
+                r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
+                r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
+                r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
+                ncol = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+                nsdf = (osdf * ow - sdf * wUpd) / (ow - wUpd);
+                nw = fmaxf(0.0f, ow - wUpd);
+                if (nw <= 0.001f) { nsdf = 0.0f; ncol = 0u; nw = 0.0f; }
+            }
+            vp->sdf = nsdf;
+            vp->weight = nw;
+            *reinterpret_cast<uint32_t*>(vp->color) = ncol;
+            // per-block count of voxels with (uint)weight != 0 (GC decision, :606/:625)
+            const bool was = ow >= 1.0f, now = nw >= 1.0f;
+            dcount += (int)now - (int)was;
+            nupd++;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            dcount += __shfl_xor(dcount, off);
+            nupd += __shfl_xor(nupd, off);
+        }
+        if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[(uint32_t)e.w / BF_VOXELS_PER_BLOCK], (uint32_t)dcount);
+        updated += nupd;
+    }
+    if (lane == 0 && updated) atomicAdd((unsigned long long*)&A.stats->voxelsUpdated, updated);
+}
+
+// garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
+// classification deleteHashEntryElement (VoxelUtilHashSDF.h:739-826) needs: a victim sitting in
+// its bucket with offset == 0 is deleted without the bucket lock; every other victim touches
+// a collision list and goes to the serial path.
+__global__ __launch_bounds__(256) void k_gc_identify(HashArgs A, int4* simple, unsigned long long* listV) {
+    const uint32_t nvis = A.ctrl[C_VISIBLE];
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nvis; b += gridDim.x * blockDim.x) {
+        const int4 e = A.visible[b];
+        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
+        if (A.blockCount[blk] != 0) continue;
+        const uint32_t h = hash_bucket(e.x, e.y, e.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
+        int slot = -1;
+        uint32_t off = 0;
+        for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+            int4 a, c;
+            load_entry(A.hash, hp + j, a, c);
+            if (a.x == e.x && a.y == e.y && a.z == e.z && a.w != BF_FREE_ENTRY) { slot = (int)(hp + j); off = (uint32_t)c.x; break; }
+        }
+        if (slot >= 0 && off == 0) {
+            const uint32_t k = atomicAdd(&A.ctrl[C_GC_SIMPLE], 1u);
+            simple[k] = make_int4(slot, e.w, 0, 0);
+        } else {
+            const uint32_t k = atomicAdd(&A.ctrl[C_GC_LIST], 1u);
+            if (k < GC_LIST_CAP) listV[k] = block_key(e.x, e.y, e.z);
+        }
+    }
+}
+
+// garbageCollectFreeKernel (:648-668), in-bucket deletes: one wave per victim frees the slot,
+// pushes the block onto the heap (appendHeap, VoxelUtilHashSDF.h:541-546) and zeroes its voxels.
+__global__ __launch_bounds__(256) void k_gc_free_simple(HashArgs A, const int4* simple) {
+    const uint32_t n = A.ctrl[C_GC_SIMPLE];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t k = wave; k < n; k += nwaves) {
+        const int4 v = simple[k];
+        const uint32_t blk = (uint32_t)v.y / BF_VOXELS_PER_BLOCK;
+        if (lane == 0) {
+            int4* e = reinterpret_cast<int4*>(A.hash + v.x);
+            e[0] = make_int4(0, 0, 0, BF_FREE_ENTRY);
+            e[1] = make_int4(0, 0, 0, 0);
+            const uint32_t addr = atomicAdd(&A.ctrl[C_HEAP], 1u);
+            A.heap[addr + 1] = blk;
+            A.blockPos[blk] = make_int4(0, 0, 0, 0);
+            A.blockCount[blk] = 0;
+        }
+        int4* vz = reinterpret_cast<int4*>(A.voxels + (size_t)blk * BF_VOXELS_PER_BLOCK);
+        for (int q = lane; q < BF_VOXELS_PER_BLOCK * 12 / 16; q += 64) vz[q] = make_int4(0, 0, 0, 0);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stats->gcFreed, (unsigned long long)n);
+}
+
+// deleteHashEntryElement collision-list cases, serial in ascending block-key order with the
+// reference's per-bucket try-lock semantics (one list delete per bucket per GC pass).
+__global__ void k_gc_free_list(HashArgs A, unsigned long long* listV) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t n = min(A.ctrl[C_GC_LIST], GC_LIST_CAP);
+    for (uint32_t a = 1; a < n; a++) {  // insertion sort (n is tiny)
+        unsigned long long k = listV[a];
+        int b = (int)a - 1;
+        while (b >= 0 && listV[b] > k) { listV[b + 1] = listV[b]; b--; }
+        listV[b + 1] = k;
+    }
+    uint32_t locked[64];
+    uint32_t nlocked = 0;
+    auto try_lock = [&](uint32_t h) -> bool {
+        for (uint32_t q = 0; q < nlocked; q++)
+            if (locked[q] == h) return false;
+        if (nlocked < 64) locked[nlocked++] = h;
+        return true;
+    };
+    uint32_t freed = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const i3 b = key_block(listV[k]);
+        const uint32_t h = hash_bucket(b.x, b.y, b.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
+        int delPtr = -1;
+        bool handled = false;
+        for (uint32_t j = 0; j < BF_HASH_BUCKET_SIZE && !handled; j++) {
+            const uint32_t i = hp + j;
+            BFHashEntry curr = A.hash[i];
+            if (curr.x == b.x && curr.y == b.y && curr.z == b.z && curr.ptr != BF_FREE_ENTRY) {
+                handled = true;
+                if (curr.offset != 0) {
+                    if (!try_lock(h)) break;
+                    delPtr = curr.ptr;
+                    const uint32_t nextIdx = (i + curr.offset) % A.numEntries;
+                    A.hash[i] = A.hash[nextIdx];
+                    BFHashEntry& nx = A.hash[nextIdx];
+                    nx.x = nx.y = nx.z = 0; nx.offset = 0; nx.ptr = BF_FREE_ENTRY;
+                } else {
+                    delPtr = curr.ptr;
+                    BFHashEntry& c = A.hash[i];
+                    c.x = c.y = c.z = 0; c.offset = 0; c.ptr = BF_FREE_ENTRY;
+                }
+            }
+        }
+        if (!handled) {
+            const uint32_t last = hp + BF_HASH_BUCKET_SIZE - 1;
+            uint32_t prevIdx = last;
+            uint32_t i = (last + A.hash[last].offset) % A.numEntries;
+            for (uint32_t it = 0; it < A.maxList; it++) {
+                const BFHashEntry curr = A.hash[i];
+                if (curr.x == b.x && curr.y == b.y && curr.z == b.z && curr.ptr != BF_FREE_ENTRY) {
+                    if (!try_lock(h)) break;
+                    delPtr = curr.ptr;
+                    BFHashEntry& c = A.hash[i];
+                    c.x = c.y = c.z = 0; c.offset = 0; c.ptr = BF_FREE_ENTRY;
+                    A.hash[prevIdx].offset = curr.offset;
+                    break;
+                }
+                if (curr.offset == 0) break;
+                prevIdx = i;
+                i = (last + curr.offset) % A.numEntries;
+            }
+        }
+        if (delPtr >= 0) {
+            const uint32_t blk = (uint32_t)delPtr / BF_VOXELS_PER_BLOCK;
+            const uint32_t addr = A.ctrl[C_HEAP]++;
+            A.heap[addr + 1] = blk;
+            A.blockPos[blk] = make_int4(0, 0, 0, 0);
+            A.blockCount[blk] = 0;
+            int4* vz = reinterpret_cast<int4*>(A.voxels + (size_t)blk * BF_VOXELS_PER_BLOCK);
+            for (int q = 0; q < BF_VOXELS_PER_BLOCK * 12 / 16; q++) vz[q] = make_int4(0, 0, 0, 0);
+            freed++;
+        }
+    }
+    A.stats->gcFreed += freed;
+}
+
+__global__ void k_gc_begin(uint32_t* ctrl, BFTsdfStats* stats) {
+    if (threadIdx.x == 0) {
+        stats->gcBlocks += ctrl[C_VISIBLE];
+        ctrl[C_GC_SIMPLE] = 0;
+        ctrl[C_GC_LIST] = 0;
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* heap, BFVoxel* vox, int4* bp, uint32_t* bc,
+                          int4* vis, uint32_t* ctrl, BFTsdfStats* st, const uint32_t* bitMask) {
+    HashArgs a;
+    a.hash = hash; a.heap = heap; a.voxels = vox; a.blockPos = bp; a.blockCount = bc; a.visible = vis; a.ctrl = ctrl; a.stats = st;
+    a.numBuckets = cfg.hp.hashNumBuckets;
+    a.numEntries = cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE;
+    a.numBlocks = cfg.hp.numSDFBlocks;
+    a.maxList = cfg.hp.hashMaxCollisionLinkedListSize;
+    a.voxelSize = cfg.hp.virtualVoxelSize;
+    a.truncation = cfg.hp.truncation;
+    a.truncScale = cfg.hp.truncScale;
+    a.maxIntegrationDistance = cfg.hp.maxIntegrationDistance;
+    a.weightMax = (float)cfg.hp.integrationWeightMax;
+    a.shardCount = cfg.shardCount;
+    a.shardIndex = cfg.shardIndex;
+    a.shardChunk = cfg.shardChunk > 0 ? cfg.shardChunk : 1.0f;
+    a.bitMask = bitMask;
+    a.streamExtents = cfg.hp.streamingVoxelExtents;
+    a.streamGridDims = cfg.hp.streamingGridDimensions;
+    a.streamMinGridPos = cfg.hp.streamingMinGridPos;
+    return a;
+}
+
+Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
+    BF_REQUIRE(cfg.hp.hashNumBuckets > 0 && cfg.hp.numSDFBlocks > 0, BF_ERR_ARG, "empty hash/heap");
+    BF_REQUIRE(cfg.hp.numSDFBlocks <= (1u << 22), BF_ERR_CAPACITY, "numSDFBlocks exceeds the int ptr range (4194304 blocks)");
+    BF_REQUIRE((uint64_t)cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE < (1ull << 31), BF_ERR_CAPACITY, "hash too large");
+    BF_REQUIRE(cfg.hp.virtualVoxelSize > 0, BF_ERR_ARG, "voxel size");
+    E_ = cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE;
+    B_ = cfg.hp.numSDFBlocks;
+    if (cfg_.candCapacity == 0) cfg_.candCapacity = 1u << 21;
+    if (cfg_.shardCount == 0) cfg_.shardCount = 1;
+    uint32_t setSize = 1;
+    while (setSize < 2 * cfg_.candCapacity) setSize <<= 1;
+    candSetMask_ = setSize - 1;
+    hash_.alloc(E_);
+    heap_.alloc(B_);
+    voxels_.alloc((size_t)B_ * BF_VOXELS_PER_BLOCK);
+    blockPos_.alloc(B_);
+    visible_.alloc(B_);
+    ctrl_.alloc(C_COUNT);
+    stats_.alloc(1);
+    cand_.alloc(cfg_.candCapacity);
+    candSet_.alloc(setSize);
+    candSlot_.alloc(cfg_.candCapacity);
+    ovf_.alloc(OVF_CAP);
+    gcSimple_.alloc(B_);
+    gcList_.alloc(GC_LIST_CAP);
+    blockCount_.alloc(B_);
+    hipDeviceProp_t prop;
+    int dev = 0;
+    BF_HIP(hipGetDevice(&dev));
+    BF_HIP(hipGetDeviceProperties(&prop, dev));
+    numCUs_ = prop.multiProcessorCount;
+    BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(stats_.p, 0, sizeof(BFTsdfStats), stream_));
+    float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    std::memcpy(T_.m, I, 64);
+    std::memcpy(Tinv_.m, I, 64);
+    reset();
+}
+
+Scene::~Scene() {}
+
+size_t Scene::deviceBytes() const {
+    return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + ctrl_.bytes() +
+           stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
+           gcList_.bytes() + blockCount_.bytes();
+}
+
+// CUDASceneRepHashSDF::reset (.h:147-155) -> resetCUDA (.cu:67-111)
+void Scene::reset() {
+    const unsigned grid = (unsigned)numCUs_ * 8;
+    k_reset_hash<<<grid, 256, 0, stream_>>>(hash_.p, E_);
+    BF_LAUNCH_CHECK();
+    k_reset_heap<<<grid, 256, 0, stream_>>>(heap_.p, blockPos_.p, blockCount_.p, B_, ctrl_.p);
+    BF_LAUNCH_CHECK();
+    BF_HIP(hipMemsetAsync(voxels_.p, 0, voxels_.bytes(), stream_));
+    cfg_.hp.numOccupiedBlocks = 0;
+}
+
+void Scene::beginOp() {
+    k_begin_op<<<1, 64, 0, stream_>>>(ctrl_.p, stats_.p);
+    BF_LAUNCH_CHECK();
+}
+
+void Scene::alloc(const float* depth, const BFDepthCameraParams& cam, const uint32_t* bitMask) {
+    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
+    dim3 g(div_up(cam.imageWidth, ALLOC_TILE), div_up(cam.imageHeight, ALLOC_TILE));
+    k_alloc_collect<<<g, 256, 0, stream_>>>(A, depth, cam, T_, Tinv_, cand_.p, cfg_.candCapacity);
+    BF_LAUNCH_CHECK();
+    const unsigned grid = (unsigned)numCUs_ * 4;
+    k_alloc_insert<<<grid, 256, 0, stream_>>>(A, cand_.p, cfg_.candCapacity, candSet_.p, candSetMask_, candSlot_.p, ovf_.p);
+    BF_LAUNCH_CHECK();
+    k_alloc_overflow<<<1, 64, 0, stream_>>>(A, ovf_.p);
+    BF_LAUNCH_CHECK();
+    k_alloc_cleanup<<<grid, 256, 0, stream_>>>(ctrl_.p, cfg_.candCapacity, candSlot_.p, candSet_.p);
+    BF_LAUNCH_CHECK();
+}
+
+void Scene::compactify(const BFMat4& T, const BFDepthCameraParams& cam) {
+    T_ = T;
+    Tinv_ = mat4_inverse(T);
+    beginOp();
+    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
+    k_compactify<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_);
+    BF_LAUNCH_CHECK();
+}
+
+// CUDASceneRepHashSDF::integrate (.h:65-83) / deIntegrate (.h:85-108)
+void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color, const BFDepthCameraParams& cam, bool deint,
+                      const uint32_t* bitMask) {
+    BF_REQUIRE(depth != nullptr, BF_ERR_ARG, "depth is null");
+    T_ = T;
+    Tinv_ = mat4_inverse(T);
+    beginOp();
+    if (!deint) alloc(depth, cam, bitMask);
+    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
+    const unsigned grid = (unsigned)numCUs_ * 4;
+    k_compactify<<<grid, 256, 0, stream_>>>(A, cam, Tinv_);
+    BF_LAUNCH_CHECK();
+    const unsigned igrid = (unsigned)numCUs_ * 8;
+    if (deint)
+        k_integrate<true><<<igrid, 256, 0, stream_>>>(A, depth, reinterpret_cast<const uint32_t*>(color), cam, Tinv_);
+    else
+        k_integrate<false><<<igrid, 256, 0, stream_>>>(A, depth, reinterpret_cast<const uint32_t*>(color), cam, Tinv_);
+    BF_LAUNCH_CHECK();
+}
+
+// CUDASceneRepHashSDF::garbageCollect (.h:110-126)
+void Scene::garbageCollect() {
+    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
+    k_gc_begin<<<1, 64, 0, stream_>>>(ctrl_.p, stats_.p);
+    BF_LAUNCH_CHECK();
+    const unsigned grid = (unsigned)numCUs_ * 2;
+    k_gc_identify<<<grid, 256, 0, stream_>>>(A, gcSimple_.p, gcList_.p);
+    BF_LAUNCH_CHECK();
+    k_gc_free_simple<<<grid, 256, 0, stream_>>>(A, gcSimple_.p);
+    BF_LAUNCH_CHECK();
+    k_gc_free_list<<<1, 64, 0, stream_>>>(A, gcList_.p);
+    BF_LAUNCH_CHECK();
+}
+
+uint32_t Scene::heapFreeCount() {
+    uint32_t c = 0;
+    BF_HIP(hipMemcpyAsync(&c, ctrl_.p + C_HEAP, 4, hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    return c + 1;  // .h:168-172
+}
+
+uint32_t Scene::numVisible() {
+    uint32_t c = 0;
+    BF_HIP(hipMemcpyAsync(&c, ctrl_.p + C_VISIBLE, 4, hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    return c;
+}
+
+uint32_t Scene::errorFlags() {
+    uint32_t c = 0;
+    BF_HIP(hipMemcpyAsync(&c, ctrl_.p + C_ERR, 4, hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    return c;
+}
+
+BFTsdfStats Scene::stats() {
+    BFTsdfStats s;
+    BF_HIP(hipMemcpyAsync(&s, stats_.p, sizeof(s), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    return s;
+}
+
+void Scene::resetStats() { BF_HIP(hipMemsetAsync(stats_.p, 0, sizeof(BFTsdfStats), stream_)); }
+
+void Scene::exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels) {
+    if (hash) BF_HIP(hipMemcpyAsync(hash, hash_.p, hash_.bytes(), hipMemcpyDeviceToHost, stream_));
+    if (heap) BF_HIP(hipMemcpyAsync(heap, heap_.p, heap_.bytes(), hipMemcpyDeviceToHost, stream_));
+    if (heapCounter) BF_HIP(hipMemcpyAsync(heapCounter, ctrl_.p + C_HEAP, 4, hipMemcpyDeviceToHost, stream_));
+    if (voxels) BF_HIP(hipMemcpyAsync(voxels, voxels_.p, voxels_.bytes(), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+}
+
+uint32_t Scene::exportVisible(int4* out, uint32_t cap) {
+    uint32_t n = numVisible();
+    n = std::min(n, cap);
+    if (n) BF_HIP(hipMemcpyAsync(out, visible_.p, n * sizeof(int4), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    return n;
+}
+
+}  // namespace bf

@@ -1,0 +1,145 @@
+/*
+ * bf/types.h — plain-old-data layouts shared by the HIP library, the C ABI,
+ * the CPU oracle and the ctypes binding.
+ *
+ * Every struct mirrors the byte layout of the reference structure it replaces
+ * so a FriedLiver-shaped host can hand its buffers over unchanged:
+ *
+ *   BFMat4              <- float4x4        Source/SiftGPU/cuda_SimpleMatrixUtil.h:855-875 (row-major m11..m44)
+ *   BFHashEntry         <- HashEntry       Source/DepthSensing/VoxelUtilHashSDF.h:56-74   (32 B, __align__(16))
+ *   BFVoxel             <- Voxel           Source/DepthSensing/VoxelUtilHashSDF.h:77-98   (12 B)
+ *   BFHashParams        <- HashParams      Source/DepthSensing/CUDAHashParams.h:10-36     (224 B)
+ *   BFDepthCameraParams <- DepthCameraParams Source/DepthSensing/CUDADepthCameraParams.h:7-19 (32 B)
+ *   BFRayCastParams     <- RayCastParams   Source/DepthSensing/CUDARayCastParams.h:8-27   (192 B)
+ *   BFEntryJ            <- EntryJ          Source/SiftGPU/SIFTImageManager.h:45-60        (32 B)
+ *
+ * C99/C++ compatible; no HIP or torch types.
+ */
+#ifndef BF_TYPES_H
+#define BF_TYPES_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BF_SDF_BLOCK_SIZE 8            /* VoxelUtilHashSDF.h:40 */
+#define BF_HASH_BUCKET_SIZE 4          /* VoxelUtilHashSDF.h:41 */
+#define BF_VOXELS_PER_BLOCK 512
+#define BF_LOCK_ENTRY (-1)             /* VoxelUtilHashSDF.h:52 */
+#define BF_FREE_ENTRY (-2)             /* VoxelUtilHashSDF.h:53 */
+#define BF_INVALID_IMAGE 0xFFFFFFFFu   /* EntryJ::setInvalid, SIFTImageManager.h:51-54 */
+
+typedef struct BFMat4 {
+    float m[16]; /* row-major: m[r*4+c] */
+} BFMat4;
+
+typedef struct BFFloat3 { float x, y, z; } BFFloat3;
+typedef struct BFInt3 { int32_t x, y, z; } BFInt3;
+
+typedef struct __attribute__((aligned(16))) BFHashEntry {
+    int32_t x, y, z;   /* SDF block coordinate (lower-left corner / 8) */
+    int32_t ptr;       /* voxel index of the block's first voxel (= heap block * 512), or FREE/LOCK */
+    uint32_t offset;   /* collision-list offset relative to the bucket's last slot */
+    int32_t pad[3];
+} BFHashEntry;
+
+typedef struct BFVoxel {
+    float sdf;
+    float weight;
+    uint8_t color[4];
+} BFVoxel;
+
+typedef struct __attribute__((aligned(16))) BFHashParams {
+    BFMat4 rigidTransform;          /* camera -> world */
+    BFMat4 rigidTransformInverse;   /* world -> camera */
+    uint32_t hashNumBuckets;
+    uint32_t hashBucketSize;
+    uint32_t hashMaxCollisionLinkedListSize;
+    uint32_t numSDFBlocks;
+    int32_t SDFBlockSize;
+    float virtualVoxelSize;
+    uint32_t numOccupiedBlocks;
+    float maxIntegrationDistance;
+    float truncScale;
+    float truncation;
+    uint32_t integrationWeightSample;
+    uint32_t integrationWeightMax;
+    BFFloat3 streamingVoxelExtents;
+    BFInt3 streamingGridDimensions;
+    BFInt3 streamingMinGridPos;
+    uint32_t streamingInitialChunkListSize;
+    uint32_t dummy[2];
+} BFHashParams;
+
+typedef struct __attribute__((aligned(16))) BFDepthCameraParams {
+    float fx, fy, mx, my;
+    uint32_t imageWidth, imageHeight;
+    float sensorDepthWorldMin;  /* render depth min (frustum) */
+    float sensorDepthWorldMax;  /* render depth max (frustum) */
+} BFDepthCameraParams;
+
+typedef struct __attribute__((aligned(16))) BFRayCastParams {
+    BFMat4 viewMatrix;          /* world -> camera */
+    BFMat4 viewMatrixInverse;   /* camera -> world */
+    float mx, my, fx, fy;
+    uint32_t width, height;
+    uint32_t numOccupiedSDFBlocks;
+    uint32_t maxNumVertices;
+    int32_t splatMinimum;
+    float minDepth, maxDepth;
+    float rayIncrement;
+    float thresSampleDist;
+    float thresDist;
+    uint8_t useGradients;
+    uint8_t pad_[3];
+    uint32_t dummy0;
+} BFRayCastParams;
+
+typedef struct BFEntryJ {
+    uint32_t imgIdx_i;
+    uint32_t imgIdx_j;
+    BFFloat3 pos_i;   /* camera-space point in frame i */
+    BFFloat3 pos_j;   /* camera-space point in frame j */
+} BFEntryJ;
+
+/* Per-frame dense-term cache (CUDACachedFrame, Source/CUDACacheUtil.h:10-53), as a
+ * struct of device pointers, one per cached frame. All images are W*H (80x60 default). */
+typedef struct BFCachedFrame {
+    const float* depth;          /* d_depthDownsampled */
+    const float* campos;         /* d_cameraposDownsampled, float4 per pixel (x,y,z,w) */
+    const float* normals;        /* d_normalsDownsampled, float4 per pixel */
+    const uint8_t* normalsU8;    /* d_normalsDownsampledUCHAR4, uchar4 per pixel */
+    const float* intensity;      /* d_intensityDownsampled */
+    const float* intensityDeriv; /* d_intensityDerivsDownsampled, float2 per pixel */
+} BFCachedFrame;
+
+/* Device-side counters used by the bench to compute algorithmic bytes. */
+typedef struct BFTsdfStats {
+    uint64_t pixels;          /* P: pixels read by alloc (valid or not) */
+    uint64_t candidates;      /* U: candidate (absent, in-frustum) block lookups emitted by alloc */
+    uint64_t allocated;       /* A: new hash entries written */
+    uint64_t scanned;         /* blocks scanned by compactify (allocated blocks read) */
+    uint64_t visible;         /* Nv summed over compactify calls */
+    uint64_t voxelsUpdated;   /* V: voxels read-modify-written inside the truncation band */
+    uint64_t gcBlocks;        /* blocks whose weights were scanned by GC */
+    uint64_t gcFreed;         /* blocks freed by GC */
+    uint64_t allocOverflow;   /* candidates dropped: candidate buffer / heap exhausted */
+    uint64_t integrateOps;    /* integrate + de-integrate calls */
+} BFTsdfStats;
+
+#ifdef __cplusplus
+} /* extern "C" */
+
+static_assert(sizeof(BFMat4) == 64, "float4x4 is 64 B");
+static_assert(sizeof(BFHashEntry) == 32, "HashEntry is 32 B");
+static_assert(sizeof(BFVoxel) == 12, "Voxel is 12 B");
+static_assert(sizeof(BFHashParams) == 224, "HashParams is 224 B");
+static_assert(sizeof(BFDepthCameraParams) == 32, "DepthCameraParams is 32 B");
+static_assert(sizeof(BFRayCastParams) == 192, "RayCastParams is 192 B");
+static_assert(__builtin_offsetof(BFRayCastParams, useGradients) == 184, "m_useGradients at 184");
+static_assert(sizeof(BFEntryJ) == 32, "EntryJ is 32 B");
+#endif
+
+#endif /* BF_TYPES_H */

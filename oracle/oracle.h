@@ -1,0 +1,94 @@
+/*
+ * oracle/oracle.h — TEST INFRASTRUCTURE: the CPU restatement ("bf_cpu") of the
+ * reference's TSDF / raycast / bundle-adjustment arithmetic, used as the parity
+ * checker and as bench.py's cpu_baseline leg. Nothing in the product
+ * (bundlefusion_amd/) links, loads or calls this library.
+ *
+ * Parity status: the reference cannot be compiled or run here (SURVEY.md §8(c):
+ * VS2013/CUDA 7/D3D11/mLib, no nvcc) and ships no tests, fixtures or golden
+ * vectors. The oracle is therefore pinned only by analytic
+ * known-answer tests written from the cited reference lines (tests/test_oracle_*.py)
+ * and by committed fixtures it generated itself — "parity unpinned" against a
+ * running reference, as DESIGN.md states.
+ */
+#ifndef BF_ORACLE_H
+#define BF_ORACLE_H
+
+#include "../include/bf/types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- TSDF scene (CUDASceneRepHashSDF semantics, serial schedule) ---------- */
+typedef struct ORScene ORScene;
+ORScene* or_scene_create(const BFHashParams* params);
+void or_scene_destroy(ORScene* s);
+void or_scene_reset(ORScene* s);
+/* integrate (deintegrate=0) / de-integrate (deintegrate=1) one frame with camera->world T.
+ * depth: float[W*H] metres (-inf invalid); color: uchar4[W*H] or NULL. */
+void or_scene_integrate(ORScene* s, const float T[16], const float* depth, const uint8_t* color,
+                        const BFDepthCameraParams* cam, int deintegrate, const uint32_t* bitMask);
+void or_scene_garbage_collect(ORScene* s);
+uint32_t or_scene_compactify(ORScene* s, const float T[16], const BFDepthCameraParams* cam);
+uint32_t or_scene_heap_free_count(const ORScene* s);
+uint32_t or_scene_num_occupied(const ORScene* s);
+/* full dump (debugHash): hash[E], heap[B], voxels[B*512] */
+void or_scene_export(const ORScene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter,
+                     BFVoxel* voxels);
+/* occupied (visible) list of the last compactify: entries[numOccupied] */
+void or_scene_export_visible(const ORScene* s, BFHashEntry* out);
+void or_scene_get_stats(const ORScene* s, BFTsdfStats* out);
+
+/* Dense-grid variant of config 1 (one frame -> dense n^3 TSDF, no hash). Restates the
+ * per-voxel arithmetic of integrateDepthMapKernel over a dense volume. */
+void or_dense_integrate(const float T[16], const float* depth, const uint8_t* color,
+                        const BFDepthCameraParams* cam, const BFHashParams* params,
+                        const int origin[3], int n, BFVoxel* grid);
+
+/* ---- raycast (CUDARayCastSDF::render semantics) ----------------------------- */
+void or_raycast(const ORScene* s, const BFRayCastParams* rp, const BFDepthCameraParams* cam,
+                const float T[16], float* depth, float* depth4, float* normals, float* colors,
+                float* rayMin, float* rayMax);
+
+/* ---- Lie helpers (LieDerivUtil.h) ------------------------------------------ */
+void or_pose_to_matrix(const float rot[3], const float trans[3], float M[16]);
+void or_matrix_to_pose(const float M[16], float rot[3], float trans[3]);
+void or_matrix_inverse(const float M[16], float out[16]);
+
+/* ---- bundle adjustment (CUDASolverBundling::solve semantics) --------------- */
+typedef struct ORSolveParams {
+    uint32_t numImages;
+    uint32_t numCorr;
+    uint32_t nNonLin;
+    uint32_t nLin;
+    uint32_t maxCorrPerImage;
+    const float* weightsSparse;     /* [nNonLin] */
+    const float* weightsDenseDepth; /* [nNonLin] */
+    const float* weightsDenseColor; /* [nNonLin] */
+    /* dense term inputs (may be NULL when weights are 0) */
+    const BFCachedFrame* cache;     /* host pointers */
+    uint32_t cacheW, cacheH;
+    float intrinsics[4];            /* fx, fy, mx, my of the cache frames */
+    float denseDistThresh, denseNormalThresh, denseColorThresh, denseColorGradientMin;
+    float denseDepthMin, denseDepthMax;
+    uint32_t denseOverlapSubsample;
+} ORSolveParams;
+
+typedef struct ORSolveResult {
+    uint32_t gnIterations;      /* GN iterations executed */
+    uint32_t pcgIterations;     /* total PCG iterations executed */
+    float maxResidual;          /* computeMaxResidual */
+    int32_t maxResidualIndex;
+    float finalEnergy;          /* EvalResidual with the last weightSparse */
+} ORSolveResult;
+
+/* corr: EntryJ[numCorr] (entries may be invalidated in place by the row cap);
+ * validImages: int[numImages]; rot/trans: float3[numImages] in/out. */
+void or_ba_solve(BFEntryJ* corr, const int* validImages, const ORSolveParams* p, float* rot,
+                 float* trans, ORSolveResult* res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,534 @@
+// oracle/tsdf.cpp — TEST INFRASTRUCTURE (CPU oracle, see oracle.h header).
+//
+// Serial CPU restatement of the reference voxel-hash scene: every reference kernel is
+// executed as if its threads ran one after another (a legal schedule of the racy
+// reference: with one thread at a time every try-lock succeeds and the host alloc
+// loop of CUDASceneRepHashSDF.h:335-348 converges after one effective pass).
+// Citations are to /root/reference/FriedLiver/Source/DepthSensing/.
+#include "oracle.h"
+#include "or_math.h"
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+using namespace orc;
+
+namespace {
+
+const float MINF = -std::numeric_limits<float>::infinity();
+const float PINF = std::numeric_limits<float>::infinity();
+
+struct Scene {
+    BFHashParams hp;
+    std::vector<BFHashEntry> hash;      // d_hash
+    std::vector<BFHashEntry> compact;   // d_hashCompactified (first numOccupied valid)
+    std::vector<uint32_t> heap;         // d_heap
+    uint32_t heapCounter;               // d_heapCounter
+    std::vector<BFVoxel> voxels;        // d_SDFBlocks
+    std::vector<int> mutex;             // d_hashBucketMutex
+    std::vector<int> decision;          // d_hashDecision (GC)
+    uint32_t numOccupied;
+    m4 T, Tinv;
+    BFDepthCameraParams cam;
+    BFTsdfStats stats;
+};
+
+m4 toM4(const float* p) { m4 m; std::memcpy(m.e, p, 64); return m; }
+
+// ---- VoxelUtilHashSDF.h restatements ---------------------------------------
+
+// computeHashPos, VoxelUtilHashSDF.h:225-234 (wrapping int32 multiplies)
+uint32_t hashPos(const Scene& s, i3 p) {
+    int32_t a = (int32_t)((uint32_t)p.x * 73856093u);
+    int32_t b = (int32_t)((uint32_t)p.y * 19349669u);
+    int32_t c = (int32_t)((uint32_t)p.z * 83492791u);
+    int res = (a ^ b ^ c) % (int)s.hp.hashNumBuckets;
+    if (res < 0) res += (int)s.hp.hashNumBuckets;
+    return (uint32_t)res;
+}
+
+float truncation(const Scene& s, float z) { return s.hp.truncation + s.hp.truncScale * z; }  // :272-274
+
+// worldToVirtualVoxelPos :283-287 (round half away from zero via sign)
+i3 worldToVirtualVoxelPos(const Scene& s, f3 pos) {
+    f3 p = pos / s.hp.virtualVoxelSize;
+    f3 sg = mk((float)sgn(p.x), (float)sgn(p.y), (float)sgn(p.z));
+    f3 q = p + sg * 0.5f;
+    return {f2i(q.x), f2i(q.y), f2i(q.z)};
+}
+// virtualVoxelPosToSDFBlock :290-299
+i3 virtualVoxelPosToSDFBlock(i3 v) {
+    if (v.x < 0) v.x -= BF_SDF_BLOCK_SIZE - 1;
+    if (v.y < 0) v.y -= BF_SDF_BLOCK_SIZE - 1;
+    if (v.z < 0) v.z -= BF_SDF_BLOCK_SIZE - 1;
+    return {v.x / BF_SDF_BLOCK_SIZE, v.y / BF_SDF_BLOCK_SIZE, v.z / BF_SDF_BLOCK_SIZE};
+}
+f3 virtualVoxelPosToWorld(const Scene& s, i3 p) {  // :308-310
+    return mk((float)p.x, (float)p.y, (float)p.z) * s.hp.virtualVoxelSize;
+}
+f3 SDFBlockToWorld(const Scene& s, i3 b) {  // :313-315
+    return virtualVoxelPosToWorld(s, {b.x * BF_SDF_BLOCK_SIZE, b.y * BF_SDF_BLOCK_SIZE, b.z * BF_SDF_BLOCK_SIZE});
+}
+i3 worldToSDFBlock(const Scene& s, f3 w) { return virtualVoxelPosToSDFBlock(worldToVirtualVoxelPos(s, w)); }
+
+// DepthCameraUtil.h:71-107 + :137-144 (frustum test against c_depthCameraParams)
+f3 cameraToKinectProj(const BFDepthCameraParams& c, f3 pos) {
+    float px = pos.x * c.fx / pos.z + c.mx;
+    float py = pos.y * c.fy / pos.z + c.my;
+    f3 r;
+    r.x = (2.0f * px - ((float)c.imageWidth - 1.0f)) / ((float)c.imageWidth - 1.0f);
+    r.y = (((float)c.imageHeight - 1.0f) - 2.0f * py) / ((float)c.imageHeight - 1.0f);
+    r.z = (pos.z - c.sensorDepthWorldMin) / (c.sensorDepthWorldMax - c.sensorDepthWorldMin);
+    return r;
+}
+bool isInCameraFrustumApprox(const BFDepthCameraParams& c, const m4& viewInv, f3 pos) {
+    f3 pc = xform(viewInv, pos);
+    f3 pp = cameraToKinectProj(c, pc);
+    // pProj *= 0.95: operator*=(float3&, float) (cutil_math.h:761) takes 0.95 as 0.95f
+    pp = pp * 0.95f;
+    return !(pp.x < -1.0f || pp.x > 1.0f || pp.y < -1.0f || pp.y > 1.0f || pp.z < 0.0f || pp.z > 1.0f);
+}
+// isSDFBlockInCameraFrustumApprox :322-326
+bool blockInFrustum(const Scene& s, i3 b) {
+    f3 w = SDFBlockToWorld(s, b) + mk(1, 1, 1) * (s.hp.virtualVoxelSize * 0.5f * (BF_SDF_BLOCK_SIZE - 1.0f));
+    return isInCameraFrustumApprox(s.cam, s.Tinv, w);
+}
+
+bool samePos(const BFHashEntry& e, i3 p) { return e.x == p.x && e.y == p.y && e.z == p.z; }
+
+void deleteHashEntry(BFHashEntry& e) { e.x = e.y = e.z = 0; e.offset = 0; e.ptr = BF_FREE_ENTRY; }  // :382-386
+void deleteVoxel(BFVoxel& v) { v.sdf = 0; v.weight = 0; v.color[0] = v.color[1] = v.color[2] = v.color[3] = 0; }
+
+uint32_t numEntries(const Scene& s) { return s.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE; }
+
+// getHashEntryForSDFBlockPos :440-485
+BFHashEntry getHashEntryForSDFBlockPos(const Scene& s, i3 b) {
+    uint32_t h = hashPos(s, b), hp = h * BF_HASH_BUCKET_SIZE;
+    BFHashEntry entry{};
+    entry.x = b.x; entry.y = b.y; entry.z = b.z; entry.offset = 0; entry.ptr = BF_FREE_ENTRY;
+    for (uint32_t j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+        const BFHashEntry& curr = s.hash[j + hp];
+        if (samePos(curr, b) && curr.ptr != BF_FREE_ENTRY) return curr;
+    }
+    const uint32_t last = (h + 1) * BF_HASH_BUCKET_SIZE - 1;
+    uint32_t i = last;
+    for (uint32_t it = 0; it < s.hp.hashMaxCollisionLinkedListSize; it++) {
+        const BFHashEntry& curr = s.hash[i];
+        if (samePos(curr, b) && curr.ptr != BF_FREE_ENTRY) return curr;
+        if (curr.offset == 0) break;
+        i = (last + curr.offset) % numEntries(s);
+    }
+    return entry;
+}
+
+// consumeHeap / appendHeap :535-546
+uint32_t consumeHeap(Scene& s) { uint32_t addr = s.heapCounter--; return s.heap[addr]; }
+void appendHeap(Scene& s, uint32_t ptr) { uint32_t addr = s.heapCounter++; s.heap[addr + 1] = ptr; }
+
+// allocBlock :549-655 (serial: every atomicExch try-lock succeeds unless the bucket
+// was already locked in this pass by an earlier thread)
+bool allocBlock(Scene& s, i3 pos) {
+    uint32_t h = hashPos(s, pos), hp = h * BF_HASH_BUCKET_SIZE;
+    int firstEmpty = -1;
+    for (uint32_t j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+        uint32_t i = j + hp;
+        const BFHashEntry& curr = s.hash[i];
+        if (samePos(curr, pos) && curr.ptr != BF_FREE_ENTRY) return false;
+        if (firstEmpty == -1 && curr.ptr == BF_FREE_ENTRY) firstEmpty = (int)i;
+    }
+    const uint32_t last = (h + 1) * BF_HASH_BUCKET_SIZE - 1;
+    uint32_t i = last;
+    for (uint32_t it = 0; it < s.hp.hashMaxCollisionLinkedListSize; it++) {
+        const BFHashEntry& curr = s.hash[i];
+        if (samePos(curr, pos) && curr.ptr != BF_FREE_ENTRY) return false;
+        if (curr.offset == 0) break;
+        i = (last + curr.offset) % numEntries(s);
+    }
+    if (s.heapCounter == 0xFFFFFFFFu || s.heapCounter >= s.hp.numSDFBlocks) {  // heap exhausted (unchecked in ref)
+        s.stats.allocOverflow++;
+        return false;
+    }
+    if (firstEmpty != -1) {
+        int prev = s.mutex[h]; s.mutex[h] = BF_LOCK_ENTRY;
+        if (prev != BF_LOCK_ENTRY) {
+            BFHashEntry& e = s.hash[firstEmpty];
+            e.x = pos.x; e.y = pos.y; e.z = pos.z; e.offset = 0;
+            e.ptr = (int32_t)(consumeHeap(s) * BF_VOXELS_PER_BLOCK);
+            s.stats.allocated++;
+            return true;
+        }
+        return false;
+    }
+    int offset = 0;
+    for (uint32_t it = 0; it < s.hp.hashMaxCollisionLinkedListSize;) {
+        offset++;
+        i = (last + (uint32_t)offset) % numEntries(s);
+        if ((offset % BF_HASH_BUCKET_SIZE) == 0) continue;  // never a last bucket slot
+        const BFHashEntry& curr = s.hash[i];
+        if (curr.ptr == BF_FREE_ENTRY) {
+            int prev = s.mutex[h]; s.mutex[h] = BF_LOCK_ENTRY;
+            if (prev != BF_LOCK_ENTRY) {
+                BFHashEntry lastEntry = s.hash[last];
+                uint32_t h2 = i / BF_HASH_BUCKET_SIZE;
+                prev = s.mutex[h2]; s.mutex[h2] = BF_LOCK_ENTRY;
+                if (prev != BF_LOCK_ENTRY) {
+                    BFHashEntry& e = s.hash[i];
+                    e.x = pos.x; e.y = pos.y; e.z = pos.z;
+                    e.offset = lastEntry.offset;
+                    e.ptr = (int32_t)(consumeHeap(s) * BF_VOXELS_PER_BLOCK);
+                    lastEntry.offset = (uint32_t)offset;
+                    s.hash[last] = lastEntry;
+                    s.stats.allocated++;
+                    return true;
+                }
+            }
+            return false;
+        }
+        it++;
+    }
+    return false;
+}
+
+// deleteHashEntryElement :739-826
+bool deleteHashEntryElement(Scene& s, i3 b) {
+    uint32_t h = hashPos(s, b), hp = h * BF_HASH_BUCKET_SIZE;
+    for (uint32_t j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+        uint32_t i = j + hp;
+        const BFHashEntry curr = s.hash[i];
+        if (samePos(curr, b) && curr.ptr != BF_FREE_ENTRY) {
+            if (curr.offset != 0) {
+                int prev = s.mutex[h]; s.mutex[h] = BF_LOCK_ENTRY;
+                if (prev == BF_LOCK_ENTRY) return false;
+                appendHeap(s, (uint32_t)curr.ptr / BF_VOXELS_PER_BLOCK);
+                uint32_t nextIdx = (i + curr.offset) % numEntries(s);
+                s.hash[i] = s.hash[nextIdx];
+                deleteHashEntry(s.hash[nextIdx]);
+                return true;
+            } else {
+                appendHeap(s, (uint32_t)curr.ptr / BF_VOXELS_PER_BLOCK);
+                deleteHashEntry(s.hash[i]);
+                return true;
+            }
+        }
+    }
+    const uint32_t last = (h + 1) * BF_HASH_BUCKET_SIZE - 1;
+    uint32_t i = last;
+    BFHashEntry curr = s.hash[i];
+    uint32_t prevIdx = i;
+    i = (last + curr.offset) % numEntries(s);
+    for (uint32_t it = 0; it < s.hp.hashMaxCollisionLinkedListSize; it++) {
+        curr = s.hash[i];
+        if (samePos(curr, b) && curr.ptr != BF_FREE_ENTRY) {
+            int prev = s.mutex[h]; s.mutex[h] = BF_LOCK_ENTRY;
+            if (prev == BF_LOCK_ENTRY) return false;
+            appendHeap(s, (uint32_t)curr.ptr / BF_VOXELS_PER_BLOCK);
+            deleteHashEntry(s.hash[i]);
+            BFHashEntry p = s.hash[prevIdx];
+            p.offset = curr.offset;
+            s.hash[prevIdx] = p;
+            return true;
+        }
+        if (curr.offset == 0) return false;
+        prevIdx = i;
+        i = (last + curr.offset) % numEntries(s);
+    }
+    return false;
+}
+
+void resetMutex(Scene& s) { std::fill(s.mutex.begin(), s.mutex.end(), BF_FREE_ENTRY); }  // :58-65
+
+// DepthCameraUtil.h:114-119 (kinectDepthToSkeleton)
+f3 depthToSkeleton(const BFDepthCameraParams& c, uint32_t ux, uint32_t uy, float depth) {
+    const float x = ((float)ux - c.mx) / c.fx;
+    const float y = ((float)uy - c.my) / c.fy;
+    return mk(depth * x, depth * y, depth);
+}
+
+// allocKernel, CUDASceneRepHashSDF.cu:165-251, one pixel
+void allocPixel(Scene& s, const float* depth, uint32_t x, uint32_t y, const uint32_t* bitMask, bool count) {
+    const BFDepthCameraParams& c = s.cam;
+    float d = depth[y * c.imageWidth + x];
+    if (d == MINF || d == 0.0f) return;
+    if (d >= s.hp.maxIntegrationDistance) return;
+    float t = truncation(s, d);
+    float minDepth = std::min(s.hp.maxIntegrationDistance, d - t);
+    float maxDepth = std::min(s.hp.maxIntegrationDistance, d + t);
+    if (minDepth >= maxDepth) return;
+    f3 rayMin = xform(s.T, depthToSkeleton(c, x, y, minDepth));
+    f3 rayMax = xform(s.T, depthToSkeleton(c, x, y, maxDepth));
+    f3 rayDir = normalize(rayMax - rayMin);
+    i3 id = worldToSDFBlock(s, rayMin);
+    i3 idEnd = worldToSDFBlock(s, rayMax);
+    f3 step = mk((float)sgn(rayDir.x), (float)sgn(rayDir.y), (float)sgn(rayDir.z));
+    auto clamp01 = [](float v) { return std::max(0.0f, std::min(v, 1.0f)); };
+    i3 idc = {id.x + f2i(clamp01(step.x)), id.y + f2i(clamp01(step.y)), id.z + f2i(clamp01(step.z))};
+    f3 boundaryPos = SDFBlockToWorld(s, idc) - mk(1, 1, 1) * (0.5f * s.hp.virtualVoxelSize);
+    f3 tMax = (boundaryPos - rayMin) / rayDir;
+    f3 tDelta = (step * (float)BF_SDF_BLOCK_SIZE * s.hp.virtualVoxelSize) / rayDir;
+    i3 idBound = {f2i((float)idEnd.x + step.x), f2i((float)idEnd.y + step.y), f2i((float)idEnd.z + step.z)};
+    if (rayDir.x == 0.0f) { tMax.x = PINF; tDelta.x = PINF; }
+    if (boundaryPos.x - rayMin.x == 0.0f) { tMax.x = PINF; tDelta.x = PINF; }
+    if (rayDir.y == 0.0f) { tMax.y = PINF; tDelta.y = PINF; }
+    if (boundaryPos.y - rayMin.y == 0.0f) { tMax.y = PINF; tDelta.y = PINF; }
+    if (rayDir.z == 0.0f) { tMax.z = PINF; tDelta.z = PINF; }
+    if (boundaryPos.z - rayMin.z == 0.0f) { tMax.z = PINF; tDelta.z = PINF; }
+    (void)bitMask;  // chunk streaming bitmask: streaming is disabled (zParametersDefault.txt:100)
+    for (uint32_t iter = 0; iter < 1024; iter++) {
+        if (blockInFrustum(s, id)) {
+            // count a candidate lookup only for blocks that are absent (what the HIP alloc emits)
+            BFHashEntry e = getHashEntryForSDFBlockPos(s, id);
+            if (e.ptr == BF_FREE_ENTRY) { if (count) s.stats.candidates++; allocBlock(s, id); }
+        }
+        if (tMax.x < tMax.y && tMax.x < tMax.z) {
+            id.x = f2i((float)id.x + step.x);
+            if (id.x == idBound.x) return;
+            tMax.x += tDelta.x;
+        } else if (tMax.z < tMax.y) {
+            id.z = f2i((float)id.z + step.z);
+            if (id.z == idBound.z) return;
+            tMax.z += tDelta.z;
+        } else {
+            id.y = f2i((float)id.y + step.y);
+            if (id.y == idBound.y) return;
+            tMax.y += tDelta.y;
+        }
+    }
+}
+
+// compactifyHashAllInOneKernel :324-366 (order: table order; the HIP build's order differs,
+// consumers are order-independent)
+uint32_t compactify(Scene& s) {
+    s.numOccupied = 0;
+    const uint32_t E = numEntries(s);
+    for (uint32_t i = 0; i < E; i++) {
+        const BFHashEntry& e = s.hash[i];
+        if (e.ptr != BF_FREE_ENTRY) {
+            s.stats.scanned++;
+            if (blockInFrustum(s, {e.x, e.y, e.z})) s.compact[s.numOccupied++] = e;
+        }
+    }
+    s.stats.visible += s.numOccupied;
+    s.hp.numOccupiedBlocks = s.numOccupied;
+    return s.numOccupied;
+}
+
+// integrateDepthMapKernel<deIntegrate>, CUDASceneRepHashSDF.cu:420-521
+void integrateBlock(Scene& s, const BFHashEntry& entry, const float* depthImg, const uint8_t* colorImg,
+                    bool deIntegrate, uint64_t& updated) {
+    const BFDepthCameraParams& c = s.cam;
+    i3 base = {entry.x * BF_SDF_BLOCK_SIZE, entry.y * BF_SDF_BLOCK_SIZE, entry.z * BF_SDF_BLOCK_SIZE};
+    for (uint32_t i = 0; i < BF_VOXELS_PER_BLOCK; i++) {
+        i3 pi = {base.x + (int)(i % 8), base.y + (int)((i % 64) / 8), base.z + (int)(i / 64)};
+        f3 pf = xform(s.Tinv, virtualVoxelPosToWorld(s, pi));
+        // cameraToKinectScreenInt: make_int2(pImage + 0.5) then make_uint2 (DepthCameraUtil.h:78-88)
+        float sx = pf.x * c.fx / pf.z + c.mx;
+        float sy = pf.y * c.fy / pf.z + c.my;
+        uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
+        if (!(ux < c.imageWidth && uy < c.imageHeight)) continue;
+        float depth = depthImg[uy * c.imageWidth + ux];
+        if (!colorImg) continue;  // color stays MINF -> no update (:441-448)
+        const uint8_t* cc = colorImg + 4 * (uy * c.imageWidth + ux);
+        if (depth == MINF) continue;
+        if (!(depth < s.hp.maxIntegrationDistance)) continue;
+        float sdf = depth - pf.z;
+        float tr = truncation(s, depth);
+        if (!(std::fabs(sdf) < tr)) continue;
+        if (sdf >= 0.0f) sdf = std::fmin(tr, sdf); else sdf = std::fmax(-tr, sdf);
+        const float wUpd = 1.0f;  // :465-466
+        BFVoxel& v = s.voxels[(size_t)entry.ptr + i];
+        BFVoxel nv;
+        float oc[3] = {(float)v.color[0], (float)v.color[1], (float)v.color[2]};
+        float cu[3] = {(float)cc[0], (float)cc[1], (float)cc[2]};
+        float res[3];
+        if (!deIntegrate) {
+            for (int k = 0; k < 3; k++) res[k] = (v.weight == 0.0f) ? cu[k] : 0.2f * cu[k] + 0.8f * oc[k];
+            for (int k = 0; k < 3; k++) {
+                float r = std::round(res[k]);
+                r = std::fmax(0.0f, std::fmin(r, 254.5f));
+                nv.color[k] = (uint8_t)r;
+            }
+            nv.color[3] = 255;
+            nv.sdf = (sdf * wUpd + v.sdf * v.weight) / (wUpd + v.weight);
+            nv.weight = std::min((float)s.hp.integrationWeightMax, wUpd + v.weight);
+        } else {
+            for (int k = 0; k < 3; k++) {
+                float r = (oc[k] * v.weight - cu[k] * wUpd) / (v.weight - wUpd);
+                r = std::round(r);
+                r = std::fmax(0.0f, std::fmin(r, 254.5f));
+                nv.color[k] = (uint8_t)r;
+            }
+            nv.color[3] = 255;
+            nv.sdf = (v.sdf * v.weight - sdf * wUpd) / (v.weight - wUpd);
+            nv.weight = std::max(0.0f, v.weight - wUpd);
+            if (nv.weight <= 0.001f) { nv.sdf = 0.0f; nv.color[0] = nv.color[1] = nv.color[2] = nv.color[3] = 0; nv.weight = 0.0f; }
+        }
+        v = nv;
+        updated++;
+    }
+}
+
+void setTransform(Scene& s, const float* T, const BFDepthCameraParams* cam) {
+    s.T = toM4(T);
+    s.Tinv = inverse(s.T);
+    std::memcpy(s.hp.rigidTransform.m, s.T.e, 64);
+    std::memcpy(s.hp.rigidTransformInverse.m, s.Tinv.e, 64);
+    s.cam = *cam;
+}
+
+}  // namespace
+
+struct ORScene { Scene s; };
+
+extern "C" {
+
+ORScene* or_scene_create(const BFHashParams* params) {
+    ORScene* o = new ORScene();
+    o->s.hp = *params;
+    Scene& s = o->s;
+    const size_t E = (size_t)params->hashNumBuckets * BF_HASH_BUCKET_SIZE;
+    s.hash.resize(E);
+    s.compact.resize(E);
+    s.heap.resize(params->numSDFBlocks);
+    s.voxels.resize((size_t)params->numSDFBlocks * BF_VOXELS_PER_BLOCK);
+    s.mutex.resize(params->hashNumBuckets);
+    s.decision.resize(E);
+    or_scene_reset(o);
+    return o;
+}
+
+void or_scene_destroy(ORScene* o) { delete o; }
+
+// CUDASceneRepHashSDF::reset (.h:147-155) -> resetCUDA (.cu:67-111)
+void or_scene_reset(ORScene* o) {
+    Scene& s = o->s;
+    const uint32_t B = s.hp.numSDFBlocks;
+    s.heapCounter = B - 1;
+    for (uint32_t i = 0; i < B; i++) s.heap[i] = B - i - 1;
+    for (auto& v : s.voxels) deleteVoxel(v);
+    for (auto& e : s.hash) deleteHashEntry(e);
+    for (auto& e : s.compact) deleteHashEntry(e);
+    resetMutex(s);
+    s.numOccupied = 0;
+    s.hp.numOccupiedBlocks = 0;
+    std::memset(&s.stats, 0, sizeof(s.stats));
+    float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    s.T = toM4(I);
+    s.Tinv = toM4(I);
+}
+
+// CUDASceneRepHashSDF::integrate (.h:65-83) / deIntegrate (.h:85-108)
+void or_scene_integrate(ORScene* o, const float T[16], const float* depth, const uint8_t* color,
+                        const BFDepthCameraParams* cam, int deintegrate, const uint32_t* bitMask) {
+    Scene& s = o->s;
+    setTransform(s, T, cam);
+    s.stats.integrateOps++;
+    if (!deintegrate) {
+        // alloc (.h:328-352): repeat {reset bucket mutex; alloc pass} until the heap free
+        // count is unchanged. Serially, a pass inserts at most one block per bucket (the
+        // bucket stays locked for the rest of the pass, VoxelUtilHashSDF.h:604-611).
+        s.stats.pixels += (uint64_t)cam->imageWidth * cam->imageHeight;
+        uint32_t prevFree = s.heapCounter + 1;
+        for (int pass = 0;; pass++) {
+            resetMutex(s);
+            for (uint32_t y = 0; y < cam->imageHeight; y++)
+                for (uint32_t x = 0; x < cam->imageWidth; x++) allocPixel(s, depth, x, y, bitMask, pass == 0);
+            uint32_t currFree = s.heapCounter + 1;
+            if (currFree == prevFree) break;
+            prevFree = currFree;
+        }
+        resetMutex(s);
+    }
+    compactify(s);
+    uint64_t updated = 0;
+#pragma omp parallel for reduction(+ : updated) schedule(dynamic, 64)
+    for (long b = 0; b < (long)s.numOccupied; b++) integrateBlock(s, s.compact[b], depth, color, deintegrate != 0, updated);
+    s.stats.voxelsUpdated += updated;
+}
+
+uint32_t or_scene_compactify(ORScene* o, const float T[16], const BFDepthCameraParams* cam) {
+    setTransform(o->s, T, cam);
+    return compactify(o->s);
+}
+
+// CUDASceneRepHashSDF::garbageCollect (.h:110-126): identify (.cu:584-631), mutex reset,
+// free (.cu:648-668) over the last compacted list. Free threads run serially in ascending
+// block-coordinate order (the canonical order the HIP build also uses for collision-list
+// deletes; simple in-bucket deletes are order-independent).
+void or_scene_garbage_collect(ORScene* o) {
+    Scene& s = o->s;
+    if (s.numOccupied == 0) return;
+    std::vector<BFHashEntry> victims;
+    for (uint32_t b = 0; b < s.numOccupied; b++) {
+        const BFHashEntry& e = s.compact[b];
+        uint32_t maxW = 0;
+        for (uint32_t i = 0; i < BF_VOXELS_PER_BLOCK; i++) {
+            uint32_t w = (uint32_t)s.voxels[(size_t)e.ptr + i].weight;  // max as uint (.cu:606)
+            maxW = std::max(maxW, w);
+        }
+        s.stats.gcBlocks++;
+        if (maxW == 0) victims.push_back(e);
+    }
+    std::sort(victims.begin(), victims.end(), [](const BFHashEntry& a, const BFHashEntry& b) {
+        if (a.x != b.x) return a.x < b.x;
+        if (a.y != b.y) return a.y < b.y;
+        return a.z < b.z;
+    });
+    resetMutex(s);
+    for (const BFHashEntry& e : victims) {
+        if (deleteHashEntryElement(s, {e.x, e.y, e.z})) {
+            for (uint32_t i = 0; i < BF_VOXELS_PER_BLOCK; i++) deleteVoxel(s.voxels[(size_t)e.ptr + i]);
+            s.stats.gcFreed++;
+        }
+    }
+}
+
+uint32_t or_scene_heap_free_count(const ORScene* o) { return o->s.heapCounter + 1; }  // .h:168-172
+uint32_t or_scene_num_occupied(const ORScene* o) { return o->s.numOccupied; }
+
+void or_scene_export(const ORScene* o, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels) {
+    const Scene& s = o->s;
+    if (hash) std::memcpy(hash, s.hash.data(), s.hash.size() * sizeof(BFHashEntry));
+    if (heap) std::memcpy(heap, s.heap.data(), s.heap.size() * sizeof(uint32_t));
+    if (heapCounter) *heapCounter = s.heapCounter;
+    if (voxels) std::memcpy(voxels, s.voxels.data(), s.voxels.size() * sizeof(BFVoxel));
+}
+
+void or_scene_export_visible(const ORScene* o, BFHashEntry* out) {
+    std::memcpy(out, o->s.compact.data(), o->s.numOccupied * sizeof(BFHashEntry));
+}
+
+void or_scene_get_stats(const ORScene* o, BFTsdfStats* out) { *out = o->s.stats; }
+
+// Config 1: one frame into a dense n^3 grid whose voxel (0,0,0) sits at virtual voxel
+// `origin`; same per-voxel arithmetic as integrateDepthMapKernel<false>.
+void or_dense_integrate(const float T[16], const float* depth, const uint8_t* color,
+                        const BFDepthCameraParams* cam, const BFHashParams* params,
+                        const int origin[3], int n, BFVoxel* grid) {
+    ORScene tmp;  // only hp/cam/T are used by integrateBlock
+    Scene& s = tmp.s;
+    s.hp = *params;
+    setTransform(s, T, cam);
+    const int nb = n / BF_SDF_BLOCK_SIZE;
+    s.voxels.assign((size_t)nb * nb * nb * BF_VOXELS_PER_BLOCK, BFVoxel{});
+    for (auto& v : s.voxels) deleteVoxel(v);
+    uint64_t upd = 0;
+    for (int bz = 0; bz < nb; bz++)
+        for (int by = 0; by < nb; by++)
+            for (int bx = 0; bx < nb; bx++) {
+                BFHashEntry e{};
+                e.x = origin[0] / 8 + bx; e.y = origin[1] / 8 + by; e.z = origin[2] / 8 + bz;
+                e.ptr = ((bz * nb + by) * nb + bx) * BF_VOXELS_PER_BLOCK;
+                integrateBlock(s, e, depth, color, false, upd);
+            }
+    for (int bz = 0; bz < nb; bz++)
+        for (int by = 0; by < nb; by++)
+            for (int bx = 0; bx < nb; bx++)
+                for (int i = 0; i < BF_VOXELS_PER_BLOCK; i++) {
+                    int x = bx * 8 + i % 8, y = by * 8 + (i % 64) / 8, z = bz * 8 + i / 64;
+                    grid[((size_t)z * n + y) * n + x] = s.voxels[(size_t)((bz * nb + by) * nb + bx) * 512 + i];
+                }
+}
+
+}  // extern "C"

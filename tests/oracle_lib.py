@@ -1,0 +1,192 @@
+"""ctypes binding of the CPU oracle (oracle/_build/libbf_oracle.so) — test infrastructure only."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from bundlefusion_amd import abi
+
+REPO = abi.REPO
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libbf_oracle.so")
+_lib = None
+
+
+def build_oracle() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "-j8"], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            build_oracle()
+        L = C.CDLL(ORACLE_LIB)
+        L.or_scene_create.restype = C.c_void_p
+        L.or_scene_create.argtypes = [C.c_void_p]
+        for n in ("or_scene_destroy", "or_scene_reset", "or_scene_garbage_collect"):
+            getattr(L, n).argtypes = [C.c_void_p]
+            getattr(L, n).restype = None
+        L.or_scene_integrate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.or_scene_integrate.restype = None
+        L.or_scene_compactify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_scene_compactify.restype = C.c_uint32
+        L.or_scene_heap_free_count.argtypes = [C.c_void_p]
+        L.or_scene_heap_free_count.restype = C.c_uint32
+        L.or_scene_num_occupied.argtypes = [C.c_void_p]
+        L.or_scene_num_occupied.restype = C.c_uint32
+        L.or_scene_export.argtypes = [C.c_void_p] * 5
+        L.or_scene_export.restype = None
+        L.or_scene_export_visible.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_scene_export_visible.restype = None
+        L.or_scene_get_stats.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_scene_get_stats.restype = None
+        L.or_matrix_inverse.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_matrix_inverse.restype = None
+        L.or_dense_integrate.argtypes = [C.c_void_p] * 6 + [C.c_int, C.c_void_p]
+        L.or_dense_integrate.restype = None
+        _lib = L
+    return _lib
+
+
+def _m(T) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(T, np.float32).reshape(16))
+
+
+class OracleScene:
+    """Serial CPU restatement of CUDASceneRepHashSDF (oracle/tsdf.cpp)."""
+
+    def __init__(self, params: abi.BFHashParams):
+        self.params = params
+        self.h = lib().or_scene_create(C.byref(params))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_scene_destroy(self.h)
+            self.h = None
+
+    def integrate(self, T, depth: np.ndarray, color: np.ndarray | None, cam, deintegrate=False):
+        depth = np.ascontiguousarray(depth, np.float32)
+        col = None if color is None else np.ascontiguousarray(color, np.uint8)
+        T = _m(T)
+        lib().or_scene_integrate(self.h, T.ctypes.data, depth.ctypes.data, None if col is None else col.ctypes.data,
+                                 C.byref(cam), int(deintegrate), None)
+
+    def deIntegrate(self, T, depth, color, cam):
+        self.integrate(T, depth, color, cam, deintegrate=True)
+
+    def garbageCollect(self):
+        lib().or_scene_garbage_collect(self.h)
+
+    def compactify(self, T, cam) -> int:
+        return lib().or_scene_compactify(self.h, _m(T).ctypes.data, C.byref(cam))
+
+    def getHeapFreeCount(self) -> int:
+        return lib().or_scene_heap_free_count(self.h)
+
+    def numOccupied(self) -> int:
+        return lib().or_scene_num_occupied(self.h)
+
+    def export(self):
+        E = self.params.hashNumBuckets * 4
+        B = self.params.numSDFBlocks
+        h = np.empty(E, abi.HASH_ENTRY_DTYPE)
+        heap = np.empty(B, np.uint32)
+        hc = C.c_uint32()
+        vox = np.empty(B * 512, abi.VOXEL_DTYPE)
+        lib().or_scene_export(self.h, h.ctypes.data, heap.ctypes.data, C.addressof(hc), vox.ctypes.data)
+        return h, heap, hc.value, vox
+
+    def export_visible(self) -> np.ndarray:
+        n = self.numOccupied()
+        out = np.empty(n, abi.HASH_ENTRY_DTYPE)
+        if n:
+            lib().or_scene_export_visible(self.h, out.ctypes.data)
+        return out
+
+    def stats(self) -> dict:
+        s = abi.BFTsdfStats()
+        lib().or_scene_get_stats(self.h, C.byref(s))
+        return {k: getattr(s, k) for k, _ in abi.BFTsdfStats._fields_}
+
+
+def matrix_inverse(T) -> np.ndarray:
+    out = np.empty(16, np.float32)
+    lib().or_matrix_inverse(_m(T).ctypes.data, out.ctypes.data)
+    return out.reshape(4, 4)
+
+
+def dense_integrate(T, depth, color, cam, params, origin, n) -> np.ndarray:
+    grid = np.empty(n * n * n, abi.VOXEL_DTYPE)
+    depth = np.ascontiguousarray(depth, np.float32)
+    color = np.ascontiguousarray(color, np.uint8)
+    org = np.asarray(origin, np.int32)
+    lib().or_dense_integrate(_m(T).ctypes.data, depth.ctypes.data, color.ctypes.data, C.byref(cam), C.byref(params),
+                             org.ctypes.data, n, grid.ctypes.data)
+    return grid.reshape(n, n, n)
+
+
+# ---- hash-state comparison helpers (shared by CPU and GPU tests) ----------------------------
+def blocks_of(hash_entries: np.ndarray) -> dict:
+    """{(x,y,z): ptr} of every allocated entry."""
+    occ = hash_entries[hash_entries["ptr"] != abi.FREE_ENTRY]
+    return {(int(e["x"]), int(e["y"]), int(e["z"])): int(e["ptr"]) for e in occ}
+
+
+def block_voxels(vox: np.ndarray, ptr: int) -> np.ndarray:
+    return vox[ptr: ptr + 512]
+
+
+def check_hash_invariants(params, hash_entries, heap, heap_counter):
+    """debugHash (CUDASceneRepHashSDF.h:179-314): no duplicate positions, heap/pool partition,
+    every entry reachable from its own bucket (slot or collision list)."""
+    B = params.numSDFBlocks
+    nb = params.hashNumBuckets
+    E = nb * 4
+    free = heap[: heap_counter + 1] if heap_counter != 0xFFFFFFFF else heap[:0]
+    assert len(set(free.tolist())) == len(free), "duplicate free pointers in heap"
+    occ_idx = np.nonzero(hash_entries["ptr"] != abi.FREE_ENTRY)[0]
+    assert not np.any(hash_entries["ptr"][occ_idx] == abi.LOCK_ENTRY), "entry left locked"
+    ptrs = hash_entries["ptr"][occ_idx] // 512
+    assert len(set(ptrs.tolist())) == len(ptrs), "two entries share a block"
+    assert not (set(ptrs.tolist()) & set(free.tolist())), "ptr both free and allocated"
+    assert len(ptrs) + len(free) == B, f"leak: {len(ptrs)} allocated + {len(free)} free != {B}"
+    pos = set()
+    for i in occ_idx:
+        e = hash_entries[i]
+        key = (int(e["x"]), int(e["y"]), int(e["z"]))
+        assert key not in pos, f"duplicate block {key}"
+        pos.add(key)
+        h = bucket_of(key, nb)
+        if i // 4 == h:
+            continue
+        # must be on bucket h's collision list
+        last = h * 4 + 3
+        j = last
+        found = False
+        for _ in range(params.hashMaxCollisionLinkedListSize + 1):
+            off = int(hash_entries[j]["offset"])
+            if off == 0:
+                break
+            j = (last + off) % E
+            if j == i:
+                found = True
+                break
+        assert found, f"entry {key} at {i} unreachable from bucket {h}"
+
+
+def bucket_of(key, num_buckets: int) -> int:
+    """computeHashPos (VoxelUtilHashSDF.h:225-234) in int32 wrapping arithmetic."""
+    def i32(v: int) -> int:
+        v &= 0xFFFFFFFF
+        return v - (1 << 32) if v >= (1 << 31) else v
+
+    x, y, z = (int(v) for v in key)
+    r = i32(i32(x * 73856093) ^ i32(y * 19349669) ^ i32(z * 83492791))
+    res = (abs(r) % num_buckets) * (1 if r >= 0 else -1)  # C % truncates toward zero
+    if res < 0:
+        res += num_buckets
+    return res

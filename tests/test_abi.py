@@ -1,0 +1,58 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/bf/bf.h declares,
+and the ctypes struct layouts match the header's static_asserts. No GPU calls."""
+import ctypes as C
+import os
+import subprocess
+
+import bundlefusion_amd as bfa
+from bundlefusion_amd import abi
+
+
+def test_library_exists_and_loads():
+    assert os.path.exists(abi.LIB_PATH)
+    L = bfa.lib()
+    assert L.bf_abi_version() == 1
+
+
+def test_every_declared_symbol_is_exported():
+    names = abi.header_functions()
+    assert len(names) >= 30
+    L = C.CDLL(abi.LIB_PATH)
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_exported_symbols_have_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", abi.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for n in abi.header_functions():
+        assert n in exported, n
+
+
+def test_struct_layouts():
+    assert C.sizeof(abi.BFHashParams) == 224
+    assert C.sizeof(abi.BFDepthCameraParams) == 32
+    assert C.sizeof(abi.BFRayCastParams) == 192
+    assert abi.HASH_ENTRY_DTYPE.itemsize == 32
+    assert abi.VOXEL_DTYPE.itemsize == 12
+    assert abi.ENTRYJ_DTYPE.itemsize == 32
+
+
+def test_error_path_without_device():
+    """A null handle returns an error status and a message instead of crashing."""
+    rc = bfa.lib().bf_scene_reset(None)
+    assert rc < 0
+    assert b"null" in bfa.lib().bf_last_error()
+
+
+def test_synthetic_stream_host():
+    scene = bfa.synth_scene(0)
+    cam = bfa.depth_camera(80, 60, fx=577.87 / 8, fy=577.87 / 8)
+    d1, c1 = bfa.synth_render_host(scene, bfa.synth_pose(3), cam, 1, 3)
+    d2, c2 = bfa.synth_render_host(scene, bfa.synth_pose(3), cam, 1, 3)
+    assert (d1 == d2).all() and (c1 == c2).all()
+    valid = d1[d1 > 0]
+    assert valid.size > 0.9 * d1.size
+    assert valid.min() >= 0.1 and valid.max() <= 4.0
+    # 1 mm quantisation (.sens ushort/1000 convention)
+    assert abs(valid * 1000 - (valid * 1000).round()).max() < 1e-2
