@@ -70,7 +70,6 @@ public:
     const int4* dVisible() const { return visible_.p; }
     const uint32_t* dCtrl() const { return ctrl_.p; }
     uint32_t* dCtrlMut() { return ctrl_.p; }
-    BFTsdfStats* dStats() { return stats_.p; }
     size_t deviceBytes() const;
 
 private:
@@ -88,7 +87,7 @@ private:
     DevBuf<int4> blockPos_;
     DevBuf<int4> visible_;
     DevBuf<uint32_t> ctrl_;
-    DevBuf<BFTsdfStats> stats_;
+    DevBuf<unsigned long long> stats_;  // [64 slots][16]
     DevBuf<unsigned long long> cand_;
     DevBuf<unsigned long long> candSet_;
     DevBuf<int> candSlot_;

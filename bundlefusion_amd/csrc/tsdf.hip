@@ -37,7 +37,7 @@ struct HashArgs {
     uint32_t* blockCount;
     int4* visible;
     uint32_t* ctrl;
-    BFTsdfStats* stats;
+    unsigned long long* stats;  // [STAT_SLOTS][16] counters, field order of BFTsdfStats
     uint32_t numBuckets, numEntries, numBlocks, maxList;
     float voxelSize, truncation, truncScale, maxIntegrationDistance, weightMax;
     uint32_t shardCount, shardIndex;
@@ -53,6 +53,32 @@ __device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     unsigned l = lane_id();
     return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS };
+constexpr int STAT_SLOTS = 64;
+
+// Workgroup-level counter flush: wave shuffle-reduce, LDS add, then one global atomic per
+// workgroup into one of 64 slots (no single hot word; summed on the host at query time).
+// Every thread of the workgroup must call it (it contains a barrier).
+__device__ void flush_stats2(unsigned long long* stats, int f0, unsigned long long v0, int f1, unsigned long long v1) {
+    __shared__ unsigned long long s_st[2];
+    if (threadIdx.x < 2) s_st[threadIdx.x] = 0;
+    __syncthreads();
+    for (int off = 32; off > 0; off >>= 1) {
+        v0 += __shfl_xor(v0, off);
+        v1 += __shfl_xor(v1, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (v0) atomicAdd(&s_st[0], v0);
+        if (v1) atomicAdd(&s_st[1], v1);
+    }
+    __syncthreads();
+    const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) % STAT_SLOTS) * 16;
+    if (threadIdx.x == 0) {
+        if (s_st[0]) atomicAdd(&stats[slot + f0], s_st[0]);
+        if (s_st[1] && f1 >= 0) atomicAdd(&stats[slot + f1], s_st[1]);
+    }
 }
 
 __device__ __forceinline__ void load_entry(const BFHashEntry* h, uint32_t i, int4& a, int4& b) {
@@ -133,12 +159,12 @@ __global__ void k_reset_heap(uint32_t* heap, int4* blockPos, uint32_t* blockCoun
 }
 
 // Per-op counter reset (replaces the reference's memset + D2H of d_hashCompactifiedCounter).
-__global__ void k_begin_op(uint32_t* ctrl, BFTsdfStats* stats) {
+__global__ void k_begin_op(uint32_t* ctrl, unsigned long long* stats) {
     if (threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
         ctrl[C_CAND] = 0;
         ctrl[C_OVF] = 0;
-        stats->integrateOps++;
+        stats[S_OPS]++;
     }
 }
 
@@ -230,13 +256,8 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
             tMax.y += tDelta.y;
         }
     }
-    // stats (one atomic per wave)
-    unsigned long long tot = emitted;
-    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
-    if (lane_id() == 0) {
-        atomicAdd((unsigned long long*)&A.stats->candidates, tot);
-        atomicAdd((unsigned long long*)&A.stats->pixels, 64ull);
-    }
+    const bool inImage = x < cam.imageWidth && y < cam.imageHeight;
+    flush_stats2(A.stats, S_CAND, emitted, S_PIXELS, inImage ? 1ull : 0ull);
 }
 
 // allocBlock, VoxelUtilHashSDF.h:549-655 (bucket path), lock-free: global dedup, CAS on the
@@ -315,9 +336,7 @@ __global__ __launch_bounds__(256) void k_alloc_insert(HashArgs A, const unsigned
             }
         }
     }
-    unsigned long long tot = allocated;
-    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
-    if (lane == 0 && tot) atomicAdd((unsigned long long*)&A.stats->allocated, tot);
+    flush_stats2(A.stats, S_ALLOC, allocated, -1, 0);
 }
 
 // allocBlock collision-list path (VoxelUtilHashSDF.h:573-654), serial: bucket-full candidates
@@ -375,7 +394,7 @@ __global__ void k_alloc_overflow(HashArgs A, const unsigned long long* ovf) {
         e.ptr = (int)(blk * BF_VOXELS_PER_BLOCK);
         A.blockPos[blk] = make_int4(pos.x, pos.y, pos.z, 1);
         if (blk + 1 > A.ctrl[C_HIGHWATER]) A.ctrl[C_HIGHWATER] = blk + 1;
-        A.stats->allocated++;
+        A.stats[S_ALLOC]++;
     }
 }
 
@@ -400,20 +419,17 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         const bool alloc = bp.w != 0;
         const bool keep = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
         const unsigned long long m = __ballot(keep);
-        scanned += __popcll(__ballot(alloc));
+        scanned += alloc ? 1 : 0;
         if (m) {
             const int leader = __ffsll((long long)m) - 1;
             uint32_t b0 = 0;
             if ((int)lane == leader) b0 = atomicAdd(&A.ctrl[C_VISIBLE], (uint32_t)__popcll(m));
             b0 = __shfl(b0, leader);
             if (keep) A.visible[b0 + __popcll(m & lanemask_lt())] = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
-            vis += __popcll(m);
+            if (keep) vis++;
         }
     }
-    if (lane == 0) {
-        atomicAdd((unsigned long long*)&A.stats->scanned, scanned);
-        atomicAdd((unsigned long long*)&A.stats->visible, vis);
-    }
+    flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
 }
 
 // integrateDepthMapKernel<deIntegrate>, CUDASceneRepHashSDF.cu:420-521. One wave per block:
@@ -432,69 +448,93 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
     unsigned long long updated = 0;
     for (uint32_t b = wave; b < nvis; b += nwaves) {
         const int4 e = A.visible[b];
-        const int bx = e.x * BF_SDF_BLOCK_SIZE, by = e.y * BF_SDF_BLOCK_SIZE, bz = e.z * BF_SDF_BLOCK_SIZE;
-        int dcount = 0;
-        uint32_t nupd = 0;
-#pragma unroll 2
+        const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
+        // phase 1: project the lane's 8 voxels and issue all depth gathers back to back
+        float depth[BF_SDF_BLOCK_SIZE], pz[BF_SDF_BLOCK_SIZE];
+        uint32_t pix[BF_SDF_BLOCK_SIZE];
+#pragma unroll
         for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
-            const f3 pf = xform(Tinv, vvox_to_world(bx + lx, by + ly, bz + z, A.voxelSize));
+            const f3 pf = xform(Tinv, vvox_to_world(bx, by, bz + z, A.voxelSize));
             const float sx = pf.x * cam.fx / pf.z + cam.mx;
             const float sy = pf.y * cam.fy / pf.z + cam.my;
             const uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
-            if (!(ux < W && uy < H)) continue;
-            if (!colorImg) continue;  // color stays MINF (:441-448)
-            const float depth = depthImg[uy * W + ux];
-            if (depth == -INFINITY) continue;
-            if (!(depth < A.maxIntegrationDistance)) continue;
-            float sdf = depth - pf.z;
-            const float tr = A.truncation + A.truncScale * depth;
-            if (!(fabsf(sdf) < tr)) continue;
+            const bool on = ux < W && uy < H && colorImg != nullptr;  // colour NULL: no update (:441-448)
+            pix[z] = on ? uy * W + ux : 0xFFFFFFFFu;
+            pz[z] = pf.z;
+            depth[z] = on ? depthImg[pix[z]] : -INFINITY;
+        }
+        // phase 2: band test, then issue the in-band voxel and colour loads together
+        float sdfv[BF_SDF_BLOCK_SIZE], osdf[BF_SDF_BLOCK_SIZE], ow[BF_SDF_BLOCK_SIZE];
+        uint32_t oc[BF_SDF_BLOCK_SIZE], cc[BF_SDF_BLOCK_SIZE];
+        uint32_t band = 0;
+#pragma unroll
+        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
+            const float dz = depth[z];
+            float sdf = dz - pz[z];
+            const float tr = A.truncation + A.truncScale * dz;
+            const bool in = dz != -INFINITY && dz < A.maxIntegrationDistance && fabsf(sdf) < tr;
             sdf = (sdf >= 0.0f) ? fminf(tr, sdf) : fmaxf(-tr, sdf);
-            const uint32_t c = colorImg[uy * W + ux];
+            sdfv[z] = sdf;
+            osdf[z] = 0.0f; ow[z] = 0.0f; oc[z] = 0u; cc[z] = 0u;
+            if (in) {
+                band |= 1u << z;
+                const BFVoxel* vp = A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane);
+                osdf[z] = vp->sdf;
+                ow[z] = vp->weight;
+                oc[z] = *reinterpret_cast<const uint32_t*>(vp->color);
+                cc[z] = colorImg[pix[z]];
+            }
+        }
+        // phase 3: running average (integrate) or its inverse (de-integrate), store
+        int dcount = 0;
+        uint32_t nupd = 0;
+#pragma unroll
+        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
+            if (!(band & (1u << z))) continue;
+            const uint32_t c = cc[z];
             const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
-            BFVoxel* vp = A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane);
-            const float osdf = vp->sdf, ow = vp->weight;
-            const uint32_t oc = *reinterpret_cast<const uint32_t*>(vp->color);
-            const float oc0 = (float)(oc & 0xFF), oc1 = (float)((oc >> 8) & 0xFF), oc2 = (float)((oc >> 16) & 0xFF);
+            const uint32_t o = oc[z];
+            const float oc0 = (float)(o & 0xFF), oc1 = (float)((o >> 8) & 0xFF), oc2 = (float)((o >> 16) & 0xFF);
+            const float w0 = ow[z], s0 = osdf[z], sdf = sdfv[z];
             float r0, r1, r2, nsdf, nw;
             uint32_t ncol;
             if (!DEINT) {
-                if (ow == 0.0f) { r0 = cu0; r1 = cu1; r2 = cu2; }
+                if (w0 == 0.0f) { r0 = cu0; r1 = cu1; r2 = cu2; }
                 else { r0 = 0.2f * cu0 + 0.8f * oc0; r1 = 0.2f * cu1 + 0.8f * oc1; r2 = 0.2f * cu2 + 0.8f * oc2; }
                 r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
                 r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
                 r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
                 ncol = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
-                nsdf = (sdf * wUpd + osdf * ow) / (wUpd + ow);
-                nw = fminf(A.weightMax, wUpd + ow);
+                nsdf = (sdf * wUpd + s0 * w0) / (wUpd + w0);
+                nw = fminf(A.weightMax, wUpd + w0);
             } else {
-                r0 = (oc0 * ow - cu0 * wUpd) / (ow - wUpd);
-                r1 = (oc1 * ow - cu1 * wUpd) / (ow - wUpd);
-                r2 = (oc2 * ow - cu2 * wUpd) / (ow - wUpd);
+                r0 = (oc0 * w0 - cu0 * wUpd) / (w0 - wUpd);
+                r1 = (oc1 * w0 - cu1 * wUpd) / (w0 - wUpd);
+                r2 = (oc2 * w0 - cu2 * wUpd) / (w0 - wUpd);
                 r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
                 r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
                 r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
                 ncol = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
-                nsdf = (osdf * ow - sdf * wUpd) / (ow - wUpd);
-                nw = fmaxf(0.0f, ow - wUpd);
+                nsdf = (s0 * w0 - sdf * wUpd) / (w0 - wUpd);
+                nw = fmaxf(0.0f, w0 - wUpd);
                 if (nw <= 0.001f) { nsdf = 0.0f; ncol = 0u; nw = 0.0f; }
             }
+            BFVoxel* vp = A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane);
             vp->sdf = nsdf;
             vp->weight = nw;
             *reinterpret_cast<uint32_t*>(vp->color) = ncol;
             // per-block count of voxels with (uint)weight != 0 (GC decision, :606/:625)
-            const bool was = ow >= 1.0f, now = nw >= 1.0f;
-            dcount += (int)now - (int)was;
+            dcount += (int)(nw >= 1.0f) - (int)(w0 >= 1.0f);
             nupd++;
         }
-        for (int off = 32; off > 0; off >>= 1) {
-            dcount += __shfl_xor(dcount, off);
-            nupd += __shfl_xor(nupd, off);
+        const unsigned long long anyChange = __ballot(dcount != 0);
+        if (anyChange) {
+            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
+            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[(uint32_t)e.w / BF_VOXELS_PER_BLOCK], (uint32_t)dcount);
         }
-        if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[(uint32_t)e.w / BF_VOXELS_PER_BLOCK], (uint32_t)dcount);
         updated += nupd;
     }
-    if (lane == 0 && updated) atomicAdd((unsigned long long*)&A.stats->voxelsUpdated, updated);
+    flush_stats2(A.stats, S_VOXELS, updated, -1, 0);
 }
 
 // garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
@@ -507,6 +547,7 @@ __global__ __launch_bounds__(256) void k_gc_identify(HashArgs A, int4* simple, u
         const int4 e = A.visible[b];
         const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
         if (A.blockCount[blk] != 0) continue;
+        if (A.blockPos[blk].w == 0) continue;  // already freed by an earlier GC on this list
         const uint32_t h = hash_bucket(e.x, e.y, e.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
         int slot = -1;
         uint32_t off = 0;
@@ -547,7 +588,7 @@ __global__ __launch_bounds__(256) void k_gc_free_simple(HashArgs A, const int4* 
         int4* vz = reinterpret_cast<int4*>(A.voxels + (size_t)blk * BF_VOXELS_PER_BLOCK);
         for (int q = lane; q < BF_VOXELS_PER_BLOCK * 12 / 16; q += 64) vz[q] = make_int4(0, 0, 0, 0);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stats->gcFreed, (unsigned long long)n);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.stats[S_GCFREED], (unsigned long long)n);
 }
 
 // deleteHashEntryElement collision-list cases, serial in ascending block-key order with the
@@ -624,12 +665,12 @@ __global__ void k_gc_free_list(HashArgs A, unsigned long long* listV) {
             freed++;
         }
     }
-    A.stats->gcFreed += freed;
+    A.stats[S_GCFREED] += freed;
 }
 
-__global__ void k_gc_begin(uint32_t* ctrl, BFTsdfStats* stats) {
+__global__ void k_gc_begin(uint32_t* ctrl, unsigned long long* stats) {
     if (threadIdx.x == 0) {
-        stats->gcBlocks += ctrl[C_VISIBLE];
+        stats[S_GCBLOCKS] += ctrl[C_VISIBLE];
         ctrl[C_GC_SIMPLE] = 0;
         ctrl[C_GC_LIST] = 0;
     }
@@ -639,7 +680,7 @@ __global__ void k_gc_begin(uint32_t* ctrl, BFTsdfStats* stats) {
 
 // ------------------------------------------------------------------------------------
 static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* heap, BFVoxel* vox, int4* bp, uint32_t* bc,
-                          int4* vis, uint32_t* ctrl, BFTsdfStats* st, const uint32_t* bitMask) {
+                          int4* vis, uint32_t* ctrl, unsigned long long* st, const uint32_t* bitMask) {
     HashArgs a;
     a.hash = hash; a.heap = heap; a.voxels = vox; a.blockPos = bp; a.blockCount = bc; a.visible = vis; a.ctrl = ctrl; a.stats = st;
     a.numBuckets = cfg.hp.hashNumBuckets;
@@ -679,7 +720,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     blockPos_.alloc(B_);
     visible_.alloc(B_);
     ctrl_.alloc(C_COUNT);
-    stats_.alloc(1);
+    stats_.alloc(STAT_SLOTS * 16);
     cand_.alloc(cfg_.candCapacity);
     candSet_.alloc(setSize);
     candSlot_.alloc(cfg_.candCapacity);
@@ -693,7 +734,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
-    BF_HIP(hipMemsetAsync(stats_.p, 0, sizeof(BFTsdfStats), stream_));
+    BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
     float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     std::memcpy(T_.m, I, 64);
     std::memcpy(Tinv_.m, I, 64);
@@ -803,13 +844,19 @@ uint32_t Scene::errorFlags() {
 }
 
 BFTsdfStats Scene::stats() {
-    BFTsdfStats s;
-    BF_HIP(hipMemcpyAsync(&s, stats_.p, sizeof(s), hipMemcpyDeviceToHost, stream_));
+    std::vector<unsigned long long> h(STAT_SLOTS * 16);
+    BF_HIP(hipMemcpyAsync(h.data(), stats_.p, stats_.bytes(), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
+    uint64_t sum[16] = {0};
+    for (int sl = 0; sl < STAT_SLOTS; sl++)
+        for (int f = 0; f < 16; f++) sum[f] += h[sl * 16 + f];
+    BFTsdfStats s;
+    static_assert(sizeof(BFTsdfStats) == 10 * 8, "stats layout");
+    std::memcpy(&s, sum, sizeof(s));
     return s;
 }
 
-void Scene::resetStats() { BF_HIP(hipMemsetAsync(stats_.p, 0, sizeof(BFTsdfStats), stream_)); }
+void Scene::resetStats() { BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_)); }
 
 void Scene::exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels) {
     if (hash) BF_HIP(hipMemcpyAsync(hash, hash_.p, hash_.bytes(), hipMemcpyDeviceToHost, stream_));
