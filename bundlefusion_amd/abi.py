@@ -136,3 +136,20 @@ def u32p(a: np.ndarray):
 
 def vp(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
+
+
+class BFCachedFrame(C.Structure):
+    _fields_ = [("depth", C.c_void_p), ("campos", C.c_void_p), ("normals", C.c_void_p), ("normalsU8", C.c_void_p),
+                ("intensity", C.c_void_p), ("intensityDeriv", C.c_void_p)]
+
+
+class BFSolverOptions(C.Structure):
+    _fields_ = [("denseDistThresh", C.c_float), ("denseNormalThresh", C.c_float), ("denseColorThresh", C.c_float),
+                ("denseColorGradientMin", C.c_float), ("denseDepthMin", C.c_float), ("denseDepthMax", C.c_float),
+                ("denseOverlapSubsample", C.c_uint32), ("verifyOptDistThresh", C.c_float)]
+
+
+class BFSolveResult(C.Structure):
+    _fields_ = [("gnIterations", C.c_uint32), ("pcgIterations", C.c_uint32), ("maxResidual", C.c_float),
+                ("maxResidualIndex", C.c_int32), ("energy", C.c_float), ("highResidualCount", C.c_uint32),
+                ("numDensePairs", C.c_uint32), ("error", C.c_uint32)]

@@ -1,6 +1,7 @@
 // api.cpp — the C ABI (include/bf/bf.h). Catches every C++ exception at the boundary and
 // turns it into a status code + bf_last_error() message.
 #include "../../include/bf/bf.h"
+#include "ba.h"
 #include "bf_runtime.h"
 #include "synth.h"
 #include "tsdf.h"
@@ -18,6 +19,11 @@ void synth_render_device(const BFSynthScene& sc, const BFMat4& T, const BFDepthC
 void synth_render_host(const BFSynthScene& sc, const BFMat4& T, const BFDepthCameraParams& cam, uint32_t noiseSeed,
                        uint32_t frame, float* depth, uint8_t* color);
 void synth_scene_default(uint32_t seed, BFSynthScene* out);
+uint32_t synth_correspondences(const BFSynthScene& sc, const float* poses, uint32_t K, const BFDepthCameraParams& cam,
+                               uint32_t maxPerPair, float minCovis, float noise, float outlierFrac, uint32_t seed,
+                               BFEntryJ* out, uint32_t cap);
+void synth_cache_frame(const BFSynthScene& sc, const BFMat4& T, const BFDepthCameraParams& cam, float* depth, float* campos,
+                       float* normals, uint8_t* normalsU8, float* intensity, float* intensityDeriv);
 
 // General cofactor inverse, cuda_SimpleMatrixUtil.h:980-1090 (host side of setLastRigidTransform,
 // CUDASceneRepHashSDF.h:128-134).
@@ -95,6 +101,11 @@ struct bf_timer {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
+struct bf_solver {
+    hipStream_t stream = nullptr;
+    Solver* solver = nullptr;
+};
+
 extern "C" {
 
 int bf_abi_version(void) { return BF_ABI_VERSION; }
@@ -128,22 +139,27 @@ int bf_free(void* dptr) {
 }
 int bf_memcpy_h2d(void* dst, const void* src, size_t bytes) {
     BF_TRY
+    BF_HIP(hipDeviceSynchronize());  // ordered after work on every scene/solver stream
     BF_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
     BF_CATCH
 }
 int bf_memcpy_d2h(void* dst, const void* src, size_t bytes) {
     BF_TRY
+    BF_HIP(hipDeviceSynchronize());  // ordered after work on every scene/solver stream
     BF_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     BF_CATCH
 }
 int bf_memcpy_d2d(void* dst, const void* src, size_t bytes) {
     BF_TRY
+    BF_HIP(hipDeviceSynchronize());  // ordered after work on every scene/solver stream
     BF_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
     BF_CATCH
 }
 int bf_memset(void* dptr, int value, size_t bytes) {
     BF_TRY
+    BF_HIP(hipDeviceSynchronize());
     BF_HIP(hipMemset(dptr, value, bytes));
+    BF_HIP(hipDeviceSynchronize());
     BF_CATCH
 }
 int bf_timer_create(bf_timer** out) {
@@ -326,6 +342,141 @@ int bf_synth_render_host(const BFSynthScene* scene, const float T[16], const BFD
     BF_TRY
     BF_REQUIRE(scene && T && cam && depth, BF_ERR_ARG, "null argument");
     synth_render_host(*scene, to_mat(T), *cam, noiseSeed, frame, depth, color);
+    BF_CATCH
+}
+int bf_synth_correspondences(const BFSynthScene* scene, const float* poses, uint32_t K, const BFDepthCameraParams* cam,
+                             uint32_t maxPerPair, float minCovis, float noise, float outlierFrac, uint32_t seed,
+                             BFEntryJ* out, uint32_t cap, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(scene && poses && cam && out && n, BF_ERR_ARG, "null argument");
+    *n = synth_correspondences(*scene, poses, K, *cam, maxPerPair, minCovis, noise, outlierFrac, seed, out, cap);
+    BF_CATCH
+}
+int bf_synth_cache_frame(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam, float* depth,
+                         float* campos, float* normals, uint8_t* normalsU8, float* intensity, float* intensityDeriv) {
+    BF_TRY
+    BF_REQUIRE(scene && T && cam && depth && campos && normals && normalsU8 && intensity && intensityDeriv, BF_ERR_ARG,
+               "null argument");
+    synth_cache_frame(*scene, to_mat(T), *cam, depth, campos, normals, normalsU8, intensity, intensityDeriv);
+    BF_CATCH
+}
+
+// ---- bundle adjustment ---------------------------------------------------------------------
+int bf_solver_create(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* o, bf_solver** out) {
+    BF_TRY
+    BF_REQUIRE(out, BF_ERR_ARG, "null argument");
+    SolverConfig cfg{};
+    cfg.maxImages = maxImages;
+    cfg.maxCorr = maxCorr;
+    cfg.denseDistThresh = (o && o->denseDistThresh > 0) ? o->denseDistThresh : 0.15f;
+    cfg.denseNormalThresh = (o && o->denseNormalThresh > 0) ? o->denseNormalThresh : 0.97f;
+    cfg.denseColorThresh = (o && o->denseColorThresh > 0) ? o->denseColorThresh : 0.1f;
+    cfg.denseColorGradientMin = (o && o->denseColorGradientMin > 0) ? o->denseColorGradientMin : 0.005f;
+    cfg.denseDepthMin = (o && o->denseDepthMin > 0) ? o->denseDepthMin : 0.5f;
+    cfg.denseDepthMax = (o && o->denseDepthMax > 0) ? o->denseDepthMax : 4.0f;
+    cfg.denseOverlapSubsample = (o && o->denseOverlapSubsample) ? o->denseOverlapSubsample : 4;
+    cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
+    bf_solver* s = new bf_solver();
+    try {
+        BF_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        s->solver = new Solver(cfg, s->stream);
+    } catch (...) {
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+        delete s;
+        throw;
+    }
+    *out = s;
+    BF_CATCH
+}
+int bf_solver_destroy(bf_solver* s) {
+    BF_TRY
+    if (s) {
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        delete s->solver;
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+        delete s;
+    }
+    BF_CATCH
+}
+int bf_solver_solve(bf_solver* s, BFEntryJ* corr, uint32_t nCorr, const int* valid, uint32_t nImages, uint32_t nNonLin,
+                    uint32_t nLin, const float* wSparse, const float* wDenseDepth, const float* wDenseColor,
+                    const BFCachedFrame* cache, uint32_t cacheW, uint32_t cacheH, const float intrinsics[4], float* rot,
+                    float* trans, int rebuildJT, int findMaxResidual) {
+    BF_TRY
+    BF_REQUIRE(s && valid && rot && trans && wSparse, BF_ERR_ARG, "null argument");
+    BF_REQUIRE(nCorr == 0 || corr, BF_ERR_ARG, "null correspondences");
+    SolveArgs a{};
+    a.corr = corr; a.numCorr = nCorr; a.valid = valid; a.numImages = nImages; a.nNonLin = nNonLin; a.nLin = nLin;
+    a.wSparse = wSparse; a.wDenseDepth = wDenseDepth; a.wDenseColor = wDenseColor;
+    a.cache = cache; a.cacheW = cacheW; a.cacheH = cacheH;
+    if (intrinsics) std::memcpy(a.intrinsics, intrinsics, 16);
+    a.rot = rot; a.trans = trans; a.rebuildJT = rebuildJT != 0; a.findMaxResidual = findMaxResidual != 0;
+    s->solver->solve(a);
+    BF_CATCH
+}
+int bf_solver_result(bf_solver* s, BFSolveResult* out) {
+    BF_TRY
+    BF_REQUIRE(s && out, BF_ERR_ARG, "null argument");
+    SolveResult r = s->solver->result();
+    out->gnIterations = r.gnIterations;
+    out->pcgIterations = r.pcgIterations;
+    out->maxResidual = r.maxResidual;
+    out->maxResidualIndex = r.maxResidualIndex;
+    out->energy = r.energy;
+    out->highResidualCount = r.highResidualCount;
+    out->numDensePairs = r.numDensePairs;
+    out->error = r.error;
+    BF_CATCH
+}
+int bf_solver_num_entries_per_row(bf_solver* s, const int** dptr) {
+    BF_TRY
+    BF_REQUIRE(s && dptr, BF_ERR_ARG, "null argument");
+    *dptr = s->solver->numEntriesPerRow();
+    BF_CATCH
+}
+int bf_solver_synchronize(bf_solver* s) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null solver");
+    BF_HIP(hipStreamSynchronize(s->stream));
+    BF_CATCH
+}
+int bf_solver_timer_start(bf_solver* s, bf_timer* t) {
+    BF_TRY
+    BF_REQUIRE(s && t, BF_ERR_ARG, "null argument");
+    BF_HIP(hipEventRecord(t->a, s->stream));
+    BF_CATCH
+}
+int bf_solver_timer_stop(bf_solver* s, bf_timer* t, float* ms) {
+    BF_TRY
+    BF_REQUIRE(s && t && ms, BF_ERR_ARG, "null argument");
+    BF_HIP(hipEventRecord(t->b, s->stream));
+    BF_HIP(hipEventSynchronize(t->b));
+    BF_HIP(hipEventElapsedTime(ms, t->a, t->b));
+    BF_CATCH
+}
+int bf_solver_matrices_to_poses(bf_solver* s, const float* T, uint32_t n, float* rot, float* trans, const int* valid) {
+    BF_TRY
+    BF_REQUIRE(s && T && rot && trans && valid, BF_ERR_ARG, "null argument");
+    matrices_to_poses(T, n, rot, trans, valid, s->stream);
+    BF_CATCH
+}
+int bf_solver_poses_to_matrices(bf_solver* s, const float* rot, const float* trans, uint32_t n, float* T, const int* valid) {
+    BF_TRY
+    BF_REQUIRE(s && T && rot && trans && valid, BF_ERR_ARG, "null argument");
+    poses_to_matrices(rot, trans, n, T, valid, s->stream);
+    BF_CATCH
+}
+int bf_solver_invalidate_image_pair(bf_solver* s, BFEntryJ* corr, uint32_t nCorr, uint32_t i, uint32_t j) {
+    BF_TRY
+    BF_REQUIRE(s && (corr || nCorr == 0), BF_ERR_ARG, "null argument");
+    invalidate_image_pair(corr, nCorr, i, j, s->stream);
+    BF_CATCH
+}
+int bf_solver_check_invalid_frames(bf_solver* s, int* valid, uint32_t nImages, BFEntryJ* corr, uint32_t nCorr,
+                                   int comprehensive) {
+    BF_TRY
+    BF_REQUIRE(s && valid, BF_ERR_ARG, "null argument");
+    check_invalid_frames(s->solver->numEntriesPerRow(), valid, nImages, corr, nCorr, comprehensive != 0, s->stream);
     BF_CATCH
 }
 

@@ -1,0 +1,109 @@
+// ba.h — MI355X sparse-then-dense bundle adjuster (replaces CUDASolverBundling,
+// Source/Solver/CUDASolverBundling.h/.cpp, and solveBundlingStub, Source/Solver/SolverBundling.cu).
+//
+// Device layout (all resident in HBM, sized for maxImages / maxCorr at construction):
+//   rowCount/rowStart/rowLen   per-image CSR of correspondence indices, built deterministically
+//                              (ascending correspondence index, as a serial replay of the
+//                              reference's atomic table build, SolverBundling.cu:1226-1248)
+//   entries                    per row entry, rebuilt each GN iteration: {T_self*p_self, other},
+//                              {T_other*p_other} — 32 B, streamed contiguously by the PCG loop
+//   vec                        per-image 8-float vectors: x is the caller's (rot, trans);
+//                              delta, r, z, p, Ap, M (Jacobi preconditioner)
+//   dense                      block-sparse JtJ: per-image 6x6 diagonal blocks, per-pair 6x6
+//                              off-diagonal blocks, Jtr (instead of the reference's (6N)^2 matrix)
+//   ctrl                       device-resident solver state (tickets, early-exit flags, scalars)
+// A solve is enqueued asynchronously on the solver's stream: PCG early exit and GN convergence
+// are evaluated on the device, so there is no host round trip inside solve (the reference
+// copies scanAlpha to the host every PCG iteration, SolverBundling.cu:1089).
+#pragma once
+#include "bf_math.h"
+#include "bf_runtime.h"
+
+namespace bf {
+
+struct SolverConfig {
+    uint32_t maxImages;
+    uint32_t maxCorr;
+    float denseDistThresh;        // s_denseDistThresh 0.15
+    float denseNormalThresh;      // s_denseNormalThresh 0.97
+    float denseColorThresh;       // s_denseColorThresh 0.1
+    float denseColorGradientMin;  // s_denseColorGradientMin 0.005
+    float denseDepthMin;          // s_denseDepthMin 0.5
+    float denseDepthMax;          // s_denseDepthMax 4.0
+    uint32_t denseOverlapSubsample;  // s_denseOverlapCheckSubsampleFactor 4
+    float verifyOptDistThresh;    // 0.02 (CUDASolverBundling.cpp:34)
+};
+
+struct SolveArgs {
+    BFEntryJ* corr;
+    uint32_t numCorr;
+    const int* valid;
+    uint32_t numImages;
+    uint32_t nNonLin, nLin;
+    const float* wSparse;  // host arrays [nNonLin]
+    const float* wDenseDepth;
+    const float* wDenseColor;
+    const BFCachedFrame* cache;  // device array [numImages] or null
+    uint32_t cacheW, cacheH;
+    float intrinsics[4];
+    float* rot;    // device float3[numImages], in/out
+    float* trans;  // device float3[numImages], in/out
+    bool rebuildJT;
+    bool findMaxResidual;
+};
+
+struct SolveResult {
+    uint32_t gnIterations;
+    uint32_t pcgIterations;
+    float maxResidual;
+    int32_t maxResidualIndex;
+    float energy;
+    uint32_t highResidualCount;
+    uint32_t numDensePairs;
+    uint32_t error;
+};
+
+class Solver {
+public:
+    Solver(const SolverConfig& cfg, hipStream_t stream);
+    ~Solver();
+    void solve(const SolveArgs& a);       // async
+    SolveResult result();                 // synchronizes
+    const int* numEntriesPerRow() const { return rowCount_.p; }  // getVarToCorrNumEntriesPerRow
+    hipStream_t stream() const { return stream_; }
+    const SolverConfig& config() const { return cfg_; }
+    size_t deviceBytes() const;
+
+private:
+    SolverConfig cfg_;
+    hipStream_t stream_;
+    uint32_t maxCorrPerImage_;
+    uint32_t maxPairs_;
+    int numCUs_;
+    DevBuf<int> rowCount_, rowStart_, rowLen_, fill_;
+    DevBuf<int> rowTmp_, rowIdx_;
+    DevBuf<float4> entries_;
+    DevBuf<float> vec_;     // [N][8] per field
+    DevBuf<float> img_;     // per-image scalars [2][N]
+    DevBuf<float> T_;       // [N][16]
+    DevBuf<float> Tinv_;    // [N][16]
+    DevBuf<uint32_t> ctrl_;
+    DevBuf<float> part_;    // per-workgroup partials
+    DevBuf<int> partIdx_;
+    DevBuf<uint2> pairs_;
+    DevBuf<float> pairW_;
+    DevBuf<float> pairBlk_;  // [maxPairs][36]
+    DevBuf<float> diag_;     // [N][36]
+    DevBuf<float> jtr_;      // [N][6]
+    DevBuf<float> apDense_;  // [N][8]
+};
+
+// SBA.cu:75-119 — float4x4 <-> (rot, trans) for valid images
+void matrices_to_poses(const float* T, uint32_t n, float* rot, float* trans, const int* valid, hipStream_t s);
+void poses_to_matrices(const float* rot, const float* trans, uint32_t n, float* T, const int* valid, hipStream_t s);
+// SIFTImageManager.cu:692-793
+void invalidate_image_pair(BFEntryJ* corr, uint32_t n, uint32_t i, uint32_t j, hipStream_t s);
+void check_invalid_frames(const int* numEntries, int* valid, uint32_t numImages, BFEntryJ* corr, uint32_t nCorr,
+                          bool comprehensive, hipStream_t s);
+
+}  // namespace bf

@@ -1,0 +1,956 @@
+// ba.hip — gfx950 kernels + host class for the bundle adjuster (see ba.h for the layout).
+//
+// Reference: Source/Solver/SolverBundling.cu, SolverBundlingEquationsLie.h,
+// SolverBundlingDenseUtil.h, LieDerivUtil.h (cited per kernel below).
+//
+// The sparse term is rewritten around two identities of the reference's Lie Jacobian
+// (evalLie_dAlpha/dBeta/dGamma, LieDerivUtil.h:231-242):
+//   da*w.x + db*w.y + dc*w.z = w x P      and      (da.g, db.g, dc.g) = P x g
+// so with P_s = T_self p_self and P_o = T_other p_other fixed for a GN iteration, one row entry of
+// image v contributes   g = w[(pRot_v x P_s + pTrans_v) - (pRot_o x P_o + pTrans_o)],
+//   Ap_rot(v) += P_s x g,   Ap_trans(v) += g
+// (applyJDevice + applyJTDevice, SolverBundlingEquationsLie.h:154-228, with the +-1 sign of the
+// row folded in). The PCG loop streams 32 B per row entry and gathers only the N-sized p vector.
+#include "ba.h"
+#include "lie.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace bf {
+
+namespace {
+
+constexpr float FLOAT_EPSILON = 0.000001f;  // Source/SolverUtil.h:9
+constexpr int WG = 256;
+constexpr int SORT_CAP = 8192;  // LDS row sort capacity
+
+enum VecField { V_DELTA = 0, V_R, V_Z, V_P, V_AP, V_M, V_NUM };
+enum CtrlWord {
+    K_TICKET = 0, K_PCG_DONE, K_GN_DONE, K_GN_ITERS, K_PCG_ITERS, K_RDOTZ, K_NPAIRS, K_LAST_W,
+    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_COUNT = 16
+};
+
+struct BA {
+    BFEntryJ* corr;
+    uint32_t nCorr;
+    const int* valid;
+    uint32_t N, maxN, cap;
+    int *rowCount, *rowStart, *rowLen, *fill, *rowTmp, *rowIdx;
+    float4* entries;
+    float* vec;
+    float* img;
+    float* T;
+    float* Tinv;
+    uint32_t* ctrl;
+    float* part;
+    int* partIdx;
+    float* rot;
+    float* trans;
+    uint2* pairs;
+    float* pairW;
+    float* pairBlk;
+    float* diag;
+    float* jtr;
+    float* apDense;
+    uint32_t maxPairs;
+    const BFCachedFrame* cache;
+    uint32_t cw, ch;
+    float fx, fy, mx, my;
+    float distT, normT, colT, gradMin, dmin, dmax, verifyT;
+    uint32_t sub;
+};
+
+__device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ float* vptr(const BA& a, int field, uint32_t v) { return a.vec + ((size_t)field * a.maxN + v) * 8; }
+__device__ __forceinline__ void vload(const BA& a, int field, uint32_t v, f3& r, f3& t) {
+    const float4* p = reinterpret_cast<const float4*>(vptr(a, field, v));
+    float4 x = p[0], y = p[1];
+    r = mk3(x.x, x.y, x.z);
+    t = mk3(y.x, y.y, y.z);
+}
+__device__ __forceinline__ void vstore(const BA& a, int field, uint32_t v, f3 r, f3 t) {
+    float4* p = reinterpret_cast<float4*>(vptr(a, field, v));
+    p[0] = make_float4(r.x, r.y, r.z, 0.0f);
+    p[1] = make_float4(t.x, t.y, t.z, 0.0f);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ float ctrlf(const uint32_t* c, int k) { return __uint_as_float(c[k]); }
+__device__ __forceinline__ m4 loadm4(const float* p) {
+    m4 m;
+    const float4* q = reinterpret_cast<const float4*>(p);
+    for (int r = 0; r < 4; r++) {
+        float4 v = q[r];
+        m.e[r * 4 + 0] = v.x; m.e[r * 4 + 1] = v.y; m.e[r * 4 + 2] = v.z; m.e[r * 4 + 3] = v.w;
+    }
+    return m;
+}
+__device__ __forceinline__ bool corr_valid(const BFEntryJ& e) { return e.imgIdx_i != BF_INVALID_IMAGE; }
+
+// "Last workgroup" hand-off (MI355X_MICROARCH.md visibility rules): every workgroup publishes with
+// an agent-scope release + ticket; the last arriver acquires before reading everyone's data.
+__device__ bool last_block(uint32_t* ticket) {
+    __shared__ int isLast;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned t = atomicAdd(ticket, 1u);
+        isLast = (t == gridDim.x * gridDim.y - 1) ? 1 : 0;
+        if (isLast) __threadfence();
+    }
+    __syncthreads();
+    return isLast != 0;
+}
+
+// deterministic block reduction (fixed tree) of one float per thread
+__device__ float block_sum(float v, float* sh) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+        __syncthreads();
+    }
+    const float r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+// ---- correspondence table (BuildVariablesToCorrespondencesTableDevice, SolverBundling.cu:1226-1248) ----
+__global__ void k_count(BA a) {
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < a.nCorr; c += gridDim.x * blockDim.x) {
+        const BFEntryJ e = a.corr[c];
+        if (!corr_valid(e)) continue;
+        atomicAdd(&a.rowCount[e.imgIdx_i], 1);
+        atomicAdd(&a.rowCount[e.imgIdx_j], 1);
+    }
+}
+__global__ void k_scan(BA a) {  // one workgroup: exclusive scan of rowCount -> rowStart
+    __shared__ int sh[WG];
+    int carry = 0;
+    for (uint32_t base = 0; base < a.N; base += WG) {
+        const uint32_t v = base + threadIdx.x;
+        const int c = v < a.N ? a.rowCount[v] : 0;
+        sh[threadIdx.x] = c;
+        __syncthreads();
+        for (int off = 1; off < WG; off <<= 1) {
+            int t = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (v < a.N) { a.rowStart[v] = carry + sh[threadIdx.x] - c; a.fill[v] = 0; }
+        carry += sh[WG - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.rowStart[a.N] = carry;
+}
+__global__ void k_fill(BA a) {
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < a.nCorr; c += gridDim.x * blockDim.x) {
+        const BFEntryJ e = a.corr[c];
+        if (!corr_valid(e)) continue;
+        const int k0 = atomicAdd(&a.fill[e.imgIdx_i], 1);
+        a.rowTmp[a.rowStart[e.imgIdx_i] + k0] = (int)c;
+        const int k1 = atomicAdd(&a.fill[e.imgIdx_j], 1);
+        a.rowTmp[a.rowStart[e.imgIdx_j] + k1] = (int)c;
+    }
+}
+// Sort each row by correspondence index (the serial order of the reference's table build), then
+// apply the per-image cap: a correspondence ranked >= cap in either of its rows is invalidated.
+__global__ __launch_bounds__(WG) void k_sort_rows(BA a) {
+    __shared__ int sh[SORT_CAP];
+    const uint32_t v = blockIdx.x;
+    if (v >= a.N) return;
+    const int n = a.rowCount[v], s0 = a.rowStart[v];
+    if (n > SORT_CAP) { if (threadIdx.x == 0) atomicOr(&a.ctrl[K_ERROR], 1u); return; }
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int k = threadIdx.x; k < P; k += WG) sh[k] = k < n ? a.rowTmp[s0 + k] : 0x7FFFFFFF;
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int k = threadIdx.x; k < P; k += WG) {
+                const int p2 = k ^ stride;
+                if (p2 > k) {
+                    const bool up = (k & size) == 0;
+                    const int x = sh[k], y = sh[p2];
+                    if ((x > y) == up) { sh[k] = y; sh[p2] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int k = threadIdx.x; k < n; k += WG) {
+        a.rowTmp[s0 + k] = sh[k];
+        if ((uint32_t)k >= a.cap) {  // invalidate (setInvalid, SolverBundling.cu:1241-1245)
+            a.corr[sh[k]].imgIdx_i = BF_INVALID_IMAGE;
+            a.corr[sh[k]].imgIdx_j = BF_INVALID_IMAGE;
+        }
+    }
+}
+// keep the entries that survived the cap (stable), rowLen = kept count
+__global__ __launch_bounds__(WG) void k_compact_rows(BA a) {
+    __shared__ int base;
+    const uint32_t v = blockIdx.x;
+    if (v >= a.N) return;
+    const int n = min(a.rowCount[v], (int)a.cap), s0 = a.rowStart[v];
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    for (int k0 = 0; k0 < n; k0 += WG) {
+        const int k = k0 + threadIdx.x;
+        bool keep = false;
+        int c = 0;
+        if (k < n) { c = a.rowTmp[s0 + k]; keep = corr_valid(a.corr[c]); }
+        __shared__ int cnt[WG / 64];
+        const unsigned long long m = __ballot(keep);
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) cnt[w] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int q = 0; q < w; q++) off += cnt[q];
+        const unsigned l = lane_id();
+        if (keep) a.rowIdx[s0 + off + __popcll(m & ((l == 0) ? 0ull : (~0ull >> (64 - l))))] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) { int t = 0; for (int q = 0; q < WG / 64; q++) t += cnt[q]; base += t; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.rowLen[v] = base;
+}
+
+// ---- per GN iteration -------------------------------------------------------------------------
+// convertLiePosesToMatricesCU (SolverBundling.cu:1114-1121); also resets the PCG state of this
+// GN iteration. gated: no-op once the GN loop converged on the device.
+__global__ void k_transforms(BA a, float wSparse, int useDense, int gated, int setState) {
+    if (gated && a.ctrl[K_GN_DONE]) return;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.N; v += gridDim.x * blockDim.x) {
+        const m4 T = pose_to_matrix(mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                                    mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]));
+        const m4 Ti = inverse44(T);
+        float4* t = reinterpret_cast<float4*>(a.T + (size_t)v * 16);
+        float4* ti = reinterpret_cast<float4*>(a.Tinv + (size_t)v * 16);
+        for (int r = 0; r < 4; r++) {
+            t[r] = make_float4(T.e[r * 4], T.e[r * 4 + 1], T.e[r * 4 + 2], T.e[r * 4 + 3]);
+            ti[r] = make_float4(Ti.e[r * 4], Ti.e[r * 4 + 1], Ti.e[r * 4 + 2], Ti.e[r * 4 + 3]);
+        }
+        float4* ad = reinterpret_cast<float4*>(a.apDense + (size_t)v * 8);
+        ad[0] = make_float4(0, 0, 0, 0);
+        ad[1] = make_float4(0, 0, 0, 0);
+    }
+    if (setState && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ctrl[K_PCG_DONE] = 0;
+        a.ctrl[K_TICKET] = 0;
+        a.ctrl[K_LAST_W] = __float_as_uint(wSparse);
+        a.ctrl[K_USE_DENSE] = (uint32_t)useDense;
+    }
+}
+
+// world points of every row entry for this GN iteration: {T_self p_self, other}, {T_other p_other}
+__global__ __launch_bounds__(WG) void k_entries(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+        const int s0 = a.rowStart[v], n = a.rowLen[v];
+        for (int k = lane; k < n; k += 64) {
+            const BFEntryJ e = a.corr[a.rowIdx[s0 + k]];
+            const bool isI = (e.imgIdx_i == v);
+            const uint32_t other = isI ? e.imgIdx_j : e.imgIdx_i;
+            const f3 ps = isI ? mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z) : mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z);
+            const f3 po = isI ? mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z) : mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z);
+            const f3 Ps = xf(loadm4(a.T + (size_t)v * 16), ps);
+            const f3 Po = xf(loadm4(a.T + (size_t)other * 16), po);
+            a.entries[2 * (s0 + k)] = make_float4(Ps.x, Ps.y, Ps.z, __uint_as_float(other));
+            a.entries[2 * (s0 + k) + 1] = make_float4(Po.x, Po.y, Po.z, 0.0f);
+        }
+    }
+}
+
+// evalMinusJTFDevice (SolverBundlingEquationsLie.h:63-148) + PCGInit_Kernel1/2 (SolverBundling.cu:755-794)
+__global__ __launch_bounds__(WG) void k_init(BA a, float wSparse) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+        const int s0 = a.rowStart[v], n = a.rowLen[v];
+        float rr[3] = {0, 0, 0}, rt[3] = {0, 0, 0}, pr[3] = {0, 0, 0};
+        for (int k = lane; k < n; k += 64) {
+            const float4 A = a.entries[2 * (s0 + k)], B = a.entries[2 * (s0 + k) + 1];
+            const f3 Ps = mk3(A.x, A.y, A.z), Po = mk3(B.x, B.y, B.z);
+            const f3 r = Ps - Po;         // sign * (T_i p_i - T_j p_j)
+            const f3 c = cross3(Ps, r);   // (dot(da,r), dot(db,r), dot(dc,r)) of P_s
+            rr[0] += c.x; rr[1] += c.y; rr[2] += c.z;
+            rt[0] += r.x; rt[1] += r.y; rt[2] += r.z;
+            pr[0] += Ps.z * Ps.z + Ps.y * Ps.y;  // |dAlpha|^2
+            pr[1] += Ps.z * Ps.z + Ps.x * Ps.x;  // |dBeta|^2
+            pr[2] += Ps.y * Ps.y + Ps.x * Ps.x;  // |dGamma|^2
+        }
+        for (int q = 0; q < 3; q++) { rr[q] = wave_sum(rr[q]); rt[q] = wave_sum(rt[q]); pr[q] = wave_sum(pr[q]); }
+        if (lane == 0) {
+            const float cnt = (float)n;
+            f3 resR = mk3(-wSparse * rr[0], -wSparse * rr[1], -wSparse * rr[2]);
+            f3 resT = mk3(-wSparse * rt[0], -wSparse * rt[1], -wSparse * rt[2]);
+            if (useDense) {
+                const float* j = a.jtr + (size_t)v * 6;
+                resR = resR - mk3(j[3], j[4], j[5]);
+                resT = resT - mk3(j[0], j[1], j[2]);
+            }
+            auto inv = [](float x) { return x > FLOAT_EPSILON ? 1.0f / x : 1.0f; };
+            const f3 mR = mk3(inv(pr[0]), inv(pr[1]), inv(pr[2]));
+            const f3 mT = mk3(inv(cnt), inv(cnt), inv(cnt));
+            const f3 pR = mul3(mR, resR), pT = mul3(mT, resT);
+            vstore(a, V_M, v, mR, mT);
+            vstore(a, V_R, v, resR, resT);
+            vstore(a, V_P, v, pR, pT);
+            vstore(a, V_DELTA, v, mk3(0, 0, 0), mk3(0, 0, 0));
+            a.img[v] = dot3(resR, pR) + dot3(resT, pT);
+        }
+    }
+    if (last_block(&a.ctrl[K_TICKET])) {
+        float s = 0.0f;
+        for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) s += a.img[v];
+        s = block_sum(s, sh);
+        if (threadIdx.x == 0) {
+            a.ctrl[K_RDOTZ] = __float_as_uint(s);
+            a.ctrl[K_TICKET] = 0;
+            vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
+        }
+    }
+}
+
+// One PCG iteration (PCGIteration, SolverBundling.cu:1024-1108) in one launch: every wave
+// computes Ap for its rows (sparse JtJp + dense diagonal block), waves also apply the dense
+// off-diagonal pair blocks; the last workgroup then does the global dot products and the
+// alpha / beta updates (Kernel1b, Kernel2, Kernel3) and the Lie update on the exiting iteration.
+__global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int nLin) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+        const int s0 = a.rowStart[v], n = a.rowLen[v];
+        f3 pRv, pTv;
+        vload(a, V_P, v, pRv, pTv);
+        float ar[3] = {0, 0, 0}, at[3] = {0, 0, 0};
+        if (wSparse > 0.0f) {
+            for (int k = lane; k < n; k += 64) {
+                const float4 A = a.entries[2 * (s0 + k)], B = a.entries[2 * (s0 + k) + 1];
+                const f3 Ps = mk3(A.x, A.y, A.z), Po = mk3(B.x, B.y, B.z);
+                const uint32_t o = __float_as_uint(A.w);
+                f3 pRo, pTo;
+                vload(a, V_P, o, pRo, pTo);
+                const f3 g = (cross3(pRv, Ps) + pTv - (cross3(pRo, Po) + pTo)) * wSparse;
+                const f3 c = cross3(Ps, g);
+                ar[0] += c.x; ar[1] += c.y; ar[2] += c.z;
+                at[0] += g.x; at[1] += g.y; at[2] += g.z;
+            }
+            for (int q = 0; q < 3; q++) { ar[q] = wave_sum(ar[q]); at[q] = wave_sum(at[q]); }
+        }
+        if (lane == 0) {
+            f3 apR = mk3(ar[0], ar[1], ar[2]), apT = mk3(at[0], at[1], at[2]);
+            if (useDense) {  // diagonal block [trans | rot] x [pTrans | pRot]
+                const float* D = a.diag + (size_t)v * 36;
+                const float pv[6] = {pTv.x, pTv.y, pTv.z, pRv.x, pRv.y, pRv.z};
+                float o6[6];
+                for (int r = 0; r < 6; r++) {
+                    float s = 0.0f;
+                    for (int c = 0; c < 6; c++) s += D[r * 6 + c] * pv[c];
+                    o6[r] = s;
+                }
+                apT = apT + mk3(o6[0], o6[1], o6[2]);
+                apR = apR + mk3(o6[3], o6[4], o6[5]);
+            }
+            vstore(a, V_AP, v, apR, apT);
+        }
+    }
+    if (useDense) {  // off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j)
+        const uint32_t np = a.ctrl[K_NPAIRS];
+        for (uint32_t k = wave; k < np; k += nw) {
+            if (a.pairW[k] == 0.0f) continue;
+            const uint2 pr = a.pairs[k];
+            const float* Bk = a.pairBlk + (size_t)k * 36;
+            f3 r, t;
+            float o = 0.0f;
+            if (lane < 6) {
+                vload(a, V_P, pr.x, r, t);
+                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+                for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
+                if (pr.y > 0) atomicAdd(&a.apDense[(size_t)pr.y * 8 + (lane < 3 ? 4 + lane : lane - 3)], o);
+            } else if (lane < 12) {
+                vload(a, V_P, pr.y, r, t);
+                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+                const int c0 = lane - 6;
+                for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
+                if (pr.x > 0) atomicAdd(&a.apDense[(size_t)pr.x * 8 + (c0 < 3 ? 4 + c0 : c0 - 3)], o);
+            }
+        }
+    }
+    if (!last_block(&a.ctrl[K_TICKET])) return;
+    // ---- finisher (one workgroup): Kernel1b, Kernel2, host early-out test, Kernel3 ----
+    float d = 0.0f;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+        f3 pR, pT, aR, aT;
+        vload(a, V_P, v, pR, pT);
+        vload(a, V_AP, v, aR, aT);
+        if (useDense) {
+            float4* ad = reinterpret_cast<float4*>(a.apDense + (size_t)v * 8);
+            const float4 x = ad[0], y = ad[1];
+            aR = aR + mk3(x.x, x.y, x.z);
+            aT = aT + mk3(y.x, y.y, y.z);
+            ad[0] = make_float4(0, 0, 0, 0);
+            ad[1] = make_float4(0, 0, 0, 0);
+            vstore(a, V_AP, v, aR, aT);
+        }
+        d += dot3(pR, aR) + dot3(pT, aT);
+    }
+    const float pAp = block_sum(d, sh);
+    const float rDotzOld = ctrlf(a.ctrl, K_RDOTZ);
+    const float alpha = (pAp > FLOAT_EPSILON) ? rDotzOld / pAp : 0.0f;
+    float b = 0.0f;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+        f3 dR, dT, pR, pT, rR, rT, aR, aT, mR, mT;
+        vload(a, V_DELTA, v, dR, dT);
+        vload(a, V_P, v, pR, pT);
+        vload(a, V_R, v, rR, rT);
+        vload(a, V_AP, v, aR, aT);
+        vload(a, V_M, v, mR, mT);
+        dR = dR + alpha * pR;
+        dT = dT + alpha * pT;
+        rR = rR - alpha * aR;
+        rT = rT - alpha * aT;
+        const f3 zR = mul3(mR, rR), zT = mul3(mT, rT);
+        vstore(a, V_DELTA, v, dR, dT);
+        vstore(a, V_R, v, rR, rT);
+        vstore(a, V_Z, v, zR, zT);
+        b += dot3(zR, rR) + dot3(zT, rT);
+    }
+    const float rDotzNew = block_sum(b, sh);
+    const bool last = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+    const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew / rDotzOld : 0.0f;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+        f3 zR, zT, pR, pT;
+        vload(a, V_Z, v, zR, zT);
+        vload(a, V_P, v, pR, pT);
+        vstore(a, V_P, v, zR + beta * pR, zT + beta * pT);
+        if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
+            f3 dR, dT;
+            vload(a, V_DELTA, v, dR, dT);
+            f3 nr, nt;
+            lie_update(dR, dT, mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                       mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
+            a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
+            a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+        }
+    }
+    if (threadIdx.x == 0) {
+        a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
+        a.ctrl[K_PCG_ITERS]++;
+        if (last) a.ctrl[K_PCG_DONE] = 1;
+        a.ctrl[K_TICKET] = 0;
+    }
+}
+
+// EvalGNConvergence (SolverBundling.cu:694-749) + the early-out test of solveBundlingStub (:1204-1210)
+__global__ void k_gn_end(BA a, int gnIndex, int nNonLin) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE]) return;
+    float m = 0.0f;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+        if (a.valid[v] == 0) continue;
+        f3 dR, dT;
+        vload(a, V_DELTA, v, dR, dT);
+        const float r = fmaxf(fmaxf(fmaxf(fabsf(dR.x), fabsf(dT.x)), fmaxf(fabsf(dR.y), fabsf(dT.y))), fmaxf(fabsf(dR.z), fabsf(dT.z)));
+        m = fmaxf(m, r);
+    }
+    sh[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmaxf(sh[threadIdx.x], sh[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.ctrl[K_GN_ITERS]++;
+        if (gnIndex < nNonLin - 1 && sh[0] < 0.005f) a.ctrl[K_GN_DONE] = 1;
+    }
+}
+
+// ---- dense term (BuildDenseSystem, SolverBundling.cu:308-471) ----------------------------------
+__device__ __forceinline__ f3 d2c(const BA& a, int x, int y, float depth) {  // CUDACameraUtil.h:15-19
+    const float xx = ((float)x - a.mx) / a.fx, yy = ((float)y - a.my) / a.fy;
+    return mk3(depth * xx, depth * yy, depth);
+}
+__device__ __forceinline__ void bilinear(const BA& a, float x, float y, const float* img, int comp, float* out) {
+    const int W = (int)a.cw, H = (int)a.ch;
+    const int px = (int)floorf(x), py = (int)floorf(y);
+    const float alpha = x - (float)px, beta = y - (float)py;
+    float s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, w0 = 0, w1 = 0;
+    const int qx[4] = {px, px + 1, px, px + 1}, qy[4] = {py, py, py + 1, py + 1};
+    const float wt[4] = {1.0f - alpha, alpha, 1.0f - alpha, alpha};
+    for (int t = 0; t < 4; t++) {
+        if ((unsigned)qx[t] < (unsigned)W && (unsigned)qy[t] < (unsigned)H) {
+            const float* v = img + ((size_t)qy[t] * W + qx[t]) * comp;
+            if (v[0] != -INFINITY) {
+                float* s = t < 2 ? s0 : s1;
+                for (int k = 0; k < comp; k++) s[k] += wt[t] * v[k];
+                if (t < 2) w0 += wt[t]; else w1 += wt[t];
+            }
+        }
+    }
+    float ss[4] = {0, 0, 0, 0}, ww = 0;
+    if (w0 > 0.0f) { for (int k = 0; k < comp; k++) ss[k] += (1.0f - beta) * (s0[k] / w0); ww += (1.0f - beta); }
+    if (w1 > 0.0f) { for (int k = 0; k < comp; k++) ss[k] += beta * (s1[k] / w1); ww += beta; }
+    for (int k = 0; k < comp; k++) out[k] = (ww > 0.0f) ? ss[k] / ww : -INFINITY;
+}
+
+__global__ void k_dense_reset(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.N * 36; k += gridDim.x * blockDim.x) a.diag[k] = 0.0f;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.N * 6; k += gridDim.x * blockDim.x) a.jtr[k] = 0.0f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctrl[K_NPAIRS] = 0;
+}
+
+// FindImageImageCorr_Kernel<true> (SolverBundling.cu:29-79), one wave per (i, j), i < j
+__global__ void k_dense_overlap(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t i = blockIdx.x, j = blockIdx.y;
+    if (i >= j || j >= a.N) return;
+    if (a.valid[i] == 0 || a.valid[j] == 0) return;
+    const m4 t = mul44(loadm4(a.Tinv + (size_t)i * 16), loadm4(a.T + (size_t)j * 16));
+    // computeAngleDiff (SolverBundlingDenseUtil.h:416-424)
+    const f3 x1 = normalize3(mk3(1.0f, 1.0f, 1.0f));
+    const f3 v1 = mul3v(rot_of(t), x1);
+    if (!(fabsf(acosf(fmaxf(-1.0f, fminf(dot3(x1, v1), 1.0f)))) < 0.52f)) return;
+    const uint32_t W = a.cw, H = a.ch, subW = W / a.sub;
+    const float* tgt = a.cache[i].depth;
+    const float* src = a.cache[j].depth;
+    int found = 0;
+    for (uint32_t tid = threadIdx.x; tid < 512; tid += blockDim.x) {
+        const uint32_t x = (tid % subW) * a.sub, y = (tid / subW) * a.sub, idx = y * W + x;
+        if (idx >= W * H) continue;
+        const f3 cj = d2c(a, (int)x, (int)y, src[idx]);  // findDenseCorr depth-only (:22-42)
+        if (!(cj.z > a.dmin && cj.z < a.dmax)) continue;
+        const f3 s2t = xf(t, cj);
+        const float u = s2t.x * a.fx / s2t.z + a.mx, vv = s2t.y * a.fy / s2t.z + a.my;
+        const int tx = (int)roundf(u), ty = (int)roundf(vv);
+        if (!(tx >= 0 && ty >= 0 && tx < (int)W && ty < (int)H)) continue;
+        const f3 ct = d2c(a, tx, ty, tgt[ty * W + tx]);
+        if (!(ct.z > a.dmin && ct.z < a.dmax)) continue;
+        if (length3(s2t - ct) <= a.distT) found++;
+    }
+    for (int off = 32; off > 0; off >>= 1) found += __shfl_xor(found, off);
+    if (threadIdx.x == 0 && found > 10) {
+        const uint32_t k = atomicAdd(&a.ctrl[K_NPAIRS], 1u);
+        if (k < a.maxPairs) a.pairs[k] = make_uint2(i, j);
+    }
+}
+
+// FindDenseCorrespondences_Kernel (:92-160, uchar4-normal variant :152-184) + WeightDenseCorrespondences (:162-180)
+__global__ void k_dense_count(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t np = min(a.ctrl[K_NPAIRS], a.maxPairs);
+    for (uint32_t k = blockIdx.x; k < np; k += gridDim.x) {
+        const uint2 pr = a.pairs[k];
+        const m4 t = mul44(loadm4(a.Tinv + (size_t)pr.x * 16), loadm4(a.T + (size_t)pr.y * 16));
+        const m3 R = rot_of(t);
+        const BFCachedFrame fi = a.cache[pr.x], fj = a.cache[pr.y];
+        const uint32_t W = a.cw, H = a.ch;
+        int count = 0;
+        for (uint32_t idx = threadIdx.x; idx < W * H; idx += blockDim.x) {
+            const int x = (int)(idx % W), y = (int)(idx / W);
+            const f3 cj = d2c(a, x, y, fj.depth[idx]);
+            if (!(cj.z > a.dmin && cj.z < a.dmax)) continue;
+            const uint32_t nj = reinterpret_cast<const uint32_t*>(fj.normalsU8)[idx];
+            if (nj == 0) continue;
+            f3 nrmj = mk3((float)(nj & 0xFF), (float)((nj >> 8) & 0xFF), (float)((nj >> 16) & 0xFF)) / 255.0f * 2.0f - mk3(1.0f, 1.0f, 1.0f);
+            nrmj = mul3v(R, nrmj);
+            const f3 s2t = xf(t, cj);
+            const float u = s2t.x * a.fx / s2t.z + a.mx, vv = s2t.y * a.fy / s2t.z + a.my;
+            const int tx = (int)roundf(u), ty = (int)roundf(vv);
+            if (!(tx >= 0 && ty >= 0 && tx < (int)W && ty < (int)H)) continue;
+            const f3 ct = d2c(a, tx, ty, fi.depth[ty * W + tx]);
+            if (!(ct.z > a.dmin && ct.z < a.dmax)) continue;
+            const uint32_t ni = reinterpret_cast<const uint32_t*>(fi.normalsU8)[ty * W + tx];
+            if (ni == 0) continue;
+            const f3 nrmi = mk3((float)(ni & 0xFF), (float)((ni >> 8) & 0xFF), (float)((ni >> 16) & 0xFF)) / 255.0f * 2.0f - mk3(1.0f, 1.0f, 1.0f);
+            if (dot3(nrmj, nrmi) >= a.normT && length3(s2t - ct) <= a.distT) count++;
+        }
+        for (int off = 32; off > 0; off >>= 1) count += __shfl_xor(count, off);
+        __shared__ int wc[WG / 64];
+        if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = count;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (uint32_t q = 0; q < blockDim.x / 64; q++) tot += wc[q];
+            float x = (float)tot;
+            if (x > 0) x = (x < 800) ? 0.0f : 1.0f / fminf(logf(x), 9.0f);
+            a.pairW[k] = x;
+        }
+        __syncthreads();
+    }
+}
+
+// BuildDenseSystem_Kernel<depth, color> (:182-306): one workgroup per overlapping pair; every
+// thread accumulates its pixels' 6x6 outer products (addToLocalSystem, DenseUtil.h:229-288) in
+// registers, then one workgroup reduction and one set of global adds per pair.
+__global__ __launch_bounds__(WG) void k_dense_build(BA a, float wDepth, float wColor) {
+    __shared__ float red[WG / 64][90];
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t np = min(a.ctrl[K_NPAIRS], a.maxPairs);
+    const bool useDepth = wDepth > 0.0f;
+    const bool useColor = !useDepth || wColor > 0.0f;
+    for (uint32_t k = blockIdx.x; k < np; k += gridDim.x) {
+        const float pw = a.pairW[k];
+        if (pw == 0.0f) continue;  // uniform per workgroup
+        const uint2 pr = a.pairs[k];
+        const uint32_t i = pr.x, j = pr.y;
+        const m4 Ti = loadm4(a.T + (size_t)i * 16), Tj = loadm4(a.T + (size_t)j * 16);
+        const m4 Tiinv = loadm4(a.Tinv + (size_t)i * 16), Tjinv = loadm4(a.Tinv + (size_t)j * 16);
+        const m4 t = mul44(Tiinv, Tj);
+        const BFCachedFrame fi = a.cache[i], fj = a.cache[j];
+        float acc[90];  // [0,21) ii upper, [21,42) jj upper, [42,78) ij (row b of i . col c of j), [78,84) jtr_i, [84,90) jtr_j
+        for (int q = 0; q < 90; q++) acc[q] = 0.0f;
+        const uint32_t W = a.cw, H = a.ch;
+        for (uint32_t src = threadIdx.x; src < W * H; src += blockDim.x) {
+            // findDenseCorr with camera positions + float4 normals (DenseUtil.h:79-113)
+            const float4 cp = reinterpret_cast<const float4*>(fj.campos)[src];
+            if (!(cp.z > a.dmin && cp.z < a.dmax)) continue;
+            const f3 cps = mk3(cp.x, cp.y, cp.z);
+            const float4 nj = reinterpret_cast<const float4*>(fj.normals)[src];
+            if (nj.x == -INFINITY) continue;
+            const f3 nrmj = mk3(t.e[0] * nj.x + t.e[1] * nj.y + t.e[2] * nj.z + t.e[3] * nj.w,
+                                t.e[4] * nj.x + t.e[5] * nj.y + t.e[6] * nj.z + t.e[7] * nj.w,
+                                t.e[8] * nj.x + t.e[9] * nj.y + t.e[10] * nj.z + t.e[11] * nj.w);
+            const float nrmjw = t.e[12] * nj.x + t.e[13] * nj.y + t.e[14] * nj.z + t.e[15] * nj.w;
+            const f3 s2t = xf(t, cps);
+            const float u = s2t.x * a.fx / s2t.z + a.mx, vv = s2t.y * a.fy / s2t.z + a.my;
+            const int tx = (int)roundf(u), ty = (int)roundf(vv);
+            if (!(tx >= 0 && ty >= 0 && tx < (int)W && ty < (int)H)) continue;
+            float ci[4], ni[4];
+            bilinear(a, u, vv, fi.campos, 4, ci);
+            if (!(ci[2] > a.dmin && ci[2] < a.dmax)) continue;
+            bilinear(a, u, vv, fi.normals, 4, ni);
+            if (ni[0] == -INFINITY) continue;
+            const f3 cpt = mk3(ci[0], ci[1], ci[2]), nT = mk3(ni[0], ni[1], ni[2]);
+            const float dn = nrmj.x * ni[0] + nrmj.y * ni[1] + nrmj.z * ni[2] + nrmjw * ni[3];
+            if (!(dn >= a.normT && length3(s2t - cpt) <= a.distT)) continue;
+            // rows of the two terms; accumulate J^T W J and J^T W r
+            for (int term = 0; term < 2; term++) {
+                float Ji[6] = {0, 0, 0, 0, 0, 0}, Jj[6] = {0, 0, 0, 0, 0, 0};
+                float res = 0.0f, w = 0.0f;
+                if (term == 0) {
+                    if (!useDepth) continue;
+                    res = dot3(cpt - s2t, nT);
+                    w = wDepth * pw * powf(fmaxf(0.0f, 1.0f - cpt.z / 2.0f), 2.5f);
+                    if (i > 0) { const m36 J = deriv_i(Tjinv, Ti, cps); for (int c = 0; c < 6; c++) Ji[c] = -dot3(mk3(J.e[c], J.e[6 + c], J.e[12 + c]), nT); }
+                    if (j > 0) { const m36 J = deriv_j(Tiinv, Tj, cps); for (int c = 0; c < 6; c++) Jj[c] = -dot3(mk3(J.e[c], J.e[6 + c], J.e[12 + c]), nT); }
+                } else {
+                    if (!useColor) continue;
+                    float dI[2], It;
+                    bilinear(a, u, vv, fi.intensityDeriv, 2, dI);
+                    bilinear(a, u, vv, fi.intensity, 1, &It);
+                    res = It - fj.intensity[src];
+                    if (!(dI[0] != -INFINITY && fabsf(res) < a.colT && sqrtf(dI[0] * dI[0] + dI[1] * dI[1]) > a.gradMin)) continue;
+                    const float wSq = s2t.z * s2t.z;
+                    const float d00 = a.fx / s2t.z, d11 = a.fy / s2t.z, d02 = -a.fx * s2t.x / wSq, d12 = -a.fy * s2t.y / wSq;
+                    if (i > 0) {
+                        const m36 J = deriv_i(Tjinv, Ti, cps);
+                        for (int c = 0; c < 6; c++) Ji[c] = dI[0] * (d00 * J.e[c] + 0.0f * J.e[6 + c] + d02 * J.e[12 + c]) + dI[1] * (0.0f * J.e[c] + d11 * J.e[6 + c] + d12 * J.e[12 + c]);
+                    }
+                    if (j > 0) {
+                        const m36 J = deriv_j(Tiinv, Tj, cps);
+                        for (int c = 0; c < 6; c++) Jj[c] = dI[0] * (d00 * J.e[c] + 0.0f * J.e[6 + c] + d02 * J.e[12 + c]) + dI[1] * (0.0f * J.e[c] + d11 * J.e[6 + c] + d12 * J.e[12 + c]);
+                    }
+                    w = wColor * pw * fmaxf(0.0f, 1.0f - fabsf(res) / (1.15f * a.colT));
+                }
+                int q = 0;
+                for (int r = 0; r < 6; r++)
+                    for (int c = r; c < 6; c++, q++) {
+                        acc[q] += Ji[r] * Ji[c] * w;
+                        acc[21 + q] += Jj[r] * Jj[c] * w;
+                    }
+                for (int r = 0; r < 6; r++)
+                    for (int c = 0; c < 6; c++) acc[42 + r * 6 + c] += Ji[r] * Jj[c] * w;
+                for (int r = 0; r < 6; r++) { acc[78 + r] += Ji[r] * res * w; acc[84 + r] += Jj[r] * res * w; }
+            }
+        }
+        for (int q = 0; q < 90; q++) {
+            const float s = wave_sum(acc[q]);
+            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x < 90) {
+            float s = 0.0f;
+            for (uint32_t wv = 0; wv < blockDim.x / 64; wv++) s += red[wv][threadIdx.x];
+            const int q = threadIdx.x;
+            if (q < 42) {  // symmetric diagonal block entry (r, c), r <= c -> both halves
+                const int qq = q < 21 ? q : q - 21;
+                int r = 0, c = 0, t2 = 0;
+                for (r = 0; r < 6; r++) { if (qq < t2 + (6 - r)) { c = r + (qq - t2); break; } t2 += 6 - r; }
+                float* D = a.diag + (size_t)(q < 21 ? i : j) * 36;
+                atomicAdd(&D[r * 6 + c], s);
+                if (r != c) atomicAdd(&D[c * 6 + r], s);
+            } else if (q < 78) {  // B(row j-index c, col i-index r) = (J_i^T W J_j)^T
+                const int r = (q - 42) / 6, c = (q - 42) % 6;
+                a.pairBlk[(size_t)k * 36 + c * 6 + r] = s;
+            } else if (q < 84) {
+                atomicAdd(&a.jtr[(size_t)i * 6 + (q - 78)], s);
+            } else {
+                atomicAdd(&a.jtr[(size_t)j * 6 + (q - 84)], s);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- residual analysis (EvalMaxResidual :511-564, EvalResidual :570-614, CountHighResiduals :657-687) ----
+__global__ __launch_bounds__(WG) void k_residuals(BA a) {
+    __shared__ float shv[WG];
+    __shared__ int shi[WG];
+    __shared__ float she[WG];
+    __shared__ int shc[WG];
+    const float w = ctrlf(a.ctrl, K_LAST_W);
+    float best = 0.0f, e = 0.0f;
+    int bi = 0x7FFFFFFF, cnt = 0;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < a.nCorr; c += gridDim.x * blockDim.x) {
+        const BFEntryJ x = a.corr[c];
+        if (!corr_valid(x)) continue;
+        const f3 r = xf(loadm4(a.T + (size_t)x.imgIdx_i * 16), mk3(x.pos_i.x, x.pos_i.y, x.pos_i.z)) -
+                     xf(loadm4(a.T + (size_t)x.imgIdx_j * 16), mk3(x.pos_j.x, x.pos_j.y, x.pos_j.z));
+        const f3 ar = mk3(fabsf(r.x), fabsf(r.y), fabsf(r.z)) * w;
+        const float m = fmaxf(ar.z, fmaxf(ar.x, ar.y));  // evalAbsMaxResidualDevice (EquationsLie.h:27-40)
+        if (m > best || (m == best && (int)c < bi)) { best = m; bi = (int)c; }
+        e += w * dot3(r, r);                              // evalFDevice (:42-57)
+        if (m > a.verifyT) cnt++;
+    }
+    shv[threadIdx.x] = best; shi[threadIdx.x] = bi; she[threadIdx.x] = e; shc[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int s = WG / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            const float v2 = shv[threadIdx.x + s];
+            const int i2 = shi[threadIdx.x + s];
+            if (v2 > shv[threadIdx.x] || (v2 == shv[threadIdx.x] && i2 < shi[threadIdx.x])) { shv[threadIdx.x] = v2; shi[threadIdx.x] = i2; }
+            she[threadIdx.x] += she[threadIdx.x + s];
+            shc[threadIdx.x] += shc[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.part[blockIdx.x * 2] = shv[0];
+        a.part[blockIdx.x * 2 + 1] = she[0];
+        a.partIdx[blockIdx.x * 2] = shi[0];
+        a.partIdx[blockIdx.x * 2 + 1] = shc[0];
+    }
+    if (!last_block(&a.ctrl[K_TICKET])) return;
+    if (threadIdx.x == 0) {
+        float mv = 0.0f, en = 0.0f;
+        int mi = 0x7FFFFFFF, hc = 0;
+        for (uint32_t b = 0; b < gridDim.x; b++) {
+            const float v2 = a.part[b * 2];
+            const int i2 = a.partIdx[b * 2];
+            if (v2 > mv || (v2 == mv && i2 < mi)) { mv = v2; mi = i2; }
+            en += a.part[b * 2 + 1];
+            hc += a.partIdx[b * 2 + 1];
+        }
+        if (!(w > 0.0f) || mi == 0x7FFFFFFF) { mv = 0.0f; mi = 0; }
+        a.ctrl[K_MAXRES] = __float_as_uint(mv);
+        a.ctrl[K_MAXIDX] = (uint32_t)mi;
+        a.ctrl[K_ENERGY] = __float_as_uint(en);
+        a.ctrl[K_HIGHCOUNT] = (uint32_t)hc;
+        a.ctrl[K_TICKET] = 0;
+    }
+}
+
+__global__ void k_solve_begin(uint32_t* ctrl) {
+    if (threadIdx.x < K_COUNT && threadIdx.x != K_ERROR) ctrl[threadIdx.x] = 0;
+}
+
+// ---- SBA.cu / SIFTImageManager.cu helpers ----
+__global__ void k_m2p(const float* T, uint32_t n, float* rot, float* trans, const int* valid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && valid[i]) {
+        m4 M;
+        for (int k = 0; k < 16; k++) M.e[k] = T[(size_t)i * 16 + k];
+        f3 r, t;
+        matrix_to_pose(M, r, t);
+        rot[3 * i] = r.x; rot[3 * i + 1] = r.y; rot[3 * i + 2] = r.z;
+        trans[3 * i] = t.x; trans[3 * i + 1] = t.y; trans[3 * i + 2] = t.z;
+    }
+}
+__global__ void k_p2m(const float* rot, const float* trans, uint32_t n, float* T, const int* valid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && valid[i]) {
+        const m4 M = pose_to_matrix(mk3(rot[3 * i], rot[3 * i + 1], rot[3 * i + 2]), mk3(trans[3 * i], trans[3 * i + 1], trans[3 * i + 2]));
+        for (int k = 0; k < 16; k++) T[(size_t)i * 16 + k] = M.e[k];
+    }
+}
+__global__ void k_invalidate_pair(BFEntryJ* corr, uint32_t n, uint32_t i, uint32_t j) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n && corr[c].imgIdx_i == i && corr[c].imgIdx_j == j) { corr[c].imgIdx_i = BF_INVALID_IMAGE; corr[c].imgIdx_j = BF_INVALID_IMAGE; }
+}
+__global__ void k_check_frames(const int* numEntries, int* valid, uint32_t numImages, BFEntryJ* corr, uint32_t nCorr, int comprehensive) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < numImages && numEntries[t] == 0) valid[t] = 0;
+    if (comprehensive) {
+        for (uint32_t c = t; c < nCorr; c += gridDim.x * blockDim.x) {
+            const BFEntryJ e = corr[c];
+            if (corr_valid(e) && (numEntries[e.imgIdx_i] == 0 || numEntries[e.imgIdx_j] == 0)) {
+                corr[c].imgIdx_i = BF_INVALID_IMAGE;
+                corr[c].imgIdx_j = BF_INVALID_IMAGE;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
+    BF_REQUIRE(cfg.maxImages >= 2 && cfg.maxCorr >= 1, BF_ERR_ARG, "solver capacity");
+    // maxCorrPerImage = clamp(maxRes / maxImages, 1000, 4000) (CUDASolverBundling.cpp:37)
+    maxCorrPerImage_ = std::min(4000u, std::max(1000u, cfg.maxCorr / cfg.maxImages));
+    maxPairs_ = cfg.maxImages * (cfg.maxImages - 1) / 2;
+    const uint32_t N = cfg.maxImages;
+    rowCount_.alloc(N + 1);
+    rowStart_.alloc(N + 1);
+    rowLen_.alloc(N + 1);
+    fill_.alloc(N + 1);
+    rowTmp_.alloc(2 * (size_t)cfg.maxCorr + 1);
+    rowIdx_.alloc(2 * (size_t)cfg.maxCorr + 1);
+    entries_.alloc(4 * (size_t)cfg.maxCorr + 2);
+    vec_.alloc((size_t)V_NUM * N * 8);
+    img_.alloc(2 * (size_t)N);
+    T_.alloc((size_t)N * 16);
+    Tinv_.alloc((size_t)N * 16);
+    ctrl_.alloc(K_COUNT);
+    part_.alloc(2 * 4096);
+    partIdx_.alloc(2 * 4096);
+    pairs_.alloc(maxPairs_);
+    pairW_.alloc(maxPairs_);
+    pairBlk_.alloc((size_t)maxPairs_ * 36);
+    diag_.alloc((size_t)N * 36);
+    jtr_.alloc((size_t)N * 6);
+    apDense_.alloc((size_t)N * 8);
+    int dev = 0;
+    hipDeviceProp_t prop;
+    BF_HIP(hipGetDevice(&dev));
+    BF_HIP(hipGetDeviceProperties(&prop, dev));
+    numCUs_ = prop.multiProcessorCount;
+    BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(apDense_.p, 0, apDense_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
+}
+
+Solver::~Solver() {}
+
+size_t Solver::deviceBytes() const {
+    return rowCount_.bytes() * 4 + rowTmp_.bytes() + rowIdx_.bytes() + entries_.bytes() + vec_.bytes() + img_.bytes() +
+           T_.bytes() + Tinv_.bytes() + pairs_.bytes() + pairW_.bytes() + pairBlk_.bytes() + diag_.bytes() + jtr_.bytes();
+}
+
+// CUDASolverBundling::solve (CUDASolverBundling.cpp:187-284) -> solveBundlingStub (SolverBundling.cu:1137-1220)
+void Solver::solve(const SolveArgs& s) {
+    BF_REQUIRE(s.numImages > 1 && s.numImages <= cfg_.maxImages, BF_ERR_ARG, "numImages out of range");
+    BF_REQUIRE(s.numCorr <= cfg_.maxCorr, BF_ERR_CAPACITY, "numCorr exceeds solver capacity");
+    BF_REQUIRE(s.nNonLin > 0 && s.wSparse, BF_ERR_ARG, "nNonLin / weights");
+    BA a{};
+    a.corr = s.corr; a.nCorr = s.numCorr; a.valid = s.valid; a.N = s.numImages; a.maxN = cfg_.maxImages; a.cap = maxCorrPerImage_;
+    a.rowCount = rowCount_.p; a.rowStart = rowStart_.p; a.rowLen = rowLen_.p; a.fill = fill_.p; a.rowTmp = rowTmp_.p; a.rowIdx = rowIdx_.p;
+    a.entries = entries_.p; a.vec = vec_.p; a.img = img_.p; a.T = T_.p; a.Tinv = Tinv_.p; a.ctrl = ctrl_.p;
+    a.part = part_.p; a.partIdx = partIdx_.p; a.rot = s.rot; a.trans = s.trans;
+    a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p; a.apDense = apDense_.p;
+    a.maxPairs = s.numImages * (s.numImages - 1) / 2;
+    a.cache = s.cache; a.cw = s.cacheW; a.ch = s.cacheH;
+    a.fx = s.intrinsics[0]; a.fy = s.intrinsics[1]; a.mx = s.intrinsics[2]; a.my = s.intrinsics[3];
+    a.distT = cfg_.denseDistThresh; a.normT = cfg_.denseNormalThresh; a.colT = cfg_.denseColorThresh;
+    a.gradMin = cfg_.denseColorGradientMin; a.dmin = cfg_.denseDepthMin; a.dmax = cfg_.denseDepthMax;
+    a.sub = cfg_.denseOverlapSubsample ? cfg_.denseOverlapSubsample : 4;
+    a.verifyT = cfg_.verifyOptDistThresh;
+
+    const unsigned corrGrid = std::max(1u, std::min(div_up(s.numCorr, WG), (unsigned)numCUs_ * 8));
+    const unsigned rowGrid = std::max(1u, std::min(div_up((size_t)s.numImages * 64, WG), (unsigned)numCUs_ * 4));
+    k_solve_begin<<<1, 64, 0, stream_>>>(ctrl_.p);
+    BF_LAUNCH_CHECK();
+    if (s.rebuildJT) {
+        BF_HIP(hipMemsetAsync(rowCount_.p, 0, sizeof(int) * (s.numImages + 1), stream_));
+        if (s.numCorr) k_count<<<corrGrid, WG, 0, stream_>>>(a);
+        k_scan<<<1, WG, 0, stream_>>>(a);
+        if (s.numCorr) k_fill<<<corrGrid, WG, 0, stream_>>>(a);
+        k_sort_rows<<<s.numImages, WG, 0, stream_>>>(a);
+        k_compact_rows<<<s.numImages, WG, 0, stream_>>>(a);
+        BF_LAUNCH_CHECK();
+    }
+    for (uint32_t it = 0; it < s.nNonLin; it++) {
+        const float wS = s.wSparse[it];
+        const float wD = s.wDenseDepth ? s.wDenseDepth[it] : 0.0f;
+        const float wC = s.wDenseColor ? s.wDenseColor[it] : 0.0f;
+        const bool dense = (wD > 0.0f || wC > 0.0f) && s.cache != nullptr;
+        k_transforms<<<div_up(s.numImages, 64), 64, 0, stream_>>>(a, wS, dense ? 1 : 0, 1, 1);
+        if (dense) {
+            k_dense_reset<<<64, WG, 0, stream_>>>(a);
+            k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);
+            k_dense_count<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 8), WG, 0, stream_>>>(a);
+            k_dense_build<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 4), WG, 0, stream_>>>(a, wD, wC);
+            BF_LAUNCH_CHECK();
+        }
+        k_entries<<<rowGrid, WG, 0, stream_>>>(a);
+        k_init<<<rowGrid, WG, 0, stream_>>>(a, wS);
+        BF_LAUNCH_CHECK();
+        for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+        BF_LAUNCH_CHECK();
+        k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
+        BF_LAUNCH_CHECK();
+    }
+    if (s.findMaxResidual) {
+        // T from the final poses (ctrl untouched), then computeMaxResidual with the weightSparse of
+        // the last GN iteration that ran (CUDASolverBundling.cpp:313-427)
+        k_transforms<<<div_up(s.numImages, 64), 64, 0, stream_>>>(a, 0.0f, 0, 0, 0);
+        k_residuals<<<corrGrid, WG, 0, stream_>>>(a);
+        BF_LAUNCH_CHECK();
+    }
+}
+
+SolveResult Solver::result() {
+    uint32_t c[K_COUNT];
+    BF_HIP(hipMemcpyAsync(c, ctrl_.p, sizeof(c), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    SolveResult r{};
+    r.gnIterations = c[K_GN_ITERS];
+    r.pcgIterations = c[K_PCG_ITERS];
+    std::memcpy(&r.maxResidual, &c[K_MAXRES], 4);
+    r.maxResidualIndex = (int32_t)c[K_MAXIDX];
+    std::memcpy(&r.energy, &c[K_ENERGY], 4);
+    r.highResidualCount = c[K_HIGHCOUNT];
+    r.numDensePairs = c[K_NPAIRS];
+    r.error = c[K_ERROR];
+    return r;
+}
+
+void matrices_to_poses(const float* T, uint32_t n, float* rot, float* trans, const int* valid, hipStream_t s) {
+    if (!n) return;
+    k_m2p<<<div_up(n, 64), 64, 0, s>>>(T, n, rot, trans, valid);
+    BF_LAUNCH_CHECK();
+}
+void poses_to_matrices(const float* rot, const float* trans, uint32_t n, float* T, const int* valid, hipStream_t s) {
+    if (!n) return;
+    k_p2m<<<div_up(n, 64), 64, 0, s>>>(rot, trans, n, T, valid);
+    BF_LAUNCH_CHECK();
+}
+void invalidate_image_pair(BFEntryJ* corr, uint32_t n, uint32_t i, uint32_t j, hipStream_t s) {
+    if (!n) return;
+    k_invalidate_pair<<<div_up(n, 128), 128, 0, s>>>(corr, n, i, j);
+    BF_LAUNCH_CHECK();
+}
+void check_invalid_frames(const int* numEntries, int* valid, uint32_t numImages, BFEntryJ* corr, uint32_t nCorr,
+                          bool comprehensive, hipStream_t s) {
+    const uint32_t n = std::max(numImages, comprehensive ? nCorr : 0u);
+    k_check_frames<<<std::max(1u, std::min(div_up(n, 256), 4096u)), 256, 0, s>>>(numEntries, valid, numImages, corr, nCorr,
+                                                                                  comprehensive ? 1 : 0);
+    BF_LAUNCH_CHECK();
+}
+
+}  // namespace bf

@@ -34,6 +34,8 @@ int bf_device_synchronize(void);
 /* device memory helpers (so hosts need no HIP headers) */
 int bf_malloc(void** dptr, size_t bytes);
 int bf_free(void* dptr);
+/* Blocking copies: device-synchronize first, so they are ordered after all work queued on the
+ * scene and solver streams (host plumbing, never inside a timed region). */
 int bf_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int bf_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int bf_memcpy_d2d(void* dst, const void* src, size_t bytes);
@@ -90,6 +92,49 @@ int bf_scene_device_bytes(bf_scene* s, uint64_t* bytes);
 int bf_scene_timer_start(bf_scene* s, bf_timer* t);
 int bf_scene_timer_stop(bf_scene* s, bf_timer* t, float* ms); /* synchronizes */
 
+/* ---- bundle adjustment: CUDASolverBundling (Solver/CUDASolverBundling.h/.cpp) ---------- */
+typedef struct bf_solver bf_solver;
+
+typedef struct BFSolverOptions {   /* zParametersBundlingDefault.txt defaults when 0 */
+    float denseDistThresh;         /* s_denseDistThresh = 0.15 */
+    float denseNormalThresh;       /* s_denseNormalThresh = 0.97 */
+    float denseColorThresh;        /* s_denseColorThresh = 0.1 */
+    float denseColorGradientMin;   /* s_denseColorGradientMin = 0.005 */
+    float denseDepthMin;           /* s_denseDepthMin = 0.5 */
+    float denseDepthMax;           /* s_denseDepthMax = 4.0 */
+    uint32_t denseOverlapSubsample;/* s_denseOverlapCheckSubsampleFactor = 4 */
+    float verifyOptDistThresh;     /* 0.02 (CUDASolverBundling.cpp:34) */
+} BFSolverOptions;
+
+/* ctor (CUDASolverBundling.cpp:24-136): capacity maxImages x maxCorr residuals */
+int bf_solver_create(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* opts, bf_solver** out);
+int bf_solver_destroy(bf_solver* s);
+/* CUDASolverBundling::solve (CUDASolverBundling.cpp:187-284) -> solveBundlingStub
+ * (SolverBundling.cu:1137). Device pointers: corr EntryJ[nCorr] (may be invalidated in place by
+ * the per-image cap), valid int[nImages], rot/trans float3[nImages] (in/out, se(3) [omega|t]),
+ * cache BFCachedFrame[nImages] (device array of device pointers) or NULL. Host pointers: the
+ * per-GN-iteration weights [nNonLin]. Enqueued asynchronously on the solver's stream; no host
+ * round trip until bf_solver_result. */
+int bf_solver_solve(bf_solver* s, BFEntryJ* corr, uint32_t nCorr, const int* valid, uint32_t nImages,
+                    uint32_t nNonLin, uint32_t nLin, const float* wSparse, const float* wDenseDepth,
+                    const float* wDenseColor, const BFCachedFrame* cache, uint32_t cacheW, uint32_t cacheH,
+                    const float intrinsics[4], float* rot, float* trans, int rebuildJT, int findMaxResidual);
+/* synchronizes; getMaxResidual inputs, iteration counts (CUDASolverBundling.cpp:429-476) */
+int bf_solver_result(bf_solver* s, BFSolveResult* out);
+/* getVarToCorrNumEntriesPerRow: device int[nImages] of the last table build */
+int bf_solver_num_entries_per_row(bf_solver* s, const int** dptr);
+int bf_solver_synchronize(bf_solver* s);
+int bf_solver_timer_start(bf_solver* s, bf_timer* t);
+int bf_solver_timer_stop(bf_solver* s, bf_timer* t, float* ms); /* synchronizes */
+/* convertMatricesToPosesCU / convertPosesToMatricesCU (SBA.cu:75-119), on the solver's stream */
+int bf_solver_matrices_to_poses(bf_solver* s, const float* T, uint32_t n, float* rot, float* trans, const int* valid);
+int bf_solver_poses_to_matrices(bf_solver* s, const float* rot, const float* trans, uint32_t n, float* T, const int* valid);
+/* SIFTImageManager::InvalidateImageToImageCU (SIFTImageManager.cu:692-719) */
+int bf_solver_invalidate_image_pair(bf_solver* s, BFEntryJ* corr, uint32_t nCorr, uint32_t i, uint32_t j);
+/* CheckForInvalidFrames[Simple]CU (SIFTImageManager.cu:725-793), using the last table build */
+int bf_solver_check_invalid_frames(bf_solver* s, int* valid, uint32_t nImages, BFEntryJ* corr, uint32_t nCorr,
+                                   int comprehensive);
+
 /* ---- synthetic RGB-D stream (seeded analytic room) ------------ */
 typedef struct BFSynthScene {
     uint32_t seed;
@@ -108,6 +153,18 @@ int bf_synth_render(const BFSynthScene* scene, const float T[16], const BFDepthC
 /* same arithmetic on the host (tests) into host buffers */
 int bf_synth_render_host(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam,
                          uint32_t noiseSeed, uint32_t frame, float* depth, uint8_t* color);
+/* Stand-in for the SIFT front end: for every pair of the K camera->world poses (HOST float[16*K])
+ * whose views share >= minCovis of sampled surface points, up to maxPerPair EntryJ correspondences
+ * (camera-space points in each frame, SIFTImageManager.cu:610-686 convention) with N(0, noise^2)
+ * jitter and an outlierFrac share of 0.1-0.3 m outliers. Writes HOST EntryJ[cap]; *n = count. */
+int bf_synth_correspondences(const BFSynthScene* scene, const float* poses, uint32_t K, const BFDepthCameraParams* cam,
+                             uint32_t maxPerPair, float minCovis, float noise, float outlierFrac, uint32_t seed,
+                             BFEntryJ* out, uint32_t cap, uint32_t* n);
+/* Dense-term cache frame of one view (CUDACache::storeFrame, CUDACache.cpp:45-86, from a noiseless
+ * render): HOST buffers depth[W*H], campos[4*W*H], normals[4*W*H], normalsU8[4*W*H],
+ * intensity[W*H], intensityDeriv[2*W*H]; cam is the cache resolution camera. */
+int bf_synth_cache_frame(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam, float* depth,
+                         float* campos, float* normals, uint8_t* normalsU8, float* intensity, float* intensityDeriv);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,18 @@ typedef struct BFCachedFrame {
     const float* intensityDeriv; /* d_intensityDerivsDownsampled, float2 per pixel */
 } BFCachedFrame;
 
+/* Outcome of one bundle-adjustment solve (CUDASolverBundling::solve + computeMaxResidual). */
+typedef struct BFSolveResult {
+    uint32_t gnIterations;       /* Gauss-Newton iterations executed (early exit at max|delta| < 0.005) */
+    uint32_t pcgIterations;      /* PCG iterations executed over all GN iterations */
+    float maxResidual;           /* max_c max_k w*|r_c,k| (EvalMaxResidual + host max) */
+    int32_t maxResidualIndex;    /* its correspondence index (lowest on ties) */
+    float energy;                /* sum_c w |r_c|^2 (EvalResidual) */
+    uint32_t highResidualCount;  /* correspondences with max residual > verifyOptDistThresh */
+    uint32_t numDensePairs;      /* overlapping image pairs found by the dense term (last GN iter) */
+    uint32_t error;              /* bit 1: a row exceeded the sort capacity */
+} BFSolveResult;
+
 /* Device-side counters used by the bench to compute algorithmic bytes. */
 typedef struct BFTsdfStats {
     uint64_t pixels;          /* P: pixels read by alloc (valid or not) */

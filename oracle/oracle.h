@@ -87,6 +87,8 @@ typedef struct ORSolveResult {
  * validImages: int[numImages]; rot/trans: float3[numImages] in/out. */
 void or_ba_solve(BFEntryJ* corr, const int* validImages, const ORSolveParams* p, float* rot,
                  float* trans, ORSolveResult* res);
+void or_ba_dense_system(const int* validImages, const ORSolveParams* p, const float* rot, const float* trans,
+                        float* jtjOut, float* jtrOut, double* energyOut, uint32_t* pairsOut);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,222 @@
+"""GPU parity of the HIP bundle adjuster (bf_solver_*) against the CPU oracle (oracle/ba.cpp).
+
+Float sums are reduced in a different order on the GPU (wave reductions + per-workgroup partials)
+than in the oracle (index order), so solutions are compared within the tolerances SURVEY.md §4/§8c
+set for the solver: rotation <= 1e-3 rad, translation <= 1 mm per pose, final energy rel <= 1e-2.
+Integer outcomes (per-image cap invalidation, pair invalidation, invalid-frame detection, the
+argmax residual index) are bit-exact.
+"""
+import numpy as np
+import pytest
+
+import bundlefusion_amd as bfa
+from ba_problem import make_problem, pose_diff, pose_errors
+from oracle_ba import matrix_to_pose, max_corr_per_image, pose_to_matrix, solve
+
+pytestmark = pytest.mark.gpu
+
+ROT_TOL, TRANS_TOL = 1e-3, 1e-3
+INVALID = 0xFFFFFFFF
+
+
+def gpu_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_corr=None, corr=None):
+    from bundlefusion_amd.solver import DeviceCache, SolverBundling
+    K = prob["K"]
+    corr = prob["corr"] if corr is None else corr
+    max_corr = max_corr or max(K * 4000, len(corr))
+    S = SolverBundling(K, max_corr)
+    d_corr = bfa.DeviceArray.from_host(corr if len(corr) else np.zeros(1, corr.dtype))
+    d_valid = bfa.DeviceArray.from_host(prob["valid"].astype(np.int32))
+    d_rot = bfa.DeviceArray.from_host(prob["rot"].astype(np.float32))
+    d_trans = bfa.DeviceArray.from_host(prob["trans"].astype(np.float32))
+    cache = DeviceCache(prob["cache"]) if use_cache else None
+    S.solve(d_corr, len(corr), d_valid, K, n_nonlin, n_lin, ws, wd, wc,
+            cache=cache.table if cache else None, cache_w=cache.W if cache else 0, cache_h=cache.H if cache else 0,
+            intrinsics=prob.get("intrinsics", (0, 0, 0, 0)), rot=d_rot, trans=d_trans)
+    res = S.result()
+    out = d_rot.download(), d_trans.download(), d_corr.download()[:len(corr)], res
+    S.close()
+    return out
+
+
+def oracle_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_corr=None, corr=None):
+    K = prob["K"]
+    corr = prob["corr"] if corr is None else corr
+    max_corr = max_corr or max(K * 4000, len(corr))
+    return solve(corr, prob["valid"], prob["rot"], prob["trans"], n_nonlin, n_lin, ws, wd, wc,
+                 cache=prob.get("cache") if use_cache else None, intrinsics=prob.get("intrinsics", (0, 0, 0, 0)),
+                 max_corr_per_img=max_corr_per_image(K, max_corr))
+
+
+def assert_parity(g, o, rot_tol=ROT_TOL, trans_tol=TRANS_TOL, energy_rtol=1e-2, same_argmax=True):
+    gr, gt_, gc, gres = g
+    orot, otr, oc, ores = o
+    er, et = pose_diff(gr, gt_, orot, otr)
+    assert er <= rot_tol and et <= trans_tol, (er, et, gres, ores)
+    assert gres["error"] == 0, gres
+    np.testing.assert_array_equal(gc["i"] == INVALID, oc["i"] == INVALID)
+    if same_argmax:
+        assert gres["maxResidualIndex"] == ores["maxResidualIndex"], (gres, ores)
+    # a residual moves by at most ~ |p| * rotation diff + translation diff between the two solutions
+    assert gres["maxResidual"] == pytest.approx(ores["maxResidual"], abs=4.0 * er + et + 1e-5)
+    assert gres["energy"] == pytest.approx(ores["finalEnergy"], rel=energy_rtol, abs=1e-7)
+    return er, et
+
+
+def smoke_ba():
+    """Tiny global solve on cuda:0 checked against the oracle (used by __graft_entry__.smoke)."""
+    prob = make_problem(K=6, max_per_pair=20, outliers=0.0)
+    assert_parity(gpu_solve(prob, 2, 50, [1, 1]), oracle_solve(prob, 2, 50, [1, 1]))
+
+
+@pytest.mark.parametrize("K,n_lin", [(6, 1), (6, 5), (6, 10), (12, 8), (32, 20)])
+def test_single_gn_step_parity_tight(K, n_lin):
+    """One Gauss-Newton step, n_lin PCG iterations: the HIP iterates track the oracle's to float
+    rounding (~1e-7). Measured on MI355X (tools/ba_trace.py): beyond ~10-15 iterations on the small
+    chains float32 CG loses conjugacy once the residual is tiny and the two summation orders drift
+    apart chaotically (1e-4..1e-3), which is why the full schedules use the SURVEY tolerances."""
+    prob = make_problem(K=K, max_per_pair=30, outliers=0.01)
+    g, o = gpu_solve(prob, 1, n_lin, [1]), oracle_solve(prob, 1, n_lin, [1])
+    assert g[3]["pcgIterations"] == o[3]["pcgIterations"] == n_lin
+    assert_parity(g, o, rot_tol=3e-6, trans_tol=3e-6, energy_rtol=1e-4)
+
+
+@pytest.mark.parametrize("n_lin", [1, 4])
+def test_dense_single_gn_step_parity_tight(n_lin):
+    """Dense depth + colour system (BuildDenseSystem, SolverBundling.cu:182-306) through the first PCG
+    iterations: pins the block-sparse dense JtJ/Jtr build and its PCG product against the oracle."""
+    prob = make_problem(K=6, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
+    args = (1, n_lin, [1], [1000], [50])
+    g, o = gpu_solve(prob, *args, use_cache=True), oracle_solve(prob, *args, use_cache=True)
+    assert g[3]["numDensePairs"] > 0
+    assert_parity(g, o, rot_tol=5e-6, trans_tol=5e-6, energy_rtol=1e-4)
+
+
+def test_global_sparse_schedule():
+    """Global solve schedule (SBA.cpp:34-39: sparse 1, dense off, 3 GN x 150 PCG) over 12 keyframes.
+
+    This chain is ill-conditioned along the trajectory and the GN exit test (max|delta| < 0.005,
+    SolverBundling.cu:1205) lands within rounding of its threshold on the second step, so the two
+    implementations may legitimately take 2 vs 3 GN steps; both must then reach the same energy
+    and the same accuracy against ground truth, and stay within 5 mm / 5 mrad of each other."""
+    prob = make_problem(K=12, max_per_pair=60, outliers=0.0)
+    g = gpu_solve(prob, 3, 150, [1, 1, 1])
+    o = oracle_solve(prob, 3, 150, [1, 1, 1])
+    if g[3]["gnIterations"] == o[3]["gnIterations"]:
+        assert_parity(g, o)
+    else:
+        assert_parity(g, o, rot_tol=5e-3, trans_tol=5e-3, energy_rtol=3e-2, same_argmax=False)
+    for rot, trans in ((g[0], g[1]), (o[0], o[1])):
+        er, et = pose_errors(rot, trans, prob["gt"])
+        assert er < 4e-3 and et < 7e-3
+
+
+def test_global_sparse_parity_with_outliers():
+    prob = make_problem(K=16, max_per_pair=40, outliers=0.02, seed=5)
+    assert_parity(gpu_solve(prob, 3, 150, [1, 1, 1]), oracle_solve(prob, 3, 150, [1, 1, 1]))
+
+
+def test_per_image_cap_invalidation_exact():
+    """BuildVariablesToCorrespondencesTableDevice (SolverBundling.cu:1226-1248) with cap 1000."""
+    prob = make_problem(K=6, stride=2, max_per_pair=256, outliers=0.0)
+    counts = np.bincount(np.concatenate([prob["corr"]["i"], prob["corr"]["j"]]), minlength=6)
+    assert counts.max() > 1000
+    max_corr = 6 * 1000
+    g = gpu_solve(prob, 2, 40, [1, 1], max_corr=max_corr)
+    o = oracle_solve(prob, 2, 40, [1, 1], max_corr=max_corr)
+    assert (o[2]["i"] == INVALID).sum() > 0
+    assert_parity(g, o)
+
+
+def test_local_dense_parity():
+    """Local solve with the dense depth term on the 80x60 cache (SBA.cpp:28-33 schedule shape)."""
+    prob = make_problem(K=6, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
+    args = (3, 100, [1, 1, 1], [1000, 1000, 1000], [0, 0, 0])
+    g = gpu_solve(prob, *args, use_cache=True)
+    o = oracle_solve(prob, *args, use_cache=True)
+    assert g[3]["numDensePairs"] > 0
+    assert_parity(g, o)
+
+
+def test_local_dense_color_parity():
+    """Dense depth + colour (global end-of-sequence schedule shape, SBA.cpp:41-44)."""
+    prob = make_problem(K=5, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.1, 0.003))
+    args = (2, 60, [1, 1], [1000, 1000], [50, 50])
+    assert_parity(gpu_solve(prob, *args, use_cache=True), oracle_solve(prob, *args, use_cache=True))
+
+
+def test_reference_local_schedule_runs():
+    """The reference's own local weights [1,1,1] / depth [1,2,3] / colour 0 (tiny dense weights)."""
+    prob = make_problem(K=6, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
+    args = (3, 100, [1, 1, 1], [1, 2, 3], [0, 0, 0])
+    assert_parity(gpu_solve(prob, *args, use_cache=True), oracle_solve(prob, *args, use_cache=True))
+
+
+def test_no_correspondences():
+    prob = make_problem(K=4, max_per_pair=5)
+    empty = prob["corr"][:0]
+    g = gpu_solve(prob, 2, 10, [1, 1], corr=empty)
+    o = oracle_solve(prob, 2, 10, [1, 1], corr=empty)
+    # delta = 0, but the Lie update still round-trips exp/log (computeLieUpdate): ulp-level changes
+    np.testing.assert_allclose(g[0], o[0], atol=1e-6)
+    np.testing.assert_allclose(g[1], o[1], atol=1e-6)
+    np.testing.assert_allclose(g[0], prob["rot"], atol=1e-6)
+    assert g[3]["maxResidual"] == 0.0 and g[3]["energy"] == 0.0
+
+
+def test_matrices_poses_roundtrip():
+    """convertMatricesToPosesCU / convertPosesToMatricesCU (SBA.cu:75-119) vs the oracle's Lie maps."""
+    from bundlefusion_amd.solver import SolverBundling
+    rng = np.random.default_rng(4)
+    n = 64
+    rot = (rng.normal(size=(n, 3)) * rng.choice([1e-4, 0.1, 1.0, 2.5], size=(n, 1))).astype(np.float32)
+    trans = rng.normal(size=(n, 3)).astype(np.float32)
+    T = np.stack([pose_to_matrix(rot[k], trans[k]) for k in range(n)]).astype(np.float32)
+    valid = np.ones(n, np.int32)
+    valid[5] = 0
+    S = SolverBundling(n, 4000)
+    dT = bfa.DeviceArray.from_host(T)
+    dR = bfa.DeviceArray.from_host(np.zeros((n, 3), np.float32))
+    dt = bfa.DeviceArray.from_host(np.zeros((n, 3), np.float32))
+    dv = bfa.DeviceArray.from_host(valid)
+    S.matrices_to_poses(dT, n, dR, dt, dv)
+    r2, t2 = dR.download(), dt.download()
+    for k in range(n):
+        if k == 5:
+            continue
+        ro, to = matrix_to_pose(T[k])
+        np.testing.assert_allclose(r2[k], ro, atol=2e-6)
+        np.testing.assert_allclose(t2[k], to, atol=2e-5)
+    dT2 = bfa.DeviceArray.from_host(np.zeros((n, 4, 4), np.float32))
+    S.poses_to_matrices(dR, dt, n, dT2, dv)
+    T2 = dT2.download()
+    for k in range(n):
+        if k != 5:
+            np.testing.assert_allclose(T2[k], T[k], atol=5e-5)
+    S.close()
+
+
+def test_invalidate_pair_and_check_frames():
+    """InvalidateImageToImageCU (SIFTImageManager.cu:692-719) + CheckForInvalidFramesCU (:725-793)."""
+    from bundlefusion_amd.solver import SolverBundling
+    prob = make_problem(K=6, max_per_pair=20)
+    corr = prob["corr"].copy()
+    # isolate image 5: invalidate every pair touching it
+    S = SolverBundling(6, 24000)
+    d_corr = bfa.DeviceArray.from_host(corr)
+    for i in range(5):
+        S.invalidate_image_pair(d_corr, len(corr), i, 5)
+    c2 = d_corr.download()
+    touched = (corr["j"] == 5) & (corr["i"] < 5)
+    assert touched.any()
+    np.testing.assert_array_equal(c2["i"] == INVALID, touched)
+    # build the table through a solve, then check frames: image 5 has no entries -> invalid
+    d_valid = bfa.DeviceArray.from_host(np.ones(6, np.int32))
+    d_rot = bfa.DeviceArray.from_host(prob["rot"])
+    d_trans = bfa.DeviceArray.from_host(prob["trans"])
+    S.solve(d_corr, len(corr), d_valid, 6, 1, 5, [1.0], rot=d_rot, trans=d_trans)
+    S.result()
+    S.check_invalid_frames(d_valid, 6, d_corr, len(corr), comprehensive=True)
+    S.synchronize()
+    np.testing.assert_array_equal(d_valid.download(), [1, 1, 1, 1, 1, 0])
+    S.close()
