@@ -1,0 +1,230 @@
+"""bench.py — frames/s of integrate + global BA on a synthetic 640x480 stream at 4 mm voxels
+(BASELINE.json metric), plus ms/GN-iter of the global solve.
+
+A step is one submap (10 frames) of the reconstruction loop (bf_recon: per frame one integrate,
+up to 10 re-integration queue ops and GC; per submap one local solve (11 frames, dense term on the
+80x60 cache) and one global solve over all keyframes so far, with max-residual removal and the
+trajectory update that feeds the queue). W warmup submaps run untimed, then K submaps are timed.
+Every input (frames, cache frames, correspondences) is resident in HBM before timing starts.
+
+Multi-GPU (torchrun, one process per GPU): the TSDF is sharded by 1 m chunk ownership
+(every GPU sees every frame and integrates only the blocks it owns); the
+bundle adjustment is replicated on every rank (deterministic inputs, identical solves), so there
+is no data-path collective. The host-side barrier / max-over-ranks uses gloo.
+
+roofline: the dominant kernel is k_integrate; its launches are timed with HIP events on the scene
+stream inside the timed region; algorithmic bytes per launch = 16 B per visible block (list
+entry) + 24 B per voxel updated inside the truncation band (12 B read + 12 B write) + 8 B per
+pixel (depth + colour read once), from the device counters of the same launches.
+cpu_baseline: the CPU oracle (oracle/, serial C++ restatement) timed on a bounded sample of the
+same workload on this host, scaled by the GPU run's op counts to frames/s.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(stream, params, gpu, budget_s=20.0):
+    """Oracle (port) timing on a bounded sample, scaled to frames/s with the GPU run's op counts."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_ba import max_corr_per_image, solve
+    from oracle_lib import OracleScene
+
+    t_start = time.perf_counter()
+    P = stream.cam.imageWidth * stream.cam.imageHeight
+    ora = OracleScene(params)
+    n = min(4, stream.F)
+    depth = [stream.depth.download_range(f * P * 4, P * 4).view(np.float32).reshape(stream.cam.imageHeight, -1)
+             for f in range(n)]
+    color = [stream.color.download_range(f * P * 4, P * 4).reshape(stream.cam.imageHeight, -1, 4) for f in range(n)]
+    t0 = time.perf_counter()
+    for f in range(n):
+        ora.integrate(stream.gt[f], depth[f], color[f], stream.cam)
+    t_int = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    ora.integrate(stream.gt[n - 1], depth[n - 1], color[n - 1], stream.cam, deintegrate=True)
+    t_deint = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ora.garbageCollect()
+    t_gc = time.perf_counter() - t0
+    del ora
+    # global BA at the final keyframe count: one GN iteration with a few PCG iterations,
+    # scaled to the GPU's average PCG iterations per global solve
+    K = gpu["keyframes"]
+    ncorr = int(stream.global_prefix[K - 1])
+    corr = stream.global_host[:ncorr]
+    rot = np.zeros((K, 3), np.float32)
+    trans = np.zeros((K, 3), np.float32)
+    from oracle_ba import matrix_to_pose
+    for k in range(K):
+        rot[k], trans[k] = matrix_to_pose(stream.gt[k * stream.S])
+    maxc = max_corr_per_image(K + 1, 25 * (K + 1) * K // 2)
+    t0 = time.perf_counter()
+    solve(corr, np.ones(K, np.int32), rot, trans, 1, 1, [1.0], max_corr_per_img=maxc)
+    t_one = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    solve(corr, np.ones(K, np.int32), rot, trans, 1, 6, [1.0], max_corr_per_img=maxc)
+    t_pcg = max(1e-9, (time.perf_counter() - t0 - t_one) / 5.0)
+    t_gn = max(1e-9, t_one - t_pcg)
+    per_solve = gpu["gn_per_solve"] * t_gn + gpu["pcg_per_solve"] * t_pcg
+    ops_per_frame = gpu["ops_per_frame"]
+    frame_s = (ops_per_frame * (t_int + t_deint) / 2.0) + t_gc + per_solve / stream.S
+    sample = (f"oracle TSDF: {n} integrates + 1 de-integrate + 1 GC at {stream.cam.imageWidth}x"
+              f"{stream.cam.imageHeight} @ {params.virtualVoxelSize * 1000:.0f} mm ({t_int * 1e3:.0f} / "
+              f"{t_deint * 1e3:.0f} / {t_gc * 1e3:.0f} ms); oracle global BA at K={K}, Nc={ncorr}: "
+              f"{t_gn * 1e3:.0f} ms/GN setup + {t_pcg * 1e3:.0f} ms/PCG iter; scaled by the GPU run's "
+              f"{ops_per_frame:.2f} ops/frame and {gpu['gn_per_solve']:.2f} GN / {gpu['pcg_per_solve']:.1f} PCG "
+              f"per global solve (local solves not counted); {time.perf_counter() - t_start:.0f} s of CPU work")
+    return {"value": 1.0 / frame_s, "unit": "frames/s", "cores": 1, "kind": "port", "sample": sample,
+            "ms_per_gn_iter": (t_gn + t_pcg * gpu["pcg_per_solve"] / max(gpu["gn_per_solve"], 1e-9)) * 1e3}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=498, help="timed submaps (10 frames each)")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed submaps before timing")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--voxel", type=float, default=0.004)
+    ap.add_argument("--buckets", type=int, default=1 << 23)
+    ap.add_argument("--blocks", type=int, default=1 << 21)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=None, help="JSON with per-launch HBM bytes of k_integrate (PMC pass)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side barrier / max only (gloo)
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+
+    import bundlefusion_amd as bfa
+    from bundlefusion_amd.abi import BFSceneOptions
+    from bundlefusion_amd.recon import Recon, recon_options
+    from bundlefusion_amd.stream import SyntheticStream
+
+    bfa.check(bfa.lib().bf_set_device(local_rank))
+    S = 10
+    F = S * (args.warmup + args.steps) + 1
+    t_setup = time.perf_counter()
+    stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log)
+    params = bfa.hash_params(voxel_size=args.voxel, num_buckets=args.buckets, num_blocks=args.blocks)
+    K = stream.K
+    opts = recon_options(F, enableTiming=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
+                         maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2))
+    so = BFSceneOptions()
+    so.shardCount, so.shardIndex, so.shardChunk = world, rank, 1.0
+    rc = Recon(params, stream.cam, opts, so)
+    stream.attach(rc)
+    log(f"setup {time.perf_counter() - t_setup:.1f}s: {F} frames, {K} keyframes, "
+        f"{len(stream.global_host)} global correspondences")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    f0 = S * args.warmup
+    for f in range(f0):
+        rc.process_frame(f)
+    rc.synchronize()
+    rc.reset_stats()
+    barrier()
+    rc.synchronize()
+    t0 = time.perf_counter()
+    last = time.perf_counter()
+    for f in range(f0, S * (args.warmup + args.steps)):
+        rc.process_frame(f)
+        if time.perf_counter() - last > 30.0:
+            log(f"  frame {f}")
+            last = time.perf_counter()
+    rc.synchronize()
+    dt = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = rc.stats()
+    ss = rc.scene_stats()
+    frames = S * args.steps
+    P = args.width * args.height
+    launches = max(1, st["integrateLaunches"])
+    alg_bytes = 16 * ss["visible"] + 24 * ss["voxelsUpdated"] + 8 * P * launches
+    per_launch_bytes = alg_bytes / launches
+    per_launch_s = st["integrateKernelMs"] / 1e3 / launches
+    achieved = per_launch_bytes / per_launch_s / 1e9
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        traffic = json.load(open(args.traffic)).get("k_integrate_bytes_per_launch")
+    gn = max(1, st["globalGnIterations"])
+    ms_gn = st["globalSolveMs"] / gn
+    out = {
+        "metric": "frames/s integrate+global-BA on 640x480 @4mm voxels",
+        "value": frames / dt,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded analytic room, GPU-rendered depth/colour with the sensor noise model, "
+                "EntryJ stand-in correspondences)",
+        "config": {"workload": f"{F - 1}-frame {args.width}x{args.height} stream, {args.voxel * 1000:.0f} mm voxels, "
+                               f"2^{args.buckets.bit_length() - 1} buckets, 2^{args.blocks.bit_length() - 1} blocks; "
+                               f"local 2x100 + global 3x150 GN x PCG per submap",
+                   "frames_timed": frames, "keyframes_final": K,
+                   "parallelism": f"tsdf-chunk-shard{world}+ba-replicated" if world > 1 else "single"},
+        "ms_per_gn_iter": ms_gn,
+        "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "launches": st["integrateLaunches"], "avg_launch_us": per_launch_s * 1e6,
+                     "alg_bytes_per_launch": per_launch_bytes},
+        "loop": {"ops_per_frame": (st["integrations"] + st["deintegrations"]) / max(1, st["frames"]),
+                 "fix_ops": st["fixOps"], "local_solves": st["localSolves"], "global_solves": st["globalSolves"],
+                 "global_gn_iters": st["globalGnIterations"], "global_pcg_iters": st["globalPcgIterations"],
+                 "removed_pairs": st["removedPairs"], "global_solve_ms": st["globalSolveMs"],
+                 "local_solve_ms": st["localSolveMs"], "integrate_kernel_ms": st["integrateKernelMs"],
+                 "heap_free": rc.heap_free_count()},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        gpu = {"keyframes": int(min(K, (args.warmup + args.steps))),
+               "gn_per_solve": st["globalGnIterations"] / max(1, st["globalSolves"]),
+               "pcg_per_solve": st["globalPcgIterations"] / max(1, st["globalSolves"]),
+               "ops_per_frame": out["loop"]["ops_per_frame"]}
+        try:
+            out["cpu_baseline"] = cpu_baseline(stream, params, gpu)
+        except Exception as e:  # the baseline is reported, not the target: keep the GPU line
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    rc.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,13 @@ class DeviceArray:
         check(lib().bf_memcpy_d2h(out.ctypes.data_as(C.c_void_p), self.ptr, C.c_size_t(self.nbytes)))
         return out
 
+    def download_range(self, offset: int, nbytes: int) -> np.ndarray:
+        """nbytes starting at byte offset, as uint8."""
+        assert 0 <= offset and offset + nbytes <= self.nbytes
+        out = np.empty(nbytes, np.uint8)
+        check(lib().bf_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr.value + offset), C.c_size_t(nbytes)))
+        return out
+
     def zero(self) -> None:
         check(lib().bf_memset(self.ptr, 0, C.c_size_t(self.nbytes)))
 

@@ -153,3 +153,25 @@ class BFSolveResult(C.Structure):
     _fields_ = [("gnIterations", C.c_uint32), ("pcgIterations", C.c_uint32), ("maxResidual", C.c_float),
                 ("maxResidualIndex", C.c_int32), ("energy", C.c_float), ("highResidualCount", C.c_uint32),
                 ("numDensePairs", C.c_uint32), ("error", C.c_uint32)]
+
+
+class BFFixOp(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("frame", C.c_uint32), ("oldT", C.c_float * 16), ("newT", C.c_float * 16)]
+
+
+class BFReconOptions(C.Structure):
+    _fields_ = [("maxFrames", C.c_uint32), ("submapSize", C.c_uint32), ("maxFrameFixes", C.c_uint32),
+                ("topNActive", C.c_uint32), ("minPoseDistSqrt", C.c_float),
+                ("localNonLin", C.c_uint32), ("localLin", C.c_uint32), ("globalNonLin", C.c_uint32),
+                ("globalLin", C.c_uint32), ("maxKeyframes", C.c_uint32), ("maxLocalCorr", C.c_uint32),
+                ("maxGlobalCorr", C.c_uint32), ("maxResidualThresh", C.c_float), ("useLocalDense", C.c_int32),
+                ("cacheWidth", C.c_uint32), ("cacheHeight", C.c_uint32), ("cacheIntrinsics", C.c_float * 4),
+                ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("solver", BFSolverOptions)]
+
+
+class BFReconStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "frames", "integrations", "deintegrations", "fixOps", "localSolves", "globalSolves",
+        "globalGnIterations", "globalPcgIterations", "localGnIterations", "localPcgIterations",
+        "removedPairs", "integrateLaunches")] + [
+        ("integrateKernelMs", C.c_double), ("localSolveMs", C.c_double), ("globalSolveMs", C.c_double)]

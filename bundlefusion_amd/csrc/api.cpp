@@ -2,11 +2,14 @@
 // turns it into a status code + bf_last_error() message.
 #include "../../include/bf/bf.h"
 #include "ba.h"
+#include "recon.h"
+#include "trajectory.h"
 #include "bf_runtime.h"
 #include "synth.h"
 #include "tsdf.h"
 
 #include <cstring>
+#include <limits>
 #include <string>
 
 namespace bf {
@@ -365,17 +368,7 @@ int bf_synth_cache_frame(const BFSynthScene* scene, const float T[16], const BFD
 int bf_solver_create(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* o, bf_solver** out) {
     BF_TRY
     BF_REQUIRE(out, BF_ERR_ARG, "null argument");
-    SolverConfig cfg{};
-    cfg.maxImages = maxImages;
-    cfg.maxCorr = maxCorr;
-    cfg.denseDistThresh = (o && o->denseDistThresh > 0) ? o->denseDistThresh : 0.15f;
-    cfg.denseNormalThresh = (o && o->denseNormalThresh > 0) ? o->denseNormalThresh : 0.97f;
-    cfg.denseColorThresh = (o && o->denseColorThresh > 0) ? o->denseColorThresh : 0.1f;
-    cfg.denseColorGradientMin = (o && o->denseColorGradientMin > 0) ? o->denseColorGradientMin : 0.005f;
-    cfg.denseDepthMin = (o && o->denseDepthMin > 0) ? o->denseDepthMin : 0.5f;
-    cfg.denseDepthMax = (o && o->denseDepthMax > 0) ? o->denseDepthMax : 4.0f;
-    cfg.denseOverlapSubsample = (o && o->denseOverlapSubsample) ? o->denseOverlapSubsample : 4;
-    cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
+    const SolverConfig cfg = make_solver_config(maxImages, maxCorr, o);
     bf_solver* s = new bf_solver();
     try {
         BF_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
@@ -477,6 +470,194 @@ int bf_solver_check_invalid_frames(bf_solver* s, int* valid, uint32_t nImages, B
     BF_TRY
     BF_REQUIRE(s && valid, BF_ERR_ARG, "null argument");
     check_invalid_frames(s->solver->numEntriesPerRow(), valid, nImages, corr, nCorr, comprehensive != 0, s->stream);
+    BF_CATCH
+}
+
+
+// ---- reconstruction loop ----------------------------------------------------------------
+struct bf_recon {
+    Recon* r = nullptr;
+};
+
+int bf_recon_create(const BFHashParams* params, const BFSceneOptions* sceneOpts, const BFDepthCameraParams* cam,
+                    const BFReconOptions* opts, bf_recon** out) {
+    BF_TRY
+    BF_REQUIRE(params && cam && opts && out, BF_ERR_ARG, "null argument");
+    bf_recon* h = new bf_recon();
+    try {
+        h->r = new Recon(*params, sceneOpts, *cam, *opts);
+    } catch (...) {
+        delete h;
+        throw;
+    }
+    *out = h;
+    BF_CATCH
+}
+int bf_recon_destroy(bf_recon* r) {
+    BF_TRY
+    if (r) {
+        delete r->r;
+        delete r;
+    }
+    BF_CATCH
+}
+int bf_recon_set_frame(bf_recon* r, uint32_t f, const float* depth, const uint8_t* color, const BFCachedFrame* cache,
+                       const float Tinc[16]) {
+    BF_TRY
+    BF_REQUIRE(r && depth && Tinc, BF_ERR_ARG, "null argument");
+    r->r->setFrame(f, depth, color, cache, to_mat(Tinc));
+    BF_CATCH
+}
+int bf_recon_set_local_correspondences(bf_recon* r, uint32_t submap, BFEntryJ* corr, uint32_t n) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->setLocalCorrespondences(submap, corr, n);
+    BF_CATCH
+}
+int bf_recon_set_global_correspondences(bf_recon* r, BFEntryJ* corr, uint32_t n, const uint32_t* prefix,
+                                        uint32_t numKeyframes) {
+    BF_TRY
+    BF_REQUIRE(r && (prefix || numKeyframes == 0), BF_ERR_ARG, "null argument");
+    r->r->setGlobalCorrespondences(corr, n, prefix, numKeyframes);
+    BF_CATCH
+}
+int bf_recon_set_initial_pose(bf_recon* r, const float T0[16]) {
+    BF_TRY
+    BF_REQUIRE(r && T0, BF_ERR_ARG, "null argument");
+    r->r->setInitialPose(to_mat(T0));
+    BF_CATCH
+}
+int bf_recon_process_frame(bf_recon* r, uint32_t f) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->processFrame(f);
+    BF_CATCH
+}
+int bf_recon_finish(bf_recon* r) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->finish();
+    BF_CATCH
+}
+int bf_recon_synchronize(bf_recon* r) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->synchronize();
+    BF_CATCH
+}
+int bf_recon_stats(bf_recon* r, BFReconStats* out) {
+    BF_TRY
+    BF_REQUIRE(r && out, BF_ERR_ARG, "null argument");
+    *out = r->r->stats();
+    BF_CATCH
+}
+int bf_recon_reset_stats(bf_recon* r) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->resetStats();
+    BF_CATCH
+}
+int bf_recon_scene_stats(bf_recon* r, BFTsdfStats* out) {
+    BF_TRY
+    BF_REQUIRE(r && out, BF_ERR_ARG, "null argument");
+    r->r->synchronize();
+    *out = r->r->scene().stats();
+    BF_CATCH
+}
+int bf_recon_heap_free_count(bf_recon* r, uint32_t* count) {
+    BF_TRY
+    BF_REQUIRE(r && count, BF_ERR_ARG, "null argument");
+    *count = r->r->scene().heapFreeCount();
+    BF_CATCH
+}
+int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n) {
+    BF_TRY
+    BF_REQUIRE(r && T, BF_ERR_ARG, "null argument");
+    r->r->trajectory(reinterpret_cast<BFMat4*>(T), n);
+    BF_CATCH
+}
+
+int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->synchronize();
+    r->r->scene().exportState(hash, heap, heapCounter, voxels);
+    BF_CATCH
+}
+int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(r && n && (out || cap == 0), BF_ERR_ARG, "null argument");
+    const auto& log = r->r->opLog();
+    *n = (uint32_t)log.size();
+    for (uint32_t i = 0; i < cap && i < log.size(); i++) out[i] = log[i];
+    BF_CATCH
+}
+
+// ---- re-integration queue (host) ----------------------------------------------------------
+struct bf_traj {
+    TrajectoryManager* tm = nullptr;
+    std::vector<FixOp> ops;
+};
+
+int bf_traj_create(uint32_t maxFrames, uint32_t topNActive, float minPoseDistSqrt, bf_traj** out) {
+    BF_TRY
+    BF_REQUIRE(out && maxFrames > 0, BF_ERR_ARG, "bad argument");
+    bf_traj* t = new bf_traj();
+    t->tm = new TrajectoryManager(maxFrames, topNActive ? topNActive : 30u, minPoseDistSqrt);
+    *out = t;
+    BF_CATCH
+}
+int bf_traj_destroy(bf_traj* t) {
+    BF_TRY
+    if (t) {
+        delete t->tm;
+        delete t;
+    }
+    BF_CATCH
+}
+int bf_traj_add_frame(bf_traj* t, int32_t type, const float T[16], uint32_t idx) {
+    BF_TRY
+    BF_REQUIRE(t, BF_ERR_ARG, "null traj");
+    BF_REQUIRE(type == 0 || type == 1, BF_ERR_ARG, "type must be Integrated (0) or NotIntegrated_NoTransform (1)");
+    BFMat4 m;
+    if (type == 0) {
+        BF_REQUIRE(T, BF_ERR_ARG, "null transform");
+        m = to_mat(T);
+    } else {
+        for (float& v : m.m) v = -std::numeric_limits<float>::infinity();
+    }
+    t->tm->addFrame((FrameType)type, m, idx);
+    BF_CATCH
+}
+int bf_traj_update_optimized(bf_traj* t, const float* T, uint32_t numFrames) {
+    BF_TRY
+    BF_REQUIRE(t && (T || numFrames == 0), BF_ERR_ARG, "null argument");
+    t->tm->updateOptimizedTransforms(reinterpret_cast<const BFMat4*>(T), numFrames);
+    BF_CATCH
+}
+int bf_traj_next_fixes(bf_traj* t, uint32_t maxFixes, BFFixOp* ops, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(t && n && (ops || maxFixes == 0), BF_ERR_ARG, "null argument");
+    *n = t->tm->nextFixes(maxFixes, t->ops);
+    for (uint32_t i = 0; i < *n; i++) {
+        ops[i].kind = (int32_t)t->ops[i].kind;
+        ops[i].frame = t->ops[i].frame;
+        std::memcpy(ops[i].oldT, t->ops[i].oldT.m, 64);
+        std::memcpy(ops[i].newT, t->ops[i].newT.m, 64);
+    }
+    BF_CATCH
+}
+int bf_traj_frame_info(bf_traj* t, uint32_t idx, int32_t* type, float* dist) {
+    BF_TRY
+    BF_REQUIRE(t, BF_ERR_ARG, "null traj");
+    if (type) *type = (int32_t)t->tm->type(idx);
+    if (dist) *dist = t->tm->dist(idx);
+    BF_CATCH
+}
+int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]) {
+    BF_TRY
+    BF_REQUIRE(T && out, BF_ERR_ARG, "null argument");
+    pose_helper_matrix_to_pose(to_mat(T), out);
     BF_CATCH
 }
 

@@ -16,6 +16,7 @@
 // are evaluated on the device, so there is no host round trip inside solve (the reference
 // copies scanAlpha to the host every PCG iteration, SolverBundling.cu:1089).
 #pragma once
+#include "../../include/bf/bf.h"
 #include "bf_math.h"
 #include "bf_runtime.h"
 
@@ -73,8 +74,10 @@ public:
     hipStream_t stream() const { return stream_; }
     const SolverConfig& config() const { return cfg_; }
     size_t deviceBytes() const;
+    KernelClock& solveClock() { return solveClock_; }  // whole-solve device time (ms/GN-iter)
 
 private:
+    KernelClock solveClock_;
     SolverConfig cfg_;
     hipStream_t stream_;
     uint32_t maxCorrPerImage_;
@@ -97,6 +100,8 @@ private:
     DevBuf<float> jtr_;      // [N][6]
     DevBuf<float> apDense_;  // [N][8]
 };
+
+SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* opts);
 
 // SBA.cu:75-119 — float4x4 <-> (rot, trans) for valid images
 void matrices_to_poses(const float* T, uint32_t n, float* rot, float* trans, const int* valid, hipStream_t s);

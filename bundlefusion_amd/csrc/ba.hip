@@ -807,6 +807,22 @@ __global__ void k_check_frames(const int* numEntries, int* valid, uint32_t numIm
 
 }  // namespace
 
+// zParametersBundlingDefault.txt defaults for every option left 0
+SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* o) {
+    SolverConfig cfg{};
+    cfg.maxImages = maxImages;
+    cfg.maxCorr = maxCorr;
+    cfg.denseDistThresh = (o && o->denseDistThresh > 0) ? o->denseDistThresh : 0.15f;
+    cfg.denseNormalThresh = (o && o->denseNormalThresh > 0) ? o->denseNormalThresh : 0.97f;
+    cfg.denseColorThresh = (o && o->denseColorThresh > 0) ? o->denseColorThresh : 0.1f;
+    cfg.denseColorGradientMin = (o && o->denseColorGradientMin > 0) ? o->denseColorGradientMin : 0.005f;
+    cfg.denseDepthMin = (o && o->denseDepthMin > 0) ? o->denseDepthMin : 0.5f;
+    cfg.denseDepthMax = (o && o->denseDepthMax > 0) ? o->denseDepthMax : 4.0f;
+    cfg.denseOverlapSubsample = (o && o->denseOverlapSubsample) ? o->denseOverlapSubsample : 4;
+    cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
+    return cfg;
+}
+
 // ------------------------------------------------------------------------------------------------
 Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
     BF_REQUIRE(cfg.maxImages >= 2 && cfg.maxCorr >= 1, BF_ERR_ARG, "solver capacity");
@@ -873,6 +889,8 @@ void Solver::solve(const SolveArgs& s) {
 
     const unsigned corrGrid = std::max(1u, std::min(div_up(s.numCorr, WG), (unsigned)numCUs_ * 8));
     const unsigned rowGrid = std::max(1u, std::min(div_up((size_t)s.numImages * 64, WG), (unsigned)numCUs_ * 4));
+    const bool timed = solveClock_.enabled();
+    if (timed) solveClock_.start(stream_);
     k_solve_begin<<<1, 64, 0, stream_>>>(ctrl_.p);
     BF_LAUNCH_CHECK();
     if (s.rebuildJT) {
@@ -912,6 +930,7 @@ void Solver::solve(const SolveArgs& s) {
         k_residuals<<<corrGrid, WG, 0, stream_>>>(a);
         BF_LAUNCH_CHECK();
     }
+    if (timed) solveClock_.stop(stream_);
 }
 
 SolveResult Solver::result() {

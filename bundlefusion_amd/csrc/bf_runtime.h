@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace bf {
 
@@ -62,6 +63,72 @@ struct DevBuf {
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     size_t bytes() const { return n * sizeof(T); }
+};
+
+// Live per-launch timing of one kernel with HIP events on the stream it is launched on, for
+// the roofline figure bench.py reports. A ring of event pairs; a slot is harvested (event
+// synchronize + elapsed time) only when the ring wraps, i.e. ~RING launches later, so the
+// host never waits on work it just queued.
+class KernelClock {
+public:
+    static constexpr size_t RING = 512;
+    ~KernelClock() { destroy(); }
+    void enable(bool on) {
+        if (on && a_.empty()) {
+            a_.resize(RING);
+            b_.resize(RING);
+            for (size_t i = 0; i < RING; i++) {
+                BF_HIP(hipEventCreate(&a_[i]));
+                BF_HIP(hipEventCreate(&b_[i]));
+            }
+        }
+        on_ = on;
+    }
+    bool enabled() const { return on_; }
+    void start(hipStream_t s) {
+        if (pending_ == RING) harvest(head_);
+        BF_HIP(hipEventRecord(a_[head_], s));
+    }
+    void stop(hipStream_t s) {
+        BF_HIP(hipEventRecord(b_[head_], s));
+        head_ = (head_ + 1) % RING;
+        pending_++;
+    }
+    // drains every pending slot (synchronizes on the newest event)
+    double totalMs() {
+        while (pending_) harvest((head_ + RING - pending_) % RING);
+        return total_;
+    }
+    uint64_t launches() {
+        totalMs();
+        return n_;
+    }
+    void reset() {
+        totalMs();
+        total_ = 0.0;
+        n_ = 0;
+    }
+
+private:
+    void harvest(size_t slot) {
+        BF_HIP(hipEventSynchronize(b_[slot]));
+        float ms = 0.0f;
+        BF_HIP(hipEventElapsedTime(&ms, a_[slot], b_[slot]));
+        total_ += ms;
+        n_++;
+        pending_--;
+    }
+    void destroy() {
+        for (auto e : a_) (void)hipEventDestroy(e);
+        for (auto e : b_) (void)hipEventDestroy(e);
+        a_.clear();
+        b_.clear();
+    }
+    std::vector<hipEvent_t> a_, b_;
+    size_t head_ = 0, pending_ = 0;
+    double total_ = 0.0;
+    uint64_t n_ = 0;
+    bool on_ = false;
 };
 
 }  // namespace bf

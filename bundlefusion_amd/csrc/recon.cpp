@@ -1,0 +1,337 @@
+// recon.cpp — see recon.h.
+#include "recon.h"
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+
+namespace bf {
+
+BFMat4 mat4_mul(const BFMat4& a, const BFMat4& b);  // api.cpp
+
+namespace {
+const float NEG_INF = -std::numeric_limits<float>::infinity();
+BFMat4 ninf_mat() {
+    BFMat4 m;
+    for (float& v : m.m) v = NEG_INF;
+    return m;
+}
+BFMat4 identity() {
+    BFMat4 m{};
+    m.m[0] = m.m[5] = m.m[10] = m.m[15] = 1.0f;
+    return m;
+}
+template <class T>
+T or_default(T v, T d) { return v ? v : d; }
+}  // namespace
+
+Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCameraParams& cam, const BFReconOptions& o)
+    : opt_(o), cam_(cam) {
+    opt_.submapSize = or_default(o.submapSize, 10u);
+    opt_.maxFrameFixes = or_default(o.maxFrameFixes, 10u);
+    opt_.topNActive = or_default(o.topNActive, 30u);
+    opt_.localNonLin = or_default(o.localNonLin, 2u);
+    opt_.localLin = or_default(o.localLin, 100u);
+    opt_.globalNonLin = or_default(o.globalNonLin, 3u);
+    opt_.globalLin = or_default(o.globalLin, 150u);
+    opt_.maxResidualThresh = o.maxResidualThresh > 0 ? o.maxResidualThresh : 0.08f;
+    opt_.cacheWidth = or_default(o.cacheWidth, 80u);
+    opt_.cacheHeight = or_default(o.cacheHeight, 60u);
+    BF_REQUIRE(opt_.maxFrames > 0, BF_ERR_ARG, "maxFrames");
+    const uint32_t S = opt_.submapSize;
+    const uint32_t maxSubmaps = (opt_.maxFrames + S - 1) / S;
+    opt_.maxKeyframes = std::max(or_default(o.maxKeyframes, maxSubmaps + 1), 2u);
+    opt_.maxLocalCorr = or_default(o.maxLocalCorr, (S + 1) * S / 2 * 25u);
+    opt_.maxGlobalCorr = or_default(o.maxGlobalCorr, opt_.maxKeyframes * 1000u);
+
+    BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
+    BF_HIP(hipStreamCreateWithFlags(&baStream_, hipStreamNonBlocking));
+    SceneConfig sc{};
+    sc.hp = hp;
+    if (so) {
+        sc.candCapacity = so->candidateCapacity;
+        sc.shardCount = so->shardCount;
+        sc.shardIndex = so->shardIndex;
+        sc.shardChunk = so->shardChunk;
+    }
+    scene_.reset(new Scene(sc, sceneStream_));
+    local_.reset(new Solver(make_solver_config(S + 1, opt_.maxLocalCorr, &opt_.solver), baStream_));
+    global_.reset(new Solver(make_solver_config(opt_.maxKeyframes, opt_.maxGlobalCorr, &opt_.solver), baStream_));
+    tm_.reset(new TrajectoryManager(opt_.maxFrames, opt_.topNActive, opt_.minPoseDistSqrt));
+    if (opt_.enableTiming) {
+        scene_->integrateClock().enable(true);
+        local_->solveClock().enable(true);
+        global_->solveClock().enable(true);
+    }
+
+    frames_.resize(opt_.maxFrames);
+    localCorr_.assign(maxSubmaps, {nullptr, 0});
+    localTraj_.resize(maxSubmaps);
+    globalT_.assign(opt_.maxKeyframes, identity());
+    globalValid_.assign(opt_.maxKeyframes, 1);
+    complete_.resize(opt_.maxFrames);
+
+    const uint32_t L = S + 1, K = opt_.maxKeyframes;
+    dLocalRot_.alloc(3 * L);
+    dLocalTrans_.alloc(3 * L);
+    dLocalT_.alloc(16 * L);
+    dLocalValid_.alloc(L);
+    dLocalCache_.alloc(L);
+    dGlobalRot_.alloc(3 * K);
+    dGlobalTrans_.alloc(3 * K);
+    dGlobalT_.alloc(16 * K);
+    dGlobalValid_.alloc(K);
+    dSeedT_.alloc(16);
+    dOne_.alloc(1);
+    std::vector<int> ones(std::max(L, K), 1);
+    BF_HIP(hipMemcpyAsync(dLocalValid_.p, ones.data(), 4 * L, hipMemcpyHostToDevice, baStream_));
+    BF_HIP(hipMemcpyAsync(dGlobalValid_.p, ones.data(), 4 * K, hipMemcpyHostToDevice, baStream_));
+    BF_HIP(hipMemcpyAsync(dOne_.p, ones.data(), 4, hipMemcpyHostToDevice, baStream_));
+    BF_HIP(hipMemsetAsync(dGlobalRot_.p, 0, dGlobalRot_.bytes(), baStream_));
+    BF_HIP(hipMemsetAsync(dGlobalTrans_.p, 0, dGlobalTrans_.bytes(), baStream_));
+    BF_HIP(hipStreamSynchronize(baStream_));
+}
+
+Recon::~Recon() {
+    if (sceneStream_) (void)hipStreamSynchronize(sceneStream_);
+    if (baStream_) (void)hipStreamSynchronize(baStream_);
+    scene_.reset();
+    local_.reset();
+    global_.reset();
+    if (sceneStream_) (void)hipStreamDestroy(sceneStream_);
+    if (baStream_) (void)hipStreamDestroy(baStream_);
+}
+
+void Recon::setFrame(uint32_t f, const float* depth, const uint8_t* color, const BFCachedFrame* cache, const BFMat4& Tinc) {
+    BF_REQUIRE(f < opt_.maxFrames, BF_ERR_CAPACITY, "frame index beyond maxFrames");
+    FrameRef& r = frames_[f];
+    r.depth = depth;
+    r.color = color;
+    r.cache = cache ? *cache : BFCachedFrame{};
+    r.Tinc = Tinc;
+    r.set = true;
+}
+
+void Recon::setLocalCorrespondences(uint32_t submap, BFEntryJ* corr, uint32_t n) {
+    BF_REQUIRE(submap < localCorr_.size(), BF_ERR_CAPACITY, "submap index");
+    BF_REQUIRE(n <= opt_.maxLocalCorr, BF_ERR_CAPACITY, "local correspondences exceed maxLocalCorr");
+    localCorr_[submap] = {corr, n};
+}
+
+void Recon::setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes) {
+    BF_REQUIRE(n <= opt_.maxGlobalCorr, BF_ERR_CAPACITY, "global correspondences exceed maxGlobalCorr");
+    globalCorr_ = corr;
+    globalCorrN_ = n;
+    globalPrefix_.assign(prefix, prefix + numKeyframes);
+}
+
+void Recon::setInitialPose(const BFMat4& T0) {
+    globalT_[0] = T0;
+    BF_HIP(hipMemcpyAsync(dSeedT_.p, T0.m, 64, hipMemcpyHostToDevice, baStream_));
+    matrices_to_poses(dSeedT_.p, 1, dGlobalRot_.p, dGlobalTrans_.p, dOne_.p, baStream_);
+    BF_HIP(hipStreamSynchronize(baStream_));
+}
+
+void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
+    if (!opt_.recordOps) return;
+    BFFixOp e{};
+    e.kind = kind;
+    e.frame = frame;
+    if (T) std::memcpy(kind == 1 ? e.oldT : e.newT, T->m, 64);
+    log_.push_back(e);
+}
+
+// reintegrate() (DepthSensing.cpp:854-902)
+void Recon::runReintegrate() {
+    tm_->nextFixes(opt_.maxFrameFixes, ops_);
+    for (const FixOp& op : ops_) {
+        const FrameRef& fr = frames_[op.frame];
+        BF_REQUIRE(fr.set, BF_ERR_STATE, "re-integration of a frame that is not in the frame store");
+        if (op.kind == FixKind::DeIntegrate || op.kind == FixKind::ReIntegrate) {
+            scene_->integrate(op.oldT, fr.depth, fr.color, cam_, true, nullptr);
+            logOp(1, op.frame, &op.oldT);
+            st_.deintegrations++;
+        }
+        if (op.kind == FixKind::Integrate || op.kind == FixKind::ReIntegrate) {
+            scene_->integrate(op.newT, fr.depth, fr.color, cam_, false, nullptr);
+            logOp(2, op.frame, &op.newT);
+            st_.integrations++;
+        }
+        st_.fixOps++;
+    }
+    scene_->garbageCollect();
+    logOp(4, 0, nullptr);
+}
+
+void Recon::processFrame(uint32_t f) {
+    BF_REQUIRE(f == numFrames_, BF_ERR_STATE, "frames must be processed in order");
+    BF_REQUIRE(f < opt_.maxFrames && frames_[f].set, BF_ERR_STATE, "frame not in the frame store");
+    const uint32_t S = opt_.submapSize;
+    const uint32_t s = f / S;
+    if (f % S == 0 && f > 0) endSubmap(s - 1, S + 1);
+    runReintegrate();
+    FrameRef& fr = frames_[f];
+    fr.Tlocal = (f % S == 0) ? identity() : mat4_mul(frames_[f - 1].Tlocal, fr.Tinc);
+    const BFMat4 T = mat4_mul(globalT_[s], fr.Tlocal);  // getCurrentIntegrationFrame
+    scene_->integrate(T, fr.depth, fr.color, cam_, false, nullptr);
+    logOp(2, f, &T);
+    st_.integrations++;
+    tm_->addFrame(FrameType::Integrated, T, f);
+    numFrames_++;
+    st_.frames++;
+}
+
+void Recon::finish() {
+    const uint32_t S = opt_.submapSize;
+    if (numFrames_ == 0) return;
+    const uint32_t s = (numFrames_ - 1) / S;
+    if (s != lastSubmapSolved_) endSubmap(s, numFrames_ - s * S);
+}
+
+// end of submap s: optimizeLocal -> processGlobal/optimizeGlobal -> updateTrajectory
+void Recon::endSubmap(uint32_t s, uint32_t n) {
+    const uint32_t S = opt_.submapSize;
+    const uint32_t base = s * S;
+    // ---- local solve over frames base .. base+n-1 (first frame fixed) ----------------------
+    std::vector<BFMat4> Tl(n);
+    std::vector<BFCachedFrame> cache(n);
+    bool haveCache = opt_.useLocalDense != 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const FrameRef& fr = frames_[base + i];
+        BF_REQUIRE(fr.set, BF_ERR_STATE, "local solve over a frame not in the frame store");
+        // the submap's last local frame is the next submap's first: chain it from frame S-1
+        Tl[i] = (i < S) ? fr.Tlocal : mat4_mul(frames_[base + S - 1].Tlocal, fr.Tinc);
+        cache[i] = fr.cache;
+        if (!fr.cache.depth) haveCache = false;
+    }
+    std::vector<BFMat4>& traj = localTraj_[s];
+    traj = Tl;
+    const auto& lc = localCorr_[s];
+    if (n >= 2 && lc.first && lc.second > 0) {
+        BF_HIP(hipMemcpyAsync(dLocalT_.p, Tl.data(), 64 * n, hipMemcpyHostToDevice, baStream_));
+        if (haveCache)
+            BF_HIP(hipMemcpyAsync(dLocalCache_.p, cache.data(), sizeof(BFCachedFrame) * n, hipMemcpyHostToDevice, baStream_));
+        matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_.p, dLocalValid_.p, baStream_);
+        std::vector<float> ws(opt_.localNonLin, 1.0f), wd(opt_.localNonLin), wc(opt_.localNonLin, 0.0f);
+        for (uint32_t i = 0; i < opt_.localNonLin; i++) wd[i] = haveCache ? (float)(i + 1) : 0.0f;  // SBA.cpp:28-31
+        SolveArgs a{};
+        a.corr = lc.first;
+        a.numCorr = lc.second;
+        a.valid = dLocalValid_.p;
+        a.numImages = n;
+        a.nNonLin = opt_.localNonLin;
+        a.nLin = opt_.localLin;
+        a.wSparse = ws.data();
+        a.wDenseDepth = wd.data();
+        a.wDenseColor = wc.data();
+        a.cache = haveCache ? dLocalCache_.p : nullptr;
+        a.cacheW = opt_.cacheWidth;
+        a.cacheH = opt_.cacheHeight;
+        std::memcpy(a.intrinsics, opt_.cacheIntrinsics, sizeof(a.intrinsics));
+        a.rot = dLocalRot_.p;
+        a.trans = dLocalTrans_.p;
+        a.rebuildJT = true;
+        a.findMaxResidual = false;  // optimizeLocal: no max residual removal (OnlineBundler.cpp:255)
+        local_->solve(a);
+        poses_to_matrices(dLocalRot_.p, dLocalTrans_.p, n, dLocalT_.p, dLocalValid_.p, baStream_);
+        BF_HIP(hipMemcpyAsync(traj.data(), dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
+        const SolveResult r = local_->result();  // synchronizes the BA stream
+        st_.localSolves++;
+        st_.localGnIterations += r.gnIterations;
+        st_.localPcgIterations += r.pcgIterations;
+    }
+    // ---- global solve over keyframes 0..s ---------------------------------------------------
+    const uint32_t nk = s + 1;
+    BF_REQUIRE(nk < opt_.maxKeyframes, BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
+    const uint32_t ncorr = (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_;
+    if (nk >= 2 && globalCorr_ && ncorr > 0) {
+        std::vector<float> ws(opt_.globalNonLin, 1.0f), wz(opt_.globalNonLin, 0.0f);  // SBA.cpp:34-39, dense off
+        SolveArgs a{};
+        a.corr = globalCorr_;
+        a.numCorr = ncorr;
+        a.valid = dGlobalValid_.p;
+        a.numImages = nk;
+        a.nNonLin = opt_.globalNonLin;
+        a.nLin = opt_.globalLin;
+        a.wSparse = ws.data();
+        a.wDenseDepth = wz.data();
+        a.wDenseColor = wz.data();
+        a.rot = dGlobalRot_.p;
+        a.trans = dGlobalTrans_.p;
+        a.rebuildJT = true;
+        a.findMaxResidual = true;
+        global_->solve(a);
+        const SolveResult r = global_->result();
+        st_.globalSolves++;
+        st_.globalGnIterations += r.gnIterations;
+        st_.globalPcgIterations += r.pcgIterations;
+        // removeMaxResidualCUDA (SBA.cpp:164-203) with getMaxResidual's exemption (CUDASolverBundling.cpp:429-452)
+        if (r.maxResidual > opt_.maxResidualThresh && r.maxResidualIndex >= 0) {
+            BFEntryJ e{};
+            BF_HIP(hipMemcpyAsync(&e, globalCorr_ + r.maxResidualIndex, sizeof(e), hipMemcpyDeviceToHost, baStream_));
+            BF_HIP(hipStreamSynchronize(baStream_));
+            if (!(e.imgIdx_i == 0 && e.imgIdx_j < 10) && e.imgIdx_i != BF_INVALID_IMAGE) {
+                invalidate_image_pair(globalCorr_, ncorr, e.imgIdx_i, e.imgIdx_j, baStream_);
+                check_invalid_frames(global_->numEntriesPerRow(), dGlobalValid_.p, nk, globalCorr_, ncorr, false,
+                                     baStream_);
+                st_.removedPairs++;
+            }
+        }
+        poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
+        BF_HIP(hipMemcpyAsync(globalT_.data(), dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
+        BF_HIP(hipMemcpyAsync(globalValid_.data(), dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
+        BF_HIP(hipStreamSynchronize(baStream_));
+    }
+    // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
+    if (n == S + 1) {
+        globalT_[s + 1] = mat4_mul(globalT_[s], traj[S]);
+        BF_HIP(hipMemcpyAsync(dSeedT_.p, globalT_[s + 1].m, 64, hipMemcpyHostToDevice, baStream_));
+        matrices_to_poses(dSeedT_.p, 1, dGlobalRot_.p + 3 * (s + 1), dGlobalTrans_.p + 3 * (s + 1), dOne_.p, baStream_);
+        BF_HIP(hipStreamSynchronize(baStream_));
+    }
+    // ---- updateTrajectoryCU (OnlineBundler.cu:73-110) + TrajectoryManager::updateOptimizedTransform
+    const uint32_t nf = std::min(base + n, numFrames_);
+    const uint32_t optimized = std::min(base + std::min(n, S), nf);
+    for (uint32_t g = 0; g < optimized; g++) {
+        const uint32_t k = g / S;
+        complete_[g] = globalValid_[k] ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();
+    }
+    tm_->updateOptimizedTransforms(complete_.data(), optimized);
+    lastSubmapSolved_ = s;
+}
+
+void Recon::synchronize() {
+    BF_HIP(hipStreamSynchronize(sceneStream_));
+    BF_HIP(hipStreamSynchronize(baStream_));
+}
+
+BFReconStats Recon::stats() {
+    synchronize();
+    BFReconStats s = st_;
+    if (opt_.enableTiming) {
+        s.integrateKernelMs = scene_->integrateClock().totalMs();
+        s.integrateLaunches = scene_->integrateClock().launches();
+        s.localSolveMs = local_->solveClock().totalMs();
+        s.globalSolveMs = global_->solveClock().totalMs();
+    }
+    return s;
+}
+
+void Recon::resetStats() {
+    synchronize();
+    st_ = BFReconStats{};
+    scene_->resetStats();
+    scene_->integrateClock().reset();
+    local_->solveClock().reset();
+    global_->solveClock().reset();
+}
+
+void Recon::trajectory(BFMat4* out, uint32_t n) const {
+    for (uint32_t i = 0; i < n && i < opt_.maxFrames; i++) {
+        const bool integrated = i < tm_->numAddedFrames() &&
+                                (tm_->type(i) == FrameType::Integrated || tm_->type(i) == FrameType::ReIntegration);
+        out[i] = integrated ? tm_->integrated(i) : ninf_mat();
+    }
+}
+
+}  // namespace bf

@@ -1,0 +1,96 @@
+// recon.h — the per-frame reconstruction loop with on-the-fly re-integration and the
+// hierarchical (local submap -> global keyframe) bundle adjustment, i.e. the parts of
+// DepthSensing.cpp's frame loop (Source/DepthSensing/DepthSensing.cpp:1003-1056, reintegrate
+// :854-902) and OnlineBundler (Source/OnlineBundler.cpp:242-416, OnlineBundler.cu:6-140) that sit
+// on the north-star path. Correspondence *production* (SiftGPU) is out of scope: EntryJ lists
+// are inputs, as if the matcher had filled SIFTImageManager's global correspondence array.
+//
+// Ordering per frame f (submap size S, s = f / S):
+//   1. if f is the first frame of submap s > 0: end of submap s-1 -> local solve over its S+1
+//      frames (dense term on the 80x60 cache), global solve over keyframes 0..s-1 with max
+//      residual removal, seed keyframe s = global[s-1] * local[s-1][S] (initNextGlobalTransformCU),
+//      trajectory update complete[g] = global[g/S] * local[g/S][g%S] (updateTrajectoryCU)
+//   2. reintegrate(): up to maxFrameFixes de-/re-/integrate ops from the TrajectoryManager, then GC
+//   3. integrate frame f with global[s] * L[f] and addFrame(Integrated), where L chains the front
+//      end's frame-to-frame estimates Tinc inside the submap (L = I at its first frame)
+// TSDF work runs on the scene stream, BA on its own stream; the host waits on the BA stream only
+// for the poses it needs (as the reference copies them device->host, TrajectoryManager.cpp:38).
+#pragma once
+#include <array>
+#include <memory>
+#include <vector>
+
+#include "../../include/bf/bf.h"
+#include "ba.h"
+#include "trajectory.h"
+#include "tsdf.h"
+
+namespace bf {
+
+class Recon {
+public:
+    Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCameraParams& cam, const BFReconOptions& opt);
+    ~Recon();
+
+    void setFrame(uint32_t f, const float* depth, const uint8_t* color, const BFCachedFrame* cache, const BFMat4& Tinc);
+    void setLocalCorrespondences(uint32_t submap, BFEntryJ* corr, uint32_t n);
+    // global EntryJ list ordered by max(i, j); prefix[k] = #entries with max(i, j) <= k
+    void setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes);
+    void setInitialPose(const BFMat4& T0);
+    void processFrame(uint32_t f);
+    void finish();  // end of sequence: solve the last (partial) submap
+    void synchronize();
+
+    BFReconStats stats();
+    void resetStats();
+    void trajectory(BFMat4* out, uint32_t n) const;   // integrated transform per frame (-inf if none)
+    Scene& scene() { return *scene_; }
+    const std::vector<BFFixOp>& opLog() const { return log_; }
+
+private:
+    void endSubmap(uint32_t s, uint32_t numFrames);
+    void runReintegrate();
+
+    BFReconOptions opt_;
+    BFDepthCameraParams cam_;
+    hipStream_t sceneStream_ = nullptr, baStream_ = nullptr;
+    std::unique_ptr<Scene> scene_;
+    std::unique_ptr<Solver> local_, global_;
+    std::unique_ptr<TrajectoryManager> tm_;
+
+    struct FrameRef {
+        const float* depth = nullptr;
+        const uint8_t* color = nullptr;
+        BFCachedFrame cache{};
+        BFMat4 Tinc{};    // front-end estimate: camera f in camera f-1 coordinates
+        BFMat4 Tlocal{};  // chained estimate relative to the submap's first frame
+        bool set = false;
+    };
+    std::vector<FrameRef> frames_;
+    std::vector<std::pair<BFEntryJ*, uint32_t>> localCorr_;
+    BFEntryJ* globalCorr_ = nullptr;
+    uint32_t globalCorrN_ = 0;
+    std::vector<uint32_t> globalPrefix_;
+
+    std::vector<BFMat4> globalT_;        // host copy of the keyframe poses
+    std::vector<int> globalValid_;
+    std::vector<std::vector<BFMat4>> localTraj_;  // per submap, S+1 local poses
+    std::vector<BFMat4> complete_;
+    std::vector<FixOp> ops_;
+    uint32_t lastSubmapSolved_ = 0xFFFFFFFFu;
+    uint32_t numFrames_ = 0;
+
+    DevBuf<float> dLocalRot_, dLocalTrans_, dLocalT_;
+    DevBuf<int> dLocalValid_;
+    DevBuf<BFCachedFrame> dLocalCache_;
+    DevBuf<float> dGlobalRot_, dGlobalTrans_, dGlobalT_;
+    DevBuf<int> dGlobalValid_;
+    DevBuf<float> dSeedT_;
+    DevBuf<int> dOne_;
+
+    BFReconStats st_{};
+    std::vector<BFFixOp> log_;
+    void logOp(int kind, uint32_t frame, const BFMat4* T);
+};
+
+}  // namespace bf

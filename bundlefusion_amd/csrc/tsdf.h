@@ -71,6 +71,7 @@ public:
     const uint32_t* dCtrl() const { return ctrl_.p; }
     uint32_t* dCtrlMut() { return ctrl_.p; }
     size_t deviceBytes() const;
+    KernelClock& integrateClock() { return integrateClock_; }  // k_integrate launches (bench roofline)
 
 private:
     void alloc(const float* depth, const BFDepthCameraParams& cam, const uint32_t* bitMask);
@@ -97,6 +98,7 @@ private:
     DevBuf<uint32_t> blockCount_;
     uint32_t candSetMask_;
     int numCUs_;
+    KernelClock integrateClock_;
 };
 
 }  // namespace bf

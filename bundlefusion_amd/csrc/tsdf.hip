@@ -801,11 +801,14 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     k_compactify<<<grid, 256, 0, stream_>>>(A, cam, Tinv_);
     BF_LAUNCH_CHECK();
     const unsigned igrid = (unsigned)numCUs_ * 8;
+    const bool timed = integrateClock_.enabled();
+    if (timed) integrateClock_.start(stream_);
     if (deint)
         k_integrate<true><<<igrid, 256, 0, stream_>>>(A, depth, reinterpret_cast<const uint32_t*>(color), cam, Tinv_);
     else
         k_integrate<false><<<igrid, 256, 0, stream_>>>(A, depth, reinterpret_cast<const uint32_t*>(color), cam, Tinv_);
     BF_LAUNCH_CHECK();
+    if (timed) integrateClock_.stop(stream_);
 }
 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)

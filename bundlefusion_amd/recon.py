@@ -1,0 +1,166 @@
+"""Python binding of the reconstruction loop (bf_recon_*) and of the re-integration queue
+(bf_traj_*): mirrors of DepthSensing.cpp's frame loop and TrajectoryManager
+(Source/TrajectoryManager.h:6-118)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import check, lib
+from .abi import BFFixOp, BFReconOptions, BFReconStats, BFTsdfStats
+
+FIX_DEINTEGRATE, FIX_INTEGRATE, FIX_REINTEGRATE, OP_GC = 1, 2, 3, 4
+
+
+def _mat(T):
+    a = np.ascontiguousarray(np.asarray(T, np.float32).reshape(16))
+    return (C.c_float * 16)(*a.tolist())
+
+
+class TrajectoryManager:
+    """bf_traj_*: addFrame / updateOptimizedTransform / reintegrate() list logic."""
+
+    INTEGRATED, NOT_INTEGRATED_NO_TRANSFORM = 0, 1
+
+    def __init__(self, max_frames: int, top_n_active: int = 30, min_pose_dist_sqrt: float = 0.0):
+        self.h = C.c_void_p()
+        check(lib().bf_traj_create(C.c_uint32(max_frames), C.c_uint32(top_n_active), C.c_float(min_pose_dist_sqrt),
+                                   C.byref(self.h)))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().bf_traj_destroy(self.h)
+        except Exception:
+            pass
+
+    def add_frame(self, typ: int, T, idx: int):
+        check(lib().bf_traj_add_frame(self.h, C.c_int32(typ), _mat(T if T is not None else np.zeros(16)), C.c_uint32(idx)))
+
+    def update_optimized(self, T: np.ndarray):
+        T = np.ascontiguousarray(np.asarray(T, np.float32).reshape(-1, 16))
+        check(lib().bf_traj_update_optimized(self.h, T.ctypes.data_as(C.c_void_p), C.c_uint32(T.shape[0])))
+
+    def next_fixes(self, max_fixes: int = 10):
+        ops = (BFFixOp * max(1, max_fixes))()
+        n = C.c_uint32()
+        check(lib().bf_traj_next_fixes(self.h, C.c_uint32(max_fixes), ops, C.byref(n)))
+        return [(ops[i].kind, ops[i].frame, np.array(ops[i].oldT[:], np.float32), np.array(ops[i].newT[:], np.float32))
+                for i in range(n.value)]
+
+    def frame_info(self, idx: int):
+        t = C.c_int32()
+        d = C.c_float()
+        check(lib().bf_traj_frame_info(self.h, C.c_uint32(idx), C.byref(t), C.byref(d)))
+        return t.value, d.value
+
+
+def pose_helper_matrix_to_pose(T) -> np.ndarray:
+    out = (C.c_float * 6)()
+    check(lib().bf_pose_helper_matrix_to_pose(_mat(T), out))
+    return np.array(out[:], np.float32)
+
+
+def recon_options(max_frames: int, **kw) -> BFReconOptions:
+    o = BFReconOptions()
+    o.maxFrames = max_frames
+    o.useLocalDense = 1
+    for k, v in kw.items():
+        if k == "cacheIntrinsics":
+            o.cacheIntrinsics[:] = [float(x) for x in v]
+        else:
+            setattr(o, k, v)
+    return o
+
+
+class Recon:
+    """bf_recon_*: frame loop with on-the-fly re-integration and local/global BA."""
+
+    def __init__(self, params, cam, opts: BFReconOptions, scene_opts=None):
+        self.h = C.c_void_p()
+        self.cam = cam
+        self.params = params
+        check(lib().bf_recon_create(C.byref(params), C.byref(scene_opts) if scene_opts is not None else None,
+                                    C.byref(cam), C.byref(opts), C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().bf_recon_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_frame(self, f: int, depth_ptr: int, color_ptr: int, cache=None, Tinc=None):
+        Tinc = np.eye(4, dtype=np.float32) if Tinc is None else Tinc
+        check(lib().bf_recon_set_frame(self.h, C.c_uint32(f), C.c_void_p(depth_ptr), C.c_void_p(color_ptr),
+                                       C.byref(cache) if cache is not None else None, _mat(Tinc)))
+
+    def set_local_correspondences(self, submap: int, corr_ptr: int, n: int):
+        check(lib().bf_recon_set_local_correspondences(self.h, C.c_uint32(submap), C.c_void_p(corr_ptr), C.c_uint32(n)))
+
+    def set_global_correspondences(self, corr_ptr: int, n: int, prefix: np.ndarray):
+        prefix = np.ascontiguousarray(prefix, np.uint32)
+        self._prefix = prefix
+        check(lib().bf_recon_set_global_correspondences(self.h, C.c_void_p(corr_ptr), C.c_uint32(n),
+                                                        prefix.ctypes.data_as(C.c_void_p), C.c_uint32(len(prefix))))
+
+    def set_initial_pose(self, T0):
+        check(lib().bf_recon_set_initial_pose(self.h, _mat(T0)))
+
+    def process_frame(self, f: int):
+        check(lib().bf_recon_process_frame(self.h, C.c_uint32(f)))
+
+    def finish(self):
+        check(lib().bf_recon_finish(self.h))
+
+    def synchronize(self):
+        check(lib().bf_recon_synchronize(self.h))
+
+    def stats(self) -> dict:
+        s = BFReconStats()
+        check(lib().bf_recon_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in BFReconStats._fields_}
+
+    def reset_stats(self):
+        check(lib().bf_recon_reset_stats(self.h))
+
+    def scene_stats(self) -> dict:
+        s = BFTsdfStats()
+        check(lib().bf_recon_scene_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in BFTsdfStats._fields_}
+
+    def heap_free_count(self) -> int:
+        c = C.c_uint32()
+        check(lib().bf_recon_heap_free_count(self.h, C.byref(c)))
+        return c.value
+
+    def trajectory(self, n: int) -> np.ndarray:
+        T = np.zeros((n, 4, 4), np.float32)
+        check(lib().bf_recon_trajectory(self.h, T.ctypes.data_as(C.c_void_p), C.c_uint32(n)))
+        return T
+
+    def export(self):
+        """(hash entries, heap, heapCounter, voxels) of the loop's scene, as SceneRepHashSDF.export."""
+        from .abi import HASH_ENTRY_DTYPE, VOXEL_DTYPE
+        E = self.params.hashNumBuckets * 4
+        B = self.params.numSDFBlocks
+        hash_ = np.empty(E, HASH_ENTRY_DTYPE)
+        heap = np.empty(B, np.uint32)
+        hc = C.c_uint32()
+        vox = np.empty(B * 512, VOXEL_DTYPE)
+        check(lib().bf_recon_export(self.h, hash_.ctypes.data_as(C.c_void_p), heap.ctypes.data_as(C.c_void_p),
+                                    C.byref(hc), vox.ctypes.data_as(C.c_void_p)))
+        return hash_, heap, hc.value, vox
+
+    def op_log(self):
+        n = C.c_uint32()
+        check(lib().bf_recon_op_log(self.h, None, C.c_uint32(0), C.byref(n)))
+        ops = (BFFixOp * max(1, n.value))()
+        check(lib().bf_recon_op_log(self.h, ops, C.c_uint32(n.value), C.byref(n)))
+        return [(ops[i].kind, ops[i].frame, np.array(ops[i].oldT[:], np.float32), np.array(ops[i].newT[:], np.float32))
+                for i in range(n.value)]

@@ -1,0 +1,114 @@
+"""Seeded synthetic RGB-D stream for the reconstruction loop (SURVEY.md §8(d) "Concrete synthetic
+inputs"): GT trajectory, device-resident depth/colour frames (the CUDAImageManager frame store),
+80x60 dense-term cache frames, per-submap local and global keyframe EntryJ correspondences, and the
+front end's drifted per-frame pose estimates. Everything the loop reads is resident in HBM before
+the first frame is processed."""
+from __future__ import annotations
+
+import ctypes as C
+import time
+
+import numpy as np
+
+from . import DeviceArray, abi, check, depth_camera, lib, synth_pose, synth_scene
+from .abi import ENTRYJ_DTYPE, BFCachedFrame
+from .solver import synth_cache_frames, synth_correspondences
+
+
+def _rodrigues(w):
+    th = float(np.linalg.norm(w))
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+class SyntheticStream:
+    def __init__(self, num_frames: int, width=640, height=480, submap=10, seed=0, drift=(0.05, 0.002),
+                 max_per_pair=25, outliers=0.02, cache_w=80, cache_h=60, log=None):
+        t0 = time.perf_counter()
+        self.F, self.S = num_frames, submap
+        self.log = log or (lambda *a: None)
+        self.scene = synth_scene(seed)
+        f = 577.87 * width / 640.0
+        self.cam = depth_camera(width, height, fx=f, fy=f)
+        self.cache_cam = depth_camera(cache_w, cache_h, fx=f * cache_w / width, fy=f * cache_h / height)
+        self.cache_intrinsics = (self.cache_cam.fx, self.cache_cam.fy, self.cache_cam.mx, self.cache_cam.my)
+        self.gt = np.stack([synth_pose(i) for i in range(num_frames)]).astype(np.float32)
+        self.num_submaps = (num_frames + submap - 1) // submap
+        self.K = self.num_submaps  # keyframe = first frame of each submap
+
+        # device frame store (depth f32, colour uchar4), rendered on the GPU with the noise model
+        P = width * height
+        self.depth = DeviceArray((num_frames, height, width), np.float32)
+        self.color = DeviceArray((num_frames, height, width, 4), np.uint8)
+        for i in range(num_frames):
+            check(lib().bf_synth_render(C.byref(self.scene), abi.mat(self.gt[i]), C.byref(self.cam), C.c_uint32(1),
+                                        C.c_uint32(i), C.c_void_p(self.depth.ptr.value + 4 * P * i),
+                                        C.c_void_p(self.color.ptr.value + 4 * P * i)))
+        check(lib().bf_device_synchronize())
+        self.log(f"rendered {num_frames} frames {width}x{height} in {time.perf_counter() - t0:.1f}s")
+
+        # front-end frame-to-frame estimates (stand-in for computeSiftTransformCU): GT motion with a
+        # random-walk error per frame, so both the local and the global solve have drift to remove
+        rng = np.random.default_rng(seed + 3)
+        self.tinc = np.zeros((num_frames, 4, 4), np.float32)
+        self.tinc[0] = np.eye(4)
+        for i in range(1, num_frames):
+            step = np.eye(4)
+            step[:3, :3] = _rodrigues(rng.normal(size=3) * np.deg2rad(drift[0]))
+            step[:3, 3] = rng.normal(size=3) * drift[1]
+            rel = np.linalg.inv(self.gt[i - 1].astype(np.float64)) @ self.gt[i].astype(np.float64)
+            self.tinc[i] = (rel @ step).astype(np.float32)
+
+        # dense-term cache frames (80x60), one slab per field
+        t1 = time.perf_counter()
+        cf = synth_cache_frames(self.scene, self.gt, self.cache_cam)
+        self.cache_arrays = {k: DeviceArray.from_host(v) for k, v in cf.items()}
+        self.cache = []
+        for i in range(num_frames):
+            c = BFCachedFrame()
+            for k, v in cf.items():
+                setattr(c, k, self.cache_arrays[k].ptr.value + i * v[0].nbytes)
+            self.cache.append(c)
+        self.log(f"cache frames in {time.perf_counter() - t1:.1f}s")
+
+        # local correspondences per submap (frames base..base+S, local indices)
+        t2 = time.perf_counter()
+        locs, self.local_off, self.local_n = [], [], []
+        off = 0
+        for s in range(self.num_submaps):
+            base = s * submap
+            poses = self.gt[base:min(base + submap + 1, num_frames)]
+            c = synth_correspondences(self.scene, poses, self.cam, max_per_pair=max_per_pair, min_covis=0.3,
+                                      noise=0.0015, outlier_frac=0.0, seed=1000 + s) if len(poses) > 1 else \
+                np.zeros(0, ENTRYJ_DTYPE)
+            locs.append(c)
+            self.local_off.append(off)
+            self.local_n.append(len(c))
+            off += len(c)
+        allloc = np.concatenate(locs) if off else np.zeros(1, ENTRYJ_DTYPE)
+        self.local_corr = DeviceArray.from_host(allloc)
+        # global keyframe correspondences, ordered by max(i, j) as keyframes arrive
+        kf = self.gt[::submap][: self.K]
+        g = synth_correspondences(self.scene, kf, self.cam, max_per_pair=max_per_pair, min_covis=0.3, noise=0.0015,
+                                  outlier_frac=outliers, seed=2)
+        order = np.argsort(np.maximum(g["i"], g["j"]), kind="stable")
+        g = g[order]
+        self.global_host = g
+        self.global_corr = DeviceArray.from_host(g if len(g) else np.zeros(1, ENTRYJ_DTYPE))
+        mx = np.maximum(g["i"], g["j"])
+        self.global_prefix = np.searchsorted(mx, np.arange(self.K), side="right").astype(np.uint32)
+        self.log(f"correspondences: {off} local, {len(g)} global in {time.perf_counter() - t2:.1f}s")
+
+    def attach(self, recon, frames=None):
+        """Register every frame, correspondence list and the initial pose with a Recon."""
+        P4 = 4 * self.cam.imageWidth * self.cam.imageHeight
+        for i in range(self.F if frames is None else frames):
+            recon.set_frame(i, self.depth.ptr.value + P4 * i, self.color.ptr.value + P4 * i, self.cache[i], self.tinc[i])
+        for s in range(self.num_submaps):
+            if self.local_n[s]:
+                recon.set_local_correspondences(s, self.local_corr.ptr.value + 32 * self.local_off[s], self.local_n[s])
+        recon.set_global_correspondences(self.global_corr.ptr.value, len(self.global_host), self.global_prefix)
+        recon.set_initial_pose(self.gt[0])

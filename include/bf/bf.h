@@ -166,6 +166,95 @@ int bf_synth_correspondences(const BFSynthScene* scene, const float* poses, uint
 int bf_synth_cache_frame(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam, float* depth,
                          float* campos, float* normals, uint8_t* normalsU8, float* intensity, float* intensityDeriv);
 
+/* ---- reconstruction loop: integrate + re-integration queue + local/global BA ------------
+ * The frame loop of DepthSensing.cpp (integrate :1003-1056, reintegrate :854-902) driven by
+ * TrajectoryManager (TrajectoryManager.cpp:8-200) and the OnlineBundler local->global
+ * hierarchy (OnlineBundler.cpp:242-416). Frames are borrowed device pointers that must stay
+ * resident (the CUDAImageManager frame store); correspondences are EntryJ inputs. */
+typedef struct BFFixOp {
+    int32_t kind;     /* 1 de-integrate (oldT), 2 integrate (newT), 3 re-integrate (oldT -> newT) */
+    uint32_t frame;
+    float oldT[16];
+    float newT[16];
+} BFFixOp;
+
+typedef struct BFReconOptions {
+    uint32_t maxFrames;          /* frame-store / trajectory capacity */
+    uint32_t submapSize;         /* s_submapSize = 10 */
+    uint32_t maxFrameFixes;      /* s_maxFrameFixes = 10 */
+    uint32_t topNActive;         /* s_topNActive = 30 */
+    float minPoseDistSqrt;       /* s_minPoseDistSqrt = 0 */
+    uint32_t localNonLin, localLin;    /* s_numLocalNonLinIterations 2 / s_numLocalLinIterations 100 */
+    uint32_t globalNonLin, globalLin;  /* s_numGlobalNonLinIterations 3 / s_numGlobalLinIterations 150 */
+    uint32_t maxKeyframes;       /* global solver images */
+    uint32_t maxLocalCorr;       /* per submap */
+    uint32_t maxGlobalCorr;
+    float maxResidualThresh;     /* s_optMaxResThresh = 0.08 */
+    int32_t useLocalDense;       /* SBA::m_bUseLocalDense = true */
+    uint32_t cacheWidth, cacheHeight;  /* 80 x 60 */
+    float cacheIntrinsics[4];    /* fx fy mx my of the cache resolution */
+    int32_t enableTiming;        /* record k_integrate / solve device times (bench) */
+    int32_t recordOps;           /* keep a log of every scene call (parity replay in tests) */
+    BFSolverOptions solver;
+} BFReconOptions;
+
+typedef struct BFReconStats {
+    uint64_t frames;             /* processFrame calls */
+    uint64_t integrations;       /* scene integrate calls (new frames + fixes) */
+    uint64_t deintegrations;
+    uint64_t fixOps;             /* re-integration queue ops (de-, re-, integrate) */
+    uint64_t localSolves, globalSolves;
+    uint64_t globalGnIterations, globalPcgIterations;
+    uint64_t localGnIterations, localPcgIterations;
+    uint64_t removedPairs;       /* max-residual removals */
+    uint64_t integrateLaunches;  /* timed k_integrate launches */
+    double integrateKernelMs;    /* summed device time of those launches */
+    double localSolveMs, globalSolveMs;  /* summed device time of the solves */
+} BFReconStats;
+
+typedef struct bf_recon bf_recon;
+int bf_recon_create(const BFHashParams* params, const BFSceneOptions* sceneOpts, const BFDepthCameraParams* cam,
+                    const BFReconOptions* opts, bf_recon** out);
+int bf_recon_destroy(bf_recon* r);
+/* frame store entry f: device depth / colour, HOST BFCachedFrame of device pointers (or NULL),
+ * and the front end's frame-to-frame estimate Tinc (camera f expressed in camera f-1; the
+ * stand-in for computeSiftTransformCU, OnlineBundler.cu:6-71; ignored for f = 0) */
+int bf_recon_set_frame(bf_recon* r, uint32_t f, const float* depth, const uint8_t* color,
+                       const BFCachedFrame* cache, const float Tinc[16]);
+int bf_recon_set_local_correspondences(bf_recon* r, uint32_t submap, BFEntryJ* corr, uint32_t n);
+/* global list ordered by max(i,j); prefix[k] (HOST) = number of entries with max(i,j) <= k */
+int bf_recon_set_global_correspondences(bf_recon* r, BFEntryJ* corr, uint32_t n, const uint32_t* prefix,
+                                        uint32_t numKeyframes);
+int bf_recon_set_initial_pose(bf_recon* r, const float T0[16]);
+int bf_recon_process_frame(bf_recon* r, uint32_t f);
+int bf_recon_finish(bf_recon* r);
+int bf_recon_synchronize(bf_recon* r);
+int bf_recon_stats(bf_recon* r, BFReconStats* out);
+int bf_recon_scene_stats(bf_recon* r, BFTsdfStats* out);
+int bf_recon_reset_stats(bf_recon* r);  /* zero loop + scene counters and the device clocks */
+int bf_recon_heap_free_count(bf_recon* r, uint32_t* count);
+/* integrated camera->world transform per frame (HOST float[16*n], -inf rows when not integrated) */
+int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n);
+/* debugHash-style dump of the loop's scene (same layout as bf_scene_export) */
+int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
+/* with recordOps: the scene calls issued so far, in order (kind 1 de-integrate with oldT,
+ * 2 integrate with newT, 4 garbage collect); copies min(cap, total) entries, *n = total */
+int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n);
+
+/* ---- re-integration queue alone (host; TrajectoryManager.h:6-118) ---------------------- */
+typedef struct bf_traj bf_traj;
+
+int bf_traj_create(uint32_t maxFrames, uint32_t topNActive, float minPoseDistSqrt, bf_traj** out);
+int bf_traj_destroy(bf_traj* t);
+/* type: 0 Integrated, 1 NotIntegrated_NoTransform (T ignored) */
+int bf_traj_add_frame(bf_traj* t, int32_t type, const float T[16], uint32_t idx);
+int bf_traj_update_optimized(bf_traj* t, const float* T, uint32_t numFrames);
+/* reintegrate() list logic: up to maxFixes ops into ops[maxFixes]; *n = count */
+int bf_traj_next_fixes(bf_traj* t, uint32_t maxFixes, BFFixOp* ops, uint32_t* n);
+int bf_traj_frame_info(bf_traj* t, uint32_t idx, int32_t* type, float* dist);
+/* PoseHelper::MatrixToPose (PoseHelper.h:332-362): out[6] = [translation part | omega] */
+int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,6 +90,15 @@ void or_ba_solve(BFEntryJ* corr, const int* validImages, const ORSolveParams* p,
 void or_ba_dense_system(const int* validImages, const ORSolveParams* p, const float* rot, const float* trans,
                         float* jtjOut, float* jtrOut, double* energyOut, uint32_t* pairsOut);
 
+/* TrajectoryManager + reintegrate() list logic (traj.cpp) */
+void or_pose_helper_matrix_to_pose(const float* T, float out[6]);
+void* or_traj_create(unsigned maxFrames, unsigned topN, float minDist);
+void or_traj_destroy(void* h);
+void or_traj_add_frame(void* h, int type, const float* T, unsigned idx);
+void or_traj_update_optimized(void* h, const float* T, unsigned numFrames);
+unsigned or_traj_next_fixes(void* h, unsigned maxFixes, int* kinds, unsigned* frames, float* oldT, float* newT);
+void or_traj_frame_info(void* h, unsigned idx, int* type, float* dist);
+
 #ifdef __cplusplus
 }
 #endif
