@@ -13,9 +13,10 @@ bundle adjustment is replicated on every rank (deterministic inputs, identical s
 is no data-path collective. The host-side barrier / max-over-ranks uses gloo.
 
 roofline: the dominant kernel is k_integrate; its launches are timed with HIP events on the scene
-stream inside the timed region; algorithmic bytes per launch = 16 B per visible block (list
-entry) + 24 B per voxel updated inside the truncation band (12 B read + 12 B write) + 8 B per
-pixel (depth + colour read once), from the device counters of the same launches.
+stream inside the timed region; algorithmic bytes per launch = 16 B per block of its work list
+(the band-culled visible list entry) + 24 B per voxel updated inside the truncation band (12 B
+read + 12 B write) + 8 B per pixel (depth + colour read once), from the device counters of the
+same launches.
 cpu_baseline: the CPU oracle (oracle/, serial C++ restatement) timed on a bounded sample of the
 same workload on this host, scaled by the GPU run's op counts to frames/s.
 """
@@ -96,6 +97,56 @@ def cpu_baseline(stream, params, gpu, budget_s=20.0):
             "ms_per_gn_iter": (t_gn + t_pcg * gpu["pcg_per_solve"] / max(gpu["gn_per_solve"], 1e-9)) * 1e3}
 
 
+def global_solve_timing(stream, K, reps=3):
+    """ms per GN iteration of a standalone global solve (3 GN x 150 PCG, the reference's global
+    schedule) over the final K keyframes and their correspondences, timed with HIP events on the
+    solver stream (no TSDF work competing for the CUs)."""
+    import bundlefusion_amd as bfa
+    from bundlefusion_amd.solver import SolverBundling
+    rng = np.random.default_rng(7)
+    kf = stream.gt[::stream.S][:K].astype(np.float64)
+    T = np.empty((K, 4, 4), np.float32)
+    D = np.eye(4)
+    for k in range(K):  # GT with a random-walk drift (0.05 deg, 2 mm per keyframe), SURVEY §8(d)
+        if k:
+            w = rng.normal(size=3) * np.deg2rad(0.05)
+            th = np.linalg.norm(w)
+            A = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]]) / th
+            step = np.eye(4)
+            step[:3, :3] = np.eye(3) + np.sin(th) * A + (1 - np.cos(th)) * A @ A
+            step[:3, 3] = rng.normal(size=3) * 0.002
+            D = D @ step
+        T[k] = (kf[k] @ D).astype(np.float32)
+    n = int(stream.global_prefix[K - 1])
+    S = SolverBundling(K + 1, max(1000, 25 * (K + 1) * K // 2))
+    dT = bfa.DeviceArray.from_host(T)
+    dv = bfa.DeviceArray.from_host(np.ones(K, np.int32))
+    dr = bfa.DeviceArray((K, 3), np.float32)
+    dt = bfa.DeviceArray((K, 3), np.float32)
+    corr = bfa.DeviceArray.from_host(stream.global_host[:n])
+    L = bfa.lib()
+    timer = C.c_void_p()
+    bfa.check(L.bf_timer_create(C.byref(timer)))
+    ms_tot, gn_tot, pcg_tot = 0.0, 0, 0
+    for r in range(reps + 1):
+        corr.upload(stream.global_host[:n])
+        S.matrices_to_poses(dT, K, dr, dt, dv)
+        S.synchronize()
+        ms = C.c_float()
+        bfa.check(L.bf_solver_timer_start(S.h, timer))
+        S.solve(corr, n, dv, K, 3, 150, [1.0, 1.0, 1.0], rot=dr, trans=dt)
+        bfa.check(L.bf_solver_timer_stop(S.h, timer, C.byref(ms)))
+        res = S.result()
+        if r:  # first solve is warmup
+            ms_tot += ms.value
+            gn_tot += res["gnIterations"]
+            pcg_tot += res["pcgIterations"]
+    bfa.check(L.bf_timer_destroy(timer))
+    S.close()
+    return {"ms_per_gn_iter": ms_tot / max(1, gn_tot), "keyframes": K, "correspondences": n,
+            "gn_iters": gn_tot / reps, "pcg_iters": pcg_tot / reps, "ms_per_solve": ms_tot / reps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,7 +181,7 @@ def main():
     stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log)
     params = bfa.hash_params(voxel_size=args.voxel, num_buckets=args.buckets, num_blocks=args.blocks)
     K = stream.K
-    opts = recon_options(F, enableTiming=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
+    opts = recon_options(F, enableTiming=1, asyncBundling=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
                          maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2))
     so = BFSceneOptions()
     so.shardCount, so.shardIndex, so.shardChunk = world, rank, 1.0
@@ -170,7 +221,7 @@ def main():
     frames = S * args.steps
     P = args.width * args.height
     launches = max(1, st["integrateLaunches"])
-    alg_bytes = 16 * ss["visible"] + 24 * ss["voxelsUpdated"] + 8 * P * launches
+    alg_bytes = 16 * ss["bandBlocks"] + 24 * ss["voxelsUpdated"] + 8 * P * launches
     per_launch_bytes = alg_bytes / launches
     per_launch_s = st["integrateKernelMs"] / 1e3 / launches
     achieved = per_launch_bytes / per_launch_s / 1e9
@@ -178,7 +229,8 @@ def main():
     if args.traffic and os.path.exists(args.traffic):
         traffic = json.load(open(args.traffic)).get("k_integrate_bytes_per_launch")
     gn = max(1, st["globalGnIterations"])
-    ms_gn = st["globalSolveMs"] / gn
+    ms_gn_loop = st["globalSolveMs"] / gn
+    solo = global_solve_timing(stream, min(K, args.warmup + args.steps))
     out = {
         "metric": "frames/s integrate+global-BA on 640x480 @4mm voxels",
         "value": frames / dt,
@@ -198,7 +250,8 @@ def main():
                                f"local 2x100 + global 3x150 GN x PCG per submap",
                    "frames_timed": frames, "keyframes_final": K,
                    "parallelism": f"tsdf-chunk-shard{world}+ba-replicated" if world > 1 else "single"},
-        "ms_per_gn_iter": ms_gn,
+        "ms_per_gn_iter": solo["ms_per_gn_iter"],
+        "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
         "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "launches": st["integrateLaunches"], "avg_launch_us": per_launch_s * 1e6,
@@ -208,7 +261,10 @@ def main():
                  "global_gn_iters": st["globalGnIterations"], "global_pcg_iters": st["globalPcgIterations"],
                  "removed_pairs": st["removedPairs"], "global_solve_ms": st["globalSolveMs"],
                  "local_solve_ms": st["localSolveMs"], "integrate_kernel_ms": st["integrateKernelMs"],
-                 "heap_free": rc.heap_free_count()},
+                 "heap_free": rc.heap_free_count(),
+                 "per_op": {"visible_blocks": ss["visible"] / launches, "band_blocks": ss["bandBlocks"] / launches,
+                            "voxels_updated": ss["voxelsUpdated"] / launches,
+                            "allocated_blocks": ss["scanned"] / launches}},
     }
     if rank == 0 and not args.no_cpu_baseline:
         gpu = {"keyframes": int(min(K, (args.warmup + args.steps))),

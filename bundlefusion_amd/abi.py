@@ -82,7 +82,7 @@ class BFRayCastParams(C.Structure):
 class BFTsdfStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",
-        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps")]
+        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks")]
 
 
 class BFSceneOptions(C.Structure):
@@ -166,7 +166,8 @@ class BFReconOptions(C.Structure):
                 ("globalLin", C.c_uint32), ("maxKeyframes", C.c_uint32), ("maxLocalCorr", C.c_uint32),
                 ("maxGlobalCorr", C.c_uint32), ("maxResidualThresh", C.c_float), ("useLocalDense", C.c_int32),
                 ("cacheWidth", C.c_uint32), ("cacheHeight", C.c_uint32), ("cacheIntrinsics", C.c_float * 4),
-                ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("solver", BFSolverOptions)]
+                ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("asyncBundling", C.c_int32),
+                ("solver", BFSolverOptions)]
 
 
 class BFReconStats(C.Structure):

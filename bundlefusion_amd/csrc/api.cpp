@@ -539,6 +539,12 @@ int bf_recon_finish(bf_recon* r) {
     r->r->finish();
     BF_CATCH
 }
+int bf_recon_reintegrate(bf_recon* r) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->reintegrate();
+    BF_CATCH
+}
 int bf_recon_synchronize(bf_recon* r) {
     BF_TRY
     BF_REQUIRE(r, BF_ERR_ARG, "null recon");

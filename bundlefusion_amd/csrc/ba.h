@@ -62,6 +62,7 @@ struct SolveResult {
     uint32_t highResidualCount;
     uint32_t numDensePairs;
     uint32_t error;
+    uint32_t removedI = 0xFFFFFFFFu, removedJ = 0xFFFFFFFFu;  // pair invalidated by removeMaxResidualAsync
 };
 
 class Solver {
@@ -70,6 +71,13 @@ public:
     ~Solver();
     void solve(const SolveArgs& a);       // async
     SolveResult result();                 // synchronizes
+    // async variants for the reconstruction loop: copy the result words into pinned host memory
+    // (K_COUNT = 16 words) and decode them once the stream has passed that point
+    void resultAsync(uint32_t* pinnedCtrl);
+    static SolveResult decodeResult(const uint32_t* ctrl);
+    static constexpr uint32_t kResultWords = 16;
+    // device-side SBA::removeMaxResidualCUDA after a solve with findMaxResidual
+    void removeMaxResidualAsync(BFEntryJ* corr, uint32_t n, int* valid, uint32_t numImages, float thresh);
     const int* numEntriesPerRow() const { return rowCount_.p; }  // getVarToCorrNumEntriesPerRow
     hipStream_t stream() const { return stream_; }
     const SolverConfig& config() const { return cfg_; }
@@ -102,6 +110,10 @@ private:
 };
 
 SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* opts);
+
+// initNextGlobalTransformCU: rot/trans[s+1] = log(exp(rot/trans[s]) * exp(localRot/Trans[last]))
+void seed_keyframe(const float* localRot, const float* localTrans, uint32_t last, float* rot, float* trans, uint32_t s,
+                   hipStream_t st);
 
 // SBA.cu:75-119 — float4x4 <-> (rot, trans) for valid images
 void matrices_to_poses(const float* T, uint32_t n, float* rot, float* trans, const int* valid, hipStream_t s);

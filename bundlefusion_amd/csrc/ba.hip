@@ -29,7 +29,7 @@ constexpr int SORT_CAP = 8192;  // LDS row sort capacity
 enum VecField { V_DELTA = 0, V_R, V_Z, V_P, V_AP, V_M, V_NUM };
 enum CtrlWord {
     K_TICKET = 0, K_PCG_DONE, K_GN_DONE, K_GN_ITERS, K_PCG_ITERS, K_RDOTZ, K_NPAIRS, K_LAST_W,
-    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_COUNT = 16
+    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J, K_COUNT = 16
 };
 
 struct BA {
@@ -765,7 +765,8 @@ __global__ __launch_bounds__(WG) void k_residuals(BA a) {
 }
 
 __global__ void k_solve_begin(uint32_t* ctrl) {
-    if (threadIdx.x < K_COUNT && threadIdx.x != K_ERROR) ctrl[threadIdx.x] = 0;
+    if (threadIdx.x < K_COUNT && threadIdx.x != K_ERROR)
+        ctrl[threadIdx.x] = (threadIdx.x == K_RM_I || threadIdx.x == K_RM_J) ? BF_INVALID_IMAGE : 0u;
 }
 
 // ---- SBA.cu / SIFTImageManager.cu helpers ----
@@ -803,6 +804,48 @@ __global__ void k_check_frames(const int* numEntries, int* valid, uint32_t numIm
             }
         }
     }
+}
+
+// initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 = global[s] * local[last]
+__global__ void k_seed_keyframe(const float* localRot, const float* localTrans, uint32_t last, float* rot, float* trans,
+                                uint32_t s) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const m4 G = pose_to_matrix(mk3(rot[3 * s], rot[3 * s + 1], rot[3 * s + 2]), mk3(trans[3 * s], trans[3 * s + 1], trans[3 * s + 2]));
+    const m4 L = pose_to_matrix(mk3(localRot[3 * last], localRot[3 * last + 1], localRot[3 * last + 2]),
+                                mk3(localTrans[3 * last], localTrans[3 * last + 1], localTrans[3 * last + 2]));
+    f3 r, t;
+    matrix_to_pose(mul44(G, L), r, t);
+    rot[3 * (s + 1)] = r.x; rot[3 * (s + 1) + 1] = r.y; rot[3 * (s + 1) + 2] = r.z;
+    trans[3 * (s + 1)] = t.x; trans[3 * (s + 1) + 1] = t.y; trans[3 * (s + 1) + 2] = t.z;
+}
+
+// SBA::removeMaxResidualCUDA (SBA.cpp:164-203) + getMaxResidual (CUDASolverBundling.cpp:429-452) on
+// the device: pick the pair of the max residual when it exceeds the threshold and is not (0, <10)
+__global__ void k_pick_maxres_pair(uint32_t* ctrl, const BFEntryJ* corr, float thresh) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t pi = BF_INVALID_IMAGE, pj = BF_INVALID_IMAGE;
+    const float mr = __uint_as_float(ctrl[K_MAXRES]);
+    if (mr > thresh) {
+        const BFEntryJ e = corr[ctrl[K_MAXIDX]];
+        if (e.imgIdx_i != BF_INVALID_IMAGE && !(e.imgIdx_i == 0 && e.imgIdx_j < 10)) {
+            pi = e.imgIdx_i;
+            pj = e.imgIdx_j;
+        }
+    }
+    ctrl[K_RM_I] = pi;
+    ctrl[K_RM_J] = pj;
+}
+__global__ void k_invalidate_picked_pair(const uint32_t* ctrl, BFEntryJ* corr, uint32_t n) {
+    const uint32_t i = ctrl[K_RM_I], j = ctrl[K_RM_J];
+    if (i == BF_INVALID_IMAGE) return;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+        if (corr[c].imgIdx_i == i && corr[c].imgIdx_j == j) { corr[c].imgIdx_i = BF_INVALID_IMAGE; corr[c].imgIdx_j = BF_INVALID_IMAGE; }
+}
+// CheckForInvalidFramesSimpleCU (SIFTImageManager.cu:725-745), only after a removal
+__global__ void k_check_frames_if_removed(const uint32_t* ctrl, const int* numEntries, int* valid, uint32_t numImages) {
+    if (ctrl[K_RM_I] == BF_INVALID_IMAGE) return;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < numImages && numEntries[t] == 0) valid[t] = 0;
 }
 
 }  // namespace
@@ -937,6 +980,22 @@ SolveResult Solver::result() {
     uint32_t c[K_COUNT];
     BF_HIP(hipMemcpyAsync(c, ctrl_.p, sizeof(c), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
+    return decodeResult(c);
+}
+
+void Solver::resultAsync(uint32_t* pinnedCtrl) {
+    BF_HIP(hipMemcpyAsync(pinnedCtrl, ctrl_.p, sizeof(uint32_t) * K_COUNT, hipMemcpyDeviceToHost, stream_));
+}
+
+void Solver::removeMaxResidualAsync(BFEntryJ* corr, uint32_t n, int* valid, uint32_t numImages, float thresh) {
+    k_pick_maxres_pair<<<1, 64, 0, stream_>>>(ctrl_.p, corr, thresh);
+    BF_LAUNCH_CHECK();
+    if (n) k_invalidate_picked_pair<<<std::max(1u, std::min(div_up(n, 256), 1024u)), 256, 0, stream_>>>(ctrl_.p, corr, n);
+    k_check_frames_if_removed<<<div_up(numImages, 64), 64, 0, stream_>>>(ctrl_.p, rowCount_.p, valid, numImages);
+    BF_LAUNCH_CHECK();
+}
+
+SolveResult Solver::decodeResult(const uint32_t* c) {
     SolveResult r{};
     r.gnIterations = c[K_GN_ITERS];
     r.pcgIterations = c[K_PCG_ITERS];
@@ -946,7 +1005,15 @@ SolveResult Solver::result() {
     r.highResidualCount = c[K_HIGHCOUNT];
     r.numDensePairs = c[K_NPAIRS];
     r.error = c[K_ERROR];
+    r.removedI = c[K_RM_I];
+    r.removedJ = c[K_RM_J];
     return r;
+}
+
+void seed_keyframe(const float* localRot, const float* localTrans, uint32_t last, float* rot, float* trans, uint32_t s,
+                   hipStream_t st) {
+    k_seed_keyframe<<<1, 64, 0, st>>>(localRot, localTrans, last, rot, trans, s);
+    BF_LAUNCH_CHECK();
 }
 
 void matrices_to_poses(const float* T, uint32_t n, float* rot, float* trans, const int* valid, hipStream_t s) {

@@ -11,6 +11,7 @@ BFMat4 mat4_mul(const BFMat4& a, const BFMat4& b);  // api.cpp
 
 namespace {
 const float NEG_INF = -std::numeric_limits<float>::infinity();
+constexpr uint32_t RING = 8;  // bundling results in flight before the loop waits for the oldest
 BFMat4 ninf_mat() {
     BFMat4 m;
     for (float& v : m.m) v = NEG_INF;
@@ -23,6 +24,12 @@ BFMat4 identity() {
 }
 template <class T>
 T or_default(T v, T d) { return v ? v : d; }
+template <class T>
+T* pinned(size_t n) {
+    void* p = nullptr;
+    BF_HIP(hipHostMalloc(&p, sizeof(T) * std::max<size_t>(n, 1), hipHostMallocDefault));
+    return static_cast<T*>(p);
+}
 }  // namespace
 
 Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCameraParams& cam, const BFReconOptions& o)
@@ -64,14 +71,17 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
         global_->solveClock().enable(true);
     }
 
+    const uint32_t L = S + 1, K = opt_.maxKeyframes;
     frames_.resize(opt_.maxFrames);
-    localCorr_.assign(maxSubmaps, {nullptr, 0});
-    localTraj_.resize(maxSubmaps);
-    globalT_.assign(opt_.maxKeyframes, identity());
-    globalValid_.assign(opt_.maxKeyframes, 1);
+    localCorr_.assign(maxSubmaps + 1, {nullptr, 0});
+    localTraj_.resize(maxSubmaps + 1);
+    localKnown_.assign(maxSubmaps + 1, 0);
+    kf_.assign(K, identity());
+    kfSolved_.assign(K, 0);
+    globalT_.assign(K, identity());
+    globalValid_.assign(K, 1);
     complete_.resize(opt_.maxFrames);
 
-    const uint32_t L = S + 1, K = opt_.maxKeyframes;
     dLocalRot_.alloc(3 * L);
     dLocalTrans_.alloc(3 * L);
     dLocalT_.alloc(16 * L);
@@ -90,11 +100,28 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     BF_HIP(hipMemsetAsync(dGlobalRot_.p, 0, dGlobalRot_.bytes(), baStream_));
     BF_HIP(hipMemsetAsync(dGlobalTrans_.p, 0, dGlobalTrans_.bytes(), baStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
+
+    ring_.resize(RING);
+    for (Pending& p : ring_) {
+        BF_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+        p.localT = pinned<float>(16 * L);
+        p.globalT = pinned<float>(16 * (size_t)K);
+        p.valid = pinned<int>(K);
+        p.ctrl = pinned<uint32_t>(2 * Solver::kResultWords);
+        p.localInit = pinned<float>(16 * L);
+        p.cacheTable = pinned<BFCachedFrame>(L);
+    }
 }
 
 Recon::~Recon() {
     if (sceneStream_) (void)hipStreamSynchronize(sceneStream_);
     if (baStream_) (void)hipStreamSynchronize(baStream_);
+    for (Pending& p : ring_) {
+        if (p.done) (void)hipEventDestroy(p.done);
+        for (void* q : {(void*)p.localT, (void*)p.globalT, (void*)p.valid, (void*)p.ctrl, (void*)p.localInit,
+                        (void*)p.cacheTable})
+            if (q) (void)hipHostFree(q);
+    }
     scene_.reset();
     local_.reset();
     global_.reset();
@@ -126,6 +153,8 @@ void Recon::setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t*
 }
 
 void Recon::setInitialPose(const BFMat4& T0) {
+    kf_[0] = T0;
+    kfSolved_[0] = 1;
     globalT_[0] = T0;
     BF_HIP(hipMemcpyAsync(dSeedT_.p, T0.m, 64, hipMemcpyHostToDevice, baStream_));
     matrices_to_poses(dSeedT_.p, 1, dGlobalRot_.p, dGlobalTrans_.p, dOne_.p, baStream_);
@@ -168,11 +197,19 @@ void Recon::processFrame(uint32_t f) {
     BF_REQUIRE(f < opt_.maxFrames && frames_[f].set, BF_ERR_STATE, "frame not in the frame store");
     const uint32_t S = opt_.submapSize;
     const uint32_t s = f / S;
-    if (f % S == 0 && f > 0) endSubmap(s - 1, S + 1);
-    runReintegrate();
+    applyPending(false);
     FrameRef& fr = frames_[f];
+    if (f % S == 0 && f > 0) {
+        endSubmap(s - 1, S + 1);
+        if (!opt_.asyncBundling) applyPending(true);
+        if (!kfSolved_[s]) {  // solver result not back yet: dead-reckon the new keyframe
+            BF_REQUIRE(s < kf_.size(), BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
+            kf_[s] = mat4_mul(kf_[s - 1], mat4_mul(frames_[f - 1].Tlocal, fr.Tinc));
+        }
+    }
+    runReintegrate();
     fr.Tlocal = (f % S == 0) ? identity() : mat4_mul(frames_[f - 1].Tlocal, fr.Tinc);
-    const BFMat4 T = mat4_mul(globalT_[s], fr.Tlocal);  // getCurrentIntegrationFrame
+    const BFMat4 T = mat4_mul(kf_[s], fr.Tlocal);  // getCurrentIntegrationFrame
     scene_->integrate(T, fr.depth, fr.color, cam_, false, nullptr);
     logOp(2, f, &T);
     st_.integrations++;
@@ -181,37 +218,54 @@ void Recon::processFrame(uint32_t f) {
     st_.frames++;
 }
 
+void Recon::reintegrate() {
+    applyPending(false);
+    runReintegrate();
+}
+
 void Recon::finish() {
     const uint32_t S = opt_.submapSize;
     if (numFrames_ == 0) return;
     const uint32_t s = (numFrames_ - 1) / S;
-    if (s != lastSubmapSolved_) endSubmap(s, numFrames_ - s * S);
+    if (s != lastSubmapEnqueued_) endSubmap(s, numFrames_ - s * S);
+    synchronize();
 }
 
-// end of submap s: optimizeLocal -> processGlobal/optimizeGlobal -> updateTrajectory
+// end of submap s: optimizeLocal -> processGlobal/optimizeGlobal -> initNextGlobalTransform, all
+// enqueued on the BA stream; the poses come back through pinned memory and an event
 void Recon::endSubmap(uint32_t s, uint32_t n) {
     const uint32_t S = opt_.submapSize;
     const uint32_t base = s * S;
+    if (inflight_.size() == RING) {  // ring full: wait for the oldest result
+        Pending& old = ring_[inflight_.front()];
+        BF_HIP(hipEventSynchronize(old.done));
+        apply(old);
+        inflight_.pop_front();
+    }
+    const uint32_t slot = ringNext_;
+    ringNext_ = (ringNext_ + 1) % RING;
+    Pending& P = ring_[slot];
+    P.submap = s;
+    P.numLocal = n;
+    P.localSolved = P.globalSolved = false;
+
     // ---- local solve over frames base .. base+n-1 (first frame fixed) ----------------------
-    std::vector<BFMat4> Tl(n);
-    std::vector<BFCachedFrame> cache(n);
     bool haveCache = opt_.useLocalDense != 0;
     for (uint32_t i = 0; i < n; i++) {
         const FrameRef& fr = frames_[base + i];
         BF_REQUIRE(fr.set, BF_ERR_STATE, "local solve over a frame not in the frame store");
         // the submap's last local frame is the next submap's first: chain it from frame S-1
-        Tl[i] = (i < S) ? fr.Tlocal : mat4_mul(frames_[base + S - 1].Tlocal, fr.Tinc);
-        cache[i] = fr.cache;
+        const BFMat4 Tl = (i < S) ? fr.Tlocal : mat4_mul(frames_[base + S - 1].Tlocal, fr.Tinc);
+        std::memcpy(P.localInit + 16 * i, Tl.m, 64);
+        P.cacheTable[i] = fr.cache;
         if (!fr.cache.depth) haveCache = false;
     }
-    std::vector<BFMat4>& traj = localTraj_[s];
-    traj = Tl;
+    BF_HIP(hipMemcpyAsync(dLocalT_.p, P.localInit, 64 * n, hipMemcpyHostToDevice, baStream_));
+    matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_.p, dLocalValid_.p, baStream_);
     const auto& lc = localCorr_[s];
     if (n >= 2 && lc.first && lc.second > 0) {
-        BF_HIP(hipMemcpyAsync(dLocalT_.p, Tl.data(), 64 * n, hipMemcpyHostToDevice, baStream_));
         if (haveCache)
-            BF_HIP(hipMemcpyAsync(dLocalCache_.p, cache.data(), sizeof(BFCachedFrame) * n, hipMemcpyHostToDevice, baStream_));
-        matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_.p, dLocalValid_.p, baStream_);
+            BF_HIP(hipMemcpyAsync(dLocalCache_.p, P.cacheTable, sizeof(BFCachedFrame) * n, hipMemcpyHostToDevice, baStream_));
         std::vector<float> ws(opt_.localNonLin, 1.0f), wd(opt_.localNonLin), wc(opt_.localNonLin, 0.0f);
         for (uint32_t i = 0; i < opt_.localNonLin; i++) wd[i] = haveCache ? (float)(i + 1) : 0.0f;  // SBA.cpp:28-31
         SolveArgs a{};
@@ -233,16 +287,16 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         a.rebuildJT = true;
         a.findMaxResidual = false;  // optimizeLocal: no max residual removal (OnlineBundler.cpp:255)
         local_->solve(a);
+        local_->resultAsync(P.ctrl);
+        P.localSolved = true;
         poses_to_matrices(dLocalRot_.p, dLocalTrans_.p, n, dLocalT_.p, dLocalValid_.p, baStream_);
-        BF_HIP(hipMemcpyAsync(traj.data(), dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
-        const SolveResult r = local_->result();  // synchronizes the BA stream
-        st_.localSolves++;
-        st_.localGnIterations += r.gnIterations;
-        st_.localPcgIterations += r.pcgIterations;
+        BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
+    } else {
+        std::memcpy(P.localT, P.localInit, 64 * n);
     }
     // ---- global solve over keyframes 0..s ---------------------------------------------------
     const uint32_t nk = s + 1;
-    BF_REQUIRE(nk < opt_.maxKeyframes, BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
+    BF_REQUIRE(nk + 1 <= opt_.maxKeyframes, BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
     const uint32_t ncorr = (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_;
     if (nk >= 2 && globalCorr_ && ncorr > 0) {
         std::vector<float> ws(opt_.globalNonLin, 1.0f), wz(opt_.globalNonLin, 0.0f);  // SBA.cpp:34-39, dense off
@@ -261,48 +315,80 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         a.rebuildJT = true;
         a.findMaxResidual = true;
         global_->solve(a);
-        const SolveResult r = global_->result();
+        // removeMaxResidualCUDA with getMaxResidual's (0, <10) exemption, on the device
+        global_->removeMaxResidualAsync(globalCorr_, ncorr, dGlobalValid_.p, nk, opt_.maxResidualThresh);
+        global_->resultAsync(P.ctrl + Solver::kResultWords);
+        P.globalSolved = true;
+    }
+    poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
+    BF_HIP(hipMemcpyAsync(P.globalT, dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
+    BF_HIP(hipMemcpyAsync(P.valid, dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
+    P.numKeyframes = nk;
+    // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
+    if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_.p, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_);
+    BF_HIP(hipEventRecord(P.done, baStream_));
+    inflight_.push_back(slot);
+    lastSubmapEnqueued_ = s;
+}
+
+void Recon::applyPending(bool block) {
+    while (!inflight_.empty()) {
+        Pending& P = ring_[inflight_.front()];
+        if (block) {
+            BF_HIP(hipEventSynchronize(P.done));
+        } else {
+            const hipError_t q = hipEventQuery(P.done);
+            if (q == hipErrorNotReady) break;
+            BF_HIP(q);
+        }
+        apply(P);
+        inflight_.pop_front();
+    }
+}
+
+// updateTrajectoryCU (OnlineBundler.cu:73-110) + TrajectoryManager::updateOptimizedTransform
+void Recon::apply(Pending& P) {
+    const uint32_t S = opt_.submapSize, s = P.submap, n = P.numLocal, nk = P.numKeyframes;
+    std::vector<BFMat4>& traj = localTraj_[s];
+    traj.resize(n);
+    std::memcpy(traj.data(), P.localT, 64 * n);
+    localKnown_[s] = 1;
+    std::memcpy(globalValid_.data(), P.valid, 4 * nk);
+    for (uint32_t k = 0; k < nk; k++) {
+        if (!globalValid_[k]) continue;
+        std::memcpy(globalT_[k].m, P.globalT + 16 * k, 64);
+        kf_[k] = globalT_[k];
+        kfSolved_[k] = 1;
+    }
+    if (n == S + 1 && globalValid_[s]) {
+        kf_[s + 1] = mat4_mul(globalT_[s], traj[S]);
+        kfSolved_[s + 1] = 1;
+    }
+    if (P.localSolved) {
+        const SolveResult r = Solver::decodeResult(P.ctrl);
+        st_.localSolves++;
+        st_.localGnIterations += r.gnIterations;
+        st_.localPcgIterations += r.pcgIterations;
+    }
+    if (P.globalSolved) {
+        const SolveResult r = Solver::decodeResult(P.ctrl + Solver::kResultWords);
         st_.globalSolves++;
         st_.globalGnIterations += r.gnIterations;
         st_.globalPcgIterations += r.pcgIterations;
-        // removeMaxResidualCUDA (SBA.cpp:164-203) with getMaxResidual's exemption (CUDASolverBundling.cpp:429-452)
-        if (r.maxResidual > opt_.maxResidualThresh && r.maxResidualIndex >= 0) {
-            BFEntryJ e{};
-            BF_HIP(hipMemcpyAsync(&e, globalCorr_ + r.maxResidualIndex, sizeof(e), hipMemcpyDeviceToHost, baStream_));
-            BF_HIP(hipStreamSynchronize(baStream_));
-            if (!(e.imgIdx_i == 0 && e.imgIdx_j < 10) && e.imgIdx_i != BF_INVALID_IMAGE) {
-                invalidate_image_pair(globalCorr_, ncorr, e.imgIdx_i, e.imgIdx_j, baStream_);
-                check_invalid_frames(global_->numEntriesPerRow(), dGlobalValid_.p, nk, globalCorr_, ncorr, false,
-                                     baStream_);
-                st_.removedPairs++;
-            }
-        }
-        poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
-        BF_HIP(hipMemcpyAsync(globalT_.data(), dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
-        BF_HIP(hipMemcpyAsync(globalValid_.data(), dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
-        BF_HIP(hipStreamSynchronize(baStream_));
+        if (r.removedI != BF_INVALID_IMAGE) st_.removedPairs++;
     }
-    // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
-    if (n == S + 1) {
-        globalT_[s + 1] = mat4_mul(globalT_[s], traj[S]);
-        BF_HIP(hipMemcpyAsync(dSeedT_.p, globalT_[s + 1].m, 64, hipMemcpyHostToDevice, baStream_));
-        matrices_to_poses(dSeedT_.p, 1, dGlobalRot_.p + 3 * (s + 1), dGlobalTrans_.p + 3 * (s + 1), dOne_.p, baStream_);
-        BF_HIP(hipStreamSynchronize(baStream_));
-    }
-    // ---- updateTrajectoryCU (OnlineBundler.cu:73-110) + TrajectoryManager::updateOptimizedTransform
-    const uint32_t nf = std::min(base + n, numFrames_);
-    const uint32_t optimized = std::min(base + std::min(n, S), nf);
+    const uint32_t optimized = std::min(S * s + std::min(n, S), numFrames_);
     for (uint32_t g = 0; g < optimized; g++) {
         const uint32_t k = g / S;
-        complete_[g] = globalValid_[k] ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();
+        complete_[g] = (globalValid_[k] && localKnown_[k]) ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();
     }
     tm_->updateOptimizedTransforms(complete_.data(), optimized);
-    lastSubmapSolved_ = s;
 }
 
 void Recon::synchronize() {
     BF_HIP(hipStreamSynchronize(sceneStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
+    applyPending(true);
 }
 
 BFReconStats Recon::stats() {

@@ -6,17 +6,20 @@
 // are inputs, as if the matcher had filled SIFTImageManager's global correspondence array.
 //
 // Ordering per frame f (submap size S, s = f / S):
-//   1. if f is the first frame of submap s > 0: end of submap s-1 -> local solve over its S+1
-//      frames (dense term on the 80x60 cache), global solve over keyframes 0..s-1 with max
-//      residual removal, seed keyframe s = global[s-1] * local[s-1][S] (initNextGlobalTransformCU),
-//      trajectory update complete[g] = global[g/S] * local[g/S][g%S] (updateTrajectoryCU)
+//   0. pick up finished bundling results (async mode): poses -> trajectory -> TrajectoryManager
+//   1. if f is the first frame of submap s > 0: enqueue the end of submap s-1 on the BA stream —
+//      local solve over its S+1 frames (dense term on the 80x60 cache), global solve over
+//      keyframes 0..s-1, device-side max residual removal (SBA.cpp:164-203), seed of keyframe s
+//      = global[s-1] * local[s-1][S] (initNextGlobalTransformCU), async copies of the poses
 //   2. reintegrate(): up to maxFrameFixes de-/re-/integrate ops from the TrajectoryManager, then GC
-//   3. integrate frame f with global[s] * L[f] and addFrame(Integrated), where L chains the front
-//      end's frame-to-frame estimates Tinc inside the submap (L = I at its first frame)
-// TSDF work runs on the scene stream, BA on its own stream; the host waits on the BA stream only
-// for the poses it needs (as the reference copies them device->host, TrajectoryManager.cpp:38).
+//   3. integrate frame f with kf[s] * L[f] and addFrame(Integrated), where L chains the front end's
+//      frame-to-frame estimates Tinc inside the submap (L = I at its first frame) and kf[s] is the
+//      keyframe pose — from the solver when its result has arrived, else dead-reckoned
+// In async mode the TSDF never waits for the solver, as the reference's reconstruction thread
+// never waits for its bundling thread; in sync mode step 1 waits, which makes runs repeatable.
 #pragma once
 #include <array>
+#include <deque>
 #include <memory>
 #include <vector>
 
@@ -38,8 +41,9 @@ public:
     void setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes);
     void setInitialPose(const BFMat4& T0);
     void processFrame(uint32_t f);
-    void finish();  // end of sequence: solve the last (partial) submap
-    void synchronize();
+    void finish();       // end of sequence: solve the last (partial) submap and wait for all results
+    void reintegrate();  // one render-loop iteration without a new frame: apply results, fix ops, GC
+    void synchronize();  // drain both streams and apply every pending bundling result
 
     BFReconStats stats();
     void resetStats();
@@ -48,8 +52,22 @@ public:
     const std::vector<BFFixOp>& opLog() const { return log_; }
 
 private:
+    struct Pending {  // one submap's bundling results in flight
+        uint32_t submap = 0, numLocal = 0, numKeyframes = 0;
+        bool localSolved = false, globalSolved = false;
+        hipEvent_t done = nullptr;
+        float* localT = nullptr;    // pinned [S+1][16]
+        float* globalT = nullptr;   // pinned [maxKeyframes][16]
+        int* valid = nullptr;       // pinned [maxKeyframes]
+        uint32_t* ctrl = nullptr;   // pinned [2][kResultWords]: local, global solver words
+        float* localInit = nullptr;          // pinned staging [S+1][16] (H2D of the initial local poses)
+        BFCachedFrame* cacheTable = nullptr; // pinned staging [S+1] (H2D of the local cache table)
+    };
     void endSubmap(uint32_t s, uint32_t numFrames);
+    void applyPending(bool block);
+    void apply(Pending& p);
     void runReintegrate();
+    void logOp(int kind, uint32_t frame, const BFMat4* T);
 
     BFReconOptions opt_;
     BFDepthCameraParams cam_;
@@ -72,13 +90,20 @@ private:
     uint32_t globalCorrN_ = 0;
     std::vector<uint32_t> globalPrefix_;
 
-    std::vector<BFMat4> globalT_;        // host copy of the keyframe poses
+    std::vector<BFMat4> kf_;            // keyframe poses used for integration (solver or dead reckoning)
+    std::vector<char> kfSolved_;        // kf_[k] came from the solver
+    std::vector<BFMat4> globalT_;       // last solver keyframe poses
     std::vector<int> globalValid_;
     std::vector<std::vector<BFMat4>> localTraj_;  // per submap, S+1 local poses
+    std::vector<char> localKnown_;
     std::vector<BFMat4> complete_;
     std::vector<FixOp> ops_;
-    uint32_t lastSubmapSolved_ = 0xFFFFFFFFu;
+    uint32_t lastSubmapEnqueued_ = 0xFFFFFFFFu;
     uint32_t numFrames_ = 0;
+
+    std::vector<Pending> ring_;
+    std::deque<uint32_t> inflight_;     // ring indices in submap order
+    uint32_t ringNext_ = 0;
 
     DevBuf<float> dLocalRot_, dLocalTrans_, dLocalT_;
     DevBuf<int> dLocalValid_;
@@ -90,7 +115,6 @@ private:
 
     BFReconStats st_{};
     std::vector<BFFixOp> log_;
-    void logOp(int kind, uint32_t frame, const BFMat4* T);
 };
 
 }  // namespace bf

@@ -7,7 +7,12 @@
 //   voxels    BFVoxel[B * 512]    12-B AoS voxels, one 6 KiB run per block
 //   blockPos  int4[B]             per heap block: {x, y, z, allocated} — lets compactify stream
 //                                 only the allocated pool prefix instead of the whole hash table
-//   visible   int4[B]             compacted frustum list {x, y, z, ptr} (16 B vs 32 B HashEntry)
+//   visible   int4[B]             compacted frustum list {x, y, z, ptr} (16 B vs 32 B HashEntry);
+//                                 GC walks this list, as the reference walks d_hashCompactified
+//   band      int4[B]             the subset of `visible` whose voxels can reach the truncation band
+//                                 of the current depth map (conservative cull against per-8x8-tile
+//                                 depth bounds) — the list integrate walks
+//   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op
 //   ctrl      uint32[16]          device-resident counters (heap counter, visible count, ...)
 //   cand/candSet/candSlot/ovf     alloc scratch (per-op candidate list, global dedup set)
 //   victims                       GC scratch
@@ -28,6 +33,8 @@ enum Ctrl {
     C_GC_SIMPLE = 5,   // GC victims deletable without touching a collision list
     C_GC_LIST = 6,     // GC victims that touch a collision list (serial path)
     C_ERR = 7,         // error bits (1: candidate buffer overflow, 2: heap exhausted, 4: dedup set full)
+    C_BAND = 8,        // blocks of the visible list that may hold a voxel inside the truncation band
+    C_TICKET = 9,      // last-workgroup ticket of k_alloc_insert (self-resetting)
     C_COUNT = 16
 };
 
@@ -87,6 +94,9 @@ private:
     DevBuf<BFVoxel> voxels_;
     DevBuf<int4> blockPos_;
     DevBuf<int4> visible_;
+    DevBuf<int4> band_;
+    DevBuf<float2> tiles_;
+    uint32_t tilesCap_ = 0;
     DevBuf<uint32_t> ctrl_;
     DevBuf<unsigned long long> stats_;  // [64 slots][16]
     DevBuf<unsigned long long> cand_;
@@ -98,6 +108,7 @@ private:
     DevBuf<uint32_t> blockCount_;
     uint32_t candSetMask_;
     int numCUs_;
+    unsigned integrateGrid_[2] = {0, 0};
     KernelClock integrateClock_;
 };
 

@@ -36,6 +36,9 @@ struct HashArgs {
     int4* blockPos;
     uint32_t* blockCount;
     int4* visible;
+    int4* band;
+    const float2* tiles;
+    uint32_t tilesW, tilesH;
     uint32_t* ctrl;
     unsigned long long* stats;  // [STAT_SLOTS][16] counters, field order of BFTsdfStats
     uint32_t numBuckets, numEntries, numBlocks, maxList;
@@ -55,7 +58,14 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
-enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS };
+// 12-B voxel as one 4-byte-aligned unit, so loads/stores become single dwordx3 accesses
+struct __attribute__((packed, aligned(4))) Vox3 {
+    uint32_t a, b, c;
+};
+
+enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS,
+                 S_BAND };
+constexpr int DEPTH_TILE = 8;  // 8x8-pixel depth-bound tiles for the band cull
 constexpr int STAT_SLOTS = 64;
 
 // Workgroup-level counter flush: wave shuffle-reduce, LDS add, then one global atomic per
@@ -162,10 +172,81 @@ __global__ void k_reset_heap(uint32_t* heap, int4* blockPos, uint32_t* blockCoun
 __global__ void k_begin_op(uint32_t* ctrl, unsigned long long* stats) {
     if (threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
+        ctrl[C_BAND] = 0;
         ctrl[C_CAND] = 0;
         ctrl[C_OVF] = 0;
         stats[S_OPS]++;
     }
+}
+
+// Per-op counter reset fused with the depth-bound tiles of the band cull: one wave per 8x8 tile
+// reduces min / max over the depths integrate would accept (not -inf, below
+// maxIntegrationDistance, CUDASceneRepHashSDF.cu:450-457). Empty tiles get (+inf, -inf).
+__global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned long long* stats,
+                                                        const float* __restrict__ depthImg, uint32_t W, uint32_t H,
+                                                        uint32_t tilesW, uint32_t tilesH, float maxDist, float2* tiles) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl[C_VISIBLE] = 0;
+        ctrl[C_BAND] = 0;
+        ctrl[C_CAND] = 0;
+        ctrl[C_OVF] = 0;
+        stats[S_OPS]++;
+    }
+    const uint32_t lane = lane_id();
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (t >= tilesW * tilesH) return;
+    const uint32_t x = (t % tilesW) * DEPTH_TILE + (lane & 7), y = (t / tilesW) * DEPTH_TILE + (lane >> 3);
+    float lo = INFINITY, hi = -INFINITY;
+    if (x < W && y < H) {
+        const float d = depthImg[y * W + x];
+        if (d != -INFINITY && d < maxDist) { lo = d; hi = d; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off));
+        hi = fmaxf(hi, __shfl_xor(hi, off));
+    }
+    if (lane == 0) tiles[t] = make_float2(lo, hi);
+}
+
+// Conservative test that a block may contain a voxel integrate will update: project the 8 voxel-
+// centre corners (convex hull -> bounding pixel rectangle, grown by one pixel), take the depth
+// bounds of the covered tiles and reject when every depth is too far behind or in front of the
+// block for |d - z| < truncation + truncScale * d to hold (1 cm slack for rounding). Exactness:
+// a rejected block has no voxel with an in-band sample, so skipping it changes no voxel.
+__device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx, int by,
+                                 int bz) {
+    const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
+    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
+    float zlo = INFINITY, zhi = -INFINITY, xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
+        const f3 p = xform(Tinv, w);
+        if (!(p.z > 1e-3f)) return true;  // straddles the camera plane: keep
+        const float sx = p.x * cam.fx / p.z + cam.mx, sy = p.y * cam.fy / p.z + cam.my;
+        zlo = fminf(zlo, p.z); zhi = fmaxf(zhi, p.z);
+        xlo = fminf(xlo, sx); xhi = fmaxf(xhi, sx);
+        ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
+    }
+    const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
+    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
+    if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) return false;  // every voxel off-screen
+    const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
+    const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
+    const int tx0 = x0 / DEPTH_TILE, tx1 = x1 / DEPTH_TILE, ty0 = y0 / DEPTH_TILE, ty1 = y1 / DEPTH_TILE;
+    if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > 64) return true;  // very close block: not worth the walk
+    float dlo = INFINITY, dhi = -INFINITY;
+    for (int ty = ty0; ty <= ty1; ty++)
+        for (int tx = tx0; tx <= tx1; tx++) {
+            const float2 t = A.tiles[ty * A.tilesW + tx];
+            dlo = fminf(dlo, t.x);
+            dhi = fmaxf(dhi, t.y);
+        }
+    if (!(dlo <= dhi)) return false;  // no integrable depth under the block
+    const float slack = 0.01f;
+    if (dlo * (1.0f - A.truncScale) >= zhi + A.truncation + slack) return false;  // surface far behind
+    if (dhi * (1.0f + A.truncScale) <= zlo - A.truncation - slack) return false;  // surface far in front
+    return true;
 }
 
 // allocKernel, CUDASceneRepHashSDF.cu:165-251: per-pixel DDA over 8^3-block cells. Emits the
@@ -213,33 +294,28 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
         if (bp.z - rayMin.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
     }
 
+    // phase 1: walk the ray's blocks and collect the tile's distinct in-frustum owned blocks in
+    // the LDS set (compute only; no global memory on the DDA's critical path)
     unsigned long long emitted = 0;
     for (uint32_t iter = 0; iter < 1024 && active; iter++) {
-        bool want = false;
-        unsigned long long key = 0;
         if (block_in_frustum(cam, Tinv, id.x, id.y, id.z, A.voxelSize) && owned(A, id.x, id.y, id.z) &&
             !streamed_out(A, id.x, id.y, id.z)) {
-            key = block_key(id.x, id.y, id.z);
+            const unsigned long long key = block_key(id.x, id.y, id.z);
             uint32_t h = mix_hash(key) & (LDS_SET - 1);
-            want = true;  // if the tile set is congested, emit anyway (global dedup follows)
+            bool placed = false;
             for (int p = 0; p < 16; p++) {
-                unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
-                if (old == EMPTY_KEY) break;
-                if (old == key) { want = false; break; }
+                const unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
+                if (old == EMPTY_KEY || old == key) { placed = true; break; }
                 h = (h + 1) & (LDS_SET - 1);
             }
-            if (want) want = (lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY);
-        }
-        const unsigned long long m = __ballot(want);
-        if (want) {
-            const int leader = __ffsll((long long)m) - 1;
-            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
-            uint32_t base = 0;
-            if ((int)lane_id() == leader) base = atomicAdd(&A.ctrl[C_CAND], (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (base + rank < candCap) cand[base + rank] = key;
-            else atomicOr(&A.ctrl[C_ERR], 1u);
-            emitted++;
+            // congested tile set (rare): look the block up right here and emit it if absent
+            // (duplicates are removed by the global dedup in k_alloc_insert)
+            if (!placed && lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY) {
+                const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
+                if (k < candCap) cand[k] = key;
+                else atomicOr(&A.ctrl[C_ERR], 1u);
+                emitted++;
+            }
         }
         // traverse (CUDASceneRepHashSDF.cu:231-246)
         if (tMax.x < tMax.y && tMax.x < tMax.z) {
@@ -256,9 +332,33 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
             tMax.y += tDelta.y;
         }
     }
+    __syncthreads();
+    // phase 2: every thread checks a share of the distinct blocks against the hash in parallel
+    // (one round of lookups instead of one per DDA step) and emits the absent ones
+    for (int k0 = 0; k0 < LDS_SET; k0 += blockDim.x) {
+        const unsigned long long key = set[k0 + threadIdx.x];
+        bool want = false;
+        if (key != EMPTY_KEY) {
+            const i3 b = key_block(key);
+            want = lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY;
+        }
+        const unsigned long long m = __ballot(want);
+        if (want) {
+            const int leader = __ffsll((long long)m) - 1;
+            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+            uint32_t base = 0;
+            if ((int)lane_id() == leader) base = atomicAdd(&A.ctrl[C_CAND], (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (base + rank < candCap) cand[base + rank] = key;
+            else atomicOr(&A.ctrl[C_ERR], 1u);
+            emitted++;
+        }
+    }
     const bool inImage = x < cam.imageWidth && y < cam.imageHeight;
     flush_stats2(A.stats, S_CAND, emitted, S_PIXELS, inImage ? 1ull : 0ull);
 }
+
+__device__ void alloc_overflow_serial(const HashArgs& A, const unsigned long long* ovf);
 
 // allocBlock, VoxelUtilHashSDF.h:549-655 (bucket path), lock-free: global dedup, CAS on the
 // slot's ptr, wave-aggregated heap pop.
@@ -337,12 +437,25 @@ __global__ __launch_bounds__(256) void k_alloc_insert(HashArgs A, const unsigned
         }
     }
     flush_stats2(A.stats, S_ALLOC, allocated, -1, 0);
+    // the last workgroup to finish replays the bucket-full candidates serially (the collision-
+    // list path), so no separate launch is needed: release fence + ticket, acquire on the winner
+    __shared__ bool s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(&A.ctrl[C_TICKET], 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x == 0) {
+        __threadfence();
+        A.ctrl[C_TICKET] = 0;
+        if (A.ctrl[C_OVF]) alloc_overflow_serial(A, ovf);
+    }
 }
 
 // allocBlock collision-list path (VoxelUtilHashSDF.h:573-654), serial: bucket-full candidates
 // are rare at the configured load factor; one lane replays the reference insert for each.
-__global__ void k_alloc_overflow(HashArgs A, const unsigned long long* ovf) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void alloc_overflow_serial(const HashArgs& A, const unsigned long long* ovf) {
     const uint32_t n = min(A.ctrl[C_OVF], OVF_CAP);
     for (uint32_t k = 0; k < n; k++) {
         const i3 pos = key_block(ovf[k]);
@@ -398,6 +511,11 @@ __global__ void k_alloc_overflow(HashArgs A, const unsigned long long* ovf) {
     }
 }
 
+__global__ void k_alloc_overflow(HashArgs A, const unsigned long long* ovf) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    alloc_overflow_serial(A, ovf);
+}
+
 __global__ void k_alloc_cleanup(const uint32_t* ctrl, uint32_t candCap, const int* candSlot, unsigned long long* candSet) {
     const uint32_t n = min(ctrl[C_CAND], candCap);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -408,28 +526,58 @@ __global__ void k_alloc_cleanup(const uint32_t* ctrl, uint32_t candCap, const in
 
 // compactifyHashAllInOneKernel, CUDASceneRepHashSDF.cu:324-366: stream the allocated pool
 // prefix [0, highWater), keep the in-frustum blocks; wave ballot + one atomic per wave.
-__global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraParams cam, BFMat4 Tinv) {
+template <bool BAND>
+__global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraParams cam, BFMat4 Tinv, uint32_t candCap,
+                                                    const int* __restrict__ candSlot, unsigned long long* candSet) {
+    if (BAND) {  // release this op's alloc dedup-set slots (was k_alloc_cleanup)
+        const uint32_t n = min(A.ctrl[C_CAND], candCap);
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+            const int sl = candSlot[i];
+            if (sl >= 0) candSet[sl] = EMPTY_KEY;
+        }
+    }
+    // one list append per workgroup iteration: wave ballots -> LDS prefix over the 4 waves ->
+    // a single atomic per list (instead of one per wave on the hot counter)
+    __shared__ uint32_t s_cnt[2][4], s_base[2];
     const uint32_t hw = A.ctrl[C_HIGHWATER];
-    const uint32_t lane = lane_id();
-    unsigned long long scanned = 0, vis = 0;
-    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < hw; base += gridDim.x * blockDim.x) {
-        const uint32_t i = base + lane;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    unsigned long long scanned = 0, vis = 0, band = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < hw; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
         int4 bp = make_int4(0, 0, 0, 0);
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
         const bool keep = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
-        const unsigned long long m = __ballot(keep);
-        scanned += alloc ? 1 : 0;
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            uint32_t b0 = 0;
-            if ((int)lane == leader) b0 = atomicAdd(&A.ctrl[C_VISIBLE], (uint32_t)__popcll(m));
-            b0 = __shfl(b0, leader);
-            if (keep) A.visible[b0 + __popcll(m & lanemask_lt())] = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
-            if (keep) vis++;
+        const bool inb = BAND && keep && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z);
+        const unsigned long long m0 = __ballot(keep), m1 = __ballot(inb);
+        if (lane == 0) {
+            s_cnt[0][wv] = (uint32_t)__popcll(m0);
+            s_cnt[1][wv] = (uint32_t)__popcll(m1);
         }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            const uint32_t tot = s_cnt[threadIdx.x][0] + s_cnt[threadIdx.x][1] + s_cnt[threadIdx.x][2] + s_cnt[threadIdx.x][3];
+            s_base[threadIdx.x] = tot ? atomicAdd(&A.ctrl[threadIdx.x == 0 ? C_VISIBLE : C_BAND], tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t off0 = s_base[0], off1 = s_base[1];
+        for (uint32_t k = 0; k < wv; k++) {
+            off0 += s_cnt[0][k];
+            off1 += s_cnt[1][k];
+        }
+        const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
+        if (keep) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
+        if (inb) A.band[off1 + __popcll(m1 & lanemask_lt())] = ent;
+        scanned += alloc ? 1 : 0;
+        vis += keep ? 1 : 0;
+        band += inb ? 1 : 0;
+        __syncthreads();  // s_cnt / s_base reuse
     }
     flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
+    if (BAND) {
+        __syncthreads();  // thread 0 of the first flush reads its LDS sums before they are reset
+        flush_stats2(A.stats, S_BAND, band, -1, 0);
+    }
 }
 
 // integrateDepthMapKernel<deIntegrate>, CUDASceneRepHashSDF.cu:420-521. One wave per block:
@@ -438,7 +586,7 @@ template <bool DEINT>
 __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __restrict__ depthImg,
                                                    const uint32_t* __restrict__ colorImg, BFDepthCameraParams cam,
                                                    BFMat4 Tinv) {
-    const uint32_t nvis = A.ctrl[C_VISIBLE];
+    const uint32_t nvis = A.ctrl[C_BAND];
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -447,7 +595,7 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
     const float wUpd = 1.0f;  // weightUpdate forced to 1 (:465-466)
     unsigned long long updated = 0;
     for (uint32_t b = wave; b < nvis; b += nwaves) {
-        const int4 e = A.visible[b];
+        const int4 e = A.band[b];
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         // phase 1: project the lane's 8 voxels and issue all depth gathers back to back
         float depth[BF_SDF_BLOCK_SIZE], pz[BF_SDF_BLOCK_SIZE];
@@ -478,10 +626,11 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
             osdf[z] = 0.0f; ow[z] = 0.0f; oc[z] = 0u; cc[z] = 0u;
             if (in) {
                 band |= 1u << z;
-                const BFVoxel* vp = A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane);
-                osdf[z] = vp->sdf;
-                ow[z] = vp->weight;
-                oc[z] = *reinterpret_cast<const uint32_t*>(vp->color);
+                // one 12-B load per voxel (global_load_dwordx3) instead of three dword loads
+                const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane));
+                osdf[z] = __uint_as_float(v.a);
+                ow[z] = __uint_as_float(v.b);
+                oc[z] = v.c;
                 cc[z] = colorImg[pix[z]];
             }
         }
@@ -519,10 +668,11 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
                 nw = fmaxf(0.0f, w0 - wUpd);
                 if (nw <= 0.001f) { nsdf = 0.0f; ncol = 0u; nw = 0.0f; }
             }
-            BFVoxel* vp = A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane);
-            vp->sdf = nsdf;
-            vp->weight = nw;
-            *reinterpret_cast<uint32_t*>(vp->color) = ncol;
+            Vox3 nv;
+            nv.a = __float_as_uint(nsdf);
+            nv.b = __float_as_uint(nw);
+            nv.c = ncol;
+            *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane)) = nv;  // dwordx3 store
             // per-block count of voxels with (uint)weight != 0 (GC decision, :606/:625)
             dcount += (int)(nw >= 1.0f) - (int)(w0 >= 1.0f);
             nupd++;
@@ -683,6 +833,7 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
                           int4* vis, uint32_t* ctrl, unsigned long long* st, const uint32_t* bitMask) {
     HashArgs a;
     a.hash = hash; a.heap = heap; a.voxels = vox; a.blockPos = bp; a.blockCount = bc; a.visible = vis; a.ctrl = ctrl; a.stats = st;
+    a.band = nullptr; a.tiles = nullptr; a.tilesW = a.tilesH = 0;
     a.numBuckets = cfg.hp.hashNumBuckets;
     a.numEntries = cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE;
     a.numBlocks = cfg.hp.numSDFBlocks;
@@ -719,6 +870,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     voxels_.alloc((size_t)B_ * BF_VOXELS_PER_BLOCK);
     blockPos_.alloc(B_);
     visible_.alloc(B_);
+    band_.alloc(B_);
     ctrl_.alloc(C_COUNT);
     stats_.alloc(STAT_SLOTS * 16);
     cand_.alloc(cfg_.candCapacity);
@@ -733,6 +885,13 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
+    // k_integrate walks its block list with a static grid stride: size the grid to exactly the
+    // resident workgroups, so every wave gets the same share in one round (no tail round)
+    int occ0 = 0, occ1 = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false>, 256, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true>, 256, 0));
+    integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
+    integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
     float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -744,7 +903,8 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
 Scene::~Scene() {}
 
 size_t Scene::deviceBytes() const {
-    return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + ctrl_.bytes() +
+    return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
+           tiles_.bytes() + ctrl_.bytes() +
            stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
            gcList_.bytes() + blockCount_.bytes();
 }
@@ -770,13 +930,12 @@ void Scene::alloc(const float* depth, const BFDepthCameraParams& cam, const uint
     dim3 g(div_up(cam.imageWidth, ALLOC_TILE), div_up(cam.imageHeight, ALLOC_TILE));
     k_alloc_collect<<<g, 256, 0, stream_>>>(A, depth, cam, T_, Tinv_, cand_.p, cfg_.candCapacity);
     BF_LAUNCH_CHECK();
-    const unsigned grid = (unsigned)numCUs_ * 4;
+    // few candidates per op in steady state: a small grid keeps the last-workgroup ticket cheap
+    const unsigned grid = 64;
     k_alloc_insert<<<grid, 256, 0, stream_>>>(A, cand_.p, cfg_.candCapacity, candSet_.p, candSetMask_, candSlot_.p, ovf_.p);
     BF_LAUNCH_CHECK();
-    k_alloc_overflow<<<1, 64, 0, stream_>>>(A, ovf_.p);
-    BF_LAUNCH_CHECK();
-    k_alloc_cleanup<<<grid, 256, 0, stream_>>>(ctrl_.p, cfg_.candCapacity, candSlot_.p, candSet_.p);
-    BF_LAUNCH_CHECK();
+    // k_alloc_insert's last workgroup runs the serial collision-list inserts; the dedup-set
+    // cleanup runs inside the following k_compactify
 }
 
 void Scene::compactify(const BFMat4& T, const BFDepthCameraParams& cam) {
@@ -784,7 +943,7 @@ void Scene::compactify(const BFMat4& T, const BFDepthCameraParams& cam) {
     Tinv_ = mat4_inverse(T);
     beginOp();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_compactify<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_);
+    k_compactify<false><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr);
     BF_LAUNCH_CHECK();
 }
 
@@ -794,13 +953,24 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     BF_REQUIRE(depth != nullptr, BF_ERR_ARG, "depth is null");
     T_ = T;
     Tinv_ = mat4_inverse(T);
-    beginOp();
+    const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
+    if (tw * th > tilesCap_) {
+        tiles_.alloc((size_t)tw * th);
+        tilesCap_ = tw * th;
+    }
+    k_begin_op_tiles<<<div_up((size_t)tw * th * 64, 256), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p);
+    BF_LAUNCH_CHECK();
     if (!deint) alloc(depth, cam, bitMask);
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
+    A.band = band_.p;
+    A.tiles = tiles_.p;
+    A.tilesW = tw;
+    A.tilesH = th;
     const unsigned grid = (unsigned)numCUs_ * 4;
-    k_compactify<<<grid, 256, 0, stream_>>>(A, cam, Tinv_);
+    k_compactify<true><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p);
     BF_LAUNCH_CHECK();
-    const unsigned igrid = (unsigned)numCUs_ * 8;
+    const unsigned igrid = deint ? integrateGrid_[1] : integrateGrid_[0];
     const bool timed = integrateClock_.enabled();
     if (timed) integrateClock_.start(stream_);
     if (deint)
@@ -854,7 +1024,7 @@ BFTsdfStats Scene::stats() {
     for (int sl = 0; sl < STAT_SLOTS; sl++)
         for (int f = 0; f < 16; f++) sum[f] += h[sl * 16 + f];
     BFTsdfStats s;
-    static_assert(sizeof(BFTsdfStats) == 10 * 8, "stats layout");
+    static_assert(sizeof(BFTsdfStats) == 11 * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
     return s;
 }

@@ -118,6 +118,9 @@ class Recon:
     def finish(self):
         check(lib().bf_recon_finish(self.h))
 
+    def reintegrate(self):
+        check(lib().bf_recon_reintegrate(self.h))
+
     def synchronize(self):
         check(lib().bf_recon_synchronize(self.h))
 

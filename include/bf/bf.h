@@ -195,6 +195,9 @@ typedef struct BFReconOptions {
     float cacheIntrinsics[4];    /* fx fy mx my of the cache resolution */
     int32_t enableTiming;        /* record k_integrate / solve device times (bench) */
     int32_t recordOps;           /* keep a log of every scene call (parity replay in tests) */
+    int32_t asyncBundling;       /* 1: solves run on their own stream and their poses are picked up
+                                    by the frame loop when ready (the reference's bundling thread);
+                                    0: the loop waits for each submap's solves (deterministic) */
     BFSolverOptions solver;
 } BFReconOptions;
 
@@ -228,6 +231,9 @@ int bf_recon_set_global_correspondences(bf_recon* r, BFEntryJ* corr, uint32_t n,
 int bf_recon_set_initial_pose(bf_recon* r, const float T0[16]);
 int bf_recon_process_frame(bf_recon* r, uint32_t f);
 int bf_recon_finish(bf_recon* r);
+/* a loop iteration without a new frame (the reference keeps calling reintegrate() from its render
+ * loop after scanning ends): pick up results, run up to maxFrameFixes queue ops, GC */
+int bf_recon_reintegrate(bf_recon* r);
 int bf_recon_synchronize(bf_recon* r);
 int bf_recon_stats(bf_recon* r, BFReconStats* out);
 int bf_recon_scene_stats(bf_recon* r, BFTsdfStats* out);

@@ -139,6 +139,7 @@ typedef struct BFTsdfStats {
     uint64_t gcFreed;         /* blocks freed by GC */
     uint64_t allocOverflow;   /* candidates dropped: candidate buffer / heap exhausted */
     uint64_t integrateOps;    /* integrate + de-integrate calls */
+    uint64_t bandBlocks;      /* visible blocks that passed the truncation-band cull (integrate's list) */
 } BFTsdfStats;
 
 #ifdef __cplusplus

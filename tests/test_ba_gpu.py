@@ -55,12 +55,24 @@ def assert_parity(g, o, rot_tol=ROT_TOL, trans_tol=TRANS_TOL, energy_rtol=1e-2, 
     assert er <= rot_tol and et <= trans_tol, (er, et, gres, ores)
     assert gres["error"] == 0, gres
     np.testing.assert_array_equal(gc["i"] == INVALID, oc["i"] == INVALID)
-    if same_argmax:
-        assert gres["maxResidualIndex"] == ores["maxResidualIndex"], (gres, ores)
     # a residual moves by at most ~ |p| * rotation diff + translation diff between the two solutions
-    assert gres["maxResidual"] == pytest.approx(ores["maxResidual"], abs=4.0 * er + et + 1e-5)
+    tol = 4.0 * er + et + 1e-5
+    if same_argmax and gres["maxResidualIndex"] != ores["maxResidualIndex"]:
+        # near-tied maxima may swap within that tolerance: the GPU's pick must be a maximum too
+        r = residual_inf(oc[gres["maxResidualIndex"]], orot, otr)
+        assert r >= ores["maxResidual"] - tol, (gres, ores, r)
+    assert gres["maxResidual"] == pytest.approx(ores["maxResidual"], abs=tol)
     assert gres["energy"] == pytest.approx(ores["finalEnergy"], rel=energy_rtol, abs=1e-7)
     return er, et
+
+
+def residual_inf(e, rot, trans):
+    """|T_i p_i - T_j p_j|_inf of one EntryJ under the given poses (evalAbsMaxResidualDevice)."""
+    Ti = pose_to_matrix(rot[e["i"]], trans[e["i"]]).astype(np.float64)
+    Tj = pose_to_matrix(rot[e["j"]], trans[e["j"]]).astype(np.float64)
+    a = Ti[:3, :3] @ e["pos_i"] + Ti[:3, 3]
+    b = Tj[:3, :3] @ e["pos_j"] + Tj[:3, 3]
+    return float(np.max(np.abs(a - b)))
 
 
 def smoke_ba():

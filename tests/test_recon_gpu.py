@@ -20,30 +20,35 @@ from tsdf_compare import compare_states
 pytestmark = pytest.mark.gpu
 
 
-def run_loop(F=40, W=160, H=120, voxel=0.01, record=True, drift=(0.05, 0.002)):
-    st = SyntheticStream(F, width=W, height=H, drift=drift)
+def run_loop(F=40, W=160, H=120, voxel=0.01, record=True, drift=(0.05, 0.002), async_ba=0, outliers=0.0):
+    # outlier-free correspondences: with 4 keyframes a single solve cannot yet have removed the
+    # 0.1-0.3 m outliers of the newest pairs, and this loop checks drift removal, not robustness
+    st = SyntheticStream(F, width=W, height=H, drift=drift, outliers=outliers)
     params = bfa.hash_params(voxel_size=voxel, num_buckets=1 << 16, num_blocks=1 << 15)
     K = st.K
     opts = recon_options(F, recordOps=int(record), cacheWidth=80, cacheHeight=60, cacheIntrinsics=st.cache_intrinsics,
-                         maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2), maxKeyframes=K + 1)
+                         maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2), maxKeyframes=K + 1, asyncBundling=async_ba)
     rc = Recon(params, st.cam, opts)
     st.attach(rc)
     for f in range(F):
         rc.process_frame(f)
+    rc.finish()  # last submap's solves; then let the queue catch up as the render loop would
+    for _ in range(30):
+        rc.reintegrate()
     rc.synchronize()
     return st, params, rc
 
 
-@pytest.fixture(scope="module")
-def loop():
-    return run_loop()
+@pytest.fixture(scope="module", params=[0, 1], ids=["sync", "async"])
+def loop(request):
+    return run_loop(async_ba=request.param)
 
 
 def test_replay_parity_bit_exact(loop):
     st, params, rc = loop
     ops = rc.op_log()
     kinds = [k for k, _, _, _ in ops]
-    assert kinds.count(FIX_DEINTEGRATE) > 0 and kinds.count(OP_GC) == st.F
+    assert kinds.count(FIX_DEINTEGRATE) > 0 and kinds.count(OP_GC) == st.F + 30
     depth = st.depth.download()
     color = st.color.download()
     ora = OracleScene(params)
@@ -76,8 +81,8 @@ def test_queue_invariants(loop):
 def test_loop_corrects_drift(loop):
     st, _, rc = loop
     s = rc.stats()
-    assert s["localSolves"] == st.num_submaps - 1
-    assert s["globalSolves"] >= st.num_submaps - 2
+    assert s["localSolves"] == st.num_submaps
+    assert s["globalSolves"] >= st.num_submaps - 1
     assert s["fixOps"] > 0 and s["deintegrations"] > 0
     # dead reckoning of the front end vs the poses the volume holds now
     dr = [st.gt[0].astype(np.float64)]
@@ -86,5 +91,5 @@ def test_loop_corrects_drift(loop):
     traj = rc.trajectory(st.F)
     err_dr = np.array([np.linalg.norm(dr[f][:3, 3] - st.gt[f][:3, 3]) for f in range(st.F)])
     err_loop = np.array([np.linalg.norm(traj[f][:3, 3] - st.gt[f][:3, 3]) for f in range(st.F)])
-    settled = st.F - 2 * st.S  # the newest submaps are not re-integrated yet
+    settled = st.F
     assert np.mean(err_loop[:settled]) < 0.5 * np.mean(err_dr[:settled]), (err_loop[:settled], err_dr[:settled])

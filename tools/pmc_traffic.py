@@ -1,0 +1,37 @@
+"""Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE),
+corrected as MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE counts 64 B per 128-B request
+on wide streaming reads, so it is doubled; WRITE_SIZE is taken as is. Both counters are in KB.
+Usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv KERNEL_REGEX OUT.json"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def per_dispatch(path, counter, rx):
+    vals = defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter or not rx.search(r.get("Kernel_Name", "")):
+            continue
+        vals[r.get("Dispatch_Id") or r.get("Correlation_Id")] += float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    fetch_csv, write_csv, kernel, out = sys.argv[1:5]
+    rx = re.compile(kernel)
+    f = per_dispatch(fetch_csv, "FETCH_SIZE", rx)
+    w = per_dispatch(write_csv, "WRITE_SIZE", rx)
+    fetch_b = 2.0 * 1024.0 * sum(f) / max(1, len(f))
+    write_b = 1024.0 * sum(w) / max(1, len(w))
+    res = {"kernel": kernel, "dispatches_fetch": len(f), "dispatches_write": len(w),
+           "fetch_bytes_per_launch_corrected": fetch_b, "write_bytes_per_launch": write_b,
+           "k_integrate_bytes_per_launch": fetch_b + write_b,
+           "correction": "FETCH_SIZE x2 (gfx950 half-count on 128-B requests), KB -> bytes"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
