@@ -158,7 +158,9 @@ def main():
     ap.add_argument("--buckets", type=int, default=1 << 23)
     ap.add_argument("--blocks", type=int, default=1 << 21)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=None, help="JSON with per-launch HBM bytes of k_integrate (PMC pass)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_k_integrate_traffic.json"),
+                    help="JSON with per-launch HBM bytes of k_integrate from the PMC passes of "
+                         "tools/profile_bench.sh on this same command (committed under profiles/)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -228,6 +230,7 @@ def main():
     traffic = None
     if args.traffic and os.path.exists(args.traffic):
         traffic = json.load(open(args.traffic)).get("k_integrate_bytes_per_launch")
+        traffic_src = os.path.relpath(args.traffic, REPO)
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
     solo = global_solve_timing(stream, min(K, args.warmup + args.steps))
@@ -254,6 +257,7 @@ def main():
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
         "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src if traffic is not None else None,
                      "launches": st["integrateLaunches"], "avg_launch_us": per_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes},
         "loop": {"ops_per_frame": (st["integrations"] + st["deintegrations"]) / max(1, st["frames"]),

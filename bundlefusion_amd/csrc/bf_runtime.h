@@ -94,6 +94,18 @@ public:
         head_ = (head_ + 1) % RING;
         pending_++;
     }
+    // event pair for hipExtLaunchKernelGGL, which stamps them at the dispatch's own start and
+    // end (no queue gap between a separately recorded start event and the kernel): slot(), launch
+    // with the pair, then commit()
+    void slot(hipEvent_t& a, hipEvent_t& b) {
+        if (pending_ == RING) harvest(head_);
+        a = a_[head_];
+        b = b_[head_];
+    }
+    void commit() {
+        head_ = (head_ + 1) % RING;
+        pending_++;
+    }
     // drains every pending slot (synchronizes on the newest event)
     double totalMs() {
         while (pending_) harvest((head_ + RING - pending_) % RING);

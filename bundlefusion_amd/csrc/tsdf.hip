@@ -15,6 +15,8 @@
 //    integrate kernel, instead of re-reading 512 voxels per block.
 #include "tsdf.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -971,14 +973,16 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     k_compactify<true><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p);
     BF_LAUNCH_CHECK();
     const unsigned igrid = deint ? integrateGrid_[1] : integrateGrid_[0];
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = integrateClock_.enabled();
-    if (timed) integrateClock_.start(stream_);
+    if (timed) integrateClock_.slot(ev0, ev1);
+    const uint32_t* col = reinterpret_cast<const uint32_t*>(color);
     if (deint)
-        k_integrate<true><<<igrid, 256, 0, stream_>>>(A, depth, reinterpret_cast<const uint32_t*>(color), cam, Tinv_);
+        hipExtLaunchKernelGGL(k_integrate<true>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
     else
-        k_integrate<false><<<igrid, 256, 0, stream_>>>(A, depth, reinterpret_cast<const uint32_t*>(color), cam, Tinv_);
+        hipExtLaunchKernelGGL(k_integrate<false>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
     BF_LAUNCH_CHECK();
-    if (timed) integrateClock_.stop(stream_);
+    if (timed) integrateClock_.commit();
 }
 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)
