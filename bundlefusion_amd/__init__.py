@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 from . import abi
-from .abi import (BFDepthCameraParams, BFHashParams, BFSceneOptions, BFSynthScene, BFTsdfStats,
+from .abi import (BFDepthCameraParams, BFHashParams, BFRayCastParams, BFSceneOptions, BFSynthScene, BFTsdfStats,
                   HASH_ENTRY_DTYPE, VOXEL_DTYPE)
 
 __all__ = ["lib", "BFError", "DeviceArray", "SceneRepHashSDF", "hash_params", "depth_camera",
@@ -214,6 +214,20 @@ class SceneRepHashSDF:
                                     vox.ctypes.data_as(C.c_void_p)))
         return hash_, heap, hc.value, vox
 
+    def raycast(self, T, cam: BFDepthCameraParams, rp, want_intervals=False):
+        """CUDARayCastSDF::render from camera->world T; returns host (depth, depth4, normals, colors
+        [, rayMin, rayMax])."""
+        W, H = rp.width, rp.height
+        outs = [DeviceArray((H, W), np.float32), DeviceArray((H, W, 4), np.float32), DeviceArray((H, W, 4), np.float32),
+                DeviceArray((H, W, 4), np.float32)]
+        iv = [DeviceArray((H, W), np.float32), DeviceArray((H, W), np.float32)] if want_intervals else [None, None]
+        check(lib().bf_scene_raycast(self.h, abi.mat(T), C.byref(cam), C.byref(rp), *[o.ptr for o in outs],
+                                     *[(a.ptr if a is not None else None) for a in iv]))
+        res = [o.download() for o in outs]
+        if want_intervals:
+            res += [a.download() for a in iv]
+        return tuple(res)
+
     def export_visible(self) -> np.ndarray:
         cap = self.params.numSDFBlocks
         out = np.empty((cap, 4), np.int32)
@@ -223,6 +237,24 @@ class SceneRepHashSDF:
 
 
 # ---- synthetic stream ----------------------------------------------------------------------
+def raycast_params(width=640, height=480, fx=577.87, fy=577.87, mx=None, my=None, min_depth=0.1, max_depth=4.0,
+                   truncation=0.06, ray_increment_factor=0.8, thres_sample_dist_factor=50.5, thres_dist_factor=50.0,
+                   use_gradients=False) -> BFRayCastParams:
+    """CUDARayCastSDF::parametersFromGlobalAppState (CUDARayCastSDF.h:24-51), zParametersDefault.txt:35-56."""
+    p = BFRayCastParams()
+    p.width, p.height = width, height
+    p.fx, p.fy = fx, fy
+    p.mx = (width - 1) / 2.0 if mx is None else mx
+    p.my = (height - 1) / 2.0 if my is None else my
+    p.minDepth, p.maxDepth = min_depth, max_depth
+    inc = np.float32(ray_increment_factor) * np.float32(truncation)
+    p.rayIncrement = float(inc)
+    p.thresSampleDist = float(np.float32(thres_sample_dist_factor) * inc)
+    p.thresDist = float(np.float32(thres_dist_factor) * inc)
+    p.useGradients = 1 if use_gradients else 0
+    return p
+
+
 def synth_scene(seed=0) -> BFSynthScene:
     s = BFSynthScene()
     check(lib().bf_synth_scene_default(C.c_uint32(seed), C.byref(s)))

@@ -292,6 +292,14 @@ int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* 
     *n = s->scene->exportVisible(reinterpret_cast<int4*>(out4), cap);
     BF_CATCH
 }
+int bf_scene_raycast(bf_scene* s, const float T[16], const BFDepthCameraParams* cam, const BFRayCastParams* rp, float* depth,
+                     float* depth4, float* normals, float* colors, float* rayMin, float* rayMax) {
+    BF_TRY
+    BF_REQUIRE(s && T && cam && rp, BF_ERR_ARG, "null argument");
+    s->scene->raycast(to_mat(T), *cam, *rp, depth, reinterpret_cast<float4*>(depth4), reinterpret_cast<float4*>(normals),
+                      reinterpret_cast<float4*>(colors), rayMin, rayMax);
+    BF_CATCH
+}
 int bf_scene_synchronize(bf_scene* s) {
     BF_TRY
     BF_REQUIRE(s, BF_ERR_ARG, "null scene");

@@ -1,0 +1,336 @@
+// raycast.hip — gfx950 raycaster of the voxel-hash TSDF (replaces CUDARayCastSDF,
+// /root/reference/FriedLiver/Source/DepthSensing/CUDARayCastSDF.cu/.cpp, RayCastSDFUtil.h, and the
+// D3D11 ray-interval splatting of DX11RayIntervalSplatting.cpp + Shaders/RayIntervalSplatting.hlsl).
+//
+//  * Ray-interval splat without a rasteriser: one wave per visible block projects the block's 8
+//    corners (cameraToDepthProj), takes the NDC bounding rectangle and depth range, and updates the
+//    covered pixels with atomicMin / atomicMax on order-preserving integer encodings of the world
+//    depth. Coverage follows the D3D11 pixel-centre rule (left/top edges inclusive); the depth
+//    tests are those of the two passes with depth clipping disabled (min pass: LESS against a
+//    depth buffer cleared to 1, so quads with NDC z >= 1 never write; max pass: GREATER against 0).
+//  * renderKernel / traverseCoarseGridSimpleSampleAll: one thread per pixel marches the splatted
+//    interval in rayIncrement steps with trilinear SDF samples (8 voxel fetches, any zero weight
+//    invalidates the sample), 3 linear-bisection refinements at a + -> - crossing. A per-thread
+//    one-entry block cache skips the hash probe when consecutive fetches hit the same block
+//    (results are unchanged: it caches the lookup, not the voxel).
+//  * computeNormals from the camera-space points (or the SDF gradient when useGradients).
+#include "hash_dev.h"
+#include "tsdf.h"
+
+#include <cstring>
+
+namespace bf {
+
+BFMat4 mat4_inverse(const BFMat4& M);  // api.cpp
+
+namespace {
+
+const float MINF_F = -__builtin_inff();
+
+__device__ __forceinline__ uint32_t enc_f(float f) {  // monotone float -> uint32
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float dec_f(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); }
+
+struct RayArgs {
+    const BFHashEntry* hash;
+    const BFVoxel* voxels;
+    uint32_t numBuckets, numEntries, maxList;
+    float voxelSize;
+};
+
+// cameraToDepthProj (RayCastSDFUtil.h:208-222)
+__device__ __forceinline__ f3 camera_to_depth_proj(const BFRayCastParams& p, f3 pos) {
+    const float px = pos.x * p.fx / pos.z + p.mx;
+    const float py = pos.y * p.fy / pos.z + p.my;
+    f3 r;
+    r.x = (2.0f * px - ((float)p.width - 1.0f)) / ((float)p.width - 1.0f);
+    r.y = (((float)p.height - 1.0f) - 2.0f * py) / ((float)p.height - 1.0f);
+    r.z = (pos.z - p.minDepth) / (p.maxDepth - p.minDepth);
+    return r;
+}
+// depthToCamera with the ray-cast intrinsics (RayCastSDFUtil.h:201-206)
+__device__ __forceinline__ f3 rc_depth_to_camera(const BFRayCastParams& p, uint32_t ux, uint32_t uy, float depth) {
+    const float x = ((float)ux - p.mx) / p.fx;
+    const float y = ((float)uy - p.my) / p.fy;
+    return mk3(depth * x, depth * y, depth);
+}
+
+__device__ __forceinline__ f3 fmin3(f3 a, f3 b) { return mk3(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
+__device__ __forceinline__ f3 fmax3(f3 a, f3 b) { return mk3(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
+
+__global__ void k_splat_clear(uint32_t* smin, uint32_t* smax, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        smin[i] = enc_f(__builtin_inff());
+        smax[i] = enc_f(-__builtin_inff());
+    }
+}
+
+// rayIntervalSplatKernel (CUDARayCastSDF.cu:101-190) for both passes + the raster of its quads
+__global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible, const uint32_t* ctrl, float voxelSize,
+                                               BFDepthCameraParams cam, BFRayCastParams rp, uint32_t* smin, uint32_t* smax) {
+    const uint32_t n = ctrl[C_VISIBLE];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const BFMat4 V = rp.viewMatrix;
+    for (uint32_t b = wave; b < n; b += nwaves) {
+        const int4 e = visible[b];
+        if (!block_in_frustum(cam, V, e.x, e.y, e.z, voxelSize)) continue;  // :107 (isSDFBlockInCameraFrustumApprox)
+        const f3 wv = block_to_world(e.x, e.y, e.z, voxelSize);
+        const float hv = voxelSize / 2.0f;
+        const f3 MINV = mk3(wv.x - hv, wv.y - hv, wv.z - hv);
+        const float ext = (float)BF_SDF_BLOCK_SIZE * voxelSize;
+        const f3 maxv = mk3(MINV.x + ext, MINV.y + ext, MINV.z + ext);
+        const f3 p000 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, MINV.y, MINV.z)));
+        const f3 p100 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, MINV.y, MINV.z)));
+        const f3 p010 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, maxv.y, MINV.z)));
+        const f3 p001 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, MINV.y, maxv.z)));
+        const f3 p110 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, maxv.y, MINV.z)));
+        const f3 p011 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, maxv.y, maxv.z)));
+        const f3 p101 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, MINV.y, maxv.z)));
+        const f3 p111 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, maxv.y, maxv.z)));
+        const f3 mn = fmin3(fmin3(fmin3(p000, p100), fmin3(p010, p001)), fmin3(fmin3(p110, p011), fmin3(p101, p111)));
+        const f3 mx = fmax3(fmax3(fmax3(p000, p100), fmax3(p010, p001)), fmax3(fmax3(p110, p011), fmax3(p101, p111)));
+        // depthProjToCameraZ (RayCastSDFUtil.h:196-199)
+        const float dwMin = mn.z * (rp.maxDepth - rp.minDepth) + rp.minDepth;
+        const float dwMax = mx.z * (rp.maxDepth - rp.minDepth) + rp.minDepth;
+        const bool minOk = mn.z < 1.0f;  // LESS vs depth cleared to 1 (NDC z clamped to [0,1])
+        const bool maxOk = mx.z > 0.0f;  // GREATER vs depth cleared to 0
+        if (!minOk && !maxOk) continue;
+        const float W = (float)rp.width, H = (float)rp.height;
+        const float left = (mn.x + 1.0f) * 0.5f * W, right = (mx.x + 1.0f) * 0.5f * W;
+        const float top = (1.0f - mx.y) * 0.5f * H, bottom = (1.0f - mn.y) * 0.5f * H;
+        if (!(left < right) || !(top < bottom)) continue;  // empty or NaN
+        const float fx0 = ceilf(left - 0.5f), fx1 = ceilf(right - 0.5f) - 1.0f;
+        const float fy0 = ceilf(top - 0.5f), fy1 = ceilf(bottom - 0.5f) - 1.0f;
+        if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) continue;
+        const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
+        const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
+        if (x1 < x0 || y1 < y0) continue;
+        const uint32_t w = (uint32_t)(x1 - x0 + 1), npx = w * (uint32_t)(y1 - y0 + 1);
+        const uint32_t emin = enc_f(dwMin), emax = enc_f(dwMax);
+        for (uint32_t k = lane; k < npx; k += 64) {
+            const uint32_t idx = (uint32_t)(y0 + (int)(k / w)) * rp.width + (uint32_t)(x0 + (int)(k % w));
+            if (minOk) atomicMin(&smin[idx], emin);
+            if (maxOk) atomicMax(&smax[idx], emax);
+        }
+    }
+}
+
+// getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417) with a one-entry per-thread block cache
+struct BlockCache {
+    int bx = INT_MIN, by = 0, bz = 0, ptr = BF_FREE_ENTRY;
+};
+__device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 pos, float& sdf, float& weight, uint32_t& color) {
+    const i3 v = world_to_vvox(pos, R.voxelSize);
+    const i3 b = vvox_to_block(v);
+    if (b.x != c.bx || b.y != c.by || b.z != c.bz) {
+        c.bx = b.x; c.by = b.y; c.bz = b.z;
+        c.ptr = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
+    }
+    if (c.ptr == BF_FREE_ENTRY) {  // deleteVoxel
+        sdf = 0.0f; weight = 0.0f; color = 0u;
+        return;
+    }
+    int lx = v.x % BF_SDF_BLOCK_SIZE, ly = v.y % BF_SDF_BLOCK_SIZE, lz = v.z % BF_SDF_BLOCK_SIZE;
+    if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
+    if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
+    if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
+    const BFVoxel* vp = R.voxels + c.ptr + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+    sdf = vp->sdf;
+    weight = vp->weight;
+    color = *reinterpret_cast<const uint32_t*>(vp->color);
+}
+
+__device__ __forceinline__ float frac1(float v) { return v - floorf(v); }
+
+// trilinearInterpolationSimpleFastFast (RayCastSDFUtil.h:96-116). On a zero-weight corner it returns
+// false with dist holding the partial sum, which gradientForPoint then uses as the reference does.
+__device__ bool trilinear(const RayArgs& R, BlockCache& c, f3 pos, float& dist, uint32_t& rgb) {
+    const float oSet = R.voxelSize;
+    const f3 posDual = pos - mk3(oSet / 2.0f, oSet / 2.0f, oSet / 2.0f);
+    const f3 vv = pos / R.voxelSize;
+    const f3 weight = mk3(frac1(vv.x), frac1(vv.y), frac1(vv.z));
+    dist = 0.0f;
+    f3 colorFloat = mk3(0.0f, 0.0f, 0.0f);
+    const f3 offs[8] = {mk3(0.0f, 0.0f, 0.0f), mk3(oSet, 0.0f, 0.0f), mk3(0.0f, oSet, 0.0f), mk3(0.0f, 0.0f, oSet),
+                        mk3(oSet, oSet, 0.0f), mk3(0.0f, oSet, oSet), mk3(oSet, 0.0f, oSet), mk3(oSet, oSet, oSet)};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        float sdf, w;
+        uint32_t col;
+        get_voxel(R, c, posDual + offs[k], sdf, w, col);
+        if (w == 0.0f) return false;
+        const f3 vColor = mk3((float)(col & 0xFF), (float)((col >> 8) & 0xFF), (float)((col >> 16) & 0xFF));
+        const float a = (k == 1 || k == 4 || k == 6 || k == 7) ? weight.x : 1.0f - weight.x;
+        const float bq = (k == 2 || k == 4 || k == 5 || k == 7) ? weight.y : 1.0f - weight.y;
+        const float cq = (k == 3 || k == 5 || k == 6 || k == 7) ? weight.z : 1.0f - weight.z;
+        const float wt = a * bq * cq;
+        dist += wt * sdf;
+        colorFloat += wt * vColor;
+    }
+    // make_uchar3(float, float, float): float -> unsigned char conversion
+    rgb = (uint32_t)(uint8_t)colorFloat.x | ((uint32_t)(uint8_t)colorFloat.y << 8) | ((uint32_t)(uint8_t)colorFloat.z << 16);
+    return true;
+}
+
+// gradientForPoint (RayCastSDFUtil.h:172-194)
+__device__ f3 gradient_for_point(const RayArgs& R, BlockCache& c, f3 pos) {
+    const float vs = R.voxelSize;
+    const f3 offset = mk3(vs, vs, vs);
+    float dp00, d0p0, d00p, d100, d010, d001;
+    uint32_t col;
+    trilinear(R, c, pos - mk3(0.5f * offset.x, 0.0f, 0.0f), dp00, col);
+    trilinear(R, c, pos - mk3(0.0f, 0.5f * offset.y, 0.0f), d0p0, col);
+    trilinear(R, c, pos - mk3(0.0f, 0.0f, 0.5f * offset.z), d00p, col);
+    trilinear(R, c, pos + mk3(0.5f * offset.x, 0.0f, 0.0f), d100, col);
+    trilinear(R, c, pos + mk3(0.0f, 0.5f * offset.y, 0.0f), d010, col);
+    trilinear(R, c, pos + mk3(0.0f, 0.0f, 0.5f * offset.z), d001, col);
+    const f3 grad = mk3((dp00 - d100) / offset.x, (d0p0 - d010) / offset.y, (d00p - d001) / offset.z);
+    const float l = length3(grad);
+    if (l == 0.0f) return mk3(0.0f, 0.0f, 0.0f);
+    return (-grad) / l;
+}
+
+// renderKernel (CUDARayCastSDF.cu:17-57) + traverseCoarseGridSimpleSampleAll (RayCastSDFUtil.h:224-290)
+__global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
+                                                const uint32_t* __restrict__ smax, float* d_depth, float4* d_depth4,
+                                                float4* d_normals, float4* d_colors, float* outMin, float* outMax) {
+    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= rp.width || y >= rp.height) return;
+    const uint32_t pix = y * rp.width + x;
+    const float MINF = -__builtin_inff();
+    d_depth[pix] = MINF;
+    d_depth4[pix] = make_float4(MINF, MINF, MINF, MINF);
+    d_normals[pix] = make_float4(MINF, MINF, MINF, MINF);
+    d_colors[pix] = make_float4(MINF, MINF, MINF, MINF);
+    const uint32_t emn = smin[pix], emx = smax[pix];
+    // min target cleared to -inf, max target to 0 (DX11RayIntervalSplatting.cpp:174,203)
+    float minInterval = (emn == enc_f(__builtin_inff())) ? MINF : dec_f(emn);
+    float maxInterval = (emx == enc_f(-__builtin_inff())) ? 0.0f : dec_f(emx);
+    if (outMin) outMin[pix] = minInterval;
+    if (outMax) outMax[pix] = maxInterval;
+
+    const f3 camDir = normalize3(rc_depth_to_camera(rp, x, y, 1.0f));
+    const f3 worldCamPos = xform(rp.viewMatrixInverse, mk3(0.0f, 0.0f, 0.0f));
+    const f3 w4 = xform4(rp.viewMatrixInverse, camDir, 0.0f);
+    const f3 worldDir = normalize3(w4);
+    if (minInterval == 0.0f || minInterval == MINF) return;
+    if (maxInterval == 0.0f || maxInterval == MINF) return;
+    minInterval = fmaxf(minInterval, rp.minDepth);
+    maxInterval = fminf(maxInterval, rp.maxDepth);
+
+    BlockCache cache;
+    float lastSdf = 0.0f, lastAlpha = 0.0f;
+    int lastWeight = 0;
+    const float depthToRayLength = 1.0f / camDir.z;
+    float rayCurrent = depthToRayLength * fmaxf(rp.minDepth, minInterval);
+    const float rayEnd = depthToRayLength * fminf(rp.maxDepth, maxInterval);
+    while (rayCurrent < rayEnd) {
+        const f3 cur = worldCamPos + rayCurrent * worldDir;
+        float dist;
+        uint32_t rgb;
+        if (trilinear(R, cache, cur, dist, rgb)) {
+            if (lastWeight > 0 && lastSdf > 0.0f && dist < 0.0f) {
+                // findIntersectionBisection (RayCastSDFUtil.h:130-156), 3 iterations
+                float a = lastAlpha, aDist = lastSdf, b = rayCurrent, bDist = dist, c = 0.0f;
+                uint32_t rgb2 = 0;
+                bool ok = true;
+                for (int it = 0; it < 3; it++) {
+                    c = a + (aDist / (aDist - bDist)) * (b - a);
+                    float cDist;
+                    if (!trilinear(R, cache, worldCamPos + c * worldDir, cDist, rgb2)) { ok = false; break; }
+                    if (aDist * cDist > 0.0f) { a = c; aDist = cDist; }
+                    else { b = c; bDist = cDist; }
+                }
+                const float alpha = c;
+                if (ok && fabsf(lastSdf - dist) < rp.thresSampleDist) {
+                    if (fabsf(dist) < rp.thresDist) {
+                        const float depth = alpha / depthToRayLength;
+                        d_depth[pix] = depth;
+                        const f3 cp = rc_depth_to_camera(rp, x, y, depth);
+                        d_depth4[pix] = make_float4(cp.x, cp.y, cp.z, 1.0f);
+                        d_colors[pix] = make_float4((float)(rgb2 & 0xFF) / 255.f, (float)((rgb2 >> 8) & 0xFF) / 255.f,
+                                                    (float)((rgb2 >> 16) & 0xFF) / 255.f, 1.0f);
+                        if (rp.useGradients) {
+                            const f3 iso = worldCamPos + alpha * worldDir;
+                            const f3 nrm = -gradient_for_point(R, cache, iso);
+                            const f3 n = xform4(rp.viewMatrix, nrm, 0.0f);
+                            d_normals[pix] = make_float4(n.x, n.y, n.z, 1.0f);
+                        }
+                        return;
+                    }
+                }
+            }
+            lastSdf = dist;
+            lastAlpha = rayCurrent;
+            lastWeight = 1;
+            rayCurrent += rp.rayIncrement;
+        } else {
+            lastWeight = 0;
+            rayCurrent += rp.rayIncrement;
+        }
+    }
+}
+
+// computeNormalsDevice (CameraUtil.cu:665-692)
+__global__ void k_normals(float4* out, const float4* in, uint32_t W, uint32_t H) {
+    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const float MINF = -__builtin_inff();
+    float4 o = make_float4(MINF, MINF, MINF, MINF);
+    if (x > 0 && x < W - 1 && y > 0 && y < H - 1) {
+        const float4 CC = in[y * W + x], PC = in[(y + 1) * W + x], CP = in[y * W + x + 1];
+        const float4 MC = in[(y - 1) * W + x], CM = in[y * W + x - 1];
+        if (CC.x != MINF && PC.x != MINF && CP.x != MINF && MC.x != MINF && CM.x != MINF) {
+            const f3 n = cross3(mk3(PC.x, PC.y, PC.z) - mk3(MC.x, MC.y, MC.z), mk3(CP.x, CP.y, CP.z) - mk3(CM.x, CM.y, CM.z));
+            const float l = length3(n);
+            if (l > 0.0f) o = make_float4(n.x / -l, n.y / -l, n.z / -l, 1.0f);
+        }
+    }
+    out[y * W + x] = o;
+}
+
+}  // namespace
+
+void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRayCastParams& rpIn, float* depth, float4* depth4,
+                    float4* normals, float4* colors, float* rayMin, float* rayMax) {
+    BF_REQUIRE(depth && depth4 && normals && colors, BF_ERR_ARG, "raycast outputs");
+    BF_REQUIRE(rpIn.width > 0 && rpIn.height > 0, BF_ERR_ARG, "raycast size");
+    compactify(T, cam);  // setLastRigidTransformAndCompactify (CUDASceneRepHashSDF.h:128-139)
+    BFRayCastParams rp = rpIn;
+    rp.viewMatrixInverse = T;  // CUDARayCastSDF::rayIntervalSplatting sets both from the transform
+    rp.viewMatrix = Tinv_;
+    const size_t P = (size_t)rp.width * rp.height;
+    if (P > splatCap_) {
+        splatMin_.alloc(P);
+        splatMax_.alloc(P);
+        splatCap_ = P;
+    }
+    k_splat_clear<<<std::max(1u, std::min(div_up(P, 256), 2048u)), 256, 0, stream_>>>(splatMin_.p, splatMax_.p, (uint32_t)P);
+    BF_LAUNCH_CHECK();
+    k_splat<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp, splatMin_.p,
+                                                          splatMax_.p);
+    BF_LAUNCH_CHECK();
+    RayArgs R;
+    R.hash = hash_.p;
+    R.voxels = voxels_.p;
+    R.numBuckets = cfg_.hp.hashNumBuckets;
+    R.numEntries = E_;
+    R.maxList = cfg_.hp.hashMaxCollisionLinkedListSize;
+    R.voxelSize = cfg_.hp.virtualVoxelSize;
+    const dim3 g(div_up(rp.width, 16), div_up(rp.height, 16));
+    const bool timed = renderClock_.enabled();
+    if (timed) renderClock_.start(stream_);
+    k_render<<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax);
+    BF_LAUNCH_CHECK();
+    if (timed) renderClock_.stop(stream_);
+    if (!rp.useGradients) {
+        k_normals<<<g, 256, 0, stream_>>>(normals, depth4, rp.width, rp.height);
+        BF_LAUNCH_CHECK();
+    }
+}
+
+}  // namespace bf

@@ -80,6 +80,15 @@ public:
     size_t deviceBytes() const;
     KernelClock& integrateClock() { return integrateClock_; }  // k_integrate launches (bench roofline)
 
+    // CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) after setLastRigidTransformAndCompactify:
+    // frustum compactify for camera T (cam = depth-camera frustum params), ray-interval splat
+    // (min / max target), renderKernel, computeNormals (unless rp.useGradients). Outputs are
+    // device arrays of rp.width * rp.height: depth f32, depth4 / normals / colors float4.
+    // rayMin / rayMax (optional, device f32) receive the splatted intervals.
+    void raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRayCastParams& rp, float* depth, float4* depth4,
+                 float4* normals, float4* colors, float* rayMin, float* rayMax);
+    KernelClock& renderClock() { return renderClock_; }
+
 private:
     void alloc(const float* depth, const BFDepthCameraParams& cam, const uint32_t* bitMask);
     void beginOp();
@@ -110,6 +119,9 @@ private:
     int numCUs_;
     unsigned integrateGrid_[2] = {0, 0};
     KernelClock integrateClock_;
+    KernelClock renderClock_;
+    DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
+    size_t splatCap_ = 0;
 };
 
 }  // namespace bf

@@ -14,6 +14,7 @@
 //  * GC reads a per-block count of voxels with (uint)weight != 0, maintained by the
 //    integrate kernel, instead of re-reading 512 voxels per block.
 #include "tsdf.h"
+#include "hash_dev.h"
 
 #include <hip/hip_ext.h>
 
@@ -93,32 +94,11 @@ __device__ void flush_stats2(unsigned long long* stats, int f0, unsigned long lo
     }
 }
 
-__device__ __forceinline__ void load_entry(const BFHashEntry* h, uint32_t i, int4& a, int4& b) {
-    const int4* p = reinterpret_cast<const int4*>(h + i);
-    a = p[0];
-    b = p[1];
-}
+__device__ __forceinline__ void load_entry(const BFHashEntry* h, uint32_t i, int4& a, int4& b) { hash_load_entry(h, i, a, b); }
 
 // getHashEntryForSDFBlockPos, VoxelUtilHashSDF.h:440-485 -> ptr or FREE
-__device__ int lookup_ptr(const HashArgs& A, int x, int y, int z) {
-    const uint32_t h = hash_bucket(x, y, z, A.numBuckets);
-    const uint32_t hp = h * BF_HASH_BUCKET_SIZE;
-#pragma unroll
-    for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
-        int4 a, b;
-        load_entry(A.hash, hp + j, a, b);
-        if (a.x == x && a.y == y && a.z == z && a.w != BF_FREE_ENTRY) return a.w;
-    }
-    const uint32_t last = hp + BF_HASH_BUCKET_SIZE - 1;
-    uint32_t i = last;
-    for (uint32_t it = 0; it < A.maxList; it++) {
-        int4 a, b;
-        load_entry(A.hash, i, a, b);
-        if (a.x == x && a.y == y && a.z == z && a.w != BF_FREE_ENTRY) return a.w;
-        if (b.x == 0) break;
-        i = (last + (uint32_t)b.x) % A.numEntries;
-    }
-    return BF_FREE_ENTRY;
+__device__ __forceinline__ int lookup_ptr(const HashArgs& A, int x, int y, int z) {
+    return hash_lookup(A.hash, A.numBuckets, A.numEntries, A.maxList, x, y, z);
 }
 
 // Spatial ownership for multi-GPU sharding: the chunk of the block's corner (worldToChunks

@@ -86,6 +86,14 @@ int bf_scene_reset_stats(bf_scene* s);
 int bf_scene_export(bf_scene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
 /* visible list of the last compactify to HOST: int32 {x,y,z,ptr} x n */
 int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n);
+/* CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) preceded by setLastRigidTransformAndCompactify
+ * (CUDASceneRepHashSDF.h:128-139): camera->world T, frustum camera params cam (render depth range),
+ * ray-cast params rp (intrinsics, size, minDepth/maxDepth, rayIncrement, thresholds, useGradients;
+ * the view matrices are derived from T). Device outputs of rp->width*rp->height: depth f32, depth4 /
+ * normals / colors float4 (MINF where no surface); rayMin / rayMax (optional) receive the splatted
+ * ray intervals (rayIntervalSplatCUDA + the D3D11 min/max passes). */
+int bf_scene_raycast(bf_scene* s, const float T[16], const BFDepthCameraParams* cam, const BFRayCastParams* rp, float* depth,
+                     float* depth4, float* normals, float* colors, float* rayMin, float* rayMax);
 int bf_scene_synchronize(bf_scene* s);
 int bf_scene_device_bytes(bf_scene* s, uint64_t* bytes);
 /* time the next operations on the scene's stream */

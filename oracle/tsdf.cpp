@@ -532,3 +532,243 @@ void or_dense_integrate(const float T[16], const float* depth, const uint8_t* co
 }
 
 }  // extern "C"
+
+// ---- raycast: CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) ----------------------------
+namespace {
+
+// cameraToDepthProj (RayCastSDFUtil.h:208-222)
+f3 rcProj(const BFRayCastParams& p, f3 pos) {
+    f3 r;
+    const float px = pos.x * p.fx / pos.z + p.mx, py = pos.y * p.fy / pos.z + p.my;
+    r.x = (2.0f * px - ((float)p.width - 1.0f)) / ((float)p.width - 1.0f);
+    r.y = (((float)p.height - 1.0f) - 2.0f * py) / ((float)p.height - 1.0f);
+    r.z = (pos.z - p.minDepth) / (p.maxDepth - p.minDepth);
+    return r;
+}
+f3 rcDepthToCamera(const BFRayCastParams& p, uint32_t ux, uint32_t uy, float depth) {
+    const float x = ((float)ux - p.mx) / p.fx, y = ((float)uy - p.my) / p.fy;
+    return {depth * x, depth * y, depth};
+}
+f3 fmin3(f3 a, f3 b) { return {std::fmin(a.x, b.x), std::fmin(a.y, b.y), std::fmin(a.z, b.z)}; }
+f3 fmax3(f3 a, f3 b) { return {std::fmax(a.x, b.x), std::fmax(a.y, b.y), std::fmax(a.z, b.z)}; }
+
+struct Quad {  // the 6 vertices of rayIntervalSplatKernel (CUDARayCastSDF.cu:170-180) as a rectangle
+    float minX, maxX, minY, maxY, ndcZ, depthWorld;
+};
+
+// D3D11 raster of one pass: pixel centres inside [left, right) x [top, bottom) (top-left rule for an
+// axis-aligned rectangle), depth test on the NDC z clamped to [0, 1] (depth clip disabled), the pixel
+// shader writes the world depth.
+void rasterPass(const std::vector<Quad>& quads, const BFRayCastParams& p, bool minPass, std::vector<float>& target) {
+    const uint32_t W = p.width, H = p.height;
+    std::vector<float> zbuf((size_t)W * H, minPass ? 1.0f : 0.0f);
+    target.assign((size_t)W * H, minPass ? MINF : 0.0f);
+    for (const Quad& q : quads) {
+        const float Wf = (float)W, Hf = (float)H;
+        const float left = (q.minX + 1.0f) * 0.5f * Wf, right = (q.maxX + 1.0f) * 0.5f * Wf;
+        const float top = (1.0f - q.maxY) * 0.5f * Hf, bottom = (1.0f - q.minY) * 0.5f * Hf;
+        if (!(left < right) || !(top < bottom)) continue;
+        const float z = std::fmin(std::fmax(q.ndcZ, 0.0f), 1.0f);
+        for (uint32_t py = 0; py < H; py++) {
+            const float cy = (float)py + 0.5f;
+            if (!(top <= cy && cy < bottom)) continue;
+            for (uint32_t px = 0; px < W; px++) {
+                const float cx = (float)px + 0.5f;
+                if (!(left <= cx && cx < right)) continue;
+                float& zb = zbuf[(size_t)py * W + px];
+                if (minPass ? (z < zb) : (z > zb)) {
+                    zb = z;
+                    target[(size_t)py * W + px] = q.depthWorld;
+                }
+            }
+        }
+    }
+}
+
+// getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417)
+BFVoxel getVoxelWorld(const Scene& s, f3 pos) {
+    const i3 v = worldToVirtualVoxelPos(s, pos);
+    const BFHashEntry e = getHashEntryForSDFBlockPos(s, virtualVoxelPosToSDFBlock(v));
+    BFVoxel out;
+    if (e.ptr == BF_FREE_ENTRY) {
+        deleteVoxel(out);
+        return out;
+    }
+    int lx = v.x % BF_SDF_BLOCK_SIZE, ly = v.y % BF_SDF_BLOCK_SIZE, lz = v.z % BF_SDF_BLOCK_SIZE;
+    if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
+    if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
+    if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
+    return s.voxels[(size_t)e.ptr + (size_t)(lz * 64 + ly * 8 + lx)];
+}
+
+float frac1(float v) { return v - std::floor(v); }
+
+// trilinearInterpolationSimpleFastFast (RayCastSDFUtil.h:96-116), literal corner order
+bool trilinear(const Scene& s, f3 pos, float& dist, uint8_t rgb[3]) {
+    const float oSet = s.hp.virtualVoxelSize;
+    const f3 posDual = pos - mk(oSet / 2.0f, oSet / 2.0f, oSet / 2.0f);
+    const f3 vv = pos / s.hp.virtualVoxelSize;
+    const f3 w = {frac1(vv.x), frac1(vv.y), frac1(vv.z)};
+    dist = 0.0f;
+    f3 colorFloat = {0.0f, 0.0f, 0.0f};
+    auto tap = [&](f3 off, float fx, float fy, float fz) {
+        const BFVoxel v = getVoxelWorld(s, posDual + off);
+        if (v.weight == 0) return false;
+        const f3 vColor = {(float)v.color[0], (float)v.color[1], (float)v.color[2]};
+        const float wt = fx * fy * fz;
+        dist += wt * v.sdf;
+        colorFloat = colorFloat + wt * vColor;
+        return true;
+    };
+    if (!tap({0.0f, 0.0f, 0.0f}, 1.0f - w.x, 1.0f - w.y, 1.0f - w.z)) return false;
+    if (!tap({oSet, 0.0f, 0.0f}, w.x, 1.0f - w.y, 1.0f - w.z)) return false;
+    if (!tap({0.0f, oSet, 0.0f}, 1.0f - w.x, w.y, 1.0f - w.z)) return false;
+    if (!tap({0.0f, 0.0f, oSet}, 1.0f - w.x, 1.0f - w.y, w.z)) return false;
+    if (!tap({oSet, oSet, 0.0f}, w.x, w.y, 1.0f - w.z)) return false;
+    if (!tap({0.0f, oSet, oSet}, 1.0f - w.x, w.y, w.z)) return false;
+    if (!tap({oSet, 0.0f, oSet}, w.x, 1.0f - w.y, w.z)) return false;
+    if (!tap({oSet, oSet, oSet}, w.x, w.y, w.z)) return false;
+    rgb[0] = (uint8_t)colorFloat.x;
+    rgb[1] = (uint8_t)colorFloat.y;
+    rgb[2] = (uint8_t)colorFloat.z;
+    return true;
+}
+
+f3 gradientForPoint(const Scene& s, f3 pos) {  // RayCastSDFUtil.h:172-194
+    const float vs = s.hp.virtualVoxelSize;
+    const f3 off = {vs, vs, vs};
+    float dp00, d0p0, d00p, d100, d010, d001;
+    uint8_t c[3];
+    trilinear(s, pos - mk(0.5f * off.x, 0.0f, 0.0f), dp00, c);
+    trilinear(s, pos - mk(0.0f, 0.5f * off.y, 0.0f), d0p0, c);
+    trilinear(s, pos - mk(0.0f, 0.0f, 0.5f * off.z), d00p, c);
+    trilinear(s, pos + mk(0.5f * off.x, 0.0f, 0.0f), d100, c);
+    trilinear(s, pos + mk(0.0f, 0.5f * off.y, 0.0f), d010, c);
+    trilinear(s, pos + mk(0.0f, 0.0f, 0.5f * off.z), d001, c);
+    const f3 g = {(dp00 - d100) / off.x, (d0p0 - d010) / off.y, (d00p - d001) / off.z};
+    const float l = length(g);
+    if (l == 0.0f) return {0.0f, 0.0f, 0.0f};
+    return mk(-g.x, -g.y, -g.z) / l;
+}
+
+}  // namespace
+
+extern "C" void or_raycast(const ORScene* o, const BFRayCastParams* rpIn, const BFDepthCameraParams* cam, const float T[16],
+                           float* depth, float* depth4, float* normals, float* colors, float* rayMin, float* rayMax) {
+    Scene& s = const_cast<ORScene*>(o)->s;
+    setTransform(s, T, cam);
+    compactify(s);  // setLastRigidTransformAndCompactify
+    BFRayCastParams p = *rpIn;
+    std::memcpy(p.viewMatrixInverse.m, s.T.e, 64);
+    std::memcpy(p.viewMatrix.m, s.Tinv.e, 64);
+    const m4 V = s.Tinv, Vinv = s.T;
+    const uint32_t W = p.width, H = p.height;
+    // rayIntervalSplatKernel, both passes
+    std::vector<Quad> qmin, qmax;
+    const float vs = s.hp.virtualVoxelSize;
+    for (uint32_t i = 0; i < s.numOccupied; i++) {
+        const BFHashEntry& e = s.compact[i];
+        if (e.ptr == BF_FREE_ENTRY || !blockInFrustum(s, {e.x, e.y, e.z})) continue;
+        const f3 wv = SDFBlockToWorld(s, {e.x, e.y, e.z});
+        const f3 MINV = {wv.x - vs / 2.0f, wv.y - vs / 2.0f, wv.z - vs / 2.0f};
+        const float ext = (float)BF_SDF_BLOCK_SIZE * vs;
+        const f3 maxv = {MINV.x + ext, MINV.y + ext, MINV.z + ext};
+        const f3 p000 = rcProj(p, xform(V, mk(MINV.x, MINV.y, MINV.z)));
+        const f3 p100 = rcProj(p, xform(V, mk(maxv.x, MINV.y, MINV.z)));
+        const f3 p010 = rcProj(p, xform(V, mk(MINV.x, maxv.y, MINV.z)));
+        const f3 p001 = rcProj(p, xform(V, mk(MINV.x, MINV.y, maxv.z)));
+        const f3 p110 = rcProj(p, xform(V, mk(maxv.x, maxv.y, MINV.z)));
+        const f3 p011 = rcProj(p, xform(V, mk(MINV.x, maxv.y, maxv.z)));
+        const f3 p101 = rcProj(p, xform(V, mk(maxv.x, MINV.y, maxv.z)));
+        const f3 p111 = rcProj(p, xform(V, mk(maxv.x, maxv.y, maxv.z)));
+        const f3 mn = fmin3(fmin3(fmin3(p000, p100), fmin3(p010, p001)), fmin3(fmin3(p110, p011), fmin3(p101, p111)));
+        const f3 mx = fmax3(fmax3(fmax3(p000, p100), fmax3(p010, p001)), fmax3(fmax3(p110, p011), fmax3(p101, p111)));
+        qmin.push_back({mn.x, mx.x, mn.y, mx.y, mn.z, mn.z * (p.maxDepth - p.minDepth) + p.minDepth});
+        qmax.push_back({mn.x, mx.x, mn.y, mx.y, mx.z, mx.z * (p.maxDepth - p.minDepth) + p.minDepth});
+    }
+    std::vector<float> tmin, tmax;
+    rasterPass(qmin, p, true, tmin);
+    rasterPass(qmax, p, false, tmax);
+    if (rayMin) std::memcpy(rayMin, tmin.data(), 4 * tmin.size());
+    if (rayMax) std::memcpy(rayMax, tmax.data(), 4 * tmax.size());
+    // renderKernel + traverseCoarseGridSimpleSampleAll
+    std::vector<float> d4((size_t)W * H * 4, MINF);
+    for (uint32_t y = 0; y < H; y++)
+        for (uint32_t x = 0; x < W; x++) {
+            const size_t pix = (size_t)y * W + x;
+            depth[pix] = MINF;
+            for (int k = 0; k < 4; k++) depth4[4 * pix + k] = normals[4 * pix + k] = colors[4 * pix + k] = MINF;
+            const f3 camDir = normalize(rcDepthToCamera(p, x, y, 1.0f));
+            const f3 worldCamPos = xform(Vinv, mk(0.0f, 0.0f, 0.0f));
+            const f3 worldDir = normalize(xform4(Vinv, camDir, 0.0f));
+            float minI = tmin[pix], maxI = tmax[pix];
+            if (minI == 0 || minI == MINF) continue;
+            if (maxI == 0 || maxI == MINF) continue;
+            minI = std::fmax(minI, p.minDepth);
+            maxI = std::fmin(maxI, p.maxDepth);
+            float lastSdf = 0.0f, lastAlpha = 0.0f;
+            int lastWeight = 0;
+            const float d2r = 1.0f / camDir.z;
+            float rayCurrent = d2r * std::fmax(p.minDepth, minI);
+            const float rayEnd = d2r * std::fmin(p.maxDepth, maxI);
+            while (rayCurrent < rayEnd) {
+                const f3 cur = worldCamPos + rayCurrent * worldDir;
+                float dist;
+                uint8_t rgb[3];
+                if (trilinear(s, cur, dist, rgb)) {
+                    if (lastWeight > 0 && lastSdf > 0.0f && dist < 0.0f) {
+                        float a = lastAlpha, aDist = lastSdf, b = rayCurrent, bDist = dist, c = 0.0f;
+                        uint8_t rgb2[3] = {0, 0, 0};
+                        bool ok = true;
+                        for (int it = 0; it < 3; it++) {  // findIntersectionBisection
+                            c = a + (aDist / (aDist - bDist)) * (b - a);
+                            float cDist;
+                            if (!trilinear(s, worldCamPos + c * worldDir, cDist, rgb2)) { ok = false; break; }
+                            if (aDist * cDist > 0.0) { a = c; aDist = cDist; }
+                            else { b = c; bDist = cDist; }
+                        }
+                        const float alpha = c;
+                        if (ok && std::fabs(lastSdf - dist) < p.thresSampleDist && std::fabs(dist) < p.thresDist) {
+                            const float dd = alpha / d2r;
+                            depth[pix] = dd;
+                            const f3 cp = rcDepthToCamera(p, x, y, dd);
+                            depth4[4 * pix] = cp.x; depth4[4 * pix + 1] = cp.y; depth4[4 * pix + 2] = cp.z; depth4[4 * pix + 3] = 1.0f;
+                            colors[4 * pix] = rgb2[0] / 255.f; colors[4 * pix + 1] = rgb2[1] / 255.f;
+                            colors[4 * pix + 2] = rgb2[2] / 255.f; colors[4 * pix + 3] = 1.0f;
+                            if (p.useGradients) {
+                                const f3 g = gradientForPoint(s, worldCamPos + alpha * worldDir);
+                                const f3 n = xform4(V, mk(-g.x, -g.y, -g.z), 0.0f);
+                                normals[4 * pix] = n.x; normals[4 * pix + 1] = n.y; normals[4 * pix + 2] = n.z; normals[4 * pix + 3] = 1.0f;
+                            }
+                            break;
+                        }
+                    }
+                    lastSdf = dist;
+                    lastAlpha = rayCurrent;
+                    lastWeight = 1;
+                    rayCurrent += p.rayIncrement;
+                } else {
+                    lastWeight = 0;
+                    rayCurrent += p.rayIncrement;
+                }
+            }
+        }
+    if (!p.useGradients) {  // computeNormalsDevice (CameraUtil.cu:665-692)
+        for (uint32_t y = 0; y < H; y++)
+            for (uint32_t x = 0; x < W; x++) {
+                float* out = normals + 4 * ((size_t)y * W + x);
+                out[0] = out[1] = out[2] = out[3] = MINF;
+                if (!(x > 0 && x < W - 1 && y > 0 && y < H - 1)) continue;
+                auto at = [&](uint32_t xx, uint32_t yy) {
+                    const float* q = depth4 + 4 * ((size_t)yy * W + xx);
+                    return f3{q[0], q[1], q[2]};
+                };
+                const f3 CC = at(x, y), PC = at(x, y + 1), CP = at(x + 1, y), MC = at(x, y - 1), CM = at(x - 1, y);
+                if (CC.x != MINF && PC.x != MINF && CP.x != MINF && MC.x != MINF && CM.x != MINF) {
+                    const f3 n = cross(PC - MC, CP - CM);
+                    const float l = length(n);
+                    if (l > 0.0f) { out[0] = n.x / -l; out[1] = n.y / -l; out[2] = n.z / -l; out[3] = 1.0f; }
+                }
+            }
+    }
+}

@@ -48,6 +48,8 @@ def lib() -> C.CDLL:
         L.or_matrix_inverse.restype = None
         L.or_dense_integrate.argtypes = [C.c_void_p] * 6 + [C.c_int, C.c_void_p]
         L.or_dense_integrate.restype = None
+        L.or_raycast.argtypes = [C.c_void_p] * 10
+        L.or_raycast.restype = None
         _lib = L
     return _lib
 
@@ -83,6 +85,20 @@ class OracleScene:
 
     def compactify(self, T, cam) -> int:
         return lib().or_scene_compactify(self.h, _m(T).ctypes.data, C.byref(cam))
+
+    def raycast(self, T, cam, rp, want_intervals=False):
+        """CUDARayCastSDF::render restated (oracle/tsdf.cpp or_raycast)."""
+        W, H = rp.width, rp.height
+        depth = np.empty((H, W), np.float32)
+        d4 = np.empty((H, W, 4), np.float32)
+        nrm = np.empty((H, W, 4), np.float32)
+        col = np.empty((H, W, 4), np.float32)
+        rmin = np.empty((H, W), np.float32)
+        rmax = np.empty((H, W), np.float32)
+        lib().or_raycast(self.h, C.addressof(rp), C.addressof(cam), _m(T).ctypes.data, depth.ctypes.data, d4.ctypes.data,
+                         nrm.ctypes.data, col.ctypes.data, rmin.ctypes.data, rmax.ctypes.data)
+        res = (depth, d4, nrm, col)
+        return res + (rmin, rmax) if want_intervals else res
 
     def getHeapFreeCount(self) -> int:
         return lib().or_scene_heap_free_count(self.h)
