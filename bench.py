@@ -12,11 +12,11 @@ Multi-GPU (torchrun, one process per GPU): the TSDF is sharded by 1 m chunk owne
 bundle adjustment is replicated on every rank (deterministic inputs, identical solves), so there
 is no data-path collective. The host-side barrier / max-over-ranks uses gloo.
 
-roofline: the dominant kernel is k_integrate; its launches are timed with HIP events on the scene
-stream inside the timed region; algorithmic bytes per launch = 16 B per block of its work list
-(the band-culled visible list entry) + 24 B per voxel updated inside the truncation band (12 B
-read + 12 B write) + 8 B per pixel (depth + colour read once), from the device counters of the
-same launches.
+roofline: the dominant kernel role is the voxel update pass (k_integrate for new frames and
+integrate-only fixes, k_reintegrate for a fix's fused de-integration + integration); its launches
+are timed with dispatch-stamped HIP events on the scene stream inside the timed region; algorithmic
+bytes per launch = 16 B per work-list block + 24 B per voxel read-modify-written (12 B read + 12 B
+write) + 8 B per pixel (depth + colour read once), from the device counters of the same launches.
 cpu_baseline: the CPU oracle (oracle/, serial C++ restatement) timed on a bounded sample of the
 same workload on this host, scaled by the GPU run's op counts to frames/s.
 """
@@ -158,7 +158,7 @@ def main():
     ap.add_argument("--buckets", type=int, default=1 << 23)
     ap.add_argument("--blocks", type=int, default=1 << 21)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_k_integrate_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_update_pass_traffic.json"),
                     help="JSON with per-launch HBM bytes of k_integrate from the PMC passes of "
                          "tools/profile_bench.sh on this same command (committed under profiles/)")
     args = ap.parse_args()
@@ -222,14 +222,19 @@ def main():
     ss = rc.scene_stats()
     frames = S * args.steps
     P = args.width * args.height
-    launches = max(1, st["integrateLaunches"])
-    alg_bytes = 16 * ss["bandBlocks"] + 24 * ss["voxelsUpdated"] + 8 * P * launches
+    # the voxel-update passes: k_integrate (new frames, integrate-only fixes) and k_reintegrate
+    # (a fix's de-integration + integration fused into one pass); together they are the dominant
+    # kernel role. Algorithmic bytes from the device counters of the same launches.
+    launches = max(1, st["integrateLaunches"] + st["reintegrateLaunches"])
+    kernel_ms = st["integrateKernelMs"] + st["reintegrateKernelMs"]
+    alg_bytes = 16 * ss["bandBlocks"] + 24 * ss["voxelsRMW"] + 8 * P * launches
     per_launch_bytes = alg_bytes / launches
-    per_launch_s = st["integrateKernelMs"] / 1e3 / launches
+    per_launch_s = kernel_ms / 1e3 / launches
     achieved = per_launch_bytes / per_launch_s / 1e9
     traffic = None
     if args.traffic and os.path.exists(args.traffic):
-        traffic = json.load(open(args.traffic)).get("k_integrate_bytes_per_launch")
+        tj = json.load(open(args.traffic))
+        traffic = tj.get("bytes_per_launch", tj.get("k_integrate_bytes_per_launch"))
         traffic_src = os.path.relpath(args.traffic, REPO)
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
@@ -255,21 +260,46 @@ def main():
                    "parallelism": f"tsdf-chunk-shard{world}+ba-replicated" if world > 1 else "single"},
         "ms_per_gn_iter": solo["ms_per_gn_iter"],
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
-        "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_integrate+k_reintegrate (voxel update passes)", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src if traffic is not None else None,
-                     "launches": st["integrateLaunches"], "avg_launch_us": per_launch_s * 1e6,
+                     "launches": launches, "avg_launch_us": per_launch_s * 1e6,
+                     "k_integrate": {"launches": st["integrateLaunches"],
+                                     "avg_us": st["integrateKernelMs"] * 1e3 / max(1, st["integrateLaunches"])},
+                     "k_reintegrate": {"launches": st["reintegrateLaunches"],
+                                       "avg_us": st["reintegrateKernelMs"] * 1e3 / max(1, st["reintegrateLaunches"])},
                      "alg_bytes_per_launch": per_launch_bytes},
         "loop": {"ops_per_frame": (st["integrations"] + st["deintegrations"]) / max(1, st["frames"]),
                  "fix_ops": st["fixOps"], "local_solves": st["localSolves"], "global_solves": st["globalSolves"],
                  "global_gn_iters": st["globalGnIterations"], "global_pcg_iters": st["globalPcgIterations"],
                  "removed_pairs": st["removedPairs"], "global_solve_ms": st["globalSolveMs"],
                  "local_solve_ms": st["localSolveMs"], "integrate_kernel_ms": st["integrateKernelMs"],
+                 "reintegrate_kernel_ms": st["reintegrateKernelMs"],
                  "heap_free": rc.heap_free_count(),
-                 "per_op": {"visible_blocks": ss["visible"] / launches, "band_blocks": ss["bandBlocks"] / launches,
-                            "voxels_updated": ss["voxelsUpdated"] / launches,
-                            "allocated_blocks": ss["scanned"] / launches}},
+                 "per_pass": {"work_list_blocks": ss["bandBlocks"] / launches, "voxels_rmw": ss["voxelsRMW"] / launches,
+                              "voxel_updates": ss["voxelsUpdated"] / launches,
+                              "allocated_blocks_scanned_per_compactify": ss["scanned"] / max(1, ss["integrateOps"])}},
     }
+    # raycast (visualizeFrame's render, reported beside the metric): 20 renders from the last pose
+    W_, H_ = args.width, args.height
+    rpr = bfa.raycast_params(W_, H_, fx=stream.cam.fx, fy=stream.cam.fy)
+    routs = [bfa.DeviceArray((H_, W_), np.float32)] + [bfa.DeviceArray((H_, W_, 4), np.float32) for _ in range(3)]
+    Tlast = stream.gt[S * (args.warmup + args.steps) - 1]
+    rc.render_time()  # enables the render clock
+    rc.raycast_device(Tlast, rpr, routs)
+    rc.synchronize()
+    ms0, n0 = rc.render_time()
+    t_r = time.perf_counter()
+    for _ in range(20):
+        rc.raycast_device(Tlast, rpr, routs)
+    rc.synchronize()
+    t_r = (time.perf_counter() - t_r) / 20
+    ms1, n1 = rc.render_time()
+    rdepth = routs[0].download()
+    out["raycast"] = {"ms_per_render": t_r * 1e3, "k_render_us": (ms1 - ms0) / max(1, n1 - n0) * 1e3,
+                      "valid_fraction": float(np.isfinite(rdepth).mean()),
+                      "note": "compactify + interval splat + renderKernel + computeNormals at 640x480 from the last pose"}
     if rank == 0 and not args.no_cpu_baseline:
         gpu = {"keyframes": int(min(K, (args.warmup + args.steps))),
                "gn_per_solve": st["globalGnIterations"] / max(1, st["globalSolves"]),

@@ -168,6 +168,11 @@ class SceneRepHashSDF:
         check(lib().bf_scene_deintegrate(self.h, abi.mat(T), depth.ptr, color.ptr if color is not None else None,
                                          C.byref(cam), bitmask.ptr if bitmask is not None else None))
 
+    def reintegrate(self, Told, Tnew, depth: DeviceArray, color: DeviceArray | None, cam: BFDepthCameraParams):
+        """deIntegrate(Told) + integrate(Tnew) of one frame as one fused voxel pass."""
+        check(lib().bf_scene_reintegrate(self.h, abi.mat(Told), abi.mat(Tnew), depth.ptr,
+                                         color.ptr if color is not None else None, C.byref(cam)))
+
     def garbageCollect(self):
         check(lib().bf_scene_garbage_collect(self.h))
 

@@ -82,7 +82,7 @@ class BFRayCastParams(C.Structure):
 class BFTsdfStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",
-        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks")]
+        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks", "voxelsRMW")]
 
 
 class BFSceneOptions(C.Structure):
@@ -175,4 +175,5 @@ class BFReconStats(C.Structure):
         "frames", "integrations", "deintegrations", "fixOps", "localSolves", "globalSolves",
         "globalGnIterations", "globalPcgIterations", "localGnIterations", "localPcgIterations",
         "removedPairs", "integrateLaunches")] + [
-        ("integrateKernelMs", C.c_double), ("localSolveMs", C.c_double), ("globalSolveMs", C.c_double)]
+        ("integrateKernelMs", C.c_double), ("localSolveMs", C.c_double), ("globalSolveMs", C.c_double),
+        ("reintegrateLaunches", C.c_uint64), ("reintegrateKernelMs", C.c_double)]

@@ -237,6 +237,13 @@ int bf_scene_deintegrate(bf_scene* s, const float T[16], const float* depth, con
     s->scene->integrate(to_mat(T), depth, color, *cam, true, bitMask);
     BF_CATCH
 }
+int bf_scene_reintegrate(bf_scene* s, const float Told[16], const float Tnew[16], const float* depth, const uint8_t* color,
+                         const BFDepthCameraParams* cam) {
+    BF_TRY
+    BF_REQUIRE(s && Told && Tnew && cam, BF_ERR_ARG, "null argument");
+    s->scene->reintegrate(to_mat(Told), to_mat(Tnew), depth, color, *cam);
+    BF_CATCH
+}
 int bf_scene_garbage_collect(bf_scene* s) {
     BF_TRY
     BF_REQUIRE(s, BF_ERR_ARG, "null scene");
@@ -596,6 +603,24 @@ int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* he
     BF_REQUIRE(r, BF_ERR_ARG, "null recon");
     r->r->synchronize();
     r->r->scene().exportState(hash, heap, heapCounter, voxels);
+    BF_CATCH
+}
+int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, float* depth, float* depth4, float* normals,
+                     float* colors) {
+    BF_TRY
+    BF_REQUIRE(r && T && rp, BF_ERR_ARG, "null argument");
+    r->r->scene().raycast(to_mat(T), r->r->camera(), *rp, depth, reinterpret_cast<float4*>(depth4),
+                          reinterpret_cast<float4*>(normals), reinterpret_cast<float4*>(colors), nullptr, nullptr);
+    BF_CATCH
+}
+int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches) {
+    BF_TRY
+    BF_REQUIRE(r && ms && launches, BF_ERR_ARG, "null argument");
+    r->r->synchronize();
+    auto& clk = r->r->scene().renderClock();
+    if (!clk.enabled()) clk.enable(true);
+    *ms = clk.totalMs();
+    *launches = clk.launches();
     BF_CATCH
 }
 int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n) {

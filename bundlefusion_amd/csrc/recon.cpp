@@ -67,6 +67,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     tm_.reset(new TrajectoryManager(opt_.maxFrames, opt_.topNActive, opt_.minPoseDistSqrt));
     if (opt_.enableTiming) {
         scene_->integrateClock().enable(true);
+        scene_->reintegrateClock().enable(true);
         local_->solveClock().enable(true);
         global_->solveClock().enable(true);
     }
@@ -176,12 +177,17 @@ void Recon::runReintegrate() {
     for (const FixOp& op : ops_) {
         const FrameRef& fr = frames_[op.frame];
         BF_REQUIRE(fr.set, BF_ERR_STATE, "re-integration of a frame that is not in the frame store");
-        if (op.kind == FixKind::DeIntegrate || op.kind == FixKind::ReIntegrate) {
+        if (op.kind == FixKind::ReIntegrate) {  // deIntegrate(old) + integrate(new), one fused voxel pass
+            scene_->reintegrate(op.oldT, op.newT, fr.depth, fr.color, cam_);
+            logOp(1, op.frame, &op.oldT);
+            logOp(2, op.frame, &op.newT);
+            st_.deintegrations++;
+            st_.integrations++;
+        } else if (op.kind == FixKind::DeIntegrate) {
             scene_->integrate(op.oldT, fr.depth, fr.color, cam_, true, nullptr);
             logOp(1, op.frame, &op.oldT);
             st_.deintegrations++;
-        }
-        if (op.kind == FixKind::Integrate || op.kind == FixKind::ReIntegrate) {
+        } else if (op.kind == FixKind::Integrate) {
             scene_->integrate(op.newT, fr.depth, fr.color, cam_, false, nullptr);
             logOp(2, op.frame, &op.newT);
             st_.integrations++;
@@ -397,6 +403,8 @@ BFReconStats Recon::stats() {
     if (opt_.enableTiming) {
         s.integrateKernelMs = scene_->integrateClock().totalMs();
         s.integrateLaunches = scene_->integrateClock().launches();
+        s.reintegrateKernelMs = scene_->reintegrateClock().totalMs();
+        s.reintegrateLaunches = scene_->reintegrateClock().launches();
         s.localSolveMs = local_->solveClock().totalMs();
         s.globalSolveMs = global_->solveClock().totalMs();
     }
@@ -408,6 +416,7 @@ void Recon::resetStats() {
     st_ = BFReconStats{};
     scene_->resetStats();
     scene_->integrateClock().reset();
+    scene_->reintegrateClock().reset();
     local_->solveClock().reset();
     global_->solveClock().reset();
 }

@@ -49,6 +49,7 @@ public:
     void resetStats();
     void trajectory(BFMat4* out, uint32_t n) const;   // integrated transform per frame (-inf if none)
     Scene& scene() { return *scene_; }
+    const BFDepthCameraParams& camera() const { return cam_; }
     const std::vector<BFFixOp>& opLog() const { return log_; }
 
 private:

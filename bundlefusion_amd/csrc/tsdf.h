@@ -13,6 +13,7 @@
 //                                 of the current depth map (conservative cull against per-8x8-tile
 //                                 depth bounds) — the list integrate walks
 //   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op
+//   flags     uint8[B]            fused re-integration: which of the two poses' lists a block is on
 //   ctrl      uint32[16]          device-resident counters (heap counter, visible count, ...)
 //   cand/candSet/candSlot/ovf     alloc scratch (per-op candidate list, global dedup set)
 //   victims                       GC scratch
@@ -56,6 +57,10 @@ public:
     // pointers (float / uchar4 per pixel, W*H of cam). T is camera->world.
     void integrate(const BFMat4& T, const float* depth, const uint8_t* color, const BFDepthCameraParams& cam,
                    bool deint, const uint32_t* bitMask);
+    // re-integration of one frame: de-integrate with Told then integrate with Tnew, fused into one
+    // voxel pass (identical voxel results to the two calls)
+    void reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* depth, const uint8_t* color,
+                     const BFDepthCameraParams& cam);
     void garbageCollect();
     void compactify(const BFMat4& T, const BFDepthCameraParams& cam);
 
@@ -79,6 +84,7 @@ public:
     uint32_t* dCtrlMut() { return ctrl_.p; }
     size_t deviceBytes() const;
     KernelClock& integrateClock() { return integrateClock_; }  // k_integrate launches (bench roofline)
+    KernelClock& reintegrateClock() { return reintegrateClock_; }  // k_reintegrate launches
 
     // CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) after setLastRigidTransformAndCompactify:
     // frustum compactify for camera T (cam = depth-camera frustum params), ray-interval splat
@@ -118,8 +124,12 @@ private:
     uint32_t candSetMask_;
     int numCUs_;
     unsigned integrateGrid_[2] = {0, 0};
+    int integrateZC_ = 8;
     KernelClock integrateClock_;
+    KernelClock reintegrateClock_;
     KernelClock renderClock_;
+    DevBuf<uint8_t> blockFlags_;  // per block: bit 0 on the de-integration list, bit 1 on the integration list
+    unsigned reintegrateGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;
 };

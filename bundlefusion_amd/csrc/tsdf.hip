@@ -19,6 +19,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -67,7 +68,7 @@ struct __attribute__((packed, aligned(4))) Vox3 {
 };
 
 enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS,
-                 S_BAND };
+                 S_BAND, S_RMW };
 constexpr int DEPTH_TILE = 8;  // 8x8-pixel depth-bound tiles for the band cull
 constexpr int STAT_SLOTS = 64;
 
@@ -166,13 +167,14 @@ __global__ void k_begin_op(uint32_t* ctrl, unsigned long long* stats) {
 // maxIntegrationDistance, CUDASceneRepHashSDF.cu:450-457). Empty tiles get (+inf, -inf).
 __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned long long* stats,
                                                         const float* __restrict__ depthImg, uint32_t W, uint32_t H,
-                                                        uint32_t tilesW, uint32_t tilesH, float maxDist, float2* tiles) {
+                                                        uint32_t tilesW, uint32_t tilesH, float maxDist, float2* tiles,
+                                                        uint32_t nops) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
         ctrl[C_BAND] = 0;
         ctrl[C_CAND] = 0;
         ctrl[C_OVF] = 0;
-        stats[S_OPS]++;
+        stats[S_OPS] += nops;
     }
     const uint32_t lane = lane_id();
     const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -508,10 +510,19 @@ __global__ void k_alloc_cleanup(const uint32_t* ctrl, uint32_t candCap, const in
 
 // compactifyHashAllInOneKernel, CUDASceneRepHashSDF.cu:324-366: stream the allocated pool
 // prefix [0, highWater), keep the in-frustum blocks; wave ballot + one atomic per wave.
-template <bool BAND>
+enum CompactMode { CM_FRUSTUM = 0, CM_INTEGRATE = 1, CM_REINT_OLD = 2, CM_REINT_NEW = 3 };
+
+// MODE selects the lists a pass builds:
+//   CM_FRUSTUM    visible (the API's compactify / the raycaster)
+//   CM_INTEGRATE  visible (GC list) + band (integrate's work list); releases the alloc dedup set
+//   CM_REINT_OLD  flags |= 1 and the work list for the de-integration pose of a fused
+//                 re-integration (no visible list: the reference's GC sees the integrate's list)
+//   CM_REINT_NEW  visible + flags |= 2, appending to the work list only blocks not already on it
+template <int MODE>
 __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraParams cam, BFMat4 Tinv, uint32_t candCap,
-                                                    const int* __restrict__ candSlot, unsigned long long* candSet) {
-    if (BAND) {  // release this op's alloc dedup-set slots (was k_alloc_cleanup)
+                                                    const int* __restrict__ candSlot, unsigned long long* candSet,
+                                                    uint8_t* flags) {
+    if (MODE == CM_INTEGRATE || MODE == CM_REINT_NEW) {  // release this op's alloc dedup-set slots
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
             const int sl = candSlot[i];
@@ -529,9 +540,16 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         int4 bp = make_int4(0, 0, 0, 0);
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
-        const bool keep = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
-        const bool inb = BAND && keep && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z);
-        const unsigned long long m0 = __ballot(keep), m1 = __ballot(inb);
+        const bool inFr = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
+        bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z);
+        if (MODE == CM_REINT_OLD && inb) flags[i] = 1;
+        if (MODE == CM_REINT_NEW && inb) {
+            const uint8_t f = flags[i];
+            flags[i] = f | 2;
+            inb = (f & 1) == 0;  // already on the work list from the de-integration pass
+        }
+        const bool keepVis = MODE != CM_REINT_OLD && inFr;
+        const unsigned long long m0 = __ballot(keepVis), m1 = __ballot(inb);
         if (lane == 0) {
             s_cnt[0][wv] = (uint32_t)__popcll(m0);
             s_cnt[1][wv] = (uint32_t)__popcll(m1);
@@ -548,23 +566,73 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
             off1 += s_cnt[1][k];
         }
         const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
-        if (keep) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
+        if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
         if (inb) A.band[off1 + __popcll(m1 & lanemask_lt())] = ent;
         scanned += alloc ? 1 : 0;
-        vis += keep ? 1 : 0;
+        vis += inFr ? 1 : 0;
         band += inb ? 1 : 0;
         __syncthreads();  // s_cnt / s_base reuse
     }
     flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
-    if (BAND) {
+    if (MODE != CM_FRUSTUM) {
         __syncthreads();  // thread 0 of the first flush reads its LDS sums before they are reset
         flush_stats2(A.stats, S_BAND, band, -1, 0);
     }
 }
 
+// Voxel update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:486-514), weightUpdate = 1.
+__device__ __forceinline__ void voxel_integrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
+    const float wUpd = 1.0f;
+    const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
+    const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
+    float r0, r1, r2;
+    if (w0 == 0.0f) { r0 = cu0; r1 = cu1; r2 = cu2; }
+    else { r0 = 0.2f * cu0 + 0.8f * oc0; r1 = 0.2f * cu1 + 0.8f * oc1; r2 = 0.2f * cu2 + 0.8f * oc2; }
+    r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
+    r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
+    r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
+    col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+    s0 = (sdf * wUpd + s0 * w0) / (wUpd + w0);
+    w0 = fminf(weightMax, wUpd + w0);
+}
+__device__ __forceinline__ void voxel_deintegrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c) {
+    const float wUpd = 1.0f;
+    const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
+    const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
+    float r0 = (oc0 * w0 - cu0 * wUpd) / (w0 - wUpd);
+    float r1 = (oc1 * w0 - cu1 * wUpd) / (w0 - wUpd);
+    float r2 = (oc2 * w0 - cu2 * wUpd) / (w0 - wUpd);
+    r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
+    r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
+    r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
+    col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+    s0 = (s0 * w0 - sdf * wUpd) / (w0 - wUpd);
+    w0 = fmaxf(0.0f, w0 - wUpd);
+    if (w0 <= 0.001f) { s0 = 0.0f; col = 0u; w0 = 0.0f; }
+}
+
+// Projection + band test of one voxel for one pose (CUDASceneRepHashSDF.cu:429-466): pixel index
+// (or ~0 when off-screen / no colour) and camera z; the depth gather is issued by the caller.
+__device__ __forceinline__ uint32_t voxel_pixel(const BFDepthCameraParams& cam, const BFMat4& Tinv, int x, int y, int z,
+                                                float voxelSize, bool haveColor, float& pz) {
+    const f3 pf = xform(Tinv, vvox_to_world(x, y, z, voxelSize));
+    const float sx = pf.x * cam.fx / pf.z + cam.mx;
+    const float sy = pf.y * cam.fy / pf.z + cam.my;
+    const uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
+    pz = pf.z;
+    return (ux < cam.imageWidth && uy < cam.imageHeight && haveColor) ? uy * cam.imageWidth + ux : 0xFFFFFFFFu;
+}
+__device__ __forceinline__ bool voxel_in_band(const HashArgs& A, float dz, float pz, float& sdf) {
+    sdf = dz - pz;
+    const float tr = A.truncation + A.truncScale * dz;
+    const bool in = dz != -INFINITY && dz < A.maxIntegrationDistance && fabsf(sdf) < tr;
+    sdf = (sdf >= 0.0f) ? fminf(tr, sdf) : fmaxf(-tr, sdf);
+    return in;
+}
+
 // integrateDepthMapKernel<deIntegrate>, CUDASceneRepHashSDF.cu:420-521. One wave per block:
 // lane = (y, x) of a z-slice, 8 slices. Voxel bytes are touched only inside the band.
-template <bool DEINT>
+template <bool DEINT, int ZC>
 __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __restrict__ depthImg,
                                                    const uint32_t* __restrict__ colorImg, BFDepthCameraParams cam,
                                                    BFMat4 Tinv) {
@@ -579,54 +647,60 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
     for (uint32_t b = wave; b < nvis; b += nwaves) {
         const int4 e = A.band[b];
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
-        // phase 1: project the lane's 8 voxels and issue all depth gathers back to back
-        float depth[BF_SDF_BLOCK_SIZE], pz[BF_SDF_BLOCK_SIZE];
-        uint32_t pix[BF_SDF_BLOCK_SIZE];
+        int dcount = 0;
+        uint32_t nupd = 0;
+        // ZC z-slices per round (8: one round, most ILP; 4: two rounds, fewer VGPRs, more waves)
 #pragma unroll
-        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
+        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
+        // phase 1: project the lane's voxels and issue the depth gathers back to back
+        float depth[ZC], pz[ZC];
+        uint32_t pix[ZC];
+#pragma unroll
+        for (int zi = 0; zi < ZC; zi++) {
+            const int z = z0 + zi;
             const f3 pf = xform(Tinv, vvox_to_world(bx, by, bz + z, A.voxelSize));
             const float sx = pf.x * cam.fx / pf.z + cam.mx;
             const float sy = pf.y * cam.fy / pf.z + cam.my;
             const uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
             const bool on = ux < W && uy < H && colorImg != nullptr;  // colour NULL: no update (:441-448)
-            pix[z] = on ? uy * W + ux : 0xFFFFFFFFu;
-            pz[z] = pf.z;
-            depth[z] = on ? depthImg[pix[z]] : -INFINITY;
+            pix[zi] = on ? uy * W + ux : 0xFFFFFFFFu;
+            pz[zi] = pf.z;
+            depth[zi] = on ? depthImg[pix[zi]] : -INFINITY;
         }
         // phase 2: band test, then issue the in-band voxel and colour loads together
-        float sdfv[BF_SDF_BLOCK_SIZE], osdf[BF_SDF_BLOCK_SIZE], ow[BF_SDF_BLOCK_SIZE];
-        uint32_t oc[BF_SDF_BLOCK_SIZE], cc[BF_SDF_BLOCK_SIZE];
+        float sdfv[ZC], osdf[ZC], ow[ZC];
+        uint32_t oc[ZC], cc[ZC];
         uint32_t band = 0;
 #pragma unroll
-        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
-            const float dz = depth[z];
-            float sdf = dz - pz[z];
+        for (int zi = 0; zi < ZC; zi++) {
+            const int z = z0 + zi;
+            const float dz = depth[zi];
+            float sdf = dz - pz[zi];
             const float tr = A.truncation + A.truncScale * dz;
             const bool in = dz != -INFINITY && dz < A.maxIntegrationDistance && fabsf(sdf) < tr;
             sdf = (sdf >= 0.0f) ? fminf(tr, sdf) : fmaxf(-tr, sdf);
-            sdfv[z] = sdf;
-            osdf[z] = 0.0f; ow[z] = 0.0f; oc[z] = 0u; cc[z] = 0u;
+            sdfv[zi] = sdf;
+            osdf[zi] = 0.0f; ow[zi] = 0.0f; oc[zi] = 0u; cc[zi] = 0u;
             if (in) {
-                band |= 1u << z;
+                band |= 1u << zi;
                 // one 12-B load per voxel (global_load_dwordx3) instead of three dword loads
                 const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane));
-                osdf[z] = __uint_as_float(v.a);
-                ow[z] = __uint_as_float(v.b);
-                oc[z] = v.c;
-                cc[z] = colorImg[pix[z]];
+                osdf[zi] = __uint_as_float(v.a);
+                ow[zi] = __uint_as_float(v.b);
+                oc[zi] = v.c;
+                cc[zi] = colorImg[pix[zi]];
             }
         }
         // phase 3: running average (integrate) or its inverse (de-integrate), store
-        int dcount = 0;
-        uint32_t nupd = 0;
 #pragma unroll
-        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++) {
-            if (!(band & (1u << z))) continue;
-            const uint32_t c = cc[z];
+        for (int zi = 0; zi < ZC; zi++) {
+            const int z = z0 + zi;
+            if (!(band & (1u << zi))) continue;
+            const uint32_t c = cc[zi];
             const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
-            const uint32_t o = oc[z];
+            const uint32_t o = oc[zi];
             const float oc0 = (float)(o & 0xFF), oc1 = (float)((o >> 8) & 0xFF), oc2 = (float)((o >> 16) & 0xFF);
-            const float w0 = ow[z], s0 = osdf[z], sdf = sdfv[z];
+            const float w0 = ow[zi], s0 = osdf[zi], sdf = sdfv[zi];
             float r0, r1, r2, nsdf, nw;
             uint32_t ncol;
             if (!DEINT) {
@@ -659,6 +733,7 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
             dcount += (int)(nw >= 1.0f) - (int)(w0 >= 1.0f);
             nupd++;
         }
+        }  // z0
         const unsigned long long anyChange = __ballot(dcount != 0);
         if (anyChange) {
             for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
@@ -666,7 +741,94 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
         }
         updated += nupd;
     }
-    flush_stats2(A.stats, S_VOXELS, updated, -1, 0);
+    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, updated);
+}
+
+// Fused re-integration of one frame (DepthSensing.cpp:893-894: deIntegrate(old) then integrate(new)):
+// one pass over the union of both work lists; per voxel the de-integration with the old pose and
+// the integration with the new pose are applied in that order in registers, so each voxel is read
+// and written once instead of twice. Per-voxel arithmetic, order and outcome are those of the two
+// separate passes (the hash is not modified between them: alloc(new) runs first and de-integration
+// never allocates; the old pose's list is built before that alloc).
+template <int ZC>
+__global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __restrict__ depthImg,
+                                                     const uint32_t* __restrict__ colorImg, BFDepthCameraParams cam,
+                                                     BFMat4 TinvOld, BFMat4 TinvNew, uint8_t* flags) {
+    const uint32_t nlist = A.ctrl[C_BAND];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int lx = lane & 7, ly = lane >> 3;
+    const bool haveColor = colorImg != nullptr;
+    unsigned long long updated = 0, rmw = 0;
+    for (uint32_t b = wave; b < nlist; b += nwaves) {
+        const int4 e = A.band[b];
+        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
+        const uint8_t f = flags[blk];
+        const bool doOld = (f & 1) != 0, doNew = (f & 2) != 0;
+        const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
+        int dcount = 0;
+        uint32_t nupd = 0, nrmw = 0;
+#pragma unroll
+        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
+            float dO[ZC], dN[ZC], pzO[ZC], pzN[ZC];
+            uint32_t pixO[ZC], pixN[ZC];
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) {
+                const int z = bz + z0 + zi;
+                pixO[zi] = doOld ? voxel_pixel(cam, TinvOld, bx, by, z, A.voxelSize, haveColor, pzO[zi]) : 0xFFFFFFFFu;
+                pixN[zi] = doNew ? voxel_pixel(cam, TinvNew, bx, by, z, A.voxelSize, haveColor, pzN[zi]) : 0xFFFFFFFFu;
+                dO[zi] = pixO[zi] != 0xFFFFFFFFu ? depthImg[pixO[zi]] : -INFINITY;
+                dN[zi] = pixN[zi] != 0xFFFFFFFFu ? depthImg[pixN[zi]] : -INFINITY;
+            }
+            float sO[ZC], sN[ZC], vs[ZC], vw[ZC];
+            uint32_t vc[ZC], cO[ZC], cN[ZC];
+            uint32_t inO = 0, inN = 0;
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) {
+                const int z = z0 + zi;
+                if (doOld && voxel_in_band(A, dO[zi], pzO[zi], sO[zi])) inO |= 1u << zi;
+                if (doNew && voxel_in_band(A, dN[zi], pzN[zi], sN[zi])) inN |= 1u << zi;
+                vs[zi] = 0.0f; vw[zi] = 0.0f; vc[zi] = 0u; cO[zi] = 0u; cN[zi] = 0u;
+                if ((inO | inN) & (1u << zi)) {
+                    const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane));
+                    vs[zi] = __uint_as_float(v.a);
+                    vw[zi] = __uint_as_float(v.b);
+                    vc[zi] = v.c;
+                }
+                if (inO & (1u << zi)) cO[zi] = colorImg[pixO[zi]];
+                if (inN & (1u << zi)) cN[zi] = colorImg[pixN[zi]];
+            }
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) {
+                const int z = z0 + zi;
+                const bool o = (inO >> zi) & 1, n = (inN >> zi) & 1;
+                if (!o && !n) continue;
+                float s0 = vs[zi], w = vw[zi];
+                uint32_t col = vc[zi];
+                const float wStart = w;
+                if (o) voxel_deintegrate(s0, w, col, sO[zi], cO[zi]);
+                if (n) voxel_integrate(s0, w, col, sN[zi], cN[zi], A.weightMax);
+                Vox3 nv;
+                nv.a = __float_as_uint(s0);
+                nv.b = __float_as_uint(w);
+                nv.c = col;
+                *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane)) = nv;
+                dcount += (int)(w >= 1.0f) - (int)(wStart >= 1.0f);
+                nupd += (uint32_t)o + (uint32_t)n;
+                nrmw++;
+            }
+        }
+        const unsigned long long anyChange = __ballot(dcount != 0);
+        if (anyChange) {
+            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
+            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
+        }
+        if (lane == 0) flags[blk] = 0;  // every lane read the flags before the first round
+        updated += nupd;
+        rmw += nrmw;
+    }
+    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
 }
 
 // garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
@@ -853,6 +1015,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     blockPos_.alloc(B_);
     visible_.alloc(B_);
     band_.alloc(B_);
+    blockFlags_.alloc(B_);
     ctrl_.alloc(C_COUNT);
     stats_.alloc(STAT_SLOTS * 16);
     cand_.alloc(cfg_.candCapacity);
@@ -870,11 +1033,26 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     // k_integrate walks its block list with a static grid stride: size the grid to exactly the
     // resident workgroups, so every wave gets the same share in one round (no tail round)
     int occ0 = 0, occ1 = 0;
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false>, 256, 0));
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true>, 256, 0));
+    const char* zcEnv = std::getenv("BF_INTEGRATE_ZC");  // tuning knob: z-slices per round (8 or 4)
+    integrateZC_ = zcEnv ? std::atoi(zcEnv) : 4;
+    if (integrateZC_ != 2 && integrateZC_ != 8) integrateZC_ = 4;
+    if (integrateZC_ == 2) {
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 2>, 256, 0));
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 2>, 256, 0));
+    } else if (integrateZC_ == 4) {
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
+    } else {
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 8>, 256, 0));
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 8>, 256, 0));
+    }
+    int occR = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occR, k_reintegrate<4>, 256, 0));
+    reintegrateGrid_ = (unsigned)std::max(1, occR) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(blockFlags_.p, 0, blockFlags_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
     float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     std::memcpy(T_.m, I, 64);
@@ -886,6 +1064,7 @@ Scene::~Scene() {}
 
 size_t Scene::deviceBytes() const {
     return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
+           blockFlags_.bytes() +
            tiles_.bytes() + ctrl_.bytes() +
            stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
            gcList_.bytes() + blockCount_.bytes();
@@ -899,6 +1078,7 @@ void Scene::reset() {
     k_reset_heap<<<grid, 256, 0, stream_>>>(heap_.p, blockPos_.p, blockCount_.p, B_, ctrl_.p);
     BF_LAUNCH_CHECK();
     BF_HIP(hipMemsetAsync(voxels_.p, 0, voxels_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(blockFlags_.p, 0, blockFlags_.bytes(), stream_));
     cfg_.hp.numOccupiedBlocks = 0;
 }
 
@@ -925,7 +1105,7 @@ void Scene::compactify(const BFMat4& T, const BFDepthCameraParams& cam) {
     Tinv_ = mat4_inverse(T);
     beginOp();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_compactify<false><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr);
+    k_compactify<CM_FRUSTUM><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr, nullptr);
     BF_LAUNCH_CHECK();
 }
 
@@ -941,7 +1121,7 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
         tilesCap_ = tw * th;
     }
     k_begin_op_tiles<<<div_up((size_t)tw * th * 64, 256), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p);
+        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p, 1u);
     BF_LAUNCH_CHECK();
     if (!deint) alloc(depth, cam, bitMask);
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
@@ -950,19 +1130,69 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     A.tilesW = tw;
     A.tilesH = th;
     const unsigned grid = (unsigned)numCUs_ * 4;
-    k_compactify<true><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p);
+    k_compactify<CM_INTEGRATE><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p, nullptr);
     BF_LAUNCH_CHECK();
     const unsigned igrid = deint ? integrateGrid_[1] : integrateGrid_[0];
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = integrateClock_.enabled();
     if (timed) integrateClock_.slot(ev0, ev1);
     const uint32_t* col = reinterpret_cast<const uint32_t*>(color);
-    if (deint)
-        hipExtLaunchKernelGGL(k_integrate<true>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-    else
-        hipExtLaunchKernelGGL(k_integrate<false>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+    if (integrateZC_ == 2) {
+        if (deint)
+            hipExtLaunchKernelGGL(k_integrate<true, 2>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+        else
+            hipExtLaunchKernelGGL(k_integrate<false, 2>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+    } else if (integrateZC_ == 4) {
+        if (deint)
+            hipExtLaunchKernelGGL(k_integrate<true, 4>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+        else
+            hipExtLaunchKernelGGL(k_integrate<false, 4>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+    } else {
+        if (deint)
+            hipExtLaunchKernelGGL(k_integrate<true, 8>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+        else
+            hipExtLaunchKernelGGL(k_integrate<false, 8>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+    }
     BF_LAUNCH_CHECK();
     if (timed) integrateClock_.commit();
+}
+
+// reintegrate() fix of one frame (DepthSensing.cpp:890-895): deIntegrate(Told) + integrate(Tnew)
+// as one fused voxel pass (k_reintegrate). Lists: the de-integration pose's band list is built
+// before alloc(new), as the reference's deIntegrate compactifies before integrate allocates.
+void Scene::reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* depth, const uint8_t* color,
+                        const BFDepthCameraParams& cam) {
+    BF_REQUIRE(depth != nullptr, BF_ERR_ARG, "depth is null");
+    const BFMat4 TinvOld = mat4_inverse(Told);
+    const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
+    if (tw * th > tilesCap_) {
+        tiles_.alloc((size_t)tw * th);
+        tilesCap_ = tw * th;
+    }
+    k_begin_op_tiles<<<div_up((size_t)tw * th * 64, 256), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p, 2u);
+    BF_LAUNCH_CHECK();
+    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
+    A.band = band_.p;
+    A.tiles = tiles_.p;
+    A.tilesW = tw;
+    A.tilesH = th;
+    const unsigned grid = (unsigned)numCUs_ * 4;
+    k_compactify<CM_REINT_OLD><<<grid, 256, 0, stream_>>>(A, cam, TinvOld, 0u, nullptr, nullptr, blockFlags_.p);
+    BF_LAUNCH_CHECK();
+    T_ = Tnew;
+    Tinv_ = mat4_inverse(Tnew);
+    alloc(depth, cam, nullptr);
+    k_compactify<CM_REINT_NEW><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p,
+                                                           blockFlags_.p);
+    BF_LAUNCH_CHECK();
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    const bool timed = reintegrateClock_.enabled();
+    if (timed) reintegrateClock_.slot(ev0, ev1);
+    hipExtLaunchKernelGGL(k_reintegrate<4>, dim3(reintegrateGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, depth,
+                          reinterpret_cast<const uint32_t*>(color), cam, TinvOld, Tinv_, blockFlags_.p);
+    BF_LAUNCH_CHECK();
+    if (timed) reintegrateClock_.commit();
 }
 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)
@@ -1008,7 +1238,7 @@ BFTsdfStats Scene::stats() {
     for (int sl = 0; sl < STAT_SLOTS; sl++)
         for (int f = 0; f < 16; f++) sum[f] += h[sl * 16 + f];
     BFTsdfStats s;
-    static_assert(sizeof(BFTsdfStats) == 11 * 8, "stats layout");
+    static_assert(sizeof(BFTsdfStats) == 12 * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
     return s;
 }

@@ -147,6 +147,16 @@ class Recon:
         check(lib().bf_recon_trajectory(self.h, T.ctypes.data_as(C.c_void_p), C.c_uint32(n)))
         return T
 
+    def raycast_device(self, T, rp, outs):
+        """render into preallocated DeviceArrays (depth, depth4, normals, colors)"""
+        check(lib().bf_recon_raycast(self.h, _mat(T), C.byref(rp), *[o.ptr for o in outs]))
+
+    def render_time(self):
+        ms = C.c_double()
+        n = C.c_uint64()
+        check(lib().bf_recon_render_time(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     def export(self):
         """(hash entries, heap, heapCounter, voxels) of the loop's scene, as SceneRepHashSDF.export."""
         from .abi import HASH_ENTRY_DTYPE, VOXEL_DTYPE

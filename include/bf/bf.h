@@ -70,6 +70,11 @@ int bf_scene_deintegrate(bf_scene* s, const float T[16], const float* depth, con
                          const BFDepthCameraParams* cam, const uint32_t* bitMask);
 /* garbageCollect (CUDASceneRepHashSDF.h:110-126 -> garbageCollectIdentifyCUDA,
  * resetHashBucketMutexCUDA, garbageCollectFreeCUDA, CUDASceneRepHashSDF.cu:113,633,671) */
+/* One re-integration fix (DepthSensing.cpp:890-895): bf_scene_deintegrate(Told) followed by
+ * bf_scene_integrate(Tnew) of the same frame, fused into one voxel pass; the resulting scene is
+ * identical to the two calls. */
+int bf_scene_reintegrate(bf_scene* s, const float Told[16], const float Tnew[16], const float* depth, const uint8_t* color,
+                         const BFDepthCameraParams* cam);
 int bf_scene_garbage_collect(bf_scene* s);
 /* setLastRigidTransformAndCompactify (CUDASceneRepHashSDF.h:136-139); nVisible may be NULL
  * (otherwise this call synchronizes to read it back) */
@@ -221,6 +226,8 @@ typedef struct BFReconStats {
     uint64_t integrateLaunches;  /* timed k_integrate launches */
     double integrateKernelMs;    /* summed device time of those launches */
     double localSolveMs, globalSolveMs;  /* summed device time of the solves */
+    uint64_t reintegrateLaunches;  /* timed k_reintegrate launches (fused de-/re-integration) */
+    double reintegrateKernelMs;
 } BFReconStats;
 
 typedef struct bf_recon bf_recon;
@@ -249,6 +256,12 @@ int bf_recon_reset_stats(bf_recon* r);  /* zero loop + scene counters and the de
 int bf_recon_heap_free_count(bf_recon* r, uint32_t* count);
 /* integrated camera->world transform per frame (HOST float[16*n], -inf rows when not integrated) */
 int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n);
+/* visualizeFrame's render (DepthSensing.cpp:790-793): bf_scene_raycast on the loop's scene with its
+ * depth camera; device outputs as bf_scene_raycast */
+int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, float* depth, float* depth4, float* normals,
+                     float* colors);
+/* summed device time / count of the renderKernel launches since the first call (enables the clock) */
+int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches);
 /* debugHash-style dump of the loop's scene (same layout as bf_scene_export) */
 int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
 /* with recordOps: the scene calls issued so far, in order (kind 1 de-integrate with oldT,

@@ -139,7 +139,9 @@ typedef struct BFTsdfStats {
     uint64_t gcFreed;         /* blocks freed by GC */
     uint64_t allocOverflow;   /* candidates dropped: candidate buffer / heap exhausted */
     uint64_t integrateOps;    /* integrate + de-integrate calls */
-    uint64_t bandBlocks;      /* visible blocks that passed the truncation-band cull (integrate's list) */
+    uint64_t bandBlocks;      /* blocks on the voxel-update work lists (band-culled) */
+    uint64_t voxelsRMW;       /* voxels read-modify-written by the update passes (a fused re-integration
+                                 applies two updates to a voxel in one read + write) */
 } BFTsdfStats;
 
 #ifdef __cplusplus

@@ -153,3 +153,29 @@ def test_full_resolution_frame(scene):
         pair.integrate(k, T, d, c)
     pair.gc()
     assert pair.compare() > 10000
+
+
+@pytest.mark.parametrize("shift", [0.0, 0.004, 0.03, 0.15])
+def test_fused_reintegrate_parity(scene, shift):
+    """Scene::reintegrate (one fused voxel pass) == deIntegrate(old) + integrate(new) in the oracle,
+    for pose changes from none (identical lists) to 15 cm (largely disjoint lists, new blocks)."""
+    cam = small_cam()
+    p = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 17, num_blocks=1 << 16)
+    pair = Pair(p, cam)
+    frames = render_frames(scene, cam, [0, 5, 10, 15])
+    for k, (T, d, c) in enumerate(frames):
+        pair.integrate(k, T, d, c)
+    pair.gc()
+    rng = np.random.default_rng(7)
+    for k in (1, 2):
+        T, d, c = frames[k]
+        T2 = T.copy()
+        T2[:3, 3] += rng.normal(size=3) * shift
+        dd, cc = pair._upload(k, d, c)
+        pair.gpu.reintegrate(T, T2, dd, cc, cam)
+        pair.ora.integrate(T, d, c, cam, deintegrate=True)
+        pair.ora.integrate(T2, d, c, cam)
+        pair.compare()
+        pair.gc()
+        pair.compare()
+    assert pair.gpu.errorFlags() == 0

@@ -27,7 +27,7 @@ def main():
     write_b = 1024.0 * sum(w) / max(1, len(w))
     res = {"kernel": kernel, "dispatches_fetch": len(f), "dispatches_write": len(w),
            "fetch_bytes_per_launch_corrected": fetch_b, "write_bytes_per_launch": write_b,
-           "k_integrate_bytes_per_launch": fetch_b + write_b,
+           "bytes_per_launch": fetch_b + write_b,
            "correction": "FETCH_SIZE x2 (gfx950 half-count on 128-B requests), KB -> bytes"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
