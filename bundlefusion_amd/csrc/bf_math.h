@@ -40,10 +40,18 @@ BF_HD int sgn(float v) { return (0.0f < v) - (v < 0.0f); }
 // float -> int with CUDA cvt.rzi.s32.f32 semantics (truncate, saturate, NaN -> 0): the
 // conversion make_int3(float3) (cutil_math.h:179) performs in the reference kernels.
 BF_HD int f2i(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // v_cvt_i32_f32 truncates, saturates out-of-range values and maps NaN to 0: exactly the
+    // semantics above, in one instruction (inline asm: the C++ cast would be UB out of range)
+    int r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+#else
     if (v != v) return 0;
     if (v >= 2147483648.0f) return INT_MAX;
     if (v <= -2147483648.0f) return INT_MIN;
     return (int)v;
+#endif
 }
 
 struct m4 { float e[16]; };  // row-major, cuda_SimpleMatrixUtil.h:855-875

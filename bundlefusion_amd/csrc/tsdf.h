@@ -13,7 +13,7 @@
 //                                 of the current depth map (conservative cull against per-8x8-tile
 //                                 depth bounds) — the list integrate walks
 //   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op
-//   flags     uint8[B]            fused re-integration: which of the two poses' lists a block is on
+//   flags     uint8[B]            fused re-integration: per work-list entry, which pose(s) update it
 //   ctrl      uint32[16]          device-resident counters (heap counter, visible count, ...)
 //   cand/candSet/candSlot/ovf     alloc scratch (per-op candidate list, global dedup set)
 //   victims                       GC scratch
@@ -128,7 +128,7 @@ private:
     KernelClock integrateClock_;
     KernelClock reintegrateClock_;
     KernelClock renderClock_;
-    DevBuf<uint8_t> blockFlags_;  // per block: bit 0 on the de-integration list, bit 1 on the integration list
+    DevBuf<uint8_t> blockFlags_;  // per work-list entry of a fused re-integration: bit 0 de-integrate, bit 1 integrate
     unsigned reintegrateGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;

@@ -278,12 +278,13 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
         if (bp.z - rayMin.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
     }
 
-    // phase 1: walk the ray's blocks and collect the tile's distinct in-frustum owned blocks in
-    // the LDS set (compute only; no global memory on the DDA's critical path)
+    // phase 1: walk the ray's blocks and collect the tile's distinct blocks in the LDS set (compute
+    // only, no global memory on the DDA's critical path). The per-block tests (frustum, ownership,
+    // streaming mask) depend only on the block, so they run once per distinct block in phase 2
+    // instead of once per DDA step: same emitted set, far fewer projections.
     unsigned long long emitted = 0;
     for (uint32_t iter = 0; iter < 1024 && active; iter++) {
-        if (block_in_frustum(cam, Tinv, id.x, id.y, id.z, A.voxelSize) && owned(A, id.x, id.y, id.z) &&
-            !streamed_out(A, id.x, id.y, id.z)) {
+        {
             const unsigned long long key = block_key(id.x, id.y, id.z);
             uint32_t h = mix_hash(key) & (LDS_SET - 1);
             bool placed = false;
@@ -292,9 +293,10 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
                 if (old == EMPTY_KEY || old == key) { placed = true; break; }
                 h = (h + 1) & (LDS_SET - 1);
             }
-            // congested tile set (rare): look the block up right here and emit it if absent
+            // congested tile set (rare): test and look the block up right here, emit it if absent
             // (duplicates are removed by the global dedup in k_alloc_insert)
-            if (!placed && lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY) {
+            if (!placed && block_in_frustum(cam, Tinv, id.x, id.y, id.z, A.voxelSize) && owned(A, id.x, id.y, id.z) &&
+                !streamed_out(A, id.x, id.y, id.z) && lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY) {
                 const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
                 if (k < candCap) cand[k] = key;
                 else atomicOr(&A.ctrl[C_ERR], 1u);
@@ -324,7 +326,8 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
         bool want = false;
         if (key != EMPTY_KEY) {
             const i3 b = key_block(key);
-            want = lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY;
+            want = block_in_frustum(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
+                   !streamed_out(A, b.x, b.y, b.z) && lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY;
         }
         const unsigned long long m = __ballot(want);
         if (want) {
@@ -510,19 +513,22 @@ __global__ void k_alloc_cleanup(const uint32_t* ctrl, uint32_t candCap, const in
 
 // compactifyHashAllInOneKernel, CUDASceneRepHashSDF.cu:324-366: stream the allocated pool
 // prefix [0, highWater), keep the in-frustum blocks; wave ballot + one atomic per wave.
-enum CompactMode { CM_FRUSTUM = 0, CM_INTEGRATE = 1, CM_REINT_OLD = 2, CM_REINT_NEW = 3 };
+enum CompactMode { CM_FRUSTUM = 0, CM_INTEGRATE = 1, CM_REINT = 2 };
 
 // MODE selects the lists a pass builds:
 //   CM_FRUSTUM    visible (the API's compactify / the raycaster)
 //   CM_INTEGRATE  visible (GC list) + band (integrate's work list); releases the alloc dedup set
-//   CM_REINT_OLD  flags |= 1 and the work list for the de-integration pose of a fused
-//                 re-integration (no visible list: the reference's GC sees the integrate's list)
-//   CM_REINT_NEW  visible + flags |= 2, appending to the work list only blocks not already on it
+//   CM_REINT      fused re-integration, after alloc(new): visible for the new pose (GC list) and
+//                 one work list of the blocks on either pose's band list, with per-entry flags
+//                 (bit 0: de-integrate with TinvOld, bit 1: integrate with Tinv). Blocks alloc(new)
+//                 just created may land on the de-integration side; their voxels are zero and a
+//                 de-integration leaves a zero voxel zero, so the result equals the reference's
+//                 deIntegrate-before-alloc order.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraParams cam, BFMat4 Tinv, uint32_t candCap,
                                                     const int* __restrict__ candSlot, unsigned long long* candSet,
-                                                    uint8_t* flags) {
-    if (MODE == CM_INTEGRATE || MODE == CM_REINT_NEW) {  // release this op's alloc dedup-set slots
+                                                    uint8_t* listFlags, BFMat4 TinvOld) {
+    if (MODE == CM_INTEGRATE || MODE == CM_REINT) {  // release this op's alloc dedup-set slots
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
             const int sl = candSlot[i];
@@ -542,13 +548,14 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         const bool alloc = bp.w != 0;
         const bool inFr = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
         bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z);
-        if (MODE == CM_REINT_OLD && inb) flags[i] = 1;
-        if (MODE == CM_REINT_NEW && inb) {
-            const uint8_t f = flags[i];
-            flags[i] = f | 2;
-            inb = (f & 1) == 0;  // already on the work list from the de-integration pass
+        uint8_t fl = 0;
+        if (MODE == CM_REINT) {
+            const bool inOld = alloc && block_in_frustum(cam, TinvOld, bp.x, bp.y, bp.z, A.voxelSize) &&
+                               block_may_update(A, cam, TinvOld, bp.x, bp.y, bp.z);
+            fl = (uint8_t)((inOld ? 1 : 0) | (inb ? 2 : 0));
+            inb = fl != 0;
         }
-        const bool keepVis = MODE != CM_REINT_OLD && inFr;
+        const bool keepVis = inFr;
         const unsigned long long m0 = __ballot(keepVis), m1 = __ballot(inb);
         if (lane == 0) {
             s_cnt[0][wv] = (uint32_t)__popcll(m0);
@@ -567,7 +574,11 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         }
         const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
         if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
-        if (inb) A.band[off1 + __popcll(m1 & lanemask_lt())] = ent;
+        if (inb) {
+            const uint32_t k = off1 + __popcll(m1 & lanemask_lt());
+            A.band[k] = ent;
+            if (MODE == CM_REINT) listFlags[k] = fl;
+        }
         scanned += alloc ? 1 : 0;
         vis += inFr ? 1 : 0;
         band += inb ? 1 : 0;
@@ -764,7 +775,7 @@ __global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __
     for (uint32_t b = wave; b < nlist; b += nwaves) {
         const int4 e = A.band[b];
         const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
-        const uint8_t f = flags[blk];
+        const uint8_t f = flags[b];
         const bool doOld = (f & 1) != 0, doNew = (f & 2) != 0;
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         int dcount = 0;
@@ -824,7 +835,6 @@ __global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __
             for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
             if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
         }
-        if (lane == 0) flags[blk] = 0;  // every lane read the flags before the first round
         updated += nupd;
         rmw += nrmw;
     }
@@ -1078,7 +1088,6 @@ void Scene::reset() {
     k_reset_heap<<<grid, 256, 0, stream_>>>(heap_.p, blockPos_.p, blockCount_.p, B_, ctrl_.p);
     BF_LAUNCH_CHECK();
     BF_HIP(hipMemsetAsync(voxels_.p, 0, voxels_.bytes(), stream_));
-    BF_HIP(hipMemsetAsync(blockFlags_.p, 0, blockFlags_.bytes(), stream_));
     cfg_.hp.numOccupiedBlocks = 0;
 }
 
@@ -1105,7 +1114,7 @@ void Scene::compactify(const BFMat4& T, const BFDepthCameraParams& cam) {
     Tinv_ = mat4_inverse(T);
     beginOp();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_compactify<CM_FRUSTUM><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr, nullptr);
+    k_compactify<CM_FRUSTUM><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr, nullptr, Tinv_);
     BF_LAUNCH_CHECK();
 }
 
@@ -1130,7 +1139,8 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     A.tilesW = tw;
     A.tilesH = th;
     const unsigned grid = (unsigned)numCUs_ * 4;
-    k_compactify<CM_INTEGRATE><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p, nullptr);
+    k_compactify<CM_INTEGRATE><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p, nullptr,
+                                                          Tinv_);
     BF_LAUNCH_CHECK();
     const unsigned igrid = deint ? integrateGrid_[1] : integrateGrid_[0];
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1158,8 +1168,7 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
 }
 
 // reintegrate() fix of one frame (DepthSensing.cpp:890-895): deIntegrate(Told) + integrate(Tnew)
-// as one fused voxel pass (k_reintegrate). Lists: the de-integration pose's band list is built
-// before alloc(new), as the reference's deIntegrate compactifies before integrate allocates.
+// as one fused voxel pass (k_reintegrate) over one compactify scan (CM_REINT).
 void Scene::reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* depth, const uint8_t* color,
                         const BFDepthCameraParams& cam) {
     BF_REQUIRE(depth != nullptr, BF_ERR_ARG, "depth is null");
@@ -1178,13 +1187,11 @@ void Scene::reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* dep
     A.tilesW = tw;
     A.tilesH = th;
     const unsigned grid = (unsigned)numCUs_ * 4;
-    k_compactify<CM_REINT_OLD><<<grid, 256, 0, stream_>>>(A, cam, TinvOld, 0u, nullptr, nullptr, blockFlags_.p);
-    BF_LAUNCH_CHECK();
     T_ = Tnew;
     Tinv_ = mat4_inverse(Tnew);
     alloc(depth, cam, nullptr);
-    k_compactify<CM_REINT_NEW><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p,
-                                                           blockFlags_.p);
+    k_compactify<CM_REINT><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p,
+                                                      blockFlags_.p, TinvOld);
     BF_LAUNCH_CHECK();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = reintegrateClock_.enabled();
