@@ -163,13 +163,9 @@ def main():
                          "tools/profile_bench.sh on this same command (committed under profiles/)")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side barrier / max only (gloo)
-        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    from bundlefusion_amd.dist import HostGroup, env_rank
+    rank, world, local_rank = env_rank()
+    group = HostGroup(rank, world)  # host-side barrier / max only (gloo)
 
     import bundlefusion_amd as bfa
     from bundlefusion_amd.abi import BFSceneOptions
@@ -193,8 +189,7 @@ def main():
         f"{len(stream.global_host)} global correspondences")
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        group.barrier()
 
     f0 = S * args.warmup
     for f in range(f0):
@@ -213,11 +208,7 @@ def main():
     rc.synchronize()
     dt = time.perf_counter() - t0
     barrier()
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = group.max(dt)
     st = rc.stats()
     ss = rc.scene_stats()
     frames = S * args.steps
@@ -312,8 +303,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     rc.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,69 @@
+"""Host-side multi-process plumbing for one process per GPU (torchrun): rank discovery, a gloo
+group for barriers and max-over-ranks timing, and the TSDF shard assignment. The data path has no
+collective: each rank integrates only the 1 m chunks it owns."""
+from __future__ import annotations
+
+import os
+
+
+def env_rank():
+    """(rank, world_size, local_rank) from the torchrun environment (1 process when unset)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+class HostGroup:
+    """gloo process group used only for host synchronisation (barrier, max of a float)."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, value: float) -> float:
+        if self.dist is None:
+            return value
+        import torch
+        t = torch.tensor([value], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, value: float) -> float:
+        if self.dist is None:
+            return value
+        import torch
+        t = torch.tensor([value], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+
+
+def chunk_owner(bx: int, by: int, bz: int, voxel_size: float, shard_count: int, chunk: float = 1.0) -> int:
+    """Shard owning block (bx, by, bz): computeHashPos of its 1 m chunk (worldToChunks rounding,
+    CUDASceneRepHashSDF.cu:136-150) mod shard_count — the host mirror of owned() in csrc/tsdf.hip."""
+    import numpy as np
+    w = np.float32(bx * 8) * np.float32(voxel_size), np.float32(by * 8) * np.float32(voxel_size), \
+        np.float32(bz * 8) * np.float32(voxel_size)
+    c = []
+    for v in w:
+        q = np.float32(v / np.float32(chunk))
+        s = np.float32(np.sign(q)) * np.float32(0.5)
+        c.append(int(np.trunc(np.float32(q + s))))
+    x, y, z = c
+    a = np.int32(np.uint32(x & 0xFFFFFFFF) * np.uint32(73856093) & 0xFFFFFFFF)
+    b = np.int32(np.uint32(y & 0xFFFFFFFF) * np.uint32(19349669) & 0xFFFFFFFF)
+    d = np.int32(np.uint32(z & 0xFFFFFFFF) * np.uint32(83492791) & 0xFFFFFFFF)
+    h = int(np.int32(a ^ b ^ d))
+    r = int(np.fmod(h, shard_count))
+    return r + shard_count if r < 0 else r
