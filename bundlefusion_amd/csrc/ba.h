@@ -4,7 +4,11 @@
 // Device layout (all resident in HBM, sized for maxImages / maxCorr at construction):
 //   rowCount/rowStart/rowLen   per-image CSR of correspondence indices, built deterministically
 //                              (ascending correspondence index, as a serial replay of the
-//                              reference's atomic table build, SolverBundling.cu:1226-1248)
+//                              reference's atomic table build, SolverBundling.cu:1226-1248) by a
+//                              tiled stable counting sort (tileCnt: per-row, per-tile counts)
+//   chunks                     every row cut into chunks of CH entries: the work unit of one wave
+//                              in the GN/PCG kernels; chunk partials are summed per row in chunk
+//                              order by the finishing workgroup (deterministic, no float atomics)
 //   entries                    per row entry, rebuilt each GN iteration: {T_self*p_self, other},
 //                              {T_other*p_other} — 32 B, streamed contiguously by the PCG loop
 //   vec                        per-image 8-float vectors: x is the caller's (rot, trans);
@@ -91,7 +95,12 @@ private:
     uint32_t maxCorrPerImage_;
     uint32_t maxPairs_;
     int numCUs_;
-    DevBuf<int> rowCount_, rowStart_, rowLen_, fill_;
+    uint32_t maxTiles_;
+    size_t maxChunks_;
+    DevBuf<int> rowCount_, rowStart_, rowLen_;
+    DevBuf<int> tileCnt_, rowChunk_, chunkRow_;
+    DevBuf<float4> chunkPart_;
+    DevBuf<unsigned long long> probe_;
     DevBuf<int> rowTmp_, rowIdx_;
     DevBuf<float4> entries_;
     DevBuf<float> vec_;     // [N][8] per field

@@ -15,6 +15,8 @@
 #include "lie.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -24,12 +26,15 @@ namespace {
 
 constexpr float FLOAT_EPSILON = 0.000001f;  // Source/SolverUtil.h:9
 constexpr int WG = 256;
-constexpr int SORT_CAP = 8192;  // LDS row sort capacity
+constexpr uint32_t TILE = 256;  // correspondences per table-build tile
+constexpr int CH = 512;        // row entries per chunk: the work unit of one wave in the GN/PCG kernels
+constexpr int CPL = CH / 64;   // chunk entries per lane
 
 enum VecField { V_DELTA = 0, V_R, V_Z, V_P, V_AP, V_M, V_NUM };
 enum CtrlWord {
     K_TICKET = 0, K_PCG_DONE, K_GN_DONE, K_GN_ITERS, K_PCG_ITERS, K_RDOTZ, K_NPAIRS, K_LAST_W,
-    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J, K_COUNT = 16
+    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J, K_COUNT = 16,
+    K_NCHUNK = K_COUNT, K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
 };
 
 struct BA {
@@ -37,7 +42,12 @@ struct BA {
     uint32_t nCorr;
     const int* valid;
     uint32_t N, maxN, cap;
-    int *rowCount, *rowStart, *rowLen, *fill, *rowTmp, *rowIdx;
+    int *rowCount, *rowStart, *rowLen, *rowTmp, *rowIdx;
+    int* tileCnt;  // [N][nTiles]
+    uint32_t nTiles;
+    int *rowChunk, *chunkRow;  // chunks of row v: [rowChunk[v], rowChunk[v+1]); chunk -> row
+    float4* chunkPart;         // [chunk][3] per-chunk partial sums
+    unsigned long long* probe; // development timing probe (BF_BA_PROBE=1), else null
     float4* entries;
     float* vec;
     float* img;
@@ -91,42 +101,106 @@ __device__ __forceinline__ m4 loadm4(const float* p) {
 }
 __device__ __forceinline__ bool corr_valid(const BFEntryJ& e) { return e.imgIdx_i != BF_INVALID_IMAGE; }
 
-// "Last workgroup" hand-off (MI355X_MICROARCH.md visibility rules): every workgroup publishes with
-// an agent-scope release + ticket; the last arriver acquires before reading everyone's data.
+// In-launch hand-offs (MI355X_MICROARCH.md §inter-workgroup visibility, "valid forms" row 1): the
+// producer stores its payload write-through (sc1: 8-B agent-scope atomic stores to global memory),
+// drains its stores (s_waitcnt vmcnt(0)) and then adds to an agent-scope counter; the adder that
+// draws the last ticket reads the payload with sc1 loads (which bypass this CU's L1). No release or
+// acquire fence is needed, so the hand-off costs no L2 write-back per wave.
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void st_wt(float4* p, float4 v) {
+    gu64* q = (gu64*)(p);
+    __hip_atomic_store(q, ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, ((uint64_t)__float_as_uint(v.w) << 32) | __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 ld_wt(const float4* p) {
+    gu64* q = (gu64*)(p);
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)), __uint_as_float((uint32_t)b),
+                       __uint_as_float((uint32_t)(b >> 32)));
+}
+__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) { __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) { return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_wt(float* p, float v) { st_wt(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
+__device__ __forceinline__ float ld_wtf(const float* p) { return __uint_as_float(ld_wt(reinterpret_cast<const uint32_t*>(p))); }
+__device__ __forceinline__ uint32_t ticket_add(uint32_t* p) {
+    return __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// "Last workgroup" hand-off: every wave drains its write-through stores, one lane takes a ticket;
+// the workgroup holding the last ticket continues (and reads the hand-off with ld_wt).
 __device__ bool last_block(uint32_t* ticket) {
     __shared__ int isLast;
+    drain_stores();
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned t = atomicAdd(ticket, 1u);
-        isLast = (t == gridDim.x * gridDim.y - 1) ? 1 : 0;
-        if (isLast) __threadfence();
-    }
+    if (threadIdx.x == 0) isLast = (ticket_add(ticket) == gridDim.x * gridDim.y - 1) ? 1 : 0;
     __syncthreads();
     return isLast != 0;
 }
 
-// deterministic block reduction (fixed tree) of one float per thread
+// deterministic block reduction of one float per thread: fixed butterfly per wave, then the wave
+// sums in wave order
 __device__ float block_sum(float v, float* sh) {
-    sh[threadIdx.x] = v;
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-        __syncthreads();
-    }
-    const float r = sh[0];
+    float r = 0.0f;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); w++) r += sh[w];
     __syncthreads();
     return r;
 }
 
 // ---- correspondence table (BuildVariablesToCorrespondencesTableDevice, SolverBundling.cu:1226-1248) ----
-__global__ void k_count(BA a) {
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < a.nCorr; c += gridDim.x * blockDim.x) {
-        const BFEntryJ e = a.corr[c];
-        if (!corr_valid(e)) continue;
-        atomicAdd(&a.rowCount[e.imgIdx_i], 1);
-        atomicAdd(&a.rowCount[e.imgIdx_j], 1);
+// The reference appends (image -> correspondence) pairs with atomics and drops an append once the row
+// holds maxCorrPerImage entries. The deterministic replay here is a stable counting sort: rows list
+// their correspondences in ascending index order (the serial order of that loop), an entry ranked
+// >= cap in either of its rows invalidates the correspondence. Three passes over tiles of TILE
+// consecutive correspondences: per-tile row histograms, a per-row scan over tiles, and a placement
+// pass that ranks each entry inside its tile with wave ballots (no global atomics, no row sort).
+__device__ __forceinline__ bool corr_rows(const BA& a, uint32_t c, uint32_t& i, uint32_t& j) {
+    const uint2 ij = *reinterpret_cast<const uint2*>(&a.corr[c].imgIdx_i);
+    i = ij.x; j = ij.y;
+    return i != BF_INVALID_IMAGE && i < a.N && j < a.N;
+}
+__global__ __launch_bounds__(64) void k_tile_count(BA a) {
+    extern __shared__ int hist[];  // [N]
+    const uint32_t t = blockIdx.x;
+    for (uint32_t r = threadIdx.x; r < a.N; r += 64) hist[r] = 0;
+    __syncthreads();
+    const uint32_t c1 = min((t + 1) * TILE, a.nCorr);
+    for (uint32_t c = t * TILE + threadIdx.x; c < c1; c += 64) {
+        uint32_t i, j;
+        if (!corr_rows(a, c, i, j)) continue;
+        atomicAdd(&hist[i], 1);
+        atomicAdd(&hist[j], 1);
     }
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < a.N; r += 64) a.tileCnt[(size_t)r * a.nTiles + t] = hist[r];
+}
+// one workgroup per row: exclusive scan of the row's tile counts (in place), rowCount = total
+__global__ __launch_bounds__(WG) void k_tile_scan(BA a) {
+    __shared__ int sh[WG];
+    const uint32_t r = blockIdx.x;
+    int* cnt = a.tileCnt + (size_t)r * a.nTiles;
+    int carry = 0;
+    for (uint32_t base = 0; base < a.nTiles; base += WG) {
+        const uint32_t t = base + threadIdx.x;
+        const int c = t < a.nTiles ? cnt[t] : 0;
+        sh[threadIdx.x] = c;
+        __syncthreads();
+        for (int off = 1; off < WG; off <<= 1) {
+            const int x = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (t < a.nTiles) cnt[t] = carry + sh[threadIdx.x] - c;
+        carry += sh[WG - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.rowCount[r] = carry;
 }
 __global__ void k_scan(BA a) {  // one workgroup: exclusive scan of rowCount -> rowStart
     __shared__ int sh[WG];
@@ -142,51 +216,52 @@ __global__ void k_scan(BA a) {  // one workgroup: exclusive scan of rowCount -> 
             sh[threadIdx.x] += t;
             __syncthreads();
         }
-        if (v < a.N) { a.rowStart[v] = carry + sh[threadIdx.x] - c; a.fill[v] = 0; }
+        if (v < a.N) a.rowStart[v] = carry + sh[threadIdx.x] - c;
         carry += sh[WG - 1];
         __syncthreads();
     }
     if (threadIdx.x == 0) a.rowStart[a.N] = carry;
 }
-__global__ void k_fill(BA a) {
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < a.nCorr; c += gridDim.x * blockDim.x) {
-        const BFEntryJ e = a.corr[c];
-        if (!corr_valid(e)) continue;
-        const int k0 = atomicAdd(&a.fill[e.imgIdx_i], 1);
-        a.rowTmp[a.rowStart[e.imgIdx_i] + k0] = (int)c;
-        const int k1 = atomicAdd(&a.fill[e.imgIdx_j], 1);
-        a.rowTmp[a.rowStart[e.imgIdx_j] + k1] = (int)c;
-    }
-}
-// Sort each row by correspondence index (the serial order of the reference's table build), then
-// apply the per-image cap: a correspondence ranked >= cap in either of its rows is invalidated.
-__global__ __launch_bounds__(WG) void k_sort_rows(BA a) {
-    __shared__ int sh[SORT_CAP];
-    const uint32_t v = blockIdx.x;
-    if (v >= a.N) return;
-    const int n = a.rowCount[v], s0 = a.rowStart[v];
-    if (n > SORT_CAP) { if (threadIdx.x == 0) atomicOr(&a.ctrl[K_ERROR], 1u); return; }
-    int P = 1;
-    while (P < n) P <<= 1;
-    for (int k = threadIdx.x; k < P; k += WG) sh[k] = k < n ? a.rowTmp[s0 + k] : 0x7FFFFFFF;
+// placement: one wave per tile, 64 correspondences per step. Each distinct row key of the step is
+// resolved in one ballot round: an entry's slot = row start + the row's tile offset + entries of
+// that row placed earlier in this tile + lower lanes of this step holding the same row (an i entry
+// precedes the j entry of the same correspondence).
+__global__ __launch_bounds__(64) void k_tile_fill(BA a) {
+    extern __shared__ int run[];  // [N] entries placed so far in this tile, per row
+    const uint32_t t = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t r = lane; r < a.N; r += 64) run[r] = 0;
     __syncthreads();
-    for (int size = 2; size <= P; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int k = threadIdx.x; k < P; k += WG) {
-                const int p2 = k ^ stride;
-                if (p2 > k) {
-                    const bool up = (k & size) == 0;
-                    const int x = sh[k], y = sh[p2];
-                    if ((x > y) == up) { sh[k] = y; sh[p2] = x; }
-                }
-            }
+    const uint64_t lower = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t c1 = min((t + 1) * TILE, a.nCorr);
+    for (uint32_t c0 = t * TILE; c0 < c1; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        uint32_t i = BF_INVALID_IMAGE, j = BF_INVALID_IMAGE;
+        const bool ok = c < c1 && corr_rows(a, c, i, j);
+        uint64_t pendI = __ballot(ok), pendJ = pendI;
+        int posI = -1, posJ = -1;
+        while (pendI | pendJ) {
+            const int src = pendI ? __ffsll((unsigned long long)pendI) - 1 : __ffsll((unsigned long long)pendJ) - 1;
+            const uint32_t key = __shfl(pendI ? i : j, src);
+            const bool hi = ok && i == key, hj = ok && j == key;
+            const uint64_t mi = __ballot(hi), mj = __ballot(hj);
+            const int base = a.rowStart[key] + a.tileCnt[(size_t)key * a.nTiles + t] + run[key];
+            const int below = __popcll(mi & lower) + __popcll(mj & lower);
+            if (hi) posI = base + below;
+            if (hj) posJ = base + below + (hi ? 1 : 0);
             __syncthreads();
+            if (lane == 0) run[key] += __popcll(mi) + __popcll(mj);
+            __syncthreads();
+            pendI &= ~mi;
+            pendJ &= ~mj;
         }
-    for (int k = threadIdx.x; k < n; k += WG) {
-        a.rowTmp[s0 + k] = sh[k];
-        if ((uint32_t)k >= a.cap) {  // invalidate (setInvalid, SolverBundling.cu:1241-1245)
-            a.corr[sh[k]].imgIdx_i = BF_INVALID_IMAGE;
-            a.corr[sh[k]].imgIdx_j = BF_INVALID_IMAGE;
+        if (ok) {
+            a.rowTmp[posI] = (int)c;
+            a.rowTmp[posJ] = (int)c;
+            // setInvalid (SolverBundling.cu:1241-1245) for an entry past the per-image cap
+            if (posI - a.rowStart[i] >= (int)a.cap || posJ - a.rowStart[j] >= (int)a.cap) {
+                a.corr[c].imgIdx_i = BF_INVALID_IMAGE;
+                a.corr[c].imgIdx_j = BF_INVALID_IMAGE;
+            }
         }
     }
 }
@@ -219,6 +294,41 @@ __global__ __launch_bounds__(WG) void k_compact_rows(BA a) {
     if (threadIdx.x == 0) a.rowLen[v] = base;
 }
 
+// chunk table: row v (v >= 1; image 0 is fixed) is cut into ceil(rowLen / CH) chunks of CH entries
+__global__ void k_chunks(BA a) {  // one workgroup
+    __shared__ int sh[WG];
+    int carry = 0;
+    for (uint32_t base = 0; base < a.N; base += WG) {
+        const uint32_t v = base + threadIdx.x;
+        const int c = (v >= 1 && v < a.N) ? (a.rowLen[v] + CH - 1) / CH : 0;
+        sh[threadIdx.x] = c;
+        __syncthreads();
+        for (int off = 1; off < WG; off <<= 1) {
+            const int x = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += x;
+            __syncthreads();
+        }
+        const int s = carry + sh[threadIdx.x] - c;
+        if (v < a.N) {
+            a.rowChunk[v] = s;
+            for (int q = 0; q < c; q++) a.chunkRow[s + q] = (int)v;
+        }
+        carry += sh[WG - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.rowChunk[a.N] = carry;
+        a.ctrl[K_NCHUNK] = (uint32_t)carry;
+    }
+}
+__device__ __forceinline__ void chunk_range(const BA& a, uint32_t c, uint32_t& v, int& k0, int& k1) {
+    v = (uint32_t)a.chunkRow[c];
+    const int s0 = a.rowStart[v];
+    k0 = s0 + ((int)c - a.rowChunk[v]) * CH;
+    k1 = min(s0 + a.rowLen[v], k0 + CH);
+}
+
 // ---- per GN iteration -------------------------------------------------------------------------
 // convertLiePosesToMatricesCU (SolverBundling.cu:1114-1121); also resets the PCG state of this
 // GN iteration. gated: no-op once the GN loop converged on the device.
@@ -246,43 +356,94 @@ __global__ void k_transforms(BA a, float wSparse, int useDense, int gated, int s
     }
 }
 
+// chunk partials are handed to the finishing workgroup write-through (see last_block)
+__device__ __forceinline__ void put_part(const BA& a, uint32_t c, int f, f3 s) {
+    st_wt(a.chunkPart + (size_t)c * 3 + f, make_float4(s.x, s.y, s.z, 0.0f));
+}
+// PCGInit per row: r = -Jtr, Jacobi preconditioner, p = M r; returns r.z
+__device__ float init_row(const BA& a, uint32_t v, f3 rr, f3 rt, f3 pr, float wSparse, int useDense) {
+    const float cnt = (float)a.rowLen[v];
+    f3 resR = mk3(-wSparse * rr.x, -wSparse * rr.y, -wSparse * rr.z);
+    f3 resT = mk3(-wSparse * rt.x, -wSparse * rt.y, -wSparse * rt.z);
+    if (useDense) {
+        const float* j = a.jtr + (size_t)v * 6;
+        resR = resR - mk3(j[3], j[4], j[5]);
+        resT = resT - mk3(j[0], j[1], j[2]);
+    }
+    auto inv = [](float x) { return x > FLOAT_EPSILON ? 1.0f / x : 1.0f; };
+    const f3 mR = mk3(inv(pr.x), inv(pr.y), inv(pr.z));
+    const f3 mT = mk3(inv(cnt), inv(cnt), inv(cnt));
+    const f3 pR = mul3(mR, resR), pT = mul3(mT, resT);
+    vstore(a, V_M, v, mR, mT);
+    vstore(a, V_R, v, resR, resT);
+    vstore(a, V_P, v, pR, pT);
+    vstore(a, V_DELTA, v, mk3(0, 0, 0), mk3(0, 0, 0));
+    return dot3(resR, pR) + dot3(resT, pT);
+}
+
 // world points of every row entry for this GN iteration: {T_self p_self, other}, {T_other p_other}
 __global__ __launch_bounds__(WG) void k_entries(BA a) {
     if (a.ctrl[K_GN_DONE]) return;
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
-        const int s0 = a.rowStart[v], n = a.rowLen[v];
-        for (int k = lane; k < n; k += 64) {
-            const BFEntryJ e = a.corr[a.rowIdx[s0 + k]];
+    const uint32_t nch = a.ctrl[K_NCHUNK];
+    for (uint32_t c = wave; c < nch; c += nw) {
+        uint32_t v;
+        int k0, k1;
+        chunk_range(a, c, v, k0, k1);
+        const m4 Tv = loadm4(a.T + (size_t)v * 16);
+        int idx[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; u++) idx[u] = a.rowIdx[min(k0 + (int)lane + 64 * u, k1 - 1)];
+        BFEntryJ ev[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; u++) ev[u] = a.corr[idx[u]];
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            const int k = k0 + (int)lane + 64 * u;
+            if (k >= k1) break;
+            const BFEntryJ e = ev[u];
             const bool isI = (e.imgIdx_i == v);
             const uint32_t other = isI ? e.imgIdx_j : e.imgIdx_i;
             const f3 ps = isI ? mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z) : mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z);
             const f3 po = isI ? mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z) : mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z);
-            const f3 Ps = xf(loadm4(a.T + (size_t)v * 16), ps);
+            const f3 Ps = xf(Tv, ps);
             const f3 Po = xf(loadm4(a.T + (size_t)other * 16), po);
-            a.entries[2 * (s0 + k)] = make_float4(Ps.x, Ps.y, Ps.z, __uint_as_float(other));
-            a.entries[2 * (s0 + k) + 1] = make_float4(Po.x, Po.y, Po.z, 0.0f);
+            a.entries[2 * k] = make_float4(Ps.x, Ps.y, Ps.z, __uint_as_float(other));
+            a.entries[2 * k + 1] = make_float4(Po.x, Po.y, Po.z, 0.0f);
         }
     }
 }
 
-// evalMinusJTFDevice (SolverBundlingEquationsLie.h:63-148) + PCGInit_Kernel1/2 (SolverBundling.cu:755-794)
+// evalMinusJTFDevice (SolverBundlingEquationsLie.h:63-148) + PCGInit_Kernel1/2 (SolverBundling.cu:755-794).
+// Every wave reduces one chunk; the last workgroup sums each row's chunk partials (chunk order),
+// initialises the row and sums r.z.
 __global__ __launch_bounds__(WG) void k_init(BA a, float wSparse) {
     __shared__ float sh[WG];
     if (a.ctrl[K_GN_DONE]) return;
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nch = a.ctrl[K_NCHUNK];
     const int useDense = (int)a.ctrl[K_USE_DENSE];
-    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
-        const int s0 = a.rowStart[v], n = a.rowLen[v];
+    for (uint32_t c = wave; c < nch; c += nw) {
+        uint32_t v;
+        int k0, k1;
+        chunk_range(a, c, v, k0, k1);
         float rr[3] = {0, 0, 0}, rt[3] = {0, 0, 0}, pr[3] = {0, 0, 0};
-        for (int k = lane; k < n; k += 64) {
-            const float4 A = a.entries[2 * (s0 + k)], B = a.entries[2 * (s0 + k) + 1];
-            const f3 Ps = mk3(A.x, A.y, A.z), Po = mk3(B.x, B.y, B.z);
+        float4 A[CPL], B[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            const int k = min(k0 + (int)lane + 64 * u, k1 - 1);
+            A[u] = a.entries[2 * k];
+            B[u] = a.entries[2 * k + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            f3 Ps = mk3(A[u].x, A[u].y, A[u].z), Po = mk3(B[u].x, B[u].y, B[u].z);
+            if (k0 + (int)lane + 64 * u >= k1) { Ps = mk3(0, 0, 0); Po = Ps; }
             const f3 r = Ps - Po;         // sign * (T_i p_i - T_j p_j)
-            const f3 c = cross3(Ps, r);   // (dot(da,r), dot(db,r), dot(dc,r)) of P_s
-            rr[0] += c.x; rr[1] += c.y; rr[2] += c.z;
+            const f3 cr = cross3(Ps, r);  // (dot(da,r), dot(db,r), dot(dc,r)) of P_s
+            rr[0] += cr.x; rr[1] += cr.y; rr[2] += cr.z;
             rt[0] += r.x; rt[1] += r.y; rt[2] += r.z;
             pr[0] += Ps.z * Ps.z + Ps.y * Ps.y;  // |dAlpha|^2
             pr[1] += Ps.z * Ps.z + Ps.x * Ps.x;  // |dBeta|^2
@@ -290,82 +451,167 @@ __global__ __launch_bounds__(WG) void k_init(BA a, float wSparse) {
         }
         for (int q = 0; q < 3; q++) { rr[q] = wave_sum(rr[q]); rt[q] = wave_sum(rt[q]); pr[q] = wave_sum(pr[q]); }
         if (lane == 0) {
-            const float cnt = (float)n;
-            f3 resR = mk3(-wSparse * rr[0], -wSparse * rr[1], -wSparse * rr[2]);
-            f3 resT = mk3(-wSparse * rt[0], -wSparse * rt[1], -wSparse * rt[2]);
-            if (useDense) {
-                const float* j = a.jtr + (size_t)v * 6;
-                resR = resR - mk3(j[3], j[4], j[5]);
-                resT = resT - mk3(j[0], j[1], j[2]);
-            }
-            auto inv = [](float x) { return x > FLOAT_EPSILON ? 1.0f / x : 1.0f; };
-            const f3 mR = mk3(inv(pr[0]), inv(pr[1]), inv(pr[2]));
-            const f3 mT = mk3(inv(cnt), inv(cnt), inv(cnt));
-            const f3 pR = mul3(mR, resR), pT = mul3(mT, resT);
-            vstore(a, V_M, v, mR, mT);
-            vstore(a, V_R, v, resR, resT);
-            vstore(a, V_P, v, pR, pT);
-            vstore(a, V_DELTA, v, mk3(0, 0, 0), mk3(0, 0, 0));
-            a.img[v] = dot3(resR, pR) + dot3(resT, pT);
+            put_part(a, c, 0, mk3(rr[0], rr[1], rr[2]));
+            put_part(a, c, 1, mk3(rt[0], rt[1], rt[2]));
+            put_part(a, c, 2, mk3(pr[0], pr[1], pr[2]));
         }
     }
-    if (last_block(&a.ctrl[K_TICKET])) {
-        float s = 0.0f;
-        for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) s += a.img[v];
-        s = block_sum(s, sh);
-        if (threadIdx.x == 0) {
-            a.ctrl[K_RDOTZ] = __float_as_uint(s);
-            a.ctrl[K_TICKET] = 0;
-            vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
+    if (!last_block(&a.ctrl[K_TICKET])) return;
+    float s = 0.0f;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+        f3 sR = mk3(0, 0, 0), sT = sR, sP = sR;
+        for (int c = a.rowChunk[v]; c < a.rowChunk[v + 1]; c++) {
+            const float4 x = ld_wt(a.chunkPart + (size_t)c * 3), y = ld_wt(a.chunkPart + (size_t)c * 3 + 1),
+                         z = ld_wt(a.chunkPart + (size_t)c * 3 + 2);
+            sR = sR + mk3(x.x, x.y, x.z);
+            sT = sT + mk3(y.x, y.y, y.z);
+            sP = sP + mk3(z.x, z.y, z.z);
         }
+        s += init_row(a, v, sR, sT, sP, wSparse, useDense);
+    }
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) {
+        a.ctrl[K_RDOTZ] = __float_as_uint(s);
+        a.ctrl[K_TICKET] = 0;
+        vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
     }
 }
 
+// Ap of row v for the finisher: the sparse part handed over by the row's last chunk wave, plus the
+// dense diagonal block and the dense off-diagonal atomics (reset for the next iteration)
+__device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, int useDense, f3 pR, f3 pT, f3& aR, f3& aT) {
+    aR = mk3(0, 0, 0);
+    aT = mk3(0, 0, 0);
+    if (nch) {  // sparse part: the row's chunk partials, in chunk order
+        const int c1 = a.rowChunk[v + 1];
+#pragma unroll 4
+        for (int c = a.rowChunk[v]; c < c1; c++) {
+            const float4 x = ld_wt(a.chunkPart + (size_t)c * 3), y = ld_wt(a.chunkPart + (size_t)c * 3 + 1);
+            aR = aR + mk3(x.x, x.y, x.z);
+            aT = aT + mk3(y.x, y.y, y.z);
+        }
+    }
+    if (useDense) {  // diagonal block [trans | rot] x [pTrans | pRot]
+        const float* D = a.diag + (size_t)v * 36;
+        const float pv[6] = {pT.x, pT.y, pT.z, pR.x, pR.y, pR.z};
+        float o6[6];
+        for (int r = 0; r < 6; r++) {
+            float s = 0.0f;
+            for (int c = 0; c < 6; c++) s += D[r * 6 + c] * pv[c];
+            o6[r] = s;
+        }
+        aT = aT + mk3(o6[0], o6[1], o6[2]);
+        aR = aR + mk3(o6[3], o6[4], o6[5]);
+        float4* ad = reinterpret_cast<float4*>(a.apDense + (size_t)v * 8);
+        const float4 x = ld_wt(ad), y = ld_wt(ad + 1);  // agent-scope atomics of this launch
+        aR = aR + mk3(x.x, x.y, x.z);
+        aT = aT + mk3(y.x, y.y, y.z);
+        ad[0] = make_float4(0, 0, 0, 0);
+        ad[1] = make_float4(0, 0, 0, 0);
+    }
+}
+
+// PCG finisher with each thread's R rows held in registers: all loads issue up front, then the
+// two block reductions, then the stores (z and Ap never go to memory). Same arithmetic as the
+// multi-pass form below.
+template <int R>
+__device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, bool& lastOut) {
+    f3 pR[R], pT[R], aR[R], aT[R], dR[R], dT[R], rR[R], rT[R], mR[R], mT[R];
+    float d = 0.0f;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        const uint32_t v = 1 + threadIdx.x + q * WG;
+        if (v < a.N) {
+            vload(a, V_P, v, pR[q], pT[q]);
+            vload(a, V_DELTA, v, dR[q], dT[q]);
+            vload(a, V_R, v, rR[q], rT[q]);
+            vload(a, V_M, v, mR[q], mT[q]);
+            pcg_ap(a, v, nch, useDense, pR[q], pT[q], aR[q], aT[q]);
+            d += dot3(pR[q], aR[q]) + dot3(pT[q], aT[q]);
+        }
+    }
+    const float pAp = block_sum(d, sh);
+    const float rDotzOld = ctrlf(a.ctrl, K_RDOTZ);
+    const float alpha = (pAp > FLOAT_EPSILON) ? rDotzOld / pAp : 0.0f;
+    float b = 0.0f;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        if (1 + threadIdx.x + q * WG < a.N) {
+            dR[q] = dR[q] + alpha * pR[q];
+            dT[q] = dT[q] + alpha * pT[q];
+            rR[q] = rR[q] - alpha * aR[q];
+            rT[q] = rT[q] - alpha * aT[q];
+            mR[q] = mul3(mR[q], rR[q]);  // z
+            mT[q] = mul3(mT[q], rT[q]);
+            b += dot3(mR[q], rR[q]) + dot3(mT[q], rT[q]);
+        }
+    }
+    const float rDotzNew = block_sum(b, sh);
+    const bool last = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+    const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew / rDotzOld : 0.0f;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        const uint32_t v = 1 + threadIdx.x + q * WG;
+        if (v < a.N) {
+            vstore(a, V_DELTA, v, dR[q], dT[q]);
+            vstore(a, V_R, v, rR[q], rT[q]);
+            vstore(a, V_P, v, mR[q] + beta * pR[q], mT[q] + beta * pT[q]);
+            if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
+                f3 nr, nt;
+                lie_update(dR[q], dT[q], mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                           mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
+                a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
+                a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+            }
+        }
+    }
+    lastOut = last;
+    return rDotzNew;
+}
+
 // One PCG iteration (PCGIteration, SolverBundling.cu:1024-1108) in one launch: every wave
-// computes Ap for its rows (sparse JtJp + dense diagonal block), waves also apply the dense
-// off-diagonal pair blocks; the last workgroup then does the global dot products and the
-// alpha / beta updates (Kernel1b, Kernel2, Kernel3) and the Lie update on the exiting iteration.
+// computes the sparse JtJp partial of its chunks; waves also apply the dense off-diagonal pair
+// blocks. The last workgroup then sums each row's partials in chunk order, adds the dense diagonal
+// block, does the global dot products and the alpha / beta updates (Kernel1b, Kernel2, Kernel3) and
+// the Lie update on the exiting iteration.
 __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int nLin) {
     __shared__ float sh[WG];
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const unsigned long long tStart = a.probe ? wall_clock64() : 0ull;
     const int useDense = (int)a.ctrl[K_USE_DENSE];
-    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
-        const int s0 = a.rowStart[v], n = a.rowLen[v];
+    const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
+    for (uint32_t c = wave; c < nch; c += nw) {
+        uint32_t v;
+        int k0, k1;
+        chunk_range(a, c, v, k0, k1);
         f3 pRv, pTv;
         vload(a, V_P, v, pRv, pTv);
         float ar[3] = {0, 0, 0}, at[3] = {0, 0, 0};
-        if (wSparse > 0.0f) {
-            for (int k = lane; k < n; k += 64) {
-                const float4 A = a.entries[2 * (s0 + k)], B = a.entries[2 * (s0 + k) + 1];
-                const f3 Ps = mk3(A.x, A.y, A.z), Po = mk3(B.x, B.y, B.z);
-                const uint32_t o = __float_as_uint(A.w);
-                f3 pRo, pTo;
-                vload(a, V_P, o, pRo, pTo);
-                const f3 g = (cross3(pRv, Ps) + pTv - (cross3(pRo, Po) + pTo)) * wSparse;
-                const f3 c = cross3(Ps, g);
-                ar[0] += c.x; ar[1] += c.y; ar[2] += c.z;
-                at[0] += g.x; at[1] += g.y; at[2] += g.z;
-            }
-            for (int q = 0; q < 3; q++) { ar[q] = wave_sum(ar[q]); at[q] = wave_sum(at[q]); }
+        // all CH/64 entries of this lane are loaded before any is used (clamped indices, masked
+        // sums: no per-entry branch), so a chunk costs one HBM round trip plus one L2 gather
+        float4 A[CPL], B[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            const int k = min(k0 + (int)lane + 64 * u, k1 - 1);
+            A[u] = a.entries[2 * k];
+            B[u] = a.entries[2 * k + 1];
         }
-        if (lane == 0) {
-            f3 apR = mk3(ar[0], ar[1], ar[2]), apT = mk3(at[0], at[1], at[2]);
-            if (useDense) {  // diagonal block [trans | rot] x [pTrans | pRot]
-                const float* D = a.diag + (size_t)v * 36;
-                const float pv[6] = {pTv.x, pTv.y, pTv.z, pRv.x, pRv.y, pRv.z};
-                float o6[6];
-                for (int r = 0; r < 6; r++) {
-                    float s = 0.0f;
-                    for (int c = 0; c < 6; c++) s += D[r * 6 + c] * pv[c];
-                    o6[r] = s;
-                }
-                apT = apT + mk3(o6[0], o6[1], o6[2]);
-                apR = apR + mk3(o6[3], o6[4], o6[5]);
-            }
-            vstore(a, V_AP, v, apR, apT);
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            const f3 Ps = mk3(A[u].x, A[u].y, A[u].z), Po = mk3(B[u].x, B[u].y, B[u].z);
+            const uint32_t o = __float_as_uint(A[u].w);
+            f3 pRo, pTo;
+            vload(a, V_P, o, pRo, pTo);
+            f3 g = (cross3(pRv, Ps) + pTv - (cross3(pRo, Po) + pTo)) * wSparse;
+            f3 cr = cross3(Ps, g);
+            if (k0 + (int)lane + 64 * u >= k1) { g = mk3(0, 0, 0); cr = g; }
+            ar[0] += cr.x; ar[1] += cr.y; ar[2] += cr.z;
+            at[0] += g.x; at[1] += g.y; at[2] += g.z;
         }
+        for (int q = 0; q < 3; q++) { ar[q] = wave_sum(ar[q]); at[q] = wave_sum(at[q]); }
+        if (lane == 0) { put_part(a, c, 0, mk3(ar[0], ar[1], ar[2])); put_part(a, c, 1, mk3(at[0], at[1], at[2])); }
     }
     if (useDense) {  // off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j)
         const uint32_t np = a.ctrl[K_NPAIRS];
@@ -389,68 +635,87 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
             }
         }
     }
+    if (a.probe && threadIdx.x == 0) {
+        __hip_atomic_store((gu64*)&a.probe[16 + 2 * blockIdx.x], (uint64_t)tStart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)&a.probe[17 + 2 * blockIdx.x], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!last_block(&a.ctrl[K_TICKET])) return;
+    const unsigned long long tFin = a.probe ? wall_clock64() : 0ull;
     // ---- finisher (one workgroup): Kernel1b, Kernel2, host early-out test, Kernel3 ----
-    float d = 0.0f;
-    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
-        f3 pR, pT, aR, aT;
-        vload(a, V_P, v, pR, pT);
-        vload(a, V_AP, v, aR, aT);
-        if (useDense) {
-            float4* ad = reinterpret_cast<float4*>(a.apDense + (size_t)v * 8);
-            const float4 x = ad[0], y = ad[1];
-            aR = aR + mk3(x.x, x.y, x.z);
-            aT = aT + mk3(y.x, y.y, y.z);
-            ad[0] = make_float4(0, 0, 0, 0);
-            ad[1] = make_float4(0, 0, 0, 0);
+    float rDotzNew;
+    bool last;
+    if (a.N <= 2 * WG + 1) {
+        rDotzNew = pcg_finish_regs<2>(a, sh, nch, useDense, iter, nLin, last);
+    } else {
+        float d = 0.0f;
+        for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+            f3 pR, pT, aR, aT;
+            vload(a, V_P, v, pR, pT);
+            pcg_ap(a, v, nch, useDense, pR, pT, aR, aT);
             vstore(a, V_AP, v, aR, aT);
+            d += dot3(pR, aR) + dot3(pT, aT);
         }
-        d += dot3(pR, aR) + dot3(pT, aT);
-    }
-    const float pAp = block_sum(d, sh);
-    const float rDotzOld = ctrlf(a.ctrl, K_RDOTZ);
-    const float alpha = (pAp > FLOAT_EPSILON) ? rDotzOld / pAp : 0.0f;
-    float b = 0.0f;
-    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
-        f3 dR, dT, pR, pT, rR, rT, aR, aT, mR, mT;
-        vload(a, V_DELTA, v, dR, dT);
-        vload(a, V_P, v, pR, pT);
-        vload(a, V_R, v, rR, rT);
-        vload(a, V_AP, v, aR, aT);
-        vload(a, V_M, v, mR, mT);
-        dR = dR + alpha * pR;
-        dT = dT + alpha * pT;
-        rR = rR - alpha * aR;
-        rT = rT - alpha * aT;
-        const f3 zR = mul3(mR, rR), zT = mul3(mT, rT);
-        vstore(a, V_DELTA, v, dR, dT);
-        vstore(a, V_R, v, rR, rT);
-        vstore(a, V_Z, v, zR, zT);
-        b += dot3(zR, rR) + dot3(zT, rT);
-    }
-    const float rDotzNew = block_sum(b, sh);
-    const bool last = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
-    const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew / rDotzOld : 0.0f;
-    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
-        f3 zR, zT, pR, pT;
-        vload(a, V_Z, v, zR, zT);
-        vload(a, V_P, v, pR, pT);
-        vstore(a, V_P, v, zR + beta * pR, zT + beta * pT);
-        if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
-            f3 dR, dT;
+        const float pAp = block_sum(d, sh);
+        const float rDotzOld = ctrlf(a.ctrl, K_RDOTZ);
+        const float alpha = (pAp > FLOAT_EPSILON) ? rDotzOld / pAp : 0.0f;
+        float b = 0.0f;
+        for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+            f3 dR, dT, pR, pT, rR, rT, aR, aT, mR, mT;
             vload(a, V_DELTA, v, dR, dT);
-            f3 nr, nt;
-            lie_update(dR, dT, mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
-                       mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
-            a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
-            a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+            vload(a, V_P, v, pR, pT);
+            vload(a, V_R, v, rR, rT);
+            vload(a, V_AP, v, aR, aT);
+            vload(a, V_M, v, mR, mT);
+            dR = dR + alpha * pR;
+            dT = dT + alpha * pT;
+            rR = rR - alpha * aR;
+            rT = rT - alpha * aT;
+            const f3 zR = mul3(mR, rR), zT = mul3(mT, rT);
+            vstore(a, V_DELTA, v, dR, dT);
+            vstore(a, V_R, v, rR, rT);
+            vstore(a, V_Z, v, zR, zT);
+            b += dot3(zR, rR) + dot3(zT, rT);
         }
+        const float rDotzNew_ = block_sum(b, sh);
+        const bool last_ = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+        const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew_ / rDotzOld : 0.0f;
+        for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
+            f3 zR, zT, pR, pT;
+            vload(a, V_Z, v, zR, zT);
+            vload(a, V_P, v, pR, pT);
+            vstore(a, V_P, v, zR + beta * pR, zT + beta * pT);
+            if (last_) {  // computeLieUpdate (LieDerivUtil.h:301-307)
+                f3 dR, dT;
+                vload(a, V_DELTA, v, dR, dT);
+                f3 nr, nt;
+                lie_update(dR, dT, mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                           mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
+                a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
+                a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+            }
+        }
+        rDotzNew = rDotzNew_;
+        last = last_;
     }
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
         a.ctrl[K_PCG_ITERS]++;
         if (last) a.ctrl[K_PCG_DONE] = 1;
         a.ctrl[K_TICKET] = 0;
+        if (a.probe) {  // (per-WG stamps are handed over write-through, like the payloads)
+            unsigned long long t0 = ~0ull, t1 = 0, dur = 0, lastStart = 0;
+            for (uint32_t b = 0; b < gridDim.x; b++) {
+                const unsigned long long s0 = __hip_atomic_load((gu64*)&a.probe[16 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long s1 = __hip_atomic_load((gu64*)&a.probe[17 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                t0 = s0 < t0 ? s0 : t0;
+                t1 = s1 > t1 ? s1 : t1;
+                lastStart = s0 > lastStart ? s0 : lastStart;
+                dur += s1 - s0;
+            }
+            const unsigned long long t2 = wall_clock64();
+            a.probe[2] += t1 - t0; a.probe[3] += tFin - t0; a.probe[4] += t2 - t0; a.probe[5] += 1;
+            a.probe[6] += dur / gridDim.x; a.probe[7] += lastStart - t0;
+        }
     }
 }
 
@@ -739,22 +1004,36 @@ __global__ __launch_bounds__(WG) void k_residuals(BA a) {
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        a.part[blockIdx.x * 2] = shv[0];
-        a.part[blockIdx.x * 2 + 1] = she[0];
-        a.partIdx[blockIdx.x * 2] = shi[0];
-        a.partIdx[blockIdx.x * 2 + 1] = shc[0];
+        st_wt(&a.part[blockIdx.x * 2], shv[0]);
+        st_wt(&a.part[blockIdx.x * 2 + 1], she[0]);
+        st_wt(reinterpret_cast<uint32_t*>(&a.partIdx[blockIdx.x * 2]), (uint32_t)shi[0]);
+        st_wt(reinterpret_cast<uint32_t*>(&a.partIdx[blockIdx.x * 2 + 1]), (uint32_t)shc[0]);
     }
     if (!last_block(&a.ctrl[K_TICKET])) return;
-    if (threadIdx.x == 0) {
-        float mv = 0.0f, en = 0.0f;
-        int mi = 0x7FFFFFFF, hc = 0;
-        for (uint32_t b = 0; b < gridDim.x; b++) {
-            const float v2 = a.part[b * 2];
-            const int i2 = a.partIdx[b * 2];
-            if (v2 > mv || (v2 == mv && i2 < mi)) { mv = v2; mi = i2; }
-            en += a.part[b * 2 + 1];
-            hc += a.partIdx[b * 2 + 1];
+    // all threads fold the per-workgroup partials, then one fixed tree (deterministic)
+    float mv = 0.0f, en = 0.0f;
+    int mi = 0x7FFFFFFF, hc = 0;
+    for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+        const float v2 = ld_wtf(&a.part[b * 2]);
+        const int i2 = (int)ld_wt(reinterpret_cast<const uint32_t*>(&a.partIdx[b * 2]));
+        if (v2 > mv || (v2 == mv && i2 < mi)) { mv = v2; mi = i2; }
+        en += ld_wtf(&a.part[b * 2 + 1]);
+        hc += (int)ld_wt(reinterpret_cast<const uint32_t*>(&a.partIdx[b * 2 + 1]));
+    }
+    shv[threadIdx.x] = mv; shi[threadIdx.x] = mi; she[threadIdx.x] = en; shc[threadIdx.x] = hc;
+    __syncthreads();
+    for (int s = WG / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            const float v2 = shv[threadIdx.x + s];
+            const int i2 = shi[threadIdx.x + s];
+            if (v2 > shv[threadIdx.x] || (v2 == shv[threadIdx.x] && i2 < shi[threadIdx.x])) { shv[threadIdx.x] = v2; shi[threadIdx.x] = i2; }
+            she[threadIdx.x] += she[threadIdx.x + s];
+            shc[threadIdx.x] += shc[threadIdx.x + s];
         }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        mv = shv[0]; mi = shi[0]; en = she[0]; hc = shc[0];
         if (!(w > 0.0f) || mi == 0x7FFFFFFF) { mv = 0.0f; mi = 0; }
         a.ctrl[K_MAXRES] = __float_as_uint(mv);
         a.ctrl[K_MAXIDX] = (uint32_t)mi;
@@ -876,7 +1155,17 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     rowCount_.alloc(N + 1);
     rowStart_.alloc(N + 1);
     rowLen_.alloc(N + 1);
-    fill_.alloc(N + 1);
+    BF_REQUIRE(cfg.maxImages <= 16384, BF_ERR_CAPACITY, "maxImages > 16384 (LDS row histograms)");
+    maxTiles_ = div_up(cfg.maxCorr, TILE);
+    maxChunks_ = div_up(2 * (size_t)cfg.maxCorr, (size_t)CH) + N;
+    tileCnt_.alloc((size_t)maxTiles_ * N + 1);
+    rowChunk_.alloc(N + 1);
+    if (const char* e = getenv("BF_BA_PROBE"); e && e[0] == '1') {
+        probe_.alloc(16 + 2 * 65536);
+        BF_HIP(hipMemset(probe_.p, 0, probe_.bytes()));
+    }
+    chunkRow_.alloc(maxChunks_ + 1);
+    chunkPart_.alloc(3 * (size_t)maxChunks_ + 3);
     rowTmp_.alloc(2 * (size_t)cfg.maxCorr + 1);
     rowIdx_.alloc(2 * (size_t)cfg.maxCorr + 1);
     entries_.alloc(4 * (size_t)cfg.maxCorr + 2);
@@ -884,7 +1173,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     img_.alloc(2 * (size_t)N);
     T_.alloc((size_t)N * 16);
     Tinv_.alloc((size_t)N * 16);
-    ctrl_.alloc(K_COUNT);
+    ctrl_.alloc(K_CTRL_WORDS);
     part_.alloc(2 * 4096);
     partIdx_.alloc(2 * 4096);
     pairs_.alloc(maxPairs_);
@@ -904,10 +1193,18 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
 }
 
-Solver::~Solver() {}
+Solver::~Solver() {
+    if (probe_.p) {  // development probe: where the time of one PCG launch goes (100 MHz clock)
+        unsigned long long h[8];
+        if (hipMemcpy(h, probe_.p, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess && h[5])
+            fprintf(stderr, "[bf probe] k_pcg launches=%llu chunk-phase=%.2fus finisher-start=%.2fus end=%.2fus "
+                    "mean-WG=%.2fus last-WG-start=%.2fus\n", h[5], h[2] * 0.01 / h[5], h[3] * 0.01 / h[5], h[4] * 0.01 / h[5],
+                    h[6] * 0.01 / h[5], h[7] * 0.01 / h[5]);
+    }
+}
 
 size_t Solver::deviceBytes() const {
-    return rowCount_.bytes() * 4 + rowTmp_.bytes() + rowIdx_.bytes() + entries_.bytes() + vec_.bytes() + img_.bytes() +
+    return rowCount_.bytes() * 3 + tileCnt_.bytes() + rowChunk_.bytes() + chunkRow_.bytes() + chunkPart_.bytes() + rowTmp_.bytes() + rowIdx_.bytes() + entries_.bytes() + vec_.bytes() + img_.bytes() +
            T_.bytes() + Tinv_.bytes() + pairs_.bytes() + pairW_.bytes() + pairBlk_.bytes() + diag_.bytes() + jtr_.bytes();
 }
 
@@ -918,11 +1215,13 @@ void Solver::solve(const SolveArgs& s) {
     BF_REQUIRE(s.nNonLin > 0 && s.wSparse, BF_ERR_ARG, "nNonLin / weights");
     BA a{};
     a.corr = s.corr; a.nCorr = s.numCorr; a.valid = s.valid; a.N = s.numImages; a.maxN = cfg_.maxImages; a.cap = maxCorrPerImage_;
-    a.rowCount = rowCount_.p; a.rowStart = rowStart_.p; a.rowLen = rowLen_.p; a.fill = fill_.p; a.rowTmp = rowTmp_.p; a.rowIdx = rowIdx_.p;
+    a.rowCount = rowCount_.p; a.rowStart = rowStart_.p; a.rowLen = rowLen_.p; a.rowTmp = rowTmp_.p; a.rowIdx = rowIdx_.p;
     a.entries = entries_.p; a.vec = vec_.p; a.img = img_.p; a.T = T_.p; a.Tinv = Tinv_.p; a.ctrl = ctrl_.p;
     a.part = part_.p; a.partIdx = partIdx_.p; a.rot = s.rot; a.trans = s.trans;
     a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p; a.apDense = apDense_.p;
     a.maxPairs = s.numImages * (s.numImages - 1) / 2;
+    a.tileCnt = tileCnt_.p; a.nTiles = div_up(s.numCorr, TILE);
+    a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.probe = probe_.p;
     a.cache = s.cache; a.cw = s.cacheW; a.ch = s.cacheH;
     a.fx = s.intrinsics[0]; a.fy = s.intrinsics[1]; a.mx = s.intrinsics[2]; a.my = s.intrinsics[3];
     a.distT = cfg_.denseDistThresh; a.normT = cfg_.denseNormalThresh; a.colT = cfg_.denseColorThresh;
@@ -931,18 +1230,21 @@ void Solver::solve(const SolveArgs& s) {
     a.verifyT = cfg_.verifyOptDistThresh;
 
     const unsigned corrGrid = std::max(1u, std::min(div_up(s.numCorr, WG), (unsigned)numCUs_ * 8));
-    const unsigned rowGrid = std::max(1u, std::min(div_up((size_t)s.numImages * 64, WG), (unsigned)numCUs_ * 4));
+    // chunk kernels: one wave per chunk of CH row entries, up to 16 waves per CU
+    const size_t chunkBound = div_up(2 * (size_t)s.numCorr, (size_t)CH) + s.numImages;
+    const unsigned rowGrid = std::max(1u, std::min(div_up(chunkBound, (size_t)(WG / 64)), (unsigned)numCUs_ * 4));
     const bool timed = solveClock_.enabled();
     if (timed) solveClock_.start(stream_);
     k_solve_begin<<<1, 64, 0, stream_>>>(ctrl_.p);
     BF_LAUNCH_CHECK();
     if (s.rebuildJT) {
-        BF_HIP(hipMemsetAsync(rowCount_.p, 0, sizeof(int) * (s.numImages + 1), stream_));
-        if (s.numCorr) k_count<<<corrGrid, WG, 0, stream_>>>(a);
+        const size_t lds = sizeof(int) * s.numImages;
+        if (a.nTiles) k_tile_count<<<a.nTiles, 64, lds, stream_>>>(a);
+        k_tile_scan<<<s.numImages, WG, 0, stream_>>>(a);
         k_scan<<<1, WG, 0, stream_>>>(a);
-        if (s.numCorr) k_fill<<<corrGrid, WG, 0, stream_>>>(a);
-        k_sort_rows<<<s.numImages, WG, 0, stream_>>>(a);
+        if (a.nTiles) k_tile_fill<<<a.nTiles, 64, lds, stream_>>>(a);
         k_compact_rows<<<s.numImages, WG, 0, stream_>>>(a);
+        k_chunks<<<1, WG, 0, stream_>>>(a);
         BF_LAUNCH_CHECK();
     }
     for (uint32_t it = 0; it < s.nNonLin; it++) {

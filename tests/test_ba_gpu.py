@@ -124,8 +124,17 @@ def test_global_sparse_schedule():
 
 
 def test_global_sparse_parity_with_outliers():
+    """3 GN x 150 PCG with 2 % outliers. 150 float32 CG iterations per step are past the point where
+    the two summation orders stay in lock-step (see test_single_gn_step_parity_tight), so the
+    solutions are held to the same energy (1e-3 relative), to 5 mrad / 5 mm of each other and to
+    the same accuracy against ground truth."""
     prob = make_problem(K=16, max_per_pair=40, outliers=0.02, seed=5)
-    assert_parity(gpu_solve(prob, 3, 150, [1, 1, 1]), oracle_solve(prob, 3, 150, [1, 1, 1]))
+    g = gpu_solve(prob, 3, 150, [1, 1, 1])
+    o = oracle_solve(prob, 3, 150, [1, 1, 1])
+    assert_parity(g, o, rot_tol=5e-3, trans_tol=5e-3, energy_rtol=1e-3)
+    eg = pose_errors(g[0], g[1], prob["gt"])
+    eo = pose_errors(o[0], o[1], prob["gt"])
+    assert eg[0] <= 1.5 * eo[0] + 1e-3 and eg[1] <= 1.5 * eo[1] + 1e-3, (eg, eo)
 
 
 def test_per_image_cap_invalidation_exact():
@@ -232,3 +241,37 @@ def test_invalidate_pair_and_check_frames():
     S.synchronize()
     np.testing.assert_array_equal(d_valid.download(), [1, 1, 1, 1, 1, 0])
     S.close()
+
+
+def test_per_image_cap_shuffled_order():
+    """Cap invalidation follows correspondence index order, whatever the (i, j) layout of the
+    array: shuffled correspondences give every 64-wide placement step many distinct rows."""
+    prob = make_problem(K=6, stride=2, max_per_pair=256, outliers=0.0)
+    perm = np.random.default_rng(3).permutation(len(prob["corr"]))
+    corr = prob["corr"][perm].copy()
+    max_corr = 6 * 1000
+    g = gpu_solve(prob, 2, 40, [1, 1], max_corr=max_corr, corr=corr)
+    o = oracle_solve(prob, 2, 40, [1, 1], max_corr=max_corr, corr=corr)
+    assert (o[2]["i"] == INVALID).sum() > 0
+    assert_parity(g, o)
+
+
+def test_solve_bit_deterministic():
+    """Chunk partials are handed between waves and workgroups inside a launch (write-through stores +
+    agent-scope tickets) and reduced in a fixed order: two solves of the same problem must agree bit
+    for bit. A stale hand-off would show up as run-to-run differences."""
+    prob = make_problem(K=40, max_per_pair=40, outliers=0.02, seed=11)
+    a = gpu_solve(prob, 3, 60, [1, 1, 1])
+    b = gpu_solve(prob, 3, 60, [1, 1, 1])
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert a[3] == b[3]
+
+
+def test_many_images_multipass_finisher():
+    """More than 2 x 256 images: the PCG finisher takes its multi-pass path (rows do not fit the
+    register-resident form); one GN step with a few PCG iterations tracks the oracle tightly."""
+    prob = make_problem(K=560, stride=1, max_per_pair=4, outliers=0.0, drift=(0.05, 0.002))
+    g, o = gpu_solve(prob, 1, 5, [1]), oracle_solve(prob, 1, 5, [1])
+    assert g[3]["pcgIterations"] == o[3]["pcgIterations"] == 5
+    assert_parity(g, o, rot_tol=2e-5, trans_tol=2e-5, energy_rtol=1e-4)
