@@ -591,6 +591,28 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
     }
 }
 
+// ---- divisions whose result only feeds an integer ------------------------------------------------
+// f2i(num / den + m + 0.5f) and roundf(num / den) with the quotient of the reference's IEEE division.
+// The quotient is first formed as num * rcp(den) (v_rcp_f32, 1 ulp): |q_approx - q| <= 2^-22 |q|.
+// The integer outcome is a step function of the quotient, monotone through the remaining rounded
+// additions, so it can only differ when a step (an integer for f2i, a half-integer for roundf) lies
+// within that bound plus the rounding of the later additions. Such lanes (~1e-4 of them), and
+// non-finite quotients, redo the IEEE division: the result is bit-identical to the plain code.
+__device__ __forceinline__ int proj_coord(float num, float den, float m) {
+    const float qa = num * __builtin_amdgcn_rcpf(den);
+    float t = (qa + m) + 0.5f;
+    const float eps = (fabsf(qa) + 2.0f * fabsf(t) + 2.0f) * 0x1p-21f;
+    if (!(fabsf(t - rintf(t)) > eps)) t = (num / den + m) + 0.5f;
+    return f2i(t);
+}
+__device__ __forceinline__ float round_quot(float num, float den, float rden) {
+    float q = num * rden;
+    const float aq = fabsf(q);
+    const float eps = (aq + 1.0f) * 0x1p-21f;
+    if (!(fabsf((aq - floorf(aq)) - 0.5f) > eps)) q = num / den;
+    return roundf(q);
+}
+
 // Voxel update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:486-514), weightUpdate = 1.
 __device__ __forceinline__ void voxel_integrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
     const float wUpd = 1.0f;
@@ -610,12 +632,10 @@ __device__ __forceinline__ void voxel_deintegrate(float& s0, float& w0, uint32_t
     const float wUpd = 1.0f;
     const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
     const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
-    float r0 = (oc0 * w0 - cu0 * wUpd) / (w0 - wUpd);
-    float r1 = (oc1 * w0 - cu1 * wUpd) / (w0 - wUpd);
-    float r2 = (oc2 * w0 - cu2 * wUpd) / (w0 - wUpd);
-    r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
-    r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
-    r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
+    const float den = w0 - wUpd, rden = __builtin_amdgcn_rcpf(den);
+    float r0 = fmaxf(0.0f, fminf(round_quot(oc0 * w0 - cu0 * wUpd, den, rden), 254.5f));
+    float r1 = fmaxf(0.0f, fminf(round_quot(oc1 * w0 - cu1 * wUpd, den, rden), 254.5f));
+    float r2 = fmaxf(0.0f, fminf(round_quot(oc2 * w0 - cu2 * wUpd, den, rden), 254.5f));
     col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
     s0 = (s0 * w0 - sdf * wUpd) / (w0 - wUpd);
     w0 = fmaxf(0.0f, w0 - wUpd);
@@ -627,9 +647,7 @@ __device__ __forceinline__ void voxel_deintegrate(float& s0, float& w0, uint32_t
 __device__ __forceinline__ uint32_t voxel_pixel(const BFDepthCameraParams& cam, const BFMat4& Tinv, int x, int y, int z,
                                                 float voxelSize, bool haveColor, float& pz) {
     const f3 pf = xform(Tinv, vvox_to_world(x, y, z, voxelSize));
-    const float sx = pf.x * cam.fx / pf.z + cam.mx;
-    const float sy = pf.y * cam.fy / pf.z + cam.my;
-    const uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
+    const uint32_t ux = (uint32_t)proj_coord(pf.x * cam.fx, pf.z, cam.mx), uy = (uint32_t)proj_coord(pf.y * cam.fy, pf.z, cam.my);
     pz = pf.z;
     return (ux < cam.imageWidth && uy < cam.imageHeight && haveColor) ? uy * cam.imageWidth + ux : 0xFFFFFFFFu;
 }
@@ -670,9 +688,8 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
         for (int zi = 0; zi < ZC; zi++) {
             const int z = z0 + zi;
             const f3 pf = xform(Tinv, vvox_to_world(bx, by, bz + z, A.voxelSize));
-            const float sx = pf.x * cam.fx / pf.z + cam.mx;
-            const float sy = pf.y * cam.fy / pf.z + cam.my;
-            const uint32_t ux = (uint32_t)f2i(sx + 0.5f), uy = (uint32_t)f2i(sy + 0.5f);
+            const uint32_t ux = (uint32_t)proj_coord(pf.x * cam.fx, pf.z, cam.mx);
+            const uint32_t uy = (uint32_t)proj_coord(pf.y * cam.fy, pf.z, cam.my);
             const bool on = ux < W && uy < H && colorImg != nullptr;  // colour NULL: no update (:441-448)
             pix[zi] = on ? uy * W + ux : 0xFFFFFFFFu;
             pz[zi] = pf.z;
@@ -724,12 +741,10 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
                 nsdf = (sdf * wUpd + s0 * w0) / (wUpd + w0);
                 nw = fminf(A.weightMax, wUpd + w0);
             } else {
-                r0 = (oc0 * w0 - cu0 * wUpd) / (w0 - wUpd);
-                r1 = (oc1 * w0 - cu1 * wUpd) / (w0 - wUpd);
-                r2 = (oc2 * w0 - cu2 * wUpd) / (w0 - wUpd);
-                r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
-                r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
-                r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
+                const float den = w0 - wUpd, rden = __builtin_amdgcn_rcpf(den);
+                r0 = fmaxf(0.0f, fminf(round_quot(oc0 * w0 - cu0 * wUpd, den, rden), 254.5f));
+                r1 = fmaxf(0.0f, fminf(round_quot(oc1 * w0 - cu1 * wUpd, den, rden), 254.5f));
+                r2 = fmaxf(0.0f, fminf(round_quot(oc2 * w0 - cu2 * wUpd, den, rden), 254.5f));
                 ncol = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
                 nsdf = (s0 * w0 - sdf * wUpd) / (w0 - wUpd);
                 nw = fmaxf(0.0f, w0 - wUpd);
