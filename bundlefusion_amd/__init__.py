@@ -173,6 +173,17 @@ class SceneRepHashSDF:
         check(lib().bf_scene_reintegrate(self.h, abi.mat(Told), abi.mat(Tnew), depth.ptr,
                                          color.ptr if color is not None else None, C.byref(cam)))
 
+    def apply_ops(self, ops, cam: BFDepthCameraParams):
+        """A sequence of (T, depth, color, deintegrate) voxel ops as one pass (bf_scene_apply_ops):
+        the scene equals the one the sequential integrate / deIntegrate calls produce."""
+        arr = (abi.BFVoxelOp * max(1, len(ops)))()
+        for k, (T, depth, color, deint) in enumerate(ops):
+            arr[k].T = abi.mat(T)
+            arr[k].depth = depth.ptr
+            arr[k].color = color.ptr if color is not None else None
+            arr[k].deintegrate = 1 if deint else 0
+        check(lib().bf_scene_apply_ops(self.h, arr, len(ops), C.byref(cam)))
+
     def garbageCollect(self):
         check(lib().bf_scene_garbage_collect(self.h))
 

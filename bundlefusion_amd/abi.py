@@ -155,6 +155,14 @@ class BFSolveResult(C.Structure):
                 ("numDensePairs", C.c_uint32), ("error", C.c_uint32)]
 
 
+class BFVoxelOp(C.Structure):  # include/bf/bf.h
+    _fields_ = [("T", C.c_float * 16), ("depth", C.c_void_p), ("color", C.c_void_p), ("deintegrate", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+MAX_VOXEL_OPS = 20
+
+
 class BFFixOp(C.Structure):
     _fields_ = [("kind", C.c_int32), ("frame", C.c_uint32), ("oldT", C.c_float * 16), ("newT", C.c_float * 16)]
 

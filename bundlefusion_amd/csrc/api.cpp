@@ -244,6 +244,15 @@ int bf_scene_reintegrate(bf_scene* s, const float Told[16], const float Tnew[16]
     s->scene->reintegrate(to_mat(Told), to_mat(Tnew), depth, color, *cam);
     BF_CATCH
 }
+int bf_scene_apply_ops(bf_scene* s, const BFVoxelOp* ops, uint32_t n, const BFDepthCameraParams* cam) {
+    BF_TRY
+    BF_REQUIRE(s && cam && (ops || n == 0), BF_ERR_ARG, "null argument");
+    BF_REQUIRE(n <= BF_MAX_VOXEL_OPS && n <= Scene::kMaxOps, BF_ERR_ARG, "too many ops");
+    VoxelOp v[BF_MAX_VOXEL_OPS];
+    for (uint32_t k = 0; k < n; k++) v[k] = VoxelOp{to_mat(ops[k].T), ops[k].depth, ops[k].color, ops[k].deintegrate != 0};
+    s->scene->applyOps(v, n, *cam);
+    BF_CATCH
+}
 int bf_scene_garbage_collect(bf_scene* s) {
     BF_TRY
     BF_REQUIRE(s, BF_ERR_ARG, "null scene");

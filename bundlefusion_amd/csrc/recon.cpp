@@ -1,6 +1,8 @@
 // recon.cpp — see recon.h.
 #include "recon.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstring>
 #include <limits>
@@ -35,6 +37,7 @@ T* pinned(size_t n) {
 Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCameraParams& cam, const BFReconOptions& o)
     : opt_(o), cam_(cam) {
     opt_.submapSize = or_default(o.submapSize, 10u);
+    if (const char* e = std::getenv("BF_BATCH_FIXES")) batchFixes_ = e[0] != '0';
     opt_.maxFrameFixes = or_default(o.maxFrameFixes, 10u);
     opt_.topNActive = or_default(o.topNActive, 30u);
     opt_.localNonLin = or_default(o.localNonLin, 2u);
@@ -68,6 +71,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     if (opt_.enableTiming) {
         scene_->integrateClock().enable(true);
         scene_->reintegrateClock().enable(true);
+        scene_->applyClock().enable(true);
         local_->solveClock().enable(true);
         global_->solveClock().enable(true);
     }
@@ -171,29 +175,42 @@ void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
     log_.push_back(e);
 }
 
-// reintegrate() (DepthSensing.cpp:854-902)
+// reintegrate() (DepthSensing.cpp:854-902). The frame's fixes are applied as one op batch
+// (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls), or, with
+// BF_BATCH_FIXES=0, one scene pass per fix.
 void Recon::runReintegrate() {
     tm_->nextFixes(opt_.maxFrameFixes, ops_);
+    std::vector<VoxelOp>& batch = batch_;
+    batch.clear();
     for (const FixOp& op : ops_) {
         const FrameRef& fr = frames_[op.frame];
         BF_REQUIRE(fr.set, BF_ERR_STATE, "re-integration of a frame that is not in the frame store");
-        if (op.kind == FixKind::ReIntegrate) {  // deIntegrate(old) + integrate(new), one fused voxel pass
-            scene_->reintegrate(op.oldT, op.newT, fr.depth, fr.color, cam_);
+        if (op.kind == FixKind::ReIntegrate) {  // deIntegrate(old) + integrate(new)
+            if (batchFixes_) {
+                batch.push_back(VoxelOp{op.oldT, fr.depth, fr.color, true});
+                batch.push_back(VoxelOp{op.newT, fr.depth, fr.color, false});
+            } else {
+                scene_->reintegrate(op.oldT, op.newT, fr.depth, fr.color, cam_);
+            }
             logOp(1, op.frame, &op.oldT);
             logOp(2, op.frame, &op.newT);
             st_.deintegrations++;
             st_.integrations++;
         } else if (op.kind == FixKind::DeIntegrate) {
-            scene_->integrate(op.oldT, fr.depth, fr.color, cam_, true, nullptr);
+            if (batchFixes_) batch.push_back(VoxelOp{op.oldT, fr.depth, fr.color, true});
+            else scene_->integrate(op.oldT, fr.depth, fr.color, cam_, true, nullptr);
             logOp(1, op.frame, &op.oldT);
             st_.deintegrations++;
         } else if (op.kind == FixKind::Integrate) {
-            scene_->integrate(op.newT, fr.depth, fr.color, cam_, false, nullptr);
+            if (batchFixes_) batch.push_back(VoxelOp{op.newT, fr.depth, fr.color, false});
+            else scene_->integrate(op.newT, fr.depth, fr.color, cam_, false, nullptr);
             logOp(2, op.frame, &op.newT);
             st_.integrations++;
         }
         st_.fixOps++;
     }
+    for (size_t k = 0; k < batch.size(); k += Scene::kMaxOps)
+        scene_->applyOps(batch.data() + k, (uint32_t)std::min<size_t>(Scene::kMaxOps, batch.size() - k), cam_);
     scene_->garbageCollect();
     logOp(4, 0, nullptr);
 }
@@ -403,8 +420,8 @@ BFReconStats Recon::stats() {
     if (opt_.enableTiming) {
         s.integrateKernelMs = scene_->integrateClock().totalMs();
         s.integrateLaunches = scene_->integrateClock().launches();
-        s.reintegrateKernelMs = scene_->reintegrateClock().totalMs();
-        s.reintegrateLaunches = scene_->reintegrateClock().launches();
+        s.reintegrateKernelMs = scene_->reintegrateClock().totalMs() + scene_->applyClock().totalMs();
+        s.reintegrateLaunches = scene_->reintegrateClock().launches() + scene_->applyClock().launches();
         s.localSolveMs = local_->solveClock().totalMs();
         s.globalSolveMs = global_->solveClock().totalMs();
     }
@@ -417,6 +434,7 @@ void Recon::resetStats() {
     scene_->resetStats();
     scene_->integrateClock().reset();
     scene_->reintegrateClock().reset();
+    scene_->applyClock().reset();
     local_->solveClock().reset();
     global_->solveClock().reset();
 }

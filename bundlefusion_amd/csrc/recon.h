@@ -99,6 +99,8 @@ private:
     std::vector<char> localKnown_;
     std::vector<BFMat4> complete_;
     std::vector<FixOp> ops_;
+    std::vector<VoxelOp> batch_;
+    bool batchFixes_ = true;  // BF_BATCH_FIXES=0: one scene pass per fix (A/B and debugging)
     uint32_t lastSubmapEnqueued_ = 0xFFFFFFFFu;
     uint32_t numFrames_ = 0;
 

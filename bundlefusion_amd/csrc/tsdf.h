@@ -47,8 +47,18 @@ struct SceneConfig {
     float shardChunk;        // ownership chunk edge in metres (default 1 m, the streaming chunk)
 };
 
+// One voxel op of a batch: integrate (deint = false) or de-integrate one frame at pose T (camera ->
+// world); depth / color are device pointers (float / uchar4 per pixel).
+struct VoxelOp {
+    BFMat4 T;
+    const float* depth;
+    const uint8_t* color;
+    bool deint;
+};
+
 class Scene {
 public:
+    static constexpr uint32_t kMaxOps = 20;  // a frame's fixes: <= 10 re-integrations, 2 voxel ops each
     Scene(const SceneConfig& cfg, hipStream_t stream);
     ~Scene();
 
@@ -61,6 +71,13 @@ public:
     // voxel pass (identical voxel results to the two calls)
     void reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* depth, const uint8_t* color,
                      const BFDepthCameraParams& cam);
+    // a sequence of integrate / de-integrate ops (reintegrate(), DepthSensing.cpp:854-902) as ONE
+    // voxel pass: alloc for every integrate op, one compactify scan with a per-block op mask, and
+    // a kernel that applies the ops to each voxel in sequence order (one read, one write). Voxel
+    // values equal the sequential calls; `visible` is the frustum list of the last op, as the
+    // reference's garbageCollect after the loop sees it.
+    void applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& cam);
+    KernelClock& applyClock() { return applyClock_; }  // k_apply_ops launches
     void garbageCollect();
     void compactify(const BFMat4& T, const BFDepthCameraParams& cam);
 
@@ -128,6 +145,12 @@ private:
     KernelClock integrateClock_;
     KernelClock reintegrateClock_;
     KernelClock renderClock_;
+    DevBuf<uint32_t> blockMask_;  // per work-list entry of an op batch: which ops may update it
+    DevBuf<uint32_t> blockBirth_;  // per heap block: epoch << 8 | (255 - first op) of the batch that allocated it
+    DevBuf<uint8_t> candOp_;       // per alloc candidate of a batch: the integrate op that emitted it
+    uint32_t batchEpoch_ = 0;
+    KernelClock applyClock_;
+    unsigned applyGrid_ = 0;
     DevBuf<uint8_t> blockFlags_;  // per work-list entry of a fused re-integration: bit 0 de-integrate, bit 1 integrate
     unsigned reintegrateGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat

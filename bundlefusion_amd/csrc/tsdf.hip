@@ -56,6 +56,23 @@ struct HashArgs {
     BFInt3 streamMinGridPos;
 };
 
+// Sequence of voxel ops (integrate / de-integrate one depth map at one pose) applied as one pass
+// (Scene::applyOps). Passed by value as a kernel argument: 3x4 matrices, image pointers, op kinds.
+struct OpTable {
+    float tinv[Scene::kMaxOps][12];  // world -> camera, rows 0-2
+    float t[Scene::kMaxOps][12];     // camera -> world (alloc DDA)
+    const float* depth[Scene::kMaxOps];
+    const uint32_t* color[Scene::kMaxOps];
+    uint8_t intIdx[Scene::kMaxOps];  // op index of the i-th integrate op
+    uint32_t n, deintMask, nInt, tileStride;
+};
+__host__ __device__ __forceinline__ BFMat4 op_mat(const float* m) {
+    BFMat4 r;
+    for (int i = 0; i < 12; i++) r.m[i] = m[i];
+    r.m[12] = 0.0f; r.m[13] = 0.0f; r.m[14] = 0.0f; r.m[15] = 1.0f;
+    return r;
+}
+
 __device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     unsigned l = lane_id();
@@ -198,7 +215,7 @@ __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned
 // block for |d - z| < truncation + truncScale * d to hold (1 cm slack for rounding). Exactness:
 // a rejected block has no voxel with an in-band sample, so skipping it changes no voxel.
 __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx, int by,
-                                 int bz) {
+                                 int bz, const float2* __restrict__ tiles) {
     const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
     const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
     float zlo = INFINITY, zhi = -INFINITY, xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
@@ -222,7 +239,7 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
     float dlo = INFINITY, dhi = -INFINITY;
     for (int ty = ty0; ty <= ty1; ty++)
         for (int tx = tx0; tx <= tx1; tx++) {
-            const float2 t = A.tiles[ty * A.tilesW + tx];
+            const float2 t = tiles[ty * A.tilesW + tx];
             dlo = fminf(dlo, t.x);
             dhi = fmaxf(dhi, t.y);
         }
@@ -235,9 +252,10 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
 
 // allocKernel, CUDASceneRepHashSDF.cu:165-251: per-pixel DDA over 8^3-block cells. Emits the
 // absent, in-frustum, owned blocks (deduplicated per tile in LDS) into `cand`.
-__global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* __restrict__ depthImg,
-                                                       BFDepthCameraParams cam, BFMat4 T, BFMat4 Tinv,
-                                                       unsigned long long* __restrict__ cand, uint32_t candCap) {
+__device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __restrict__ depthImg,
+                                              const BFDepthCameraParams& cam, const BFMat4& T, const BFMat4& Tinv,
+                                              unsigned long long* __restrict__ cand, uint32_t candCap,
+                                              uint8_t* __restrict__ candOp = nullptr, uint8_t opIdx = 0) {
     __shared__ unsigned long long set[LDS_SET];
     for (int k = threadIdx.x; k < LDS_SET; k += blockDim.x) set[k] = EMPTY_KEY;
     __syncthreads();
@@ -298,7 +316,10 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
             if (!placed && block_in_frustum(cam, Tinv, id.x, id.y, id.z, A.voxelSize) && owned(A, id.x, id.y, id.z) &&
                 !streamed_out(A, id.x, id.y, id.z) && lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY) {
                 const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
-                if (k < candCap) cand[k] = key;
+                if (k < candCap) {
+                    cand[k] = key;
+                    if (candOp) candOp[k] = opIdx;
+                }
                 else atomicOr(&A.ctrl[C_ERR], 1u);
                 emitted++;
             }
@@ -336,13 +357,44 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
             uint32_t base = 0;
             if ((int)lane_id() == leader) base = atomicAdd(&A.ctrl[C_CAND], (uint32_t)__popcll(m));
             base = __shfl(base, leader);
-            if (base + rank < candCap) cand[base + rank] = key;
+            if (base + rank < candCap) {
+                cand[base + rank] = key;
+                if (candOp) candOp[base + rank] = opIdx;
+            }
             else atomicOr(&A.ctrl[C_ERR], 1u);
             emitted++;
         }
     }
     const bool inImage = x < cam.imageWidth && y < cam.imageHeight;
     flush_stats2(A.stats, S_CAND, emitted, S_PIXELS, inImage ? 1ull : 0ull);
+}
+__global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* __restrict__ depthImg,
+                                                       BFDepthCameraParams cam, BFMat4 T, BFMat4 Tinv,
+                                                       unsigned long long* __restrict__ cand, uint32_t candCap) {
+    alloc_collect(A, depthImg, cam, T, Tinv, cand, candCap);
+}
+// batched: blockIdx.z selects the integrate op of the table (all ops' candidates land in one list;
+// the global dedup of k_alloc_insert removes blocks several ops want)
+__global__ __launch_bounds__(256) void k_alloc_collect_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops,
+                                                           unsigned long long* __restrict__ cand, uint32_t candCap,
+                                                           uint8_t* __restrict__ candOp) {
+    const uint32_t k = ops.intIdx[blockIdx.z];
+    alloc_collect(A, ops.depth[k], cam, op_mat(ops.t[k]), op_mat(ops.tinv[k]), cand, candCap, candOp, (uint8_t)k);
+}
+// In the sequential reference a block allocated for integrate op j does not exist for the ops
+// before j. Every candidate was absent when the batch started (the collect pass reads the hash
+// before any insert), so after the inserts each one records, per block, the earliest op that asked
+// for it: birth = epoch << 8 | (255 - op), kept by atomicMax (newest epoch, then smallest op).
+__global__ __launch_bounds__(256) void k_alloc_birth(HashArgs A, const unsigned long long* __restrict__ cand,
+                                                     const uint8_t* __restrict__ candOp, uint32_t candCap, uint32_t* birth,
+                                                     uint32_t epoch) {
+    const uint32_t n = min(A.ctrl[C_CAND], candCap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const i3 b = key_block(cand[i]);
+        const int ptr = lookup_ptr(A, b.x, b.y, b.z);
+        if (ptr == BF_FREE_ENTRY) continue;  // not inserted (hash / heap full: flagged in ctrl)
+        atomicMax(&birth[(uint32_t)ptr / BF_VOXELS_PER_BLOCK], (epoch << 8) | (255u - candOp[i]));
+    }
 }
 
 __device__ void alloc_overflow_serial(const HashArgs& A, const unsigned long long* ovf);
@@ -547,11 +599,11 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
         const bool inFr = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
-        bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z);
+        bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z, A.tiles);
         uint8_t fl = 0;
         if (MODE == CM_REINT) {
             const bool inOld = alloc && block_in_frustum(cam, TinvOld, bp.x, bp.y, bp.z, A.voxelSize) &&
-                               block_may_update(A, cam, TinvOld, bp.x, bp.y, bp.z);
+                               block_may_update(A, cam, TinvOld, bp.x, bp.y, bp.z, A.tiles);
             fl = (uint8_t)((inOld ? 1 : 0) | (inb ? 2 : 0));
             inb = fl != 0;
         }
@@ -856,6 +908,195 @@ __global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __
     flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
 }
 
+// ---- op batches (Scene::applyOps) ---------------------------------------------------------------
+// per-op 8x8-tile depth bounds (blockIdx.y = op) + the per-batch counter reset
+__global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigned long long* stats, OpTable ops, uint32_t W,
+                                                         uint32_t H, uint32_t tilesW, uint32_t tilesH, float maxDist,
+                                                         float2* tiles) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        ctrl[C_VISIBLE] = 0;
+        ctrl[C_BAND] = 0;
+        ctrl[C_CAND] = 0;
+        ctrl[C_OVF] = 0;
+        stats[S_OPS] += ops.n;
+    }
+    const uint32_t lane = lane_id();
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (t >= tilesW * tilesH) return;
+    const float* depthImg = ops.depth[blockIdx.y];
+    const uint32_t x = (t % tilesW) * DEPTH_TILE + (lane & 7), y = (t / tilesW) * DEPTH_TILE + (lane >> 3);
+    float lo = INFINITY, hi = -INFINITY;
+    if (x < W && y < H) {
+        const float d = depthImg[y * W + x];
+        if (d != -INFINITY && d < maxDist) { lo = d; hi = d; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off));
+        hi = fmaxf(hi, __shfl_xor(hi, off));
+    }
+    if (lane == 0) tiles[(size_t)blockIdx.y * ops.tileStride + t] = make_float2(lo, hi);
+}
+
+// One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
+// list garbageCollect walks), work list = blocks some op may update, with the op bit mask. Also
+// releases the batch's alloc dedup-set slots.
+__global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
+                                                        const int* __restrict__ candSlot, unsigned long long* candSet,
+                                                        uint32_t* masks, const uint32_t* __restrict__ birth, uint32_t epoch) {
+    {
+        const uint32_t n = min(A.ctrl[C_CAND], candCap);
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+            const int sl = candSlot[i];
+            if (sl >= 0) candSet[sl] = EMPTY_KEY;
+        }
+    }
+    __shared__ uint32_t s_cnt[2][4], s_base[2];
+    const uint32_t hw = A.ctrl[C_HIGHWATER];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const BFMat4 TinvLast = op_mat(ops.tinv[ops.n - 1]);
+    unsigned long long scanned = 0, vis = 0, band = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < hw; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        int4 bp = make_int4(0, 0, 0, 0);
+        if (i < hw) bp = A.blockPos[i];
+        const bool alloc = bp.w != 0;
+        const bool keepVis = alloc && block_in_frustum(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
+        uint32_t mask = 0;
+        if (alloc) {
+            const uint32_t bi = birth[i];
+            // a block born in this batch at op j exists for ops j.. only (ops before it see no block)
+            const uint32_t first = (bi >> 8) == epoch ? 255u - (bi & 255u) : 0u;
+            for (uint32_t k = first; k < ops.n; k++) {
+                const BFMat4 Ti = op_mat(ops.tinv[k]);
+                if (block_in_frustum(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
+                    block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, A.tiles + (size_t)k * ops.tileStride))
+                    mask |= 1u << k;
+            }
+        }
+        const bool inb = mask != 0;
+        const unsigned long long m0 = __ballot(keepVis), m1 = __ballot(inb);
+        if (lane == 0) {
+            s_cnt[0][wv] = (uint32_t)__popcll(m0);
+            s_cnt[1][wv] = (uint32_t)__popcll(m1);
+        }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            const uint32_t tot = s_cnt[threadIdx.x][0] + s_cnt[threadIdx.x][1] + s_cnt[threadIdx.x][2] + s_cnt[threadIdx.x][3];
+            s_base[threadIdx.x] = tot ? atomicAdd(&A.ctrl[threadIdx.x == 0 ? C_VISIBLE : C_BAND], tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t off0 = s_base[0], off1 = s_base[1];
+        for (uint32_t k = 0; k < wv; k++) {
+            off0 += s_cnt[0][k];
+            off1 += s_cnt[1][k];
+        }
+        const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
+        if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
+        if (inb) {
+            const uint32_t k = off1 + __popcll(m1 & lanemask_lt());
+            A.band[k] = ent;
+            masks[k] = mask;
+        }
+        scanned += alloc ? 1 : 0;
+        vis += keepVis ? 1 : 0;
+        band += inb ? 1 : 0;
+        __syncthreads();
+    }
+    flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
+    __syncthreads();
+    flush_stats2(A.stats, S_BAND, band, -1, 0);
+}
+
+// The batch's voxel pass: one wave per work-list block, lane = (x, y), ZC z-slices per round. For
+// each op of the block's mask, in sequence order: project, gather depth, band test, then the
+// integrate / de-integrate update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:420-521) on
+// the register copy of the voxel. A voxel is loaded when the first op reaches it and stored once.
+template <int ZC>
+__global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops,
+                                                   const uint32_t* __restrict__ masks) {
+    const uint32_t nlist = A.ctrl[C_BAND];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int lx = lane & 7, ly = lane >> 3;
+    unsigned long long updated = 0, rmw = 0;
+    for (uint32_t b = wave; b < nlist; b += nwaves) {
+        const int4 e = A.band[b];
+        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
+        const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
+        int dcount = 0;
+        uint32_t nupd = 0, nrmw = 0;
+#pragma unroll
+        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
+            float vs[ZC], vw[ZC], w0[ZC];
+            uint32_t vc[ZC];
+            uint32_t loaded = 0;
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) { vs[zi] = 0.0f; vw[zi] = 0.0f; w0[zi] = 0.0f; vc[zi] = 0u; }
+            for (uint32_t mk = mask; mk; mk &= mk - 1) {
+                const uint32_t k = (uint32_t)__builtin_ctz(mk);
+                const BFMat4 Ti = op_mat(ops.tinv[k]);
+                const float* depthImg = ops.depth[k];
+                const uint32_t* colorImg = ops.color[k];
+                const bool deint = (ops.deintMask >> k) & 1u;
+                float d[ZC], pz[ZC];
+                uint32_t pix[ZC];
+#pragma unroll
+                for (int zi = 0; zi < ZC; zi++) {
+                    pix[zi] = voxel_pixel(cam, Ti, bx, by, bz + z0 + zi, A.voxelSize, colorImg != nullptr, pz[zi]);
+                    d[zi] = pix[zi] != 0xFFFFFFFFu ? depthImg[pix[zi]] : -INFINITY;
+                }
+                float sd[ZC];
+                uint32_t cc[ZC];
+                uint32_t in = 0;
+#pragma unroll
+                for (int zi = 0; zi < ZC; zi++) {
+                    cc[zi] = 0u;
+                    if (voxel_in_band(A, d[zi], pz[zi], sd[zi])) {
+                        in |= 1u << zi;
+                        cc[zi] = colorImg[pix[zi]];
+                        if (!((loaded >> zi) & 1u)) {
+                            const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane));
+                            vs[zi] = __uint_as_float(v.a);
+                            vw[zi] = __uint_as_float(v.b);
+                            vc[zi] = v.c;
+                            w0[zi] = vw[zi];
+                        }
+                    }
+                }
+                loaded |= in;
+#pragma unroll
+                for (int zi = 0; zi < ZC; zi++) {
+                    if (!((in >> zi) & 1u)) continue;
+                    if (deint) voxel_deintegrate(vs[zi], vw[zi], vc[zi], sd[zi], cc[zi]);
+                    else voxel_integrate(vs[zi], vw[zi], vc[zi], sd[zi], cc[zi], A.weightMax);
+                    nupd++;
+                }
+            }
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) {
+                if (!((loaded >> zi) & 1u)) continue;
+                Vox3 nv;
+                nv.a = __float_as_uint(vs[zi]);
+                nv.b = __float_as_uint(vw[zi]);
+                nv.c = vc[zi];
+                *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane)) = nv;
+                dcount += (int)(vw[zi] >= 1.0f) - (int)(w0[zi] >= 1.0f);
+                nrmw++;
+            }
+        }
+        const unsigned long long anyChange = __ballot(dcount != 0);
+        if (anyChange) {
+            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
+            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
+        }
+        updated += nupd;
+        rmw += nrmw;
+    }
+    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
+}
+
 // garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
 // classification deleteHashEntryElement (VoxelUtilHashSDF.h:739-826) needs: a victim sitting in
 // its bucket with offset == 0 is deleted without the bucket lock; every other victim touches
@@ -1041,6 +1282,9 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     visible_.alloc(B_);
     band_.alloc(B_);
     blockFlags_.alloc(B_);
+    blockMask_.alloc(B_);
+    blockBirth_.alloc(B_);
+    candOp_.alloc(cfg_.candCapacity);
     ctrl_.alloc(C_COUNT);
     stats_.alloc(STAT_SLOTS * 16);
     cand_.alloc(cfg_.candCapacity);
@@ -1074,10 +1318,14 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int occR = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occR, k_reintegrate<4>, 256, 0));
     reintegrateGrid_ = (unsigned)std::max(1, occR) * (unsigned)numCUs_;
+    int occA = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4>, 256, 0));
+    applyGrid_ = (unsigned)std::max(1, occA) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(blockFlags_.p, 0, blockFlags_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
     float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     std::memcpy(T_.m, I, 64);
@@ -1089,7 +1337,7 @@ Scene::~Scene() {}
 
 size_t Scene::deviceBytes() const {
     return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
-           blockFlags_.bytes() +
+           blockFlags_.bytes() + blockMask_.bytes() + blockBirth_.bytes() + candOp_.bytes() +
            tiles_.bytes() + ctrl_.bytes() +
            stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
            gcList_.bytes() + blockCount_.bytes();
@@ -1215,6 +1463,64 @@ void Scene::reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* dep
                           reinterpret_cast<const uint32_t*>(color), cam, TinvOld, Tinv_, blockFlags_.p);
     BF_LAUNCH_CHECK();
     if (timed) reintegrateClock_.commit();
+}
+
+// reintegrate() (DepthSensing.cpp:854-902) fixes of one frame as one pass: see tsdf.h
+void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& cam) {
+    if (n == 0) return;
+    BF_REQUIRE(n <= kMaxOps, BF_ERR_ARG, "too many ops in one batch");
+    OpTable tab;
+    std::memset(&tab, 0, sizeof(tab));
+    tab.n = n;
+    for (uint32_t k = 0; k < n; k++) {
+        BF_REQUIRE(ops[k].depth != nullptr, BF_ERR_ARG, "depth is null");
+        const BFMat4 Ti = mat4_inverse(ops[k].T);
+        std::memcpy(tab.tinv[k], Ti.m, 48);
+        std::memcpy(tab.t[k], ops[k].T.m, 48);
+        tab.depth[k] = ops[k].depth;
+        tab.color[k] = reinterpret_cast<const uint32_t*>(ops[k].color);
+        if (ops[k].deint) tab.deintMask |= 1u << k;
+        else tab.intIdx[tab.nInt++] = (uint8_t)k;
+    }
+    const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
+    if ((size_t)tw * th * kMaxOps > tilesCap_) {
+        tiles_.alloc((size_t)tw * th * kMaxOps);
+        tilesCap_ = tw * th * kMaxOps;
+    }
+    tab.tileStride = tw * th;
+    k_begin_ops_tiles<<<dim3(div_up((size_t)tw * th * 64, 256), n), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p);
+    BF_LAUNCH_CHECK();
+    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
+    if (++batchEpoch_ >= (1u << 24)) {  // birth stamps are epoch << 8: restart the epochs before they wrap
+        BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
+        batchEpoch_ = 1;
+    }
+    const uint32_t epoch = batchEpoch_;
+    if (tab.nInt) {
+        dim3 g(div_up(cam.imageWidth, ALLOC_TILE), div_up(cam.imageHeight, ALLOC_TILE), tab.nInt);
+        k_alloc_collect_ops<<<g, 256, 0, stream_>>>(A, cam, tab, cand_.p, cfg_.candCapacity, candOp_.p);
+        BF_LAUNCH_CHECK();
+        k_alloc_insert<<<64, 256, 0, stream_>>>(A, cand_.p, cfg_.candCapacity, candSet_.p, candSetMask_, candSlot_.p, ovf_.p);
+        BF_LAUNCH_CHECK();
+        k_alloc_birth<<<(unsigned)numCUs_, 256, 0, stream_>>>(A, cand_.p, candOp_.p, cfg_.candCapacity, blockBirth_.p, epoch);
+        BF_LAUNCH_CHECK();
+    }
+    A.band = band_.p;
+    A.tiles = tiles_.p;
+    A.tilesW = tw;
+    A.tilesH = th;
+    k_compactify_ops<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
+                                                                  blockMask_.p, blockBirth_.p, epoch);
+    BF_LAUNCH_CHECK();
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    const bool timed = applyClock_.enabled();
+    if (timed) applyClock_.slot(ev0, ev1);
+    hipExtLaunchKernelGGL(k_apply_ops<4>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    BF_LAUNCH_CHECK();
+    if (timed) applyClock_.commit();
+    T_ = ops[n - 1].T;
+    Tinv_ = mat4_inverse(T_);
 }
 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)

@@ -68,13 +68,28 @@ int bf_scene_integrate(bf_scene* s, const float T[16], const float* depth, const
                        const BFDepthCameraParams* cam, const uint32_t* bitMask);
 int bf_scene_deintegrate(bf_scene* s, const float T[16], const float* depth, const uint8_t* color,
                          const BFDepthCameraParams* cam, const uint32_t* bitMask);
-/* garbageCollect (CUDASceneRepHashSDF.h:110-126 -> garbageCollectIdentifyCUDA,
- * resetHashBucketMutexCUDA, garbageCollectFreeCUDA, CUDASceneRepHashSDF.cu:113,633,671) */
 /* One re-integration fix (DepthSensing.cpp:890-895): bf_scene_deintegrate(Told) followed by
  * bf_scene_integrate(Tnew) of the same frame, fused into one voxel pass; the resulting scene is
  * identical to the two calls. */
 int bf_scene_reintegrate(bf_scene* s, const float Told[16], const float Tnew[16], const float* depth, const uint8_t* color,
                          const BFDepthCameraParams* cam);
+/* A frame's re-integration fixes (reintegrate(), DepthSensing.cpp:854-902, the loop body's
+ * deIntegrate / integrate calls): n <= BF_MAX_VOXEL_OPS ops, each de-integrating (deintegrate != 0)
+ * or integrating one frame at pose T (camera -> world), applied in order as ONE voxel pass. Voxel
+ * values and the allocated block set equal those of the sequence of bf_scene_deintegrate /
+ * bf_scene_integrate calls; the visible list afterwards is the last op's frustum list (what the
+ * reference's garbageCollect after the loop walks). */
+#define BF_MAX_VOXEL_OPS 20
+typedef struct BFVoxelOp {
+    float T[16];
+    const float* depth;   /* device, W*H float */
+    const uint8_t* color; /* device, W*H uchar4 */
+    uint32_t deintegrate;
+    uint32_t reserved;
+} BFVoxelOp;
+int bf_scene_apply_ops(bf_scene* s, const BFVoxelOp* ops, uint32_t n, const BFDepthCameraParams* cam);
+/* garbageCollect (CUDASceneRepHashSDF.h:110-126 -> garbageCollectIdentifyCUDA,
+ * resetHashBucketMutexCUDA, garbageCollectFreeCUDA, CUDASceneRepHashSDF.cu:113,633,671) */
 int bf_scene_garbage_collect(bf_scene* s);
 /* setLastRigidTransformAndCompactify (CUDASceneRepHashSDF.h:136-139); nVisible may be NULL
  * (otherwise this call synchronizes to read it back) */

@@ -181,6 +181,88 @@ def test_fused_reintegrate_parity(scene, shift):
     assert pair.gpu.errorFlags() == 0
 
 
+def _perturbed(T, rng, shift, rot_deg=0.0):
+    T2 = T.copy()
+    T2[:3, 3] += rng.normal(size=3) * shift
+    if rot_deg:
+        w = rng.normal(size=3)
+        w *= np.deg2rad(rot_deg) / np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+        th = np.linalg.norm(w)
+        R = np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+        T2[:3, :3] = (R @ T2[:3, :3].astype(np.float64)).astype(np.float32)
+    return T2.astype(np.float32)
+
+
+@pytest.mark.parametrize("shift", [0.004, 0.05])
+def test_op_batch_parity(scene, shift):
+    """Scene::applyOps (a frame's fixes as one voxel pass: per-block op masks, voxels loaded once and
+    updated in op order) == the same integrate / deIntegrate calls one by one in the oracle, then GC
+    on both (the GC list is the last op's frustum list in both). Mixed batch: re-integrations of
+    several frames (de-integrate + integrate), a de-integration only, an integration of a frame that
+    was not in the volume, and two ops touching the same frame twice."""
+    cam = small_cam()
+    p = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 17, num_blocks=1 << 16)
+    pair = Pair(p, cam)
+    frames = render_frames(scene, cam, [0, 4, 8, 12, 16, 20])
+    for k in range(5):
+        T, d, c = frames[k]
+        pair.integrate(k, T, d, c)
+    pair.gc()
+    rng = np.random.default_rng(11)
+    cur = {k: frames[k][0] for k in range(5)}
+    for rnd in range(2):
+        ops = []
+        for k in (1, 3, 0):  # re-integrations
+            T2 = _perturbed(cur[k], rng, shift, rot_deg=0.3)
+            ops += [(cur[k], k, True), (T2, k, False)]
+            cur[k] = T2
+        if rnd == 0:
+            ops.append((cur[4], 4, True))       # de-integration only
+            del cur[4]
+            ops.append((frames[5][0], 5, False))  # integration of a new frame
+            cur[5] = frames[5][0]
+        else:
+            T2 = _perturbed(cur[5], rng, shift)
+            ops += [(cur[5], 5, True), (T2, 5, False)]
+            cur[5] = T2
+        dev = []
+        for T, k, deint in ops:
+            dd, cc = pair._upload(k, frames[k][1], frames[k][2])
+            dev.append((T, dd, cc, deint))
+            pair.ora.integrate(T, frames[k][1], frames[k][2], cam, deintegrate=deint)
+        pair.gpu.apply_ops(dev, cam)
+        assert pair.compare() > 1000
+        pair.gc()
+        pair.compare()
+    assert pair.gpu.errorFlags() == 0
+
+
+def test_op_batch_full_resolution(scene):
+    """A full 10-fix batch (20 ops) at 640x480 / 4 mm against the oracle."""
+    cam = bfa.depth_camera(640, 480)
+    p = bfa.hash_params(voxel_size=0.004, num_buckets=1 << 20, num_blocks=1 << 18)
+    pair = Pair(p, cam)
+    ids = list(range(0, 40, 4))
+    frames = render_frames(scene, cam, ids)
+    for k, (T, d, c) in enumerate(frames):
+        pair.integrate(k, T, d, c)
+    rng = np.random.default_rng(5)
+    ops = []
+    for k, (T, d, c) in enumerate(frames):
+        T2 = _perturbed(T, rng, 0.01, rot_deg=0.2)
+        ops += [(T, k, True), (T2, k, False)]
+    dev = []
+    for T, k, deint in ops:
+        dd, cc = pair._upload(k, frames[k][1], frames[k][2])
+        dev.append((T, dd, cc, deint))
+        pair.ora.integrate(T, frames[k][1], frames[k][2], cam, deintegrate=deint)
+    pair.gpu.apply_ops(dev, cam)
+    pair.gc()
+    assert pair.compare() > 10000
+    assert pair.gpu.errorFlags() == 0
+
+
 def test_chunk_sharding_partitions_the_scene(scene):
     """Multi-GPU TSDF sharding: scenes with shardCount 2, shardIndex 0 / 1 fed the
     same frames own disjoint block sets whose union — blocks and voxel payload — is the unsharded
