@@ -12,11 +12,13 @@ Multi-GPU (torchrun, one process per GPU): the TSDF is sharded by 1 m chunk owne
 bundle adjustment is replicated on every rank (deterministic inputs, identical solves), so there
 is no data-path collective. The host-side barrier / max-over-ranks uses gloo.
 
-roofline: the dominant kernel role is the voxel update pass (k_integrate for new frames and
-integrate-only fixes, k_reintegrate for a fix's fused de-integration + integration); its launches
-are timed with dispatch-stamped HIP events on the scene stream inside the timed region; algorithmic
-bytes per launch = 16 B per work-list block + 24 B per voxel read-modify-written (12 B read + 12 B
-write) + 8 B per pixel (depth + colour read once), from the device counters of the same launches.
+roofline: the dominant kernel is k_apply_ops, the op-batch voxel pass that applies a frame's
+re-integration fixes (up to 10 de-integrate + integrate pairs) with one read and one write per
+voxel; its launches are timed with dispatch-stamped HIP events on the scene stream inside the timed
+region; algorithmic bytes per launch = 20 B per work-list block (entry + op mask) + 24 B per voxel
+read + written + 8 B per pixel per op (depth + colour read once), from the device counters of the
+same launches. The kernel is VALU-issue bound (projection + band test of every voxel for every op
+of its block); roofline.valu reports that bound from the SQ_INSTS_VALU pass of the same command.
 cpu_baseline: the CPU oracle (oracle/, serial C++ restatement) timed on a bounded sample of the
 same workload on this host, scaled by the GPU run's op counts to frames/s.
 """
@@ -35,6 +37,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
+VALU_PEAK_WAVE_INSTS_PER_US = 256 * 4 * 2400 / 4
 
 
 def log(*a):
@@ -158,7 +162,7 @@ def main():
     ap.add_argument("--buckets", type=int, default=1 << 23)
     ap.add_argument("--blocks", type=int, default=1 << 21)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_update_pass_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r02_apply_pass_pmc.json"),
                     help="JSON with per-launch HBM bytes of k_integrate from the PMC passes of "
                          "tools/profile_bench.sh on this same command (committed under profiles/)")
     args = ap.parse_args()
@@ -213,20 +217,27 @@ def main():
     ss = rc.scene_stats()
     frames = S * args.steps
     P = args.width * args.height
-    # the voxel-update passes: k_integrate (new frames, integrate-only fixes) and k_reintegrate
-    # (a fix's de-integration + integration fused into one pass); together they are the dominant
-    # kernel role. Algorithmic bytes from the device counters of the same launches.
-    launches = max(1, st["integrateLaunches"] + st["reintegrateLaunches"])
-    kernel_ms = st["integrateKernelMs"] + st["reintegrateKernelMs"]
-    alg_bytes = 16 * ss["bandBlocks"] + 24 * ss["voxelsRMW"] + 8 * P * launches
+    # dominant kernel: k_apply_ops, the op-batch voxel pass that applies a frame's re-integration
+    # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Algorithmic bytes per
+    # launch from the device counters of the same launches: 20 B per work-list block (16 B entry +
+    # 4 B op mask), 24 B per voxel read + written, 8 B per pixel per op (depth + colour read once).
+    launches = max(1, st["reintegrateLaunches"])
+    kernel_ms = st["reintegrateKernelMs"]
+    alg_bytes = 20 * ss["batchBlocks"] + 24 * ss["batchVoxelsRMW"] + 8 * P * ss["batchOps"]
     per_launch_bytes = alg_bytes / launches
     per_launch_s = kernel_ms / 1e3 / launches
     achieved = per_launch_bytes / per_launch_s / 1e9
     traffic = None
+    valu = None
     if args.traffic and os.path.exists(args.traffic):
         tj = json.load(open(args.traffic))
         traffic = tj.get("bytes_per_launch", tj.get("k_integrate_bytes_per_launch"))
         traffic_src = os.path.relpath(args.traffic, REPO)
+        if "valu_insts_per_launch" in tj:  # VALU-issue bound of the same kernel (SQ_INSTS_VALU pass)
+            us = per_launch_s * 1e6
+            valu = {"wave_insts_per_launch": tj["valu_insts_per_launch"],
+                    "peak_wave_insts_per_us": VALU_PEAK_WAVE_INSTS_PER_US,
+                    "frac": tj["valu_insts_per_launch"] / (us * VALU_PEAK_WAVE_INSTS_PER_US), "source": traffic_src}
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
     solo = global_solve_timing(stream, min(K, args.warmup + args.steps))
@@ -251,26 +262,27 @@ def main():
                    "parallelism": f"tsdf-chunk-shard{world}+ba-replicated" if world > 1 else "single"},
         "ms_per_gn_iter": solo["ms_per_gn_iter"],
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
-        "roofline": {"bound": "hbm", "kernel": "k_integrate+k_reintegrate (voxel update passes)", "achieved": achieved,
+        "roofline": {"bound": "hbm", "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src if traffic is not None else None,
                      "launches": launches, "avg_launch_us": per_launch_s * 1e6,
+                     "alg_bytes_per_launch": per_launch_bytes,
+                     "per_launch": {"work_list_blocks": ss["batchBlocks"] / launches,
+                                    "voxels_rmw": ss["batchVoxelsRMW"] / launches,
+                                    "voxel_op_updates": ss["batchUpdates"] / launches,
+                                    "ops": ss["batchOps"] / launches},
+                     "valu": valu,
                      "k_integrate": {"launches": st["integrateLaunches"],
-                                     "avg_us": st["integrateKernelMs"] * 1e3 / max(1, st["integrateLaunches"])},
-                     "k_reintegrate": {"launches": st["reintegrateLaunches"],
-                                       "avg_us": st["reintegrateKernelMs"] * 1e3 / max(1, st["reintegrateLaunches"])},
-                     "alg_bytes_per_launch": per_launch_bytes},
+                                     "avg_us": st["integrateKernelMs"] * 1e3 / max(1, st["integrateLaunches"])}},
         "loop": {"ops_per_frame": (st["integrations"] + st["deintegrations"]) / max(1, st["frames"]),
                  "fix_ops": st["fixOps"], "local_solves": st["localSolves"], "global_solves": st["globalSolves"],
                  "global_gn_iters": st["globalGnIterations"], "global_pcg_iters": st["globalPcgIterations"],
                  "removed_pairs": st["removedPairs"], "global_solve_ms": st["globalSolveMs"],
                  "local_solve_ms": st["localSolveMs"], "integrate_kernel_ms": st["integrateKernelMs"],
-                 "reintegrate_kernel_ms": st["reintegrateKernelMs"],
+                 "apply_kernel_ms": st["reintegrateKernelMs"],
                  "heap_free": rc.heap_free_count(),
-                 "per_pass": {"work_list_blocks": ss["bandBlocks"] / launches, "voxels_rmw": ss["voxelsRMW"] / launches,
-                              "voxel_updates": ss["voxelsUpdated"] / launches,
-                              "allocated_blocks_scanned_per_compactify": ss["scanned"] / max(1, ss["integrateOps"])}},
+                 "allocated_blocks_scanned_per_compactify": ss["scanned"] / max(1, ss["integrateOps"])},
     }
     # raycast (visualizeFrame's render, reported beside the metric): 20 renders from the last pose
     W_, H_ = args.width, args.height

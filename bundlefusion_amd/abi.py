@@ -82,7 +82,8 @@ class BFRayCastParams(C.Structure):
 class BFTsdfStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",
-        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks", "voxelsRMW")]
+        "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks", "voxelsRMW",
+        "batchOps", "batchBlocks", "batchVoxelsRMW", "batchUpdates")]
 
 
 class BFSceneOptions(C.Structure):

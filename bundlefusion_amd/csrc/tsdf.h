@@ -12,7 +12,8 @@
 //   band      int4[B]             the subset of `visible` whose voxels can reach the truncation band
 //                                 of the current depth map (conservative cull against per-8x8-tile
 //                                 depth bounds) — the list integrate walks
-//   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op
+//   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op(s)
+//   tiles2    float2[tiles2]      the same per 32x32 pixels (footprints wider than 2x2 tiles)
 //   flags     uint8[B]            fused re-integration: per work-list entry, which pose(s) update it
 //   ctrl      uint32[16]          device-resident counters (heap counter, visible count, ...)
 //   cand/candSet/candSlot/ovf     alloc scratch (per-op candidate list, global dedup set)
@@ -128,7 +129,10 @@ private:
     DevBuf<int4> visible_;
     DevBuf<int4> band_;
     DevBuf<float2> tiles_;
-    uint32_t tilesCap_ = 0;
+    size_t tilesCap_ = 0;
+    DevBuf<float2> tiles2_;  // 32x32-pixel depth bounds
+    size_t tiles2Cap_ = 0;
+    void ensureTiles(size_t fine, size_t coarse);
     DevBuf<uint32_t> ctrl_;
     DevBuf<unsigned long long> stats_;  // [64 slots][16]
     DevBuf<unsigned long long> cand_;

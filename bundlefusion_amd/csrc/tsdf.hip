@@ -43,6 +43,8 @@ struct HashArgs {
     int4* band;
     const float2* tiles;
     uint32_t tilesW, tilesH;
+    const float2* tiles2;  // 32x32-pixel depth bounds (footprints wider than 2x2 fine tiles)
+    uint32_t tiles2W;
     uint32_t* ctrl;
     unsigned long long* stats;  // [STAT_SLOTS][16] counters, field order of BFTsdfStats
     uint32_t numBuckets, numEntries, numBlocks, maxList;
@@ -64,7 +66,7 @@ struct OpTable {
     const float* depth[Scene::kMaxOps];
     const uint32_t* color[Scene::kMaxOps];
     uint8_t intIdx[Scene::kMaxOps];  // op index of the i-th integrate op
-    uint32_t n, deintMask, nInt, tileStride;
+    uint32_t n, deintMask, nInt, tileStride, tile2Stride;
 };
 __host__ __device__ __forceinline__ BFMat4 op_mat(const float* m) {
     BFMat4 r;
@@ -85,8 +87,9 @@ struct __attribute__((packed, aligned(4))) Vox3 {
 };
 
 enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS,
-                 S_BAND, S_RMW };
-constexpr int DEPTH_TILE = 8;  // 8x8-pixel depth-bound tiles for the band cull
+                 S_BAND, S_RMW, S_BOPS, S_BBLOCKS, S_BRMW, S_BUPD };
+constexpr int DEPTH_TILE = 8;    // 8x8-pixel depth-bound tiles for the band cull
+constexpr int DEPTH_TILE2 = 32;  // coarse level: 32x32 pixels
 constexpr int STAT_SLOTS = 64;
 
 // Workgroup-level counter flush: wave shuffle-reduce, LDS add, then one global atomic per
@@ -179,13 +182,49 @@ __global__ void k_begin_op(uint32_t* ctrl, unsigned long long* stats) {
     }
 }
 
-// Per-op counter reset fused with the depth-bound tiles of the band cull: one wave per 8x8 tile
-// reduces min / max over the depths integrate would accept (not -inf, below
-// maxIntegrationDistance, CUDASceneRepHashSDF.cu:450-457). Empty tiles get (+inf, -inf).
+// Depth-bound tiles of the band cull: min / max over the depths integrate would accept (not -inf,
+// below maxIntegrationDistance, CUDASceneRepHashSDF.cu:450-457); empty tiles get (+inf, -inf).
+// Wave t < nFine reduces one 8x8 tile, the next nCoarse waves one 32x32 tile each.
+__device__ __forceinline__ void depth_tile_wave(uint32_t t, const float* __restrict__ depthImg, uint32_t W, uint32_t H,
+                                                uint32_t tilesW, uint32_t tilesH, uint32_t tiles2W, uint32_t tiles2H,
+                                                float maxDist, float2* tiles, float2* tiles2) {
+    const uint32_t lane = lane_id();
+    const uint32_t nFine = tilesW * tilesH;
+    float lo = INFINITY, hi = -INFINITY;
+    if (t < nFine) {
+        const uint32_t x = (t % tilesW) * DEPTH_TILE + (lane & 7), y = (t / tilesW) * DEPTH_TILE + (lane >> 3);
+        if (x < W && y < H) {
+            const float d = depthImg[y * W + x];
+            if (d != -INFINITY && d < maxDist) { lo = d; hi = d; }
+        }
+    } else {
+        const uint32_t c = t - nFine;
+        if (c >= tiles2W * tiles2H) return;
+        const uint32_t x = (c % tiles2W) * DEPTH_TILE2 + (lane & 31), y0 = (c / tiles2W) * DEPTH_TILE2 + (lane >> 5);
+#pragma unroll
+        for (int i = 0; i < DEPTH_TILE2 / 2; i++) {
+            const uint32_t y = y0 + 2 * i;
+            if (x < W && y < H) {
+                const float d = depthImg[y * W + x];
+                if (d != -INFINITY && d < maxDist) { lo = fminf(lo, d); hi = fmaxf(hi, d); }
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off));
+        hi = fmaxf(hi, __shfl_xor(hi, off));
+    }
+    if (lane == 0) {
+        if (t < nFine) tiles[t] = make_float2(lo, hi);
+        else tiles2[t - nFine] = make_float2(lo, hi);
+    }
+}
+
+// Per-op counter reset fused with the depth-bound tiles of the op.
 __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned long long* stats,
                                                         const float* __restrict__ depthImg, uint32_t W, uint32_t H,
-                                                        uint32_t tilesW, uint32_t tilesH, float maxDist, float2* tiles,
-                                                        uint32_t nops) {
+                                                        uint32_t tilesW, uint32_t tilesH, uint32_t tiles2W, uint32_t tiles2H,
+                                                        float maxDist, float2* tiles, float2* tiles2, uint32_t nops) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
         ctrl[C_BAND] = 0;
@@ -193,29 +232,19 @@ __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned
         ctrl[C_OVF] = 0;
         stats[S_OPS] += nops;
     }
-    const uint32_t lane = lane_id();
-    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (t >= tilesW * tilesH) return;
-    const uint32_t x = (t % tilesW) * DEPTH_TILE + (lane & 7), y = (t / tilesW) * DEPTH_TILE + (lane >> 3);
-    float lo = INFINITY, hi = -INFINITY;
-    if (x < W && y < H) {
-        const float d = depthImg[y * W + x];
-        if (d != -INFINITY && d < maxDist) { lo = d; hi = d; }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        lo = fminf(lo, __shfl_xor(lo, off));
-        hi = fmaxf(hi, __shfl_xor(hi, off));
-    }
-    if (lane == 0) tiles[t] = make_float2(lo, hi);
+    depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, depthImg, W, H, tilesW, tilesH, tiles2W, tiles2H, maxDist,
+                    tiles, tiles2);
 }
 
 // Conservative test that a block may contain a voxel integrate will update: project the 8 voxel-
 // centre corners (convex hull -> bounding pixel rectangle, grown by one pixel), take the depth
 // bounds of the covered tiles and reject when every depth is too far behind or in front of the
 // block for |d - z| < truncation + truncScale * d to hold (1 cm slack for rounding). Exactness:
-// a rejected block has no voxel with an in-band sample, so skipping it changes no voxel.
+// a rejected block has no voxel with an in-band sample, so skipping it changes no voxel. The
+// corner projections use rcp (1 ulp, far inside the one-pixel growth); footprints within 2x2 fine
+// tiles read those 4 tiles, wider ones up to 3x3 coarse (32-pixel) tiles, all loads independent.
 __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx, int by,
-                                 int bz, const float2* __restrict__ tiles) {
+                                 int bz, const float2* __restrict__ tiles, const float2* __restrict__ tiles2) {
     const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
     const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
     float zlo = INFINITY, zhi = -INFINITY, xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
@@ -224,7 +253,8 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
         const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
         const f3 p = xform(Tinv, w);
         if (!(p.z > 1e-3f)) return true;  // straddles the camera plane: keep
-        const float sx = p.x * cam.fx / p.z + cam.mx, sy = p.y * cam.fy / p.z + cam.my;
+        const float rz = __builtin_amdgcn_rcpf(p.z);
+        const float sx = p.x * cam.fx * rz + cam.mx, sy = p.y * cam.fy * rz + cam.my;
         zlo = fminf(zlo, p.z); zhi = fmaxf(zhi, p.z);
         xlo = fminf(xlo, sx); xhi = fmaxf(xhi, sx);
         ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
@@ -235,19 +265,52 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
     const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
     const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
     const int tx0 = x0 / DEPTH_TILE, tx1 = x1 / DEPTH_TILE, ty0 = y0 / DEPTH_TILE, ty1 = y1 / DEPTH_TILE;
-    if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > 64) return true;  // very close block: not worth the walk
-    float dlo = INFINITY, dhi = -INFINITY;
-    for (int ty = ty0; ty <= ty1; ty++)
-        for (int tx = tx0; tx <= tx1; tx++) {
-            const float2 t = tiles[ty * A.tilesW + tx];
-            dlo = fminf(dlo, t.x);
-            dhi = fmaxf(dhi, t.y);
-        }
+    float dlo, dhi;
+    if (tx1 - tx0 <= 1 && ty1 - ty0 <= 1) {
+        const float2 a = tiles[ty0 * A.tilesW + tx0], b = tiles[ty0 * A.tilesW + tx1];
+        const float2 c = tiles[ty1 * A.tilesW + tx0], d = tiles[ty1 * A.tilesW + tx1];
+        dlo = fminf(fminf(a.x, b.x), fminf(c.x, d.x));
+        dhi = fmaxf(fmaxf(a.y, b.y), fmaxf(c.y, d.y));
+    } else {
+        const int cx0 = x0 / DEPTH_TILE2, cx1 = x1 / DEPTH_TILE2, cy0 = y0 / DEPTH_TILE2, cy1 = y1 / DEPTH_TILE2;
+        if (cx1 - cx0 > 2 || cy1 - cy0 > 2) return true;  // very close block: keep
+        dlo = INFINITY;
+        dhi = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float2 t = tiles2[min(cy0 + j, cy1) * A.tiles2W + min(cx0 + i, cx1)];
+                dlo = fminf(dlo, t.x);
+                dhi = fmaxf(dhi, t.y);
+            }
+    }
     if (!(dlo <= dhi)) return false;  // no integrable depth under the block
     const float slack = 0.01f;
     if (dlo * (1.0f - A.truncScale) >= zhi + A.truncation + slack) return false;  // surface far behind
     if (dhi * (1.0f + A.truncScale) <= zlo - A.truncation - slack) return false;  // surface far in front
     return true;
+}
+
+// isSDFBlockInCameraFrustumApprox (VoxelUtilHashSDF.h:322-326, DepthCameraUtil.h:95-107) with the
+// five IEEE divisions replaced by rcp products. The test is a set of comparisons of monotone
+// quotients against +-1 / 0 / 1, so the fast result is taken when every compared value is farther
+// from its bound than the rcp error (<= 2^-20 relative, taken with a 4x margin); otherwise the exact
+// test decides. Identical outcome to block_in_frustum.
+__device__ __forceinline__ bool block_in_frustum_fast(const BFDepthCameraParams& c, const BFMat4& viewInv, int bx, int by,
+                                                      int bz, float voxelSize) {
+    const f3 w = block_to_world(bx, by, bz, voxelSize) + mk3(1.0f, 1.0f, 1.0f) * (voxelSize * 0.5f * (BF_SDF_BLOCK_SIZE - 1.0f));
+    const f3 pc = xform(viewInv, w);
+    const float rz = __builtin_amdgcn_rcpf(pc.z);
+    const float wm1 = (float)c.imageWidth - 1.0f, hm1 = (float)c.imageHeight - 1.0f;
+    const float px = pc.x * c.fx * rz + c.mx, py = pc.y * c.fy * rz + c.my;
+    const float x = (2.0f * px - wm1) * __builtin_amdgcn_rcpf(wm1) * 0.95f;
+    const float y = (hm1 - 2.0f * py) * __builtin_amdgcn_rcpf(hm1) * 0.95f;
+    const float z = (pc.z - c.sensorDepthWorldMin) * __builtin_amdgcn_rcpf(c.sensorDepthWorldMax - c.sensorDepthWorldMin) * 0.95f;
+    const float ex = (fabsf(x) + 4.0f) * 0x1p-18f, ey = (fabsf(y) + 4.0f) * 0x1p-18f, ez = (fabsf(z) + 1.0f) * 0x1p-18f;
+    const bool sure = fabsf(fabsf(x) - 1.0f) > ex && fabsf(fabsf(y) - 1.0f) > ey && fabsf(z - 1.0f) > ez && fabsf(z) > ez;
+    if (!sure) return block_in_frustum(c, viewInv, bx, by, bz, voxelSize);
+    return !(x < -1.0f || x > 1.0f || y < -1.0f || y > 1.0f || z < 0.0f || z > 1.0f);
 }
 
 // allocKernel, CUDASceneRepHashSDF.cu:165-251: per-pixel DDA over 8^3-block cells. Emits the
@@ -347,7 +410,7 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         bool want = false;
         if (key != EMPTY_KEY) {
             const i3 b = key_block(key);
-            want = block_in_frustum(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
+            want = block_in_frustum_fast(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
                    !streamed_out(A, b.x, b.y, b.z) && lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY;
         }
         const unsigned long long m = __ballot(want);
@@ -598,12 +661,12 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         int4 bp = make_int4(0, 0, 0, 0);
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
-        const bool inFr = alloc && block_in_frustum(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
-        bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z, A.tiles);
+        const bool inFr = alloc && block_in_frustum_fast(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
+        bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z, A.tiles, A.tiles2);
         uint8_t fl = 0;
         if (MODE == CM_REINT) {
-            const bool inOld = alloc && block_in_frustum(cam, TinvOld, bp.x, bp.y, bp.z, A.voxelSize) &&
-                               block_may_update(A, cam, TinvOld, bp.x, bp.y, bp.z, A.tiles);
+            const bool inOld = alloc && block_in_frustum_fast(cam, TinvOld, bp.x, bp.y, bp.z, A.voxelSize) &&
+                               block_may_update(A, cam, TinvOld, bp.x, bp.y, bp.z, A.tiles, A.tiles2);
             fl = (uint8_t)((inOld ? 1 : 0) | (inb ? 2 : 0));
             inb = fl != 0;
         }
@@ -650,18 +713,30 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
 // additions, so it can only differ when a step (an integer for f2i, a half-integer for roundf) lies
 // within that bound plus the rounding of the later additions. Such lanes (~1e-4 of them), and
 // non-finite quotients, redo the IEEE division: the result is bit-identical to the plain code.
+// The exact division runs only in waves where some lane needs it: the branch is taken on the wave's
+// ballot and holds an empty asm statement, so the compiler cannot if-convert (speculate) it.
 __device__ __forceinline__ int proj_coord(float num, float den, float m) {
     const float qa = num * __builtin_amdgcn_rcpf(den);
     float t = (qa + m) + 0.5f;
     const float eps = (fabsf(qa) + 2.0f * fabsf(t) + 2.0f) * 0x1p-21f;
-    if (!(fabsf(t - rintf(t)) > eps)) t = (num / den + m) + 0.5f;
+    const bool need = !(fabsf(t - rintf(t)) > eps);
+    if (__builtin_amdgcn_ballot_w64(need)) {
+        asm volatile("" ::: "memory");
+        const float te = (num / den + m) + 0.5f;
+        t = need ? te : t;
+    }
     return f2i(t);
 }
 __device__ __forceinline__ float round_quot(float num, float den, float rden) {
     float q = num * rden;
     const float aq = fabsf(q);
     const float eps = (aq + 1.0f) * 0x1p-21f;
-    if (!(fabsf((aq - floorf(aq)) - 0.5f) > eps)) q = num / den;
+    const bool need = !(fabsf((aq - floorf(aq)) - 0.5f) > eps);
+    if (__builtin_amdgcn_ballot_w64(need)) {
+        asm volatile("" ::: "memory");
+        const float e = num / den;
+        q = need ? e : q;
+    }
     return roundf(q);
 }
 
@@ -911,30 +986,18 @@ __global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __
 // ---- op batches (Scene::applyOps) ---------------------------------------------------------------
 // per-op 8x8-tile depth bounds (blockIdx.y = op) + the per-batch counter reset
 __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigned long long* stats, OpTable ops, uint32_t W,
-                                                         uint32_t H, uint32_t tilesW, uint32_t tilesH, float maxDist,
-                                                         float2* tiles) {
+                                                         uint32_t H, uint32_t tilesW, uint32_t tilesH, uint32_t tiles2W,
+                                                         uint32_t tiles2H, float maxDist, float2* tiles, float2* tiles2) {
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
         ctrl[C_BAND] = 0;
         ctrl[C_CAND] = 0;
         ctrl[C_OVF] = 0;
         stats[S_OPS] += ops.n;
+        stats[S_BOPS] += ops.n;
     }
-    const uint32_t lane = lane_id();
-    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (t >= tilesW * tilesH) return;
-    const float* depthImg = ops.depth[blockIdx.y];
-    const uint32_t x = (t % tilesW) * DEPTH_TILE + (lane & 7), y = (t / tilesW) * DEPTH_TILE + (lane >> 3);
-    float lo = INFINITY, hi = -INFINITY;
-    if (x < W && y < H) {
-        const float d = depthImg[y * W + x];
-        if (d != -INFINITY && d < maxDist) { lo = d; hi = d; }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        lo = fminf(lo, __shfl_xor(lo, off));
-        hi = fmaxf(hi, __shfl_xor(hi, off));
-    }
-    if (lane == 0) tiles[(size_t)blockIdx.y * ops.tileStride + t] = make_float2(lo, hi);
+    depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[blockIdx.y], W, H, tilesW, tilesH, tiles2W, tiles2H,
+                    maxDist, tiles + (size_t)blockIdx.y * ops.tileStride, tiles2 + (size_t)blockIdx.y * ops.tile2Stride);
 }
 
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
@@ -960,7 +1023,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         int4 bp = make_int4(0, 0, 0, 0);
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
-        const bool keepVis = alloc && block_in_frustum(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
+        const bool keepVis = alloc && block_in_frustum_fast(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
         uint32_t mask = 0;
         if (alloc) {
             const uint32_t bi = birth[i];
@@ -968,8 +1031,9 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             const uint32_t first = (bi >> 8) == epoch ? 255u - (bi & 255u) : 0u;
             for (uint32_t k = first; k < ops.n; k++) {
                 const BFMat4 Ti = op_mat(ops.tinv[k]);
-                if (block_in_frustum(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
-                    block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, A.tiles + (size_t)k * ops.tileStride))
+                if (block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
+                    block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, A.tiles + (size_t)k * ops.tileStride,
+                                     A.tiles2 + (size_t)k * ops.tile2Stride))
                     mask |= 1u << k;
             }
         }
@@ -1004,7 +1068,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
     }
     flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
     __syncthreads();
-    flush_stats2(A.stats, S_BAND, band, -1, 0);
+    flush_stats2(A.stats, S_BAND, band, S_BBLOCKS, band);
 }
 
 // The batch's voxel pass: one wave per work-list block, lane = (x, y), ZC z-slices per round. For
@@ -1095,6 +1159,8 @@ __global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraPara
         rmw += nrmw;
     }
     flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
+    __syncthreads();
+    flush_stats2(A.stats, S_BUPD, updated, S_BRMW, rmw);
 }
 
 // garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
@@ -1243,7 +1309,7 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
                           int4* vis, uint32_t* ctrl, unsigned long long* st, const uint32_t* bitMask) {
     HashArgs a;
     a.hash = hash; a.heap = heap; a.voxels = vox; a.blockPos = bp; a.blockCount = bc; a.visible = vis; a.ctrl = ctrl; a.stats = st;
-    a.band = nullptr; a.tiles = nullptr; a.tilesW = a.tilesH = 0;
+    a.band = nullptr; a.tiles = nullptr; a.tilesW = a.tilesH = 0; a.tiles2 = nullptr; a.tiles2W = 0;
     a.numBuckets = cfg.hp.hashNumBuckets;
     a.numEntries = cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE;
     a.numBlocks = cfg.hp.numSDFBlocks;
@@ -1338,7 +1404,7 @@ Scene::~Scene() {}
 size_t Scene::deviceBytes() const {
     return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
            blockFlags_.bytes() + blockMask_.bytes() + blockBirth_.bytes() + candOp_.bytes() +
-           tiles_.bytes() + ctrl_.bytes() +
+           tiles_.bytes() + tiles2_.bytes() + ctrl_.bytes() +
            stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
            gcList_.bytes() + blockCount_.bytes();
 }
@@ -1352,6 +1418,17 @@ void Scene::reset() {
     BF_LAUNCH_CHECK();
     BF_HIP(hipMemsetAsync(voxels_.p, 0, voxels_.bytes(), stream_));
     cfg_.hp.numOccupiedBlocks = 0;
+}
+
+void Scene::ensureTiles(size_t fine, size_t coarse) {
+    if (fine > tilesCap_) {
+        tiles_.alloc(fine);
+        tilesCap_ = fine;
+    }
+    if (coarse > tiles2Cap_) {
+        tiles2_.alloc(coarse);
+        tiles2Cap_ = coarse;
+    }
 }
 
 void Scene::beginOp() {
@@ -1388,12 +1465,11 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     T_ = T;
     Tinv_ = mat4_inverse(T);
     const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
-    if (tw * th > tilesCap_) {
-        tiles_.alloc((size_t)tw * th);
-        tilesCap_ = tw * th;
-    }
-    k_begin_op_tiles<<<div_up((size_t)tw * th * 64, 256), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p, 1u);
+    const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
+    ensureTiles(tw * th, tw2 * th2);
+    k_begin_op_tiles<<<div_up((size_t)(tw * th + tw2 * th2) * 64, 256), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tiles_.p,
+        tiles2_.p, 1u);
     BF_LAUNCH_CHECK();
     if (!deint) alloc(depth, cam, bitMask);
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
@@ -1401,6 +1477,8 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     A.tiles = tiles_.p;
     A.tilesW = tw;
     A.tilesH = th;
+    A.tiles2 = tiles2_.p;
+    A.tiles2W = tw2;
     const unsigned grid = (unsigned)numCUs_ * 4;
     k_compactify<CM_INTEGRATE><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p, nullptr,
                                                           Tinv_);
@@ -1437,18 +1515,19 @@ void Scene::reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* dep
     BF_REQUIRE(depth != nullptr, BF_ERR_ARG, "depth is null");
     const BFMat4 TinvOld = mat4_inverse(Told);
     const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
-    if (tw * th > tilesCap_) {
-        tiles_.alloc((size_t)tw * th);
-        tilesCap_ = tw * th;
-    }
-    k_begin_op_tiles<<<div_up((size_t)tw * th * 64, 256), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p, 2u);
+    const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
+    ensureTiles(tw * th, tw2 * th2);
+    k_begin_op_tiles<<<div_up((size_t)(tw * th + tw2 * th2) * 64, 256), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tiles_.p,
+        tiles2_.p, 2u);
     BF_LAUNCH_CHECK();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
     A.band = band_.p;
     A.tiles = tiles_.p;
     A.tilesW = tw;
     A.tilesH = th;
+    A.tiles2 = tiles2_.p;
+    A.tiles2W = tw2;
     const unsigned grid = (unsigned)numCUs_ * 4;
     T_ = Tnew;
     Tinv_ = mat4_inverse(Tnew);
@@ -1483,13 +1562,13 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
         else tab.intIdx[tab.nInt++] = (uint8_t)k;
     }
     const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
-    if ((size_t)tw * th * kMaxOps > tilesCap_) {
-        tiles_.alloc((size_t)tw * th * kMaxOps);
-        tilesCap_ = tw * th * kMaxOps;
-    }
+    const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
+    ensureTiles(tw * th * kMaxOps, tw2 * th2 * kMaxOps);
     tab.tileStride = tw * th;
-    k_begin_ops_tiles<<<dim3(div_up((size_t)tw * th * 64, 256), n), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, cfg_.hp.maxIntegrationDistance, tiles_.p);
+    tab.tile2Stride = tw2 * th2;
+    k_begin_ops_tiles<<<dim3(div_up((size_t)(tw * th + tw2 * th2) * 64, 256), n), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tiles_.p,
+        tiles2_.p);
     BF_LAUNCH_CHECK();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
     if (++batchEpoch_ >= (1u << 24)) {  // birth stamps are epoch << 8: restart the epochs before they wrap
@@ -1510,6 +1589,8 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     A.tiles = tiles_.p;
     A.tilesW = tw;
     A.tilesH = th;
+    A.tiles2 = tiles2_.p;
+    A.tiles2W = tw2;
     k_compactify_ops<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
                                                                   blockMask_.p, blockBirth_.p, epoch);
     BF_LAUNCH_CHECK();
@@ -1566,7 +1647,7 @@ BFTsdfStats Scene::stats() {
     for (int sl = 0; sl < STAT_SLOTS; sl++)
         for (int f = 0; f < 16; f++) sum[f] += h[sl * 16 + f];
     BFTsdfStats s;
-    static_assert(sizeof(BFTsdfStats) == 12 * 8, "stats layout");
+    static_assert(sizeof(BFTsdfStats) == 16 * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
     return s;
 }

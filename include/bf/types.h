@@ -142,6 +142,11 @@ typedef struct BFTsdfStats {
     uint64_t bandBlocks;      /* blocks on the voxel-update work lists (band-culled) */
     uint64_t voxelsRMW;       /* voxels read-modify-written by the update passes (a fused re-integration
                                  applies two updates to a voxel in one read + write) */
+    /* the op-batch pass alone (bf_scene_apply_ops / k_apply_ops), also counted in the totals above */
+    uint64_t batchOps;        /* voxel ops applied through batches */
+    uint64_t batchBlocks;     /* work-list blocks of the batch passes */
+    uint64_t batchVoxelsRMW;  /* voxels read + written once by a batch pass */
+    uint64_t batchUpdates;    /* voxel-op updates inside the truncation band applied by batch passes */
 } BFTsdfStats;
 
 #ifdef __cplusplus
