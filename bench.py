@@ -271,6 +271,7 @@ def main():
                      "per_launch": {"work_list_blocks": ss["batchBlocks"] / launches,
                                     "voxels_rmw": ss["batchVoxelsRMW"] / launches,
                                     "voxel_op_updates": ss["batchUpdates"] / launches,
+                                    "voxel_op_evaluations": ss["batchEvals"] / launches,
                                     "ops": ss["batchOps"] / launches},
                      "valu": valu,
                      "k_integrate": {"launches": st["integrateLaunches"],

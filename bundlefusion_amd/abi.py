@@ -83,7 +83,7 @@ class BFTsdfStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",
         "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks", "voxelsRMW",
-        "batchOps", "batchBlocks", "batchVoxelsRMW", "batchUpdates")]
+        "batchOps", "batchBlocks", "batchVoxelsRMW", "batchUpdates", "batchEvals")]
 
 
 class BFSceneOptions(C.Structure):

@@ -155,6 +155,7 @@ private:
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
     unsigned applyGrid_ = 0;
+    int applyZC_ = 4;
     DevBuf<uint8_t> blockFlags_;  // per work-list entry of a fused re-integration: bit 0 de-integrate, bit 1 integrate
     unsigned reintegrateGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat

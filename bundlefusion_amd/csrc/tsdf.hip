@@ -87,10 +87,11 @@ struct __attribute__((packed, aligned(4))) Vox3 {
 };
 
 enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS,
-                 S_BAND, S_RMW, S_BOPS, S_BBLOCKS, S_BRMW, S_BUPD };
+                 S_BAND, S_RMW, S_BOPS, S_BBLOCKS, S_BRMW, S_BUPD, S_BEVAL };
 constexpr int DEPTH_TILE = 8;    // 8x8-pixel depth-bound tiles for the band cull
 constexpr int DEPTH_TILE2 = 32;  // coarse level: 32x32 pixels
 constexpr int STAT_SLOTS = 64;
+constexpr int STAT_FIELDS = 32;  // counters per slot (BFTsdfStats uses the first sizeof/8)
 
 // Workgroup-level counter flush: wave shuffle-reduce, LDS add, then one global atomic per
 // workgroup into one of 64 slots (no single hot word; summed on the host at query time).
@@ -108,7 +109,7 @@ __device__ void flush_stats2(unsigned long long* stats, int f0, unsigned long lo
         if (v1) atomicAdd(&s_st[1], v1);
     }
     __syncthreads();
-    const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) % STAT_SLOTS) * 16;
+    const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) % STAT_SLOTS) * STAT_FIELDS;
     if (threadIdx.x == 0) {
         if (s_st[0]) atomicAdd(&stats[slot + f0], s_st[0]);
         if (s_st[1] && f1 >= 0) atomicAdd(&stats[slot + f1], s_st[1]);
@@ -1017,7 +1018,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
     const uint32_t hw = A.ctrl[C_HIGHWATER];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const BFMat4 TinvLast = op_mat(ops.tinv[ops.n - 1]);
-    unsigned long long scanned = 0, vis = 0, band = 0;
+    unsigned long long scanned = 0, vis = 0, band = 0, evals = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < hw; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         int4 bp = make_int4(0, 0, 0, 0);
@@ -1064,11 +1065,14 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         scanned += alloc ? 1 : 0;
         vis += keepVis ? 1 : 0;
         band += inb ? 1 : 0;
+        evals += (unsigned long long)__popc(mask);
         __syncthreads();
     }
     flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
     __syncthreads();
     flush_stats2(A.stats, S_BAND, band, S_BBLOCKS, band);
+    __syncthreads();
+    flush_stats2(A.stats, S_BEVAL, evals * BF_VOXELS_PER_BLOCK, -1, 0);
 }
 
 // The batch's voxel pass: one wave per work-list block, lane = (x, y), ZC z-slices per round. For
@@ -1352,7 +1356,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     blockBirth_.alloc(B_);
     candOp_.alloc(cfg_.candCapacity);
     ctrl_.alloc(C_COUNT);
-    stats_.alloc(STAT_SLOTS * 16);
+    stats_.alloc(STAT_SLOTS * STAT_FIELDS);
     cand_.alloc(cfg_.candCapacity);
     candSet_.alloc(setSize);
     candSlot_.alloc(cfg_.candCapacity);
@@ -1385,7 +1389,12 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occR, k_reintegrate<4>, 256, 0));
     reintegrateGrid_ = (unsigned)std::max(1, occR) * (unsigned)numCUs_;
     int occA = 0;
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4>, 256, 0));
+    const char* azEnv = std::getenv("BF_APPLY_ZC");  // tuning knob: z-slices per round of k_apply_ops
+    applyZC_ = azEnv ? std::atoi(azEnv) : 4;
+    if (applyZC_ != 2 && applyZC_ != 8) applyZC_ = 4;
+    if (applyZC_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<2>, 256, 0));
+    else if (applyZC_ == 8) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<8>, 256, 0));
+    else BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4>, 256, 0));
     applyGrid_ = (unsigned)std::max(1, occA) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
@@ -1597,7 +1606,12 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    hipExtLaunchKernelGGL(k_apply_ops<4>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    if (applyZC_ == 2)
+        hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    else if (applyZC_ == 8)
+        hipExtLaunchKernelGGL(k_apply_ops<8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    else
+        hipExtLaunchKernelGGL(k_apply_ops<4>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;
@@ -1640,14 +1654,14 @@ uint32_t Scene::errorFlags() {
 }
 
 BFTsdfStats Scene::stats() {
-    std::vector<unsigned long long> h(STAT_SLOTS * 16);
+    std::vector<unsigned long long> h(STAT_SLOTS * STAT_FIELDS);
     BF_HIP(hipMemcpyAsync(h.data(), stats_.p, stats_.bytes(), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
-    uint64_t sum[16] = {0};
+    uint64_t sum[STAT_FIELDS] = {0};
     for (int sl = 0; sl < STAT_SLOTS; sl++)
-        for (int f = 0; f < 16; f++) sum[f] += h[sl * 16 + f];
+        for (int f = 0; f < STAT_FIELDS; f++) sum[f] += h[sl * STAT_FIELDS + f];
     BFTsdfStats s;
-    static_assert(sizeof(BFTsdfStats) == 16 * 8, "stats layout");
+    static_assert(sizeof(BFTsdfStats) == 17 * 8 && sizeof(BFTsdfStats) <= STAT_FIELDS * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
     return s;
 }

@@ -147,6 +147,7 @@ typedef struct BFTsdfStats {
     uint64_t batchBlocks;     /* work-list blocks of the batch passes */
     uint64_t batchVoxelsRMW;  /* voxels read + written once by a batch pass */
     uint64_t batchUpdates;    /* voxel-op updates inside the truncation band applied by batch passes */
+    uint64_t batchEvals;      /* voxel-op evaluations (projection + band test) of the batch passes */
 } BFTsdfStats;
 
 #ifdef __cplusplus
