@@ -96,11 +96,13 @@ private:
     uint32_t maxPairs_;
     int numCUs_;
     uint32_t maxTiles_;
+    unsigned pcgLoopCap_ = 0;  // workgroups of the persistent PCG loop (0: per-iteration launches)
     size_t maxChunks_;
     DevBuf<int> rowCount_, rowStart_, rowLen_;
     DevBuf<int> tileCnt_, rowChunk_, chunkRow_;
     DevBuf<float4> chunkPart_;
     DevBuf<unsigned long long> probe_;
+    DevBuf<uint32_t> sync_;  // grid hand-off counters / flags (64 B apart)
     DevBuf<int> rowTmp_, rowIdx_;
     DevBuf<float4> entries_;
     DevBuf<float> vec_;     // [N][8] per field

@@ -34,7 +34,8 @@ enum VecField { V_DELTA = 0, V_R, V_Z, V_P, V_AP, V_M, V_NUM };
 enum CtrlWord {
     K_TICKET = 0, K_PCG_DONE, K_GN_DONE, K_GN_ITERS, K_PCG_ITERS, K_RDOTZ, K_NPAIRS, K_LAST_W,
     K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J, K_COUNT = 16,
-    K_NCHUNK = K_COUNT, K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
+    K_NCHUNK = K_COUNT,
+    K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
 };
 
 struct BA {
@@ -48,6 +49,7 @@ struct BA {
     int *rowChunk, *chunkRow;  // chunks of row v: [rowChunk[v], rowChunk[v+1]); chunk -> row
     float4* chunkPart;         // [chunk][3] per-chunk partial sums
     unsigned long long* probe; // development timing probe (BF_BA_PROBE=1), else null
+    uint32_t* sync;            // k_pcg_loop: 8 shard counters + top counter + 8 flag replicas, 64 B apart
     float4* entries;
     float* vec;
     float* img;
@@ -129,6 +131,29 @@ __device__ __forceinline__ uint32_t ticket_add(uint32_t* p) {
     return __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// vector fields through write-through (WT) or plain accesses
+template <bool WT>
+__device__ __forceinline__ void vload_t(const BA& a, int field, uint32_t v, f3& r, f3& t) {
+    if (WT) {
+        const float4* p = reinterpret_cast<const float4*>(vptr(a, field, v));
+        const float4 x = ld_wt(p), y = ld_wt(p + 1);
+        r = mk3(x.x, x.y, x.z);
+        t = mk3(y.x, y.y, y.z);
+    } else {
+        vload(a, field, v, r, t);
+    }
+}
+template <bool WT>
+__device__ __forceinline__ void vstore_t(const BA& a, int field, uint32_t v, f3 r, f3 t) {
+    if (WT) {
+        float4* p = reinterpret_cast<float4*>(vptr(a, field, v));
+        st_wt(p, make_float4(r.x, r.y, r.z, 0.0f));
+        st_wt(p + 1, make_float4(t.x, t.y, t.z, 0.0f));
+    } else {
+        vstore(a, field, v, r, t);
+    }
+}
+
 // "Last workgroup" hand-off: every wave drains its write-through stores, one lane takes a ticket;
 // the workgroup holding the last ticket continues (and reads the hand-off with ld_wt).
 __device__ bool last_block(uint32_t* ticket) {
@@ -136,6 +161,28 @@ __device__ bool last_block(uint32_t* ticket) {
     drain_stores();
     __syncthreads();
     if (threadIdx.x == 0) isLast = (ticket_add(ticket) == gridDim.x * gridDim.y - 1) ? 1 : 0;
+    __syncthreads();
+    return isLast != 0;
+}
+
+// Two-level arrival for grid-wide hand-offs with many workgroups (MI355X_MICROARCH.md: one counter
+// with hundreds of arrivers serialises at ~11 ns per atomic): workgroups are split into 8 shards by
+// blockIdx % 8 (the dispatcher's round-robin XCD: a placement guess for speed only, correctness does
+// not depend on it); a shard's last arriver adds to the top counter. Counters grow monotonically
+// within a launch, so round `epoch` (1-based) completes at epoch * arrivers.
+constexpr int SYNC_LINE = 16;  // words per 64-B line
+constexpr int SYNC_TOP = 8 * SYNC_LINE, SYNC_FLAG = 9 * SYNC_LINE, SYNC_WORDS = 17 * SYNC_LINE;
+__device__ bool last_block_sharded(uint32_t* sync, uint32_t epoch) {
+    __shared__ int isLast;
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t G = gridDim.x, sh = blockIdx.x & 7u;
+        const uint32_t ns = (G + 7u - sh) / 8u, nShards = G < 8u ? G : 8u;
+        int last = 0;
+        if (ticket_add(&sync[sh * SYNC_LINE]) == epoch * ns - 1u) last = ticket_add(&sync[SYNC_TOP]) == epoch * nShards - 1u;
+        isLast = last;
+    }
     __syncthreads();
     return isLast != 0;
 }
@@ -473,7 +520,45 @@ __global__ __launch_bounds__(WG) void k_init(BA a, float wSparse) {
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(s);
         a.ctrl[K_TICKET] = 0;
+        for (int w = 0; w < SYNC_WORDS; w += SYNC_LINE) a.sync[w] = 0;  // k_pcg_loop's counters and flags
         vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
+    }
+}
+
+// sparse JtJp partial of every chunk (one wave per chunk), handed over write-through
+template <bool WT>
+__device__ __forceinline__ void pcg_sparse_chunks(const BA& a, float wSparse, uint32_t wave, uint32_t nw, uint32_t nch) {
+    const uint32_t lane = lane_id();
+    for (uint32_t c = wave; c < nch; c += nw) {
+        uint32_t v;
+        int k0, k1;
+        chunk_range(a, c, v, k0, k1);
+        f3 pRv, pTv;
+        vload_t<WT>(a, V_P, v, pRv, pTv);
+        float ar[3] = {0, 0, 0}, at[3] = {0, 0, 0};
+        // all CH/64 entries of this lane are loaded before any is used (clamped indices, masked
+        // sums: no per-entry branch), so a chunk costs one HBM round trip plus one L2 gather
+        float4 A[CPL], B[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            const int k = min(k0 + (int)lane + 64 * u, k1 - 1);
+            A[u] = a.entries[2 * k];
+            B[u] = a.entries[2 * k + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; u++) {
+            const f3 Ps = mk3(A[u].x, A[u].y, A[u].z), Po = mk3(B[u].x, B[u].y, B[u].z);
+            const uint32_t o = __float_as_uint(A[u].w);
+            f3 pRo, pTo;
+            vload_t<WT>(a, V_P, o, pRo, pTo);
+            f3 g = (cross3(pRv, Ps) + pTv - (cross3(pRo, Po) + pTo)) * wSparse;
+            f3 cr = cross3(Ps, g);
+            if (k0 + (int)lane + 64 * u >= k1) { g = mk3(0, 0, 0); cr = g; }
+            ar[0] += cr.x; ar[1] += cr.y; ar[2] += cr.z;
+            at[0] += g.x; at[1] += g.y; at[2] += g.z;
+        }
+        for (int q = 0; q < 3; q++) { ar[q] = wave_sum(ar[q]); at[q] = wave_sum(at[q]); }
+        if (lane == 0) { put_part(a, c, 0, mk3(ar[0], ar[1], ar[2])); put_part(a, c, 1, mk3(at[0], at[1], at[2])); }
     }
 }
 
@@ -514,7 +599,7 @@ __device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, in
 // PCG finisher with each thread's R rows held in registers: all loads issue up front, then the
 // two block reductions, then the stores (z and Ap never go to memory). Same arithmetic as the
 // multi-pass form below.
-template <int R>
+template <int R, bool WT>
 __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, bool& lastOut) {
     f3 pR[R], pT[R], aR[R], aT[R], dR[R], dT[R], rR[R], rT[R], mR[R], mT[R];
     float d = 0.0f;
@@ -522,16 +607,16 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
     for (int q = 0; q < R; q++) {
         const uint32_t v = 1 + threadIdx.x + q * WG;
         if (v < a.N) {
-            vload(a, V_P, v, pR[q], pT[q]);
-            vload(a, V_DELTA, v, dR[q], dT[q]);
-            vload(a, V_R, v, rR[q], rT[q]);
-            vload(a, V_M, v, mR[q], mT[q]);
+            vload_t<WT>(a, V_P, v, pR[q], pT[q]);
+            vload_t<WT>(a, V_DELTA, v, dR[q], dT[q]);
+            vload_t<WT>(a, V_R, v, rR[q], rT[q]);
+            vload_t<WT>(a, V_M, v, mR[q], mT[q]);
             pcg_ap(a, v, nch, useDense, pR[q], pT[q], aR[q], aT[q]);
             d += dot3(pR[q], aR[q]) + dot3(pT[q], aT[q]);
         }
     }
     const float pAp = block_sum(d, sh);
-    const float rDotzOld = ctrlf(a.ctrl, K_RDOTZ);
+    const float rDotzOld = WT ? __uint_as_float(ld_wt(&a.ctrl[K_RDOTZ])) : ctrlf(a.ctrl, K_RDOTZ);
     const float alpha = (pAp > FLOAT_EPSILON) ? rDotzOld / pAp : 0.0f;
     float b = 0.0f;
 #pragma unroll
@@ -553,9 +638,9 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
     for (int q = 0; q < R; q++) {
         const uint32_t v = 1 + threadIdx.x + q * WG;
         if (v < a.N) {
-            vstore(a, V_DELTA, v, dR[q], dT[q]);
-            vstore(a, V_R, v, rR[q], rT[q]);
-            vstore(a, V_P, v, mR[q] + beta * pR[q], mT[q] + beta * pT[q]);
+            vstore_t<WT>(a, V_DELTA, v, dR[q], dT[q]);
+            vstore_t<WT>(a, V_R, v, rR[q], rT[q]);
+            vstore_t<WT>(a, V_P, v, mR[q] + beta * pR[q], mT[q] + beta * pT[q]);
             if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
                 f3 nr, nt;
                 lie_update(dR[q], dT[q], mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
@@ -582,37 +667,7 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
     const unsigned long long tStart = a.probe ? wall_clock64() : 0ull;
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
-    for (uint32_t c = wave; c < nch; c += nw) {
-        uint32_t v;
-        int k0, k1;
-        chunk_range(a, c, v, k0, k1);
-        f3 pRv, pTv;
-        vload(a, V_P, v, pRv, pTv);
-        float ar[3] = {0, 0, 0}, at[3] = {0, 0, 0};
-        // all CH/64 entries of this lane are loaded before any is used (clamped indices, masked
-        // sums: no per-entry branch), so a chunk costs one HBM round trip plus one L2 gather
-        float4 A[CPL], B[CPL];
-#pragma unroll
-        for (int u = 0; u < CPL; u++) {
-            const int k = min(k0 + (int)lane + 64 * u, k1 - 1);
-            A[u] = a.entries[2 * k];
-            B[u] = a.entries[2 * k + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < CPL; u++) {
-            const f3 Ps = mk3(A[u].x, A[u].y, A[u].z), Po = mk3(B[u].x, B[u].y, B[u].z);
-            const uint32_t o = __float_as_uint(A[u].w);
-            f3 pRo, pTo;
-            vload(a, V_P, o, pRo, pTo);
-            f3 g = (cross3(pRv, Ps) + pTv - (cross3(pRo, Po) + pTo)) * wSparse;
-            f3 cr = cross3(Ps, g);
-            if (k0 + (int)lane + 64 * u >= k1) { g = mk3(0, 0, 0); cr = g; }
-            ar[0] += cr.x; ar[1] += cr.y; ar[2] += cr.z;
-            at[0] += g.x; at[1] += g.y; at[2] += g.z;
-        }
-        for (int q = 0; q < 3; q++) { ar[q] = wave_sum(ar[q]); at[q] = wave_sum(at[q]); }
-        if (lane == 0) { put_part(a, c, 0, mk3(ar[0], ar[1], ar[2])); put_part(a, c, 1, mk3(at[0], at[1], at[2])); }
-    }
+    pcg_sparse_chunks<false>(a, wSparse, wave, nw, nch);
     if (useDense) {  // off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j)
         const uint32_t np = a.ctrl[K_NPAIRS];
         for (uint32_t k = wave; k < np; k += nw) {
@@ -639,13 +694,14 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
         __hip_atomic_store((gu64*)&a.probe[16 + 2 * blockIdx.x], (uint64_t)tStart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store((gu64*)&a.probe[17 + 2 * blockIdx.x], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!last_block(&a.ctrl[K_TICKET])) return;
+    if (!last_block_sharded(a.sync, 1u)) return;
+    if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
     const unsigned long long tFin = a.probe ? wall_clock64() : 0ull;
     // ---- finisher (one workgroup): Kernel1b, Kernel2, host early-out test, Kernel3 ----
     float rDotzNew;
     bool last;
     if (a.N <= 2 * WG + 1) {
-        rDotzNew = pcg_finish_regs<2>(a, sh, nch, useDense, iter, nLin, last);
+        rDotzNew = pcg_finish_regs<2, false>(a, sh, nch, useDense, iter, nLin, last);
     } else {
         float d = 0.0f;
         for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
@@ -716,6 +772,49 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
             a.probe[2] += t1 - t0; a.probe[3] += tFin - t0; a.probe[4] += t2 - t0; a.probe[5] += 1;
             a.probe[6] += dur / gridDim.x; a.probe[7] += lastStart - t0;
         }
+    }
+}
+
+// All PCG iterations of a sparse-only GN step in ONE launch (the global solve's 3 x 150 schedule
+// would otherwise pay ~450 kernel boundaries). Per iteration: every workgroup reduces its chunks,
+// takes a ticket on a counter that grows by gridDim.x per iteration; the workgroup that draws the
+// iteration's last ticket runs the finisher (write-through loads / stores of every vector it
+// touches, since the finisher moves between workgroups) and publishes the iteration number; the
+// others poll it (one lane, relaxed agent loads, bounded) and continue with sc1 loads of p. The
+// grid never exceeds the resident capacity, so every workgroup is running while others wait.
+__global__ __launch_bounds__(WG) void k_pcg_loop(BA a, float wSparse, int nLin) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
+    for (int iter = 0; iter < nLin; iter++) {
+        pcg_sparse_chunks<true>(a, wSparse, wave, nw, nch);
+        const bool fin = last_block_sharded(a.sync, (uint32_t)iter + 1u);
+        if (fin) {
+            bool last = false;
+            const float rz = pcg_finish_regs<2, true>(a, sh, nch, 0, iter, nLin, last);
+            if (threadIdx.x == 0) {
+                st_wt(&a.ctrl[K_RDOTZ], __float_as_uint(rz));
+                st_wt(&a.ctrl[K_PCG_ITERS], ld_wt(&a.ctrl[K_PCG_ITERS]) + 1u);
+                if (last) st_wt(&a.ctrl[K_PCG_DONE], 1u);
+            }
+            drain_stores();
+            __syncthreads();
+            if (threadIdx.x < 8) st_wt(&a.sync[SYNC_FLAG + threadIdx.x * SYNC_LINE], (uint32_t)iter + 1u);
+        } else {
+            if (threadIdx.x == 0) {  // one poller per workgroup, on its shard's flag replica
+                const uint32_t* flag = &a.sync[SYNC_FLAG + (blockIdx.x & 7u) * SYNC_LINE];
+                for (uint32_t spins = 0; ld_wt(flag) < (uint32_t)iter + 1u; spins++) {
+                    __builtin_amdgcn_s_sleep(8);
+                    if (spins > (1u << 22)) {  // a workgroup never arrived: give up (reported as an error)
+                        atomicOr(&a.ctrl[K_ERROR], 2u);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (ld_wt(&a.ctrl[K_PCG_DONE]) != 0u || (ld_wt(&a.ctrl[K_ERROR]) & 2u) != 0u) break;
     }
 }
 
@@ -1174,6 +1273,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     T_.alloc((size_t)N * 16);
     Tinv_.alloc((size_t)N * 16);
     ctrl_.alloc(K_CTRL_WORDS);
+    sync_.alloc(SYNC_WORDS);
     part_.alloc(2 * 4096);
     partIdx_.alloc(2 * 4096);
     pairs_.alloc(maxPairs_);
@@ -1187,8 +1287,17 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
+    // k_pcg_loop (BF_PCG_LOOP=1) needs every workgroup resident: at most the occupancy limit and 3
+    // per CU. Off by default: standalone it matches the per-iteration launches (4.03 vs 4.05 ms per
+    // GN iteration at K = 500), but in the frame loop its waiting workgroups hold CU slots that the
+    // scene stream's voxel pass needs (643 -> 375 frames/s measured).
+    int occ = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pcg_loop, WG, 0));
+    pcgLoopCap_ = 0;
+    if (const char* e = getenv("BF_PCG_LOOP"); e && e[0] == '1') pcgLoopCap_ = (unsigned)std::min(occ, 3) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(apDense_.p, 0, apDense_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
 }
@@ -1221,7 +1330,7 @@ void Solver::solve(const SolveArgs& s) {
     a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p; a.apDense = apDense_.p;
     a.maxPairs = s.numImages * (s.numImages - 1) / 2;
     a.tileCnt = tileCnt_.p; a.nTiles = div_up(s.numCorr, TILE);
-    a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.probe = probe_.p;
+    a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.probe = probe_.p; a.sync = sync_.p;
     a.cache = s.cache; a.cw = s.cacheW; a.ch = s.cacheH;
     a.fx = s.intrinsics[0]; a.fy = s.intrinsics[1]; a.mx = s.intrinsics[2]; a.my = s.intrinsics[3];
     a.distT = cfg_.denseDistThresh; a.normT = cfg_.denseNormalThresh; a.colT = cfg_.denseColorThresh;
@@ -1263,7 +1372,12 @@ void Solver::solve(const SolveArgs& s) {
         k_entries<<<rowGrid, WG, 0, stream_>>>(a);
         k_init<<<rowGrid, WG, 0, stream_>>>(a, wS);
         BF_LAUNCH_CHECK();
-        for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+        if (!dense && s.numImages <= 2 * WG + 1 && s.nLin > 1 && pcgLoopCap_ > 0) {
+            const unsigned g = std::max(1u, std::min(rowGrid, pcgLoopCap_));
+            k_pcg_loop<<<g, WG, 0, stream_>>>(a, wS, (int)s.nLin);
+        } else {
+            for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+        }
         BF_LAUNCH_CHECK();
         k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
         BF_LAUNCH_CHECK();
