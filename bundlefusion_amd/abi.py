@@ -156,6 +156,22 @@ class BFSolveResult(C.Structure):
                 ("numDensePairs", C.c_uint32), ("error", C.c_uint32)]
 
 
+class BFSensInfo(C.Structure):  # include/bf/types.h, mLib SensorData v4 header
+    _fields_ = [("version", C.c_uint32), ("sensorName", C.c_char * 256),
+                ("colorIntrinsic", C.c_float * 16), ("colorExtrinsic", C.c_float * 16),
+                ("depthIntrinsic", C.c_float * 16), ("depthExtrinsic", C.c_float * 16),
+                ("colorCompression", C.c_int32), ("depthCompression", C.c_int32),
+                ("colorWidth", C.c_uint32), ("colorHeight", C.c_uint32), ("depthWidth", C.c_uint32),
+                ("depthHeight", C.c_uint32), ("depthShift", C.c_float), ("reserved", C.c_uint32),
+                ("numFrames", C.c_uint64)]
+
+
+class BFPreprocessOptions(C.Structure):  # include/bf/types.h
+    _fields_ = [("erode", C.c_int32), ("erodeStructureSize", C.c_int32), ("erodeDepthThresh", C.c_float),
+                ("erodeFraction", C.c_float), ("depthFilter", C.c_int32), ("sigmaD", C.c_float),
+                ("sigmaR", C.c_float), ("depthShift", C.c_float)]
+
+
 class BFVoxelOp(C.Structure):  # include/bf/bf.h
     _fields_ = [("T", C.c_float * 16), ("depth", C.c_void_p), ("color", C.c_void_p), ("deintegrate", C.c_uint32),
                 ("reserved", C.c_uint32)]

@@ -7,8 +7,11 @@
 #include "bf_runtime.h"
 #include "synth.h"
 #include "tsdf.h"
+#include "io.h"
+#include "frames.h"
 
 #include <cstring>
+#include <memory>
 #include <limits>
 #include <string>
 
@@ -107,6 +110,19 @@ struct bf_timer {
 struct bf_solver {
     hipStream_t stream = nullptr;
     Solver* solver = nullptr;
+};
+struct bf_sens {
+    SensReader* r = nullptr;
+};
+struct bf_sens_writer {
+    SensWriter* w = nullptr;
+};
+struct bf_params {
+    ParamFile f;
+};
+struct bf_preproc {
+    hipStream_t stream = nullptr;
+    Preproc* p = nullptr;
 };
 
 extern "C" {
@@ -706,6 +722,240 @@ int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]) {
     BF_TRY
     BF_REQUIRE(T && out, BF_ERR_ARG, "null argument");
     pose_helper_matrix_to_pose(to_mat(T), out);
+    BF_CATCH
+}
+
+
+// ---- input formats and preprocessing ------------------------------------------------------------
+int bf_sens_open(const char* path, bf_sens** out) {
+    BF_TRY
+    BF_REQUIRE(path && out, BF_ERR_ARG, "null argument");
+    *out = nullptr;
+    std::unique_ptr<SensReader> r(new SensReader(path));
+    *out = new bf_sens{r.release()};
+    BF_CATCH
+}
+int bf_sens_close(bf_sens* s) {
+    BF_TRY
+    if (s) {
+        delete s->r;
+        delete s;
+    }
+    BF_CATCH
+}
+int bf_sens_info(const bf_sens* s, BFSensInfo* out) {
+    BF_TRY
+    BF_REQUIRE(s && out, BF_ERR_ARG, "null argument");
+    *out = s->r->info();
+    BF_CATCH
+}
+int bf_sens_frame_pose(const bf_sens* s, uint64_t frame, float camToWorld[16]) {
+    BF_TRY
+    BF_REQUIRE(s && camToWorld, BF_ERR_ARG, "null argument");
+    s->r->pose(frame, camToWorld);
+    BF_CATCH
+}
+int bf_sens_frame_timestamps(const bf_sens* s, uint64_t frame, uint64_t* tsColor, uint64_t* tsDepth) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null argument");
+    s->r->timestamps(frame, tsColor, tsDepth);
+    BF_CATCH
+}
+int bf_sens_read_depth_u16(bf_sens* s, uint64_t frame, uint16_t* out) {
+    BF_TRY
+    BF_REQUIRE(s && out, BF_ERR_ARG, "null argument");
+    s->r->depthU16(frame, out);
+    BF_CATCH
+}
+int bf_sens_read_depth(bf_sens* s, uint64_t frame, float* out) {
+    BF_TRY
+    BF_REQUIRE(s && out, BF_ERR_ARG, "null argument");
+    const BFSensInfo& in = s->r->info();
+    const size_t n = (size_t)in.depthWidth * in.depthHeight;
+    std::vector<uint16_t> d(n);
+    s->r->depthU16(frame, d.data());
+    for (size_t i = 0; i < n; i++)  // SensorDataReader.cpp:104-107
+        out[i] = d[i] == 0 ? -std::numeric_limits<float>::infinity() : (float)d[i] / in.depthShift;
+    BF_CATCH
+}
+int bf_sens_read_color(bf_sens* s, uint64_t frame, uint8_t* rgbx) {
+    BF_TRY
+    BF_REQUIRE(s && rgbx, BF_ERR_ARG, "null argument");
+    s->r->colorRGBX(frame, rgbx);
+    BF_CATCH
+}
+int bf_sens_writer_create(const char* path, const BFSensInfo* info, bf_sens_writer** out) {
+    BF_TRY
+    BF_REQUIRE(path && info && out, BF_ERR_ARG, "null argument");
+    *out = nullptr;
+    std::unique_ptr<SensWriter> w(new SensWriter(path, *info));
+    *out = new bf_sens_writer{w.release()};
+    BF_CATCH
+}
+int bf_sens_writer_add_frame(bf_sens_writer* w, const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth,
+                             const uint16_t* depth, const uint8_t* rgbx) {
+    BF_TRY
+    BF_REQUIRE(w && camToWorld && depth, BF_ERR_ARG, "null argument");
+    w->w->addFrame(camToWorld, tsColor, tsDepth, depth, rgbx);
+    BF_CATCH
+}
+int bf_sens_writer_close(bf_sens_writer* w) {
+    BF_TRY
+    if (w) {
+        std::unique_ptr<SensWriter> owned(w->w);
+        delete w;
+        owned->close();
+    }
+    BF_CATCH
+}
+
+int bf_params_create(bf_params** out) {
+    BF_TRY
+    BF_REQUIRE(out, BF_ERR_ARG, "null argument");
+    *out = new bf_params;
+    BF_CATCH
+}
+int bf_params_load(bf_params* p, const char* path) {
+    BF_TRY
+    BF_REQUIRE(p && path, BF_ERR_ARG, "null argument");
+    p->f.load(path);
+    BF_CATCH
+}
+int bf_params_destroy(bf_params* p) {
+    BF_TRY
+    delete p;
+    BF_CATCH
+}
+int bf_params_has(const bf_params* p, const char* key, int* found) {
+    BF_TRY
+    BF_REQUIRE(p && key && found, BF_ERR_ARG, "null argument");
+    *found = p->f.has(key) ? 1 : 0;
+    BF_CATCH
+}
+int bf_params_get_string(const bf_params* p, const char* key, char* buf, size_t cap) {
+    BF_TRY
+    BF_REQUIRE(p && key && buf && cap, BF_ERR_ARG, "null argument");
+    const std::string v = p->f.str(key);
+    BF_REQUIRE(v.size() < cap, BF_ERR_CAPACITY, "buffer too small for " + std::string(key));
+    std::memcpy(buf, v.c_str(), v.size() + 1);
+    BF_CATCH
+}
+int bf_params_get_floats(const bf_params* p, const char* key, float* out, uint32_t cap, uint32_t* count) {
+    BF_TRY
+    BF_REQUIRE(p && key, BF_ERR_ARG, "null argument");
+    const std::vector<float> v = p->f.floats(key);
+    if (count) *count = (uint32_t)v.size();
+    for (size_t i = 0; i < v.size() && i < cap && out; i++) out[i] = v[i];
+    BF_CATCH
+}
+int bf_params_get_number(const bf_params* p, const char* key, double* out) {
+    BF_TRY
+    BF_REQUIRE(p && key && out, BF_ERR_ARG, "null argument");
+    *out = p->f.number(key);
+    BF_CATCH
+}
+int bf_params_get_bool(const bf_params* p, const char* key, int* out) {
+    BF_TRY
+    BF_REQUIRE(p && key && out, BF_ERR_ARG, "null argument");
+    *out = p->f.boolean(key) ? 1 : 0;
+    BF_CATCH
+}
+int bf_params_hash_params(const bf_params* p, BFHashParams* o) {
+    BF_TRY
+    BF_REQUIRE(p && o, BF_ERR_ARG, "null argument");
+    const ParamFile& f = p->f;
+    std::memset(o, 0, sizeof(*o));
+    for (int i = 0; i < 16; i += 5) { o->rigidTransform.m[i] = 1.0f; o->rigidTransformInverse.m[i] = 1.0f; }
+    o->hashNumBuckets = (uint32_t)f.number("s_hashNumBuckets");
+    o->hashBucketSize = BF_HASH_BUCKET_SIZE;
+    o->hashMaxCollisionLinkedListSize = (uint32_t)f.number("s_hashMaxCollisionLinkedListSize");
+    o->numSDFBlocks = (uint32_t)f.number("s_hashNumSDFBlocks");
+    o->SDFBlockSize = BF_SDF_BLOCK_SIZE;
+    o->virtualVoxelSize = (float)f.floats("s_SDFVoxelSize").at(0);
+    o->maxIntegrationDistance = f.floats("s_SDFMaxIntegrationDistance").at(0);
+    o->truncation = f.floats("s_SDFTruncation").at(0);
+    o->truncScale = f.floats("s_SDFTruncationScale").at(0);
+    o->integrationWeightSample = (uint32_t)f.number("s_SDFIntegrationWeightSample");
+    o->integrationWeightMax = (uint32_t)f.number("s_SDFIntegrationWeightMax");
+    const std::vector<float> ext = f.floats("s_streamingVoxelExtents"), dims = f.floats("s_streamingGridDimensions"),
+                             minp = f.floats("s_streamingMinGridPos");
+    BF_REQUIRE(ext.size() == 3 && dims.size() == 3 && minp.size() == 3, BF_ERR_ARG, "streaming vectors need 3 values");
+    o->streamingVoxelExtents = BFFloat3{ext[0], ext[1], ext[2]};
+    o->streamingGridDimensions = BFInt3{(int)dims[0], (int)dims[1], (int)dims[2]};
+    o->streamingMinGridPos = BFInt3{(int)minp[0], (int)minp[1], (int)minp[2]};
+    o->streamingInitialChunkListSize = (uint32_t)f.number("s_streamingInitialChunkListSize");
+    BF_CATCH
+}
+int bf_params_raycast_params(const bf_params* p, float fx, float fy, float mx, float my, BFRayCastParams* o) {
+    BF_TRY
+    BF_REQUIRE(p && o, BF_ERR_ARG, "null argument");
+    const ParamFile& f = p->f;
+    const uint32_t rw = (uint32_t)f.number("s_rayCastWidth"), rh = (uint32_t)f.number("s_rayCastHeight");
+    const uint32_t iw = (uint32_t)f.number("s_integrationWidth"), ih = (uint32_t)f.number("s_integrationHeight");
+    if (rw != iw || rh != ih) {  // adapt intrinsics (CUDARayCastSDF.h:26-32)
+        fx *= (float)rw / (float)iw;
+        fy *= (float)rh / (float)ih;
+        mx *= (float)(rw - 1) / (float)(iw - 1);
+        my *= (float)(rh - 1) / (float)(ih - 1);
+    }
+    std::memset(o, 0, sizeof(*o));
+    o->width = rw;
+    o->height = rh;
+    o->fx = fx; o->fy = fy; o->mx = mx; o->my = my;
+    o->minDepth = f.floats("s_renderDepthMin").at(0);
+    o->maxDepth = f.floats("s_renderDepthMax").at(0);
+    o->rayIncrement = f.floats("s_SDFRayIncrementFactor").at(0) * f.floats("s_SDFTruncation").at(0);
+    o->thresSampleDist = f.floats("s_SDFRayThresSampleDistFactor").at(0) * o->rayIncrement;
+    o->thresDist = f.floats("s_SDFRayThresDistFactor").at(0) * o->rayIncrement;
+    o->useGradients = f.boolean("s_SDFUseGradients") ? 1 : 0;
+    o->maxNumVertices = (uint32_t)f.number("s_hashNumSDFBlocks") * 6;
+    BF_CATCH
+}
+int bf_params_preprocess_options(const bf_params* p, float depthShift, BFPreprocessOptions* o) {
+    BF_TRY
+    BF_REQUIRE(p && o, BF_ERR_ARG, "null argument");
+    const ParamFile& f = p->f;
+    o->erode = f.boolean("s_erodeSIFTdepth") ? 1 : 0;
+    o->erodeStructureSize = 3;      // CUDAImageManager.cpp:95-103
+    o->erodeDepthThresh = 0.05f;
+    o->erodeFraction = 0.3f;
+    o->depthFilter = f.boolean("s_depthFilter") ? 1 : 0;
+    o->sigmaD = f.floats("s_depthSigmaD").at(0);
+    o->sigmaR = f.floats("s_depthSigmaR").at(0);
+    o->depthShift = depthShift;
+    BF_CATCH
+}
+
+int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_t colorH, uint32_t integrationW,
+                      uint32_t integrationH, const BFPreprocessOptions* opt, bf_preproc** out) {
+    BF_TRY
+    BF_REQUIRE(opt && out, BF_ERR_ARG, "null argument");
+    *out = nullptr;
+    std::unique_ptr<bf_preproc> h(new bf_preproc);
+    BF_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->p = new Preproc(depthW, depthH, colorW, colorH, integrationW, integrationH, *opt, h->stream);
+    *out = h.release();
+    BF_CATCH
+}
+int bf_preproc_destroy(bf_preproc* p) {
+    BF_TRY
+    if (p) {
+        delete p->p;
+        if (p->stream) (void)hipStreamDestroy(p->stream);
+        delete p;
+    }
+    BF_CATCH
+}
+int bf_preproc_run(bf_preproc* p, const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut) {
+    BF_TRY
+    BF_REQUIRE(p && depthU16 && depthOut, BF_ERR_ARG, "null argument");
+    p->p->run(depthU16, rgbx, depthOut, colorOut);
+    BF_CATCH
+}
+int bf_preproc_synchronize(bf_preproc* p) {
+    BF_TRY
+    BF_REQUIRE(p, BF_ERR_ARG, "null argument");
+    BF_HIP(hipStreamSynchronize(p->stream));
     BF_CATCH
 }
 

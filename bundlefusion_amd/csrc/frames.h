@@ -1,0 +1,33 @@
+// frames.h — input preprocessing (CUDAImageManager::process, CUDAImageManager.cpp:22-158): see
+// frames.hip. The CPU oracle restates the same steps in oracle/frames.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/bf/types.h"
+#include "bf_runtime.h"
+
+namespace bf {
+
+struct GaussTable {  // gaussD weights per integer offset, radius (int)ceil(2 sigmaD) <= 7
+    int radius;
+    float w[15 * 15];
+};
+GaussTable gauss_table(float sigmaD);
+
+class Preproc {
+public:
+    Preproc(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_t colorH, uint32_t integrationW, uint32_t integrationH,
+            const BFPreprocessOptions& opt, hipStream_t stream);
+    // device pointers; queued on the stream
+    void run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut);
+    hipStream_t stream() const { return stream_; }
+
+private:
+    uint32_t dw_, dh_, cw_, ch_, iw_, ih_;
+    BFPreprocessOptions opt_;
+    hipStream_t stream_;
+    GaussTable gauss_{};
+    DevBuf<float> a_, b_;
+};
+
+}  // namespace bf

@@ -1,0 +1,200 @@
+// frames.hip — input preprocessing of CUDAImageManager::process (CUDAImageManager.cpp:22-158) for
+// gfx950: ushort depth -> metres (SensorDataReader.cpp:104-107), erodeDepthMap x2
+// (CUDAImageUtil.cu:701-748), gaussFilterDepthMap (:759-806), nearest resampling of depth and colour
+// to the integration size (resampleFloat / resampleUCHAR4, :93-186).
+//
+// The images are small (0.3 - 1.2 Mpixel) and every kernel is a stencil over them, so the layout is
+// the plain row-major image; each workgroup stages its tile plus halo in LDS once, so a pixel's
+// (2r+1)^2 neighbourhood is read from LDS instead of 25-81 global loads. Arithmetic follows the
+// reference expression by expression (-ffp-contract=off); the Gaussian weights depend only on the
+// integer offset, so they are a host-computed table shared with the CPU oracle.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+#include "../../include/bf/bf.h"
+#include "bf_runtime.h"
+#include "frames.h"
+
+namespace bf {
+
+namespace {
+
+constexpr int TX = 32, TY = 8;   // workgroup tile: 32 x 8 pixels, 256 threads
+constexpr int MAXR = 7;          // stencil radius cap (erode structure size / ceil(2 sigmaD))
+
+__global__ __launch_bounds__(256) void k_depth_u16(const uint16_t* __restrict__ in, float* __restrict__ out, uint32_t n,
+                                                   float shift) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint16_t d = in[i];
+    out[i] = d == 0 ? -INFINITY : (float)d / shift;
+}
+
+// stage a (TX + 2R) x (TY + 2R) tile with halo; out-of-image cells are filled but never read: the
+// callers keep the reference's `x + j >= 0 && ...` bounds tests
+template <int R>
+__device__ __forceinline__ void stage_tile(float (*t)[TX + 2 * MAXR], const float* __restrict__ in, int W, int H) {
+    const int x0 = blockIdx.x * TX - R, y0 = blockIdx.y * TY - R;
+    for (int k = threadIdx.x; k < (TX + 2 * R) * (TY + 2 * R); k += blockDim.x) {
+        const int ty = k / (TX + 2 * R), tx = k % (TX + 2 * R);
+        const int x = x0 + tx, y = y0 + ty;
+        t[ty][tx] = (x >= 0 && x < W && y >= 0 && y < H) ? in[y * W + x] : 0.0f;
+    }
+    __syncthreads();
+}
+
+// erodeDepthMapDevice (CUDAImageUtil.cu:701-739)
+template <int R>
+__global__ __launch_bounds__(256) void k_erode(float* __restrict__ out, const float* __restrict__ in, int W, int H, float dThresh,
+                                               float fracReq) {
+    __shared__ float t[TY + 2 * MAXR][TX + 2 * MAXR];
+    stage_tile<R>(t, in, W, H);
+    const int lx = threadIdx.x % TX, ly = threadIdx.x / TX;
+    const int x = blockIdx.x * TX + lx, y = blockIdx.y * TY + ly;
+    if (x >= W || y >= H) return;
+    unsigned int count = 0;
+    const float oldDepth = t[ly + R][lx + R];
+    for (int i = -R; i <= R; i++)
+        for (int j = -R; j <= R; j++)
+            if (x + j >= 0 && x + j < W && y + i >= 0 && y + i < H) {
+                const float depth = t[ly + R + i][lx + R + j];
+                if (depth == -INFINITY || depth == 0.0f || fabsf(depth - oldDepth) > dThresh) count++;
+            }
+    const unsigned int sum = (2 * R + 1) * (2 * R + 1);
+    out[y * W + x] = ((float)count / (float)sum >= fracReq) ? -INFINITY : oldDepth;
+}
+
+// gaussFilterDepthMapDevice (CUDAImageUtil.cu:759-797): m (x) outer, n (y) inner, as the reference
+template <int R>
+__global__ __launch_bounds__(256) void k_gauss(float* __restrict__ out, const float* __restrict__ in, int W, int H, float sigmaR,
+                                               GaussTable g) {
+    __shared__ float t[TY + 2 * MAXR][TX + 2 * MAXR];
+    stage_tile<R>(t, in, W, H);
+    const int lx = threadIdx.x % TX, ly = threadIdx.x / TX;
+    const int x = blockIdx.x * TX + lx, y = blockIdx.y * TY + ly;
+    if (x >= W || y >= H) return;
+    float sum = 0.0f, sumWeight = 0.0f;
+    const float depthCenter = t[ly + R][lx + R];
+    if (depthCenter != -INFINITY) {
+        for (int m = x - R; m <= x + R; m++)
+            for (int n = y - R; n <= y + R; n++)
+                if (m >= 0 && n >= 0 && m < W && n < H) {
+                    const float currentDepth = t[ly + R + (n - y)][lx + R + (m - x)];
+                    if (currentDepth != -INFINITY && fabsf(depthCenter - currentDepth) < sigmaR) {
+                        const float weight = g.w[(n - y + R) * (2 * R + 1) + (m - x + R)];
+                        sumWeight += weight;
+                        sum += weight * currentDepth;
+                    }
+                }
+    }
+    out[y * W + x] = sumWeight > 0.0f ? sum / sumWeight : -INFINITY;
+}
+
+// resampleFloat_Kernel / resampleUCHAR4_Kernel (CUDAImageUtil.cu:93-111, 160-177): nearest sample
+template <class T>
+__global__ __launch_bounds__(256) void k_resample(T* __restrict__ out, uint32_t oW, uint32_t oH, const T* __restrict__ in,
+                                                  uint32_t iW, uint32_t iH) {
+    const uint32_t x = blockIdx.x * TX + threadIdx.x % TX, y = blockIdx.y * TY + threadIdx.x / TX;
+    if (x >= oW || y >= oH) return;
+    const float scaleWidth = (float)(iW - 1) / (float)(oW - 1);
+    const float scaleHeight = (float)(iH - 1) / (float)(oH - 1);
+    const uint32_t xi = (uint32_t)((float)x * scaleWidth + 0.5f), yi = (uint32_t)((float)y * scaleHeight + 0.5f);
+    if (xi < iW && yi < iH) out[y * oW + x] = in[yi * iW + xi];
+}
+
+template <int R>
+void launch_erode(float* out, const float* in, int W, int H, float dT, float fr, hipStream_t s) {
+    k_erode<R><<<dim3(div_up(W, TX), div_up(H, TY)), 256, 0, s>>>(out, in, W, H, dT, fr);
+}
+template <int R>
+void launch_gauss(float* out, const float* in, int W, int H, float sR, const GaussTable& g, hipStream_t s) {
+    k_gauss<R><<<dim3(div_up(W, TX), div_up(H, TY)), 256, 0, s>>>(out, in, W, H, sR, g);
+}
+
+}  // namespace
+
+// gaussD (CUDAImageUtil.cu:531-534) per integer offset, kernel radius (int)ceil(2.0 * sigmaD)
+GaussTable gauss_table(float sigmaD) {
+    GaussTable g{};
+    g.radius = (int)std::ceil(2.0 * (double)sigmaD);
+    BF_REQUIRE(g.radius >= 0 && g.radius <= MAXR, BF_ERR_ARG, "sigmaD out of range (radius <= 7)");
+    for (int dy = -g.radius; dy <= g.radius; dy++)
+        for (int dx = -g.radius; dx <= g.radius; dx++) {
+            const int xx = dx * dx + dy * dy;
+            g.w[(dy + g.radius) * (2 * g.radius + 1) + (dx + g.radius)] = expf(-((float)xx / (2.0f * sigmaD * sigmaD)));
+        }
+    return g;
+}
+
+Preproc::Preproc(uint32_t dw, uint32_t dh, uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, const BFPreprocessOptions& o,
+                 hipStream_t stream)
+    : dw_(dw), dh_(dh), cw_(cw), ch_(ch), iw_(iw), ih_(ih), opt_(o), stream_(stream) {
+    BF_REQUIRE(dw && dh && iw && ih, BF_ERR_ARG, "empty image size");
+    BF_REQUIRE(o.erodeStructureSize >= 0 && o.erodeStructureSize <= MAXR, BF_ERR_ARG, "erode structure size 0..7");
+    BF_REQUIRE(o.depthShift > 0.0f, BF_ERR_ARG, "depthShift");
+    if (o.depthFilter) gauss_ = gauss_table(o.sigmaD);
+    a_.alloc((size_t)dw * dh);
+    b_.alloc((size_t)dw * dh);
+}
+
+// CUDAImageManager::process: raw -> [erode x2 (raw <-> filtered)] -> [gauss | copy] -> resample
+void Preproc::run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut) {
+    const uint32_t n = dw_ * dh_;
+    float* raw = a_.p;
+    float* filtered = b_.p;
+    k_depth_u16<<<div_up(n, 256), 256, 0, stream_>>>(depthU16, raw, n, opt_.depthShift);
+    BF_LAUNCH_CHECK();
+    const int W = (int)dw_, H = (int)dh_;
+    if (opt_.erode) {
+        for (int i = 0; i < 2; i++) {
+            float* out = (i % 2 == 0) ? filtered : raw;
+            const float* in = (i % 2 == 0) ? raw : filtered;
+            switch (opt_.erodeStructureSize) {
+                case 0: launch_erode<0>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 1: launch_erode<1>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 2: launch_erode<2>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 3: launch_erode<3>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 4: launch_erode<4>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 5: launch_erode<5>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 6: launch_erode<6>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                default: launch_erode<7>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+            }
+            BF_LAUNCH_CHECK();
+        }
+    }
+    const float* result = raw;
+    if (opt_.depthFilter) {
+        switch (gauss_.radius) {
+            case 0: launch_gauss<0>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            case 1: launch_gauss<1>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            case 2: launch_gauss<2>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            case 3: launch_gauss<3>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            case 4: launch_gauss<4>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            case 5: launch_gauss<5>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            case 6: launch_gauss<6>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+            default: launch_gauss<7>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
+        }
+        BF_LAUNCH_CHECK();
+        result = filtered;
+    }
+    if (dw_ == iw_ && dh_ == ih_) {
+        BF_HIP(hipMemcpyAsync(depthOut, result, sizeof(float) * n, hipMemcpyDeviceToDevice, stream_));
+    } else {
+        k_resample<float><<<dim3(div_up(iw_, TX), div_up(ih_, TY)), 256, 0, stream_>>>(depthOut, iw_, ih_, result, dw_, dh_);
+        BF_LAUNCH_CHECK();
+    }
+    if (rgbx && colorOut) {
+        if (cw_ == iw_ && ch_ == ih_) {
+            BF_HIP(hipMemcpyAsync(colorOut, rgbx, 4ull * cw_ * ch_, hipMemcpyDeviceToDevice, stream_));
+        } else {
+            k_resample<uchar4><<<dim3(div_up(iw_, TX), div_up(ih_, TY)), 256, 0, stream_>>>(
+                reinterpret_cast<uchar4*>(colorOut), iw_, ih_, reinterpret_cast<const uchar4*>(rgbx), cw_, ch_);
+            BF_LAUNCH_CHECK();
+        }
+    }
+}
+
+}  // namespace bf

@@ -1,0 +1,276 @@
+// io.cpp — `.sens` reader / writer and `zParameters*.txt` parser (see io.h).
+#include "io.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <limits>
+#include <sstream>
+
+#include "bf_runtime.h"
+
+namespace bf {
+
+namespace {
+
+template <class T>
+void rd(FILE* f, T* v, size_t n = 1) {
+    BF_REQUIRE(std::fread(v, sizeof(T), n, f) == n, BF_ERR_IO, "truncated .sens file");
+}
+template <class T>
+void wr(FILE* f, const T* v, size_t n = 1) {
+    BF_REQUIRE(std::fwrite(v, sizeof(T), n, f) == n, BF_ERR_IO, "write failed");
+}
+
+}  // namespace
+
+// ---- reader: header, then a frame index (offsets only; payloads are read on demand) ----------
+SensReader::SensReader(const std::string& path) {
+    f_ = std::fopen(path.c_str(), "rb");
+    BF_REQUIRE(f_ != nullptr, BF_ERR_IO, "cannot open " + path);
+    BF_REQUIRE(fseeko(f_, 0, SEEK_END) == 0, BF_ERR_IO, "seek failed");
+    const uint64_t fileSize = (uint64_t)ftello(f_);
+    BF_REQUIRE(fseeko(f_, 0, SEEK_SET) == 0, BF_ERR_IO, "seek failed");
+    rd(f_, &info_.version);
+    BF_REQUIRE(info_.version == 4, BF_ERR_IO, "unsupported .sens version " + std::to_string(info_.version));
+    uint64_t nameLen = 0;
+    rd(f_, &nameLen);
+    BF_REQUIRE(nameLen < (1u << 20), BF_ERR_IO, "corrupt sensor name length");
+    std::string name(nameLen, '\0');
+    if (nameLen) rd(f_, &name[0], nameLen);
+    std::strncpy(info_.sensorName, name.c_str(), sizeof(info_.sensorName) - 1);
+    rd(f_, info_.colorIntrinsic, 16);
+    rd(f_, info_.colorExtrinsic, 16);
+    rd(f_, info_.depthIntrinsic, 16);
+    rd(f_, info_.depthExtrinsic, 16);
+    rd(f_, &info_.colorCompression);
+    rd(f_, &info_.depthCompression);
+    rd(f_, &info_.colorWidth);
+    rd(f_, &info_.colorHeight);
+    rd(f_, &info_.depthWidth);
+    rd(f_, &info_.depthHeight);
+    rd(f_, &info_.depthShift);
+    rd(f_, &info_.numFrames);
+    BF_REQUIRE(info_.numFrames < (1ull << 32), BF_ERR_IO, "corrupt frame count");
+    frames_.resize(info_.numFrames);
+    for (uint64_t i = 0; i < info_.numFrames; i++) {
+        Frame& fr = frames_[i];
+        rd(f_, fr.camToWorld, 16);
+        rd(f_, &fr.tsColor);
+        rd(f_, &fr.tsDepth);
+        rd(f_, &fr.colorBytes);
+        rd(f_, &fr.depthBytes);
+        fr.colorOffset = (uint64_t)ftello(f_);
+        fr.depthOffset = fr.colorOffset + fr.colorBytes;
+        BF_REQUIRE(fr.colorBytes <= fileSize && fr.depthBytes <= fileSize && fr.depthOffset + fr.depthBytes <= fileSize,
+                   BF_ERR_IO, "truncated .sens file (frame " + std::to_string(i) + ")");
+        BF_REQUIRE(fseeko(f_, (off_t)(fr.depthOffset + fr.depthBytes), SEEK_SET) == 0, BF_ERR_IO, "seek failed");
+    }
+}
+
+SensReader::~SensReader() {
+    if (f_) std::fclose(f_);
+}
+
+const SensReader::Frame& SensReader::frame(uint64_t i) const {
+    BF_REQUIRE(i < frames_.size(), BF_ERR_ARG, "frame index out of range");
+    return frames_[i];
+}
+
+void SensReader::pose(uint64_t i, float camToWorld[16]) const { std::memcpy(camToWorld, frame(i).camToWorld, 64); }
+
+void SensReader::timestamps(uint64_t i, uint64_t* tsColor, uint64_t* tsDepth) const {
+    if (tsColor) *tsColor = frame(i).tsColor;
+    if (tsDepth) *tsDepth = frame(i).tsDepth;
+}
+
+void SensReader::depthU16(uint64_t i, uint16_t* out) {
+    const Frame& fr = frame(i);
+    const uint64_t n = (uint64_t)info_.depthWidth * info_.depthHeight;
+    buf_.resize(fr.depthBytes);
+    BF_REQUIRE(fseeko(f_, (off_t)fr.depthOffset, SEEK_SET) == 0, BF_ERR_IO, "seek failed");
+    if (fr.depthBytes) rd(f_, buf_.data(), fr.depthBytes);
+    if (info_.depthCompression == 0) {
+        BF_REQUIRE(fr.depthBytes == 2 * n, BF_ERR_IO, "raw depth size mismatch");
+        std::memcpy(out, buf_.data(), 2 * n);
+    } else if (info_.depthCompression == 1) {
+        uLongf len = (uLongf)(2 * n);
+        const int z = uncompress(reinterpret_cast<Bytef*>(out), &len, buf_.data(), (uLong)fr.depthBytes);
+        BF_REQUIRE(z == Z_OK && len == 2 * n, BF_ERR_IO, "zlib depth stream corrupt");
+    } else {
+        throw Error(BF_ERR_ARG, "unsupported depth compression " + std::to_string(info_.depthCompression) +
+                                    " (occi needs the vendor codec)");
+    }
+}
+
+// mLib's raw colour is RGB, 3 B per pixel; SensorDataReader widens it to RGBX (:111-113). png / jpeg
+// need an image decoder this build does not carry.
+void SensReader::colorRGBX(uint64_t i, uint8_t* out) {
+    const Frame& fr = frame(i);
+    const uint64_t n = (uint64_t)info_.colorWidth * info_.colorHeight;
+    BF_REQUIRE(info_.colorCompression == 0, BF_ERR_ARG,
+               "unsupported colour compression " + std::to_string(info_.colorCompression) + " (png/jpeg decoding not built)");
+    BF_REQUIRE(fr.colorBytes == 3 * n, BF_ERR_IO, "raw colour size mismatch");
+    buf_.resize(fr.colorBytes);
+    BF_REQUIRE(fseeko(f_, (off_t)fr.colorOffset, SEEK_SET) == 0, BF_ERR_IO, "seek failed");
+    rd(f_, buf_.data(), fr.colorBytes);
+    for (uint64_t p = 0; p < n; p++) {
+        out[4 * p + 0] = buf_[3 * p + 0];
+        out[4 * p + 1] = buf_[3 * p + 1];
+        out[4 * p + 2] = buf_[3 * p + 2];
+        out[4 * p + 3] = 255;
+    }
+}
+
+// ---- writer ------------------------------------------------------------------------------------
+SensWriter::SensWriter(const std::string& path, const BFSensInfo& info) : info_(info) {
+    BF_REQUIRE(info.colorCompression == 0 && (info.depthCompression == 0 || info.depthCompression == 1), BF_ERR_ARG,
+               "writer supports raw colour and raw / zlib depth");
+    f_ = std::fopen(path.c_str(), "wb");
+    BF_REQUIRE(f_ != nullptr, BF_ERR_IO, "cannot create " + path);
+    const uint32_t version = 4;
+    wr(f_, &version);
+    const std::string name(info.sensorName, strnlen(info.sensorName, sizeof(info.sensorName)));
+    const uint64_t nameLen = name.size();
+    wr(f_, &nameLen);
+    if (nameLen) wr(f_, name.data(), nameLen);
+    wr(f_, info.colorIntrinsic, 16);
+    wr(f_, info.colorExtrinsic, 16);
+    wr(f_, info.depthIntrinsic, 16);
+    wr(f_, info.depthExtrinsic, 16);
+    wr(f_, &info.colorCompression);
+    wr(f_, &info.depthCompression);
+    wr(f_, &info.colorWidth);
+    wr(f_, &info.colorHeight);
+    wr(f_, &info.depthWidth);
+    wr(f_, &info.depthHeight);
+    wr(f_, &info.depthShift);
+    numFramesPos_ = std::ftell(f_);
+    const uint64_t zero = 0;
+    wr(f_, &zero);
+}
+
+SensWriter::~SensWriter() {
+    try {
+        close();
+    } catch (...) {
+    }
+}
+
+void SensWriter::addFrame(const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth, const uint16_t* depth,
+                          const uint8_t* rgbx) {
+    BF_REQUIRE(f_ != nullptr, BF_ERR_STATE, "writer closed");
+    const uint64_t nd = (uint64_t)info_.depthWidth * info_.depthHeight, nc = (uint64_t)info_.colorWidth * info_.colorHeight;
+    std::vector<uint8_t> rgb(3 * nc);
+    for (uint64_t p = 0; p < nc; p++) {
+        rgb[3 * p] = rgbx ? rgbx[4 * p] : 0;
+        rgb[3 * p + 1] = rgbx ? rgbx[4 * p + 1] : 0;
+        rgb[3 * p + 2] = rgbx ? rgbx[4 * p + 2] : 0;
+    }
+    const uint8_t* dptr = reinterpret_cast<const uint8_t*>(depth);
+    uint64_t depthBytes = 2 * nd;
+    if (info_.depthCompression == 1) {
+        uLongf len = compressBound((uLong)(2 * nd));
+        buf_.resize(len);
+        BF_REQUIRE(compress2(buf_.data(), &len, dptr, (uLong)(2 * nd), Z_DEFAULT_COMPRESSION) == Z_OK, BF_ERR_IO, "zlib failed");
+        dptr = buf_.data();
+        depthBytes = len;
+    }
+    const uint64_t colorBytes = rgb.size();
+    wr(f_, camToWorld, 16);
+    wr(f_, &tsColor);
+    wr(f_, &tsDepth);
+    wr(f_, &colorBytes);
+    wr(f_, &depthBytes);
+    if (colorBytes) wr(f_, rgb.data(), colorBytes);
+    if (depthBytes) wr(f_, dptr, depthBytes);
+    numFrames_++;
+}
+
+void SensWriter::close() {
+    if (!f_) return;
+    const uint64_t numIMU = 0;
+    wr(f_, &numIMU);
+    BF_REQUIRE(std::fseek(f_, numFramesPos_, SEEK_SET) == 0, BF_ERR_IO, "seek failed");
+    wr(f_, &numFrames_);
+    std::fclose(f_);
+    f_ = nullptr;
+}
+
+// ---- zParameters: `name = value;`, `//` comments outside quotes, values up to ';' ------------
+void ParamFile::load(const std::string& path) {
+    std::ifstream in(path);
+    BF_REQUIRE(in.good(), BF_ERR_IO, "cannot open " + path);
+    std::string line;
+    while (std::getline(in, line)) {
+        std::string s;
+        bool quoted = false;
+        for (size_t i = 0; i < line.size(); i++) {  // drop the comment, keep "//" inside quotes
+            if (line[i] == '"') quoted = !quoted;
+            if (!quoted && line[i] == '/' && i + 1 < line.size() && line[i + 1] == '/') break;
+            s += line[i];
+        }
+        const size_t eq = s.find('=');
+        if (eq == std::string::npos) continue;
+        auto trim = [](std::string t) {
+            size_t a = 0, b = t.size();
+            while (a < b && std::isspace((unsigned char)t[a])) a++;
+            while (b > a && std::isspace((unsigned char)t[b - 1])) b--;
+            return t.substr(a, b - a);
+        };
+        std::string key = trim(s.substr(0, eq)), val = s.substr(eq + 1);
+        const size_t semi = val.rfind(';');
+        if (semi != std::string::npos) val = val.substr(0, semi);
+        val = trim(val);
+        if (!key.empty()) kv_[key] = val;
+    }
+}
+
+const std::string& ParamFile::raw(const std::string& key) const {
+    auto it = kv_.find(key);
+    BF_REQUIRE(it != kv_.end(), BF_ERR_ARG, "missing parameter " + key);
+    return it->second;
+}
+
+std::vector<float> ParamFile::floats(const std::string& key) const {
+    std::istringstream ss(raw(key));
+    std::vector<float> out;
+    std::string tok;
+    while (ss >> tok) {
+        if (!tok.empty() && (tok.back() == 'f' || tok.back() == 'F')) tok.pop_back();
+        char* end = nullptr;
+        const float v = std::strtof(tok.c_str(), &end);
+        BF_REQUIRE(end && *end == '\0', BF_ERR_ARG, "parameter " + key + " is not numeric: " + tok);
+        out.push_back(v);
+    }
+    return out;
+}
+
+double ParamFile::number(const std::string& key) const {
+    std::string t = raw(key);
+    if (!t.empty() && (t.back() == 'f' || t.back() == 'F')) t.pop_back();
+    char* end = nullptr;
+    const double v = std::strtod(t.c_str(), &end);
+    BF_REQUIRE(end && *end == '\0', BF_ERR_ARG, "parameter " + key + " is not a number: " + t);
+    return v;
+}
+
+bool ParamFile::boolean(const std::string& key) const {
+    const std::string& t = raw(key);
+    if (t == "true" || t == "1") return true;
+    if (t == "false" || t == "0") return false;
+    throw Error(BF_ERR_ARG, "parameter " + key + " is not a bool: " + t);
+}
+
+std::string ParamFile::str(const std::string& key) const {
+    std::string t = raw(key);
+    if (t.size() >= 2 && t.front() == '"' && t.back() == '"') t = t.substr(1, t.size() - 2);
+    return t;
+}
+
+}  // namespace bf

@@ -1,0 +1,72 @@
+// io.h — the reference's input formats (both parsers live in the
+// un-vendored mLib, so the format is restated here and pinned by round-trip tests):
+//   * `.sens` (mLib SensorData, version 4, as read by SensorDataReader.cpp:38-116): header,
+//     per-frame {camToWorld, timestamps, compressed colour, compressed depth}, IMU records.
+//   * `zParameters*.txt` (mLib ParameterFile, read by GlobalAppState / GlobalBundlingState):
+//     `name = value;` lines with `//` comments.
+// Host-only C++ (zlib for the depth stream); frames are read on demand, never all at once.
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/bf/bf.h"
+
+namespace bf {
+
+class SensReader {
+public:
+    explicit SensReader(const std::string& path);
+    ~SensReader();
+    const BFSensInfo& info() const { return info_; }
+    void pose(uint64_t frame, float camToWorld[16]) const;
+    void timestamps(uint64_t frame, uint64_t* tsColor, uint64_t* tsDepth) const;
+    void depthU16(uint64_t frame, uint16_t* out);
+    void colorRGBX(uint64_t frame, uint8_t* out);
+
+private:
+    struct Frame {
+        float camToWorld[16];
+        uint64_t tsColor, tsDepth, colorBytes, depthBytes;
+        uint64_t colorOffset, depthOffset;
+    };
+    FILE* f_ = nullptr;
+    BFSensInfo info_{};
+    std::vector<Frame> frames_;
+    std::vector<uint8_t> buf_;
+    const Frame& frame(uint64_t i) const;
+};
+
+class SensWriter {
+public:
+    SensWriter(const std::string& path, const BFSensInfo& info);
+    ~SensWriter();
+    void addFrame(const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth, const uint16_t* depth, const uint8_t* rgbx);
+    void close();
+
+private:
+    FILE* f_ = nullptr;
+    BFSensInfo info_{};
+    long numFramesPos_ = 0;
+    uint64_t numFrames_ = 0;
+    std::vector<uint8_t> buf_;
+};
+
+class ParamFile {
+public:
+    void load(const std::string& path);  // later files override earlier keys
+    bool has(const std::string& key) const { return kv_.count(key) != 0; }
+    const std::string& raw(const std::string& key) const;
+    std::vector<float> floats(const std::string& key) const;
+    double number(const std::string& key) const;
+    bool boolean(const std::string& key) const;
+    std::string str(const std::string& key) const;
+    size_t size() const { return kv_.size(); }
+
+private:
+    std::map<std::string, std::string> kv_;
+};
+
+}  // namespace bf

@@ -1,0 +1,194 @@
+"""Input formats and preprocessing over the C ABI: `.sens` reading / writing
+(mLib SensorData v4, SensorDataReader.cpp:38-116), `zParameters*.txt` (mLib ParameterFile behind
+GlobalAppState / GlobalBundlingState) and CUDAImageManager::process's preprocessing on the GPU."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import DeviceArray, abi, check, lib
+from .abi import BFHashParams, BFPreprocessOptions, BFRayCastParams, BFSensInfo
+
+
+def _mat(a) -> C.Array:
+    return abi.mat(np.asarray(a, np.float32).reshape(4, 4))
+
+
+class SensorData:
+    """Reader of a .sens file; frames are decoded on demand."""
+
+    def __init__(self, path: str):
+        self.h = C.c_void_p()
+        check(lib().bf_sens_open(path.encode(), C.byref(self.h)))
+        self.info = BFSensInfo()
+        check(lib().bf_sens_info(self.h, C.byref(self.info)))
+
+    def close(self):
+        if self.h:
+            lib().bf_sens_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self) -> int:
+        return int(self.info.numFrames)
+
+    @property
+    def sensor_name(self) -> str:
+        return self.info.sensorName.decode()
+
+    def intrinsics(self, which="depth") -> np.ndarray:
+        return np.array(getattr(self.info, which + "Intrinsic"), np.float32).reshape(4, 4)
+
+    def pose(self, f: int) -> np.ndarray:
+        T = (C.c_float * 16)()
+        check(lib().bf_sens_frame_pose(self.h, C.c_uint64(f), T))
+        return np.array(T, np.float32).reshape(4, 4)
+
+    def timestamps(self, f: int):
+        a, b = C.c_uint64(), C.c_uint64()
+        check(lib().bf_sens_frame_timestamps(self.h, C.c_uint64(f), C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def depth_u16(self, f: int) -> np.ndarray:
+        out = np.empty((self.info.depthHeight, self.info.depthWidth), np.uint16)
+        check(lib().bf_sens_read_depth_u16(self.h, C.c_uint64(f), out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def depth(self, f: int) -> np.ndarray:
+        """SensorDataReader::processDepth: d / depthShift, 0 -> -inf."""
+        out = np.empty((self.info.depthHeight, self.info.depthWidth), np.float32)
+        check(lib().bf_sens_read_depth(self.h, C.c_uint64(f), out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def color(self, f: int) -> np.ndarray:
+        out = np.empty((self.info.colorHeight, self.info.colorWidth, 4), np.uint8)
+        check(lib().bf_sens_read_color(self.h, C.c_uint64(f), out.ctypes.data_as(C.c_void_p)))
+        return out
+
+
+def write_sens(path: str, depth_u16, rgbx, poses, depth_intrinsic, color_intrinsic=None, depth_shift=1000.0,
+               zlib_depth=True, name="bundlefusion_amd synthetic", timestamps=None):
+    """SensorData::saveToFile layout: raw RGB colour, zlib (or raw) ushort depth."""
+    depth_u16 = np.ascontiguousarray(depth_u16, np.uint16)
+    rgbx = np.ascontiguousarray(rgbx, np.uint8)
+    F, dh, dw = depth_u16.shape
+    ch, cw = rgbx.shape[1:3]
+    info = BFSensInfo()
+    info.version = 4
+    info.sensorName = name.encode()[:255]
+    ident = np.eye(4, dtype=np.float32).reshape(16)
+    info.depthIntrinsic[:] = np.asarray(depth_intrinsic, np.float32).reshape(16)
+    info.colorIntrinsic[:] = np.asarray(color_intrinsic if color_intrinsic is not None else depth_intrinsic,
+                                        np.float32).reshape(16)
+    info.depthExtrinsic[:] = ident
+    info.colorExtrinsic[:] = ident
+    info.colorCompression = 0
+    info.depthCompression = 1 if zlib_depth else 0
+    info.colorWidth, info.colorHeight, info.depthWidth, info.depthHeight = cw, ch, dw, dh
+    info.depthShift = depth_shift
+    w = C.c_void_p()
+    check(lib().bf_sens_writer_create(path.encode(), C.byref(info), C.byref(w)))
+    try:
+        for f in range(F):
+            tc, td = (timestamps[f] if timestamps is not None else (f, f))
+            check(lib().bf_sens_writer_add_frame(w, _mat(poses[f]), C.c_uint64(tc), C.c_uint64(td),
+                                                 depth_u16[f].ctypes.data_as(C.c_void_p),
+                                                 rgbx[f].ctypes.data_as(C.c_void_p)))
+    finally:
+        check(lib().bf_sens_writer_close(w))
+
+
+class ParameterFile:
+    """zParameters*.txt; later loads override earlier keys."""
+
+    def __init__(self, *paths: str):
+        self.h = C.c_void_p()
+        check(lib().bf_params_create(C.byref(self.h)))
+        for p in paths:
+            self.load(p)
+
+    def load(self, path: str):
+        check(lib().bf_params_load(self.h, path.encode()))
+
+    def __del__(self):
+        try:
+            lib().bf_params_destroy(self.h)
+        except Exception:
+            pass
+
+    def __contains__(self, key: str) -> bool:
+        f = C.c_int()
+        check(lib().bf_params_has(self.h, key.encode(), C.byref(f)))
+        return bool(f.value)
+
+    def string(self, key: str) -> str:
+        buf = C.create_string_buffer(4096)
+        check(lib().bf_params_get_string(self.h, key.encode(), buf, C.c_size_t(4096)))
+        return buf.value.decode()
+
+    def floats(self, key: str) -> np.ndarray:
+        n = C.c_uint32()
+        check(lib().bf_params_get_floats(self.h, key.encode(), None, 0, C.byref(n)))
+        out = (C.c_float * max(1, n.value))()
+        check(lib().bf_params_get_floats(self.h, key.encode(), out, n.value, C.byref(n)))
+        return np.array(out[:n.value], np.float32)
+
+    def number(self, key: str) -> float:
+        v = C.c_double()
+        check(lib().bf_params_get_number(self.h, key.encode(), C.byref(v)))
+        return v.value
+
+    def boolean(self, key: str) -> bool:
+        v = C.c_int()
+        check(lib().bf_params_get_bool(self.h, key.encode(), C.byref(v)))
+        return bool(v.value)
+
+    def hash_params(self) -> BFHashParams:
+        p = BFHashParams()
+        check(lib().bf_params_hash_params(self.h, C.byref(p)))
+        return p
+
+    def raycast_params(self, fx, fy, mx, my) -> BFRayCastParams:
+        p = BFRayCastParams()
+        check(lib().bf_params_raycast_params(self.h, C.c_float(fx), C.c_float(fy), C.c_float(mx), C.c_float(my),
+                                             C.byref(p)))
+        return p
+
+    def preprocess_options(self, depth_shift=1000.0) -> BFPreprocessOptions:
+        o = BFPreprocessOptions()
+        check(lib().bf_params_preprocess_options(self.h, C.c_float(depth_shift), C.byref(o)))
+        return o
+
+
+def preprocess_options(erode=True, structure=3, erode_thresh=0.05, erode_fraction=0.3, depth_filter=True,
+                       sigma_d=2.0, sigma_r=0.05, depth_shift=1000.0) -> BFPreprocessOptions:
+    """zParametersBundlingDefault.txt values (s_erodeSIFTdepth, s_depthFilter, s_depthSigmaD/R)."""
+    return BFPreprocessOptions(1 if erode else 0, structure, erode_thresh, erode_fraction, 1 if depth_filter else 0,
+                               sigma_d, sigma_r, depth_shift)
+
+
+class Preprocessor:
+    """CUDAImageManager::process on the GPU: device in, device out."""
+
+    def __init__(self, depth_wh, color_wh, integration_wh, opts: BFPreprocessOptions):
+        self.h = C.c_void_p()
+        check(lib().bf_preproc_create(depth_wh[0], depth_wh[1], color_wh[0], color_wh[1], integration_wh[0],
+                                      integration_wh[1], C.byref(opts), C.byref(self.h)))
+        self.iw, self.ih = integration_wh
+
+    def __del__(self):
+        try:
+            lib().bf_preproc_destroy(self.h)
+        except Exception:
+            pass
+
+    def run(self, depth_u16: DeviceArray, rgbx: DeviceArray | None, depth_out: DeviceArray, color_out: DeviceArray | None):
+        check(lib().bf_preproc_run(self.h, depth_u16.ptr, rgbx.ptr if rgbx is not None else None, depth_out.ptr,
+                                   color_out.ptr if color_out is not None else None))
+        check(lib().bf_preproc_synchronize(self.h))

@@ -297,6 +297,57 @@ int bf_traj_frame_info(bf_traj* t, uint32_t idx, int32_t* type, float* dist);
 /* PoseHelper::MatrixToPose (PoseHelper.h:332-362): out[6] = [translation part | omega] */
 int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]);
 
+/* ---- input formats and preprocessing ------------------------------------ */
+/* .sens reader (mLib SensorData v4 as SensorDataReader.cpp:38-116 uses it; format restated in
+ * SURVEY.md Appendix B). Frames are read on demand. Depth: raw or zlib ushort; colour: raw RGB
+ * (png / jpeg and occi return BF_ERR_ARG: no decoder in this build). */
+typedef struct bf_sens bf_sens;
+int bf_sens_open(const char* path, bf_sens** out);
+int bf_sens_close(bf_sens* s);
+int bf_sens_info(const bf_sens* s, BFSensInfo* out);
+int bf_sens_frame_pose(const bf_sens* s, uint64_t frame, float camToWorld[16]);
+int bf_sens_frame_timestamps(const bf_sens* s, uint64_t frame, uint64_t* tsColor, uint64_t* tsDepth);
+int bf_sens_read_depth_u16(bf_sens* s, uint64_t frame, uint16_t* out);      /* host, depthW*depthH */
+/* SensorDataReader::processDepth (:104-107): d / depthShift, 0 -> -inf */
+int bf_sens_read_depth(bf_sens* s, uint64_t frame, float* out);             /* host, depthW*depthH */
+int bf_sens_read_color(bf_sens* s, uint64_t frame, uint8_t* rgbx);           /* host, colorW*colorH*4, X = 255 */
+/* writer (SensorData::saveToFile layout; numFrames patched on close): raw RGB colour, raw or zlib depth */
+typedef struct bf_sens_writer bf_sens_writer;
+int bf_sens_writer_create(const char* path, const BFSensInfo* info, bf_sens_writer** out);
+int bf_sens_writer_add_frame(bf_sens_writer* w, const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth,
+                             const uint16_t* depth, const uint8_t* rgbx);
+int bf_sens_writer_close(bf_sens_writer* w);
+
+/* zParameters*.txt (mLib ParameterFile behind GlobalAppState / GlobalBundlingState): later loads
+ * override earlier keys. Getters return BF_ERR_ARG for a missing key (the reference warns and
+ * default-constructs, GlobalAppState.h:129-131). */
+typedef struct bf_params bf_params;
+int bf_params_create(bf_params** out);
+int bf_params_load(bf_params* p, const char* path);
+int bf_params_destroy(bf_params* p);
+int bf_params_has(const bf_params* p, const char* key, int* found);
+int bf_params_get_string(const bf_params* p, const char* key, char* buf, size_t cap); /* quotes stripped */
+int bf_params_get_floats(const bf_params* p, const char* key, float* out, uint32_t cap, uint32_t* count);
+int bf_params_get_number(const bf_params* p, const char* key, double* out);
+int bf_params_get_bool(const bf_params* p, const char* key, int* out);
+/* CUDASceneRepHashSDF::parametersFromGlobalAppState (CUDASceneRepHashSDF.h:39-59) */
+int bf_params_hash_params(const bf_params* p, BFHashParams* out);
+/* CUDARayCastSDF::parametersFromGlobalAppState (CUDARayCastSDF.h:24-51) for integration intrinsics
+ * fx, fy, mx, my at s_integrationWidth x s_integrationHeight */
+int bf_params_raycast_params(const bf_params* p, float fx, float fy, float mx, float my, BFRayCastParams* out);
+/* CUDAImageManager's preprocessing options from the bundling parameters */
+int bf_params_preprocess_options(const bf_params* p, float depthShift, BFPreprocessOptions* out);
+
+/* CUDAImageManager::process (CUDAImageManager.cpp:22-158): ushort depth -> metres, erodeDepthMap x2,
+ * gaussFilterDepthMap, nearest resampling of depth and colour to the integration size. All image
+ * pointers are device pointers; work is queued on the handle's stream. */
+typedef struct bf_preproc bf_preproc;
+int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_t colorH, uint32_t integrationW,
+                      uint32_t integrationH, const BFPreprocessOptions* opt, bf_preproc** out);
+int bf_preproc_destroy(bf_preproc* p);
+int bf_preproc_run(bf_preproc* p, const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut);
+int bf_preproc_synchronize(bf_preproc* p);
+
 #ifdef __cplusplus
 }
 #endif

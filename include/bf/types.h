@@ -150,6 +150,35 @@ typedef struct BFTsdfStats {
     uint64_t batchEvals;      /* voxel-op evaluations (projection + band test) of the batch passes */
 } BFTsdfStats;
 
+/* mLib SensorData v4 header (SensorDataReader.cpp:45-60 reads these fields) */
+typedef struct BFSensInfo {
+    uint32_t version;              /* 4 */
+    char sensorName[256];          /* truncated to 255 chars */
+    float colorIntrinsic[16];      /* row-major mat4f */
+    float colorExtrinsic[16];
+    float depthIntrinsic[16];
+    float depthExtrinsic[16];
+    int32_t colorCompression;      /* -1 unknown, 0 raw (RGB, 3 B per pixel), 1 png, 2 jpeg */
+    int32_t depthCompression;      /* -1 unknown, 0 raw ushort, 1 zlib ushort, 2 occi */
+    uint32_t colorWidth, colorHeight, depthWidth, depthHeight;
+    float depthShift;              /* ushort / depthShift = metres (1000) */
+    uint32_t reserved;
+    uint64_t numFrames;
+} BFSensInfo;
+
+/* CUDAImageManager::process (CUDAImageManager.cpp:22-158) input preprocessing; defaults in
+ * brackets are zParametersBundlingDefault.txt's. */
+typedef struct BFPreprocessOptions {
+    int32_t erode;                 /* s_erodeSIFTdepth [1]: 2 passes of erodeDepthMap */
+    int32_t erodeStructureSize;    /* [3] */
+    float erodeDepthThresh;        /* [0.05] */
+    float erodeFraction;           /* [0.3] */
+    int32_t depthFilter;           /* s_depthFilter [1]: gaussFilterDepthMap */
+    float sigmaD;                  /* s_depthSigmaD [2.0] */
+    float sigmaR;                  /* s_depthSigmaR [0.05] */
+    float depthShift;              /* ushort -> metres divisor [1000] */
+} BFPreprocessOptions;
+
 #ifdef __cplusplus
 } /* extern "C" */
 

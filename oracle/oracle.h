@@ -99,6 +99,11 @@ void or_traj_update_optimized(void* h, const float* T, unsigned numFrames);
 unsigned or_traj_next_fixes(void* h, unsigned maxFixes, int* kinds, unsigned* frames, float* oldT, float* newT);
 void or_traj_frame_info(void* h, unsigned idx, int* type, float* dist);
 
+/* ---- input preprocessing (CUDAImageManager::process) ---------------------- */
+void or_preprocess(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh,
+                   const uint8_t* rgbx, uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, float* depthOut,
+                   uint8_t* colorOut);
+
 #ifdef __cplusplus
 }
 #endif

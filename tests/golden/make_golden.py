@@ -32,7 +32,17 @@ def tsdf_frame0():
     return keys, v["sdf"].copy(), v["weight"].copy(), v["color"].copy(), o.getHeapFreeCount()
 
 
+def sens_fixture():
+    """tests/golden/sens_3x40x30.sens + .npz: the independent Appendix-B encoder of tests/test_io.py on
+    seeded frames (a layout pin for the C++ reader, not a reference output)."""
+    from test_io import encode_sens, synth_frames
+    depth, rgbx, poses, K = synth_frames(F=3, w=40, h=30, seed=0)
+    open(os.path.join(HERE, "sens_3x40x30.sens"), "wb").write(encode_sens(depth, rgbx, poses, K))
+    np.savez_compressed(os.path.join(HERE, "sens_3x40x30.npz"), depth=depth, rgbx=rgbx, poses=poses)
+
+
 if __name__ == "__main__":
+    sens_fixture()
     keys, sdf, weight, color, heap_free = tsdf_frame0()
     np.savez_compressed(os.path.join(HERE, "tsdf_frame0_80x60.npz"), keys=keys, sdf=sdf, weight=weight,
                         color=color, heap_free=np.int64(heap_free))

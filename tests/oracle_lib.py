@@ -25,6 +25,9 @@ def lib() -> C.CDLL:
         if not os.path.exists(ORACLE_LIB):
             build_oracle()
         L = C.CDLL(ORACLE_LIB)
+        L.or_preprocess.restype = None
+        L.or_preprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
         L.or_scene_create.restype = C.c_void_p
         L.or_scene_create.argtypes = [C.c_void_p]
         for n in ("or_scene_destroy", "or_scene_reset", "or_scene_garbage_collect"):
@@ -206,3 +209,22 @@ def bucket_of(key, num_buckets: int) -> int:
     if res < 0:
         res += num_buckets
     return res
+
+
+def preprocess(opts, depth_u16, rgbx, integration_wh):
+    """Oracle of CUDAImageManager::process (oracle/frames.cpp)."""
+    import numpy as np
+    depth_u16 = np.ascontiguousarray(depth_u16, np.uint16)
+    dh, dw = depth_u16.shape
+    iw, ih = integration_wh
+    out_d = np.zeros((ih, iw), np.float32)
+    out_c = np.zeros((ih, iw, 4), np.uint8)
+    cp = None
+    ch = cw = 0
+    if rgbx is not None:
+        rgbx = np.ascontiguousarray(rgbx, np.uint8)
+        ch, cw = rgbx.shape[:2]
+        cp = rgbx.ctypes.data_as(C.c_void_p)
+    lib().or_preprocess(C.byref(opts), depth_u16.ctypes.data_as(C.c_void_p), dw, dh, cp, cw, ch, iw, ih,
+                        out_d.ctypes.data_as(C.c_void_p), out_c.ctypes.data_as(C.c_void_p))
+    return out_d, (out_c if rgbx is not None else None)
