@@ -188,6 +188,13 @@ def main():
     so = BFSceneOptions()
     so.shardCount, so.shardIndex, so.shardChunk = world, rank, 1.0
     rc = Recon(params, stream.cam, opts, so)
+    comm = None
+    if world > 1 and os.environ.get("BF_BA_SHARD", "1") != "0":
+        # global BA: image-pair normal-equation blocks sharded over the ranks, one RCCL all-reduce
+        # per GN iteration; the PCG then runs replicated on every GPU
+        from bundlefusion_amd.dist import Comm
+        comm = Comm(group)
+        rc.set_comm(comm)
     stream.attach(rc)
     log(f"setup {time.perf_counter() - t_setup:.1f}s: {F} frames, {K} keyframes, "
         f"{len(stream.global_host)} global correspondences")
@@ -259,7 +266,8 @@ def main():
                                f"2^{args.buckets.bit_length() - 1} buckets, 2^{args.blocks.bit_length() - 1} blocks; "
                                f"local 2x100 + global 3x150 GN x PCG per submap",
                    "frames_timed": frames, "keyframes_final": K,
-                   "parallelism": f"tsdf-chunk-shard{world}+ba-replicated" if world > 1 else "single"},
+                   "parallelism": (f"tsdf-chunk-shard{world}+ba-pair-shard{world}-rccl" if comm is not None
+                                   else f"tsdf-chunk-shard{world}+ba-replicated") if world > 1 else "single"},
         "ms_per_gn_iter": solo["ms_per_gn_iter"],
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
         "roofline": {"bound": "hbm", "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,
@@ -316,6 +324,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     rc.close()
+    if comm is not None:
+        comm.close()
     group.close()
 
 

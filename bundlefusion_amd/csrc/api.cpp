@@ -111,6 +111,9 @@ struct bf_solver {
     hipStream_t stream = nullptr;
     Solver* solver = nullptr;
 };
+struct bf_comm {
+    Comm* c = nullptr;
+};
 struct bf_sens {
     SensReader* r = nullptr;
 };
@@ -513,6 +516,62 @@ int bf_solver_check_invalid_frames(bf_solver* s, int* valid, uint32_t nImages, B
     BF_CATCH
 }
 
+int bf_solver_set_shard(bf_solver* s, uint32_t count, uint32_t index, bf_comm* comm) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null argument");
+    s->solver->setShard(count, index, comm ? comm->c : nullptr);
+    BF_CATCH
+}
+int bf_solver_export_pairs(bf_solver* s, double* stats, int32_t* pairAB, uint32_t cap, uint32_t* total) {
+    BF_TRY
+    BF_REQUIRE(s && total, BF_ERR_ARG, "null argument");
+    *total = s->solver->exportPairs(stats, pairAB, cap);
+    BF_CATCH
+}
+
+// ---- multi-GPU communicator (RCCL) --------------------------------------------------------
+int bf_comm_unique_id(uint8_t id[128]) {
+    BF_TRY
+    BF_REQUIRE(id, BF_ERR_ARG, "null argument");
+    Comm::uniqueId(id);
+    BF_CATCH
+}
+int bf_comm_create(const uint8_t id[128], int nranks, int rank, bf_comm** out) {
+    BF_TRY
+    BF_REQUIRE(id && out, BF_ERR_ARG, "null argument");
+    bf_comm* h = new bf_comm();
+    try {
+        h->c = new Comm(id, nranks, rank);
+    } catch (...) {
+        delete h;
+        throw;
+    }
+    *out = h;
+    BF_CATCH
+}
+int bf_comm_destroy(bf_comm* c) {
+    BF_TRY
+    if (c) {
+        delete c->c;
+        delete c;
+    }
+    BF_CATCH
+}
+int bf_comm_allreduce_sum_f64(bf_comm* c, double* d, size_t n) {
+    BF_TRY
+    BF_REQUIRE(c && (d || n == 0), BF_ERR_ARG, "null argument");
+    hipStream_t st = nullptr;
+    BF_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    try {
+        c->c->allreduceSum(d, n, st);
+        BF_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        (void)hipStreamDestroy(st);
+        throw;
+    }
+    BF_HIP(hipStreamDestroy(st));
+    BF_CATCH
+}
 
 // ---- reconstruction loop ----------------------------------------------------------------
 struct bf_recon {
@@ -646,6 +705,12 @@ int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches) {
     if (!clk.enabled()) clk.enable(true);
     *ms = clk.totalMs();
     *launches = clk.launches();
+    BF_CATCH
+}
+int bf_recon_set_comm(bf_recon* r, bf_comm* c) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null argument");
+    r->r->setComm(c ? c->c : nullptr);
     BF_CATCH
 }
 int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n) {

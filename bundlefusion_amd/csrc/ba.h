@@ -23,6 +23,7 @@
 #include "../../include/bf/bf.h"
 #include "bf_math.h"
 #include "bf_runtime.h"
+#include "comm.h"
 
 namespace bf {
 
@@ -37,6 +38,7 @@ struct SolverConfig {
     float denseDepthMax;          // s_denseDepthMax 4.0
     uint32_t denseOverlapSubsample;  // s_denseOverlapCheckSubsampleFactor 4
     float verifyOptDistThresh;    // 0.02 (CUDASolverBundling.cpp:34)
+    int normalEquations;          // 0 auto (assembled for sparse-only solves), 1 matrix-free, 2 assembled
 };
 
 struct SolveArgs {
@@ -55,6 +57,7 @@ struct SolveArgs {
     float* trans;  // device float3[numImages], in/out
     bool rebuildJT;
     bool findMaxResidual;
+    uint32_t pairBound = 0;  // host-known upper bound on image pairs (sharded solves; 0: read it back)
 };
 
 struct SolveResult {
@@ -86,6 +89,12 @@ public:
     hipStream_t stream() const { return stream_; }
     const SolverConfig& config() const { return cfg_; }
     size_t deviceBytes() const;
+    // sharded global solve: this handle builds the normal-equation blocks of the
+    // image pairs p with p % count == index; comm (may be null: no exchange, tests) sums them
+    void setShard(uint32_t count, uint32_t index, Comm* comm);
+    // assembled normal equations of the last GN iteration: per pair (a, b) the 28 sufficient
+    // statistics (see ba.hip, k_pair_stats); synchronizes
+    uint32_t exportPairs(double* stats, int* pairAB, uint32_t cap);
     KernelClock& solveClock() { return solveClock_; }  // whole-solve device time (ms/GN-iter)
 
 private:
@@ -118,6 +127,17 @@ private:
     DevBuf<float> diag_;     // [N][36]
     DevBuf<float> jtr_;      // [N][6]
     DevBuf<float> apDense_;  // [N][8]
+    // assembled (pair) normal equations
+    uint32_t maxPairsA_ = 0;
+    uint32_t shardCount_ = 1, shardIndex_ = 0;
+    Comm* comm_ = nullptr;
+    bool pairTable_ = false;       // pair table built for the current row table
+    uint32_t pairCountHost_ = 0;   // read back once per table build when a sharded solve needs it
+    bool lastPairMode_ = false;
+    DevBuf<int> rowSorted_, rowOther_, rowDeg_, rowNA_, pairStart_, rowPairStart_, pairA_, pairB_;
+    DevBuf<int2> pairCorr_, rowPair_;
+    DevBuf<double> pstat_, dstat_;
+    DevBuf<float> apPair_, rzPart_;
 };
 
 SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* opts);

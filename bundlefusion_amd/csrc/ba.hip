@@ -34,7 +34,7 @@ enum VecField { V_DELTA = 0, V_R, V_Z, V_P, V_AP, V_M, V_NUM };
 enum CtrlWord {
     K_TICKET = 0, K_PCG_DONE, K_GN_DONE, K_GN_ITERS, K_PCG_ITERS, K_RDOTZ, K_NPAIRS, K_LAST_W,
     K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J, K_COUNT = 16,
-    K_NCHUNK = K_COUNT,
+    K_NCHUNK = K_COUNT, K_NPAIRS_A,
     K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
 };
 
@@ -72,6 +72,12 @@ struct BA {
     float fx, fy, mx, my;
     float distT, normT, colT, gradMin, dmin, dmax, verifyT;
     uint32_t sub;
+    // assembled normal equations (pair mode)
+    int *rowSorted, *rowOther, *rowDeg, *rowNA, *pairStart, *rowPairStart, *pairA, *pairB;
+    int2 *pairCorr, *rowPair;
+    double *pstat, *dstat;
+    float *apPair, *rzPart;
+    uint32_t pairMode, shardCount, shardIndex, pairBound;
 };
 
 __device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -376,6 +382,247 @@ __device__ __forceinline__ void chunk_range(const BA& a, uint32_t c, uint32_t& v
     k1 = min(s0 + a.rowLen[v], k0 + CH);
 }
 
+// ---- assembled normal equations (pair mode) ---------------------------------------------------
+// The reference applies J^T J matrix-free: every PCG iteration streams all correspondences
+// (applyJDevice / applyJTDevice, SolverBundlingEquationsLie.h:154-228). For a sparse-only solve the
+// same operator is a sum over image pairs of 6x6 blocks, and with A_v = [-[P_v]x | I] (P_v = T_v p_v,
+// the world point of a correspondence in image v) every block is fixed by a few sums over the pair's
+// correspondences (a < b, P_a / P_b the two world points):
+//   M = sum P_b P_a^T (9), s_a = sum P_a, s_b = sum P_b, n, Q_a = sum P_a P_a^T, Q_b = sum P_b P_b^T (6 each)
+//   sum A_a^T A_b = [[tr(M) I - M, [s_a]x], [-[s_b]x, n I]]          (off-diagonal, row a)
+//   sum A_v^T A_v = [[tr(Q) I - Q, [s]x], [-[s]x, n I]]              (diagonal, summed over v's pairs)
+//   sum A_v^T r  = (-/+ (sum P_a x P_b), s_v - s_u)                     (J^T F, r = P_v - P_u)
+// The statistics are accumulated in fp64 (products of fp32 points are exact in fp64), so the
+// blocks keep the cancellation D_v p_v - sum_u B_vu p_u accurate. A PCG iteration then reads 128 B
+// per (row, pair) entry instead of 64 B per (row, correspondence) entry. Pair p is built by shard
+// p % shardCount; every other shard writes zeros, so the RCCL sum over shards reproduces the
+// single-GPU statistics bit for bit (x + 0 = x), and the replicated PCG that follows is identical on
+// every GPU (one all-reduce per GN iteration).
+constexpr int PSTAT = 28;        // doubles per pair: M[9] s_a[3] s_b[3] n Q_a[6] Q_b[6]
+constexpr int DSTAT = 10;        // doubles per image: Q[6] s[3] n
+constexpr uint32_t SORT_MAX = 4096;  // >= maxCorrPerImage (4000)
+constexpr uint32_t ROW_POS_BITS = 12;
+constexpr uint32_t PAIR_A_FLAG = 0x80000000u;
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// per row v: the row's entries ordered by (other image, position) — position order is ascending
+// correspondence index — with the row's distinct partners counted (rowDeg) and those above v (rowNA)
+__global__ __launch_bounds__(WG) void k_pair_sort(BA a) {
+    __shared__ uint32_t key[SORT_MAX];
+    __shared__ int shd[WG / 64], sha[WG / 64];
+    const uint32_t v = blockIdx.x;
+    const int n = a.rowLen[v], s0 = a.rowStart[v];
+    uint32_t P = 1;
+    while (P < (uint32_t)n) P <<= 1;
+    for (uint32_t t = threadIdx.x; t < P; t += WG) {
+        uint32_t k = 0xFFFFFFFFu;
+        if ((int)t < n) {
+            const int c = a.rowIdx[s0 + t];
+            const uint2 ij = *reinterpret_cast<const uint2*>(&a.corr[c].imgIdx_i);
+            const uint32_t u = (ij.x == v) ? ij.y : ij.x;
+            k = (u << ROW_POS_BITS) | t;
+        }
+        key[t] = k;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1) {  // bitonic sort, ascending
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P / 2; t += WG) {
+                const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
+                const uint32_t x = key[i], y = key[j];
+                if ((x > y) == ((i & size) == 0)) { key[i] = y; key[j] = x; }
+            }
+            __syncthreads();
+        }
+    }
+    int deg = 0, na = 0;
+    for (uint32_t t = threadIdx.x; t < (uint32_t)n; t += WG) {
+        const uint32_t k = key[t], u = k >> ROW_POS_BITS;
+        a.rowSorted[s0 + t] = a.rowIdx[s0 + (k & ((1u << ROW_POS_BITS) - 1))];
+        a.rowOther[s0 + t] = (int)u;
+        const bool head = (t == 0 || (key[t - 1] >> ROW_POS_BITS) != u) && u != v;  // self pairs are skipped
+        deg += head ? 1 : 0;
+        na += (head && u > v) ? 1 : 0;
+    }
+    for (int off = 32; off > 0; off >>= 1) { deg += __shfl_xor(deg, off); na += __shfl_xor(na, off); }
+    if ((threadIdx.x & 63) == 0) { shd[threadIdx.x >> 6] = deg; sha[threadIdx.x >> 6] = na; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int d = 0, m = 0;
+        for (int w = 0; w < WG / 64; w++) { d += shd[w]; m += sha[w]; }
+        a.rowDeg[v] = d;
+        a.rowNA[v] = m;
+    }
+}
+// one workgroup: exclusive scans rowNA -> pairStart (pairs (a, b > a) numbered in (a, b) order) and
+// rowDeg -> rowPairStart (each row's incident pairs)
+__device__ void block_exclusive_scan(const int* in, int* out, uint32_t n, int* sh) {
+    int carry = 0;
+    for (uint32_t base = 0; base < n; base += WG) {
+        const uint32_t v = base + threadIdx.x;
+        const int c = v < n ? in[v] : 0;
+        sh[threadIdx.x] = c;
+        __syncthreads();
+        for (int off = 1; off < WG; off <<= 1) {
+            const int x = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (v < n) out[v] = carry + sh[threadIdx.x] - c;
+        carry += sh[WG - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+    __syncthreads();
+}
+__global__ void k_pair_scan(BA a) {
+    __shared__ int sh[WG];
+    block_exclusive_scan(a.rowNA, a.pairStart, a.N, sh);
+    block_exclusive_scan(a.rowDeg, a.rowPairStart, a.N, sh);
+    if (threadIdx.x == 0) a.ctrl[K_NPAIRS_A] = (uint32_t)a.pairStart[a.N];
+}
+// one wave per row: segments (runs of one partner u) of the sorted row. Row a numbers its pairs with
+// u > a and records their correspondence runs; the row entries of pairs with u < a are filled by
+// k_pair_rows once every pair has its number.
+__device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
+template <bool OWN>
+__device__ void pair_segments(const BA& a, uint32_t v) {
+    const uint32_t lane = lane_id();
+    const int n = a.rowLen[v], s0 = a.rowStart[v];
+    int seg = 0, segA = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int t = base + (int)lane;
+        const int u = t < n ? a.rowOther[s0 + t] : -1;
+        const int prev = (t > 0 && t < n) ? a.rowOther[s0 + t - 1] : -1;
+        const bool head = t < n && u != prev && u != (int)v;
+        const uint64_t mh = __ballot(head), ma = __ballot(head && u > (int)v);
+        const int rank = seg + __popcll(mh & lanes_below(lane));
+        if (head) {
+            if (OWN && u > (int)v) {
+                int e = t + 1;
+                while (e < n && a.rowOther[s0 + e] == u) e++;
+                const int p = a.pairStart[v] + segA + __popcll(ma & lanes_below(lane));
+                a.pairA[p] = (int)v;
+                a.pairB[p] = u;
+                a.pairCorr[p] = make_int2(s0 + t, e - t);
+                a.rowPair[a.rowPairStart[v] + rank] = make_int2(p, (int)((uint32_t)u | PAIR_A_FLAG));
+            } else if (!OWN && u < (int)v) {  // pair (u, v): binary search v in u's partner list
+                int lo = a.pairStart[u], hi = a.pairStart[u + 1] - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (a.pairB[mid] < (int)v) lo = mid + 1; else hi = mid;
+                }
+                a.rowPair[a.rowPairStart[v] + rank] = make_int2(lo, u);
+            }
+        }
+        seg += __popcll(mh);
+        segA += __popcll(ma);
+    }
+}
+__global__ __launch_bounds__(64) void k_pair_fill(BA a) { pair_segments<true>(a, blockIdx.x); }
+__global__ __launch_bounds__(64) void k_pair_rows(BA a) { pair_segments<false>(a, blockIdx.x); }
+
+// per GN iteration: the sufficient statistics of every pair of this shard (one wave per pair,
+// lanes over its correspondences in ascending index order, fixed butterfly); pairs of other shards
+// and slots in [nPairs, pairBound) are written as zeros
+__global__ __launch_bounds__(WG) void k_pair_stats(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t np = a.ctrl[K_NPAIRS_A];
+    const uint32_t bound = a.pairBound > np ? a.pairBound : np;
+    if (a.pairBound && np > a.pairBound && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&a.ctrl[K_ERROR], 4u);
+    for (uint32_t p = wave; p < bound; p += nw) {
+        double* out = a.pstat + (size_t)p * PSTAT;
+        if (p >= np || p % a.shardCount != a.shardIndex) {
+            if (lane < PSTAT) out[lane] = 0.0;
+            continue;
+        }
+        const uint32_t pa = (uint32_t)a.pairA[p], pb = (uint32_t)a.pairB[p];
+        const int2 run = a.pairCorr[p];
+        const m4 Ta = loadm4(a.T + (size_t)pa * 16), Tb = loadm4(a.T + (size_t)pb * 16);
+        double M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, sa[3] = {0, 0, 0}, sb[3] = {0, 0, 0}, cnt = 0.0;
+        double qa[6] = {0, 0, 0, 0, 0, 0}, qb[6] = {0, 0, 0, 0, 0, 0};
+        for (int k = (int)lane; k < run.y; k += 64) {
+            const BFEntryJ e = a.corr[a.rowSorted[run.x + k]];
+            const bool aIsI = e.imgIdx_i == pa;
+            const f3 pA = aIsI ? mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z) : mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z);
+            const f3 pB = aIsI ? mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z) : mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z);
+            const f3 A3 = xf(Ta, pA), B3 = xf(Tb, pB);  // the world points of k_entries
+            const double A[3] = {A3.x, A3.y, A3.z}, B[3] = {B3.x, B3.y, B3.z};
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) M[r * 3 + c] += B[r] * A[c];
+                sa[r] += A[r];
+                sb[r] += B[r];
+            }
+            qa[0] += A[0] * A[0]; qa[1] += A[0] * A[1]; qa[2] += A[0] * A[2];
+            qa[3] += A[1] * A[1]; qa[4] += A[1] * A[2]; qa[5] += A[2] * A[2];
+            qb[0] += B[0] * B[0]; qb[1] += B[0] * B[1]; qb[2] += B[0] * B[2];
+            qb[3] += B[1] * B[1]; qb[4] += B[1] * B[2]; qb[5] += B[2] * B[2];
+            cnt += 1.0;
+        }
+        double s[PSTAT];
+#pragma unroll
+        for (int q = 0; q < 9; q++) s[q] = M[q];
+#pragma unroll
+        for (int q = 0; q < 3; q++) { s[9 + q] = sa[q]; s[12 + q] = sb[q]; }
+        s[15] = cnt;
+#pragma unroll
+        for (int q = 0; q < 6; q++) { s[16 + q] = qa[q]; s[22 + q] = qb[q]; }
+#pragma unroll
+        for (int q = 0; q < PSTAT; q++) s[q] = wave_sum_d(s[q]) + 0.0;  // + 0.0: no -0 (exact shard sums)
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < PSTAT; q += 2) *reinterpret_cast<double2*>(out + q) = make_double2(s[q], s[q + 1]);
+        }
+    }
+}
+
+// B_vu p_u for the row entry (pair p, orientation): rot = tr(M) w - M w + s_v x t, trans = -s_u x w + n t,
+// with M = sum P_u P_v^T (the pair's M for v = a, its transpose for v = b)
+__device__ __forceinline__ void pair_block_apply(const double* st, bool vIsA, const double w[3], const double t[3],
+                                                 double o[6]) {
+    double M[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++) M[q] = st[q];
+    const double* sv = vIsA ? st + 9 : st + 12;
+    const double* su = vIsA ? st + 12 : st + 9;
+    const double n = st[15];
+    const double tr = M[0] + M[4] + M[8];
+    double Mw[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+        Mw[r] = vIsA ? (M[r * 3] * w[0] + M[r * 3 + 1] * w[1] + M[r * 3 + 2] * w[2])
+                     : (M[r] * w[0] + M[3 + r] * w[1] + M[6 + r] * w[2]);
+    o[0] = tr * w[0] - Mw[0] + (sv[1] * t[2] - sv[2] * t[1]);
+    o[1] = tr * w[1] - Mw[1] + (sv[2] * t[0] - sv[0] * t[2]);
+    o[2] = tr * w[2] - Mw[2] + (sv[0] * t[1] - sv[1] * t[0]);
+    o[3] = -(su[1] * w[2] - su[2] * w[1]) + n * t[0];
+    o[4] = -(su[2] * w[0] - su[0] * w[2]) + n * t[1];
+    o[5] = -(su[0] * w[1] - su[1] * w[0]) + n * t[2];
+}
+// D_v p_v from the image statistics Q (xx xy xz yy yz zz), s, n
+__device__ __forceinline__ void diag_apply(const double* d, const double w[3], const double t[3], double o[6]) {
+    const double Q[9] = {d[0], d[1], d[2], d[1], d[3], d[4], d[2], d[4], d[5]};
+    const double* s = d + 6;
+    const double n = d[9], tr = d[0] + d[3] + d[5];
+#pragma unroll
+    for (int r = 0; r < 3; r++) o[r] = tr * w[r] - (Q[r * 3] * w[0] + Q[r * 3 + 1] * w[1] + Q[r * 3 + 2] * w[2]);
+    o[0] += s[1] * t[2] - s[2] * t[1];
+    o[1] += s[2] * t[0] - s[0] * t[2];
+    o[2] += s[0] * t[1] - s[1] * t[0];
+    o[3] = -(s[1] * w[2] - s[2] * w[1]) + n * t[0];
+    o[4] = -(s[2] * w[0] - s[0] * w[2]) + n * t[1];
+    o[5] = -(s[0] * w[1] - s[1] * w[0]) + n * t[2];
+}
+
 // ---- per GN iteration -------------------------------------------------------------------------
 // convertLiePosesToMatricesCU (SolverBundling.cu:1114-1121); also resets the PCG state of this
 // GN iteration. gated: no-op once the GN loop converged on the device.
@@ -408,8 +655,7 @@ __device__ __forceinline__ void put_part(const BA& a, uint32_t c, int f, f3 s) {
     st_wt(a.chunkPart + (size_t)c * 3 + f, make_float4(s.x, s.y, s.z, 0.0f));
 }
 // PCGInit per row: r = -Jtr, Jacobi preconditioner, p = M r; returns r.z
-__device__ float init_row(const BA& a, uint32_t v, f3 rr, f3 rt, f3 pr, float wSparse, int useDense) {
-    const float cnt = (float)a.rowLen[v];
+__device__ float init_row_cnt(const BA& a, uint32_t v, f3 rr, f3 rt, f3 pr, float cnt, float wSparse, int useDense) {
     f3 resR = mk3(-wSparse * rr.x, -wSparse * rr.y, -wSparse * rr.z);
     f3 resT = mk3(-wSparse * rt.x, -wSparse * rt.y, -wSparse * rt.z);
     if (useDense) {
@@ -426,6 +672,9 @@ __device__ float init_row(const BA& a, uint32_t v, f3 rr, f3 rt, f3 pr, float wS
     vstore(a, V_P, v, pR, pT);
     vstore(a, V_DELTA, v, mk3(0, 0, 0), mk3(0, 0, 0));
     return dot3(resR, pR) + dot3(resT, pT);
+}
+__device__ float init_row(const BA& a, uint32_t v, f3 rr, f3 rt, f3 pr, float wSparse, int useDense) {
+    return init_row_cnt(a, v, rr, rt, pr, (float)a.rowLen[v], wSparse, useDense);
 }
 
 // world points of every row entry for this GN iteration: {T_self p_self, other}, {T_other p_other}
@@ -565,6 +814,13 @@ __device__ __forceinline__ void pcg_sparse_chunks(const BA& a, float wSparse, ui
 // Ap of row v for the finisher: the sparse part handed over by the row's last chunk wave, plus the
 // dense diagonal block and the dense off-diagonal atomics (reset for the next iteration)
 __device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, int useDense, f3 pR, f3 pT, f3& aR, f3& aT) {
+    if (a.pairMode) {  // assembled normal equations: Ap of the row, handed over by its wave
+        const float4* q = reinterpret_cast<const float4*>(a.apPair + (size_t)v * 8);
+        const float4 x = ld_wt(q), y = ld_wt(q + 1);
+        aR = mk3(x.x, x.y, x.z);
+        aT = mk3(y.x, y.y, y.z);
+        return;
+    }
     aR = mk3(0, 0, 0);
     aT = mk3(0, 0, 0);
     if (nch) {  // sparse part: the row's chunk partials, in chunk order
@@ -654,52 +910,9 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
     return rDotzNew;
 }
 
-// One PCG iteration (PCGIteration, SolverBundling.cu:1024-1108) in one launch: every wave
-// computes the sparse JtJp partial of its chunks; waves also apply the dense off-diagonal pair
-// blocks. The last workgroup then sums each row's partials in chunk order, adds the dense diagonal
-// block, does the global dot products and the alpha / beta updates (Kernel1b, Kernel2, Kernel3) and
-// the Lie update on the exiting iteration.
-__global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int nLin) {
-    __shared__ float sh[WG];
-    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
-    const uint32_t lane = lane_id();
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    const unsigned long long tStart = a.probe ? wall_clock64() : 0ull;
-    const int useDense = (int)a.ctrl[K_USE_DENSE];
-    const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
-    pcg_sparse_chunks<false>(a, wSparse, wave, nw, nch);
-    if (useDense) {  // off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j)
-        const uint32_t np = a.ctrl[K_NPAIRS];
-        for (uint32_t k = wave; k < np; k += nw) {
-            if (a.pairW[k] == 0.0f) continue;
-            const uint2 pr = a.pairs[k];
-            const float* Bk = a.pairBlk + (size_t)k * 36;
-            f3 r, t;
-            float o = 0.0f;
-            if (lane < 6) {
-                vload(a, V_P, pr.x, r, t);
-                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-                for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
-                if (pr.y > 0) atomicAdd(&a.apDense[(size_t)pr.y * 8 + (lane < 3 ? 4 + lane : lane - 3)], o);
-            } else if (lane < 12) {
-                vload(a, V_P, pr.y, r, t);
-                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-                const int c0 = lane - 6;
-                for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
-                if (pr.x > 0) atomicAdd(&a.apDense[(size_t)pr.x * 8 + (c0 < 3 ? 4 + c0 : c0 - 3)], o);
-            }
-        }
-    }
-    if (a.probe && threadIdx.x == 0) {
-        __hip_atomic_store((gu64*)&a.probe[16 + 2 * blockIdx.x], (uint64_t)tStart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu64*)&a.probe[17 + 2 * blockIdx.x], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!last_block_sharded(a.sync, 1u)) return;
-    if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
-    const unsigned long long tFin = a.probe ? wall_clock64() : 0ull;
-    // ---- finisher (one workgroup): Kernel1b, Kernel2, host early-out test, Kernel3 ----
-    float rDotzNew;
-    bool last;
+// PCG finisher (one workgroup): Kernel1b, Kernel2, the host early-out test, Kernel3
+__device__ void pcg_finisher(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, float& rDotzNew,
+                             bool& last) {
     if (a.N <= 2 * WG + 1) {
         rDotzNew = pcg_finish_regs<2, false>(a, sh, nch, useDense, iter, nLin, last);
     } else {
@@ -753,6 +966,55 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
         rDotzNew = rDotzNew_;
         last = last_;
     }
+}
+
+// One PCG iteration (PCGIteration, SolverBundling.cu:1024-1108) in one launch: every wave
+// computes the sparse JtJp partial of its chunks; waves also apply the dense off-diagonal pair
+// blocks. The last workgroup then sums each row's partials in chunk order, adds the dense diagonal
+// block, does the global dot products and the alpha / beta updates (Kernel1b, Kernel2, Kernel3) and
+// the Lie update on the exiting iteration.
+__global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int nLin) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const unsigned long long tStart = a.probe ? wall_clock64() : 0ull;
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
+    pcg_sparse_chunks<false>(a, wSparse, wave, nw, nch);
+    if (useDense) {  // off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j)
+        const uint32_t np = a.ctrl[K_NPAIRS];
+        for (uint32_t k = wave; k < np; k += nw) {
+            if (a.pairW[k] == 0.0f) continue;
+            const uint2 pr = a.pairs[k];
+            const float* Bk = a.pairBlk + (size_t)k * 36;
+            f3 r, t;
+            float o = 0.0f;
+            if (lane < 6) {
+                vload(a, V_P, pr.x, r, t);
+                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+                for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
+                if (pr.y > 0) atomicAdd(&a.apDense[(size_t)pr.y * 8 + (lane < 3 ? 4 + lane : lane - 3)], o);
+            } else if (lane < 12) {
+                vload(a, V_P, pr.y, r, t);
+                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+                const int c0 = lane - 6;
+                for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
+                if (pr.x > 0) atomicAdd(&a.apDense[(size_t)pr.x * 8 + (c0 < 3 ? 4 + c0 : c0 - 3)], o);
+            }
+        }
+    }
+    if (a.probe && threadIdx.x == 0) {
+        __hip_atomic_store((gu64*)&a.probe[16 + 2 * blockIdx.x], (uint64_t)tStart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)&a.probe[17 + 2 * blockIdx.x], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!last_block_sharded(a.sync, 1u)) return;
+    if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
+    const unsigned long long tFin = a.probe ? wall_clock64() : 0ull;
+    // ---- finisher (one workgroup): Kernel1b, Kernel2, host early-out test, Kernel3 ----
+    float rDotzNew;
+    bool last;
+    pcg_finisher(a, sh, nch, useDense, iter, nLin, rDotzNew, last);
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
         a.ctrl[K_PCG_ITERS]++;
@@ -772,6 +1034,115 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
             a.probe[2] += t1 - t0; a.probe[3] += tFin - t0; a.probe[4] += t2 - t0; a.probe[5] += 1;
             a.probe[6] += dur / gridDim.x; a.probe[7] += lastStart - t0;
         }
+    }
+}
+
+// Pair mode, per GN iteration after the exchange: one wave per image row v >= 1 sums its incident
+// pairs (in partner order) into D_v (the diagonal block statistics), J^T F and the Jacobi
+// preconditioner, then initialises the row as PCGInit does (evalMinusJTFDevice + PCGInit_Kernel1,
+// SolverBundlingEquationsLie.h:63-148, SolverBundling.cu:755-794); the last workgroup sums r.z.
+__global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+        const int e0 = a.rowPairStart[v], e1 = a.rowPairStart[v + 1];
+        double d[DSTAT + 6];
+#pragma unroll
+        for (int q = 0; q < DSTAT + 6; q++) d[q] = 0.0;
+        for (int k = e0 + (int)lane; k < e1; k += 64) {
+            const int2 rp = a.rowPair[k];
+            const bool vIsA = ((uint32_t)rp.y & PAIR_A_FLAG) != 0;
+            const double* st = a.pstat + (size_t)rp.x * PSTAT;
+            const double* qv = st + (vIsA ? 16 : 22);
+            const double* sv = st + (vIsA ? 9 : 12);
+            const double* su = st + (vIsA ? 12 : 9);
+#pragma unroll
+            for (int q = 0; q < 6; q++) d[q] += qv[q];
+#pragma unroll
+            for (int q = 0; q < 3; q++) d[6 + q] += sv[q];
+            d[9] += st[15];
+            // sum P_v x (P_v - P_u) = -/+ sum P_a x P_b, the antisymmetric part of M = sum P_b P_a^T
+            const double sg = vIsA ? -1.0 : 1.0;
+            d[10] += sg * (st[7] - st[5]);
+            d[11] += sg * (st[2] - st[6]);
+            d[12] += sg * (st[3] - st[1]);
+#pragma unroll
+            for (int q = 0; q < 3; q++) d[13 + q] += sv[q] - su[q];
+        }
+#pragma unroll
+        for (int q = 0; q < DSTAT + 6; q++) d[q] = wave_sum_d(d[q]);
+        if (lane == 0) {
+            double* ds = a.dstat + (size_t)v * DSTAT;
+#pragma unroll
+            for (int q = 0; q < DSTAT; q += 2) *reinterpret_cast<double2*>(ds + q) = make_double2(d[q], d[q + 1]);
+            const f3 rr = mk3((float)d[10], (float)d[11], (float)d[12]);
+            const f3 rt = mk3((float)d[13], (float)d[14], (float)d[15]);
+            // |dAlpha|^2, |dBeta|^2, |dGamma|^2 summed: (Qyy + Qzz, Qxx + Qzz, Qxx + Qyy)
+            const f3 pr = mk3((float)(d[3] + d[5]), (float)(d[0] + d[5]), (float)(d[0] + d[3]));
+            st_wt(&a.rzPart[v], init_row_cnt(a, v, rr, rt, pr, (float)d[9], wSparse, 0));
+        }
+    }
+    if (!last_block(&a.ctrl[K_TICKET])) return;
+    float s = 0.0f;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) s += ld_wtf(&a.rzPart[v]);
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) {
+        a.ctrl[K_RDOTZ] = __float_as_uint(s);
+        a.ctrl[K_TICKET] = 0;
+        for (int w = 0; w < SYNC_WORDS; w += SYNC_LINE) a.sync[w] = 0;
+        vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
+    }
+}
+
+// Pair mode PCG iteration: one wave per row v >= 1, Ap_v = w (D_v p_v - sum_u B_vu p_u) in fp64 over
+// the row's pairs (the same operator as applyJ / applyJT; no second w, SolverBundlingEquationsLie.h:
+// 154-228), handed to the finisher write-through; then the finisher of k_pcg.
+__global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter, int nLin) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+        const int e0 = a.rowPairStart[v], e1 = a.rowPairStart[v + 1];
+        double o[6] = {0, 0, 0, 0, 0, 0};
+        for (int k = e0 + (int)lane; k < e1; k += 64) {
+            const int2 rp = a.rowPair[k];
+            const uint32_t u = (uint32_t)rp.y & ~PAIR_A_FLAG;
+            if (u == 0) continue;  // p_0 = 0 (image 0 fixed)
+            f3 pr, pt;
+            vload(a, V_P, u, pr, pt);
+            const double w[3] = {pr.x, pr.y, pr.z}, t[3] = {pt.x, pt.y, pt.z};
+            double b[6];
+            pair_block_apply(a.pstat + (size_t)rp.x * PSTAT, ((uint32_t)rp.y & PAIR_A_FLAG) != 0, w, t, b);
+#pragma unroll
+            for (int q = 0; q < 6; q++) o[q] += b[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 6; q++) o[q] = wave_sum_d(o[q]);
+        if (lane == 0) {
+            f3 pr, pt;
+            vload(a, V_P, v, pr, pt);
+            const double w[3] = {pr.x, pr.y, pr.z}, t[3] = {pt.x, pt.y, pt.z};
+            double dp[6];
+            diag_apply(a.dstat + (size_t)v * DSTAT, w, t, dp);
+            const double ws = wSparse;
+            float4* q = reinterpret_cast<float4*>(a.apPair + (size_t)v * 8);
+            st_wt(q, make_float4((float)(ws * (dp[0] - o[0])), (float)(ws * (dp[1] - o[1])), (float)(ws * (dp[2] - o[2])), 0.0f));
+            st_wt(q + 1, make_float4((float)(ws * (dp[3] - o[3])), (float)(ws * (dp[4] - o[4])), (float)(ws * (dp[5] - o[5])), 0.0f));
+        }
+    }
+    if (!last_block_sharded(a.sync, 1u)) return;
+    if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
+    float rDotzNew;
+    bool last;
+    pcg_finisher(a, sh, 0u, 0, iter, nLin, rDotzNew, last);
+    if (threadIdx.x == 0) {
+        a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
+        a.ctrl[K_PCG_ITERS]++;
+        if (last) a.ctrl[K_PCG_DONE] = 1;
+        a.ctrl[K_TICKET] = 0;
     }
 }
 
@@ -1241,6 +1612,8 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.denseDepthMax = (o && o->denseDepthMax > 0) ? o->denseDepthMax : 4.0f;
     cfg.denseOverlapSubsample = (o && o->denseOverlapSubsample) ? o->denseOverlapSubsample : 4;
     cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
+    cfg.normalEquations = o ? o->normalEquations : 0;
+    if (const char* e = getenv("BF_NORMAL_EQUATIONS"); e && (!o || o->normalEquations == 0)) cfg.normalEquations = atoi(e);
     return cfg;
 }
 
@@ -1282,6 +1655,22 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     diag_.alloc((size_t)N * 36);
     jtr_.alloc((size_t)N * 6);
     apDense_.alloc((size_t)N * 8);
+    // assembled normal equations: a pair has >= 1 correspondence, so pairs <= min(N(N-1)/2, maxCorr)
+    maxPairsA_ = (uint32_t)std::min<size_t>((size_t)N * (N - 1) / 2, (size_t)cfg.maxCorr);
+    rowSorted_.alloc(2 * (size_t)cfg.maxCorr + 1);
+    rowOther_.alloc(2 * (size_t)cfg.maxCorr + 1);
+    rowDeg_.alloc(N + 1);
+    rowNA_.alloc(N + 1);
+    pairStart_.alloc(N + 1);
+    rowPairStart_.alloc(N + 1);
+    pairA_.alloc(maxPairsA_ + 1);
+    pairB_.alloc(maxPairsA_ + 1);
+    pairCorr_.alloc(maxPairsA_ + 1);
+    rowPair_.alloc(2 * (size_t)maxPairsA_ + 1);
+    pstat_.alloc(((size_t)maxPairsA_ + 1) * PSTAT);
+    dstat_.alloc((size_t)N * DSTAT);
+    apPair_.alloc((size_t)N * 8);
+    rzPart_.alloc(N);
     int dev = 0;
     hipDeviceProp_t prop;
     BF_HIP(hipGetDevice(&dev));
@@ -1314,7 +1703,32 @@ Solver::~Solver() {
 
 size_t Solver::deviceBytes() const {
     return rowCount_.bytes() * 3 + tileCnt_.bytes() + rowChunk_.bytes() + chunkRow_.bytes() + chunkPart_.bytes() + rowTmp_.bytes() + rowIdx_.bytes() + entries_.bytes() + vec_.bytes() + img_.bytes() +
-           T_.bytes() + Tinv_.bytes() + pairs_.bytes() + pairW_.bytes() + pairBlk_.bytes() + diag_.bytes() + jtr_.bytes();
+           T_.bytes() + Tinv_.bytes() + pairs_.bytes() + pairW_.bytes() + pairBlk_.bytes() + diag_.bytes() + jtr_.bytes() +
+           rowSorted_.bytes() * 2 + pairA_.bytes() * 2 + pairCorr_.bytes() + rowPair_.bytes() + pstat_.bytes() + dstat_.bytes();
+}
+
+void Solver::setShard(uint32_t count, uint32_t index, Comm* comm) {
+    BF_REQUIRE(count >= 1 && index < count, BF_ERR_ARG, "shard index / count");
+    BF_REQUIRE(!comm || (comm->size() == (int)count && comm->rank() == (int)index), BF_ERR_ARG,
+               "communicator size / rank must equal the shard count / index");
+    shardCount_ = count;
+    shardIndex_ = index;
+    comm_ = comm;
+}
+
+uint32_t Solver::exportPairs(double* stats, int* pairAB, uint32_t cap) {
+    BF_HIP(hipStreamSynchronize(stream_));
+    uint32_t np = 0;
+    if (lastPairMode_) BF_HIP(hipMemcpy(&np, ctrl_.p + K_NPAIRS_A, 4, hipMemcpyDeviceToHost));
+    const uint32_t n = std::min(np, cap);
+    if (n && stats) BF_HIP(hipMemcpy(stats, pstat_.p, sizeof(double) * PSTAT * n, hipMemcpyDeviceToHost));
+    if (n && pairAB) {
+        std::vector<int> A(n), B(n);
+        BF_HIP(hipMemcpy(A.data(), pairA_.p, 4 * n, hipMemcpyDeviceToHost));
+        BF_HIP(hipMemcpy(B.data(), pairB_.p, 4 * n, hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < n; k++) { pairAB[2 * k] = A[k]; pairAB[2 * k + 1] = B[k]; }
+    }
+    return np;
 }
 
 // CUDASolverBundling::solve (CUDASolverBundling.cpp:187-284) -> solveBundlingStub (SolverBundling.cu:1137-1220)
@@ -1337,6 +1751,20 @@ void Solver::solve(const SolveArgs& s) {
     a.gradMin = cfg_.denseColorGradientMin; a.dmin = cfg_.denseDepthMin; a.dmax = cfg_.denseDepthMax;
     a.sub = cfg_.denseOverlapSubsample ? cfg_.denseOverlapSubsample : 4;
     a.verifyT = cfg_.verifyOptDistThresh;
+    a.rowSorted = rowSorted_.p; a.rowOther = rowOther_.p; a.rowDeg = rowDeg_.p; a.rowNA = rowNA_.p;
+    a.pairStart = pairStart_.p; a.rowPairStart = rowPairStart_.p; a.pairA = pairA_.p; a.pairB = pairB_.p;
+    a.pairCorr = pairCorr_.p; a.rowPair = rowPair_.p; a.pstat = pstat_.p; a.dstat = dstat_.p;
+    a.apPair = apPair_.p; a.rzPart = rzPart_.p;
+    a.shardCount = shardCount_; a.shardIndex = shardIndex_; a.pairBound = 0;
+    // assembled normal equations for sparse-only solves (auto) unless the matrix-free path is forced
+    bool denseAny = false;
+    for (uint32_t it = 0; it < s.nNonLin && s.cache; it++)
+        denseAny = denseAny || (s.wDenseDepth && s.wDenseDepth[it] > 0.0f) || (s.wDenseColor && s.wDenseColor[it] > 0.0f);
+    const bool pairMode = cfg_.normalEquations != 1 && !denseAny;
+    BF_REQUIRE(!(cfg_.normalEquations == 2 && denseAny), BF_ERR_ARG, "assembled normal equations need a sparse-only solve");
+    BF_REQUIRE(pairMode || shardCount_ == 1, BF_ERR_ARG, "sharded solves use the assembled normal equations (sparse-only)");
+    a.pairMode = pairMode ? 1u : 0u;
+    lastPairMode_ = pairMode;
 
     const unsigned corrGrid = std::max(1u, std::min(div_up(s.numCorr, WG), (unsigned)numCUs_ * 8));
     // chunk kernels: one wave per chunk of CH row entries, up to 16 waves per CU
@@ -1355,13 +1783,53 @@ void Solver::solve(const SolveArgs& s) {
         k_compact_rows<<<s.numImages, WG, 0, stream_>>>(a);
         k_chunks<<<1, WG, 0, stream_>>>(a);
         BF_LAUNCH_CHECK();
+        pairTable_ = false;
     }
+    uint32_t bound = 0;
+    if (pairMode) {
+        if (!pairTable_) {
+            k_pair_sort<<<s.numImages, WG, 0, stream_>>>(a);
+            k_pair_scan<<<1, WG, 0, stream_>>>(a);
+            k_pair_fill<<<s.numImages, 64, 0, stream_>>>(a);
+            k_pair_rows<<<s.numImages, 64, 0, stream_>>>(a);
+            BF_LAUNCH_CHECK();
+            pairTable_ = true;
+            pairCountHost_ = 0;
+        }
+        if (comm_ && comm_->size() > 1) {
+            // the all-reduce count must be known on the host: the caller's bound, or the pair count
+            // read back once per table build
+            if (s.pairBound) {
+                bound = s.pairBound;
+            } else {
+                if (!pairCountHost_) {
+                    BF_HIP(hipMemcpyAsync(&pairCountHost_, ctrl_.p + K_NPAIRS_A, 4, hipMemcpyDeviceToHost, stream_));
+                    BF_HIP(hipStreamSynchronize(stream_));
+                }
+                bound = std::max(pairCountHost_, 1u);
+            }
+            BF_REQUIRE(bound <= maxPairsA_, BF_ERR_CAPACITY, "pair bound exceeds the solver's pair capacity");
+            a.pairBound = bound;
+        }
+    }
+    const unsigned pairRowGrid = std::max(1u, std::min(div_up(s.numImages, WG / 64), (unsigned)numCUs_ * 4));
     for (uint32_t it = 0; it < s.nNonLin; it++) {
         const float wS = s.wSparse[it];
         const float wD = s.wDenseDepth ? s.wDenseDepth[it] : 0.0f;
         const float wC = s.wDenseColor ? s.wDenseColor[it] : 0.0f;
         const bool dense = (wD > 0.0f || wC > 0.0f) && s.cache != nullptr;
         k_transforms<<<div_up(s.numImages, 64), 64, 0, stream_>>>(a, wS, dense ? 1 : 0, 1, 1);
+        if (pairMode) {
+            k_pair_stats<<<(unsigned)numCUs_ * 4, WG, 0, stream_>>>(a);
+            BF_LAUNCH_CHECK();
+            if (comm_ && comm_->size() > 1) comm_->allreduceSum(pstat_.p, (size_t)bound * PSTAT, stream_);
+            k_pair_init<<<pairRowGrid, WG, 0, stream_>>>(a, wS);
+            for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+            BF_LAUNCH_CHECK();
+            k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
+            BF_LAUNCH_CHECK();
+            continue;
+        }
         if (dense) {
             k_dense_reset<<<64, WG, 0, stream_>>>(a);
             k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);

@@ -1,0 +1,46 @@
+// comm.cpp — RCCL communicator for the normal-equation all-reduce (see comm.h).
+#include "comm.h"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+
+#include "bf_runtime.h"
+
+namespace bf {
+
+#define BF_NCCL(call)                                                                                       \
+    do {                                                                                                    \
+        ncclResult_t r_ = (call);                                                                           \
+        if (r_ != ncclSuccess)                                                                              \
+            throw ::bf::Error(::bf::BF_ERR_INTERNAL, std::string(#call) + " failed: " + ncclGetErrorString(r_)); \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == Comm::kIdBytes, "RCCL unique id size");
+
+void Comm::uniqueId(uint8_t* out) {
+    ncclUniqueId id;
+    BF_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(out, id.internal, kIdBytes);
+}
+
+Comm::Comm(const uint8_t* id, int nranks, int rank) : nranks_(nranks), rank_(rank) {
+    BF_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, BF_ERR_ARG, "rank / nranks");
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, kIdBytes);
+    ncclComm_t c = nullptr;
+    BF_NCCL(ncclCommInitRank(&c, nranks, u, rank));  // collective: every rank calls it with the same id
+    comm_ = c;
+}
+
+Comm::~Comm() {
+    if (comm_) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void Comm::allreduceSum(double* buf, size_t n, hipStream_t stream) {
+    if (n == 0) return;
+    BF_NCCL(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, static_cast<ncclComm_t>(comm_), stream));
+}
+
+}  // namespace bf

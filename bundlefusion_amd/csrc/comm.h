@@ -1,0 +1,30 @@
+// comm.h — the one data-path collective of the multi-GPU build: the sum all-reduce of the global
+// bundle adjuster's normal equations over RCCL (xGMI), once per Gauss-Newton iteration
+// (SURVEY.md §8(e)3). One process per GPU; rank 0 draws the RCCL unique id, the host side hands it
+// to the other ranks over its own channel (torch.distributed / gloo in bench.py), every rank then
+// creates its communicator with bf_comm_create.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace bf {
+
+class Comm {
+public:
+    static constexpr size_t kIdBytes = 128;  // NCCL_UNIQUE_ID_BYTES
+    static void uniqueId(uint8_t* out);
+    Comm(const uint8_t* id, int nranks, int rank);
+    ~Comm();
+    int size() const { return nranks_; }
+    int rank() const { return rank_; }
+    // in-place sum over ranks of n doubles, enqueued on stream (no host synchronisation)
+    void allreduceSum(double* buf, size_t n, hipStream_t stream);
+
+private:
+    void* comm_ = nullptr;  // ncclComm_t
+    int nranks_ = 1, rank_ = 0;
+};
+
+}  // namespace bf

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstring>
 #include <limits>
+#include <unordered_set>
 
 namespace bf {
 
@@ -155,6 +156,35 @@ void Recon::setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t*
     globalCorr_ = corr;
     globalCorrN_ = n;
     globalPrefix_.assign(prefix, prefix + numKeyframes);
+    if (comm_) computePairBounds();
+}
+
+void Recon::setComm(Comm* c) {
+    BF_REQUIRE(numFrames_ == 0, BF_ERR_STATE, "set the communicator before the first frame");
+    comm_ = c;
+    global_->setShard(c ? (uint32_t)c->size() : 1u, c ? (uint32_t)c->rank() : 0u, c);
+    if (comm_ && globalCorr_) computePairBounds();
+}
+
+// The sharded global solve all-reduces its pair blocks, so the host must know how many there are:
+// count the distinct image pairs of every keyframe prefix once, from a host copy of the list
+// (removals and the per-image cap only ever drop pairs, so these counts bound every later solve).
+void Recon::computePairBounds() {
+    std::vector<BFEntryJ> h(globalCorrN_);
+    BF_HIP(hipStreamSynchronize(baStream_));
+    if (globalCorrN_) BF_HIP(hipMemcpy(h.data(), globalCorr_, sizeof(BFEntryJ) * globalCorrN_, hipMemcpyDeviceToHost));
+    std::unordered_set<uint64_t> seen;
+    pairBound_.assign(globalPrefix_.size(), 0);
+    uint32_t e = 0;
+    for (size_t s = 0; s < globalPrefix_.size(); s++) {
+        const uint32_t end = std::min(globalPrefix_[s], globalCorrN_);
+        for (; e < end; e++) {
+            const uint32_t i = h[e].imgIdx_i, j = h[e].imgIdx_j;
+            if (i == BF_INVALID_IMAGE || i == j) continue;
+            seen.insert(((uint64_t)std::min(i, j) << 32) | std::max(i, j));
+        }
+        pairBound_[s] = (uint32_t)seen.size();
+    }
 }
 
 void Recon::setInitialPose(const BFMat4& T0) {
@@ -337,6 +367,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         a.trans = dGlobalTrans_.p;
         a.rebuildJT = true;
         a.findMaxResidual = true;
+        if (comm_ && s < pairBound_.size()) a.pairBound = std::max(pairBound_[s], 1u);
         global_->solve(a);
         // removeMaxResidualCUDA with getMaxResidual's (0, <10) exemption, on the device
         global_->removeMaxResidualAsync(globalCorr_, ncorr, dGlobalValid_.p, nk, opt_.maxResidualThresh);

@@ -40,6 +40,7 @@ public:
     // global EntryJ list ordered by max(i, j); prefix[k] = #entries with max(i, j) <= k
     void setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes);
     void setInitialPose(const BFMat4& T0);
+    void setComm(Comm* c);  // shard the global solve's normal equations over c's ranks
     void processFrame(uint32_t f);
     void finish();       // end of sequence: solve the last (partial) submap and wait for all results
     void reintegrate();  // one render-loop iteration without a new frame: apply results, fix ops, GC
@@ -90,6 +91,9 @@ private:
     BFEntryJ* globalCorr_ = nullptr;
     uint32_t globalCorrN_ = 0;
     std::vector<uint32_t> globalPrefix_;
+    Comm* comm_ = nullptr;
+    std::vector<uint32_t> pairBound_;  // distinct image pairs among the entries of each keyframe prefix
+    void computePairBounds();
 
     std::vector<BFMat4> kf_;            // keyframe poses used for integration (solver or dead reckoning)
     std::vector<char> kfSolved_;        // kf_[k] came from the solver

@@ -1,6 +1,8 @@
 """Host-side multi-process plumbing for one process per GPU (torchrun): rank discovery, a gloo
-group for barriers and max-over-ranks timing, and the TSDF shard assignment. The data path has no
-collective: each rank integrates only the 1 m chunks it owns."""
+group for barriers, max-over-ranks timing and the RCCL id hand-off, and the TSDF shard assignment.
+The TSDF data path has no collective: each rank integrates only the 1 m chunks it owns (SURVEY.md
+§8(e)1). The global bundle adjustment shards its image-pair normal-equation blocks over the ranks
+and sums them with one RCCL all-reduce per Gauss-Newton iteration (Comm)."""
 from __future__ import annotations
 
 import os
@@ -44,9 +46,53 @@ class HostGroup:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def broadcast_bytes(self, data: bytes | None, n: int) -> bytes:
+        """rank 0's n bytes on every rank (the RCCL unique id hand-off)."""
+        if self.dist is None:
+            return data
+        import torch
+        t = torch.zeros(n, dtype=torch.uint8)
+        if self.rank == 0:
+            t[:] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        self.dist.broadcast(t, src=0)
+        return bytes(t.numpy().tobytes())
+
     def close(self):
         if self.dist is not None and self.dist.is_initialized():
             self.dist.destroy_process_group()
+
+
+class Comm:
+    """RCCL communicator of the C library (bf_comm_*): rank 0 draws the unique id, the host group
+    broadcasts it, every rank joins. Used by the sharded global solve (bf_recon_set_comm /
+    SolverBundling.set_shard)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, group: HostGroup):
+        import ctypes as C
+        from . import check, lib
+        self.rank, self.world = group.rank, group.world
+        uid = None
+        if group.rank == 0:
+            buf = (C.c_uint8 * self.ID_BYTES)()
+            check(lib().bf_comm_unique_id(buf))
+            uid = bytes(buf)
+        uid = group.broadcast_bytes(uid, self.ID_BYTES)
+        self.h = C.c_void_p()
+        idbuf = (C.c_uint8 * self.ID_BYTES).from_buffer_copy(uid)
+        check(lib().bf_comm_create(idbuf, C.c_int(group.world), C.c_int(group.rank), C.byref(self.h)))
+
+    def allreduce_sum_f64(self, d_array) -> None:
+        import ctypes as C
+        from . import check, lib
+        check(lib().bf_comm_allreduce_sum_f64(self.h, d_array.ptr, C.c_size_t(d_array.nbytes // 8)))
+
+    def close(self):
+        from . import lib
+        if self.h:
+            lib().bf_comm_destroy(self.h)
+            self.h = None
 
 
 def chunk_owner(bx: int, by: int, bz: int, voxel_size: float, shard_count: int, chunk: float = 1.0) -> int:

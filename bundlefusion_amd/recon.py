@@ -109,6 +109,10 @@ class Recon:
         check(lib().bf_recon_set_global_correspondences(self.h, C.c_void_p(corr_ptr), C.c_uint32(n),
                                                         prefix.ctypes.data_as(C.c_void_p), C.c_uint32(len(prefix))))
 
+    def set_comm(self, comm):
+        """Shard the global solve's normal equations over comm's ranks (bundlefusion_amd.dist.Comm)."""
+        check(lib().bf_recon_set_comm(self.h, comm.h if comm is not None else None))
+
     def set_initial_pose(self, T0):
         check(lib().bf_recon_set_initial_pose(self.h, _mat(T0)))
 

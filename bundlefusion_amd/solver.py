@@ -18,7 +18,11 @@ GLOBAL_WEIGHTS_DENSE = dict(sparse=[1.0, 1.0, 1.0], dense_depth=[1.0, 1.0, 2.0],
 class SolverBundling:
     """CUDASolverBundling over bf_solver_* (all buffers device-resident)."""
 
-    def __init__(self, max_images: int, max_corr: int, opts: BFSolverOptions | None = None):
+    def __init__(self, max_images: int, max_corr: int, opts: BFSolverOptions | None = None,
+                 normal_equations: int | None = None):
+        if normal_equations is not None:
+            opts = opts if opts is not None else BFSolverOptions()
+            opts.normalEquations = normal_equations
         self.h = C.c_void_p()
         check(lib().bf_solver_create(C.c_uint32(max_images), C.c_uint32(max_corr),
                                      C.byref(opts) if opts is not None else None, C.byref(self.h)))
@@ -55,6 +59,21 @@ class SolverBundling:
 
     def synchronize(self):
         check(lib().bf_solver_synchronize(self.h))
+
+    def set_shard(self, count: int, index: int, comm=None):
+        """Build only the pair blocks p % count == index; comm (bundlefusion_amd.dist.Comm) sums them."""
+        check(lib().bf_solver_set_shard(self.h, C.c_uint32(count), C.c_uint32(index), comm.h if comm else None))
+
+    def export_pairs(self):
+        """(stats float64[P, 28], pairs int32[P, 2]) of the last solve's assembled normal equations."""
+        total = C.c_uint32(0)
+        check(lib().bf_solver_export_pairs(self.h, None, None, C.c_uint32(0), C.byref(total)))
+        n = total.value
+        stats = np.zeros((max(n, 1), abi.PAIR_STATS), np.float64)
+        ab = np.zeros((max(n, 1), 2), np.int32)
+        check(lib().bf_solver_export_pairs(self.h, stats.ctypes.data_as(C.c_void_p), ab.ctypes.data_as(C.c_void_p),
+                                           C.c_uint32(n), C.byref(total)))
+        return stats[:n], ab[:n]
 
     def matrices_to_poses(self, T: DeviceArray, n: int, rot: DeviceArray, trans: DeviceArray, valid: DeviceArray):
         check(lib().bf_solver_matrices_to_poses(self.h, T.ptr, C.c_uint32(n), rot.ptr, trans.ptr, valid.ptr))

@@ -132,6 +132,9 @@ typedef struct BFSolverOptions {   /* zParametersBundlingDefault.txt defaults wh
     float denseDepthMax;           /* s_denseDepthMax = 4.0 */
     uint32_t denseOverlapSubsample;/* s_denseOverlapCheckSubsampleFactor = 4 */
     float verifyOptDistThresh;     /* 0.02 (CUDASolverBundling.cpp:34) */
+    int32_t normalEquations;       /* 0 auto: sparse-only solves assemble the normal equations per image
+                                      pair (fp64 statistics, one exchange per GN iteration when sharded);
+                                      1 matrix-free (the reference's applyJ/applyJT); 2 assembled */
 } BFSolverOptions;
 
 /* ctor (CUDASolverBundling.cpp:24-136): capacity maxImages x maxCorr residuals */
@@ -162,6 +165,26 @@ int bf_solver_invalidate_image_pair(bf_solver* s, BFEntryJ* corr, uint32_t nCorr
 /* CheckForInvalidFrames[Simple]CU (SIFTImageManager.cu:725-793), using the last table build */
 int bf_solver_check_invalid_frames(bf_solver* s, int* valid, uint32_t nImages, BFEntryJ* corr, uint32_t nCorr,
                                    int comprehensive);
+
+/* ---- multi-GPU: RCCL communicator for the global normal equations ----------
+ * One process per GPU. Rank 0 draws the id (bf_comm_unique_id), the host hands it to every rank,
+ * every rank calls bf_comm_create (collective). A sharded solver builds the normal-equation blocks
+ * of the image pairs p with p % nranks == rank and sums them over ranks with one RCCL all-reduce per
+ * GN iteration; the PCG that follows runs replicated, so every rank ends with the same poses (bit-
+ * identical to a single-GPU solve). */
+typedef struct bf_comm bf_comm;
+int bf_comm_unique_id(uint8_t id[128]);
+int bf_comm_create(const uint8_t id[128], int nranks, int rank, bf_comm** out);
+int bf_comm_destroy(bf_comm* c);
+/* in-place sum over ranks of n doubles (device pointer); synchronizes (tests) */
+int bf_comm_allreduce_sum_f64(bf_comm* c, double* d, size_t n);
+/* shard the solver's pairs: count shards, this is shard index; comm (count ranks) or NULL (no
+ * exchange: each shard keeps only its own blocks, for tests of the partition) */
+int bf_solver_set_shard(bf_solver* s, uint32_t count, uint32_t index, bf_comm* comm);
+/* assembled normal equations of the last GN iteration of the last solve: per image pair (a < b),
+ * 28 doubles {M = sum P_b P_a^T (row-major 9), s_a (3), s_b (3), n, Q_a (xx xy xz yy yz zz), Q_b};
+ * copies min(cap, total) pairs to host stats / pairAB (2 ints each), *total = pair count */
+int bf_solver_export_pairs(bf_solver* s, double* stats, int32_t* pairAB, uint32_t cap, uint32_t* total);
 
 /* ---- synthetic RGB-D stream (seeded analytic room) ------------ */
 typedef struct BFSynthScene {
@@ -282,6 +305,10 @@ int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* he
 /* with recordOps: the scene calls issued so far, in order (kind 1 de-integrate with oldT,
  * 2 integrate with newT, 4 garbage collect); copies min(cap, total) entries, *n = total */
 int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n);
+/* multi-GPU: shard the global solve's normal equations over comm's ranks (one RCCL all-reduce per
+ * GN iteration); call before the first frame. The all-reduce size comes from a host-side count of
+ * the image pairs of each keyframe prefix of the global correspondences (computed when they are set). */
+int bf_recon_set_comm(bf_recon* r, bf_comm* c);
 
 /* ---- re-integration queue alone (host; TrajectoryManager.h:6-118) ---------------------- */
 typedef struct bf_traj bf_traj;

@@ -19,12 +19,19 @@ ROT_TOL, TRANS_TOL = 1e-3, 1e-3
 INVALID = 0xFFFFFFFF
 
 
-def gpu_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_corr=None, corr=None):
+MODES = [bfa.abi.NORMAL_EQ_MATRIX_FREE, bfa.abi.NORMAL_EQ_ASSEMBLED]
+
+
+def gpu_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_corr=None, corr=None, mode=None,
+              shard=None, export=False):
+    """mode: normal equations (None = auto: assembled for sparse-only solves); shard = (count, index)."""
     from bundlefusion_amd.solver import DeviceCache, SolverBundling
     K = prob["K"]
     corr = prob["corr"] if corr is None else corr
     max_corr = max_corr or max(K * 4000, len(corr))
-    S = SolverBundling(K, max_corr)
+    S = SolverBundling(K, max_corr, normal_equations=mode)
+    if shard is not None:
+        S.set_shard(*shard)
     d_corr = bfa.DeviceArray.from_host(corr if len(corr) else np.zeros(1, corr.dtype))
     d_valid = bfa.DeviceArray.from_host(prob["valid"].astype(np.int32))
     d_rot = bfa.DeviceArray.from_host(prob["rot"].astype(np.float32))
@@ -35,6 +42,8 @@ def gpu_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_
             intrinsics=prob.get("intrinsics", (0, 0, 0, 0)), rot=d_rot, trans=d_trans)
     res = S.result()
     out = d_rot.download(), d_trans.download(), d_corr.download()[:len(corr)], res
+    if export:
+        out = out + (S.export_pairs(),)
     S.close()
     return out
 
@@ -81,14 +90,15 @@ def smoke_ba():
     assert_parity(gpu_solve(prob, 2, 50, [1, 1]), oracle_solve(prob, 2, 50, [1, 1]))
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("K,n_lin", [(6, 1), (6, 5), (6, 10), (12, 8), (32, 20)])
-def test_single_gn_step_parity_tight(K, n_lin):
+def test_single_gn_step_parity_tight(K, n_lin, mode):
     """One Gauss-Newton step, n_lin PCG iterations: the HIP iterates track the oracle's to float
     rounding (~1e-7). Measured on MI355X (tools/ba_trace.py): beyond ~10-15 iterations on the small
     chains float32 CG loses conjugacy once the residual is tiny and the two summation orders drift
     apart chaotically (1e-4..1e-3), which is why the full schedules use the SURVEY tolerances."""
     prob = make_problem(K=K, max_per_pair=30, outliers=0.01)
-    g, o = gpu_solve(prob, 1, n_lin, [1]), oracle_solve(prob, 1, n_lin, [1])
+    g, o = gpu_solve(prob, 1, n_lin, [1], mode=mode), oracle_solve(prob, 1, n_lin, [1])
     assert g[3]["pcgIterations"] == o[3]["pcgIterations"] == n_lin
     assert_parity(g, o, rot_tol=3e-6, trans_tol=3e-6, energy_rtol=1e-4)
 
@@ -104,7 +114,8 @@ def test_dense_single_gn_step_parity_tight(n_lin):
     assert_parity(g, o, rot_tol=5e-6, trans_tol=5e-6, energy_rtol=1e-4)
 
 
-def test_global_sparse_schedule():
+@pytest.mark.parametrize("mode", MODES)
+def test_global_sparse_schedule(mode):
     """Global solve schedule (SBA.cpp:34-39: sparse 1, dense off, 3 GN x 150 PCG) over 12 keyframes.
 
     This chain is ill-conditioned along the trajectory and the GN exit test (max|delta| < 0.005,
@@ -112,7 +123,7 @@ def test_global_sparse_schedule():
     implementations may legitimately take 2 vs 3 GN steps; both must then reach the same energy
     and the same accuracy against ground truth, and stay within 5 mm / 5 mrad of each other."""
     prob = make_problem(K=12, max_per_pair=60, outliers=0.0)
-    g = gpu_solve(prob, 3, 150, [1, 1, 1])
+    g = gpu_solve(prob, 3, 150, [1, 1, 1], mode=mode)
     o = oracle_solve(prob, 3, 150, [1, 1, 1])
     if g[3]["gnIterations"] == o[3]["gnIterations"]:
         assert_parity(g, o)
@@ -123,27 +134,32 @@ def test_global_sparse_schedule():
         assert er < 4e-3 and et < 7e-3
 
 
-def test_global_sparse_parity_with_outliers():
+@pytest.mark.parametrize("mode", MODES)
+def test_global_sparse_parity_with_outliers(mode):
     """3 GN x 150 PCG with 2 % outliers. 150 float32 CG iterations per step are past the point where
     the two summation orders stay in lock-step (see test_single_gn_step_parity_tight), so the
     solutions are held to the same energy (1e-3 relative), to 5 mrad / 5 mm of each other and to
     the same accuracy against ground truth."""
     prob = make_problem(K=16, max_per_pair=40, outliers=0.02, seed=5)
-    g = gpu_solve(prob, 3, 150, [1, 1, 1])
+    g = gpu_solve(prob, 3, 150, [1, 1, 1], mode=mode)
     o = oracle_solve(prob, 3, 150, [1, 1, 1])
-    assert_parity(g, o, rot_tol=5e-3, trans_tol=5e-3, energy_rtol=1e-3)
+    # the assembled operator is evaluated in fp64 (the reference's is fp32 matrix-free): a different
+    # but not worse CG trajectory on this ill-conditioned chain, measured 5.6 mm apart at equal energy
+    trans_tol = 5e-3 if mode == bfa.abi.NORMAL_EQ_MATRIX_FREE else 1e-2
+    assert_parity(g, o, rot_tol=5e-3, trans_tol=trans_tol, energy_rtol=1e-3)
     eg = pose_errors(g[0], g[1], prob["gt"])
     eo = pose_errors(o[0], o[1], prob["gt"])
     assert eg[0] <= 1.5 * eo[0] + 1e-3 and eg[1] <= 1.5 * eo[1] + 1e-3, (eg, eo)
 
 
-def test_per_image_cap_invalidation_exact():
+@pytest.mark.parametrize("mode", MODES)
+def test_per_image_cap_invalidation_exact(mode):
     """BuildVariablesToCorrespondencesTableDevice (SolverBundling.cu:1226-1248) with cap 1000."""
     prob = make_problem(K=6, stride=2, max_per_pair=256, outliers=0.0)
     counts = np.bincount(np.concatenate([prob["corr"]["i"], prob["corr"]["j"]]), minlength=6)
     assert counts.max() > 1000
     max_corr = 6 * 1000
-    g = gpu_solve(prob, 2, 40, [1, 1], max_corr=max_corr)
+    g = gpu_solve(prob, 2, 40, [1, 1], max_corr=max_corr, mode=mode)
     o = oracle_solve(prob, 2, 40, [1, 1], max_corr=max_corr)
     assert (o[2]["i"] == INVALID).sum() > 0
     assert_parity(g, o)
@@ -256,22 +272,90 @@ def test_per_image_cap_shuffled_order():
     assert_parity(g, o)
 
 
-def test_solve_bit_deterministic():
+@pytest.mark.parametrize("mode", MODES)
+def test_solve_bit_deterministic(mode):
     """Chunk partials are handed between waves and workgroups inside a launch (write-through stores +
     agent-scope tickets) and reduced in a fixed order: two solves of the same problem must agree bit
     for bit. A stale hand-off would show up as run-to-run differences."""
     prob = make_problem(K=40, max_per_pair=40, outliers=0.02, seed=11)
-    a = gpu_solve(prob, 3, 60, [1, 1, 1])
-    b = gpu_solve(prob, 3, 60, [1, 1, 1])
+    a = gpu_solve(prob, 3, 60, [1, 1, 1], mode=mode)
+    b = gpu_solve(prob, 3, 60, [1, 1, 1], mode=mode)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     assert a[3] == b[3]
 
 
-def test_many_images_multipass_finisher():
+@pytest.mark.parametrize("mode", MODES)
+def test_many_images_multipass_finisher(mode):
     """More than 2 x 256 images: the PCG finisher takes its multi-pass path (rows do not fit the
     register-resident form); one GN step with a few PCG iterations tracks the oracle tightly."""
     prob = make_problem(K=560, stride=1, max_per_pair=4, outliers=0.0, drift=(0.05, 0.002))
-    g, o = gpu_solve(prob, 1, 5, [1]), oracle_solve(prob, 1, 5, [1])
+    g, o = gpu_solve(prob, 1, 5, [1], mode=mode), oracle_solve(prob, 1, 5, [1])
     assert g[3]["pcgIterations"] == o[3]["pcgIterations"] == 5
     assert_parity(g, o, rot_tol=2e-5, trans_tol=2e-5, energy_rtol=1e-4)
+
+
+# ---- assembled normal equations: statistics, shard partition, RCCL exchange ----------------------
+def _initial_T(prob):
+    return np.stack([pose_to_matrix(prob["rot"][k], prob["trans"][k]) for k in range(prob["K"])])
+
+
+def test_pair_statistics_match_numpy():
+    """k_pair_stats of the first GN iteration (initial poses) against the numpy restatement
+    (tests/oracle_pairs.py): fp64 sums of the same float32 world points, order-only differences."""
+    from oracle_pairs import pair_stats
+    prob = make_problem(K=10, max_per_pair=30, outliers=0.02, seed=9)
+    g = gpu_solve(prob, 1, 3, [1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED, export=True)
+    stats, ab = g[4]
+    ref = pair_stats(g[2][g[2]["i"] != INVALID], _initial_T(prob))
+    assert len(stats) == len(ref) > 0
+    keys = [tuple(x) for x in ab]
+    assert keys == sorted(ref.keys())  # pairs numbered in (a, b) order
+    R = np.stack([ref[k] for k in keys])
+    np.testing.assert_allclose(stats, R, rtol=2e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("count", [2, 3])
+def test_shard_partition_sums_bit_exact(count):
+    """Each shard builds the pairs p % count == index and zeros elsewhere: the sum over shards (what
+    the RCCL all-reduce computes) equals the single-GPU statistics bit for bit."""
+    prob = make_problem(K=12, max_per_pair=25, outliers=0.02, seed=4)
+    full = gpu_solve(prob, 1, 2, [1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED, export=True)[4][0]
+    parts = [gpu_solve(prob, 1, 2, [1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED, shard=(count, r), export=True)[4][0]
+             for r in range(count)]
+    total = np.zeros_like(full)
+    for p in parts:
+        total = total + p
+    np.testing.assert_array_equal(total, full)
+    for r, p in enumerate(parts):  # owned rows non-zero, the others exactly zero
+        own = np.arange(len(full)) % count == r
+        assert (p[~own] == 0).all() and (np.abs(p[own]).sum(axis=1) > 0).all()
+
+
+def test_rccl_single_rank_exchange():
+    """The RCCL path of the sharded solve with one rank: the communicator is created from a drawn
+    unique id, its all-reduce is the identity, and a solve through set_shard(1, 0, comm) matches the
+    plain solve bit for bit."""
+    from bundlefusion_amd.dist import Comm, HostGroup
+    comm = Comm(HostGroup(0, 1))
+    x = np.random.default_rng(0).normal(size=1000)
+    d = bfa.DeviceArray.from_host(x)
+    comm.allreduce_sum_f64(d)
+    np.testing.assert_array_equal(d.download(), x)
+    prob = make_problem(K=8, max_per_pair=20, outliers=0.0)
+    from bundlefusion_amd.solver import SolverBundling
+    outs = []
+    for use_comm in (False, True):
+        S = SolverBundling(8, 8 * 4000)
+        if use_comm:
+            S.set_shard(1, 0, comm)
+        d_corr = bfa.DeviceArray.from_host(prob["corr"])
+        d_rot, d_trans = bfa.DeviceArray.from_host(prob["rot"]), bfa.DeviceArray.from_host(prob["trans"])
+        S.solve(d_corr, len(prob["corr"]), bfa.DeviceArray.from_host(prob["valid"]), 8, 2, 20, [1, 1],
+                rot=d_rot, trans=d_trans)
+        S.result()
+        outs.append((d_rot.download(), d_trans.download()))
+        S.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    comm.close()

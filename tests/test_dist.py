@@ -57,3 +57,67 @@ def test_chunk_ownership_partitions_and_groups_chunks(shards):
     a = chunk_owner(100, 100, 100, 0.004, shards)  # 3.2 m -> chunk 3
     b = chunk_owner(104, 96, 102, 0.004, shards)  # 3.33 m, 3.07 m, 3.26 m -> same chunk
     assert a == b
+
+
+def _id_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    g = HostGroup(rank, world)
+    uid = bytes(np.random.default_rng(7).integers(0, 256, 128, dtype=np.uint8)) if rank == 0 else None
+    got = g.broadcast_bytes(uid, 128)
+    q.put((rank, got))
+    g.close()
+
+
+def test_gloo_world2_unique_id_handoff():
+    """The RCCL unique id drawn on rank 0 reaches every rank unchanged (dist.Comm's hand-off)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_id_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = bytes(np.random.default_rng(7).integers(0, 256, 128, dtype=np.uint8))
+    assert res[0] == res[1] == expect
+
+
+def _pair_worker(rank, world, port, q):
+    """One rank of the sharded global solve's exchange, on CPU: build the statistics of the pairs
+    p % world == rank (zeros elsewhere, k_pair_stats' partition), sum over ranks (gloo standing in
+    for the RCCL all-reduce) and report the result."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import torch
+    import torch.distributed as dist
+    from ba_problem import make_problem
+    from oracle_ba import pose_to_matrix
+    from oracle_pairs import pair_stats
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    g = HostGroup(rank, world)
+    prob = make_problem(K=8, max_per_pair=10, outliers=0.02, seed=3)
+    T = np.stack([pose_to_matrix(prob["rot"][k], prob["trans"][k]) for k in range(8)])
+    full = pair_stats(prob["corr"], T)
+    keys = sorted(full)
+    mine = np.stack([full[k] + 0.0 if p % world == rank else np.zeros(28) for p, k in enumerate(keys)])
+    t = torch.from_numpy(mine.copy())
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    q.put((rank, t.numpy().copy(), np.stack([full[k] for k in keys])))
+    g.close()
+
+
+def test_gloo_world2_pair_shard_exchange_is_exact():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pair_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][0], res[r][1])
