@@ -814,16 +814,14 @@ __device__ __forceinline__ void pcg_sparse_chunks(const BA& a, float wSparse, ui
 // Ap of row v for the finisher: the sparse part handed over by the row's last chunk wave, plus the
 // dense diagonal block and the dense off-diagonal atomics (reset for the next iteration)
 __device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, int useDense, f3 pR, f3 pT, f3& aR, f3& aT) {
-    if (a.pairMode) {  // assembled normal equations: Ap of the row, handed over by its wave
+    aR = mk3(0, 0, 0);
+    aT = mk3(0, 0, 0);
+    if (a.pairMode) {  // assembled normal equations: sparse Ap of the row, handed over by its wave
         const float4* q = reinterpret_cast<const float4*>(a.apPair + (size_t)v * 8);
         const float4 x = ld_wt(q), y = ld_wt(q + 1);
         aR = mk3(x.x, x.y, x.z);
         aT = mk3(y.x, y.y, y.z);
-        return;
-    }
-    aR = mk3(0, 0, 0);
-    aT = mk3(0, 0, 0);
-    if (nch) {  // sparse part: the row's chunk partials, in chunk order
+    } else if (nch) {  // sparse part: the row's chunk partials, in chunk order
         const int c1 = a.rowChunk[v + 1];
 #pragma unroll 4
         for (int c = a.rowChunk[v]; c < c1; c++) {
@@ -910,6 +908,31 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
     return rDotzNew;
 }
 
+// dense off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j), agent-scope atomics
+__device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
+    const uint32_t lane = lane_id();
+    const uint32_t np = a.ctrl[K_NPAIRS];
+    for (uint32_t k = wave; k < np; k += nw) {
+        if (a.pairW[k] == 0.0f) continue;
+        const uint2 pr = a.pairs[k];
+        const float* Bk = a.pairBlk + (size_t)k * 36;
+        f3 r, t;
+        float o = 0.0f;
+        if (lane < 6) {
+            vload(a, V_P, pr.x, r, t);
+            const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+            for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
+            if (pr.y > 0) atomicAdd(&a.apDense[(size_t)pr.y * 8 + (lane < 3 ? 4 + lane : lane - 3)], o);
+        } else if (lane < 12) {
+            vload(a, V_P, pr.y, r, t);
+            const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+            const int c0 = lane - 6;
+            for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
+            if (pr.x > 0) atomicAdd(&a.apDense[(size_t)pr.x * 8 + (c0 < 3 ? 4 + c0 : c0 - 3)], o);
+        }
+    }
+}
+
 // PCG finisher (one workgroup): Kernel1b, Kernel2, the host early-out test, Kernel3
 __device__ void pcg_finisher(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, float& rDotzNew,
                              bool& last) {
@@ -982,28 +1005,7 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
     pcg_sparse_chunks<false>(a, wSparse, wave, nw, nch);
-    if (useDense) {  // off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j)
-        const uint32_t np = a.ctrl[K_NPAIRS];
-        for (uint32_t k = wave; k < np; k += nw) {
-            if (a.pairW[k] == 0.0f) continue;
-            const uint2 pr = a.pairs[k];
-            const float* Bk = a.pairBlk + (size_t)k * 36;
-            f3 r, t;
-            float o = 0.0f;
-            if (lane < 6) {
-                vload(a, V_P, pr.x, r, t);
-                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-                for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
-                if (pr.y > 0) atomicAdd(&a.apDense[(size_t)pr.y * 8 + (lane < 3 ? 4 + lane : lane - 3)], o);
-            } else if (lane < 12) {
-                vload(a, V_P, pr.y, r, t);
-                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-                const int c0 = lane - 6;
-                for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
-                if (pr.x > 0) atomicAdd(&a.apDense[(size_t)pr.x * 8 + (c0 < 3 ? 4 + c0 : c0 - 3)], o);
-            }
-        }
-    }
+    if (useDense) pcg_dense_offdiag(a, wave, nw);
     if (a.probe && threadIdx.x == 0) {
         __hip_atomic_store((gu64*)&a.probe[16 + 2 * blockIdx.x], (uint64_t)tStart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store((gu64*)&a.probe[17 + 2 * blockIdx.x], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1081,7 +1083,7 @@ __global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
             const f3 rt = mk3((float)d[13], (float)d[14], (float)d[15]);
             // |dAlpha|^2, |dBeta|^2, |dGamma|^2 summed: (Qyy + Qzz, Qxx + Qzz, Qxx + Qyy)
             const f3 pr = mk3((float)(d[3] + d[5]), (float)(d[0] + d[5]), (float)(d[0] + d[3]));
-            st_wt(&a.rzPart[v], init_row_cnt(a, v, rr, rt, pr, (float)d[9], wSparse, 0));
+            st_wt(&a.rzPart[v], init_row_cnt(a, v, rr, rt, pr, (float)d[9], wSparse, (int)a.ctrl[K_USE_DENSE]));
         }
     }
     if (!last_block(&a.ctrl[K_TICKET])) return;
@@ -1133,16 +1135,162 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
             st_wt(q + 1, make_float4((float)(ws * (dp[3] - o[3])), (float)(ws * (dp[4] - o[4])), (float)(ws * (dp[5] - o[5])), 0.0f));
         }
     }
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    if (useDense) pcg_dense_offdiag(a, wave, nw);
     if (!last_block_sharded(a.sync, 1u)) return;
     if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
     float rDotzNew;
     bool last;
-    pcg_finisher(a, sh, 0u, 0, iter, nLin, rDotzNew, last);
+    pcg_finisher(a, sh, 0u, useDense, iter, nLin, rDotzNew, last);
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
         a.ctrl[K_PCG_ITERS]++;
         if (last) a.ctrl[K_PCG_DONE] = 1;
         a.ctrl[K_TICKET] = 0;
+    }
+}
+
+// Small solves (N <= 64 images: the 11-frame local submaps, early global solves): every PCG
+// iteration of the GN step in ONE workgroup. p lives in LDS; each wave applies the assembled
+// operator to its rows (sparse pair blocks in fp64, dense blocks of BuildDenseSystem in fp32: the
+// diagonal block and the off-diagonal pair blocks, with the [trans | rot] order of the dense system,
+// SolverBundlingDenseUtil.h:371-411); wave 0 holds one row per lane for the vector updates and the
+// two dot products (PCGIteration Kernel1b/2/3, SolverBundling.cu:930-1022) with fixed butterflies.
+// No grid-wide hand-off and no launch per iteration.
+constexpr int SMALL_N = 64;
+constexpr int SMALL_WG = 1024;
+__global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int nLin) {
+    __shared__ float sP[SMALL_N][6], sAp[SMALL_N][6];
+    __shared__ int sLast;
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6, nw = SMALL_WG / 64;
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    const uint32_t npD = useDense ? a.ctrl[K_NPAIRS] : 0u;
+    // wave 0, lane v: row v's vectors (row 0 and rows >= N stay zero)
+    const bool own = wave == 0 && lane >= 1 && lane < a.N;
+    f3 dR = mk3(0, 0, 0), dT = dR, rR = dR, rT = dR, mR = dR, mT = dR, pR = dR, pT = dR;
+    if (wave == 0 && lane < a.N) {
+        if (own) {
+            vload(a, V_DELTA, lane, dR, dT);
+            vload(a, V_R, lane, rR, rT);
+            vload(a, V_M, lane, mR, mT);
+            vload(a, V_P, lane, pR, pT);
+        }
+        sP[lane][0] = pR.x; sP[lane][1] = pR.y; sP[lane][2] = pR.z;
+        sP[lane][3] = pT.x; sP[lane][4] = pT.y; sP[lane][5] = pT.z;
+    }
+    float rz = ctrlf(a.ctrl, K_RDOTZ);
+    int iters = 0;
+    __syncthreads();
+    for (int iter = 0; iter < nLin; iter++) {
+        for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+            double o[6] = {0, 0, 0, 0, 0, 0};
+            const int e0 = a.rowPairStart[v], e1 = a.rowPairStart[v + 1];
+            for (int k = e0 + (int)lane; k < e1; k += 64) {
+                const int2 rp = a.rowPair[k];
+                const uint32_t u = (uint32_t)rp.y & ~PAIR_A_FLAG;
+                if (u == 0) continue;
+                const double w[3] = {sP[u][0], sP[u][1], sP[u][2]}, t[3] = {sP[u][3], sP[u][4], sP[u][5]};
+                double b[6];
+                pair_block_apply(a.pstat + (size_t)rp.x * PSTAT, ((uint32_t)rp.y & PAIR_A_FLAG) != 0, w, t, b);
+#pragma unroll
+                for (int q = 0; q < 6; q++) o[q] += b[q];
+            }
+            float od[6] = {0, 0, 0, 0, 0, 0};  // dense part, [trans | rot] rows
+            for (uint32_t k = lane; k < npD; k += 64) {
+                if (a.pairW[k] == 0.0f) continue;
+                const uint2 pr = a.pairs[k];
+                const float* Bk = a.pairBlk + (size_t)k * 36;  // rows: image pr.y, columns: image pr.x
+                if (pr.y == v && pr.x > 0) {
+                    const float pv[6] = {sP[pr.x][3], sP[pr.x][4], sP[pr.x][5], sP[pr.x][0], sP[pr.x][1], sP[pr.x][2]};
+                    for (int r = 0; r < 6; r++) {
+                        float s = 0.0f;
+                        for (int c = 0; c < 6; c++) s += Bk[r * 6 + c] * pv[c];
+                        od[r] += s;
+                    }
+                } else if (pr.x == v && pr.y > 0) {
+                    const float pv[6] = {sP[pr.y][3], sP[pr.y][4], sP[pr.y][5], sP[pr.y][0], sP[pr.y][1], sP[pr.y][2]};
+                    for (int c = 0; c < 6; c++) {
+                        float s = 0.0f;
+                        for (int r = 0; r < 6; r++) s += Bk[r * 6 + c] * pv[r];
+                        od[c] += s;
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 6; q++) o[q] = wave_sum_d(o[q]);
+            if (useDense) {
+#pragma unroll
+                for (int q = 0; q < 6; q++) od[q] = wave_sum(od[q]);
+            }
+            if (lane == 0) {
+                const double w[3] = {sP[v][0], sP[v][1], sP[v][2]}, t[3] = {sP[v][3], sP[v][4], sP[v][5]};
+                double dp[6];
+                diag_apply(a.dstat + (size_t)v * DSTAT, w, t, dp);
+                const double ws = wSparse;
+                float ap[6];
+#pragma unroll
+                for (int q = 0; q < 6; q++) ap[q] = (float)(ws * (dp[q] - o[q]));
+                if (useDense) {
+                    const float* D = a.diag + (size_t)v * 36;
+                    const float pv[6] = {sP[v][3], sP[v][4], sP[v][5], sP[v][0], sP[v][1], sP[v][2]};
+                    float o6[6];
+                    for (int r = 0; r < 6; r++) {
+                        float s = 0.0f;
+                        for (int c = 0; c < 6; c++) s += D[r * 6 + c] * pv[c];
+                        o6[r] = s;
+                    }
+                    for (int q = 0; q < 3; q++) {
+                        ap[3 + q] += o6[q] + od[q];      // trans
+                        ap[q] += o6[3 + q] + od[3 + q];  // rot
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 6; q++) sAp[v][q] = ap[q];
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const f3 aR = own ? mk3(sAp[lane][0], sAp[lane][1], sAp[lane][2]) : mk3(0, 0, 0);
+            const f3 aT = own ? mk3(sAp[lane][3], sAp[lane][4], sAp[lane][5]) : mk3(0, 0, 0);
+            const float pAp = wave_sum(dot3(pR, aR) + dot3(pT, aT));
+            const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
+            dR = dR + alpha * pR;
+            dT = dT + alpha * pT;
+            rR = rR - alpha * aR;
+            rT = rT - alpha * aT;
+            const f3 zR = mul3(mR, rR), zT = mul3(mT, rT);
+            const float rzNew = wave_sum(dot3(zR, rR) + dot3(zT, rT));
+            const bool last = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+            const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
+            if (own) {
+                pR = zR + beta * pR;
+                pT = zT + beta * pT;
+                sP[lane][0] = pR.x; sP[lane][1] = pR.y; sP[lane][2] = pR.z;
+                sP[lane][3] = pT.x; sP[lane][4] = pT.y; sP[lane][5] = pT.z;
+            }
+            rz = rzNew;
+            if (lane == 0) sLast = last ? 1 : 0;
+        }
+        iters++;
+        __syncthreads();
+        if (sLast) break;
+    }
+    if (own) {
+        vstore(a, V_DELTA, lane, dR, dT);
+        vstore(a, V_R, lane, rR, rT);
+        vstore(a, V_P, lane, pR, pT);
+        // computeLieUpdate (LieDerivUtil.h:301-307) on the exiting iteration
+        f3 nr, nt;
+        lie_update(dR, dT, mk3(a.rot[3 * lane], a.rot[3 * lane + 1], a.rot[3 * lane + 2]),
+                   mk3(a.trans[3 * lane], a.trans[3 * lane + 1], a.trans[3 * lane + 2]), nr, nt);
+        a.rot[3 * lane] = nr.x; a.rot[3 * lane + 1] = nr.y; a.rot[3 * lane + 2] = nr.z;
+        a.trans[3 * lane] = nt.x; a.trans[3 * lane + 1] = nt.y; a.trans[3 * lane + 2] = nt.z;
+    }
+    if (threadIdx.x == 0) {
+        a.ctrl[K_RDOTZ] = __float_as_uint(rz);
+        a.ctrl[K_PCG_ITERS] += (uint32_t)iters;
+        a.ctrl[K_PCG_DONE] = 1;
     }
 }
 
@@ -1760,9 +1908,9 @@ void Solver::solve(const SolveArgs& s) {
     bool denseAny = false;
     for (uint32_t it = 0; it < s.nNonLin && s.cache; it++)
         denseAny = denseAny || (s.wDenseDepth && s.wDenseDepth[it] > 0.0f) || (s.wDenseColor && s.wDenseColor[it] > 0.0f);
-    const bool pairMode = cfg_.normalEquations != 1 && !denseAny;
-    BF_REQUIRE(!(cfg_.normalEquations == 2 && denseAny), BF_ERR_ARG, "assembled normal equations need a sparse-only solve");
-    BF_REQUIRE(pairMode || shardCount_ == 1, BF_ERR_ARG, "sharded solves use the assembled normal equations (sparse-only)");
+    (void)denseAny;
+    const bool pairMode = cfg_.normalEquations != 1;
+    BF_REQUIRE(pairMode || shardCount_ == 1, BF_ERR_ARG, "sharded solves use the assembled normal equations");
     a.pairMode = pairMode ? 1u : 0u;
     lastPairMode_ = pairMode;
 
@@ -1820,11 +1968,22 @@ void Solver::solve(const SolveArgs& s) {
         const bool dense = (wD > 0.0f || wC > 0.0f) && s.cache != nullptr;
         k_transforms<<<div_up(s.numImages, 64), 64, 0, stream_>>>(a, wS, dense ? 1 : 0, 1, 1);
         if (pairMode) {
+            if (dense) {
+                k_dense_reset<<<64, WG, 0, stream_>>>(a);
+                k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);
+                k_dense_count<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 8), WG, 0, stream_>>>(a);
+                k_dense_build<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 4), WG, 0, stream_>>>(a, wD, wC);
+                BF_LAUNCH_CHECK();
+            }
             k_pair_stats<<<(unsigned)numCUs_ * 4, WG, 0, stream_>>>(a);
             BF_LAUNCH_CHECK();
             if (comm_ && comm_->size() > 1) comm_->allreduceSum(pstat_.p, (size_t)bound * PSTAT, stream_);
             k_pair_init<<<pairRowGrid, WG, 0, stream_>>>(a, wS);
-            for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+            if (s.numImages <= (uint32_t)SMALL_N) {
+                if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
+            } else {
+                for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+            }
             BF_LAUNCH_CHECK();
             k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
             BF_LAUNCH_CHECK();

@@ -103,13 +103,14 @@ def test_single_gn_step_parity_tight(K, n_lin, mode):
     assert_parity(g, o, rot_tol=3e-6, trans_tol=3e-6, energy_rtol=1e-4)
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("n_lin", [1, 4])
-def test_dense_single_gn_step_parity_tight(n_lin):
+def test_dense_single_gn_step_parity_tight(n_lin, mode):
     """Dense depth + colour system (BuildDenseSystem, SolverBundling.cu:182-306) through the first PCG
     iterations: pins the block-sparse dense JtJ/Jtr build and its PCG product against the oracle."""
     prob = make_problem(K=6, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
     args = (1, n_lin, [1], [1000], [50])
-    g, o = gpu_solve(prob, *args, use_cache=True), oracle_solve(prob, *args, use_cache=True)
+    g, o = gpu_solve(prob, *args, use_cache=True, mode=mode), oracle_solve(prob, *args, use_cache=True)
     assert g[3]["numDensePairs"] > 0
     assert_parity(g, o, rot_tol=5e-6, trans_tol=5e-6, energy_rtol=1e-4)
 
@@ -165,11 +166,12 @@ def test_per_image_cap_invalidation_exact(mode):
     assert_parity(g, o)
 
 
-def test_local_dense_parity():
+@pytest.mark.parametrize("mode", MODES)
+def test_local_dense_parity(mode):
     """Local solve with the dense depth term on the 80x60 cache (SBA.cpp:28-33 schedule shape)."""
     prob = make_problem(K=6, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
     args = (3, 100, [1, 1, 1], [1000, 1000, 1000], [0, 0, 0])
-    g = gpu_solve(prob, *args, use_cache=True)
+    g = gpu_solve(prob, *args, use_cache=True, mode=mode)
     o = oracle_solve(prob, *args, use_cache=True)
     assert g[3]["numDensePairs"] > 0
     assert_parity(g, o)
