@@ -156,6 +156,8 @@ private:
     KernelClock applyClock_;
     unsigned applyGrid_ = 0;
     int applyZC_ = 4;
+    int applyKernel_ = 2;
+    int applyWpe_ = 8;
     DevBuf<uint8_t> blockFlags_;  // per work-list entry of a fused re-integration: bit 0 de-integrate, bit 1 integrate
     unsigned reintegrateGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat

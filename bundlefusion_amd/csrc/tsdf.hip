@@ -741,18 +741,24 @@ __device__ __forceinline__ float round_quot(float num, float den, float rden) {
     return roundf(q);
 }
 
+// Integrate colour blend of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:486-496): per channel
+// u8(clamp(roundf(0.2f * cu + 0.8f * oc), 0, 254.5)), or the new colour when the voxel is empty. The
+// float expression lies within 1e-5 of (cu + 4 oc) / 5, whose fractional part is a multiple of 0.2,
+// so its roundf is the integer (2 cu + 8 oc + 5) / 10 = ((2 cu + 8 oc + 5) * 6554) >> 16 (exact for
+// all 65536 (cu, oc): checked exhaustively in tests/test_oracle_tsdf.py). Integer ops replace the
+// float blend + roundf + clamp.
+__device__ __forceinline__ uint32_t blend_channel(uint32_t cu, uint32_t oc, bool empty) {
+    const uint32_t m = ((2u * cu + 8u * oc + 5u) * 6554u) >> 16;
+    return min(empty ? cu : m, 254u);
+}
+__device__ __forceinline__ uint32_t blend_color(uint32_t c, uint32_t col, bool empty) {
+    return blend_channel(c & 0xFF, col & 0xFF, empty) | (blend_channel((c >> 8) & 0xFF, (col >> 8) & 0xFF, empty) << 8) |
+           (blend_channel((c >> 16) & 0xFF, (col >> 16) & 0xFF, empty) << 16) | (255u << 24);
+}
 // Voxel update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:486-514), weightUpdate = 1.
 __device__ __forceinline__ void voxel_integrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
     const float wUpd = 1.0f;
-    const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
-    const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
-    float r0, r1, r2;
-    if (w0 == 0.0f) { r0 = cu0; r1 = cu1; r2 = cu2; }
-    else { r0 = 0.2f * cu0 + 0.8f * oc0; r1 = 0.2f * cu1 + 0.8f * oc1; r2 = 0.2f * cu2 + 0.8f * oc2; }
-    r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
-    r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
-    r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
-    col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+    col = blend_color(c, col, w0 == 0.0f);
     s0 = (sdf * wUpd + s0 * w0) / (wUpd + w0);
     w0 = fminf(weightMax, wUpd + w0);
 }
@@ -768,6 +774,45 @@ __device__ __forceinline__ void voxel_deintegrate(float& s0, float& w0, uint32_t
     s0 = (s0 * w0 - sdf * wUpd) / (w0 - wUpd);
     w0 = fmaxf(0.0f, w0 - wUpd);
     if (w0 <= 0.001f) { s0 = 0.0f; col = 0u; w0 = 0.0f; }
+}
+
+// Two voxels of one lane column, (x, y, z) and (x, y, z + 1), projected together: every float
+// operation is the scalar path's (xform's ((e0 x + e1 y) + e2 z) + e3, then fx * x, the rcp quotient,
+// + m, + 0.5), done elementwise on 2-wide vectors so that it issues as packed-FP32 instructions
+// (v_pk_mul_f32 / v_pk_add_f32: two IEEE results per instruction, no contraction). The exactness
+// check and the IEEE fallback of proj_coord follow per element.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int proj_fix(float num, float den, float qa, float m, float t) {
+    const float eps = (fabsf(qa) + 2.0f * fabsf(t) + 2.0f) * 0x1p-21f;
+    const bool need = !(fabsf(t - rintf(t)) > eps);
+    if (__builtin_amdgcn_ballot_w64(need)) {
+        asm volatile("" ::: "memory");
+        const float te = (num / den + m) + 0.5f;
+        t = need ? te : t;
+    }
+    return f2i(t);
+}
+__device__ __forceinline__ void voxel_pixel2(const BFDepthCameraParams& cam, const BFMat4& T, float wx, float wy, f2v wz,
+                                             bool haveColor, uint32_t& pix0, uint32_t& pix1, f2v& pz) {
+    const float* e = T.m;
+    f2v p[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const float b = e[4 * r] * wx + e[4 * r + 1] * wy;
+        p[r] = (f2v{b, b} + f2v{e[4 * r + 2], e[4 * r + 2]} * wz) + f2v{e[4 * r + 3], e[4 * r + 3]};
+    }
+    const f2v nx = p[0] * f2v{cam.fx, cam.fx}, ny = p[1] * f2v{cam.fy, cam.fy};
+    const f2v rz = f2v{__builtin_amdgcn_rcpf(p[2].x), __builtin_amdgcn_rcpf(p[2].y)};
+    const f2v qx = nx * rz, qy = ny * rz;
+    const f2v tx = (qx + f2v{cam.mx, cam.mx}) + f2v{0.5f, 0.5f};
+    const f2v ty = (qy + f2v{cam.my, cam.my}) + f2v{0.5f, 0.5f};
+    const uint32_t ux0 = (uint32_t)proj_fix(nx.x, p[2].x, qx.x, cam.mx, tx.x);
+    const uint32_t ux1 = (uint32_t)proj_fix(nx.y, p[2].y, qx.y, cam.mx, tx.y);
+    const uint32_t uy0 = (uint32_t)proj_fix(ny.x, p[2].x, qy.x, cam.my, ty.x);
+    const uint32_t uy1 = (uint32_t)proj_fix(ny.y, p[2].y, qy.y, cam.my, ty.y);
+    pz = p[2];
+    pix0 = (ux0 < cam.imageWidth && uy0 < cam.imageHeight && haveColor) ? uy0 * cam.imageWidth + ux0 : 0xFFFFFFFFu;
+    pix1 = (ux1 < cam.imageWidth && uy1 < cam.imageHeight && haveColor) ? uy1 * cam.imageWidth + ux1 : 0xFFFFFFFFu;
 }
 
 // Projection + band test of one voxel for one pose (CUDASceneRepHashSDF.cu:429-466): pixel index
@@ -790,7 +835,7 @@ __device__ __forceinline__ bool voxel_in_band(const HashArgs& A, float dz, float
 // integrateDepthMapKernel<deIntegrate>, CUDASceneRepHashSDF.cu:420-521. One wave per block:
 // lane = (y, x) of a z-slice, 8 slices. Voxel bytes are touched only inside the band.
 template <bool DEINT, int ZC>
-__global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __restrict__ depthImg,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_integrate(HashArgs A, const float* __restrict__ depthImg,
                                                    const uint32_t* __restrict__ colorImg, BFDepthCameraParams cam,
                                                    BFMat4 Tinv) {
     const uint32_t nvis = A.ctrl[C_BAND];
@@ -860,12 +905,7 @@ __global__ __launch_bounds__(256) void k_integrate(HashArgs A, const float* __re
             float r0, r1, r2, nsdf, nw;
             uint32_t ncol;
             if (!DEINT) {
-                if (w0 == 0.0f) { r0 = cu0; r1 = cu1; r2 = cu2; }
-                else { r0 = 0.2f * cu0 + 0.8f * oc0; r1 = 0.2f * cu1 + 0.8f * oc1; r2 = 0.2f * cu2 + 0.8f * oc2; }
-                r0 = fmaxf(0.0f, fminf(roundf(r0), 254.5f));
-                r1 = fmaxf(0.0f, fminf(roundf(r1), 254.5f));
-                r2 = fmaxf(0.0f, fminf(roundf(r2), 254.5f));
-                ncol = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+                ncol = blend_color(c, o, w0 == 0.0f);
                 nsdf = (sdf * wUpd + s0 * w0) / (wUpd + w0);
                 nw = fminf(A.weightMax, wUpd + w0);
             } else {
@@ -1093,13 +1133,16 @@ __global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraPara
         const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
         const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
+        const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
         int dcount = 0;
         uint32_t nupd = 0, nrmw = 0;
 #pragma unroll
         for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
-            float vs[ZC], vw[ZC], w0[ZC];
+            float vs[ZC], vw[ZC], w0[ZC], wz[ZC];
             uint32_t vc[ZC];
             uint32_t loaded = 0;
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) wz[zi] = (float)(bz + z0 + zi) * A.voxelSize;  // vvox_to_world z
 #pragma unroll
             for (int zi = 0; zi < ZC; zi++) { vs[zi] = 0.0f; vw[zi] = 0.0f; w0[zi] = 0.0f; vc[zi] = 0u; }
             for (uint32_t mk = mask; mk; mk &= mk - 1) {
@@ -1111,10 +1154,14 @@ __global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraPara
                 float d[ZC], pz[ZC];
                 uint32_t pix[ZC];
 #pragma unroll
-                for (int zi = 0; zi < ZC; zi++) {
-                    pix[zi] = voxel_pixel(cam, Ti, bx, by, bz + z0 + zi, A.voxelSize, colorImg != nullptr, pz[zi]);
-                    d[zi] = pix[zi] != 0xFFFFFFFFu ? depthImg[pix[zi]] : -INFINITY;
+                for (int zi = 0; zi < ZC; zi += 2) {
+                    f2v pz2;
+                    voxel_pixel2(cam, Ti, wx, wy, f2v{wz[zi], wz[zi + 1]}, colorImg != nullptr, pix[zi], pix[zi + 1], pz2);
+                    pz[zi] = pz2.x;
+                    pz[zi + 1] = pz2.y;
                 }
+#pragma unroll
+                for (int zi = 0; zi < ZC; zi++) d[zi] = pix[zi] != 0xFFFFFFFFu ? depthImg[pix[zi]] : -INFINITY;
                 float sd[ZC];
                 uint32_t cc[ZC];
                 uint32_t in = 0;
@@ -1145,6 +1192,122 @@ __global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraPara
 #pragma unroll
             for (int zi = 0; zi < ZC; zi++) {
                 if (!((loaded >> zi) & 1u)) continue;
+                Vox3 nv;
+                nv.a = __float_as_uint(vs[zi]);
+                nv.b = __float_as_uint(vw[zi]);
+                nv.c = vc[zi];
+                *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane)) = nv;
+                dcount += (int)(vw[zi] >= 1.0f) - (int)(w0[zi] >= 1.0f);
+                nrmw++;
+            }
+        }
+        const unsigned long long anyChange = __ballot(dcount != 0);
+        if (anyChange) {
+            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
+            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
+        }
+        updated += nupd;
+        rmw += nrmw;
+    }
+    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
+    __syncthreads();
+    flush_stats2(A.stats, S_BUPD, updated, S_BRMW, rmw);
+}
+
+// k_apply_ops with the memory round trips of an op batched: the ZC voxels of the lane are loaded
+// once at the start of the round (whether or not an op reaches them: +12 B per untouched voxel, but
+// no dependent load in the op loop), and the ops of the block's mask are taken two at a time —
+// both projections, then the depth AND colour gathers of both issued back to back, then the band
+// tests and updates of the first op followed by the second (sequence order, on the register copy).
+// Per pair of ops one gather round trip instead of ~4. Same arithmetic, same results.
+template <int ZC>
+__device__ __forceinline__ void apply_project(const HashArgs& A, const BFDepthCameraParams& cam, const OpTable& ops,
+                                              uint32_t k, float wx, float wy, const float* wz, uint32_t* pix, float* pz,
+                                              float* d, uint32_t* cc) {
+    const BFMat4 Ti = op_mat(ops.tinv[k]);
+    const float* depthImg = ops.depth[k];
+    const uint32_t* colorImg = ops.color[k];
+#pragma unroll
+    for (int zi = 0; zi < ZC; zi += 2) {
+        f2v pz2;
+        voxel_pixel2(cam, Ti, wx, wy, f2v{wz[zi], wz[zi + 1]}, colorImg != nullptr, pix[zi], pix[zi + 1], pz2);
+        pz[zi] = pz2.x;
+        pz[zi + 1] = pz2.y;
+    }
+#pragma unroll
+    for (int zi = 0; zi < ZC; zi++) {
+        const bool on = pix[zi] != 0xFFFFFFFFu;
+        d[zi] = on ? depthImg[pix[zi]] : -INFINITY;
+        cc[zi] = on ? colorImg[pix[zi]] : 0u;
+    }
+}
+template <int ZC>
+__device__ __forceinline__ uint32_t apply_update(const HashArgs& A, bool deint, const float* d, const float* pz,
+                                                 const uint32_t* cc, float* vs, float* vw, uint32_t* vc) {
+    uint32_t in = 0;
+#pragma unroll
+    for (int zi = 0; zi < ZC; zi++) {
+        float sd;
+        if (!voxel_in_band(A, d[zi], pz[zi], sd)) continue;
+        in |= 1u << zi;
+        if (deint) voxel_deintegrate(vs[zi], vw[zi], vc[zi], sd, cc[zi]);
+        else voxel_integrate(vs[zi], vw[zi], vc[zi], sd, cc[zi], A.weightMax);
+    }
+    return in;
+}
+template <int ZC, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops2(
+    HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks) {
+    const uint32_t nlist = A.ctrl[C_BAND];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int lx = lane & 7, ly = lane >> 3;
+    unsigned long long updated = 0, rmw = 0;
+    for (uint32_t b = wave; b < nlist; b += nwaves) {
+        const int4 e = A.band[b];
+        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
+        const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
+        const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
+        int dcount = 0;
+        uint32_t nupd = 0, nrmw = 0;
+#pragma unroll
+        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
+            float vs[ZC], vw[ZC], w0[ZC], wz[ZC];
+            uint32_t vc[ZC];
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) {
+                wz[zi] = (float)(bz + z0 + zi) * A.voxelSize;  // vvox_to_world z
+                const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane));
+                vs[zi] = __uint_as_float(v.a);
+                vw[zi] = __uint_as_float(v.b);
+                vc[zi] = v.c;
+                w0[zi] = vw[zi];
+            }
+            uint32_t touched = 0;
+            for (uint32_t mk = mask; mk;) {
+                const uint32_t k1 = (uint32_t)__builtin_ctz(mk);
+                mk &= mk - 1;
+                const bool two = mk != 0;
+                const uint32_t k2 = two ? (uint32_t)__builtin_ctz(mk) : k1;
+                if (two) mk &= mk - 1;
+                float d1[ZC], p1[ZC], d2[ZC], p2[ZC];
+                uint32_t x1[ZC], c1[ZC], x2[ZC], c2[ZC];
+                apply_project<ZC>(A, cam, ops, k1, wx, wy, wz, x1, p1, d1, c1);
+                if (two) apply_project<ZC>(A, cam, ops, k2, wx, wy, wz, x2, p2, d2, c2);
+                uint32_t in = apply_update<ZC>(A, (ops.deintMask >> k1) & 1u, d1, p1, c1, vs, vw, vc);
+                nupd += (uint32_t)__popc(in);
+                touched |= in;
+                if (two) {
+                    in = apply_update<ZC>(A, (ops.deintMask >> k2) & 1u, d2, p2, c2, vs, vw, vc);
+                    nupd += (uint32_t)__popc(in);
+                    touched |= in;
+                }
+            }
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) {
+                if (!((touched >> zi) & 1u)) continue;
                 Vox3 nv;
                 nv.a = __float_as_uint(vs[zi]);
                 nv.b = __float_as_uint(vw[zi]);
@@ -1392,7 +1555,17 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     const char* azEnv = std::getenv("BF_APPLY_ZC");  // tuning knob: z-slices per round of k_apply_ops
     applyZC_ = azEnv ? std::atoi(azEnv) : 4;
     if (applyZC_ != 2 && applyZC_ != 8) applyZC_ = 4;
-    if (applyZC_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<2>, 256, 0));
+    const char* akEnv = std::getenv("BF_APPLY_KERNEL");  // 2: batched-round-trip voxel pass (default), 1: per-op
+    applyKernel_ = akEnv ? std::atoi(akEnv) : 2;
+    const char* awEnv = std::getenv("BF_APPLY_WPE");  // occupancy target (waves per SIMD) of k_apply_ops2<2>
+    applyWpe_ = awEnv ? std::atoi(awEnv) : 8;
+    if (applyKernel_ == 2 && !azEnv) applyZC_ = 2;
+    if (applyKernel_ == 2 && applyZC_ == 8) applyZC_ = 4;
+    if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 8) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<2, 8>, 256, 0));
+    else if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 7) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<2, 7>, 256, 0));
+    else if (applyKernel_ == 2 && applyZC_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<2, 1>, 256, 0));
+    else if (applyKernel_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<4, 1>, 256, 0));
+    else if (applyZC_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<2>, 256, 0));
     else if (applyZC_ == 8) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<8>, 256, 0));
     else BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4>, 256, 0));
     applyGrid_ = (unsigned)std::max(1, occA) * (unsigned)numCUs_;
@@ -1606,7 +1779,15 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    if (applyZC_ == 2)
+    if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 8)
+        hipExtLaunchKernelGGL(k_apply_ops2<2, 8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    else if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 7)
+        hipExtLaunchKernelGGL(k_apply_ops2<2, 7>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    else if (applyKernel_ == 2 && applyZC_ == 2)
+        hipExtLaunchKernelGGL(k_apply_ops2<2, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    else if (applyKernel_ == 2)
+        hipExtLaunchKernelGGL(k_apply_ops2<4, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+    else if (applyZC_ == 2)
         hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
     else if (applyZC_ == 8)
         hipExtLaunchKernelGGL(k_apply_ops<8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);

@@ -185,3 +185,20 @@ def test_golden_fixture():
     np.testing.assert_array_equal(weight, g["weight"])
     np.testing.assert_array_equal(color, g["color"])
     assert heap_free == int(g["heap_free"])
+
+
+def test_integer_colour_blend_is_exact():
+    """csrc/tsdf.hip blend_channel: the integrate colour update u8(clamp(roundf(0.2f cu + 0.8f oc),
+    0, 254.5)) (CUDASceneRepHashSDF.cu:486-496, float32, no contraction) equals the integer form
+    min(((2 cu + 8 oc + 5) * 6554) >> 16, 254) for all 65536 (cu, oc)."""
+    import numpy as np
+    cu = np.arange(256, dtype=np.float32)[:, None]
+    oc = np.arange(256, dtype=np.float32)[None, :]
+    r = (np.float32(0.2) * cu).astype(np.float32) + (np.float32(0.8) * oc).astype(np.float32)
+    assert r.dtype == np.float32
+    t = np.trunc(r)
+    rf = t + ((r - t) >= np.float32(0.5))  # roundf for r >= 0
+    ref = np.minimum(np.maximum(rf, 0), 254.5).astype(np.uint8)
+    ci, oi = np.arange(256)[:, None], np.arange(256)[None, :]
+    alt = np.minimum(((2 * ci + 8 * oi + 5) * 6554) >> 16, 254)
+    np.testing.assert_array_equal(ref, alt)
