@@ -134,7 +134,7 @@ private:
     bool pairTable_ = false;       // pair table built for the current row table
     uint32_t pairCountHost_ = 0;   // read back once per table build when a sharded solve needs it
     bool lastPairMode_ = false;
-    DevBuf<int> rowSorted_, rowOther_, rowDeg_, rowNA_, pairStart_, rowPairStart_, pairA_, pairB_;
+    DevBuf<int> rowSorted_, rowOther_, rowSeg_, rowDeg_, rowNA_, pairStart_, rowPairStart_, pairA_, pairB_;
     DevBuf<int2> pairCorr_, rowPair_;
     DevBuf<double> pstat_, dstat_;
     DevBuf<float> apPair_, rzPart_;

@@ -73,7 +73,7 @@ struct BA {
     float distT, normT, colT, gradMin, dmin, dmax, verifyT;
     uint32_t sub;
     // assembled normal equations (pair mode)
-    int *rowSorted, *rowOther, *rowDeg, *rowNA, *pairStart, *rowPairStart, *pairA, *pairB;
+    int *rowSorted, *rowOther, *rowSeg, *rowDeg, *rowNA, *pairStart, *rowPairStart, *pairA, *pairB;
     int2 *pairCorr, *rowPair;
     double *pstat, *dstat;
     float *apPair, *rzPart;
@@ -445,6 +445,13 @@ __global__ __launch_bounds__(WG) void k_pair_sort(BA a) {
         a.rowSorted[s0 + t] = a.rowIdx[s0 + (k & ((1u << ROW_POS_BITS) - 1))];
         a.rowOther[s0 + t] = (int)u;
         const bool head = (t == 0 || (key[t - 1] >> ROW_POS_BITS) != u) && u != v;  // self pairs are skipped
+        int len = 0;
+        if (head) {  // run length of partner u, from the sorted keys in LDS
+            uint32_t e = t + 1;
+            while (e < (uint32_t)n && (key[e] >> ROW_POS_BITS) == u) e++;
+            len = (int)(e - t);
+        }
+        a.rowSeg[s0 + t] = len;
         deg += head ? 1 : 0;
         na += (head && u > v) ? 1 : 0;
     }
@@ -504,12 +511,10 @@ __device__ void pair_segments(const BA& a, uint32_t v) {
         const int rank = seg + __popcll(mh & lanes_below(lane));
         if (head) {
             if (OWN && u > (int)v) {
-                int e = t + 1;
-                while (e < n && a.rowOther[s0 + e] == u) e++;
                 const int p = a.pairStart[v] + segA + __popcll(ma & lanes_below(lane));
                 a.pairA[p] = (int)v;
                 a.pairB[p] = u;
-                a.pairCorr[p] = make_int2(s0 + t, e - t);
+                a.pairCorr[p] = make_int2(s0 + t, a.rowSeg[s0 + t]);
                 a.rowPair[a.rowPairStart[v] + rank] = make_int2(p, (int)((uint32_t)u | PAIR_A_FLAG));
             } else if (!OWN && u < (int)v) {  // pair (u, v): binary search v in u's partner list
                 int lo = a.pairStart[u], hi = a.pairStart[u + 1] - 1;
@@ -1807,6 +1812,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     maxPairsA_ = (uint32_t)std::min<size_t>((size_t)N * (N - 1) / 2, (size_t)cfg.maxCorr);
     rowSorted_.alloc(2 * (size_t)cfg.maxCorr + 1);
     rowOther_.alloc(2 * (size_t)cfg.maxCorr + 1);
+    rowSeg_.alloc(2 * (size_t)cfg.maxCorr + 1);
     rowDeg_.alloc(N + 1);
     rowNA_.alloc(N + 1);
     pairStart_.alloc(N + 1);
@@ -1899,7 +1905,7 @@ void Solver::solve(const SolveArgs& s) {
     a.gradMin = cfg_.denseColorGradientMin; a.dmin = cfg_.denseDepthMin; a.dmax = cfg_.denseDepthMax;
     a.sub = cfg_.denseOverlapSubsample ? cfg_.denseOverlapSubsample : 4;
     a.verifyT = cfg_.verifyOptDistThresh;
-    a.rowSorted = rowSorted_.p; a.rowOther = rowOther_.p; a.rowDeg = rowDeg_.p; a.rowNA = rowNA_.p;
+    a.rowSorted = rowSorted_.p; a.rowOther = rowOther_.p; a.rowSeg = rowSeg_.p; a.rowDeg = rowDeg_.p; a.rowNA = rowNA_.p;
     a.pairStart = pairStart_.p; a.rowPairStart = rowPairStart_.p; a.pairA = pairA_.p; a.pairB = pairB_.p;
     a.pairCorr = pairCorr_.p; a.rowPair = rowPair_.p; a.pstat = pstat_.p; a.dstat = dstat_.p;
     a.apPair = apPair_.p; a.rzPart = rzPart_.p;

@@ -43,4 +43,9 @@ void Comm::allreduceSum(double* buf, size_t n, hipStream_t stream) {
     BF_NCCL(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, static_cast<ncclComm_t>(comm_), stream));
 }
 
+void Comm::broadcast(float* buf, size_t n, int root, hipStream_t stream) {
+    if (n == 0) return;
+    BF_NCCL(ncclBroadcast(buf, buf, n, ncclFloat, root, static_cast<ncclComm_t>(comm_), stream));
+}
+
 }  // namespace bf

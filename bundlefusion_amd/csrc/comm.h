@@ -21,6 +21,8 @@ public:
     int rank() const { return rank_; }
     // in-place sum over ranks of n doubles, enqueued on stream (no host synchronisation)
     void allreduceSum(double* buf, size_t n, hipStream_t stream);
+    // root's n floats to every rank, in place, enqueued on stream
+    void broadcast(float* buf, size_t n, int root, hipStream_t stream);
 
 private:
     void* comm_ = nullptr;  // ncclComm_t

@@ -88,8 +88,8 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     globalValid_.assign(K, 1);
     complete_.resize(opt_.maxFrames);
 
-    dLocalRot_.alloc(3 * L);
-    dLocalTrans_.alloc(3 * L);
+    dLocalRot_.alloc(6 * L);
+    dLocalTrans_ = dLocalRot_.p + 3 * L;
     dLocalT_.alloc(16 * L);
     dLocalValid_.alloc(L);
     dLocalCache_.alloc(L);
@@ -314,9 +314,18 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         if (!fr.cache.depth) haveCache = false;
     }
     BF_HIP(hipMemcpyAsync(dLocalT_.p, P.localInit, 64 * n, hipMemcpyHostToDevice, baStream_));
-    matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_.p, dLocalValid_.p, baStream_);
+    matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_, dLocalValid_.p, baStream_);
     const auto& lc = localCorr_[s];
-    if (n >= 2 && lc.first && lc.second > 0) {
+    // multi-GPU: submap s's local solve runs on rank s % R only (the submaps are independent units,
+    // SURVEY.md §8(e)2); its poses are then broadcast so that every rank continues identically
+    const bool shardLocal = comm_ && comm_->size() > 1;
+    const int localOwner = shardLocal ? (int)(s % (uint32_t)comm_->size()) : 0;
+    const bool solveHere = !shardLocal || localOwner == comm_->rank();
+    if (n >= 2 && lc.first && lc.second > 0 && !solveHere) {
+        comm_->broadcast(dLocalRot_.p, 6 * (size_t)(S + 1), localOwner, baStream_);
+        poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
+        BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
+    } else if (n >= 2 && lc.first && lc.second > 0) {
         if (haveCache)
             BF_HIP(hipMemcpyAsync(dLocalCache_.p, P.cacheTable, sizeof(BFCachedFrame) * n, hipMemcpyHostToDevice, baStream_));
         std::vector<float> ws(opt_.localNonLin, 1.0f), wd(opt_.localNonLin), wc(opt_.localNonLin, 0.0f);
@@ -336,13 +345,14 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         a.cacheH = opt_.cacheHeight;
         std::memcpy(a.intrinsics, opt_.cacheIntrinsics, sizeof(a.intrinsics));
         a.rot = dLocalRot_.p;
-        a.trans = dLocalTrans_.p;
+        a.trans = dLocalTrans_;
         a.rebuildJT = true;
         a.findMaxResidual = false;  // optimizeLocal: no max residual removal (OnlineBundler.cpp:255)
         local_->solve(a);
         local_->resultAsync(P.ctrl);
         P.localSolved = true;
-        poses_to_matrices(dLocalRot_.p, dLocalTrans_.p, n, dLocalT_.p, dLocalValid_.p, baStream_);
+        if (shardLocal) comm_->broadcast(dLocalRot_.p, 6 * (size_t)(S + 1), localOwner, baStream_);
+        poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
         BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
     } else {
         std::memcpy(P.localT, P.localInit, 64 * n);
@@ -379,7 +389,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     BF_HIP(hipMemcpyAsync(P.valid, dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
     P.numKeyframes = nk;
     // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
-    if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_.p, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_);
+    if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_);
     BF_HIP(hipEventRecord(P.done, baStream_));
     inflight_.push_back(slot);
     lastSubmapEnqueued_ = s;

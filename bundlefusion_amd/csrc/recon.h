@@ -112,7 +112,8 @@ private:
     std::deque<uint32_t> inflight_;     // ring indices in submap order
     uint32_t ringNext_ = 0;
 
-    DevBuf<float> dLocalRot_, dLocalTrans_, dLocalT_;
+    DevBuf<float> dLocalRot_, dLocalT_;  // dLocalRot_ holds [rot 3L | trans 3L] (one broadcast)
+    float* dLocalTrans_ = nullptr;
     DevBuf<int> dLocalValid_;
     DevBuf<BFCachedFrame> dLocalCache_;
     DevBuf<float> dGlobalRot_, dGlobalTrans_, dGlobalT_;

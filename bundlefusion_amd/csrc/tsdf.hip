@@ -365,9 +365,18 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
     // streaming mask) depend only on the block, so they run once per distinct block in phase 2
     // instead of once per DDA step: same emitted set, far fewer projections.
     unsigned long long emitted = 0;
-    for (uint32_t iter = 0; iter < 1024 && active; iter++) {
-        {
-            const unsigned long long key = block_key(id.x, id.y, id.z);
+    const uint32_t lane = lane_id();
+    // The loop runs while any lane of the wave walks (wave-uniform trip) so that lanes can compare
+    // keys: a lane whose left (same pixel row) or upper neighbour pixel reaches the same block in
+    // the same step leaves the insert to it (the chain ends at a lane that inserts or emits it), so
+    // the LDS set sees far fewer same-address CAS. The emitted set is unchanged.
+    for (uint32_t iter = 0; iter < 1024; iter++) {
+        if (!__any(active)) break;
+        const unsigned long long myKey = active ? block_key(id.x, id.y, id.z) : EMPTY_KEY;
+        const unsigned long long left = __shfl_up(myKey, 1, ALLOC_TILE), up = __shfl_up(myKey, ALLOC_TILE);
+        const bool dup = ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
+        if (active && !dup) {
+            const unsigned long long key = myKey;
             uint32_t h = mix_hash(key) & (LDS_SET - 1);
             bool placed = false;
             for (int p = 0; p < 16; p++) {
@@ -389,6 +398,7 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
             }
         }
         // traverse (CUDASceneRepHashSDF.cu:231-246)
+        if (!active) continue;
         if (tMax.x < tMax.y && tMax.x < tMax.z) {
             id.x = f2i((float)id.x + step.x);
             if (id.x == idBound.x) active = false;
