@@ -313,6 +313,17 @@ def main():
     out["raycast"] = {"ms_per_render": t_r * 1e3, "k_render_us": (ms1 - ms0) / max(1, n1 - n0) * 1e3,
                       "valid_fraction": float(np.isfinite(rdepth).mean()),
                       "note": "compactify + interval splat + renderKernel + computeNormals at 640x480 from the last pose"}
+    # marching cubes over the final scene (StopScanningAndExtractIsoSurfaceMC, reported beside the metric)
+    mcp = bfa.mc_params(params.virtualVoxelSize)
+    mbuf = bfa.DeviceArray((mcp.maxNumTriangles, 3, 6), np.float32)
+    rc.extract_mesh_device(mcp, mbuf)  # warm
+    t_m = time.perf_counter()
+    nt, tt = rc.extract_mesh_device(mcp, mbuf)
+    t_m = time.perf_counter() - t_m
+    out["mesh"] = {"ms_extract": t_m * 1e3, "triangles": nt, "triangles_total": tt,
+                   "allocated_blocks": int(params.numSDFBlocks - rc.heap_free_count()),
+                   "note": "marching cubes over every allocated block (count + scan + emit), 3M-triangle cap"}
+    del mbuf
     if rank == 0 and not args.no_cpu_baseline:
         gpu = {"keyframes": int(min(K, (args.warmup + args.steps))),
                "gn_per_solve": st["globalGnIterations"] / max(1, st["globalSolves"]),

@@ -13,11 +13,11 @@ import os
 import numpy as np
 
 from . import abi
-from .abi import (BFDepthCameraParams, BFHashParams, BFRayCastParams, BFSceneOptions, BFSynthScene, BFTsdfStats,
-                  HASH_ENTRY_DTYPE, VOXEL_DTYPE)
+from .abi import (BFDepthCameraParams, BFHashParams, BFMarchingCubesParams, BFRayCastParams, BFSceneOptions,
+                  BFSynthScene, BFTsdfStats, HASH_ENTRY_DTYPE, VOXEL_DTYPE)
 
 __all__ = ["lib", "BFError", "DeviceArray", "SceneRepHashSDF", "hash_params", "depth_camera",
-           "synth_scene", "synth_pose", "synth_render", "synth_render_host"]
+           "synth_scene", "synth_pose", "synth_render", "synth_render_host", "mc_params", "mesh_merge", "mesh_save_ply"]
 
 _lib = None
 
@@ -244,12 +244,65 @@ class SceneRepHashSDF:
             res += [a.download() for a in iv]
         return tuple(res)
 
+    def extract_mesh(self, mc: BFMarchingCubesParams):
+        """CUDAMarchingCubesHashSDF::extractIsoSurface: float32 triangles [n, 3 vertices, 6] (x, y, z, r, g, b)
+        in the fixed (heap block, voxel, triTable) order, and the count before the maxNumTriangles cap."""
+        cap = int(mc.maxNumTriangles)
+        buf = DeviceArray((max(cap, 1), 3, 6), np.float32)
+        n, total = C.c_uint32(), C.c_uint32()
+        check(lib().bf_scene_extract_mesh(self.h, C.byref(mc), buf.ptr if cap else None, C.byref(n), C.byref(total)))
+        tris = buf.download_range(0, n.value * 72).view(np.float32).reshape(n.value, 3, 6) if n.value else \
+            np.zeros((0, 3, 6), np.float32)
+        return tris, total.value
+
     def export_visible(self) -> np.ndarray:
         cap = self.params.numSDFBlocks
         out = np.empty((cap, 4), np.int32)
         n = C.c_uint32()
         check(lib().bf_scene_export_visible(self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), cap, C.byref(n)))
         return out[: n.value].copy()
+
+
+# ---- mesh output ---------------------------------------------------------------------------
+def mc_params(voxel_size: float, thresh_factor: float = 10.0, max_triangles: int = 3000000, box=None) -> BFMarchingCubesParams:
+    """CUDAMarchingCubesHashSDF::parametersFromGlobalAppState (CUDAMarchingCubesHashSDF.h:19-28):
+    both thresholds = s_SDFMarchingCubeThreshFactor * s_SDFVoxelSize; box = (minCorner, maxCorner) or None."""
+    p = BFMarchingCubesParams()
+    t = float(np.float32(thresh_factor) * np.float32(voxel_size))
+    p.threshMarchingCubes = p.threshMarchingCubes2 = t
+    p.maxNumTriangles = max_triangles
+    if box is not None:
+        p.boxEnabled = 1
+        p.minCorner[:] = [float(v) for v in box[0]]
+        p.maxCorner[:] = [float(v) for v in box[1]]
+    return p
+
+
+def _tri_ptr(tris: np.ndarray):
+    t = np.ascontiguousarray(tris, np.float32)
+    assert t.size % 18 == 0
+    return t, t.ctypes.data_as(C.c_void_p), t.size // 18
+
+
+def mesh_merge(tris: np.ndarray, transform=None):
+    """saveMesh's indexed mesh (bf_mesh_merge): (vertices [nv,3], colors [nv,4], faces [nf,3])."""
+    t, ptr, n = _tri_ptr(tris)
+    v = np.empty((3 * n, 3), np.float32)
+    c = np.empty((3 * n, 4), np.float32)
+    f = np.empty((n, 3), np.uint32)
+    nv, nf = C.c_uint32(), C.c_uint32()
+    check(lib().bf_mesh_merge(ptr, C.c_uint32(n), abi.mat(transform) if transform is not None else None,
+                              abi.vp(v), abi.vp(c), abi.vp(f), C.byref(nv), C.byref(nf)))
+    return v[: nv.value].copy(), c[: nv.value].copy(), f[: nf.value].copy()
+
+
+def mesh_save_ply(path: str, tris: np.ndarray, transform=None):
+    """CUDAMarchingCubesHashSDF::saveMesh (bf_mesh_save_ply); returns (vertices, faces) written."""
+    t, ptr, n = _tri_ptr(tris)
+    nv, nf = C.c_uint32(), C.c_uint32()
+    check(lib().bf_mesh_save_ply(os.fsencode(path), ptr, C.c_uint32(n),
+                                 abi.mat(transform) if transform is not None else None, C.byref(nv), C.byref(nf)))
+    return nv.value, nf.value
 
 
 # ---- synthetic stream ----------------------------------------------------------------------

@@ -79,6 +79,12 @@ class BFRayCastParams(C.Structure):
     ]
 
 
+class BFMarchingCubesParams(C.Structure):
+    _fields_ = [("threshMarchingCubes", C.c_float), ("threshMarchingCubes2", C.c_float),
+                ("boxEnabled", C.c_uint32), ("maxNumTriangles", C.c_uint32),
+                ("minCorner", C.c_float * 3), ("maxCorner", C.c_float * 3)]
+
+
 class BFTsdfStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",

@@ -335,6 +335,13 @@ int bf_scene_raycast(bf_scene* s, const float T[16], const BFDepthCameraParams* 
                       reinterpret_cast<float4*>(colors), rayMin, rayMax);
     BF_CATCH
 }
+int bf_scene_extract_mesh(bf_scene* s, const BFMarchingCubesParams* p, BFMcTriangle* tris, uint32_t* numTriangles,
+                          uint32_t* totalTriangles) {
+    BF_TRY
+    BF_REQUIRE(s && p && numTriangles, BF_ERR_ARG, "null argument");
+    *numTriangles = s->scene->extractMesh(*p, tris, tris ? p->maxNumTriangles : 0u, totalTriangles);
+    BF_CATCH
+}
 int bf_scene_synchronize(bf_scene* s) {
     BF_TRY
     BF_REQUIRE(s, BF_ERR_ARG, "null scene");
@@ -697,6 +704,14 @@ int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, 
                           reinterpret_cast<float4*>(normals), reinterpret_cast<float4*>(colors), nullptr, nullptr);
     BF_CATCH
 }
+int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTriangle* tris, uint32_t* numTriangles,
+                          uint32_t* totalTriangles) {
+    BF_TRY
+    BF_REQUIRE(r && p && numTriangles, BF_ERR_ARG, "null argument");
+    r->r->synchronize();
+    *numTriangles = r->r->scene().extractMesh(*p, tris, tris ? p->maxNumTriangles : 0u, totalTriangles);
+    BF_CATCH
+}
 int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches) {
     BF_TRY
     BF_REQUIRE(r && ms && launches, BF_ERR_ARG, "null argument");
@@ -792,6 +807,29 @@ int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]) {
 
 
 // ---- input formats and preprocessing ------------------------------------------------------------
+int bf_mesh_merge(const BFMcTriangle* tris, uint32_t n, const float transform[16], float* vertices, float* colors,
+                  uint32_t* faces, uint32_t* numVertices, uint32_t* numFaces) {
+    BF_TRY
+    BF_REQUIRE(tris || n == 0, BF_ERR_ARG, "null triangles");
+    const Mesh m = mesh_from_triangles(tris, n, transform);
+    if (vertices) std::memcpy(vertices, m.vertices.data(), 4 * m.vertices.size());
+    if (colors) std::memcpy(colors, m.colors.data(), 4 * m.colors.size());
+    if (faces) std::memcpy(faces, m.faces.data(), 4 * m.faces.size());
+    if (numVertices) *numVertices = (uint32_t)(m.vertices.size() / 3);
+    if (numFaces) *numFaces = (uint32_t)(m.faces.size() / 3);
+    BF_CATCH
+}
+int bf_mesh_save_ply(const char* path, const BFMcTriangle* tris, uint32_t n, const float transform[16],
+                     uint32_t* numVertices, uint32_t* numFaces) {
+    BF_TRY
+    BF_REQUIRE(path && (tris || n == 0), BF_ERR_ARG, "null argument");
+    const Mesh m = mesh_from_triangles(tris, n, transform);
+    mesh_save_ply(path, m);
+    if (numVertices) *numVertices = (uint32_t)(m.vertices.size() / 3);
+    if (numFaces) *numFaces = (uint32_t)(m.faces.size() / 3);
+    BF_CATCH
+}
+
 int bf_sens_open(const char* path, bf_sens** out) {
     BF_TRY
     BF_REQUIRE(path && out, BF_ERR_ARG, "null argument");

@@ -4,6 +4,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <array>
 #include <cctype>
 #include <cmath>
 #include <cstdlib>
@@ -11,6 +12,8 @@
 #include <fstream>
 #include <limits>
 #include <sstream>
+#include <unordered_map>
+#include <unordered_set>
 
 #include "bf_runtime.h"
 
@@ -271,6 +274,99 @@ std::string ParamFile::str(const std::string& key) const {
     std::string t = raw(key);
     if (t.size() >= 2 && t.front() == '"' && t.back() == '"') t = t.substr(1, t.size() - 2);
     return t;
+}
+
+// ---- mesh output (CUDAMarchingCubesHashSDF::saveMesh, CUDAMarchingCubesHashSDF.cpp:48-105) --------
+// MeshData::mergeCloseVertices / removeDuplicateFaces / applyTransform and MeshIOf::saveToFile are
+// mLib (not vendored): restated from their documented behaviour, parity unpinned.
+namespace {
+
+struct Key3Hash {
+    size_t operator()(const std::array<int, 3>& k) const {
+        return ((size_t)(uint32_t)k[0] * 73856093u) ^ ((size_t)(uint32_t)k[1] * 19349669u) ^ ((size_t)(uint32_t)k[2] * 83492791u);
+    }
+};
+
+// toVirtualVoxelPos(v, thresh): round half away from zero of v / thresh, truncated to int
+int snap(float v, float t) {
+    const float q = v / t;
+    return (int)(q + (float)((0.0f < q) - (q < 0.0f)) * 0.5f);
+}
+
+}  // namespace
+
+Mesh mesh_from_triangles(const BFMcTriangle* tris, uint32_t n, const float* transform) {
+    const float eps = 0.00001f;  // mergeCloseVertices(0.00001f, true) (CUDAMarchingCubesHashSDF.cpp:87)
+    Mesh m;
+    std::unordered_map<std::array<int, 3>, uint32_t, Key3Hash> cell;
+    cell.reserve((size_t)n * 2);
+    std::vector<uint32_t> face;
+    face.reserve((size_t)n * 3);
+    for (uint32_t t = 0; t < n; t++)
+        for (int k = 0; k < 3; k++) {  // copyTrianglesToCPU: vertex 3t+k, colour vec4f(c, 1)
+            const BFMcVertex& v = tris[t].v[k];
+            const std::array<int, 3> key = {snap(v.p[0], eps), snap(v.p[1], eps), snap(v.p[2], eps)};
+            auto it = cell.find(key);
+            if (it != cell.end()) {
+                face.push_back(it->second);
+                continue;
+            }
+            const uint32_t id = (uint32_t)(m.vertices.size() / 3);
+            cell.emplace(key, id);
+            m.vertices.insert(m.vertices.end(), {v.p[0], v.p[1], v.p[2]});
+            m.colors.insert(m.colors.end(), {v.c[0], v.c[1], v.c[2], 1.0f});
+            face.push_back(id);
+        }
+    // degenerate faces (two corners merged) go, then removeDuplicateFaces: first face of each vertex set
+    std::unordered_set<std::array<int, 3>, Key3Hash> seen;
+    seen.reserve((size_t)n * 2);
+    for (uint32_t t = 0; t < n; t++) {
+        const uint32_t a = face[3 * t], b = face[3 * t + 1], c = face[3 * t + 2];
+        if (a == b || b == c || a == c) continue;
+        std::array<int, 3> k = {(int)a, (int)b, (int)c};
+        std::sort(k.begin(), k.end());
+        if (!seen.insert(k).second) continue;
+        m.faces.insert(m.faces.end(), {a, b, c});
+    }
+    if (transform) {  // applyTransform: affine point transform
+        const float* e = transform;
+        for (size_t i = 0; i < m.vertices.size(); i += 3) {
+            const float x = m.vertices[i], y = m.vertices[i + 1], z = m.vertices[i + 2];
+            m.vertices[i] = e[0] * x + e[1] * y + e[2] * z + e[3];
+            m.vertices[i + 1] = e[4] * x + e[5] * y + e[6] * z + e[7];
+            m.vertices[i + 2] = e[8] * x + e[9] * y + e[10] * z + e[11];
+        }
+    }
+    return m;
+}
+
+void mesh_save_ply(const std::string& path, const Mesh& m) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    BF_REQUIRE(f != nullptr, BF_ERR_IO, "cannot open " + path + " for writing");
+    const size_t nv = m.vertices.size() / 3, nf = m.faces.size() / 3;
+    std::string hdr = "ply\nformat binary_little_endian 1.0\nelement vertex " + std::to_string(nv) +
+                      "\nproperty float x\nproperty float y\nproperty float z\nproperty uchar red\nproperty uchar green\n"
+                      "property uchar blue\nproperty uchar alpha\nelement face " + std::to_string(nf) +
+                      "\nproperty list uchar int vertex_indices\nend_header\n";
+    std::vector<uint8_t> buf;
+    buf.reserve(hdr.size() + nv * 16 + nf * 13);
+    buf.insert(buf.end(), hdr.begin(), hdr.end());
+    auto put = [&](const void* p, size_t n) { buf.insert(buf.end(), (const uint8_t*)p, (const uint8_t*)p + n); };
+    for (size_t i = 0; i < nv; i++) {
+        put(&m.vertices[3 * i], 12);
+        uint8_t c[4];
+        for (int k = 0; k < 4; k++) c[k] = (uint8_t)std::lround(std::fmin(std::fmax(m.colors[4 * i + k], 0.0f), 1.0f) * 255.0f);
+        put(c, 4);
+    }
+    for (size_t i = 0; i < nf; i++) {
+        const uint8_t three = 3;
+        put(&three, 1);
+        const int32_t idx[3] = {(int32_t)m.faces[3 * i], (int32_t)m.faces[3 * i + 1], (int32_t)m.faces[3 * i + 2]};
+        put(idx, 12);
+    }
+    const bool ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    std::fclose(f);
+    BF_REQUIRE(ok, BF_ERR_IO, "short write to " + path);
 }
 
 }  // namespace bf

@@ -54,6 +54,15 @@ private:
     std::vector<uint8_t> buf_;
 };
 
+// Indexed mesh of CUDAMarchingCubesHashSDF::saveMesh (CUDAMarchingCubesHashSDF.cpp:71-100)
+struct Mesh {
+    std::vector<float> vertices;  // 3 per vertex
+    std::vector<float> colors;    // 4 per vertex (vec4f(colour, 1))
+    std::vector<uint32_t> faces;  // 3 per face
+};
+Mesh mesh_from_triangles(const BFMcTriangle* tris, uint32_t n, const float* transform);
+void mesh_save_ply(const std::string& path, const Mesh& m);
+
 class ParamFile {
 public:
     void load(const std::string& path);  // later files override earlier keys

@@ -112,6 +112,10 @@ public:
     void raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRayCastParams& rp, float* depth, float4* depth4,
                  float4* normals, float4* colors, float* rayMin, float* rayMax);
     KernelClock& renderClock() { return renderClock_; }
+    // CUDAMarchingCubesHashSDF::extractIsoSurface (CUDAMarchingCubesHashSDF.cpp:107-118) over every
+    // allocated block: writes min(total, cap) triangles to the device array out in (heap block,
+    // voxel, case-table) order, returns that count; *total = triangles before the cap. Synchronizes.
+    uint32_t extractMesh(const BFMarchingCubesParams& p, BFMcTriangle* out, uint32_t cap, uint32_t* total);
 
 private:
     void alloc(const float* depth, const BFDepthCameraParams& cam, const uint32_t* bitMask);

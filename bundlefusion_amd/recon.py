@@ -155,6 +155,13 @@ class Recon:
         """render into preallocated DeviceArrays (depth, depth4, normals, colors)"""
         check(lib().bf_recon_raycast(self.h, _mat(T), C.byref(rp), *[o.ptr for o in outs]))
 
+    def extract_mesh_device(self, mc, out):
+        """StopScanningAndExtractIsoSurfaceMC into a preallocated DeviceArray of mc.maxNumTriangles x 72 B;
+        returns (written, total)."""
+        n, total = C.c_uint32(), C.c_uint32()
+        check(lib().bf_recon_extract_mesh(self.h, C.byref(mc), out.ptr, C.byref(n), C.byref(total)))
+        return n.value, total.value
+
     def render_time(self):
         ms = C.c_double()
         n = C.c_uint64()

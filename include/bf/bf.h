@@ -115,6 +115,15 @@ int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* 
 int bf_scene_raycast(bf_scene* s, const float T[16], const BFDepthCameraParams* cam, const BFRayCastParams* rp, float* depth,
                      float* depth4, float* normals, float* colors, float* rayMin, float* rayMax);
 int bf_scene_synchronize(bf_scene* s);
+/* CUDAMarchingCubesHashSDF::extractIsoSurface (CUDAMarchingCubesHashSDF.cpp:107-118 ->
+ * resetMarchingCubesCUDA + extractIsoSurfaceCUDA, CUDAMarchingCubesSDF.cu:29-53) over every allocated
+ * block (the s_streamingEnabled = 0 path of StopScanningAndExtractIsoSurfaceMC, DepthSensing.cpp:348-352).
+ * tris: DEVICE BFMcTriangle[p->maxNumTriangles]; *numTriangles = triangles written (at most
+ * maxNumTriangles, extra ones dropped as the reference's appendTriangle does); *totalTriangles (may be
+ * NULL) = the count before that cap. Output order is fixed: heap block, voxel (z*64 + y*8 + x),
+ * triTable order (the reference's atomic append order varies run to run). Synchronizes. */
+int bf_scene_extract_mesh(bf_scene* s, const BFMarchingCubesParams* p, BFMcTriangle* tris, uint32_t* numTriangles,
+                          uint32_t* totalTriangles);
 int bf_scene_device_bytes(bf_scene* s, uint64_t* bytes);
 /* time the next operations on the scene's stream */
 int bf_scene_timer_start(bf_scene* s, bf_timer* t);
@@ -298,6 +307,10 @@ int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n);
  * depth camera; device outputs as bf_scene_raycast */
 int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, float* depth, float* depth4, float* normals,
                      float* colors);
+/* StopScanningAndExtractIsoSurfaceMC (DepthSensing.cpp:335-365) on the loop's scene: waits for the
+ * scene stream, then bf_scene_extract_mesh (tris: DEVICE BFMcTriangle[p->maxNumTriangles]) */
+int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTriangle* tris, uint32_t* numTriangles,
+                          uint32_t* totalTriangles);
 /* summed device time / count of the renderKernel launches since the first call (enables the clock) */
 int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches);
 /* debugHash-style dump of the loop's scene (same layout as bf_scene_export) */
@@ -325,6 +338,21 @@ int bf_traj_frame_info(bf_traj* t, uint32_t idx, int32_t* type, float* dist);
 int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]);
 
 /* ---- input formats and preprocessing ------------------------------------ */
+/* ---- mesh output: CUDAMarchingCubesHashSDF::saveMesh (CUDAMarchingCubesHashSDF.cpp:48-105) ------
+ * Triangle soup (HOST BFMcTriangle[n], e.g. from bf_scene_extract_mesh) -> indexed mesh as saveMesh
+ * builds it: mergeCloseVertices(1e-5, approx) (vertices snapped to a 1e-5 grid, first occurrence kept,
+ * faces remapped, degenerate faces dropped), removeDuplicateFaces (same vertex set), applyTransform.
+ * The mLib MeshData / MeshIO these call are not vendored: restated, parity unpinned.
+ * bf_mesh_merge: HOST outputs sized for the worst case (3n vertices, n faces); any may be NULL to
+ * count only. transform: row-major 4x4 or NULL. */
+int bf_mesh_merge(const BFMcTriangle* tris, uint32_t n, const float transform[16], float* vertices /* 3 per */,
+                  float* colors /* 4 per, RGBA in [0,1] */, uint32_t* faces /* 3 per */, uint32_t* numVertices,
+                  uint32_t* numFaces);
+/* ... and MeshIOf::saveToFile of the result: binary little-endian PLY (float x y z, uchar red green
+ * blue alpha, face list uchar/int). */
+int bf_mesh_save_ply(const char* path, const BFMcTriangle* tris, uint32_t n, const float transform[16],
+                     uint32_t* numVertices, uint32_t* numFaces);
+
 /* .sens reader (mLib SensorData v4 as SensorDataReader.cpp:38-116 uses it; format restated in
  * SURVEY.md Appendix B). Frames are read on demand. Depth: raw or zlib ushort; colour: raw RGB
  * (png / jpeg and occi return BF_ERR_ARG: no decoder in this build). */

@@ -179,9 +179,28 @@ typedef struct BFPreprocessOptions {
     float depthShift;              /* ushort -> metres divisor [1000] */
 } BFPreprocessOptions;
 
+/* MarchingCubesParams (Source/DepthSensing/MarchingCubesSDFUtil.h:9-22), filled as
+ * CUDAMarchingCubesHashSDF::parametersFromGlobalAppState (CUDAMarchingCubesHashSDF.h:19-28) does:
+ * both thresholds = s_SDFMarchingCubeThreshFactor [10] * s_SDFVoxelSize; maxNumTriangles =
+ * s_marchingCubesMaxNumTriangles [3 000 000]. */
+typedef struct BFMarchingCubesParams {
+    float threshMarchingCubes;     /* m_threshMarchingCubes: corner-pair sdf consistency bound */
+    float threshMarchingCubes2;    /* m_threshMarchingCubes2: per-corner |sdf| bound */
+    uint32_t boxEnabled;           /* m_boxEnabled: only voxels inside [minCorner, maxCorner] */
+    uint32_t maxNumTriangles;      /* m_maxNumTriangles: output capacity (extra triangles dropped) */
+    float minCorner[3];
+    float maxCorner[3];
+} BFMarchingCubesParams;
+
+/* MarchingCubesData::Vertex / Triangle (MarchingCubesSDFUtil.h:32-43): float3 position, float3
+ * colour in [0, 1]; 72 B per triangle. */
+typedef struct BFMcVertex { float p[3]; float c[3]; } BFMcVertex;
+typedef struct BFMcTriangle { BFMcVertex v[3]; } BFMcTriangle;
+
 #ifdef __cplusplus
 } /* extern "C" */
 
+static_assert(sizeof(BFMcTriangle) == 72, "MarchingCubesData::Triangle is 72 B");
 static_assert(sizeof(BFMat4) == 64, "float4x4 is 64 B");
 static_assert(sizeof(BFHashEntry) == 32, "HashEntry is 32 B");
 static_assert(sizeof(BFVoxel) == 12, "Voxel is 12 B");

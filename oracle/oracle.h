@@ -50,6 +50,11 @@ void or_dense_integrate(const float T[16], const float* depth, const uint8_t* co
 void or_raycast(const ORScene* s, const BFRayCastParams* rp, const BFDepthCameraParams* cam,
                 const float T[16], float* depth, float* depth4, float* normals, float* colors,
                 float* rayMin, float* rayMax);
+/* CUDAMarchingCubesHashSDF::extractIsoSurface restated: triangles of every allocated block in heap
+ * order, voxel order, triTable order; first cap written, *total before the cap */
+void or_mc_tables(uint16_t* edges, uint8_t* ntri, uint8_t* tri /* 256 x 15 */);
+void or_extract_mesh(const ORScene* s, const BFMarchingCubesParams* p, BFMcTriangle* out, uint32_t cap, uint32_t* n,
+                     uint32_t* total);
 
 /* ---- Lie helpers (LieDerivUtil.h) ------------------------------------------ */
 void or_pose_to_matrix(const float rot[3], const float trans[3], float M[16]);

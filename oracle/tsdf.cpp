@@ -7,6 +7,7 @@
 // Citations are to /root/reference/FriedLiver/Source/DepthSensing/.
 #include "oracle.h"
 #include "or_math.h"
+#include "../bundlefusion_amd/csrc/mc_tables.h"  // case tables (data; checked by tests/test_mc.py)
 
 #include <algorithm>
 #include <cstring>
@@ -770,5 +771,129 @@ extern "C" void or_raycast(const ORScene* o, const BFRayCastParams* rpIn, const 
                     if (l > 0.0f) { out[0] = n.x / -l; out[1] = n.y / -l; out[2] = n.z / -l; out[3] = 1.0f; }
                 }
             }
+    }
+}
+
+// ---- marching cubes: MarchingCubesData::extractIsoSurfaceAtPosition (MarchingCubesSDFUtil.h:119-227),
+// literal, voxel by voxel, over the allocated blocks in heap order (the GPU build's output order; the
+// reference kernel visits hash entries, CUDAMarchingCubesSDF.cu:15-27, and appends atomically).
+namespace {
+
+constexpr bf::McTables kMc = bf::make_mc_tables();
+
+BFMcVertex vertexInterp(float isolevel, f3 p1, f3 p2, float d1, float d2, const uint8_t c1[4], const uint8_t c2[4]) {
+    BFMcVertex r1, r2, res;
+    r1.p[0] = p1.x; r1.p[1] = p1.y; r1.p[2] = p1.z;
+    r1.c[0] = (float)c1[0] / 255.f; r1.c[1] = (float)c1[1] / 255.f; r1.c[2] = (float)c1[2] / 255.f;
+    r2.p[0] = p2.x; r2.p[1] = p2.y; r2.p[2] = p2.z;
+    r2.c[0] = (float)c2[0] / 255.f; r2.c[1] = (float)c2[1] / 255.f; r2.c[2] = (float)c2[2] / 255.f;
+    if (std::fabs(isolevel - d1) < 0.00001f) return r1;
+    if (std::fabs(isolevel - d2) < 0.00001f) return r2;
+    if (std::fabs(d1 - d2) < 0.00001f) return r1;
+    const float mu = (isolevel - d1) / (d2 - d1);
+    res.p[0] = p1.x + mu * (p2.x - p1.x);
+    res.p[1] = p1.y + mu * (p2.y - p1.y);
+    res.p[2] = p1.z + mu * (p2.z - p1.z);
+    res.c[0] = (float)(c1[0] + mu * (float)(c2[0] - c1[0])) / 255.f;
+    res.c[1] = (float)(c1[1] + mu * (float)(c2[1] - c1[1])) / 255.f;
+    res.c[2] = (float)(c1[2] + mu * (float)(c2[2] - c1[2])) / 255.f;
+    return res;
+}
+
+void extractIsoSurfaceAtPosition(const Scene& s, const BFMarchingCubesParams& prm, f3 worldPos, std::vector<BFMcTriangle>& out) {
+    if (prm.boxEnabled == 1) {  // isInBoxAA
+        if (worldPos.x < prm.minCorner[0] || worldPos.x > prm.maxCorner[0]) return;
+        if (worldPos.y < prm.minCorner[1] || worldPos.y > prm.maxCorner[1]) return;
+        if (worldPos.z < prm.minCorner[2] || worldPos.z > prm.maxCorner[2]) return;
+    }
+    const float isolevel = 0.0f;
+    const float P = s.hp.virtualVoxelSize / 2.0f;
+    const float M = -P;
+    uint8_t c[3];
+    const f3 p000 = worldPos + mk(M, M, M); float dist000; const bool valid000 = trilinear(s, p000, dist000, c);
+    const f3 p100 = worldPos + mk(P, M, M); float dist100; const bool valid100 = trilinear(s, p100, dist100, c);
+    const f3 p010 = worldPos + mk(M, P, M); float dist010; const bool valid010 = trilinear(s, p010, dist010, c);
+    const f3 p001 = worldPos + mk(M, M, P); float dist001; const bool valid001 = trilinear(s, p001, dist001, c);
+    const f3 p110 = worldPos + mk(P, P, M); float dist110; const bool valid110 = trilinear(s, p110, dist110, c);
+    const f3 p011 = worldPos + mk(M, P, P); float dist011; const bool valid011 = trilinear(s, p011, dist011, c);
+    const f3 p101 = worldPos + mk(P, M, P); float dist101; const bool valid101 = trilinear(s, p101, dist101, c);
+    const f3 p111 = worldPos + mk(P, P, P); float dist111; const bool valid111 = trilinear(s, p111, dist111, c);
+    if (!valid000 || !valid100 || !valid010 || !valid001 || !valid110 || !valid011 || !valid101 || !valid111) return;
+    uint32_t cubeindex = 0;
+    if (dist010 < isolevel) cubeindex += 1;
+    if (dist110 < isolevel) cubeindex += 2;
+    if (dist100 < isolevel) cubeindex += 4;
+    if (dist000 < isolevel) cubeindex += 8;
+    if (dist011 < isolevel) cubeindex += 16;
+    if (dist111 < isolevel) cubeindex += 32;
+    if (dist101 < isolevel) cubeindex += 64;
+    if (dist001 < isolevel) cubeindex += 128;
+    const float thres = prm.threshMarchingCubes;
+    const float distArray[] = {dist000, dist100, dist010, dist001, dist110, dist011, dist101, dist111};
+    for (int k = 0; k < 8; k++)
+        for (int l = 0; l < 8; l++) {
+            if (distArray[k] * distArray[l] < 0.0f) {
+                if (std::fabs(distArray[k]) + std::fabs(distArray[l]) > thres) return;
+            } else {
+                if (std::fabs(distArray[k] - distArray[l]) > thres) return;
+            }
+        }
+    for (int k = 0; k < 8; k++)
+        if (std::fabs(distArray[k]) > prm.threshMarchingCubes2) return;
+    const uint32_t et = kMc.edges[cubeindex];
+    if (et == 0 || et == 255) return;
+    const BFVoxel v = getVoxelWorld(s, worldPos);
+    BFMcVertex vertlist[12];
+    if (et & 1) vertlist[0] = vertexInterp(isolevel, p010, p110, dist010, dist110, v.color, v.color);
+    if (et & 2) vertlist[1] = vertexInterp(isolevel, p110, p100, dist110, dist100, v.color, v.color);
+    if (et & 4) vertlist[2] = vertexInterp(isolevel, p100, p000, dist100, dist000, v.color, v.color);
+    if (et & 8) vertlist[3] = vertexInterp(isolevel, p000, p010, dist000, dist010, v.color, v.color);
+    if (et & 16) vertlist[4] = vertexInterp(isolevel, p011, p111, dist011, dist111, v.color, v.color);
+    if (et & 32) vertlist[5] = vertexInterp(isolevel, p111, p101, dist111, dist101, v.color, v.color);
+    if (et & 64) vertlist[6] = vertexInterp(isolevel, p101, p001, dist101, dist001, v.color, v.color);
+    if (et & 128) vertlist[7] = vertexInterp(isolevel, p001, p011, dist001, dist011, v.color, v.color);
+    if (et & 256) vertlist[8] = vertexInterp(isolevel, p010, p011, dist010, dist011, v.color, v.color);
+    if (et & 512) vertlist[9] = vertexInterp(isolevel, p110, p111, dist110, dist111, v.color, v.color);
+    if (et & 1024) vertlist[10] = vertexInterp(isolevel, p100, p101, dist100, dist101, v.color, v.color);
+    if (et & 2048) vertlist[11] = vertexInterp(isolevel, p000, p001, dist000, dist001, v.color, v.color);
+    for (int i = 0; i < 3 * kMc.ntri[cubeindex]; i += 3) {
+        BFMcTriangle t;
+        t.v[0] = vertlist[kMc.tri[cubeindex][i + 0]];
+        t.v[1] = vertlist[kMc.tri[cubeindex][i + 1]];
+        t.v[2] = vertlist[kMc.tri[cubeindex][i + 2]];
+        out.push_back(t);
+    }
+}
+
+}  // namespace
+
+extern "C" void or_extract_mesh(const ORScene* o, const BFMarchingCubesParams* prm, BFMcTriangle* out, uint32_t cap,
+                                uint32_t* n, uint32_t* total) {
+    const Scene& s = o->s;
+    std::vector<std::pair<int, i3>> blocks;  // allocated hash entries, by heap pointer
+    for (const BFHashEntry& e : s.hash)
+        if (e.ptr != BF_FREE_ENTRY) blocks.push_back({e.ptr, i3{e.x, e.y, e.z}});
+    std::sort(blocks.begin(), blocks.end(), [](const std::pair<int, i3>& a, const std::pair<int, i3>& b) { return a.first < b.first; });
+    std::vector<BFMcTriangle> tris;
+    for (const auto& b : blocks)
+        for (int z = 0; z < BF_SDF_BLOCK_SIZE; z++)
+            for (int y = 0; y < BF_SDF_BLOCK_SIZE; y++)
+                for (int x = 0; x < BF_SDF_BLOCK_SIZE; x++) {
+                    // SDFBlockToVirtualVoxelPos(entry.pos) + threadIdx, virtualVoxelPosToWorld
+                    const i3 pi = {b.second.x * BF_SDF_BLOCK_SIZE + x, b.second.y * BF_SDF_BLOCK_SIZE + y, b.second.z * BF_SDF_BLOCK_SIZE + z};
+                    const f3 worldPos = mk((float)pi.x, (float)pi.y, (float)pi.z) * s.hp.virtualVoxelSize;
+                    extractIsoSurfaceAtPosition(s, *prm, worldPos, tris);
+                }
+    const uint32_t cnt = (uint32_t)std::min<size_t>(tris.size(), cap);
+    if (out && cnt) std::memcpy(out, tris.data(), sizeof(BFMcTriangle) * cnt);
+    if (n) *n = cnt;
+    if (total) *total = (uint32_t)tris.size();
+}
+
+extern "C" void or_mc_tables(uint16_t* edges, uint8_t* ntri, uint8_t* tri) {  // the compiled case tables
+    for (int c = 0; c < 256; c++) {
+        edges[c] = kMc.edges[c];
+        ntri[c] = kMc.ntri[c];
+        for (int k = 0; k < 15; k++) tri[c * 15 + k] = kMc.tri[c][k];
     }
 }

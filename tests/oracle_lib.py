@@ -53,12 +53,25 @@ def lib() -> C.CDLL:
         L.or_dense_integrate.restype = None
         L.or_raycast.argtypes = [C.c_void_p] * 10
         L.or_raycast.restype = None
+        L.or_extract_mesh.argtypes = [C.c_void_p] * 6
+        L.or_extract_mesh.restype = None
+        L.or_mc_tables.argtypes = [C.c_void_p] * 3
+        L.or_mc_tables.restype = None
         _lib = L
     return _lib
 
 
 def _m(T) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(T, np.float32).reshape(16))
+
+
+def mc_tables():
+    """The compiled marching-cubes case tables (mc_tables.h, shared by the kernel and the oracle)."""
+    edges = np.zeros(256, np.uint16)
+    ntri = np.zeros(256, np.uint8)
+    tri = np.zeros((256, 15), np.uint8)
+    lib().or_mc_tables(edges.ctypes.data, ntri.ctypes.data, tri.ctypes.data)
+    return edges, ntri, tri
 
 
 class OracleScene:
@@ -102,6 +115,14 @@ class OracleScene:
                          nrm.ctypes.data, col.ctypes.data, rmin.ctypes.data, rmax.ctypes.data)
         res = (depth, d4, nrm, col)
         return res + (rmin, rmax) if want_intervals else res
+
+    def extract_mesh(self, mc):
+        """extractIsoSurface restated (oracle/tsdf.cpp or_extract_mesh): float32 [n, 3, 6], total."""
+        cap = int(mc.maxNumTriangles)
+        out = np.empty((max(cap, 1), 3, 6), np.float32)
+        n, total = C.c_uint32(), C.c_uint32()
+        lib().or_extract_mesh(self.h, C.addressof(mc), out.ctypes.data, cap, C.addressof(n), C.addressof(total))
+        return out[: n.value].copy(), total.value
 
     def getHeapFreeCount(self) -> int:
         return lib().or_scene_heap_free_count(self.h)
