@@ -182,6 +182,12 @@ class BFPreprocessOptions(C.Structure):  # include/bf/types.h
                 ("sigmaR", C.c_float), ("depthShift", C.c_float)]
 
 
+class BFCacheOptions(C.Structure):  # include/bf/types.h
+    _fields_ = [("inputWidth", C.c_uint32), ("inputHeight", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("maxFrames", C.c_uint32), ("inputIntrinsics", C.c_float * 16), ("colorSigma", C.c_float),
+                ("depthSigmaD", C.c_float), ("depthSigmaR", C.c_float)]
+
+
 class BFVoxelOp(C.Structure):  # include/bf/bf.h
     _fields_ = [("T", C.c_float * 16), ("depth", C.c_void_p), ("color", C.c_void_p), ("deintegrate", C.c_uint32),
                 ("reserved", C.c_uint32)]

@@ -8,6 +8,7 @@
 #include "synth.h"
 #include "tsdf.h"
 #include "io.h"
+#include "cache.h"
 #include "frames.h"
 
 #include <cstring>
@@ -122,6 +123,10 @@ struct bf_sens_writer {
 };
 struct bf_params {
     ParamFile f;
+};
+struct bf_cache {
+    hipStream_t stream = nullptr;
+    Cache* c = nullptr;
 };
 struct bf_preproc {
     hipStream_t stream = nullptr;
@@ -807,6 +812,84 @@ int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]) {
 
 
 // ---- input formats and preprocessing ------------------------------------------------------------
+// ---- CUDACache ---------------------------------------------------------------------------------
+int bf_cache_create(const BFCacheOptions* o, bf_cache** out) {
+    BF_TRY
+    BF_REQUIRE(o && out, BF_ERR_ARG, "null argument");
+    *out = nullptr;
+    CacheConfig cfg{};
+    cfg.inputWidth = o->inputWidth; cfg.inputHeight = o->inputHeight;
+    cfg.width = o->width; cfg.height = o->height; cfg.maxFrames = o->maxFrames;
+    std::memcpy(cfg.inputIntrinsics, o->inputIntrinsics, 64);
+    cfg.colorSigma = o->colorSigma; cfg.depthSigmaD = o->depthSigmaD; cfg.depthSigmaR = o->depthSigmaR;
+    std::unique_ptr<bf_cache> h(new bf_cache);
+    BF_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    try {
+        h->c = new Cache(cfg, h->stream);
+    } catch (...) {
+        hipStreamDestroy(h->stream);
+        throw;
+    }
+    *out = h.release();
+    BF_CATCH
+}
+int bf_cache_destroy(bf_cache* c) {
+    BF_TRY
+    if (!c) return 0;
+    hipStreamSynchronize(c->stream);
+    delete c->c;
+    hipStreamDestroy(c->stream);
+    delete c;
+    BF_CATCH
+}
+int bf_cache_store_frame(bf_cache* c, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH,
+                         uint32_t* index) {
+    BF_TRY
+    BF_REQUIRE(c, BF_ERR_ARG, "null cache");
+    const uint32_t i = c->c->storeFrame(depth, color, colorW, colorH);
+    if (index) *index = i;
+    BF_CATCH
+}
+int bf_cache_copy_frame_from(bf_cache* dst, const bf_cache* src, uint32_t frame, uint32_t* index) {
+    BF_TRY
+    BF_REQUIRE(dst && src, BF_ERR_ARG, "null cache");
+    if (src->stream != dst->stream) BF_HIP(hipStreamSynchronize(src->stream));
+    const uint32_t i = dst->c->copyFrameFrom(*src->c, frame);
+    if (index) *index = i;
+    BF_CATCH
+}
+int bf_cache_increment(bf_cache* c) {
+    BF_TRY
+    BF_REQUIRE(c, BF_ERR_ARG, "null cache");
+    c->c->increment();
+    BF_CATCH
+}
+int bf_cache_num_frames(bf_cache* c, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(c && n, BF_ERR_ARG, "null argument");
+    *n = c->c->numFrames();
+    BF_CATCH
+}
+int bf_cache_frame(bf_cache* c, uint32_t index, BFCachedFrame* out) {
+    BF_TRY
+    BF_REQUIRE(c && out, BF_ERR_ARG, "null argument");
+    *out = c->c->frame(index);
+    BF_CATCH
+}
+int bf_cache_intrinsics(bf_cache* c, float K[16], float Kinv[16]) {
+    BF_TRY
+    BF_REQUIRE(c, BF_ERR_ARG, "null cache");
+    if (K) std::memcpy(K, c->c->intrinsics(), 64);
+    if (Kinv) std::memcpy(Kinv, c->c->intrinsicsInv(), 64);
+    BF_CATCH
+}
+int bf_cache_synchronize(bf_cache* c) {
+    BF_TRY
+    BF_REQUIRE(c, BF_ERR_ARG, "null cache");
+    BF_HIP(hipStreamSynchronize(c->stream));
+    BF_CATCH
+}
+
 int bf_mesh_merge(const BFMcTriangle* tris, uint32_t n, const float transform[16], float* vertices, float* colors,
                   uint32_t* faces, uint32_t* numVertices, uint32_t* numFaces) {
     BF_TRY

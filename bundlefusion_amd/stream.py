@@ -26,7 +26,7 @@ def _rodrigues(w):
 
 class SyntheticStream:
     def __init__(self, num_frames: int, width=640, height=480, submap=10, seed=0, drift=(0.05, 0.002),
-                 max_per_pair=25, outliers=0.02, cache_w=80, cache_h=60, log=None):
+                 max_per_pair=25, outliers=0.02, cache_w=80, cache_h=60, cache_source="frames", log=None):
         t0 = time.perf_counter()
         self.F, self.S = num_frames, submap
         self.log = log or (lambda *a: None)
@@ -62,17 +62,29 @@ class SyntheticStream:
             rel = np.linalg.inv(self.gt[i - 1].astype(np.float64)) @ self.gt[i].astype(np.float64)
             self.tinc[i] = (rel @ step).astype(np.float32)
 
-        # dense-term cache frames (80x60), one slab per field
+        # dense-term cache frames (80x60): "frames" builds them from the rendered frames with the
+        # reference's pipeline (CUDACache::storeFrame, called by Bundler::storeCachedFrame per input
+        # frame); "synth" renders them analytically at 80x60 (no filtering)
         t1 = time.perf_counter()
-        cf = synth_cache_frames(self.scene, self.gt, self.cache_cam)
-        self.cache_arrays = {k: DeviceArray.from_host(v) for k, v in cf.items()}
         self.cache = []
-        for i in range(num_frames):
-            c = BFCachedFrame()
-            for k, v in cf.items():
-                setattr(c, k, self.cache_arrays[k].ptr.value + i * v[0].nbytes)
-            self.cache.append(c)
-        self.log(f"cache frames in {time.perf_counter() - t1:.1f}s")
+        if cache_source == "frames":
+            from .cache import CUDACache, cache_options
+            self.cache_store = CUDACache(cache_options(width, height, f, f, self.cam.mx, self.cam.my, num_frames,
+                                                       width=cache_w, height=cache_h))
+            for i in range(num_frames):
+                self.cache_store.storeFrame(self.depth.ptr.value + 4 * P * i, self.color.ptr.value + 4 * P * i,
+                                            width, height)
+            self.cache_store.synchronize()
+            self.cache = [self.cache_store.frame(i) for i in range(num_frames)]
+        else:
+            cf = synth_cache_frames(self.scene, self.gt, self.cache_cam)
+            self.cache_arrays = {k: DeviceArray.from_host(v) for k, v in cf.items()}
+            for i in range(num_frames):
+                c = BFCachedFrame()
+                for k, v in cf.items():
+                    setattr(c, k, self.cache_arrays[k].ptr.value + i * v[0].nbytes)
+                self.cache.append(c)
+        self.log(f"cache frames ({cache_source}) in {time.perf_counter() - t1:.1f}s")
 
         # local correspondences per submap (frames base..base+S, local indices)
         t2 = time.perf_counter()

@@ -338,6 +338,30 @@ int bf_traj_frame_info(bf_traj* t, uint32_t idx, int32_t* type, float* dist);
 int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]);
 
 /* ---- input formats and preprocessing ------------------------------------ */
+/* ---- dense-term frame cache: CUDACache (Source/CUDACache.h/.cpp/.cu) ------------------------
+ * Per frame at width x height: depth, camera-space positions, float4 + uchar4 normals, intensity and
+ * its Sobel derivatives (the CUDACachedFrame the dense term reads). Device storage is owned by the
+ * cache; bf_cache_frame hands out a BFCachedFrame of device pointers for bf_solver_solve /
+ * bf_recon_set_frame. Work is queued on the cache's own stream. */
+typedef struct bf_cache bf_cache;
+int bf_cache_create(const BFCacheOptions* o, bf_cache** out);
+int bf_cache_destroy(bf_cache* c);
+/* storeFrame (CUDACache.cpp:45-94): device depth (inputWidth x inputHeight float metres, -inf invalid,
+ * the raw SIFT depth Bundler::storeCachedFrame passes) and colour (device uchar4, colorW x colorH);
+ * *index (may be NULL) = the frame slot written */
+int bf_cache_store_frame(bf_cache* c, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH,
+                         uint32_t* index);
+/* copyCacheFrameFrom (CUDACache.h:24-39): the next slot of dst = frame of src (same size);
+ * Bundler::fuseToGlobal's keyframe copy (Bundler.cpp:385-391) */
+int bf_cache_copy_frame_from(bf_cache* dst, const bf_cache* src, uint32_t frame, uint32_t* index);
+/* incrementCache (CUDACache.h:41-43): skip a slot (invalid keyframe) */
+int bf_cache_increment(bf_cache* c);
+int bf_cache_num_frames(bf_cache* c, uint32_t* n);
+int bf_cache_frame(bf_cache* c, uint32_t index, BFCachedFrame* out);
+/* m_intrinsics / m_intrinsicsInv: the input intrinsics scaled to the cache size (row-major) */
+int bf_cache_intrinsics(bf_cache* c, float K[16], float Kinv[16]);
+int bf_cache_synchronize(bf_cache* c);
+
 /* ---- mesh output: CUDAMarchingCubesHashSDF::saveMesh (CUDAMarchingCubesHashSDF.cpp:48-105) ------
  * Triangle soup (HOST BFMcTriangle[n], e.g. from bf_scene_extract_mesh) -> indexed mesh as saveMesh
  * builds it: mergeCloseVertices(1e-5, approx) (vertices snapped to a 1e-5 grid, first occurrence kept,

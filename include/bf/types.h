@@ -197,6 +197,18 @@ typedef struct BFMarchingCubesParams {
 typedef struct BFMcVertex { float p[3]; float c[3]; } BFMcVertex;
 typedef struct BFMcTriangle { BFMcVertex v[3]; } BFMcTriangle;
 
+/* CUDACache construction parameters (CUDACache::CUDACache, CUDACache.cpp:15-42, as Bundler.cpp:33-38
+ * creates it); zParametersBundlingDefault.txt values in brackets. A sigma <= 0 turns its filter off. */
+typedef struct BFCacheOptions {
+    uint32_t inputWidth, inputHeight;  /* depth input size (the SIFT depth size) */
+    uint32_t width, height;            /* s_downsampledWidth / s_downsampledHeight [80 x 60], <= 160 x 120 */
+    uint32_t maxFrames;                /* m_maxNumImages */
+    float inputIntrinsics[16];         /* row-major mat4f of the input depth camera */
+    float colorSigma;                  /* s_colorDownSigma [2.5] */
+    float depthSigmaD;                 /* s_depthDownSigmaD [1.0] */
+    float depthSigmaR;                 /* s_depthDownSigmaR [0.05] */
+} BFCacheOptions;
+
 #ifdef __cplusplus
 } /* extern "C" */
 

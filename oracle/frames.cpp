@@ -69,6 +69,24 @@ void resample(T* out, unsigned oW, unsigned oH, const T* in, unsigned iW, unsign
 }
 
 struct RGBX { uint8_t v[4]; };
+struct F4 { float x, y, z, w; };
+
+// ---- CUDACache::storeFrame (CUDACache.cpp:45-94), staged as the reference stages it ----------------
+void gaussIntensity(float* out, const float* in, float sigmaD, int W, int H) {  // CUDAImageUtil.cu:811-847
+    const int R = (int)std::ceil(2.0 * (double)sigmaD);
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float sum = 0.0f, sumWeight = 0.0f;
+            for (int m = x - R; m <= x + R; m++)
+                for (int n = y - R; n <= y + R; n++)
+                    if (m >= 0 && n >= 0 && m < W && n < H) {
+                        const float weight = expf(-((float)((m - x) * (m - x) + (n - y) * (n - y)) / (2.0f * sigmaD * sigmaD)));
+                        sumWeight += weight;
+                        sum += weight * in[n * W + m];
+                    }
+            if (sumWeight > 0.0f) out[y * W + x] = sum / sumWeight;
+        }
+}
 
 }  // namespace
 
@@ -95,4 +113,109 @@ extern "C" void or_preprocess(const BFPreprocessOptions* o, const uint16_t* dept
         if (cw == iw && ch == ih) std::memcpy(colorOut, rgbx, 4ull * cw * ch);
         else resample(reinterpret_cast<RGBX*>(colorOut), iw, ih, reinterpret_cast<const RGBX*>(rgbx), cw, ch);
     }
+}
+
+extern "C" void or_cache_store_frame(const BFCacheOptions* o, const float* depthIn, const uint8_t* color, uint32_t cw,
+                                     uint32_t ch, float* depthOut, float* camposOut, float* normalsOut, uint8_t* nu8Out,
+                                     float* intensityOut, float* derivOut, float Kout[16], float KinvOut[16]) {
+    const unsigned iW = o->inputWidth, iH = o->inputHeight, W = o->width, H = o->height;
+    const size_t n = (size_t)iW * iH;
+    // CUDACache::CUDACache: intrinsics scaled to the cache size; inverses (mat4f::getInverse)
+    float K[16], inKinv[16];
+    std::memcpy(K, o->inputIntrinsics, 64);
+    K[0] *= (float)W / (float)iW;
+    K[5] *= (float)H / (float)iH;
+    K[2] *= (float)(W - 1) / (float)(iW - 1);
+    K[6] *= (float)(H - 1) / (float)(iH - 1);
+    if (Kout) std::memcpy(Kout, K, 64);
+    if (KinvOut) or_matrix_inverse(K, KinvOut);
+    or_matrix_inverse(o->inputIntrinsics, inKinv);
+    // depth: gaussFilterDepthMap at the input size
+    std::vector<float> filt(n);
+    const float* d = depthIn;
+    if (o->depthSigmaD > 0.0f) {
+        gauss(filt.data(), depthIn, o->depthSigmaD, o->depthSigmaR, (int)iW, (int)iH);
+        d = filt.data();
+    }
+    // convertDepthFloatToCameraSpaceFloat4 (CUDAImageUtil.cu:367-384)
+    std::vector<F4> cam(n), nrm(n);
+    for (unsigned y = 0; y < iH; y++)
+        for (unsigned x = 0; x < iW; x++) {
+            F4& c = cam[y * iW + x];
+            c = {MINF, MINF, MINF, MINF};
+            const float dd = d[y * iW + x];
+            if (dd != MINF) {
+                const float* m = inKinv;
+                const float vx = (float)x * dd, vy = (float)y * dd, vz = dd, vw = dd;
+                const float cx = m[0] * vx + m[1] * vy + m[2] * vz + m[3] * vw;
+                const float cy = m[4] * vx + m[5] * vy + m[6] * vz + m[7] * vw;
+                const float cwv = m[12] * vx + m[13] * vy + m[14] * vz + m[15] * vw;
+                c = {cx, cy, cwv, 1.0f};
+            }
+        }
+    // computeNormals (CUDAImageUtil.cu:404-432)
+    for (unsigned y = 0; y < iH; y++)
+        for (unsigned x = 0; x < iW; x++) {
+            F4& out = nrm[y * iW + x];
+            out = {MINF, MINF, MINF, MINF};
+            if (x > 0 && x < iW - 1 && y > 0 && y < iH - 1) {
+                const F4 CC = cam[y * iW + x], PC = cam[(y + 1) * iW + x], CP = cam[y * iW + x + 1];
+                const F4 MC = cam[(y - 1) * iW + x], CM = cam[y * iW + x - 1];
+                if (CC.x != MINF && PC.x != MINF && CP.x != MINF && MC.x != MINF && CM.x != MINF) {
+                    const float ax = PC.x - MC.x, ay = PC.y - MC.y, az = PC.z - MC.z;
+                    const float bx = CP.x - CM.x, by = CP.y - CM.y, bz = CP.z - CM.z;
+                    const float nx = ay * bz - az * by, ny = az * bx - ax * bz, nz = ax * by - ay * bx;
+                    const float l = std::sqrt(nx * nx + ny * ny + nz * nz);
+                    if (l > 0.0f) out = {nx / -l, ny / -l, nz / -l, 0.0f};
+                }
+            }
+        }
+    // resampleFloat4 (campos, normals), convertNormalsFloat4ToUCHAR4, resampleFloat (depth)
+    resample(reinterpret_cast<F4*>(camposOut), W, H, cam.data(), iW, iH);
+    resample(reinterpret_cast<F4*>(normalsOut), W, H, nrm.data(), iW, iH);
+    for (size_t i = 0; i < (size_t)W * H; i++) {
+        const F4 p4 = reinterpret_cast<const F4*>(normalsOut)[i];
+        uint8_t* u = nu8Out + 4 * i;
+        u[0] = u[1] = u[2] = u[3] = 0;
+        if (p4.x != MINF) {
+            const float px = (p4.x + 1.0f) / 2.0f, py = (p4.y + 1.0f) / 2.0f, pz = (p4.z + 1.0f) / 2.0f;
+            u[0] = (uint8_t)std::round(px * 255); u[1] = (uint8_t)std::round(py * 255); u[2] = (uint8_t)std::round(pz * 255);
+        }
+    }
+    resample(depthOut, W, H, d, iW, iH);
+    // colour: resampleToIntensity (CUDAImageUtil.cu:224-241), gaussFilterIntensity, derivatives
+    std::vector<float> inten((size_t)W * H);
+    for (unsigned y = 0; y < H; y++)
+        for (unsigned x = 0; x < W; x++) {
+            const float sw = (float)(cw - 1) / (float)(W - 1), sh = (float)(ch - 1) / (float)(H - 1);
+            const unsigned xi = (unsigned)((float)x * sw + 0.5f), yi = (unsigned)((float)y * sh + 0.5f);
+            if (xi < cw && yi < ch) {
+                const uint8_t* c = color + 4 * ((size_t)yi * cw + xi);
+                inten[y * W + x] = (0.299f * c[0] + 0.587f * c[1] + 0.114f * c[2]) / 255.0f;
+            }
+        }
+    if (o->colorSigma > 0.0f) gaussIntensity(intensityOut, inten.data(), o->colorSigma, (int)W, (int)H);
+    else std::memcpy(intensityOut, inten.data(), 4 * inten.size());
+    const float* I = intensityOut;
+    for (unsigned y = 0; y < H; y++)
+        for (unsigned x = 0; x < W; x++) {  // computeIntensityDerivatives_Kernel (CUDAImageUtil.cu:260-296)
+            float* out = derivOut + 2 * ((size_t)y * W + x);
+            out[0] = out[1] = MINF;
+            if (x > 0 && x < W - 1 && y > 0 && y < H - 1) {
+                const float pos00 = I[(y - 1) * W + (x - 1)]; if (pos00 == MINF) continue;
+                const float pos01 = I[(y - 0) * W + (x - 1)]; if (pos01 == MINF) continue;
+                const float pos02 = I[(y + 1) * W + (x - 1)]; if (pos02 == MINF) continue;
+                const float pos10 = I[(y - 1) * W + (x - 0)]; if (pos10 == MINF) continue;
+                const float pos12 = I[(y + 1) * W + (x - 0)]; if (pos12 == MINF) continue;
+                const float pos20 = I[(y - 1) * W + (x + 1)]; if (pos20 == MINF) continue;
+                const float pos21 = I[(y - 0) * W + (x + 1)]; if (pos21 == MINF) continue;
+                const float pos22 = I[(y + 1) * W + (x + 1)]; if (pos22 == MINF) continue;
+                float resU = (-1.0f) * pos00 + (1.0f) * pos20 + (-2.0f) * pos01 + (2.0f) * pos21 + (-1.0f) * pos02 + (1.0f) * pos22;
+                resU /= 8.0f;
+                float resV = (-1.0f) * pos00 + (-2.0f) * pos10 + (-1.0f) * pos20 + (1.0f) * pos02 + (2.0f) * pos12 + (1.0f) * pos22;
+                resV /= 8.0f;
+                out[0] = resU;
+                out[1] = resV;
+            }
+        }
 }

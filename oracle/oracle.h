@@ -60,6 +60,12 @@ void or_extract_mesh(const ORScene* s, const BFMarchingCubesParams* p, BFMcTrian
 void or_pose_to_matrix(const float rot[3], const float trans[3], float M[16]);
 void or_matrix_to_pose(const float M[16], float rot[3], float trans[3]);
 void or_matrix_inverse(const float M[16], float out[16]);
+/* CUDACache::storeFrame (CUDACache.cpp:45-94) staged at the input resolution as the reference runs it:
+ * outputs at o->width x o->height (depth f32, campos / normals float4, normals uchar4, intensity f32,
+ * derivatives float2); K / Kinv = the cache intrinsics (may be NULL) */
+void or_cache_store_frame(const BFCacheOptions* o, const float* depth, const uint8_t* color, uint32_t cw, uint32_t ch,
+                          float* depthOut, float* camposOut, float* normalsOut, uint8_t* nu8Out, float* intensityOut,
+                          float* derivOut, float K[16], float Kinv[16]);
 
 /* ---- bundle adjustment (CUDASolverBundling::solve semantics) --------------- */
 typedef struct ORSolveParams {

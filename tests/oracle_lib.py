@@ -55,6 +55,8 @@ def lib() -> C.CDLL:
         L.or_raycast.restype = None
         L.or_extract_mesh.argtypes = [C.c_void_p] * 6
         L.or_extract_mesh.restype = None
+        L.or_cache_store_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32] + [C.c_void_p] * 8
+        L.or_cache_store_frame.restype = None
         L.or_mc_tables.argtypes = [C.c_void_p] * 3
         L.or_mc_tables.restype = None
         _lib = L
@@ -63,6 +65,23 @@ def lib() -> C.CDLL:
 
 def _m(T) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(T, np.float32).reshape(16))
+
+
+def cache_store_frame(opts, depth: np.ndarray, color: np.ndarray):
+    """CUDACache::storeFrame restated (oracle/frames.cpp or_cache_store_frame): dict like CUDACache.download,
+    plus the cache intrinsics K / Kinv."""
+    W, H = opts.width, opts.height
+    d = np.ascontiguousarray(depth, np.float32)
+    c = np.ascontiguousarray(color, np.uint8)
+    out = {"depth": np.empty((H, W), np.float32), "campos": np.empty((H, W, 4), np.float32),
+           "normals": np.empty((H, W, 4), np.float32), "normalsU8": np.empty((H, W, 4), np.uint8),
+           "intensity": np.empty((H, W), np.float32), "intensityDeriv": np.empty((H, W, 2), np.float32),
+           "K": np.empty(16, np.float32), "Kinv": np.empty(16, np.float32)}
+    lib().or_cache_store_frame(C.addressof(opts), d.ctypes.data, c.ctypes.data, c.shape[1], c.shape[0],
+                               *[out[k].ctypes.data for k in ("depth", "campos", "normals", "normalsU8", "intensity",
+                                                              "intensityDeriv", "K", "Kinv")])
+    out["K"], out["Kinv"] = out["K"].reshape(4, 4), out["Kinv"].reshape(4, 4)
+    return out
 
 
 def mc_tables():
