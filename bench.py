@@ -8,17 +8,22 @@ trajectory update that feeds the queue). W warmup submaps run untimed, then K su
 Every input (frames, cache frames, correspondences) is resident in HBM before timing starts.
 
 Multi-GPU (torchrun, one process per GPU): the TSDF is sharded by 1 m chunk ownership
-(every GPU sees every frame and integrates only the blocks it owns); the
-bundle adjustment is replicated on every rank (deterministic inputs, identical solves), so there
-is no data-path collective. The host-side barrier / max-over-ranks uses gloo.
+(every GPU sees every frame and integrates only the blocks it owns, no
+collective); local BA solves run round-robin by submap with an RCCL broadcast of the solved poses;
+the global solve shards its image-pair normal-equation blocks and all-reduces them over RCCL once
+per GN iteration (§8(e)3). The host-side barrier / max-over-ranks uses gloo.
 
 roofline: the dominant kernel is k_apply_ops, the op-batch voxel pass that applies a frame's
-re-integration fixes (up to 10 de-integrate + integrate pairs) with one read and one write per
-voxel; its launches are timed with dispatch-stamped HIP events on the scene stream inside the timed
-region; algorithmic bytes per launch = 20 B per work-list block (entry + op mask) + 24 B per voxel
-read + written + 8 B per pixel per op (depth + colour read once), from the device counters of the
-same launches. The kernel is VALU-issue bound (projection + band test of every voxel for every op
-of its block); roofline.valu reports that bound from the SQ_INSTS_VALU pass of the same command.
+re-integration fixes (up to 10 de-integrate + integrate pairs = 20 voxel ops) with one read and one
+write per voxel; its launches are timed with dispatch-stamped HIP events on the scene stream inside
+the timed region. achieved = SURVEY.md §8(d)'s per-op algorithmic bytes of the integrate kernel
+(8 B per pixel: depth + colour; 16 B per visible-list block; 24 B per voxel updated inside the
+truncation band) x the ops one launch applies, from the device counters of the same launches, /
+the average launch time. Because the batch reads and writes each voxel once for all its ops, the
+pass itself moves far fewer bytes (alg_bytes_pass_per_launch: 20 B per work-list block + 24 B per
+voxel read + written + 8 B per pixel per op) and the measured HBM traffic (PMC) sits between the
+two. The kernel is VALU-issue bound (projection + band test of every voxel for every op of its
+block); roofline.valu reports that bound from the SQ_INSTS_VALU pass of the same command.
 cpu_baseline: the CPU oracle (oracle/, serial C++ restatement) timed on a bounded sample of the
 same workload on this host, scaled by the GPU run's op counts to frames/s.
 """
@@ -226,12 +231,16 @@ def main():
     frames = S * args.steps
     P = args.width * args.height
     # dominant kernel: k_apply_ops, the op-batch voxel pass that applies a frame's re-integration
-    # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Algorithmic bytes per
-    # launch from the device counters of the same launches: 20 B per work-list block (16 B entry +
-    # 4 B op mask), 24 B per voxel read + written, 8 B per pixel per op (depth + colour read once).
+    # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Per launch, from the
+    # device counters of the same launches:
+    #   SURVEY §8(d) per-op bytes of the integrate kernel, summed over the launch's ops:
+    #     8 B per pixel per op + 16 B per visible-list block per op + 24 B per in-band voxel update
+    #   the fused pass's own bytes: 20 B per work-list block (16 B entry + 4 B op mask) + 24 B per
+    #     voxel read + written once + 8 B per pixel per op
     launches = max(1, st["reintegrateLaunches"])
     kernel_ms = st["reintegrateKernelMs"]
-    alg_bytes = 20 * ss["batchBlocks"] + 24 * ss["batchVoxelsRMW"] + 8 * P * ss["batchOps"]
+    alg_bytes = 8 * P * ss["batchOps"] + 16 * ss["batchBlocks"] * (ss["batchOps"] / launches) + 24 * ss["batchUpdates"]
+    pass_bytes = 20 * ss["batchBlocks"] + 24 * ss["batchVoxelsRMW"] + 8 * P * ss["batchOps"]
     per_launch_bytes = alg_bytes / launches
     per_launch_s = kernel_ms / 1e3 / launches
     achieved = per_launch_bytes / per_launch_s / 1e9
@@ -277,6 +286,9 @@ def main():
                      "traffic_source": traffic_src if traffic is not None else None,
                      "launches": launches, "avg_launch_us": per_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes,
+                     "alg_bytes_source": "SURVEY 8(d) per-op integrate bytes (8 P + 16 Nv + 24 V) x ops per launch",
+                     "alg_bytes_pass_per_launch": pass_bytes / launches,
+                     "achieved_pass": pass_bytes / launches / per_launch_s / 1e9,
                      "per_launch": {"work_list_blocks": ss["batchBlocks"] / launches,
                                     "voxels_rmw": ss["batchVoxelsRMW"] / launches,
                                     "voxel_op_updates": ss["batchUpdates"] / launches,
