@@ -193,7 +193,7 @@ class BFVoxelOp(C.Structure):  # include/bf/bf.h
                 ("reserved", C.c_uint32)]
 
 
-MAX_VOXEL_OPS = 20
+MAX_VOXEL_OPS = 24
 
 
 class BFFixOp(C.Structure):

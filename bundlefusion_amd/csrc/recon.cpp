@@ -39,6 +39,8 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     : opt_(o), cam_(cam) {
     opt_.submapSize = or_default(o.submapSize, 10u);
     if (const char* e = std::getenv("BF_BATCH_FIXES")) batchFixes_ = e[0] != '0';
+    if (const char* e = std::getenv("BF_DEFER_INTEGRATE")) deferIntegrate_ = e[0] != '0';
+    if (!batchFixes_) deferIntegrate_ = false;
     opt_.maxFrameFixes = or_default(o.maxFrameFixes, 10u);
     opt_.topNActive = or_default(o.topNActive, 30u);
     opt_.localNonLin = or_default(o.localNonLin, 2u);
@@ -212,6 +214,10 @@ void Recon::runReintegrate() {
     tm_->nextFixes(opt_.maxFrameFixes, ops_);
     std::vector<VoxelOp>& batch = batch_;
     batch.clear();
+    if (pendingInt_) {  // the previous frame's integration, in its place in the call sequence
+        batch.push_back(pendingOp_);
+        pendingInt_ = false;
+    }
     for (const FixOp& op : ops_) {
         const FrameRef& fr = frames_[op.frame];
         BF_REQUIRE(fr.set, BF_ERR_STATE, "re-integration of a frame that is not in the frame store");
@@ -263,7 +269,12 @@ void Recon::processFrame(uint32_t f) {
     runReintegrate();
     fr.Tlocal = (f % S == 0) ? identity() : mat4_mul(frames_[f - 1].Tlocal, fr.Tinc);
     const BFMat4 T = mat4_mul(kf_[s], fr.Tlocal);  // getCurrentIntegrationFrame
-    scene_->integrate(T, fr.depth, fr.color, cam_, false, nullptr);
+    if (deferIntegrate_) {
+        pendingOp_ = VoxelOp{T, fr.depth, fr.color, false};
+        pendingInt_ = true;
+    } else {
+        scene_->integrate(T, fr.depth, fr.color, cam_, false, nullptr);
+    }
     logOp(2, f, &T);
     st_.integrations++;
     tm_->addFrame(FrameType::Integrated, T, f);
@@ -274,6 +285,12 @@ void Recon::processFrame(uint32_t f) {
 void Recon::reintegrate() {
     applyPending(false);
     runReintegrate();
+}
+
+void Recon::flushIntegrate() {
+    if (!pendingInt_) return;
+    pendingInt_ = false;
+    scene_->integrate(pendingOp_.T, pendingOp_.depth, pendingOp_.color, cam_, false, nullptr);
 }
 
 void Recon::finish() {
@@ -450,6 +467,7 @@ void Recon::apply(Pending& P) {
 }
 
 void Recon::synchronize() {
+    flushIntegrate();
     BF_HIP(hipStreamSynchronize(sceneStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
     applyPending(true);

@@ -49,7 +49,10 @@ public:
     BFReconStats stats();
     void resetStats();
     void trajectory(BFMat4* out, uint32_t n) const;   // integrated transform per frame (-inf if none)
-    Scene& scene() { return *scene_; }
+    Scene& scene() {  // external access sees every frame integrated so far
+        flushIntegrate();
+        return *scene_;
+    }
     const BFDepthCameraParams& camera() const { return cam_; }
     const std::vector<BFFixOp>& opLog() const { return log_; }
 
@@ -105,6 +108,13 @@ private:
     std::vector<FixOp> ops_;
     std::vector<VoxelOp> batch_;
     bool batchFixes_ = true;  // BF_BATCH_FIXES=0: one scene pass per fix (A/B and debugging)
+    // The integration of frame f is the scene call right before frame f+1's fixes (nothing touches
+    // the scene in between), so it is deferred and runs as op 0 of that batch: one voxel pass less
+    // per frame, same call sequence. Any other scene access flushes it first. BF_DEFER_INTEGRATE=0: off.
+    bool deferIntegrate_ = true;
+    bool pendingInt_ = false;
+    VoxelOp pendingOp_{};
+    void flushIntegrate();
     uint32_t lastSubmapEnqueued_ = 0xFFFFFFFFu;
     uint32_t numFrames_ = 0;
 

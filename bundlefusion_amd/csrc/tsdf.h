@@ -59,7 +59,9 @@ struct VoxelOp {
 
 class Scene {
 public:
-    static constexpr uint32_t kMaxOps = 20;  // a frame's fixes: <= 10 re-integrations, 2 voxel ops each
+    // a frame's fixes (<= 10 re-integrations, 2 voxel ops each) + the deferred integration of the
+    // previous frame; <= 32 (op bit masks)
+    static constexpr uint32_t kMaxOps = 24;
     Scene(const SceneConfig& cfg, hipStream_t stream);
     ~Scene();
 

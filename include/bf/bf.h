@@ -79,7 +79,7 @@ int bf_scene_reintegrate(bf_scene* s, const float Told[16], const float Tnew[16]
  * values and the allocated block set equal those of the sequence of bf_scene_deintegrate /
  * bf_scene_integrate calls; the visible list afterwards is the last op's frustum list (what the
  * reference's garbageCollect after the loop walks). */
-#define BF_MAX_VOXEL_OPS 20
+#define BF_MAX_VOXEL_OPS 24
 typedef struct BFVoxelOp {
     float T[16];
     const float* depth;   /* device, W*H float */
