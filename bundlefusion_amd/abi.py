@@ -188,6 +188,12 @@ class BFCacheOptions(C.Structure):  # include/bf/types.h
                 ("depthSigmaD", C.c_float), ("depthSigmaR", C.c_float)]
 
 
+class BFCorrOptions(C.Structure):  # include/bf/types.h
+    _fields_ = [("intrinsics", C.c_float * 4), ("intrinsicsInv", C.c_float * 16), ("width", C.c_uint32),
+                ("height", C.c_uint32), ("stride", C.c_uint32), ("maxPerPair", C.c_uint32), ("minDepth", C.c_float),
+                ("maxDepth", C.c_float), ("depthThresh", C.c_float)]
+
+
 class BFVoxelOp(C.Structure):  # include/bf/bf.h
     _fields_ = [("T", C.c_float * 16), ("depth", C.c_void_p), ("color", C.c_void_p), ("deintegrate", C.c_uint32),
                 ("reserved", C.c_uint32)]

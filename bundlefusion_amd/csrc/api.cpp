@@ -812,6 +812,29 @@ int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]) {
 
 
 // ---- input formats and preprocessing ------------------------------------------------------------
+// ---- correspondences --------------------------------------------------------------------------------
+int bf_corr_save(const char* path, const BFEntryJ* corr, uint64_t n) {
+    BF_TRY
+    BF_REQUIRE(path, BF_ERR_ARG, "null path");
+    corr_save(path, corr, n);
+    BF_CATCH
+}
+int bf_corr_load(const char* path, BFEntryJ* corr, uint64_t cap, uint64_t* n) {
+    BF_TRY
+    BF_REQUIRE(path, BF_ERR_ARG, "null path");
+    const uint64_t c = corr_load(path, corr, cap);
+    if (n) *n = c;
+    BF_CATCH
+}
+int bf_corr_from_depth(const float* const* depth, const float* transforms, const float* transformsInv, uint32_t curFrame,
+                       uint32_t startFrame, const BFCorrOptions* o, BFEntryJ* out, uint32_t cap, uint32_t* n,
+                       uint32_t* total) {
+    BF_TRY
+    BF_REQUIRE(o && n, BF_ERR_ARG, "null argument");
+    *n = corr_from_depth(depth, transforms, transformsInv, curFrame, startFrame, *o, out, cap, total);
+    BF_CATCH
+}
+
 // ---- CUDACache ---------------------------------------------------------------------------------
 int bf_cache_create(const BFCacheOptions* o, bf_cache** out) {
     BF_TRY

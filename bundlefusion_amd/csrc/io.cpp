@@ -369,4 +369,30 @@ void mesh_save_ply(const std::string& path, const Mesh& m) {
     BF_REQUIRE(ok, BF_ERR_IO, "short write to " + path);
 }
 
+// ---- EntryJ dump (Bundler::saveSparseCorrsToFile, Bundler.cpp:396-409) ---------------------------
+void corr_save(const std::string& path, const BFEntryJ* corr, uint64_t n) {
+    BF_REQUIRE(corr != nullptr || n == 0, BF_ERR_ARG, "null correspondences");
+    FILE* f = std::fopen(path.c_str(), "wb");
+    BF_REQUIRE(f != nullptr, BF_ERR_IO, "cannot open " + path + " for writing");
+    bool ok = std::fwrite(&n, 8, 1, f) == 1;
+    if (n) ok = ok && std::fwrite(corr, sizeof(BFEntryJ), n, f) == n;
+    std::fclose(f);
+    BF_REQUIRE(ok, BF_ERR_IO, "short write to " + path);
+}
+
+uint64_t corr_load(const std::string& path, BFEntryJ* corr, uint64_t cap) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    BF_REQUIRE(f != nullptr, BF_ERR_IO, "cannot open " + path);
+    uint64_t n = 0;
+    bool ok = std::fread(&n, 8, 1, f) == 1;
+    const uint64_t m = std::min(n, cap);
+    if (ok && m) {
+        BF_REQUIRE(corr != nullptr, BF_ERR_ARG, "null output");
+        ok = std::fread(corr, sizeof(BFEntryJ), m, f) == m;
+    }
+    std::fclose(f);
+    BF_REQUIRE(ok, BF_ERR_IO, "truncated correspondence file " + path);
+    return n;
+}
+
 }  // namespace bf

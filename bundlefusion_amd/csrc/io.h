@@ -63,6 +63,13 @@ struct Mesh {
 Mesh mesh_from_triangles(const BFMcTriangle* tris, uint32_t n, const float* transform);
 void mesh_save_ply(const std::string& path, const Mesh& m);
 
+// Bundler::saveSparseCorrsToFile format: uint64 count + raw EntryJ records
+void corr_save(const std::string& path, const BFEntryJ* corr, uint64_t n);
+uint64_t corr_load(const std::string& path, BFEntryJ* corr, uint64_t cap);
+// EntryJ producer from depth + poses (corr.hip); device inputs / output, synchronizes
+uint32_t corr_from_depth(const float* const* depth, const float* T, const float* Tinv, uint32_t cur, uint32_t start,
+                         const BFCorrOptions& o, BFEntryJ* out, uint32_t cap, uint32_t* total);
+
 class ParamFile {
 public:
     void load(const std::string& path);  // later files override earlier keys

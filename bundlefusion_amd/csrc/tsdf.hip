@@ -19,6 +19,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -89,7 +90,7 @@ struct __attribute__((packed, aligned(4))) Vox3 {
 enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS,
                  S_BAND, S_RMW, S_BOPS, S_BBLOCKS, S_BRMW, S_BUPD, S_BEVAL };
 constexpr int DEPTH_TILE = 8;    // 8x8-pixel depth-bound tiles for the band cull
-constexpr int DEPTH_TILE2 = 32;  // coarse level: 32x32 pixels
+constexpr int DEPTH_TILE2 = 16;  // coarse level: 16x16 pixels
 constexpr int STAT_SLOTS = 64;
 constexpr int STAT_FIELDS = 32;  // counters per slot (BFTsdfStats uses the first sizeof/8)
 
@@ -201,10 +202,11 @@ __device__ __forceinline__ void depth_tile_wave(uint32_t t, const float* __restr
     } else {
         const uint32_t c = t - nFine;
         if (c >= tiles2W * tiles2H) return;
-        const uint32_t x = (c % tiles2W) * DEPTH_TILE2 + (lane & 31), y0 = (c / tiles2W) * DEPTH_TILE2 + (lane >> 5);
+        constexpr int ROWS = 64 / DEPTH_TILE2;  // pixel rows per pass of the wave
+        const uint32_t x = (c % tiles2W) * DEPTH_TILE2 + (lane % DEPTH_TILE2), y0 = (c / tiles2W) * DEPTH_TILE2 + (lane / DEPTH_TILE2);
 #pragma unroll
-        for (int i = 0; i < DEPTH_TILE2 / 2; i++) {
-            const uint32_t y = y0 + 2 * i;
+        for (int i = 0; i < DEPTH_TILE2 / ROWS; i++) {
+            const uint32_t y = y0 + ROWS * i;
             if (x < W && y < H) {
                 const float d = depthImg[y * W + x];
                 if (d != -INFINITY && d < maxDist) { lo = fminf(lo, d); hi = fmaxf(hi, d); }
@@ -240,10 +242,11 @@ __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned
 // Conservative test that a block may contain a voxel integrate will update: project the 8 voxel-
 // centre corners (convex hull -> bounding pixel rectangle, grown by one pixel), take the depth
 // bounds of the covered tiles and reject when every depth is too far behind or in front of the
-// block for |d - z| < truncation + truncScale * d to hold (1 cm slack for rounding). Exactness:
-// a rejected block has no voxel with an in-band sample, so skipping it changes no voxel. The
-// corner projections use rcp (1 ulp, far inside the one-pixel growth); footprints within 2x2 fine
-// tiles read those 4 tiles, wider ones up to 3x3 coarse (32-pixel) tiles, all loads independent.
+// block for |d - z| < truncation + truncScale * d to hold (1 mm slack for rounding, ~1000x the
+// float error). Exactness: a rejected block has no voxel with an in-band sample, so skipping it
+// changes no voxel. The corner projections use rcp (1 ulp, far inside the one-pixel growth);
+// footprints within 3x3 fine (8-pixel) tiles read those tiles, wider ones up to 3x3 coarse
+// (16-pixel) tiles, all loads independent.
 __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx, int by,
                                  int bz, const float2* __restrict__ tiles, const float2* __restrict__ tiles2) {
     const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
@@ -266,17 +269,19 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
     const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
     const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
     const int tx0 = x0 / DEPTH_TILE, tx1 = x1 / DEPTH_TILE, ty0 = y0 / DEPTH_TILE, ty1 = y1 / DEPTH_TILE;
-    float dlo, dhi;
-    if (tx1 - tx0 <= 1 && ty1 - ty0 <= 1) {
-        const float2 a = tiles[ty0 * A.tilesW + tx0], b = tiles[ty0 * A.tilesW + tx1];
-        const float2 c = tiles[ty1 * A.tilesW + tx0], d = tiles[ty1 * A.tilesW + tx1];
-        dlo = fminf(fminf(a.x, b.x), fminf(c.x, d.x));
-        dhi = fmaxf(fmaxf(a.y, b.y), fmaxf(c.y, d.y));
+    float dlo = INFINITY, dhi = -INFINITY;
+    if (tx1 - tx0 <= 2 && ty1 - ty0 <= 2) {  // footprint within 3x3 fine tiles (<= 17 px)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float2 t = tiles[min(ty0 + j, ty1) * A.tilesW + min(tx0 + i, tx1)];
+                dlo = fminf(dlo, t.x);
+                dhi = fmaxf(dhi, t.y);
+            }
     } else {
         const int cx0 = x0 / DEPTH_TILE2, cx1 = x1 / DEPTH_TILE2, cy0 = y0 / DEPTH_TILE2, cy1 = y1 / DEPTH_TILE2;
         if (cx1 - cx0 > 2 || cy1 - cy0 > 2) return true;  // very close block: keep
-        dlo = INFINITY;
-        dhi = -INFINITY;
 #pragma unroll
         for (int j = 0; j < 3; j++)
 #pragma unroll
@@ -287,7 +292,7 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
             }
     }
     if (!(dlo <= dhi)) return false;  // no integrable depth under the block
-    const float slack = 0.01f;
+    const float slack = 0.001f;  // >> the float error of zlo / zhi and of the kernel's band test
     if (dlo * (1.0f - A.truncScale) >= zhi + A.truncation + slack) return false;  // surface far behind
     if (dhi * (1.0f + A.truncScale) <= zlo - A.truncation - slack) return false;  // surface far in front
     return true;
@@ -1251,10 +1256,36 @@ __device__ __forceinline__ void apply_project(const HashArgs& A, const BFDepthCa
         cc[zi] = on ? colorImg[pix[zi]] : 0u;
     }
 }
+#ifdef BF_APPLY_DIAG
+// diagnostic build only (-DBF_APPLY_DIAG): where the voxel-op evaluations of the batch pass go
+__device__ unsigned long long g_diag[8];  // 0 off-screen, 1 invalid depth, 2 outside band, 3 updates, 4 wave-rounds, 5 dead wave-rounds
+#endif
 template <int ZC>
 __device__ __forceinline__ uint32_t apply_update(const HashArgs& A, bool deint, const float* d, const float* pz,
                                                  const uint32_t* cc, float* vs, float* vw, uint32_t* vc) {
     uint32_t in = 0;
+#ifdef BF_APPLY_DIAG
+    {
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        for (int zi = 0; zi < ZC; zi++) {
+            float sd;
+            const bool ib = voxel_in_band(A, d[zi], pz[zi], sd);
+            if (ib) c3++;
+            else if (d[zi] == -INFINITY && cc[zi] == 0u) c0++;
+            else if (d[zi] == -INFINITY || d[zi] >= A.maxIntegrationDistance) c1++;
+            else c2++;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            c0 += __shfl_xor(c0, off); c1 += __shfl_xor(c1, off); c2 += __shfl_xor(c2, off); c3 += __shfl_xor(c3, off);
+        }
+        if (lane_id() == 0) {
+            atomicAdd(&g_diag[0], (unsigned long long)c0); atomicAdd(&g_diag[1], (unsigned long long)c1);
+            atomicAdd(&g_diag[2], (unsigned long long)c2); atomicAdd(&g_diag[3], (unsigned long long)c3);
+            atomicAdd(&g_diag[4], 1ull);
+            if (c3 == 0) atomicAdd(&g_diag[5], 1ull);
+        }
+    }
+#endif
 #pragma unroll
     for (int zi = 0; zi < ZC; zi++) {
         float sd;
@@ -1845,6 +1876,14 @@ uint32_t Scene::errorFlags() {
 }
 
 BFTsdfStats Scene::stats() {
+#ifdef BF_APPLY_DIAG
+    {
+        unsigned long long d[8];
+        BF_HIP(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_diag), sizeof(d)));
+        fprintf(stderr, "APPLY_DIAG offscreen %llu invalid_depth %llu outside_band %llu updates %llu wave_rounds %llu dead_wave_rounds %llu\n",
+                d[0], d[1], d[2], d[3], d[4], d[5]);
+    }
+#endif
     std::vector<unsigned long long> h(STAT_SLOTS * STAT_FIELDS);
     BF_HIP(hipMemcpyAsync(h.data(), stats_.p, stats_.bytes(), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));

@@ -362,6 +362,24 @@ int bf_cache_frame(bf_cache* c, uint32_t index, BFCachedFrame* out);
 int bf_cache_intrinsics(bf_cache* c, float K[16], float Kinv[16]);
 int bf_cache_synchronize(bf_cache* c);
 
+/* ---- correspondences: EntryJ I/O and a producer from depth + poses ---------------------------
+ * Bundler::saveSparseCorrsToFile (Bundler.cpp:396-409): mLib BinaryDataStreamFile of a uint64 count
+ * followed by the raw 32-B EntryJ records (restated, unpinned). bf_corr_load reads min(cap, count)
+ * records into HOST memory, *n = count in the file. */
+int bf_corr_save(const char* path, const BFEntryJ* corr, uint64_t n);
+int bf_corr_load(const char* path, BFEntryJ* corr, uint64_t cap, uint64_t* n);
+/* The SiftGPU stand-in (feature matching is out of scope): for every image pair (i, curFrame),
+ * i in [startFrame, curFrame), grid pixels of frame i carried by the poses into frame curFrame whose
+ * depths agree become EntryJ {i, curFrame, pos_i, pos_j} with pos = intrinsicsInv * (d * (u, v, 1)), as
+ * AddCurrToResidualsCU (SIFTImageManager.cu:610-686) appends them; at most maxPerPair per pair, in a
+ * fixed order (pair, then a fixed permutation of the grid). depth: DEVICE array of device pointers
+ * (float, width x height, -inf invalid); transforms / transformsInv: DEVICE float4x4[...] camera ->
+ * world and its inverse. out: DEVICE EntryJ[cap]; *n = matches written (<= cap), *total (may be NULL)
+ * = matches found. Synchronizes. */
+int bf_corr_from_depth(const float* const* depth, const float* transforms, const float* transformsInv, uint32_t curFrame,
+                       uint32_t startFrame, const BFCorrOptions* o, BFEntryJ* out, uint32_t cap, uint32_t* n,
+                       uint32_t* total);
+
 /* ---- mesh output: CUDAMarchingCubesHashSDF::saveMesh (CUDAMarchingCubesHashSDF.cpp:48-105) ------
  * Triangle soup (HOST BFMcTriangle[n], e.g. from bf_scene_extract_mesh) -> indexed mesh as saveMesh
  * builds it: mergeCloseVertices(1e-5, approx) (vertices snapped to a 1e-5 grid, first occurrence kept,

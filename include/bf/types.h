@@ -209,6 +209,17 @@ typedef struct BFCacheOptions {
     float depthSigmaR;                 /* s_depthDownSigmaR [0.05] */
 } BFCacheOptions;
 
+/* EntryJ producer from depth maps + poses (bf_corr_from_depth, the SiftGPU stand-in). */
+typedef struct BFCorrOptions {
+    float intrinsics[4];       /* fx, fy, cx, cy of the depth maps (projection into frame cur) */
+    float intrinsicsInv[16];   /* row-major inverse intrinsics (AddCurrToResidualsCU's colorIntrinsicsInv) */
+    uint32_t width, height;    /* depth map size */
+    uint32_t stride;           /* sampling grid spacing in pixels */
+    uint32_t maxPerPair;       /* MAX_MATCHES_PER_IMAGE_PAIR_FILTERED [25], <= 64 */
+    float minDepth, maxDepth;  /* accepted depth range (metres) */
+    float depthThresh;         /* |depth_cur - z| agreement (metres) */
+} BFCorrOptions;
+
 #ifdef __cplusplus
 } /* extern "C" */
 

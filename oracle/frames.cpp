@@ -4,6 +4,7 @@
 // (Source/CUDAImageUtil.cu:701-739), gaussFilterDepthMap (:759-797), resampleFloat /
 // resampleUCHAR4 (:93-111, :160-177). The Gaussian weights are gaussD (:531-534) tabulated per
 // integer offset with the host expf, the same table the HIP build uses.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -218,4 +219,55 @@ extern "C" void or_cache_store_frame(const BFCacheOptions* o, const float* depth
                 out[1] = resV;
             }
         }
+}
+
+// ---- EntryJ producer from depth + poses (bundlefusion_amd/csrc/corr.hip's stand-in for the SiftGPU
+// front end; pos = intrinsicsInv * (d * (u, v, 1)) as AddCurrToResidualsCU, SIFTImageManager.cu:610-686)
+namespace {
+struct V3 { float x, y, z; };
+V3 xformP(const float* e, V3 v) {
+    return {e[0] * v.x + e[1] * v.y + e[2] * v.z + e[3] * 1.0f, e[4] * v.x + e[5] * v.y + e[6] * v.z + e[7] * 1.0f,
+            e[8] * v.x + e[9] * v.y + e[10] * v.z + e[11] * 1.0f};
+}
+int f2iC(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483648.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)v;
+}
+}  // namespace
+
+extern "C" void or_corr_from_depth(const float* const* depth, const float* T, const float* Tinv, uint32_t cur, uint32_t start,
+                                   const BFCorrOptions* o, BFEntryJ* out, uint32_t cap, uint32_t* n, uint32_t* total) {
+    const uint32_t W = o->width, H = o->height, gw = W / o->stride, gh = H / o->stride, N = gw * gh;
+    std::vector<BFEntryJ> all;
+    for (uint32_t i = start; i < cur; i++) {
+        uint32_t taken = 0;
+        for (uint32_t k = 0; k < N && taken < o->maxPerPair; k++) {
+            const uint32_t g = (uint32_t)(((uint64_t)k * 2654435761ull) % N);  // the fixed candidate permutation
+            const uint32_t u = (g % gw) * (W / gw) + (W / gw) / 2, v = (g / gw) * (H / gh) + (H / gh) / 2;
+            const float d = depth[i][v * W + u];
+            if (!(d != MINF && d >= o->minDepth && d <= o->maxDepth)) continue;
+            const V3 pi = xformP(o->intrinsicsInv, {d * (float)u, d * (float)v, d * 1.0f});
+            const V3 pj = xformP(Tinv + 16 * (size_t)cur, xformP(T + 16 * (size_t)i, pi));
+            if (!(pj.z > 0.0f)) continue;
+            const int uj = f2iC(pj.x * o->intrinsics[0] / pj.z + o->intrinsics[2] + 0.5f);
+            const int vj = f2iC(pj.y * o->intrinsics[1] / pj.z + o->intrinsics[3] + 0.5f);
+            if (uj < 0 || vj < 0 || uj >= (int)W || vj >= (int)H) continue;
+            const float d2 = depth[cur][vj * W + uj];
+            if (!(d2 != MINF && d2 >= o->minDepth && d2 <= o->maxDepth && std::fabs(d2 - pj.z) <= o->depthThresh)) continue;
+            const V3 q = xformP(o->intrinsicsInv, {d2 * (float)uj, d2 * (float)vj, d2 * 1.0f});
+            BFEntryJ e;
+            e.imgIdx_i = i;
+            e.imgIdx_j = cur;
+            e.pos_i = {pi.x, pi.y, pi.z};
+            e.pos_j = {q.x, q.y, q.z};
+            all.push_back(e);
+            taken++;
+        }
+    }
+    const uint32_t m = (uint32_t)std::min<size_t>(all.size(), cap);
+    if (m) std::memcpy(out, all.data(), sizeof(BFEntryJ) * m);
+    if (n) *n = m;
+    if (total) *total = (uint32_t)all.size();
 }

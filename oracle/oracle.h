@@ -60,6 +60,9 @@ void or_extract_mesh(const ORScene* s, const BFMarchingCubesParams* p, BFMcTrian
 void or_pose_to_matrix(const float rot[3], const float trans[3], float M[16]);
 void or_matrix_to_pose(const float M[16], float rot[3], float trans[3]);
 void or_matrix_inverse(const float M[16], float out[16]);
+/* EntryJ producer from depth + poses (see bundlefusion_amd/csrc/corr.hip): host arrays */
+void or_corr_from_depth(const float* const* depth, const float* T, const float* Tinv, uint32_t cur, uint32_t start,
+                        const BFCorrOptions* o, BFEntryJ* out, uint32_t cap, uint32_t* n, uint32_t* total);
 /* CUDACache::storeFrame (CUDACache.cpp:45-94) staged at the input resolution as the reference runs it:
  * outputs at o->width x o->height (depth f32, campos / normals float4, normals uchar4, intensity f32,
  * derivatives float2); K / Kinv = the cache intrinsics (may be NULL) */

@@ -57,6 +57,9 @@ def lib() -> C.CDLL:
         L.or_extract_mesh.restype = None
         L.or_cache_store_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32] + [C.c_void_p] * 8
         L.or_cache_store_frame.restype = None
+        L.or_corr_from_depth.argtypes = [C.c_void_p] * 3 + [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                                                             C.c_uint32, C.c_void_p, C.c_void_p]
+        L.or_corr_from_depth.restype = None
         L.or_mc_tables.argtypes = [C.c_void_p] * 3
         L.or_mc_tables.restype = None
         _lib = L
@@ -82,6 +85,20 @@ def cache_store_frame(opts, depth: np.ndarray, color: np.ndarray):
                                                               "intensityDeriv", "K", "Kinv")])
     out["K"], out["Kinv"] = out["K"].reshape(4, 4), out["Kinv"].reshape(4, 4)
     return out
+
+
+def corr_from_depth(depths, T: np.ndarray, Tinv: np.ndarray, cur: int, start: int, opts, cap: int):
+    """EntryJ producer restated (oracle/frames.cpp or_corr_from_depth); depths: list of host float arrays."""
+    from bundlefusion_amd.abi import ENTRYJ_DTYPE
+    ds = [np.ascontiguousarray(d, np.float32) for d in depths]
+    ptrs = (C.c_void_p * len(ds))(*[d.ctypes.data for d in ds])
+    T = np.ascontiguousarray(T, np.float32)
+    Ti = np.ascontiguousarray(Tinv, np.float32)
+    out = np.zeros(max(cap, 1), ENTRYJ_DTYPE)
+    n, total = C.c_uint32(), C.c_uint32()
+    lib().or_corr_from_depth(C.cast(ptrs, C.c_void_p), T.ctypes.data, Ti.ctypes.data, cur, start, C.addressof(opts),
+                             out.ctypes.data, cap, C.addressof(n), C.addressof(total))
+    return out[: n.value].copy(), total.value
 
 
 def mc_tables():
