@@ -7,14 +7,14 @@
 // Intensity and computeIntensityDerivatives. Every output pixel of the resampled images depends
 // only on the input pixel it samples and that pixel's 4-neighbourhood, so here:
 //
-//  * k_cache_geometry: one thread per CACHE pixel evaluates the bilateral depth filter at just the
+//  * k_cache_geometry: per CACHE pixel, five threads evaluate the bilateral depth filter at just the
 //    5 input pixels it needs (sample + 4 neighbours), their camera-space positions, the normal, and
-//    writes depth / campos / normals / uchar4 normals. 4 800 threads do the work of 5 x 307 200
-//    full-resolution evaluations, with the same float expressions in the same order, so the
-//    results are bit-identical to the staged pipeline (checked against the oracle, which stages).
-//  * k_cache_intensity: one workgroup per frame holds the 80x60 intensity image and its Gaussian
-//    in LDS (2 x 19 KB): resample + convertToIntensity, the Gaussian, the Sobel derivatives, one
-//    launch instead of three.
+//    writes depth / campos / normals / uchar4 normals: 5 x 4 800 filter windows (one per thread)
+//    instead of 307 200 full-resolution ones, with the same float expressions in the same order,
+//    so the results are bit-identical to the staged pipeline (checked against the oracle, which stages).
+//  * k_cache_intensity: per 16x16 tile, the resampled intensity (tile + radius + 1 halo) and its
+//    Gaussian (tile + 1 halo) are staged in LDS: resample + convertToIntensity, the Gaussian and
+//    the Sobel derivatives in one launch instead of three.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -29,9 +29,8 @@ namespace bf {
 
 namespace {
 
-constexpr int GEOM_WG = 256;
-constexpr int INT_WG = 1024;
-constexpr uint32_t MAX_CACHE_PIXELS = 160 * 120;  // the intensity pass keeps 2 images in LDS
+constexpr int GEOM_WG = 320;  // 5 waves: one per stencil point of 64 cache pixels
+constexpr uint32_t MAX_CACHE_PIXELS = 1u << 20;
 
 struct GeomArgs {
     const float* depth;
@@ -79,27 +78,37 @@ __device__ float4 campos_at(const GeomArgs& A, int x, int y, float depth) {
     return make_float4(cx, cy, cw, 1.0f);
 }
 
-__device__ __forceinline__ float4 campos_px(const GeomArgs& A, int x, int y) { return campos_at(A, x, y, filtered_at(A, x, y)); }
-
+// 64 cache pixels per workgroup; wave w evaluates the filtered depth at point w of each pixel's
+// stencil (the sample, then +y, +x, -y, -x), so each thread runs one 5x5 bilateral window; wave 0
+// then forms camera positions, the normal and the outputs from LDS.
 __global__ __launch_bounds__(GEOM_WG) void k_cache_geometry(GeomArgs A) {
-    const uint32_t p = blockIdx.x * GEOM_WG + threadIdx.x;
-    if (p >= A.oW * A.oH) return;
-    const uint32_t x = p % A.oW, y = p / A.oW;
+    __shared__ float sd[5][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t p = blockIdx.x * 64 + lane;
+    const bool on = p < A.oW * A.oH;
+    const uint32_t x = on ? p % A.oW : 0, y = on ? p / A.oW : 0;
     // resampleFloat4 / resampleFloat nearest sample (CUDAImageUtil.cu:113-150)
     const float scaleWidth = (float)(A.iW - 1) / (float)(A.oW - 1);
     const float scaleHeight = (float)(A.iH - 1) / (float)(A.oH - 1);
     const int xi = (int)(uint32_t)((float)x * scaleWidth + 0.5f), yi = (int)(uint32_t)((float)y * scaleHeight + 0.5f);
-    const float d = filtered_at(A, xi, yi);
+    const int dx[5] = {0, 0, 1, 0, -1}, dy[5] = {0, 1, 0, -1, 0};
+    const bool interior = xi > 0 && xi < (int)A.iW - 1 && yi > 0 && yi < (int)A.iH - 1;
+    float f = -INFINITY;
+    if (on && (w == 0 || interior)) f = filtered_at(A, xi + dx[w], yi + dy[w]);
+    sd[w][lane] = f;
+    __syncthreads();
+    if (w != 0 || !on) return;
+    const float d = sd[0][lane];
     const float4 CC = campos_at(A, xi, yi, d);
     A.outDepth[p] = d;
     A.outCampos[p] = CC;
     // computeNormals_Kernel (CUDAImageUtil.cu:404-432) at the sampled pixel
     float4 nrm = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    if (xi > 0 && xi < (int)A.iW - 1 && yi > 0 && yi < (int)A.iH - 1 && CC.x != -INFINITY) {
-        const float4 PC = campos_px(A, xi, yi + 1);
-        const float4 CP = campos_px(A, xi + 1, yi);
-        const float4 MC = campos_px(A, xi, yi - 1);
-        const float4 CM = campos_px(A, xi - 1, yi);
+    if (interior && CC.x != -INFINITY) {
+        const float4 PC = campos_at(A, xi, yi + 1, sd[1][lane]);
+        const float4 CP = campos_at(A, xi + 1, yi, sd[2][lane]);
+        const float4 MC = campos_at(A, xi, yi - 1, sd[3][lane]);
+        const float4 CM = campos_at(A, xi - 1, yi, sd[4][lane]);
         if (PC.x != -INFINITY && CP.x != -INFINITY && MC.x != -INFINITY && CM.x != -INFINITY) {
             const f3 n = cross3(mk3(PC.x, PC.y, PC.z) - mk3(MC.x, MC.y, MC.z), mk3(CP.x, CP.y, CP.z) - mk3(CM.x, CM.y, CM.z));
             const float l = length3(n);
@@ -125,64 +134,77 @@ struct IntArgs {
     float2* outDeriv;
 };
 
-__global__ __launch_bounds__(INT_WG) void k_cache_intensity(IntArgs A) {
-    extern __shared__ float lds[];
-    const uint32_t W = A.oW, H = A.oH, n = W * H;
-    float* I = lds;       // resampled intensity
-    float* G = lds + n;   // filtered
+// 16x16 cache pixels per workgroup: the resampled intensity of the tile + (R + 1) halo and the
+// Gaussian of the tile + 1 halo are staged in LDS, then the Sobel derivatives of the tile.
+constexpr int IT = 16;
+constexpr int IMAXR = 7;
+constexpr int IH1 = IT + 2 * (IMAXR + 1);  // staged intensity edge
+__global__ __launch_bounds__(256) void k_cache_intensity(IntArgs A) {
+    __shared__ float I[IH1 * IH1];
+    __shared__ float G[(IT + 2) * (IT + 2)];
+    const int W = (int)A.oW, H = (int)A.oH;
+    const int R = A.useGauss ? A.g.radius : 0;
+    const int h = R + 1, E = IT + 2 * h;  // staged edge for this radius
+    const int x0 = blockIdx.x * IT - h, y0 = blockIdx.y * IT - h;
     // resampleToIntensity_Kernel (CUDAImageUtil.cu:224-241) + convertToIntensity (:197-199)
     const float scaleWidth = (float)(A.cW - 1) / (float)(W - 1);
     const float scaleHeight = (float)(A.cH - 1) / (float)(H - 1);
-    for (uint32_t p = threadIdx.x; p < n; p += INT_WG) {
-        const uint32_t x = p % W, y = p / W;
-        const uint32_t xi = (uint32_t)((float)x * scaleWidth + 0.5f), yi = (uint32_t)((float)y * scaleHeight + 0.5f);
+    for (int k = threadIdx.x; k < E * E; k += 256) {
+        const int x = x0 + k % E, y = y0 + k / E;
         float v = 0.0f;
-        if (xi < A.cW && yi < A.cH) {
-            const uchar4 c = A.color[yi * A.cW + xi];
-            v = (0.299f * (float)c.x + 0.587f * (float)c.y + 0.114f * (float)c.z) / 255.0f;
+        if (x >= 0 && y >= 0 && x < W && y < H) {
+            const uint32_t xi = (uint32_t)((float)(uint32_t)x * scaleWidth + 0.5f), yi = (uint32_t)((float)(uint32_t)y * scaleHeight + 0.5f);
+            if (xi < A.cW && yi < A.cH) {
+                const uchar4 c = A.color[yi * A.cW + xi];
+                v = (0.299f * (float)c.x + 0.587f * (float)c.y + 0.114f * (float)c.z) / 255.0f;
+            }
         }
-        I[p] = v;
+        I[k] = v;
     }
     __syncthreads();
-    // gaussFilterIntensityDevice (CUDAImageUtil.cu:811-847); sigma <= 0: the unfiltered image
-    for (uint32_t p = threadIdx.x; p < n; p += INT_WG) {
-        const int x = (int)(p % W), y = (int)(p / W);
-        float out = I[p];
-        if (A.useGauss) {
-            const int R = A.g.radius;
-            float sum = 0.0f, sumWeight = 0.0f;
-            for (int m = x - R; m <= x + R; m++)
-                for (int q = y - R; q <= y + R; q++)
-                    if (m >= 0 && q >= 0 && m < (int)W && q < (int)H) {
-                        const float weight = A.g.w[(q - y + R) * (2 * R + 1) + (m - x + R)];
-                        sumWeight += weight;
-                        sum += weight * I[q * W + m];
-                    }
-            if (sumWeight > 0.0f) out = sum / sumWeight;
+    // gaussFilterIntensityDevice (CUDAImageUtil.cu:811-847) over the tile + 1 halo; sigma <= 0: unfiltered
+    for (int k = threadIdx.x; k < (IT + 2) * (IT + 2); k += 256) {
+        const int gx = blockIdx.x * IT - 1 + k % (IT + 2), gy = blockIdx.y * IT - 1 + k / (IT + 2);
+        float out = 0.0f;
+        if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
+            out = I[(gy - y0) * E + (gx - x0)];
+            if (A.useGauss) {
+                float sum = 0.0f, sumWeight = 0.0f;
+                for (int m = gx - R; m <= gx + R; m++)
+                    for (int q = gy - R; q <= gy + R; q++)
+                        if (m >= 0 && q >= 0 && m < W && q < H) {
+                            const float weight = A.g.w[(q - gy + R) * (2 * R + 1) + (m - gx + R)];
+                            sumWeight += weight;
+                            sum += weight * I[(q - y0) * E + (m - x0)];
+                        }
+                if (sumWeight > 0.0f) out = sum / sumWeight;
+            }
+            const int lx = gx - blockIdx.x * IT, ly = gy - blockIdx.y * IT;
+            if (lx >= 0 && ly >= 0 && lx < IT && ly < IT) A.outIntensity[gy * W + gx] = out;
         }
-        G[p] = out;
-        A.outIntensity[p] = out;
+        G[k] = out;
     }
     __syncthreads();
     // computeIntensityDerivatives_Kernel (CUDAImageUtil.cu:260-296)
-    for (uint32_t p = threadIdx.x; p < n; p += INT_WG) {
-        const uint32_t x = p % W, y = p / W;
-        float2 r = make_float2(-INFINITY, -INFINITY);
-        if (x > 0 && x < W - 1 && y > 0 && y < H - 1) {
-            const float pos00 = G[(y - 1) * W + (x - 1)], pos01 = G[y * W + (x - 1)], pos02 = G[(y + 1) * W + (x - 1)];
-            const float pos10 = G[(y - 1) * W + x], pos12 = G[(y + 1) * W + x];
-            const float pos20 = G[(y - 1) * W + (x + 1)], pos21 = G[y * W + (x + 1)], pos22 = G[(y + 1) * W + (x + 1)];
-            if (pos00 != -INFINITY && pos01 != -INFINITY && pos02 != -INFINITY && pos10 != -INFINITY && pos12 != -INFINITY &&
-                pos20 != -INFINITY && pos21 != -INFINITY && pos22 != -INFINITY) {
-                float resU = (-1.0f) * pos00 + (1.0f) * pos20 + (-2.0f) * pos01 + (2.0f) * pos21 + (-1.0f) * pos02 + (1.0f) * pos22;
-                resU /= 8.0f;
-                float resV = (-1.0f) * pos00 + (-2.0f) * pos10 + (-1.0f) * pos20 + (1.0f) * pos02 + (2.0f) * pos12 + (1.0f) * pos22;
-                resV /= 8.0f;
-                r = make_float2(resU, resV);
-            }
+    const int lx = threadIdx.x % IT, ly = threadIdx.x / IT;
+    const int x = blockIdx.x * IT + lx, y = blockIdx.y * IT + ly;
+    if (x >= W || y >= H) return;
+    auto g = [&](int xx, int yy) { return G[(yy - (int)blockIdx.y * IT + 1) * (IT + 2) + (xx - (int)blockIdx.x * IT + 1)]; };
+    float2 r = make_float2(-INFINITY, -INFINITY);
+    if (x > 0 && x < W - 1 && y > 0 && y < H - 1) {
+        const float pos00 = g(x - 1, y - 1), pos01 = g(x - 1, y), pos02 = g(x - 1, y + 1);
+        const float pos10 = g(x, y - 1), pos12 = g(x, y + 1);
+        const float pos20 = g(x + 1, y - 1), pos21 = g(x + 1, y), pos22 = g(x + 1, y + 1);
+        if (pos00 != -INFINITY && pos01 != -INFINITY && pos02 != -INFINITY && pos10 != -INFINITY && pos12 != -INFINITY &&
+            pos20 != -INFINITY && pos21 != -INFINITY && pos22 != -INFINITY) {
+            float resU = (-1.0f) * pos00 + (1.0f) * pos20 + (-2.0f) * pos01 + (2.0f) * pos21 + (-1.0f) * pos02 + (1.0f) * pos22;
+            resU /= 8.0f;
+            float resV = (-1.0f) * pos00 + (-2.0f) * pos10 + (-1.0f) * pos20 + (1.0f) * pos02 + (2.0f) * pos12 + (1.0f) * pos22;
+            resV /= 8.0f;
+            r = make_float2(resU, resV);
         }
-        A.outDeriv[p] = r;
     }
+    A.outDeriv[y * W + x] = r;
 }
 
 }  // namespace
@@ -192,7 +214,7 @@ BFMat4 mat4_inverse(const BFMat4& m);  // api.cpp
 Cache::Cache(const CacheConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
     BF_REQUIRE(cfg.inputWidth >= 2 && cfg.inputHeight >= 2 && cfg.width >= 2 && cfg.height >= 2, BF_ERR_ARG,
                "cache and input sizes must be >= 2");
-    BF_REQUIRE((size_t)cfg.width * cfg.height <= MAX_CACHE_PIXELS, BF_ERR_ARG, "cache size above 160x120");
+    BF_REQUIRE((size_t)cfg.width * cfg.height <= MAX_CACHE_PIXELS, BF_ERR_ARG, "cache size above 2^20 pixels");
     BF_REQUIRE(cfg.maxFrames > 0, BF_ERR_ARG, "maxFrames");
     hw_ = (size_t)cfg.width * cfg.height;
     // CUDACache::CUDACache (CUDACache.cpp:15-42): intrinsics scaled to the cache size
@@ -233,7 +255,7 @@ uint32_t Cache::storeFrame(const float* depth, const uint8_t* color, uint32_t co
     g.useGauss = cfg_.depthSigmaD > 0.0f;
     g.g = depthGauss_;
     g.outDepth = depth_.p + o; g.outCampos = campos_.p + o; g.outNormals = normals_.p + o; g.outNU8 = normalsU8_.p + o;
-    k_cache_geometry<<<div_up((uint32_t)hw_, GEOM_WG), GEOM_WG, 0, stream_>>>(g);
+    k_cache_geometry<<<div_up((uint32_t)hw_, 64u), GEOM_WG, 0, stream_>>>(g);
     BF_LAUNCH_CHECK();
     IntArgs ia{};
     ia.color = reinterpret_cast<const uchar4*>(color);
@@ -242,7 +264,7 @@ uint32_t Cache::storeFrame(const float* depth, const uint8_t* color, uint32_t co
     ia.g = colorGauss_;
     ia.outIntensity = intensity_.p + o;
     ia.outDeriv = deriv_.p + o;
-    k_cache_intensity<<<1, INT_WG, 2 * hw_ * sizeof(float), stream_>>>(ia);
+    k_cache_intensity<<<dim3(div_up(cfg_.width, (uint32_t)IT), div_up(cfg_.height, (uint32_t)IT)), 256, 0, stream_>>>(ia);
     BF_LAUNCH_CHECK();
     cur_++;
     return f;

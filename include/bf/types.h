@@ -201,7 +201,7 @@ typedef struct BFMcTriangle { BFMcVertex v[3]; } BFMcTriangle;
  * creates it); zParametersBundlingDefault.txt values in brackets. A sigma <= 0 turns its filter off. */
 typedef struct BFCacheOptions {
     uint32_t inputWidth, inputHeight;  /* depth input size (the SIFT depth size) */
-    uint32_t width, height;            /* s_downsampledWidth / s_downsampledHeight [80 x 60], <= 160 x 120 */
+    uint32_t width, height;            /* s_downsampledWidth / s_downsampledHeight [80 x 60] */
     uint32_t maxFrames;                /* m_maxNumImages */
     float inputIntrinsics[16];         /* row-major mat4f of the input depth camera */
     float colorSigma;                  /* s_colorDownSigma [2.5] */
