@@ -68,6 +68,8 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
         sc.shardChunk = so->shardChunk;
     }
     scene_.reset(new Scene(sc, sceneStream_));
+    tileStride_ = Scene::tileCount(cam_);
+    if (batchFixes_ && tileStride_ * opt_.maxFrames * sizeof(float2) <= (4ull << 30)) frameTiles_.alloc(tileStride_ * opt_.maxFrames);
     local_.reset(new Solver(make_solver_config(S + 1, opt_.maxLocalCorr, &opt_.solver), baStream_));
     global_.reset(new Solver(make_solver_config(opt_.maxKeyframes, opt_.maxGlobalCorr, &opt_.solver), baStream_));
     tm_.reset(new TrajectoryManager(opt_.maxFrames, opt_.topNActive, opt_.minPoseDistSqrt));
@@ -145,6 +147,18 @@ void Recon::setFrame(uint32_t f, const float* depth, const uint8_t* color, const
     r.cache = cache ? *cache : BFCachedFrame{};
     r.Tinc = Tinc;
     r.set = true;
+    r.tilesReady = false;
+}
+
+VoxelOp Recon::frameOp(uint32_t f, const BFMat4& T, bool deint) {
+    FrameRef& fr = frames_[f];
+    VoxelOp op{T, fr.depth, fr.color, deint};
+    if (frameTiles_.p) {
+        op.tiles = frameTiles_.p + tileStride_ * f;
+        op.tilesReady = fr.tilesReady;
+        fr.tilesReady = true;  // this batch computes them (before any op of a later batch reads them)
+    }
+    return op;
 }
 
 void Recon::setLocalCorrespondences(uint32_t submap, BFEntryJ* corr, uint32_t n) {
@@ -223,8 +237,8 @@ void Recon::runReintegrate() {
         BF_REQUIRE(fr.set, BF_ERR_STATE, "re-integration of a frame that is not in the frame store");
         if (op.kind == FixKind::ReIntegrate) {  // deIntegrate(old) + integrate(new)
             if (batchFixes_) {
-                batch.push_back(VoxelOp{op.oldT, fr.depth, fr.color, true});
-                batch.push_back(VoxelOp{op.newT, fr.depth, fr.color, false});
+                batch.push_back(frameOp(op.frame, op.oldT, true));
+                batch.push_back(frameOp(op.frame, op.newT, false));
             } else {
                 scene_->reintegrate(op.oldT, op.newT, fr.depth, fr.color, cam_);
             }
@@ -233,12 +247,12 @@ void Recon::runReintegrate() {
             st_.deintegrations++;
             st_.integrations++;
         } else if (op.kind == FixKind::DeIntegrate) {
-            if (batchFixes_) batch.push_back(VoxelOp{op.oldT, fr.depth, fr.color, true});
+            if (batchFixes_) batch.push_back(frameOp(op.frame, op.oldT, true));
             else scene_->integrate(op.oldT, fr.depth, fr.color, cam_, true, nullptr);
             logOp(1, op.frame, &op.oldT);
             st_.deintegrations++;
         } else if (op.kind == FixKind::Integrate) {
-            if (batchFixes_) batch.push_back(VoxelOp{op.newT, fr.depth, fr.color, false});
+            if (batchFixes_) batch.push_back(frameOp(op.frame, op.newT, false));
             else scene_->integrate(op.newT, fr.depth, fr.color, cam_, false, nullptr);
             logOp(2, op.frame, &op.newT);
             st_.integrations++;
@@ -270,7 +284,7 @@ void Recon::processFrame(uint32_t f) {
     fr.Tlocal = (f % S == 0) ? identity() : mat4_mul(frames_[f - 1].Tlocal, fr.Tinc);
     const BFMat4 T = mat4_mul(kf_[s], fr.Tlocal);  // getCurrentIntegrationFrame
     if (deferIntegrate_) {
-        pendingOp_ = VoxelOp{T, fr.depth, fr.color, false};
+        pendingOp_ = frameOp(f, T, false);
         pendingInt_ = true;
     } else {
         scene_->integrate(T, fr.depth, fr.color, cam_, false, nullptr);
@@ -290,7 +304,7 @@ void Recon::reintegrate() {
 void Recon::flushIntegrate() {
     if (!pendingInt_) return;
     pendingInt_ = false;
-    scene_->integrate(pendingOp_.T, pendingOp_.depth, pendingOp_.color, cam_, false, nullptr);
+    scene_->applyOps(&pendingOp_, 1, cam_);  // = integrate(); also fills the frame's tile cache
 }
 
 void Recon::finish() {

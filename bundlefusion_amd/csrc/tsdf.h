@@ -55,6 +55,10 @@ struct VoxelOp {
     const float* depth;
     const uint8_t* color;
     bool deint;
+    // optional per-depth-map cache of the band-cull depth tiles (Scene::tileCount(cam) float2: fine
+    // level, then coarse); computed by the batch unless tilesReady (tiles depend on the depth only)
+    float2* tiles = nullptr;
+    bool tilesReady = false;
 };
 
 class Scene {
@@ -80,6 +84,7 @@ public:
     // values equal the sequential calls; `visible` is the frustum list of the last op, as the
     // reference's garbageCollect after the loop sees it.
     void applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& cam);
+    static size_t tileCount(const BFDepthCameraParams& cam);  // float2 per depth map of a VoxelOp tile cache
     KernelClock& applyClock() { return applyClock_; }  // k_apply_ops launches
     void garbageCollect();
     void compactify(const BFMat4& T, const BFDepthCameraParams& cam);

@@ -67,7 +67,9 @@ struct OpTable {
     const float* depth[Scene::kMaxOps];
     const uint32_t* color[Scene::kMaxOps];
     uint8_t intIdx[Scene::kMaxOps];  // op index of the i-th integrate op
-    uint32_t n, deintMask, nInt, tileStride, tile2Stride;
+    float2* tiles[Scene::kMaxOps];   // per op: 8x8-pixel depth bounds of its depth map ...
+    float2* tiles2[Scene::kMaxOps];  // ... and the 16x16 level
+    uint32_t n, deintMask, nInt, tileMask;  // tileMask: ops whose tiles this batch computes
 };
 __host__ __device__ __forceinline__ BFMat4 op_mat(const float* m) {
     BFMat4 r;
@@ -1041,9 +1043,10 @@ __global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __
 
 // ---- op batches (Scene::applyOps) ---------------------------------------------------------------
 // per-op 8x8-tile depth bounds (blockIdx.y = op) + the per-batch counter reset
+// (ops whose depth map already has its tiles, e.g. a frame-store frame re-integrated before, skip)
 __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigned long long* stats, OpTable ops, uint32_t W,
                                                          uint32_t H, uint32_t tilesW, uint32_t tilesH, uint32_t tiles2W,
-                                                         uint32_t tiles2H, float maxDist, float2* tiles, float2* tiles2) {
+                                                         uint32_t tiles2H, float maxDist) {
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
         ctrl[C_BAND] = 0;
@@ -1052,8 +1055,9 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
         stats[S_OPS] += ops.n;
         stats[S_BOPS] += ops.n;
     }
+    if (!((ops.tileMask >> blockIdx.y) & 1u)) return;
     depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[blockIdx.y], W, H, tilesW, tilesH, tiles2W, tiles2H,
-                    maxDist, tiles + (size_t)blockIdx.y * ops.tileStride, tiles2 + (size_t)blockIdx.y * ops.tile2Stride);
+                    maxDist, ops.tiles[blockIdx.y], ops.tiles2[blockIdx.y]);
 }
 
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
@@ -1088,8 +1092,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             for (uint32_t k = first; k < ops.n; k++) {
                 const BFMat4 Ti = op_mat(ops.tinv[k]);
                 if (block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
-                    block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, A.tiles + (size_t)k * ops.tileStride,
-                                     A.tiles2 + (size_t)k * ops.tile2Stride))
+                    block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, ops.tiles[k], ops.tiles2[k]))
                     mask |= 1u << k;
             }
         }
@@ -1787,11 +1790,19 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
     const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
     ensureTiles(tw * th * kMaxOps, tw2 * th2 * kMaxOps);
-    tab.tileStride = tw * th;
-    tab.tile2Stride = tw2 * th2;
+    for (uint32_t k = 0; k < n; k++) {
+        if (ops[k].tiles) {  // the caller's per-depth-map tile cache (fine level, then the coarse level)
+            tab.tiles[k] = ops[k].tiles;
+            tab.tiles2[k] = ops[k].tiles + (size_t)tw * th;
+            if (!ops[k].tilesReady) tab.tileMask |= 1u << k;
+        } else {
+            tab.tiles[k] = tiles_.p + (size_t)k * tw * th;
+            tab.tiles2[k] = tiles2_.p + (size_t)k * tw2 * th2;
+            tab.tileMask |= 1u << k;
+        }
+    }
     k_begin_ops_tiles<<<dim3(div_up((size_t)(tw * th + tw2 * th2) * 64, 256), n), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tiles_.p,
-        tiles2_.p);
+        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance);
     BF_LAUNCH_CHECK();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
     if (++batchEpoch_ >= (1u << 24)) {  // birth stamps are epoch << 8: restart the epochs before they wrap
@@ -1852,6 +1863,11 @@ void Scene::garbageCollect() {
     BF_LAUNCH_CHECK();
     k_gc_free_list<<<1, 64, 0, stream_>>>(A, gcList_.p);
     BF_LAUNCH_CHECK();
+}
+
+size_t Scene::tileCount(const BFDepthCameraParams& cam) {
+    return (size_t)div_up(cam.imageWidth, DEPTH_TILE) * div_up(cam.imageHeight, DEPTH_TILE) +
+           (size_t)div_up(cam.imageWidth, DEPTH_TILE2) * div_up(cam.imageHeight, DEPTH_TILE2);
 }
 
 uint32_t Scene::heapFreeCount() {
