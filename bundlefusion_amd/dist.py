@@ -107,9 +107,9 @@ def chunk_owner(bx: int, by: int, bz: int, voxel_size: float, shard_count: int, 
         s = np.float32(np.sign(q)) * np.float32(0.5)
         c.append(int(np.trunc(np.float32(q + s))))
     x, y, z = c
-    a = np.int32(np.uint32(x & 0xFFFFFFFF) * np.uint32(73856093) & 0xFFFFFFFF)
-    b = np.int32(np.uint32(y & 0xFFFFFFFF) * np.uint32(19349669) & 0xFFFFFFFF)
-    d = np.int32(np.uint32(z & 0xFFFFFFFF) * np.uint32(83492791) & 0xFFFFFFFF)
-    h = int(np.int32(a ^ b ^ d))
-    r = int(np.fmod(h, shard_count))
+    # int32 products with wrap-around, done on Python ints (no numpy overflow warnings)
+    h = ((x * 73856093) ^ (y * 19349669) ^ (z * 83492791)) & 0xFFFFFFFF
+    h = h - (1 << 32) if h >= (1 << 31) else h
+    r = abs(h) % shard_count          # C's fmod/% truncates toward zero
+    r = -r if h < 0 else r
     return r + shard_count if r < 0 else r
