@@ -69,7 +69,14 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     }
     scene_.reset(new Scene(sc, sceneStream_));
     tileStride_ = Scene::tileCount(cam_);
-    if (batchFixes_ && tileStride_ * opt_.maxFrames * sizeof(float2) <= (4ull << 30)) frameTiles_.alloc(tileStride_ * opt_.maxFrames);
+    framePixels_ = (size_t)cam_.imageWidth * cam_.imageHeight;
+    // the cache costs 8 B per pixel per frame (12.3 GB for 5 000 VGA frames, next to the frame store
+    // itself); beyond 32 GB each batch rebuilds its ops' images in the scene's scratch instead
+    if (batchFixes_ && tileStride_ * opt_.maxFrames * sizeof(float2) <= (4ull << 30) &&
+        framePixels_ * opt_.maxFrames * sizeof(uint2) <= (32ull << 30)) {
+        frameTiles_.alloc(tileStride_ * opt_.maxFrames);
+        frameDC_.alloc(framePixels_ * opt_.maxFrames);
+    }
     local_.reset(new Solver(make_solver_config(S + 1, opt_.maxLocalCorr, &opt_.solver), baStream_));
     global_.reset(new Solver(make_solver_config(opt_.maxKeyframes, opt_.maxGlobalCorr, &opt_.solver), baStream_));
     tm_.reset(new TrajectoryManager(opt_.maxFrames, opt_.topNActive, opt_.minPoseDistSqrt));
@@ -155,6 +162,7 @@ VoxelOp Recon::frameOp(uint32_t f, const BFMat4& T, bool deint) {
     VoxelOp op{T, fr.depth, fr.color, deint};
     if (frameTiles_.p) {
         op.tiles = frameTiles_.p + tileStride_ * f;
+        op.dc = frameDC_.p + framePixels_ * f;
         op.tilesReady = fr.tilesReady;
         fr.tilesReady = true;  // this batch computes them (before any op of a later batch reads them)
     }

@@ -88,12 +88,15 @@ private:
         BFMat4 Tinc{};    // front-end estimate: camera f in camera f-1 coordinates
         BFMat4 Tlocal{};  // chained estimate relative to the submap's first frame
         bool set = false;
-        bool tilesReady = false;  // its band-cull depth tiles are in frameTiles_
+        bool tilesReady = false;  // its band-cull depth tiles and dc image are in frameTiles_ / frameDC_
     };
-    // per-frame band-cull depth tiles (Scene::tileCount each): computed the first time a frame's
-    // depth enters an op batch, reused by every later (re-)integration of that frame
+    // per-frame band-cull depth tiles (Scene::tileCount each) and interleaved {depth, colour} image
+    // (W*H uint2): computed the first time a frame enters an op batch, reused by every later
+    // (re-)integration of that frame
     DevBuf<float2> frameTiles_;
     size_t tileStride_ = 0;
+    DevBuf<uint2> frameDC_;
+    size_t framePixels_ = 0;
     VoxelOp frameOp(uint32_t f, const BFMat4& T, bool deint);
     std::vector<FrameRef> frames_;
     std::vector<std::pair<BFEntryJ*, uint32_t>> localCorr_;

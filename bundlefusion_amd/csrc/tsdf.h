@@ -56,8 +56,10 @@ struct VoxelOp {
     const uint8_t* color;
     bool deint;
     // optional per-depth-map cache of the band-cull depth tiles (Scene::tileCount(cam) float2: fine
-    // level, then coarse); computed by the batch unless tilesReady (tiles depend on the depth only)
+    // level, then coarse) and of the interleaved {depth bits, colour} image (W*H uint2, the voxel
+    // pass's gather source); both computed by the batch unless tilesReady (they depend on the frame only)
     float2* tiles = nullptr;
+    uint2* dc = nullptr;
     bool tilesReady = false;
 };
 
@@ -144,6 +146,8 @@ private:
     DevBuf<float2> tiles2_;  // 32x32-pixel depth bounds
     size_t tiles2Cap_ = 0;
     void ensureTiles(size_t fine, size_t coarse);
+    DevBuf<uint2> dc_;  // per-op {depth, colour} images of ops without a caller cache
+    size_t dcCap_ = 0;
     DevBuf<uint32_t> ctrl_;
     DevBuf<unsigned long long> stats_;  // [64 slots][16]
     DevBuf<unsigned long long> cand_;

@@ -69,7 +69,8 @@ struct OpTable {
     uint8_t intIdx[Scene::kMaxOps];  // op index of the i-th integrate op
     float2* tiles[Scene::kMaxOps];   // per op: 8x8-pixel depth bounds of its depth map ...
     float2* tiles2[Scene::kMaxOps];  // ... and the 16x16 level
-    uint32_t n, deintMask, nInt, tileMask;  // tileMask: ops whose tiles this batch computes
+    uint2* dc[Scene::kMaxOps];       // per op: {depth bits, colour} per pixel, one 8-B gather per voxel
+    uint32_t n, deintMask, nInt, tileMask;  // tileMask: ops whose tiles and dc image this batch computes
 };
 __host__ __device__ __forceinline__ BFMat4 op_mat(const float* m) {
     BFMat4 r;
@@ -1062,6 +1063,18 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
                     maxDist, ops.tiles[blockIdx.y], ops.tiles2[blockIdx.y]);
 }
 
+// per-op interleaved {depth, colour} image (blockIdx.y = op): the voxel pass gathers both values of
+// a pixel with one dwordx2 load from one cache line (two dword gathers from two images before).
+// Ops without colour never gather (their pixels are off-screen to integrateDepthMapKernel, :441-448).
+__global__ __launch_bounds__(256) void k_pack_dc(OpTable ops, uint32_t P) {
+    if (!((ops.tileMask >> blockIdx.y) & 1u) || ops.color[blockIdx.y] == nullptr) return;
+    const float* __restrict__ d = ops.depth[blockIdx.y];
+    const uint32_t* __restrict__ c = ops.color[blockIdx.y];
+    uint2* __restrict__ o = ops.dc[blockIdx.y];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x)
+        o[i] = make_uint2(__float_as_uint(d[i]), c[i]);
+}
+
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
 // list garbageCollect walks), work list = blocks some op may update, with the op bit mask. Also
 // releases the batch's alloc dedup-set slots.
@@ -1245,20 +1258,20 @@ __device__ __forceinline__ void apply_project(const HashArgs& A, const BFDepthCa
                                               uint32_t k, float wx, float wy, const float* wz, uint32_t* pix, float* pz,
                                               float* d, uint32_t* cc) {
     const BFMat4 Ti = op_mat(ops.tinv[k]);
-    const float* depthImg = ops.depth[k];
-    const uint32_t* colorImg = ops.color[k];
+    const uint2* dcImg = ops.dc[k];
 #pragma unroll
     for (int zi = 0; zi < ZC; zi += 2) {
         f2v pz2;
-        voxel_pixel2(cam, Ti, wx, wy, f2v{wz[zi], wz[zi + 1]}, colorImg != nullptr, pix[zi], pix[zi + 1], pz2);
+        voxel_pixel2(cam, Ti, wx, wy, f2v{wz[zi], wz[zi + 1]}, ops.color[k] != nullptr, pix[zi], pix[zi + 1], pz2);
         pz[zi] = pz2.x;
         pz[zi + 1] = pz2.y;
     }
 #pragma unroll
     for (int zi = 0; zi < ZC; zi++) {
         const bool on = pix[zi] != 0xFFFFFFFFu;
-        d[zi] = on ? depthImg[pix[zi]] : -INFINITY;
-        cc[zi] = on ? colorImg[pix[zi]] : 0u;
+        const uint2 v = on ? dcImg[pix[zi]] : make_uint2(0xFF800000u, 0u);  // off-screen: depth -inf
+        d[zi] = __uint_as_float(v.x);
+        cc[zi] = v.y;
     }
 }
 #ifdef BF_APPLY_DIAG
@@ -1792,20 +1805,34 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
     const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
     ensureTiles(tw * th * kMaxOps, tw2 * th2 * kMaxOps);
+    const size_t P = (size_t)cam.imageWidth * cam.imageHeight;
+    bool needScratch = false;
+    for (uint32_t k = 0; k < n; k++) needScratch |= ops[k].tiles == nullptr;
+    if (needScratch && dcCap_ < P * kMaxOps) {
+        dc_.alloc(P * kMaxOps);
+        dcCap_ = P * kMaxOps;
+    }
     for (uint32_t k = 0; k < n; k++) {
+        BF_REQUIRE(ops[k].tiles == nullptr || ops[k].dc != nullptr, BF_ERR_ARG, "a tile cache needs its dc image");
         if (ops[k].tiles) {  // the caller's per-depth-map tile cache (fine level, then the coarse level)
             tab.tiles[k] = ops[k].tiles;
             tab.tiles2[k] = ops[k].tiles + (size_t)tw * th;
+            tab.dc[k] = ops[k].dc;
             if (!ops[k].tilesReady) tab.tileMask |= 1u << k;
         } else {
             tab.tiles[k] = tiles_.p + (size_t)k * tw * th;
             tab.tiles2[k] = tiles2_.p + (size_t)k * tw2 * th2;
+            tab.dc[k] = dc_.p + (size_t)k * P;
             tab.tileMask |= 1u << k;
         }
     }
     k_begin_ops_tiles<<<dim3(div_up((size_t)(tw * th + tw2 * th2) * 64, 256), n), 256, 0, stream_>>>(
         ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance);
     BF_LAUNCH_CHECK();
+    if (tab.tileMask) {
+        k_pack_dc<<<dim3((unsigned)std::min<size_t>(div_up(P, 256), 1024), n), 256, 0, stream_>>>(tab, (uint32_t)P);
+        BF_LAUNCH_CHECK();
+    }
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
     if (++batchEpoch_ >= (1u << 24)) {  // birth stamps are epoch << 8: restart the epochs before they wrap
         BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
