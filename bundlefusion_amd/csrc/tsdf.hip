@@ -423,11 +423,32 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
             tMax.y += tDelta.y;
         }
     }
+    // phase 2: compact the distinct blocks to the front of the set, then every thread checks one of
+    // them against the hash (one round of parallel lookups per 256 distinct blocks — a tile reaches
+    // far fewer — instead of a round per 256 slots, each waiting on its hash loads) and emits the
+    // absent ones
+    __shared__ uint32_t s_nkeys;
+    constexpr int SLOTS_PER_THREAD = LDS_SET / 256;
+    unsigned long long mine[SLOTS_PER_THREAD];
     __syncthreads();
-    // phase 2: every thread checks a share of the distinct blocks against the hash in parallel
-    // (one round of lookups instead of one per DDA step) and emits the absent ones
-    for (int k0 = 0; k0 < LDS_SET; k0 += blockDim.x) {
-        const unsigned long long key = set[k0 + threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < SLOTS_PER_THREAD; j++) mine[j] = set[j * 256 + threadIdx.x];
+    if (threadIdx.x == 0) s_nkeys = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SLOTS_PER_THREAD; j++) {
+        const bool full = mine[j] != EMPTY_KEY;
+        const unsigned long long m = __ballot(full);
+        if (m == 0) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_nkeys, (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        if (full) set[base + __popcll(m & lanemask_lt())] = mine[j];
+    }
+    __syncthreads();
+    const uint32_t nkeys = s_nkeys;
+    for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
+        const unsigned long long key = k0 + threadIdx.x < nkeys ? set[k0 + threadIdx.x] : EMPTY_KEY;
         bool want = false;
         if (key != EMPTY_KEY) {
             const i3 b = key_block(key);
