@@ -1066,11 +1066,22 @@ __global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __
 }
 
 // ---- op batches (Scene::applyOps) ---------------------------------------------------------------
-// per-op 8x8-tile depth bounds (blockIdx.y = op) + the per-batch counter reset
-// (ops whose depth map already has its tiles, e.g. a frame-store frame re-integrated before, skip)
+// per-op interleaved {depth, colour} image: the voxel pass gathers both values of a pixel with one
+// dwordx2 load from one cache line (two dword gathers from two images before). Ops without colour
+// never gather (their pixels are off-screen to integrateDepthMapKernel, :441-448).
+__device__ __forceinline__ void pack_dc(const OpTable& ops, uint32_t k, uint32_t i0, uint32_t stride, uint32_t P) {
+    if (ops.color[k] == nullptr) return;
+    const float* __restrict__ d = ops.depth[k];
+    const uint32_t* __restrict__ c = ops.color[k];
+    uint2* __restrict__ o = ops.dc[k];
+    for (uint32_t i = i0; i < P; i += stride) o[i] = make_uint2(__float_as_uint(d[i]), c[i]);
+}
+// per-op 8x8-tile depth bounds and dc image (blockIdx.y = op; workgroups [0, tileBlocks) build the
+// tiles, the rest the dc image) + the per-batch counter reset (ops whose frame already has both,
+// e.g. a frame-store frame re-integrated before, skip)
 __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigned long long* stats, OpTable ops, uint32_t W,
                                                          uint32_t H, uint32_t tilesW, uint32_t tilesH, uint32_t tiles2W,
-                                                         uint32_t tiles2H, float maxDist) {
+                                                         uint32_t tiles2H, float maxDist, uint32_t tileBlocks) {
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         ctrl[C_VISIBLE] = 0;
         ctrl[C_BAND] = 0;
@@ -1080,20 +1091,12 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
         stats[S_BOPS] += ops.n;
     }
     if (!((ops.tileMask >> blockIdx.y) & 1u)) return;
+    if (blockIdx.x >= tileBlocks) {
+        pack_dc(ops, blockIdx.y, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H);
+        return;
+    }
     depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[blockIdx.y], W, H, tilesW, tilesH, tiles2W, tiles2H,
                     maxDist, ops.tiles[blockIdx.y], ops.tiles2[blockIdx.y]);
-}
-
-// per-op interleaved {depth, colour} image (blockIdx.y = op): the voxel pass gathers both values of
-// a pixel with one dwordx2 load from one cache line (two dword gathers from two images before).
-// Ops without colour never gather (their pixels are off-screen to integrateDepthMapKernel, :441-448).
-__global__ __launch_bounds__(256) void k_pack_dc(OpTable ops, uint32_t P) {
-    if (!((ops.tileMask >> blockIdx.y) & 1u) || ops.color[blockIdx.y] == nullptr) return;
-    const float* __restrict__ d = ops.depth[blockIdx.y];
-    const uint32_t* __restrict__ c = ops.color[blockIdx.y];
-    uint2* __restrict__ o = ops.dc[blockIdx.y];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x)
-        o[i] = make_uint2(__float_as_uint(d[i]), c[i]);
 }
 
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
@@ -1539,14 +1542,11 @@ __global__ void k_gc_free_list(HashArgs A, unsigned long long* listV) {
         }
     }
     A.stats[S_GCFREED] += freed;
-}
-
-__global__ void k_gc_begin(uint32_t* ctrl, unsigned long long* stats) {
-    if (threadIdx.x == 0) {
-        stats[S_GCBLOCKS] += ctrl[C_VISIBLE];
-        ctrl[C_GC_SIMPLE] = 0;
-        ctrl[C_GC_LIST] = 0;
-    }
+    // the pass's last kernel re-arms the victim counters for the next GC (zero after a reset, too),
+    // so GC needs no counter-reset launch of its own
+    A.stats[S_GCBLOCKS] += A.ctrl[C_VISIBLE];
+    A.ctrl[C_GC_SIMPLE] = 0;
+    A.ctrl[C_GC_LIST] = 0;
 }
 
 }  // namespace
@@ -1847,13 +1847,11 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
             tab.tileMask |= 1u << k;
         }
     }
-    k_begin_ops_tiles<<<dim3(div_up((size_t)(tw * th + tw2 * th2) * 64, 256), n), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance);
+    const uint32_t tileBlocks = (uint32_t)div_up((size_t)(tw * th + tw2 * th2) * 64, 256);
+    const uint32_t packBlocks = tab.tileMask ? (uint32_t)std::min<size_t>(div_up(P, 256), 1024) : 0u;
+    k_begin_ops_tiles<<<dim3(tileBlocks + packBlocks, n), 256, 0, stream_>>>(
+        ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tileBlocks);
     BF_LAUNCH_CHECK();
-    if (tab.tileMask) {
-        k_pack_dc<<<dim3((unsigned)std::min<size_t>(div_up(P, 256), 1024), n), 256, 0, stream_>>>(tab, (uint32_t)P);
-        BF_LAUNCH_CHECK();
-    }
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
     if (++batchEpoch_ >= (1u << 24)) {  // birth stamps are epoch << 8: restart the epochs before they wrap
         BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
@@ -1904,8 +1902,6 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)
 void Scene::garbageCollect() {
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_gc_begin<<<1, 64, 0, stream_>>>(ctrl_.p, stats_.p);
-    BF_LAUNCH_CHECK();
     const unsigned grid = (unsigned)numCUs_ * 2;
     k_gc_identify<<<grid, 256, 0, stream_>>>(A, gcSimple_.p, gcList_.p);
     BF_LAUNCH_CHECK();
