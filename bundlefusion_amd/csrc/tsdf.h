@@ -9,7 +9,7 @@
 //                                 only the allocated pool prefix instead of the whole hash table
 //   visible   int4[B]             compacted frustum list {x, y, z, ptr} (16 B vs 32 B HashEntry);
 //                                 GC walks this list, as the reference walks d_hashCompactified
-//   band      int4[B]             the subset of `visible` whose voxels can reach the truncation band
+//   band      int4[24 B]          (op batches: one bin of B entries per op count) the subset of `visible` whose voxels can reach the truncation band
 //                                 of the current depth map (conservative cull against per-8x8-tile
 //                                 depth bounds) — the list integrate walks
 //   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op(s)
@@ -37,7 +37,8 @@ enum Ctrl {
     C_ERR = 7,         // error bits (1: candidate buffer overflow, 2: heap exhausted, 4: dedup set full)
     C_BAND = 8,        // blocks of the visible list that may hold a voxel inside the truncation band
     C_TICKET = 9,      // last-workgroup ticket of k_alloc_insert (self-resetting)
-    C_COUNT = 16
+    C_OPBIN = 16,      // op batches: work-list entries per op count (1..kMaxOps -> slots 16..39)
+    C_COUNT = 48
 };
 
 struct SceneConfig {

@@ -1090,6 +1090,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
         stats[S_OPS] += ops.n;
         stats[S_BOPS] += ops.n;
     }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < Scene::kMaxOps) ctrl[C_OPBIN + threadIdx.x] = 0;
     if (!((ops.tileMask >> blockIdx.y) & 1u)) return;
     if (blockIdx.x >= tileBlocks) {
         pack_dc(ops, blockIdx.y, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H);
@@ -1104,7 +1105,8 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
 // releases the batch's alloc dedup-set slots.
 __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
-                                                        uint32_t* masks, const uint32_t* __restrict__ birth, uint32_t epoch) {
+                                                        uint32_t* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
+                                                        uint32_t binCap) {
     {
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1112,7 +1114,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             if (sl >= 0) candSet[sl] = EMPTY_KEY;
         }
     }
-    __shared__ uint32_t s_cnt[2][4], s_base[2];
+    __shared__ uint32_t s_cnt[4], s_base, s_bcnt[Scene::kMaxOps], s_bbase[Scene::kMaxOps];
     const uint32_t hw = A.ctrl[C_HIGHWATER];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const BFMat4 TinvLast = op_mat(ops.tinv[ops.n - 1]);
@@ -1136,26 +1138,27 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             }
         }
         const bool inb = mask != 0;
-        const unsigned long long m0 = __ballot(keepVis), m1 = __ballot(inb);
-        if (lane == 0) {
-            s_cnt[0][wv] = (uint32_t)__popcll(m0);
-            s_cnt[1][wv] = (uint32_t)__popcll(m1);
-        }
+        // work list: one bin per op count, so the voxel pass can hand out the costliest blocks first
+        // (entry order inside a bin is free: every block is applied by exactly one wave)
+        const uint32_t bin = inb ? (uint32_t)__popc(mask) - 1u : 0u;
+        const unsigned long long m0 = __ballot(keepVis);
+        if (threadIdx.x < Scene::kMaxOps) s_bcnt[threadIdx.x] = 0;
+        if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(m0);
         __syncthreads();
-        if (threadIdx.x < 2) {
-            const uint32_t tot = s_cnt[threadIdx.x][0] + s_cnt[threadIdx.x][1] + s_cnt[threadIdx.x][2] + s_cnt[threadIdx.x][3];
-            s_base[threadIdx.x] = tot ? atomicAdd(&A.ctrl[threadIdx.x == 0 ? C_VISIBLE : C_BAND], tot) : 0u;
-        }
+        const uint32_t local = inb ? atomicAdd(&s_bcnt[bin], 1u) : 0u;
         __syncthreads();
-        uint32_t off0 = s_base[0], off1 = s_base[1];
-        for (uint32_t k = 0; k < wv; k++) {
-            off0 += s_cnt[0][k];
-            off1 += s_cnt[1][k];
+        if (threadIdx.x == 0) {
+            const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+            s_base = tot ? atomicAdd(&A.ctrl[C_VISIBLE], tot) : 0u;
         }
+        if (threadIdx.x < ops.n && s_bcnt[threadIdx.x]) s_bbase[threadIdx.x] = atomicAdd(&A.ctrl[C_OPBIN + threadIdx.x], s_bcnt[threadIdx.x]);
+        __syncthreads();
+        uint32_t off0 = s_base;
+        for (uint32_t k = 0; k < wv; k++) off0 += s_cnt[k];
         const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
         if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
         if (inb) {
-            const uint32_t k = off1 + __popcll(m1 & lanemask_lt());
+            const size_t k = (size_t)bin * binCap + s_bbase[bin] + local;
             A.band[k] = ent;
             masks[k] = mask;
         }
@@ -1176,16 +1179,39 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
 // each op of the block's mask, in sequence order: project, gather depth, band test, then the
 // integrate / de-integrate update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:420-521) on
 // the register copy of the voxel. A voxel is loaded when the first op reaches it and stored once.
+// The batch work list as one virtual list, costliest bins first (op count n down to 1): position g
+// of the list -> its slot. A wave walks g = wave, wave + nwaves, ..., so every wave takes one entry
+// per round of a list sorted by cost and all waves end with nearly equal work (a list in scan order
+// left the average wave alive for half the launch: the waves that drew many-op blocks set its end).
+struct WorkCursor {
+    uint32_t bin, lo, hi;  // current bin and its virtual range [lo, hi)
+};
+__device__ __forceinline__ WorkCursor work_begin(const uint32_t* ctrl, uint32_t nops) {
+    const uint32_t b = nops - 1;
+    return WorkCursor{b, 0u, ctrl[C_OPBIN + b]};
+}
+// slot of virtual position g (g never decreases between calls); returns false past the end
+__device__ __forceinline__ bool work_slot(const uint32_t* ctrl, WorkCursor& c, uint32_t g, uint32_t binCap, size_t& slot) {
+    while (g >= c.hi) {
+        if (c.bin == 0) return false;
+        c.bin--;
+        c.lo = c.hi;
+        c.hi += ctrl[C_OPBIN + c.bin];
+    }
+    slot = (size_t)c.bin * binCap + (g - c.lo);
+    return true;
+}
 template <int ZC>
 __global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops,
-                                                   const uint32_t* __restrict__ masks) {
-    const uint32_t nlist = A.ctrl[C_BAND];
+                                                   const uint32_t* __restrict__ masks, uint32_t binCap) {
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const int lx = lane & 7, ly = lane >> 3;
     unsigned long long updated = 0, rmw = 0;
-    for (uint32_t b = wave; b < nlist; b += nwaves) {
+    WorkCursor cur = work_begin(A.ctrl, ops.n);
+    size_t b;
+    for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
         const int4 e = A.band[b];
         const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
         const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
@@ -1340,14 +1366,15 @@ __device__ __forceinline__ uint32_t apply_update(const HashArgs& A, bool deint, 
 }
 template <int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops2(
-    HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks) {
-    const uint32_t nlist = A.ctrl[C_BAND];
+    HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks, uint32_t binCap) {
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const int lx = lane & 7, ly = lane >> 3;
     unsigned long long updated = 0, rmw = 0;
-    for (uint32_t b = wave; b < nlist; b += nwaves) {
+    WorkCursor cur = work_begin(A.ctrl, ops.n);
+    size_t b;
+    for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
         const int4 e = A.band[b];
         const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
         const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
@@ -1593,9 +1620,9 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     voxels_.alloc((size_t)B_ * BF_VOXELS_PER_BLOCK);
     blockPos_.alloc(B_);
     visible_.alloc(B_);
-    band_.alloc(B_);
+    band_.alloc((size_t)kMaxOps * B_);  // op batches: one bin per op count
     blockFlags_.alloc(B_);
-    blockMask_.alloc(B_);
+    blockMask_.alloc((size_t)kMaxOps * B_);
     blockBirth_.alloc(B_);
     candOp_.alloc(cfg_.candCapacity);
     ctrl_.alloc(C_COUNT);
@@ -1874,25 +1901,25 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     A.tiles2 = tiles2_.p;
     A.tiles2W = tw2;
     k_compactify_ops<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
-                                                                  blockMask_.p, blockBirth_.p, epoch);
+                                                                  blockMask_.p, blockBirth_.p, epoch, B_);
     BF_LAUNCH_CHECK();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
     if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 8)
-        hipExtLaunchKernelGGL(k_apply_ops2<2, 8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops2<2, 8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     else if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 7)
-        hipExtLaunchKernelGGL(k_apply_ops2<2, 7>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops2<2, 7>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     else if (applyKernel_ == 2 && applyZC_ == 2)
-        hipExtLaunchKernelGGL(k_apply_ops2<2, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops2<2, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     else if (applyKernel_ == 2)
-        hipExtLaunchKernelGGL(k_apply_ops2<4, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops2<4, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     else if (applyZC_ == 2)
-        hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     else if (applyZC_ == 8)
-        hipExtLaunchKernelGGL(k_apply_ops<8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops<8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     else
-        hipExtLaunchKernelGGL(k_apply_ops<4>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p);
+        hipExtLaunchKernelGGL(k_apply_ops<4>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;
