@@ -30,7 +30,7 @@ namespace {
 
 constexpr unsigned long long EMPTY_KEY = ~0ull;
 constexpr int ALLOC_TILE = 16;          // 16x16 pixels per workgroup
-constexpr int LDS_SET = 2048;           // per-tile candidate dedup set (16 KiB); slot = 11 low coordinate bits
+constexpr int LDS_SET = 1024;           // per-tile candidate dedup set (8 KiB); slot = 10 low coordinate bits
 constexpr uint32_t OVF_CAP = 1u << 16;  // collision-list inserts per op (serial path)
 constexpr uint32_t GC_LIST_CAP = 4096;  // collision-list deletes per GC pass (serial path)
 
@@ -385,9 +385,9 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         const bool dup = ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
         if (active && !dup) {
             const unsigned long long key = myKey;
-            // slot from the low coordinate bits (4 + 4 + 3 = 11 bits = LDS_SET): the blocks one 16x16-pixel
+            // slot from the low coordinate bits (3 + 4 + 3 = 10 bits = LDS_SET): the blocks one 16x16-pixel
             // tile reaches span a few blocks per axis, so they land in distinct slots without a mixing hash
-            uint32_t h = ((uint32_t)id.x & 15u) | (((uint32_t)id.y & 15u) << 4) | (((uint32_t)id.z & 7u) << 8);
+            uint32_t h = ((uint32_t)id.x & 7u) | (((uint32_t)id.y & 15u) << 3) | (((uint32_t)id.z & 7u) << 7);
             bool placed = false;
             for (int p = 0; p < 16; p++) {
                 const unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
