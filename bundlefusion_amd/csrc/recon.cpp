@@ -118,6 +118,9 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     BF_HIP(hipMemsetAsync(dGlobalTrans_.p, 0, dGlobalTrans_.bytes(), baStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
 
+    const char* btEnv = std::getenv("BF_BA_THREAD");
+    baThreaded_ = btEnv && std::atoi(btEnv) == 1;  // measured: no gain in the bench (the scene stream stays fed)
+    if (baThreaded_) baThread_ = std::thread([this] { baLoop(); });
     ring_.resize(RING);
     for (Pending& p : ring_) {
         BF_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
@@ -131,6 +134,14 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
 }
 
 Recon::~Recon() {
+    if (baThread_.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(baMu_);
+            baStop_ = true;
+        }
+        baCv_.notify_all();
+        baThread_.join();
+    }
     if (sceneStream_) (void)hipStreamSynchronize(sceneStream_);
     if (baStream_) (void)hipStreamSynchronize(baStream_);
     for (Pending& p : ring_) {
@@ -195,6 +206,7 @@ void Recon::setComm(Comm* c) {
 // (removals and the per-image cap only ever drop pairs, so these counts bound every later solve).
 void Recon::computePairBounds() {
     std::vector<BFEntryJ> h(globalCorrN_);
+    baDrain();
     BF_HIP(hipStreamSynchronize(baStream_));
     if (globalCorrN_) BF_HIP(hipMemcpy(h.data(), globalCorr_, sizeof(BFEntryJ) * globalCorrN_, hipMemcpyDeviceToHost));
     std::unordered_set<uint64_t> seen;
@@ -215,6 +227,7 @@ void Recon::setInitialPose(const BFMat4& T0) {
     kf_[0] = T0;
     kfSolved_[0] = 1;
     globalT_[0] = T0;
+    baDrain();
     BF_HIP(hipMemcpyAsync(dSeedT_.p, T0.m, 64, hipMemcpyHostToDevice, baStream_));
     matrices_to_poses(dSeedT_.p, 1, dGlobalRot_.p, dGlobalTrans_.p, dOne_.p, baStream_);
     BF_HIP(hipStreamSynchronize(baStream_));
@@ -330,6 +343,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     const uint32_t base = s * S;
     if (inflight_.size() == RING) {  // ring full: wait for the oldest result
         Pending& old = ring_[inflight_.front()];
+        baWaitFor(old.job);
         BF_HIP(hipEventSynchronize(old.done));
         apply(old);
         inflight_.pop_front();
@@ -352,9 +366,23 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         P.cacheTable[i] = fr.cache;
         if (!fr.cache.depth) haveCache = false;
     }
+    const uint32_t nk = s + 1;
+    BF_REQUIRE(nk + 1 <= opt_.maxKeyframes, BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
+    P.numKeyframes = nk;
+    const std::pair<BFEntryJ*, uint32_t> lc = localCorr_[s];
+    // everything below only issues work on baStream_ from state fixed at this point: the bundling
+    // thread runs it while the frame loop goes on enqueuing scene work
+    baPost([this, s, n, S, slot, haveCache, lc, nk]() { issueSubmap(s, n, S, slot, haveCache, lc, nk); });
+    P.job = lastJob_;
+    inflight_.push_back(slot);
+    lastSubmapEnqueued_ = s;
+}
+
+void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache,
+                        std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk) {
+    Pending& P = ring_[slot];
     BF_HIP(hipMemcpyAsync(dLocalT_.p, P.localInit, 64 * n, hipMemcpyHostToDevice, baStream_));
     matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_, dLocalValid_.p, baStream_);
-    const auto& lc = localCorr_[s];
     // multi-GPU: submap s's local solve runs on rank s % R only (the submaps are independent units,
     // SURVEY.md §8(e)2); its poses are then broadcast so that every rank continues identically
     const bool shardLocal = comm_ && comm_->size() > 1;
@@ -397,8 +425,6 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
         std::memcpy(P.localT, P.localInit, 64 * n);
     }
     // ---- global solve over keyframes 0..s ---------------------------------------------------
-    const uint32_t nk = s + 1;
-    BF_REQUIRE(nk + 1 <= opt_.maxKeyframes, BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
     const uint32_t ncorr = (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_;
     if (nk >= 2 && globalCorr_ && ncorr > 0) {
         std::vector<float> ws(opt_.globalNonLin, 1.0f), wz(opt_.globalNonLin, 0.0f);  // SBA.cpp:34-39, dense off
@@ -426,17 +452,70 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
     BF_HIP(hipMemcpyAsync(P.globalT, dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
     BF_HIP(hipMemcpyAsync(P.valid, dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
-    P.numKeyframes = nk;
     // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
     if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_);
     BF_HIP(hipEventRecord(P.done, baStream_));
-    inflight_.push_back(slot);
-    lastSubmapEnqueued_ = s;
 }
+
+void Recon::baPost(std::function<void()> job) {
+    ++lastJob_;
+    if (!baThreaded_) {
+        job();
+        baDone_.store(lastJob_, std::memory_order_release);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(baMu_);
+        baJobs_.push_back(std::move(job));
+    }
+    baCv_.notify_one();
+}
+
+void Recon::baLoop() {
+    for (;;) {
+        std::function<void()> job;
+        {
+            std::unique_lock<std::mutex> lk(baMu_);
+            baCv_.wait(lk, [this] { return baStop_ || !baJobs_.empty(); });
+            if (baJobs_.empty()) return;  // stop requested and nothing left
+            job = std::move(baJobs_.front());
+            baJobs_.pop_front();
+        }
+        try {
+            job();
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(baMu_);
+            if (!baErr_) baErr_ = std::current_exception();
+        }
+        {
+            std::lock_guard<std::mutex> lk(baMu_);
+            baDone_.fetch_add(1, std::memory_order_release);
+        }
+        baDoneCv_.notify_all();
+    }
+}
+
+void Recon::baWaitFor(uint64_t job) {
+    if (baDone_.load(std::memory_order_acquire) < job) {
+        std::unique_lock<std::mutex> lk(baMu_);
+        baDoneCv_.wait(lk, [this, job] { return baDone_.load(std::memory_order_acquire) >= job; });
+    }
+    std::exception_ptr e;
+    {
+        std::lock_guard<std::mutex> lk(baMu_);
+        e = baErr_;
+        baErr_ = nullptr;
+    }
+    if (e) std::rethrow_exception(e);
+}
+
+void Recon::baDrain() { baWaitFor(lastJob_); }
 
 void Recon::applyPending(bool block) {
     while (!inflight_.empty()) {
         Pending& P = ring_[inflight_.front()];
+        if (!block && baDone_.load(std::memory_order_acquire) < P.job) break;  // not issued yet
+        baWaitFor(P.job);
         if (block) {
             BF_HIP(hipEventSynchronize(P.done));
         } else {
@@ -490,6 +569,7 @@ void Recon::apply(Pending& P) {
 
 void Recon::synchronize() {
     flushIntegrate();
+    baDrain();
     BF_HIP(hipStreamSynchronize(sceneStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
     applyPending(true);

@@ -19,8 +19,14 @@
 // never waits for its bundling thread; in sync mode step 1 waits, which makes runs repeatable.
 #pragma once
 #include <array>
+#include <atomic>
+#include <condition_variable>
 #include <deque>
+#include <exception>
+#include <functional>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/bf/bf.h"
@@ -59,6 +65,7 @@ public:
 private:
     struct Pending {  // one submap's bundling results in flight
         uint32_t submap = 0, numLocal = 0, numKeyframes = 0;
+        uint64_t job = 0;  // bundling-thread job that enqueues this submap's work (see baPost)
         bool localSolved = false, globalSolved = false;
         hipEvent_t done = nullptr;
         float* localT = nullptr;    // pinned [S+1][16]
@@ -69,6 +76,8 @@ private:
         BFCachedFrame* cacheTable = nullptr; // pinned staging [S+1] (H2D of the local cache table)
     };
     void endSubmap(uint32_t s, uint32_t numFrames);
+    void issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache, std::pair<BFEntryJ*, uint32_t> lc,
+                     uint32_t nk);
     void applyPending(bool block);
     void apply(Pending& p);
     void runReintegrate();
@@ -130,6 +139,25 @@ private:
     std::vector<Pending> ring_;
     std::deque<uint32_t> inflight_;     // ring indices in submap order
     uint32_t ringNext_ = 0;
+
+    // Bundling thread (the reference's bundling thread, OnlineBundler), BF_BA_THREAD=1: a submap's
+    // local + global solves are ~450 kernel launches; the frame loop posts them as one job and this
+    // thread issues them on baStream_ in post order, so the loop never spends the launch time. Off by
+    // default (jobs run inline): without a profiler the host issues them faster than the scene stream
+    // drains its queue, and the bench showed no difference (949 vs 949 frames/s).
+    void baPost(std::function<void()> job);  // returns the job's sequence number in lastJob_
+    void baWaitFor(uint64_t job);            // until job `job` has been issued (rethrows its error)
+    void baDrain();                          // until every posted job has been issued
+    void baLoop();
+    bool baThreaded_ = true;
+    std::thread baThread_;
+    std::mutex baMu_;
+    std::condition_variable baCv_, baDoneCv_;
+    std::deque<std::function<void()>> baJobs_;
+    bool baStop_ = false;
+    uint64_t lastJob_ = 0;           // jobs posted (frame-loop thread)
+    std::atomic<uint64_t> baDone_{0};  // jobs issued
+    std::exception_ptr baErr_;
 
     DevBuf<float> dLocalRot_, dLocalT_;  // dLocalRot_ holds [rot 3L | trans 3L] (one broadcast)
     float* dLocalTrans_ = nullptr;
