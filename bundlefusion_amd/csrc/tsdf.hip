@@ -70,7 +70,8 @@ struct OpTable {
     float2* tiles[Scene::kMaxOps];   // per op: 8x8-pixel depth bounds of its depth map ...
     float2* tiles2[Scene::kMaxOps];  // ... and the 16x16 level
     uint2* dc[Scene::kMaxOps];       // per op: {depth bits, colour} per pixel, one 8-B gather per voxel
-    uint32_t n, deintMask, nInt, tileMask;  // tileMask: ops whose tiles and dc image this batch computes
+    uint8_t tileIdx[Scene::kMaxOps];  // op index of the i-th op whose frame caches this batch fills
+    uint32_t n, deintMask, nInt, tileMask, nTile;  // tileMask: ops whose tiles and dc image this batch computes
 };
 __host__ __device__ __forceinline__ BFMat4 op_mat(const float* m) {
     BFMat4 r;
@@ -1091,13 +1092,14 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
         stats[S_BOPS] += ops.n;
     }
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < Scene::kMaxOps) ctrl[C_OPBIN + threadIdx.x] = 0;
-    if (!((ops.tileMask >> blockIdx.y) & 1u)) return;
+    if (blockIdx.y >= ops.nTile) return;  // a batch whose frames are all cached launches one workgroup
+    const uint32_t k = ops.tileIdx[blockIdx.y];
     if (blockIdx.x >= tileBlocks) {
-        pack_dc(ops, blockIdx.y, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H);
+        pack_dc(ops, k, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H);
         return;
     }
-    depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[blockIdx.y], W, H, tilesW, tilesH, tiles2W, tiles2H,
-                    maxDist, ops.tiles[blockIdx.y], ops.tiles2[blockIdx.y]);
+    depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[k], W, H, tilesW, tilesH, tiles2W, tiles2H,
+                    maxDist, ops.tiles[k], ops.tiles2[k]);
 }
 
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
@@ -1875,8 +1877,12 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
         }
     }
     const uint32_t tileBlocks = (uint32_t)div_up((size_t)(tw * th + tw2 * th2) * 64, 256);
-    const uint32_t packBlocks = tab.tileMask ? (uint32_t)std::min<size_t>(div_up(P, 256), 1024) : 0u;
-    k_begin_ops_tiles<<<dim3(tileBlocks + packBlocks, n), 256, 0, stream_>>>(
+    const uint32_t packBlocks = (uint32_t)std::min<size_t>(div_up(P, 256), 1024);
+    for (uint32_t k = 0; k < n; k++)
+        if ((tab.tileMask >> k) & 1u) tab.tileIdx[tab.nTile++] = (uint8_t)k;
+    // grid.y = the ops whose caches are built here (not every op of the batch: most are cached)
+    const dim3 tileGrid = tab.nTile ? dim3(tileBlocks + packBlocks, tab.nTile) : dim3(1, 1);
+    k_begin_ops_tiles<<<tileGrid, 256, 0, stream_>>>(
         ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tileBlocks);
     BF_LAUNCH_CHECK();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
