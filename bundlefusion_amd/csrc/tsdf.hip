@@ -1132,9 +1132,11 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             const uint32_t bi = birth[i];
             // a block born in this batch at op j exists for ops j.. only (ops before it see no block)
             const uint32_t first = (bi >> 8) == epoch ? 255u - (bi & 255u) : 0u;
-            for (uint32_t k = first; k < ops.n; k++) {
+            // k runs over every op in every lane (a wave-uniform loop keeps the op's pose and tile
+            // pointers in scalar loads; a per-lane start made them per-lane loads of the op table)
+            for (uint32_t k = 0; k < ops.n; k++) {
                 const BFMat4 Ti = op_mat(ops.tinv[k]);
-                if (block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
+                if (k >= first && block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
                     block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, ops.tiles[k], ops.tiles2[k]))
                     mask |= 1u << k;
             }
