@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--buckets", type=int, default=1 << 23)
     ap.add_argument("--blocks", type=int, default=1 << 21)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r04_apply_pass_pmc.json"),
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r05_apply_pass_pmc.json"),
                     help="JSON with per-launch HBM bytes of k_integrate from the PMC passes of "
                          "tools/profile_bench.sh on this same command (committed under profiles/)")
     args = ap.parse_args()
