@@ -1185,8 +1185,9 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
 // the register copy of the voxel. A voxel is loaded when the first op reaches it and stored once.
 // The batch work list as one virtual list, costliest bins first (op count n down to 1): position g
 // of the list -> its slot. A wave walks g = wave, wave + nwaves, ..., so every wave takes one entry
-// per round of a list sorted by cost and all waves end with nearly equal work (a list in scan order
-// left the average wave alive for half the launch: the waves that drew many-op blocks set its end).
+// per round of a list sorted by cost and all waves end with nearly equal work (with the list in scan
+// order a wave's ~9 blocks drew random op counts and the waves that drew many-op blocks set the
+// launch's end: 946 -> 824 us per launch at the bench workload).
 struct WorkCursor {
     uint32_t bin, lo, hi;  // current bin and its virtual range [lo, hi)
 };
