@@ -52,16 +52,44 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(stream, params, gpu, budget_s=20.0):
-    """Oracle (port) timing on a bounded sample, scaled to frames/s with the GPU run's op counts."""
+def host_info() -> dict:
+    """nproc, CPU model, OMP threads and measured memory GB/s of this host."""
+    import ctypes as C_
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from oracle_ba import max_corr_per_image, solve
+    from oracle_lib import lib as olib
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    L = olib()
+    L.or_host_membw.restype = C_.c_double
+    L.or_host_membw.argtypes = [C_.c_size_t, C_.c_int, C_.c_void_p]
+    thr = C_.c_int()
+    gbs = L.or_host_membw(1 << 30, 4, C_.byref(thr))
+    return {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": model,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "omp_threads": thr.value,
+            "host_mem_copy_GBps": gbs}
+
+
+def cpu_baseline(stream, params, gpu, budget_s=20.0):
+    """The CPU oracle (oracle/, C++ restatement built -O3 -fopenmp) on the box's host cores: TSDF
+    integrate / de-integrate / GC on frames of the same stream, and one full global GN iteration
+    (150 PCG iterations, the reference's global schedule) at the same (K, Nc) as the GPU's global
+    solve. Frames/s = per-frame work at the GPU run's measured op mix (ops per frame, GN iterations
+    per global solve)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_ba import matrix_to_pose, max_corr_per_image, solve
     from oracle_lib import OracleScene
 
+    hi = host_info()
     t_start = time.perf_counter()
     P = stream.cam.imageWidth * stream.cam.imageHeight
     ora = OracleScene(params)
-    n = min(4, stream.F)
+    n = min(6, stream.F)
     depth = [stream.depth.download_range(f * P * 4, P * 4).view(np.float32).reshape(stream.cam.imageHeight, -1)
              for f in range(n)]
     color = [stream.color.download_range(f * P * 4, P * 4).reshape(stream.cam.imageHeight, -1, 4) for f in range(n)]
@@ -70,41 +98,38 @@ def cpu_baseline(stream, params, gpu, budget_s=20.0):
         ora.integrate(stream.gt[f], depth[f], color[f], stream.cam)
     t_int = (time.perf_counter() - t0) / n
     t0 = time.perf_counter()
-    ora.integrate(stream.gt[n - 1], depth[n - 1], color[n - 1], stream.cam, deintegrate=True)
-    t_deint = time.perf_counter() - t0
+    for f in range(2):
+        ora.integrate(stream.gt[n - 1 - f], depth[n - 1 - f], color[n - 1 - f], stream.cam, deintegrate=True)
+    t_deint = (time.perf_counter() - t0) / 2
     t0 = time.perf_counter()
     ora.garbageCollect()
     t_gc = time.perf_counter() - t0
     del ora
-    # global BA at the final keyframe count: one GN iteration with a few PCG iterations,
-    # scaled to the GPU's average PCG iterations per global solve
+    # one global GN iteration with the full 150-iteration PCG at the GPU solve's (K, Nc)
     K = gpu["keyframes"]
     ncorr = int(stream.global_prefix[K - 1])
     corr = stream.global_host[:ncorr]
     rot = np.zeros((K, 3), np.float32)
     trans = np.zeros((K, 3), np.float32)
-    from oracle_ba import matrix_to_pose
     for k in range(K):
         rot[k], trans[k] = matrix_to_pose(stream.gt[k * stream.S])
     maxc = max_corr_per_image(K + 1, 25 * (K + 1) * K // 2)
     t0 = time.perf_counter()
-    solve(corr, np.ones(K, np.int32), rot, trans, 1, 1, [1.0], max_corr_per_img=maxc)
-    t_one = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    solve(corr, np.ones(K, np.int32), rot, trans, 1, 6, [1.0], max_corr_per_img=maxc)
-    t_pcg = max(1e-9, (time.perf_counter() - t0 - t_one) / 5.0)
-    t_gn = max(1e-9, t_one - t_pcg)
-    per_solve = gpu["gn_per_solve"] * t_gn + gpu["pcg_per_solve"] * t_pcg
+    _, _, _, res = solve(corr, np.ones(K, np.int32), rot, trans, 1, 150, [1.0], max_corr_per_img=maxc)
+    t_gn = time.perf_counter() - t0
+    per_solve = gpu["gn_per_solve"] * t_gn * (gpu["pcg_per_solve"] / max(gpu["gn_per_solve"], 1e-9)) / \
+        max(1, res["pcgIterations"])
     ops_per_frame = gpu["ops_per_frame"]
-    frame_s = (ops_per_frame * (t_int + t_deint) / 2.0) + t_gc + per_solve / stream.S
-    sample = (f"oracle TSDF: {n} integrates + 1 de-integrate + 1 GC at {stream.cam.imageWidth}x"
+    frame_s = ops_per_frame * (t_int + t_deint) / 2.0 + t_gc + per_solve / stream.S
+    sample = (f"oracle TSDF: {n} integrates + 2 de-integrates + 1 GC at {stream.cam.imageWidth}x"
               f"{stream.cam.imageHeight} @ {params.virtualVoxelSize * 1000:.0f} mm ({t_int * 1e3:.0f} / "
-              f"{t_deint * 1e3:.0f} / {t_gc * 1e3:.0f} ms); oracle global BA at K={K}, Nc={ncorr}: "
-              f"{t_gn * 1e3:.0f} ms/GN setup + {t_pcg * 1e3:.0f} ms/PCG iter; scaled by the GPU run's "
-              f"{ops_per_frame:.2f} ops/frame and {gpu['gn_per_solve']:.2f} GN / {gpu['pcg_per_solve']:.1f} PCG "
-              f"per global solve (local solves not counted); {time.perf_counter() - t_start:.0f} s of CPU work")
-    return {"value": 1.0 / frame_s, "unit": "frames/s", "cores": 1, "kind": "port", "sample": sample,
-            "ms_per_gn_iter": (t_gn + t_pcg * gpu["pcg_per_solve"] / max(gpu["gn_per_solve"], 1e-9)) * 1e3}
+              f"{t_deint * 1e3:.0f} / {t_gc * 1e3:.0f} ms per call); oracle global GN iteration at K={K}, "
+              f"Nc={ncorr}: {t_gn * 1e3:.0f} ms for {res['pcgIterations']} PCG iterations; frames/s at the GPU "
+              f"run's {ops_per_frame:.2f} ops/frame and {gpu['pcg_per_solve']:.1f} PCG iterations per global solve "
+              f"(local solves not counted); {time.perf_counter() - t_start:.0f} s of CPU work")
+    return {"value": 1.0 / frame_s, "unit": "frames/s", "cores": hi["omp_threads"], "kind": "port", "sample": sample,
+            "ms_per_gn_iter": t_gn * 1e3, "host": hi,
+            "threading": "TSDF integrate: OpenMP over visible blocks; BA: serial (1 core)"}
 
 
 def global_solve_timing(stream, K, reps=3):
@@ -160,17 +185,20 @@ def global_solve_timing(stream, K, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=498, help="timed submaps (10 frames each)")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed submaps before timing")
+    ap.add_argument("--frames", type=int, default=5000,
+                    help="stream length (BASELINE north star: 5000 frames); independent of --steps")
+    ap.add_argument("--steps", type=int, default=50, help="timed submaps (10 frames each) at the stream's tail")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed submaps right before the timed ones")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--voxel", type=float, default=0.004)
     ap.add_argument("--buckets", type=int, default=1 << 23)
     ap.add_argument("--blocks", type=int, default=1 << 21)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r05_apply_pass_pmc.json"),
-                    help="JSON with per-launch HBM bytes of k_integrate from the PMC passes of "
-                         "tools/profile_bench.sh on this same command (committed under profiles/)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "apply_pass_pmc.json"),
+                    help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
+                         "tools/profile_bench.sh (committed under profiles/); used only when its "
+                         "workload equals this run's, else traffic is null")
     args = ap.parse_args()
 
     from bundlefusion_amd.dist import HostGroup, env_rank
@@ -184,7 +212,13 @@ def main():
 
     bfa.check(bfa.lib().bf_set_device(local_rank))
     S = 10
-    F = S * (args.warmup + args.steps) + 1
+    # The stream is the BASELINE workload whatever --steps says: `frames` frames (+1 so that the
+    # last submap has its S+1-th local frame). The untimed prefix ("fill": everything before the
+    # timed submaps, warmup included) builds the scene and the keyframe set; the timed submaps are
+    # the stream's tail, where the global solve runs at its largest K.
+    frames_total = max(args.frames, S * (args.warmup + args.steps))
+    F = frames_total + 1
+    fill = frames_total - S * args.steps
     t_setup = time.perf_counter()
     stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log)
     params = bfa.hash_params(voxel_size=args.voxel, num_buckets=args.buckets, num_blocks=args.blocks)
@@ -208,28 +242,35 @@ def main():
     def barrier():
         group.barrier()
 
-    f0 = S * args.warmup
-    for f in range(f0):
+    barrier()
+    t_fill = time.perf_counter()
+    last = t_fill
+    for f in range(fill):
         rc.process_frame(f)
+        if time.perf_counter() - last > 20.0:
+            log(f"  fill frame {f}")
+            last = time.perf_counter()
     rc.synchronize()
+    t_fill = time.perf_counter() - t_fill
+    fill_stats = rc.stats()
     rc.reset_stats()
     barrier()
     rc.synchronize()
     t0 = time.perf_counter()
-    last = time.perf_counter()
-    for f in range(f0, S * (args.warmup + args.steps)):
+    for f in range(fill, frames_total):
         rc.process_frame(f)
-        if time.perf_counter() - last > 30.0:
-            log(f"  frame {f}")
-            last = time.perf_counter()
     rc.synchronize()
     dt = time.perf_counter() - t0
     barrier()
     dt = group.max(dt)
+    t_fill = group.max(t_fill)
     st = rc.stats()
     ss = rc.scene_stats()
     frames = S * args.steps
     P = args.width * args.height
+    workload = (f"{frames_total}-frame {args.width}x{args.height} stream, {args.voxel * 1000:.0f} mm voxels, "
+                f"2^{args.buckets.bit_length() - 1} buckets, 2^{args.blocks.bit_length() - 1} blocks; "
+                f"local 2x100 + global 3x150 GN x PCG per submap; timed: last {args.steps} submaps")
     # dominant kernel: k_apply_ops, the op-batch voxel pass that applies a frame's re-integration
     # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Per launch, from the
     # device counters of the same launches:
@@ -246,9 +287,12 @@ def main():
     achieved = per_launch_bytes / per_launch_s / 1e9
     traffic = None
     valu = None
-    if args.traffic and os.path.exists(args.traffic):
-        tj = json.load(open(args.traffic))
-        traffic = tj.get("bytes_per_launch", tj.get("k_integrate_bytes_per_launch"))
+    traffic_src = None
+    tj = json.load(open(args.traffic)) if args.traffic and os.path.exists(args.traffic) else {}
+    # counters are taken only from a profile of this same workload (tools/profile_bench.sh records
+    # the workload string of the bench run it profiled and averages over its timed launches)
+    if tj.get("workload") == workload and world == 1:
+        traffic = tj.get("bytes_per_launch")
         traffic_src = os.path.relpath(args.traffic, REPO)
         if "valu_insts_per_launch" in tj:  # VALU-issue bound of the same kernel (SQ_INSTS_VALU pass)
             us = per_launch_s * 1e6
@@ -257,7 +301,7 @@ def main():
                     "frac": tj["valu_insts_per_launch"] / (us * VALU_PEAK_WAVE_INSTS_PER_US), "source": traffic_src}
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
-    solo = global_solve_timing(stream, min(K, args.warmup + args.steps))
+    solo = global_solve_timing(stream, K - 1)
     out = {
         "metric": "frames/s integrate+global-BA on 640x480 @4mm voxels",
         "value": frames / dt,
@@ -272,18 +316,22 @@ def main():
         "dtype": "f32",
         "data": "synthetic (seeded analytic room, GPU-rendered depth/colour with the sensor noise model, "
                 "EntryJ stand-in correspondences)",
-        "config": {"workload": f"{F - 1}-frame {args.width}x{args.height} stream, {args.voxel * 1000:.0f} mm voxels, "
-                               f"2^{args.buckets.bit_length() - 1} buckets, 2^{args.blocks.bit_length() - 1} blocks; "
-                               f"local 2x100 + global 3x150 GN x PCG per submap",
-                   "frames_timed": frames, "keyframes_final": K,
+        "config": {"workload": workload, "frames": frames_total, "frames_fill": fill, "frames_timed": frames,
+                   "keyframes_final": K,
                    "parallelism": (f"tsdf-chunk-shard{world}+ba-pair-shard{world}-rccl" if comm is not None
                                    else f"tsdf-chunk-shard{world}+ba-replicated") if world > 1 else "single"},
+        "stream": {"frames_per_s_whole_stream": frames_total / (t_fill + dt), "fill_s": t_fill, "timed_s": dt,
+                   "fill_frames_per_s": fill / t_fill if fill else None,
+                   "fill_global_gn_iters": fill_stats["globalGnIterations"],
+                   "note": "whole stream = fill + timed tail, same loop; value is the tail (largest K, largest scene)"},
         "ms_per_gn_iter": solo["ms_per_gn_iter"],
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
         "roofline": {"bound": "hbm", "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src if traffic is not None else None,
+                     "traffic_source": traffic_src,
+                     "hbm_frac_counters": (traffic / per_launch_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                     "pass_frac": pass_bytes / launches / per_launch_s / 1e9 / HBM_PEAK_GBS,
                      "launches": launches, "avg_launch_us": per_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "alg_bytes_source": "SURVEY 8(d) per-op integrate bytes (8 P + 16 Nv + 24 V) x ops per launch",
@@ -310,7 +358,7 @@ def main():
     W_, H_ = args.width, args.height
     rpr = bfa.raycast_params(W_, H_, fx=stream.cam.fx, fy=stream.cam.fy)
     routs = [bfa.DeviceArray((H_, W_), np.float32)] + [bfa.DeviceArray((H_, W_, 4), np.float32) for _ in range(3)]
-    Tlast = stream.gt[S * (args.warmup + args.steps) - 1]
+    Tlast = stream.gt[frames_total - 1]
     rc.render_time()  # enables the render clock
     rc.raycast_device(Tlast, rpr, routs)
     rc.synchronize()
@@ -337,7 +385,7 @@ def main():
                    "note": "marching cubes over every allocated block (count + scan + emit), 3M-triangle cap"}
     del mbuf
     if rank == 0 and not args.no_cpu_baseline:
-        gpu = {"keyframes": int(min(K, (args.warmup + args.steps))),
+        gpu = {"keyframes": K - 1, "global_corr": solo["correspondences"],
                "gn_per_solve": st["globalGnIterations"] / max(1, st["globalSolves"]),
                "pcg_per_solve": st["globalPcgIterations"] / max(1, st["globalSolves"]),
                "ops_per_frame": out["loop"]["ops_per_frame"]}

@@ -7,6 +7,7 @@
 #include "bf_runtime.h"
 #include "synth.h"
 #include "tsdf.h"
+#include "image_codec.h"
 #include "io.h"
 #include "cache.h"
 #include "frames.h"
@@ -991,6 +992,20 @@ int bf_sens_read_color(bf_sens* s, uint64_t frame, uint8_t* rgbx) {
     BF_TRY
     BF_REQUIRE(s && rgbx, BF_ERR_ARG, "null argument");
     s->r->colorRGBX(frame, rgbx);
+    BF_CATCH
+}
+int bf_image_decode(const uint8_t* data, uint64_t n, int compression, uint32_t* width, uint32_t* height, uint8_t* rgbx,
+                    uint64_t cap) {
+    BF_TRY
+    BF_REQUIRE(data && width && height, BF_ERR_ARG, "null argument");
+    BF_REQUIRE(compression == 1 || compression == 2, BF_ERR_ARG, "compression must be 1 (PNG) or 2 (JPEG)");
+    const DecodedImage img = compression == 2 ? jpeg_decode(data, n) : png_decode(data, n);
+    *width = img.width;
+    *height = img.height;
+    if (rgbx) {
+        BF_REQUIRE(cap >= img.rgbx.size(), BF_ERR_CAPACITY, "output buffer too small");
+        std::memcpy(rgbx, img.rgbx.data(), img.rgbx.size());
+    }
     BF_CATCH
 }
 int bf_sens_writer_create(const char* path, const BFSensInfo* info, bf_sens_writer** out) {

@@ -39,6 +39,7 @@ struct SolverConfig {
     uint32_t denseOverlapSubsample;  // s_denseOverlapCheckSubsampleFactor 4
     float verifyOptDistThresh;    // 0.02 (CUDASolverBundling.cpp:34)
     int normalEquations;          // 0 auto (assembled for sparse-only solves), 1 matrix-free, 2 assembled
+    bool earlyOut = true;         // the reference's ENABLE_EARLY_OUT build (SolverBundling.cu:7)
 };
 
 struct SolveArgs {
@@ -105,12 +106,10 @@ private:
     uint32_t maxPairs_;
     int numCUs_;
     uint32_t maxTiles_;
-    unsigned pcgLoopCap_ = 0;  // workgroups of the persistent PCG loop (0: per-iteration launches)
     size_t maxChunks_;
     DevBuf<int> rowCount_, rowStart_, rowLen_;
     DevBuf<int> tileCnt_, rowChunk_, chunkRow_;
     DevBuf<float4> chunkPart_;
-    DevBuf<unsigned long long> probe_;
     DevBuf<uint32_t> sync_;  // grid hand-off counters / flags (64 B apart)
     DevBuf<int> rowTmp_, rowIdx_;
     DevBuf<float4> entries_;

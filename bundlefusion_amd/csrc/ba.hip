@@ -48,7 +48,6 @@ struct BA {
     uint32_t nTiles;
     int *rowChunk, *chunkRow;  // chunks of row v: [rowChunk[v], rowChunk[v+1]); chunk -> row
     float4* chunkPart;         // [chunk][3] per-chunk partial sums
-    unsigned long long* probe; // development timing probe (BF_BA_PROBE=1), else null
     uint32_t* sync;            // k_pcg_loop: 8 shard counters + top counter + 8 flag replicas, 64 B apart
     float4* entries;
     float* vec;
@@ -78,6 +77,7 @@ struct BA {
     double *pstat, *dstat;
     float *apPair, *rzPart;
     uint32_t pairMode, shardCount, shardIndex, pairBound;
+    uint32_t earlyOut;  // ENABLE_EARLY_OUT (SolverBundling.cu:7): PCG |p.Ap| < 5e-7 and GN max|delta| < 0.005 exits
 };
 
 __device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -891,7 +891,7 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
         }
     }
     const float rDotzNew = block_sum(b, sh);
-    const bool last = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+    const bool last = (iter == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
     const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew / rDotzOld : 0.0f;
 #pragma unroll
     for (int q = 0; q < R; q++) {
@@ -974,7 +974,7 @@ __device__ void pcg_finisher(const BA& a, float* sh, uint32_t nch, int useDense,
             b += dot3(zR, rR) + dot3(zT, rT);
         }
         const float rDotzNew_ = block_sum(b, sh);
-        const bool last_ = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+        const bool last_ = (iter == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
         const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew_ / rDotzOld : 0.0f;
         for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
             f3 zR, zT, pR, pT;
@@ -1006,18 +1006,12 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    const unsigned long long tStart = a.probe ? wall_clock64() : 0ull;
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
     pcg_sparse_chunks<false>(a, wSparse, wave, nw, nch);
     if (useDense) pcg_dense_offdiag(a, wave, nw);
-    if (a.probe && threadIdx.x == 0) {
-        __hip_atomic_store((gu64*)&a.probe[16 + 2 * blockIdx.x], (uint64_t)tStart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu64*)&a.probe[17 + 2 * blockIdx.x], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (!last_block_sharded(a.sync, 1u)) return;
     if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
-    const unsigned long long tFin = a.probe ? wall_clock64() : 0ull;
     // ---- finisher (one workgroup): Kernel1b, Kernel2, host early-out test, Kernel3 ----
     float rDotzNew;
     bool last;
@@ -1027,20 +1021,6 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
         a.ctrl[K_PCG_ITERS]++;
         if (last) a.ctrl[K_PCG_DONE] = 1;
         a.ctrl[K_TICKET] = 0;
-        if (a.probe) {  // (per-WG stamps are handed over write-through, like the payloads)
-            unsigned long long t0 = ~0ull, t1 = 0, dur = 0, lastStart = 0;
-            for (uint32_t b = 0; b < gridDim.x; b++) {
-                const unsigned long long s0 = __hip_atomic_load((gu64*)&a.probe[16 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long s1 = __hip_atomic_load((gu64*)&a.probe[17 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                t0 = s0 < t0 ? s0 : t0;
-                t1 = s1 > t1 ? s1 : t1;
-                lastStart = s0 > lastStart ? s0 : lastStart;
-                dur += s1 - s0;
-            }
-            const unsigned long long t2 = wall_clock64();
-            a.probe[2] += t1 - t0; a.probe[3] += tFin - t0; a.probe[4] += t2 - t0; a.probe[5] += 1;
-            a.probe[6] += dur / gridDim.x; a.probe[7] += lastStart - t0;
-        }
     }
 }
 
@@ -1266,7 +1246,7 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
             rT = rT - alpha * aT;
             const f3 zR = mul3(mR, rR), zT = mul3(mT, rT);
             const float rzNew = wave_sum(dot3(zR, rR) + dot3(zT, rT));
-            const bool last = (iter == nLin - 1) || (fabsf(pAp) < 5e-7f);
+            const bool last = (iter == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
             const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
             if (own) {
                 pR = zR + beta * pR;
@@ -1299,49 +1279,6 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
     }
 }
 
-// All PCG iterations of a sparse-only GN step in ONE launch (the global solve's 3 x 150 schedule
-// would otherwise pay ~450 kernel boundaries). Per iteration: every workgroup reduces its chunks,
-// takes a ticket on a counter that grows by gridDim.x per iteration; the workgroup that draws the
-// iteration's last ticket runs the finisher (write-through loads / stores of every vector it
-// touches, since the finisher moves between workgroups) and publishes the iteration number; the
-// others poll it (one lane, relaxed agent loads, bounded) and continue with sc1 loads of p. The
-// grid never exceeds the resident capacity, so every workgroup is running while others wait.
-__global__ __launch_bounds__(WG) void k_pcg_loop(BA a, float wSparse, int nLin) {
-    __shared__ float sh[WG];
-    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t nch = (wSparse > 0.0f) ? a.ctrl[K_NCHUNK] : 0u;
-    for (int iter = 0; iter < nLin; iter++) {
-        pcg_sparse_chunks<true>(a, wSparse, wave, nw, nch);
-        const bool fin = last_block_sharded(a.sync, (uint32_t)iter + 1u);
-        if (fin) {
-            bool last = false;
-            const float rz = pcg_finish_regs<2, true>(a, sh, nch, 0, iter, nLin, last);
-            if (threadIdx.x == 0) {
-                st_wt(&a.ctrl[K_RDOTZ], __float_as_uint(rz));
-                st_wt(&a.ctrl[K_PCG_ITERS], ld_wt(&a.ctrl[K_PCG_ITERS]) + 1u);
-                if (last) st_wt(&a.ctrl[K_PCG_DONE], 1u);
-            }
-            drain_stores();
-            __syncthreads();
-            if (threadIdx.x < 8) st_wt(&a.sync[SYNC_FLAG + threadIdx.x * SYNC_LINE], (uint32_t)iter + 1u);
-        } else {
-            if (threadIdx.x == 0) {  // one poller per workgroup, on its shard's flag replica
-                const uint32_t* flag = &a.sync[SYNC_FLAG + (blockIdx.x & 7u) * SYNC_LINE];
-                for (uint32_t spins = 0; ld_wt(flag) < (uint32_t)iter + 1u; spins++) {
-                    __builtin_amdgcn_s_sleep(8);
-                    if (spins > (1u << 22)) {  // a workgroup never arrived: give up (reported as an error)
-                        atomicOr(&a.ctrl[K_ERROR], 2u);
-                        break;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        if (ld_wt(&a.ctrl[K_PCG_DONE]) != 0u || (ld_wt(&a.ctrl[K_ERROR]) & 2u) != 0u) break;
-    }
-}
-
 // EvalGNConvergence (SolverBundling.cu:694-749) + the early-out test of solveBundlingStub (:1204-1210)
 __global__ void k_gn_end(BA a, int gnIndex, int nNonLin) {
     __shared__ float sh[WG];
@@ -1362,7 +1299,7 @@ __global__ void k_gn_end(BA a, int gnIndex, int nNonLin) {
     }
     if (threadIdx.x == 0) {
         a.ctrl[K_GN_ITERS]++;
-        if (gnIndex < nNonLin - 1 && sh[0] < 0.005f) a.ctrl[K_GN_DONE] = 1;
+        if (a.earlyOut && gnIndex < nNonLin - 1 && sh[0] < 0.005f) a.ctrl[K_GN_DONE] = 1;
     }
 }
 
@@ -1766,6 +1703,7 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.denseOverlapSubsample = (o && o->denseOverlapSubsample) ? o->denseOverlapSubsample : 4;
     cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
     cfg.normalEquations = o ? o->normalEquations : 0;
+    cfg.earlyOut = !(o && o->disableEarlyOut);
     if (const char* e = getenv("BF_NORMAL_EQUATIONS"); e && (!o || o->normalEquations == 0)) cfg.normalEquations = atoi(e);
     return cfg;
 }
@@ -1785,10 +1723,6 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     maxChunks_ = div_up(2 * (size_t)cfg.maxCorr, (size_t)CH) + N;
     tileCnt_.alloc((size_t)maxTiles_ * N + 1);
     rowChunk_.alloc(N + 1);
-    if (const char* e = getenv("BF_BA_PROBE"); e && e[0] == '1') {
-        probe_.alloc(16 + 2 * 65536);
-        BF_HIP(hipMemset(probe_.p, 0, probe_.bytes()));
-    }
     chunkRow_.alloc(maxChunks_ + 1);
     chunkPart_.alloc(3 * (size_t)maxChunks_ + 3);
     rowTmp_.alloc(2 * (size_t)cfg.maxCorr + 1);
@@ -1830,14 +1764,6 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
-    // k_pcg_loop (BF_PCG_LOOP=1) needs every workgroup resident: at most the occupancy limit and 3
-    // per CU. Off by default: standalone it matches the per-iteration launches (4.03 vs 4.05 ms per
-    // GN iteration at K = 500), but in the frame loop its waiting workgroups hold CU slots that the
-    // scene stream's voxel pass needs (643 -> 375 frames/s measured).
-    int occ = 0;
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pcg_loop, WG, 0));
-    pcgLoopCap_ = 0;
-    if (const char* e = getenv("BF_PCG_LOOP"); e && e[0] == '1') pcgLoopCap_ = (unsigned)std::min(occ, 3) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
@@ -1845,15 +1771,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
 }
 
-Solver::~Solver() {
-    if (probe_.p) {  // development probe: where the time of one PCG launch goes (100 MHz clock)
-        unsigned long long h[8];
-        if (hipMemcpy(h, probe_.p, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess && h[5])
-            fprintf(stderr, "[bf probe] k_pcg launches=%llu chunk-phase=%.2fus finisher-start=%.2fus end=%.2fus "
-                    "mean-WG=%.2fus last-WG-start=%.2fus\n", h[5], h[2] * 0.01 / h[5], h[3] * 0.01 / h[5], h[4] * 0.01 / h[5],
-                    h[6] * 0.01 / h[5], h[7] * 0.01 / h[5]);
-    }
-}
+Solver::~Solver() {}
 
 size_t Solver::deviceBytes() const {
     return rowCount_.bytes() * 3 + tileCnt_.bytes() + rowChunk_.bytes() + chunkRow_.bytes() + chunkPart_.bytes() + rowTmp_.bytes() + rowIdx_.bytes() + entries_.bytes() + vec_.bytes() + img_.bytes() +
@@ -1898,7 +1816,7 @@ void Solver::solve(const SolveArgs& s) {
     a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p; a.apDense = apDense_.p;
     a.maxPairs = s.numImages * (s.numImages - 1) / 2;
     a.tileCnt = tileCnt_.p; a.nTiles = div_up(s.numCorr, TILE);
-    a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.probe = probe_.p; a.sync = sync_.p;
+    a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.sync = sync_.p;
     a.cache = s.cache; a.cw = s.cacheW; a.ch = s.cacheH;
     a.fx = s.intrinsics[0]; a.fy = s.intrinsics[1]; a.mx = s.intrinsics[2]; a.my = s.intrinsics[3];
     a.distT = cfg_.denseDistThresh; a.normT = cfg_.denseNormalThresh; a.colT = cfg_.denseColorThresh;
@@ -1910,6 +1828,7 @@ void Solver::solve(const SolveArgs& s) {
     a.pairCorr = pairCorr_.p; a.rowPair = rowPair_.p; a.pstat = pstat_.p; a.dstat = dstat_.p;
     a.apPair = apPair_.p; a.rzPart = rzPart_.p;
     a.shardCount = shardCount_; a.shardIndex = shardIndex_; a.pairBound = 0;
+    a.earlyOut = cfg_.earlyOut ? 1u : 0u;
     // assembled normal equations for sparse-only solves (auto) unless the matrix-free path is forced
     bool denseAny = false;
     for (uint32_t it = 0; it < s.nNonLin && s.cache; it++)
@@ -2005,12 +1924,7 @@ void Solver::solve(const SolveArgs& s) {
         k_entries<<<rowGrid, WG, 0, stream_>>>(a);
         k_init<<<rowGrid, WG, 0, stream_>>>(a, wS);
         BF_LAUNCH_CHECK();
-        if (!dense && s.numImages <= 2 * WG + 1 && s.nLin > 1 && pcgLoopCap_ > 0) {
-            const unsigned g = std::max(1u, std::min(rowGrid, pcgLoopCap_));
-            k_pcg_loop<<<g, WG, 0, stream_>>>(a, wS, (int)s.nLin);
-        } else {
-            for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
-        }
+        for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
         BF_LAUNCH_CHECK();
         k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
         BF_LAUNCH_CHECK();

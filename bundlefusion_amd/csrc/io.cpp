@@ -16,6 +16,7 @@
 #include <unordered_set>
 
 #include "bf_runtime.h"
+#include "image_codec.h"
 
 namespace bf {
 
@@ -111,23 +112,32 @@ void SensReader::depthU16(uint64_t i, uint16_t* out) {
     }
 }
 
-// mLib's raw colour is RGB, 3 B per pixel; SensorDataReader widens it to RGBX (:111-113). png / jpeg
-// need an image decoder this build does not carry.
+// Colour frame -> RGBX (SensorDataReader.cpp:98-116: the reader decompresses the colour stream and
+// widens it to 4 B per pixel, :111-113). Raw colour is RGB, 3 B per pixel; PNG (1) and JPEG (2)
+// streams go through the decoders of image_codec.cpp. A decoded frame must have the header's size.
 void SensReader::colorRGBX(uint64_t i, uint8_t* out) {
     const Frame& fr = frame(i);
     const uint64_t n = (uint64_t)info_.colorWidth * info_.colorHeight;
-    BF_REQUIRE(info_.colorCompression == 0, BF_ERR_ARG,
-               "unsupported colour compression " + std::to_string(info_.colorCompression) + " (png/jpeg decoding not built)");
-    BF_REQUIRE(fr.colorBytes == 3 * n, BF_ERR_IO, "raw colour size mismatch");
     buf_.resize(fr.colorBytes);
     BF_REQUIRE(fseeko(f_, (off_t)fr.colorOffset, SEEK_SET) == 0, BF_ERR_IO, "seek failed");
-    rd(f_, buf_.data(), fr.colorBytes);
-    for (uint64_t p = 0; p < n; p++) {
-        out[4 * p + 0] = buf_[3 * p + 0];
-        out[4 * p + 1] = buf_[3 * p + 1];
-        out[4 * p + 2] = buf_[3 * p + 2];
-        out[4 * p + 3] = 255;
+    if (fr.colorBytes) rd(f_, buf_.data(), fr.colorBytes);
+    if (info_.colorCompression == 0) {
+        BF_REQUIRE(fr.colorBytes == 3 * n, BF_ERR_IO, "raw colour size mismatch");
+        for (uint64_t p = 0; p < n; p++) {
+            out[4 * p + 0] = buf_[3 * p + 0];
+            out[4 * p + 1] = buf_[3 * p + 1];
+            out[4 * p + 2] = buf_[3 * p + 2];
+            out[4 * p + 3] = 255;
+        }
+        return;
     }
+    BF_REQUIRE(info_.colorCompression == 1 || info_.colorCompression == 2, BF_ERR_ARG,
+               "unsupported colour compression " + std::to_string(info_.colorCompression));
+    const DecodedImage img = info_.colorCompression == 2 ? jpeg_decode(buf_.data(), buf_.size())
+                                                         : png_decode(buf_.data(), buf_.size());
+    BF_REQUIRE(img.width == info_.colorWidth && img.height == info_.colorHeight, BF_ERR_IO,
+               "decoded colour frame size differs from the header");
+    std::memcpy(out, img.rgbx.data(), 4 * n);
 }
 
 // ---- writer ------------------------------------------------------------------------------------

@@ -38,9 +38,6 @@ T* pinned(size_t n) {
 Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCameraParams& cam, const BFReconOptions& o)
     : opt_(o), cam_(cam) {
     opt_.submapSize = or_default(o.submapSize, 10u);
-    if (const char* e = std::getenv("BF_BATCH_FIXES")) batchFixes_ = e[0] != '0';
-    if (const char* e = std::getenv("BF_DEFER_INTEGRATE")) deferIntegrate_ = e[0] != '0';
-    if (!batchFixes_) deferIntegrate_ = false;
     opt_.maxFrameFixes = or_default(o.maxFrameFixes, 10u);
     opt_.topNActive = or_default(o.topNActive, 30u);
     opt_.localNonLin = or_default(o.localNonLin, 2u);
@@ -72,7 +69,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     framePixels_ = (size_t)cam_.imageWidth * cam_.imageHeight;
     // the cache costs 8 B per pixel per frame (12.3 GB for 5 000 VGA frames, next to the frame store
     // itself); beyond 32 GB each batch rebuilds its ops' images in the scene's scratch instead
-    if (batchFixes_ && tileStride_ * opt_.maxFrames * sizeof(float2) <= (4ull << 30) &&
+    if (tileStride_ * opt_.maxFrames * sizeof(float2) <= (4ull << 30) &&
         framePixels_ * opt_.maxFrames * sizeof(uint2) <= (32ull << 30)) {
         frameTiles_.alloc(tileStride_ * opt_.maxFrames);
         frameDC_.alloc(framePixels_ * opt_.maxFrames);
@@ -82,7 +79,6 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     tm_.reset(new TrajectoryManager(opt_.maxFrames, opt_.topNActive, opt_.minPoseDistSqrt));
     if (opt_.enableTiming) {
         scene_->integrateClock().enable(true);
-        scene_->reintegrateClock().enable(true);
         scene_->applyClock().enable(true);
         local_->solveClock().enable(true);
         global_->solveClock().enable(true);
@@ -243,8 +239,7 @@ void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
 }
 
 // reintegrate() (DepthSensing.cpp:854-902). The frame's fixes are applied as one op batch
-// (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls), or, with
-// BF_BATCH_FIXES=0, one scene pass per fix.
+// (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls).
 void Recon::runReintegrate() {
     tm_->nextFixes(opt_.maxFrameFixes, ops_);
     std::vector<VoxelOp>& batch = batch_;
@@ -257,24 +252,18 @@ void Recon::runReintegrate() {
         const FrameRef& fr = frames_[op.frame];
         BF_REQUIRE(fr.set, BF_ERR_STATE, "re-integration of a frame that is not in the frame store");
         if (op.kind == FixKind::ReIntegrate) {  // deIntegrate(old) + integrate(new)
-            if (batchFixes_) {
-                batch.push_back(frameOp(op.frame, op.oldT, true));
-                batch.push_back(frameOp(op.frame, op.newT, false));
-            } else {
-                scene_->reintegrate(op.oldT, op.newT, fr.depth, fr.color, cam_);
-            }
+            batch.push_back(frameOp(op.frame, op.oldT, true));
+            batch.push_back(frameOp(op.frame, op.newT, false));
             logOp(1, op.frame, &op.oldT);
             logOp(2, op.frame, &op.newT);
             st_.deintegrations++;
             st_.integrations++;
         } else if (op.kind == FixKind::DeIntegrate) {
-            if (batchFixes_) batch.push_back(frameOp(op.frame, op.oldT, true));
-            else scene_->integrate(op.oldT, fr.depth, fr.color, cam_, true, nullptr);
+            batch.push_back(frameOp(op.frame, op.oldT, true));
             logOp(1, op.frame, &op.oldT);
             st_.deintegrations++;
         } else if (op.kind == FixKind::Integrate) {
-            if (batchFixes_) batch.push_back(frameOp(op.frame, op.newT, false));
-            else scene_->integrate(op.newT, fr.depth, fr.color, cam_, false, nullptr);
+            batch.push_back(frameOp(op.frame, op.newT, false));
             logOp(2, op.frame, &op.newT);
             st_.integrations++;
         }
@@ -304,12 +293,8 @@ void Recon::processFrame(uint32_t f) {
     runReintegrate();
     fr.Tlocal = (f % S == 0) ? identity() : mat4_mul(frames_[f - 1].Tlocal, fr.Tinc);
     const BFMat4 T = mat4_mul(kf_[s], fr.Tlocal);  // getCurrentIntegrationFrame
-    if (deferIntegrate_) {
-        pendingOp_ = frameOp(f, T, false);
-        pendingInt_ = true;
-    } else {
-        scene_->integrate(T, fr.depth, fr.color, cam_, false, nullptr);
-    }
+    pendingOp_ = frameOp(f, T, false);
+    pendingInt_ = true;
     logOp(2, f, &T);
     st_.integrations++;
     tm_->addFrame(FrameType::Integrated, T, f);
@@ -581,8 +566,8 @@ BFReconStats Recon::stats() {
     if (opt_.enableTiming) {
         s.integrateKernelMs = scene_->integrateClock().totalMs();
         s.integrateLaunches = scene_->integrateClock().launches();
-        s.reintegrateKernelMs = scene_->reintegrateClock().totalMs() + scene_->applyClock().totalMs();
-        s.reintegrateLaunches = scene_->reintegrateClock().launches() + scene_->applyClock().launches();
+        s.reintegrateKernelMs = scene_->applyClock().totalMs();
+        s.reintegrateLaunches = scene_->applyClock().launches();
         s.localSolveMs = local_->solveClock().totalMs();
         s.globalSolveMs = global_->solveClock().totalMs();
     }
@@ -594,7 +579,6 @@ void Recon::resetStats() {
     st_ = BFReconStats{};
     scene_->resetStats();
     scene_->integrateClock().reset();
-    scene_->reintegrateClock().reset();
     scene_->applyClock().reset();
     local_->solveClock().reset();
     global_->solveClock().reset();

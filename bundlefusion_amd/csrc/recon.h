@@ -125,11 +125,9 @@ private:
     std::vector<BFMat4> complete_;
     std::vector<FixOp> ops_;
     std::vector<VoxelOp> batch_;
-    bool batchFixes_ = true;  // BF_BATCH_FIXES=0: one scene pass per fix (A/B and debugging)
     // The integration of frame f is the scene call right before frame f+1's fixes (nothing touches
     // the scene in between), so it is deferred and runs as op 0 of that batch: one voxel pass less
-    // per frame, same call sequence. Any other scene access flushes it first. BF_DEFER_INTEGRATE=0: off.
-    bool deferIntegrate_ = true;
+    // per frame, same call sequence. Any other scene access flushes it first.
     bool pendingInt_ = false;
     VoxelOp pendingOp_{};
     void flushIntegrate();

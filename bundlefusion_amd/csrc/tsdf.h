@@ -14,7 +14,6 @@
 //                                 depth bounds) — the list integrate walks
 //   tiles     float2[tiles]       per-8x8-pixel-tile min/max of the valid depths of the current op(s)
 //   tiles2    float2[tiles2]      the same per 32x32 pixels (footprints wider than 2x2 tiles)
-//   flags     uint8[B]            fused re-integration: per work-list entry, which pose(s) update it
 //   ctrl      uint32[16]          device-resident counters (heap counter, visible count, ...)
 //   cand/candSet/candSlot/ovf     alloc scratch (per-op candidate list, global dedup set)
 //   victims                       GC scratch
@@ -77,8 +76,8 @@ public:
     // pointers (float / uchar4 per pixel, W*H of cam). T is camera->world.
     void integrate(const BFMat4& T, const float* depth, const uint8_t* color, const BFDepthCameraParams& cam,
                    bool deint, const uint32_t* bitMask);
-    // re-integration of one frame: de-integrate with Told then integrate with Tnew, fused into one
-    // voxel pass (identical voxel results to the two calls)
+    // re-integration of one frame: de-integrate with Told then integrate with Tnew as a two-op
+    // applyOps batch (identical voxel results to the two calls)
     void reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* depth, const uint8_t* color,
                      const BFDepthCameraParams& cam);
     // a sequence of integrate / de-integrate ops (reintegrate(), DepthSensing.cpp:854-902) as ONE
@@ -112,7 +111,6 @@ public:
     uint32_t* dCtrlMut() { return ctrl_.p; }
     size_t deviceBytes() const;
     KernelClock& integrateClock() { return integrateClock_; }  // k_integrate launches (bench roofline)
-    KernelClock& reintegrateClock() { return reintegrateClock_; }  // k_reintegrate launches
 
     // CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) after setLastRigidTransformAndCompactify:
     // frustum compactify for camera T (cam = depth-camera frustum params), ray-interval splat
@@ -161,9 +159,7 @@ private:
     uint32_t candSetMask_;
     int numCUs_;
     unsigned integrateGrid_[2] = {0, 0};
-    int integrateZC_ = 8;
     KernelClock integrateClock_;
-    KernelClock reintegrateClock_;
     KernelClock renderClock_;
     DevBuf<uint32_t> blockMask_;  // per work-list entry of an op batch: which ops may update it
     DevBuf<uint32_t> blockBirth_;  // per heap block: epoch << 8 | (255 - first op) of the batch that allocated it
@@ -171,11 +167,6 @@ private:
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
     unsigned applyGrid_ = 0;
-    int applyZC_ = 4;
-    int applyKernel_ = 2;
-    int applyWpe_ = 8;
-    DevBuf<uint8_t> blockFlags_;  // per work-list entry of a fused re-integration: bit 0 de-integrate, bit 1 integrate
-    unsigned reintegrateGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;
 };

@@ -671,22 +671,15 @@ __global__ void k_alloc_cleanup(const uint32_t* ctrl, uint32_t candCap, const in
 
 // compactifyHashAllInOneKernel, CUDASceneRepHashSDF.cu:324-366: stream the allocated pool
 // prefix [0, highWater), keep the in-frustum blocks; wave ballot + one atomic per wave.
-enum CompactMode { CM_FRUSTUM = 0, CM_INTEGRATE = 1, CM_REINT = 2 };
+enum CompactMode { CM_FRUSTUM = 0, CM_INTEGRATE = 1 };
 
 // MODE selects the lists a pass builds:
 //   CM_FRUSTUM    visible (the API's compactify / the raycaster)
 //   CM_INTEGRATE  visible (GC list) + band (integrate's work list); releases the alloc dedup set
-//   CM_REINT      fused re-integration, after alloc(new): visible for the new pose (GC list) and
-//                 one work list of the blocks on either pose's band list, with per-entry flags
-//                 (bit 0: de-integrate with TinvOld, bit 1: integrate with Tinv). Blocks alloc(new)
-//                 just created may land on the de-integration side; their voxels are zero and a
-//                 de-integration leaves a zero voxel zero, so the result equals the reference's
-//                 deIntegrate-before-alloc order.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraParams cam, BFMat4 Tinv, uint32_t candCap,
-                                                    const int* __restrict__ candSlot, unsigned long long* candSet,
-                                                    uint8_t* listFlags, BFMat4 TinvOld) {
-    if (MODE == CM_INTEGRATE || MODE == CM_REINT) {  // release this op's alloc dedup-set slots
+                                                    const int* __restrict__ candSlot, unsigned long long* candSet) {
+    if (MODE == CM_INTEGRATE) {  // release this op's alloc dedup-set slots
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
             const int sl = candSlot[i];
@@ -705,14 +698,7 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
         const bool inFr = alloc && block_in_frustum_fast(cam, Tinv, bp.x, bp.y, bp.z, A.voxelSize);
-        bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z, A.tiles, A.tiles2);
-        uint8_t fl = 0;
-        if (MODE == CM_REINT) {
-            const bool inOld = alloc && block_in_frustum_fast(cam, TinvOld, bp.x, bp.y, bp.z, A.voxelSize) &&
-                               block_may_update(A, cam, TinvOld, bp.x, bp.y, bp.z, A.tiles, A.tiles2);
-            fl = (uint8_t)((inOld ? 1 : 0) | (inb ? 2 : 0));
-            inb = fl != 0;
-        }
+        const bool inb = MODE != CM_FRUSTUM && inFr && block_may_update(A, cam, Tinv, bp.x, bp.y, bp.z, A.tiles, A.tiles2);
         const bool keepVis = inFr;
         const unsigned long long m0 = __ballot(keepVis), m1 = __ballot(inb);
         if (lane == 0) {
@@ -732,11 +718,7 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
         }
         const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
         if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
-        if (inb) {
-            const uint32_t k = off1 + __popcll(m1 & lanemask_lt());
-            A.band[k] = ent;
-            if (MODE == CM_REINT) listFlags[k] = fl;
-        }
+        if (inb) A.band[off1 + __popcll(m1 & lanemask_lt())] = ent;
         scanned += alloc ? 1 : 0;
         vis += inFr ? 1 : 0;
         band += inb ? 1 : 0;
@@ -857,15 +839,7 @@ __device__ __forceinline__ void voxel_pixel2(const BFDepthCameraParams& cam, con
     pix1 = (ux1 < cam.imageWidth && uy1 < cam.imageHeight && haveColor) ? uy1 * cam.imageWidth + ux1 : 0xFFFFFFFFu;
 }
 
-// Projection + band test of one voxel for one pose (CUDASceneRepHashSDF.cu:429-466): pixel index
-// (or ~0 when off-screen / no colour) and camera z; the depth gather is issued by the caller.
-__device__ __forceinline__ uint32_t voxel_pixel(const BFDepthCameraParams& cam, const BFMat4& Tinv, int x, int y, int z,
-                                                float voxelSize, bool haveColor, float& pz) {
-    const f3 pf = xform(Tinv, vvox_to_world(x, y, z, voxelSize));
-    const uint32_t ux = (uint32_t)proj_coord(pf.x * cam.fx, pf.z, cam.mx), uy = (uint32_t)proj_coord(pf.y * cam.fy, pf.z, cam.my);
-    pz = pf.z;
-    return (ux < cam.imageWidth && uy < cam.imageHeight && haveColor) ? uy * cam.imageWidth + ux : 0xFFFFFFFFu;
-}
+// Band test of one voxel for one pose (CUDASceneRepHashSDF.cu:449-466): sdf clamped to +-truncation.
 __device__ __forceinline__ bool voxel_in_band(const HashArgs& A, float dz, float pz, float& sdf) {
     sdf = dz - pz;
     const float tr = A.truncation + A.truncScale * dz;
@@ -978,92 +952,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         updated += nupd;
     }
     flush_stats2(A.stats, S_VOXELS, updated, S_RMW, updated);
-}
-
-// Fused re-integration of one frame (DepthSensing.cpp:893-894: deIntegrate(old) then integrate(new)):
-// one pass over the union of both work lists; per voxel the de-integration with the old pose and
-// the integration with the new pose are applied in that order in registers, so each voxel is read
-// and written once instead of twice. Per-voxel arithmetic, order and outcome are those of the two
-// separate passes (the hash is not modified between them: alloc(new) runs first and de-integration
-// never allocates; the old pose's list is built before that alloc).
-template <int ZC>
-__global__ __launch_bounds__(256) void k_reintegrate(HashArgs A, const float* __restrict__ depthImg,
-                                                     const uint32_t* __restrict__ colorImg, BFDepthCameraParams cam,
-                                                     BFMat4 TinvOld, BFMat4 TinvNew, uint8_t* flags) {
-    const uint32_t nlist = A.ctrl[C_BAND];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const int lx = lane & 7, ly = lane >> 3;
-    const bool haveColor = colorImg != nullptr;
-    unsigned long long updated = 0, rmw = 0;
-    for (uint32_t b = wave; b < nlist; b += nwaves) {
-        const int4 e = A.band[b];
-        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
-        const uint8_t f = flags[b];
-        const bool doOld = (f & 1) != 0, doNew = (f & 2) != 0;
-        const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
-        int dcount = 0;
-        uint32_t nupd = 0, nrmw = 0;
-#pragma unroll
-        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
-            float dO[ZC], dN[ZC], pzO[ZC], pzN[ZC];
-            uint32_t pixO[ZC], pixN[ZC];
-#pragma unroll
-            for (int zi = 0; zi < ZC; zi++) {
-                const int z = bz + z0 + zi;
-                pixO[zi] = doOld ? voxel_pixel(cam, TinvOld, bx, by, z, A.voxelSize, haveColor, pzO[zi]) : 0xFFFFFFFFu;
-                pixN[zi] = doNew ? voxel_pixel(cam, TinvNew, bx, by, z, A.voxelSize, haveColor, pzN[zi]) : 0xFFFFFFFFu;
-                dO[zi] = pixO[zi] != 0xFFFFFFFFu ? depthImg[pixO[zi]] : -INFINITY;
-                dN[zi] = pixN[zi] != 0xFFFFFFFFu ? depthImg[pixN[zi]] : -INFINITY;
-            }
-            float sO[ZC], sN[ZC], vs[ZC], vw[ZC];
-            uint32_t vc[ZC], cO[ZC], cN[ZC];
-            uint32_t inO = 0, inN = 0;
-#pragma unroll
-            for (int zi = 0; zi < ZC; zi++) {
-                const int z = z0 + zi;
-                if (doOld && voxel_in_band(A, dO[zi], pzO[zi], sO[zi])) inO |= 1u << zi;
-                if (doNew && voxel_in_band(A, dN[zi], pzN[zi], sN[zi])) inN |= 1u << zi;
-                vs[zi] = 0.0f; vw[zi] = 0.0f; vc[zi] = 0u; cO[zi] = 0u; cN[zi] = 0u;
-                if ((inO | inN) & (1u << zi)) {
-                    const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane));
-                    vs[zi] = __uint_as_float(v.a);
-                    vw[zi] = __uint_as_float(v.b);
-                    vc[zi] = v.c;
-                }
-                if (inO & (1u << zi)) cO[zi] = colorImg[pixO[zi]];
-                if (inN & (1u << zi)) cN[zi] = colorImg[pixN[zi]];
-            }
-#pragma unroll
-            for (int zi = 0; zi < ZC; zi++) {
-                const int z = z0 + zi;
-                const bool o = (inO >> zi) & 1, n = (inN >> zi) & 1;
-                if (!o && !n) continue;
-                float s0 = vs[zi], w = vw[zi];
-                uint32_t col = vc[zi];
-                const float wStart = w;
-                if (o) voxel_deintegrate(s0, w, col, sO[zi], cO[zi]);
-                if (n) voxel_integrate(s0, w, col, sN[zi], cN[zi], A.weightMax);
-                Vox3 nv;
-                nv.a = __float_as_uint(s0);
-                nv.b = __float_as_uint(w);
-                nv.c = col;
-                *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane)) = nv;
-                dcount += (int)(w >= 1.0f) - (int)(wStart >= 1.0f);
-                nupd += (uint32_t)o + (uint32_t)n;
-                nrmw++;
-            }
-        }
-        const unsigned long long anyChange = __ballot(dcount != 0);
-        if (anyChange) {
-            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
-            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
-        }
-        updated += nupd;
-        rmw += nrmw;
-    }
-    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
 }
 
 // ---- op batches (Scene::applyOps) ---------------------------------------------------------------
@@ -1206,103 +1094,7 @@ __device__ __forceinline__ bool work_slot(const uint32_t* ctrl, WorkCursor& c, u
     slot = (size_t)c.bin * binCap + (g - c.lo);
     return true;
 }
-template <int ZC>
-__global__ __launch_bounds__(256) void k_apply_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops,
-                                                   const uint32_t* __restrict__ masks, uint32_t binCap) {
-    const uint32_t lane = lane_id();
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const int lx = lane & 7, ly = lane >> 3;
-    unsigned long long updated = 0, rmw = 0;
-    WorkCursor cur = work_begin(A.ctrl, ops.n);
-    size_t b;
-    for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
-        const int4 e = A.band[b];
-        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
-        const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
-        const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
-        int dcount = 0;
-        uint32_t nupd = 0, nrmw = 0;
-#pragma unroll
-        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
-            float vs[ZC], vw[ZC], w0[ZC], wz[ZC];
-            uint32_t vc[ZC];
-            uint32_t loaded = 0;
-#pragma unroll
-            for (int zi = 0; zi < ZC; zi++) wz[zi] = (float)(bz + z0 + zi) * A.voxelSize;  // vvox_to_world z
-#pragma unroll
-            for (int zi = 0; zi < ZC; zi++) { vs[zi] = 0.0f; vw[zi] = 0.0f; w0[zi] = 0.0f; vc[zi] = 0u; }
-            for (uint32_t mk = mask; mk; mk &= mk - 1) {
-                const uint32_t k = (uint32_t)__builtin_ctz(mk);
-                const BFMat4 Ti = op_mat(ops.tinv[k]);
-                const float* depthImg = ops.depth[k];
-                const uint32_t* colorImg = ops.color[k];
-                const bool deint = (ops.deintMask >> k) & 1u;
-                float d[ZC], pz[ZC];
-                uint32_t pix[ZC];
-#pragma unroll
-                for (int zi = 0; zi < ZC; zi += 2) {
-                    f2v pz2;
-                    voxel_pixel2(cam, Ti, wx, wy, f2v{wz[zi], wz[zi + 1]}, colorImg != nullptr, pix[zi], pix[zi + 1], pz2);
-                    pz[zi] = pz2.x;
-                    pz[zi + 1] = pz2.y;
-                }
-#pragma unroll
-                for (int zi = 0; zi < ZC; zi++) d[zi] = pix[zi] != 0xFFFFFFFFu ? depthImg[pix[zi]] : -INFINITY;
-                float sd[ZC];
-                uint32_t cc[ZC];
-                uint32_t in = 0;
-#pragma unroll
-                for (int zi = 0; zi < ZC; zi++) {
-                    cc[zi] = 0u;
-                    if (voxel_in_band(A, d[zi], pz[zi], sd[zi])) {
-                        in |= 1u << zi;
-                        cc[zi] = colorImg[pix[zi]];
-                        if (!((loaded >> zi) & 1u)) {
-                            const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane));
-                            vs[zi] = __uint_as_float(v.a);
-                            vw[zi] = __uint_as_float(v.b);
-                            vc[zi] = v.c;
-                            w0[zi] = vw[zi];
-                        }
-                    }
-                }
-                loaded |= in;
-#pragma unroll
-                for (int zi = 0; zi < ZC; zi++) {
-                    if (!((in >> zi) & 1u)) continue;
-                    if (deint) voxel_deintegrate(vs[zi], vw[zi], vc[zi], sd[zi], cc[zi]);
-                    else voxel_integrate(vs[zi], vw[zi], vc[zi], sd[zi], cc[zi], A.weightMax);
-                    nupd++;
-                }
-            }
-#pragma unroll
-            for (int zi = 0; zi < ZC; zi++) {
-                if (!((loaded >> zi) & 1u)) continue;
-                Vox3 nv;
-                nv.a = __float_as_uint(vs[zi]);
-                nv.b = __float_as_uint(vw[zi]);
-                nv.c = vc[zi];
-                *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane)) = nv;
-                dcount += (int)(vw[zi] >= 1.0f) - (int)(w0[zi] >= 1.0f);
-                nrmw++;
-            }
-        }
-        const unsigned long long anyChange = __ballot(dcount != 0);
-        if (anyChange) {
-            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
-            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
-        }
-        updated += nupd;
-        rmw += nrmw;
-    }
-    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
-    __syncthreads();
-    flush_stats2(A.stats, S_BUPD, updated, S_BRMW, rmw);
-}
-
-// k_apply_ops with the memory round trips of an op batched: the ZC voxels of the lane are loaded
+// k_apply_ops: the memory round trips of an op batched. The ZC voxels of the lane are loaded
 // once at the start of the round (whether or not an op reaches them: +12 B per untouched voxel, but
 // no dependent load in the op loop), and the ops of the block's mask are taken two at a time —
 // both projections, then the depth AND colour gathers of both issued back to back, then the band
@@ -1369,8 +1161,10 @@ __device__ __forceinline__ uint32_t apply_update(const HashArgs& A, bool deint, 
     }
     return in;
 }
-template <int ZC, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops2(
+// ZC = 2 z-slices per round at 8 waves per SIMD (measured best: 4 slices 941 us, 7 waves 860 us vs
+// 824 us per launch at the bench workload)
+template <int ZC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks, uint32_t binCap) {
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1626,7 +1420,6 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     blockPos_.alloc(B_);
     visible_.alloc(B_);
     band_.alloc((size_t)kMaxOps * B_);  // op batches: one bin per op count
-    blockFlags_.alloc(B_);
     blockMask_.alloc((size_t)kMaxOps * B_);
     blockBirth_.alloc(B_);
     candOp_.alloc(cfg_.candCapacity);
@@ -1646,45 +1439,14 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     numCUs_ = prop.multiProcessorCount;
     // k_integrate walks its block list with a static grid stride: size the grid to exactly the
     // resident workgroups, so every wave gets the same share in one round (no tail round)
-    int occ0 = 0, occ1 = 0;
-    const char* zcEnv = std::getenv("BF_INTEGRATE_ZC");  // tuning knob: z-slices per round (8 or 4)
-    integrateZC_ = zcEnv ? std::atoi(zcEnv) : 4;
-    if (integrateZC_ != 2 && integrateZC_ != 8) integrateZC_ = 4;
-    if (integrateZC_ == 2) {
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 2>, 256, 0));
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 2>, 256, 0));
-    } else if (integrateZC_ == 4) {
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
-    } else {
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 8>, 256, 0));
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 8>, 256, 0));
-    }
-    int occR = 0;
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occR, k_reintegrate<4>, 256, 0));
-    reintegrateGrid_ = (unsigned)std::max(1, occR) * (unsigned)numCUs_;
-    int occA = 0;
-    const char* azEnv = std::getenv("BF_APPLY_ZC");  // tuning knob: z-slices per round of k_apply_ops
-    applyZC_ = azEnv ? std::atoi(azEnv) : 4;
-    if (applyZC_ != 2 && applyZC_ != 8) applyZC_ = 4;
-    const char* akEnv = std::getenv("BF_APPLY_KERNEL");  // 2: batched-round-trip voxel pass (default), 1: per-op
-    applyKernel_ = akEnv ? std::atoi(akEnv) : 2;
-    const char* awEnv = std::getenv("BF_APPLY_WPE");  // occupancy target (waves per SIMD) of k_apply_ops2<2>
-    applyWpe_ = awEnv ? std::atoi(awEnv) : 8;
-    if (applyKernel_ == 2 && !azEnv) applyZC_ = 2;
-    if (applyKernel_ == 2 && applyZC_ == 8) applyZC_ = 4;
-    if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 8) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<2, 8>, 256, 0));
-    else if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 7) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<2, 7>, 256, 0));
-    else if (applyKernel_ == 2 && applyZC_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<2, 1>, 256, 0));
-    else if (applyKernel_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops2<4, 1>, 256, 0));
-    else if (applyZC_ == 2) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<2>, 256, 0));
-    else if (applyZC_ == 8) BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<8>, 256, 0));
-    else BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4>, 256, 0));
+    int occ0 = 0, occ1 = 0, occA = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<2>, 256, 0));
     applyGrid_ = (unsigned)std::max(1, occA) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
-    BF_HIP(hipMemsetAsync(blockFlags_.p, 0, blockFlags_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
     float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -1697,7 +1459,7 @@ Scene::~Scene() {}
 
 size_t Scene::deviceBytes() const {
     return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
-           blockFlags_.bytes() + blockMask_.bytes() + blockBirth_.bytes() + candOp_.bytes() +
+           blockMask_.bytes() + blockBirth_.bytes() + candOp_.bytes() +
            tiles_.bytes() + tiles2_.bytes() + ctrl_.bytes() +
            stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
            gcList_.bytes() + blockCount_.bytes();
@@ -1748,7 +1510,7 @@ void Scene::compactify(const BFMat4& T, const BFDepthCameraParams& cam) {
     Tinv_ = mat4_inverse(T);
     beginOp();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_compactify<CM_FRUSTUM><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr, nullptr, Tinv_);
+    k_compactify<CM_FRUSTUM><<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, Tinv_, 0u, nullptr, nullptr);
     BF_LAUNCH_CHECK();
 }
 
@@ -1774,68 +1536,30 @@ void Scene::integrate(const BFMat4& T, const float* depth, const uint8_t* color,
     A.tiles2 = tiles2_.p;
     A.tiles2W = tw2;
     const unsigned grid = (unsigned)numCUs_ * 4;
-    k_compactify<CM_INTEGRATE><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p, nullptr,
-                                                          Tinv_);
+    k_compactify<CM_INTEGRATE><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p);
     BF_LAUNCH_CHECK();
     const unsigned igrid = deint ? integrateGrid_[1] : integrateGrid_[0];
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = integrateClock_.enabled();
     if (timed) integrateClock_.slot(ev0, ev1);
     const uint32_t* col = reinterpret_cast<const uint32_t*>(color);
-    if (integrateZC_ == 2) {
-        if (deint)
-            hipExtLaunchKernelGGL(k_integrate<true, 2>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-        else
-            hipExtLaunchKernelGGL(k_integrate<false, 2>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-    } else if (integrateZC_ == 4) {
-        if (deint)
-            hipExtLaunchKernelGGL(k_integrate<true, 4>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-        else
-            hipExtLaunchKernelGGL(k_integrate<false, 4>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-    } else {
-        if (deint)
-            hipExtLaunchKernelGGL(k_integrate<true, 8>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-        else
-            hipExtLaunchKernelGGL(k_integrate<false, 8>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
-    }
+    if (deint)
+        hipExtLaunchKernelGGL(k_integrate<true, 4>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
+    else
+        hipExtLaunchKernelGGL(k_integrate<false, 4>, dim3(igrid), dim3(256), 0, stream_, ev0, ev1, 0, A, depth, col, cam, Tinv_);
     BF_LAUNCH_CHECK();
     if (timed) integrateClock_.commit();
 }
 
-// reintegrate() fix of one frame (DepthSensing.cpp:890-895): deIntegrate(Told) + integrate(Tnew)
-// as one fused voxel pass (k_reintegrate) over one compactify scan (CM_REINT).
+// reintegrate() fix of one frame (DepthSensing.cpp:890-895): deIntegrate(Told) + integrate(Tnew) as a
+// two-op batch (one alloc, one compactify scan, one voxel pass; same voxels as the two calls)
 void Scene::reintegrate(const BFMat4& Told, const BFMat4& Tnew, const float* depth, const uint8_t* color,
                         const BFDepthCameraParams& cam) {
     BF_REQUIRE(depth != nullptr, BF_ERR_ARG, "depth is null");
-    const BFMat4 TinvOld = mat4_inverse(Told);
-    const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
-    const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
-    ensureTiles(tw * th, tw2 * th2);
-    k_begin_op_tiles<<<div_up((size_t)(tw * th + tw2 * th2) * 64, 256), 256, 0, stream_>>>(
-        ctrl_.p, stats_.p, depth, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tiles_.p,
-        tiles2_.p, 2u);
-    BF_LAUNCH_CHECK();
-    HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    A.band = band_.p;
-    A.tiles = tiles_.p;
-    A.tilesW = tw;
-    A.tilesH = th;
-    A.tiles2 = tiles2_.p;
-    A.tiles2W = tw2;
-    const unsigned grid = (unsigned)numCUs_ * 4;
-    T_ = Tnew;
-    Tinv_ = mat4_inverse(Tnew);
-    alloc(depth, cam, nullptr);
-    k_compactify<CM_REINT><<<grid, 256, 0, stream_>>>(A, cam, Tinv_, cfg_.candCapacity, candSlot_.p, candSet_.p,
-                                                      blockFlags_.p, TinvOld);
-    BF_LAUNCH_CHECK();
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    const bool timed = reintegrateClock_.enabled();
-    if (timed) reintegrateClock_.slot(ev0, ev1);
-    hipExtLaunchKernelGGL(k_reintegrate<4>, dim3(reintegrateGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, depth,
-                          reinterpret_cast<const uint32_t*>(color), cam, TinvOld, Tinv_, blockFlags_.p);
-    BF_LAUNCH_CHECK();
-    if (timed) reintegrateClock_.commit();
+    VoxelOp ops[2];
+    ops[0] = VoxelOp{Told, depth, color, true};
+    ops[1] = VoxelOp{Tnew, depth, color, false};
+    applyOps(ops, 2, cam);
 }
 
 // reintegrate() (DepthSensing.cpp:854-902) fixes of one frame as one pass: see tsdf.h
@@ -1915,20 +1639,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 8)
-        hipExtLaunchKernelGGL(k_apply_ops2<2, 8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
-    else if (applyKernel_ == 2 && applyZC_ == 2 && applyWpe_ == 7)
-        hipExtLaunchKernelGGL(k_apply_ops2<2, 7>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
-    else if (applyKernel_ == 2 && applyZC_ == 2)
-        hipExtLaunchKernelGGL(k_apply_ops2<2, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
-    else if (applyKernel_ == 2)
-        hipExtLaunchKernelGGL(k_apply_ops2<4, 1>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
-    else if (applyZC_ == 2)
-        hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
-    else if (applyZC_ == 8)
-        hipExtLaunchKernelGGL(k_apply_ops<8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
-    else
-        hipExtLaunchKernelGGL(k_apply_ops<4>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
+    hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;

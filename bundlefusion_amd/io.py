@@ -72,6 +72,18 @@ class SensorData:
         return out
 
 
+def decode_image(data: bytes, compression: int) -> np.ndarray:
+    """The .sens colour-stream decoders (compression 1 = PNG, 2 = JPEG) -> H x W x 4 RGBX."""
+    buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+    w, h = C.c_uint32(), C.c_uint32()
+    check(lib().bf_image_decode(buf, C.c_uint64(len(data)), C.c_int(compression), C.byref(w), C.byref(h), None,
+                                C.c_uint64(0)))
+    out = np.empty((h.value, w.value, 4), np.uint8)
+    check(lib().bf_image_decode(buf, C.c_uint64(len(data)), C.c_int(compression), C.byref(w), C.byref(h),
+                                out.ctypes.data_as(C.c_void_p), C.c_uint64(out.nbytes)))
+    return out
+
+
 def write_sens(path: str, depth_u16, rgbx, poses, depth_intrinsic, color_intrinsic=None, depth_shift=1000.0,
                zlib_depth=True, name="bundlefusion_amd synthetic", timestamps=None):
     """SensorData::saveToFile layout: raw RGB colour, zlib (or raw) ushort depth."""

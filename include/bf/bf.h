@@ -144,6 +144,10 @@ typedef struct BFSolverOptions {   /* zParametersBundlingDefault.txt defaults wh
     int32_t normalEquations;       /* 0 auto: sparse-only solves assemble the normal equations per image
                                       pair (fp64 statistics, one exchange per GN iteration when sharded);
                                       1 matrix-free (the reference's applyJ/applyJT); 2 assembled */
+    int32_t disableEarlyOut;       /* 0: the reference build (#define ENABLE_EARLY_OUT, SolverBundling.cu:7:
+                                      a PCG step with |p.Ap| < 5e-7 is the last, and the GN loop stops when
+                                      max|delta| < 0.005, :1088-1093, :1204-1210); 1: built without it, fixed
+                                      nNonLin x nLin schedules */
 } BFSolverOptions;
 
 /* ctor (CUDASolverBundling.cpp:24-136): capacity maxImages x maxCorr residuals */
@@ -414,6 +418,11 @@ int bf_sens_writer_create(const char* path, const BFSensInfo* info, bf_sens_writ
 int bf_sens_writer_add_frame(bf_sens_writer* w, const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth,
                              const uint16_t* depth, const uint8_t* rgbx);
 int bf_sens_writer_close(bf_sens_writer* w);
+/* The colour-stream decoders behind bf_sens_read_color (colorCompression 1 = PNG, 2 = JPEG; the
+ * reference decodes through mLib, SensorDataReader.cpp:98-116): data[n] -> RGBX (X = 255). Call with
+ * rgbx = NULL to get the size; otherwise rgbx holds cap bytes (>= 4 * width * height). */
+int bf_image_decode(const uint8_t* data, uint64_t n, int compression, uint32_t* width, uint32_t* height,
+                    uint8_t* rgbx, uint64_t cap);
 
 /* zParameters*.txt (mLib ParameterFile behind GlobalAppState / GlobalBundlingState): later loads
  * override earlier keys. Getters return BF_ERR_ARG for a missing key (the reference warns and

@@ -460,7 +460,7 @@ struct Solver {
             zTrans[x] = orc::mul(mTrans[x], rTrans[x]);
             scanAlpha[1] += dot(zRot[x], rRot[x]) + dot(zTrans[x], rTrans[x]);
         }
-        if (std::fabs(scanAlpha[0]) < 5e-7) last = true;  // ENABLE_EARLY_OUT (:1088-1093)
+        if (!P.disableEarlyOut && std::fabs(scanAlpha[0]) < 5e-7) last = true;  // ENABLE_EARLY_OUT (:1088-1093)
         for (uint32_t x = 1; x < N; x++) {  // Kernel3
             const float rDotzNew = scanAlpha[1];
             float beta = 0.0f;
@@ -565,7 +565,7 @@ void or_ba_solve(BFEntryJ* corr, const int* validImages, const ORSolveParams* p,
         const bool sparse = S.wSparse > 0.0f;
         for (uint32_t li = 0; li < p->nLin; li++)
             if (S.pcgIteration(sparse, li == p->nLin - 1)) break;
-        if (it < p->nNonLin - 1 && S.gnConvergence() < 0.005f) break;
+        if (it < p->nNonLin - 1 && S.gnConvergence() < 0.005f && !p->disableEarlyOut) break;  // ENABLE_EARLY_OUT (:1204-1210)
     }
     for (uint32_t i = 0; i < S.N; i++) {
         rot[3 * i] = S.xRot[i].x; rot[3 * i + 1] = S.xRot[i].y; rot[3 * i + 2] = S.xRot[i].z;

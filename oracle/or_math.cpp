@@ -1,6 +1,7 @@
 // oracle/or_math.cpp — TEST INFRASTRUCTURE (CPU oracle, see oracle.h header).
 #include "or_math.h"
 #include "oracle.h"
+#include <algorithm>
 #include <cstring>
 
 namespace orc {
@@ -39,4 +40,31 @@ extern "C" void or_matrix_inverse(const float M[16], float out[16]) {
     std::memcpy(m.e, M, 64);
     orc::m4 r = orc::inverse(m);
     std::memcpy(out, r.e, 64);
+}
+
+// Host memory bandwidth probe for bench.py's cpu_baseline (SURVEY.md §8(d) asks for the host's
+// achieved memory GB/s next to the CPU timing): an OpenMP copy of `bytes` bytes, best of `reps`,
+// counted as read + write bytes. Returns GB/s and the thread count used.
+#include <chrono>
+#include <omp.h>
+extern "C" double or_host_membw(size_t bytes, int reps, int* threadsOut) {
+    const size_t n = bytes / sizeof(double);
+    double* a = new double[n];
+    double* b = new double[n];
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; i++) { a[i] = (double)i; b[i] = 0.0; }
+    double best = 0.0;
+    for (int r = 0; r < reps; r++) {
+        auto t0 = std::chrono::steady_clock::now();
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < n; i++) b[i] = a[i];
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        best = std::max(best, 2.0 * (double)(n * sizeof(double)) / s / 1e9);
+    }
+    if (threadsOut) *threadsOut = omp_get_max_threads();
+    volatile double sink = b[n / 2];
+    (void)sink;
+    delete[] a;
+    delete[] b;
+    return best;
 }

@@ -87,6 +87,7 @@ typedef struct ORSolveParams {
     float denseDistThresh, denseNormalThresh, denseColorThresh, denseColorGradientMin;
     float denseDepthMin, denseDepthMax;
     uint32_t denseOverlapSubsample;
+    uint32_t disableEarlyOut;       /* 1: built without ENABLE_EARLY_OUT (SolverBundling.cu:7) */
 } ORSolveParams;
 
 typedef struct ORSolveResult {

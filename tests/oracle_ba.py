@@ -18,7 +18,7 @@ class ORSolveParams(C.Structure):
                 ("cache", C.c_void_p), ("cacheW", C.c_uint32), ("cacheH", C.c_uint32), ("intrinsics", C.c_float * 4),
                 ("denseDistThresh", C.c_float), ("denseNormalThresh", C.c_float), ("denseColorThresh", C.c_float),
                 ("denseColorGradientMin", C.c_float), ("denseDepthMin", C.c_float), ("denseDepthMax", C.c_float),
-                ("denseOverlapSubsample", C.c_uint32)]
+                ("denseOverlapSubsample", C.c_uint32), ("disableEarlyOut", C.c_uint32)]
 
 
 class ORSolveResult(C.Structure):
@@ -90,8 +90,9 @@ def _params(N, n_corr, n_nonlin, n_lin, w_sparse, w_depth, w_color, cache, intri
 
 def solve(corr: np.ndarray, valid: np.ndarray, rot: np.ndarray, trans: np.ndarray, n_nonlin: int, n_lin: int,
           w_sparse, w_depth=None, w_color=None, cache: dict | None = None, intrinsics=(0, 0, 0, 0),
-          max_corr_per_img=4000, dense=None):
-    """Oracle solve; returns (rot, trans, corr_after, result dict). Inputs are not modified."""
+          max_corr_per_img=4000, dense=None, early_out=True):
+    """Oracle solve; returns (rot, trans, corr_after, result dict). Inputs are not modified.
+    early_out=False: the reference built without ENABLE_EARLY_OUT (fixed schedule)."""
     corr = np.ascontiguousarray(corr.copy())
     valid = np.ascontiguousarray(valid, np.int32)
     rot = np.ascontiguousarray(rot, np.float32).copy()
@@ -99,6 +100,7 @@ def solve(corr: np.ndarray, valid: np.ndarray, rot: np.ndarray, trans: np.ndarra
     keep = []
     p = _params(valid.shape[0], len(corr), n_nonlin, n_lin, w_sparse, w_depth, w_color, cache, intrinsics,
                 max_corr_per_img, dense, keep)
+    p.disableEarlyOut = 0 if early_out else 1
     res = ORSolveResult()
     _lib().or_ba_solve(corr.ctypes.data, valid.ctypes.data, C.addressof(p), rot.ctypes.data, trans.ctypes.data,
                        C.addressof(res))

@@ -29,17 +29,28 @@ def synth_frames(F=3, w=40, h=30, seed=0):
     return depth, rgbx, poses, K
 
 
-def encode_sens(depth, rgbx, poses, K, name=b"py-encoder", zlib_depth=True, shift=1000.0):
-    """Independent encoder of the v4 layout (Appendix B), used to pin the C++ reader."""
+def encode_sens(depth, rgbx, poses, K, name=b"py-encoder", zlib_depth=True, shift=1000.0, color_codec=None,
+                jpeg_quality=90):
+    """Independent encoder of the v4 layout (Appendix B), used to pin the C++ reader. color_codec:
+    None = raw RGB (colorCompression 0), "png" (1) or "jpeg" (2) through PIL (build container only)."""
     F, h, w = depth.shape
     out = [struct.pack("<IQ", 4, len(name)), name]
     ident = np.eye(4, dtype=np.float32)
     for m in (K, ident, K, ident):
         out.append(np.asarray(m, "<f4").tobytes())
-    out.append(struct.pack("<ii", 0, 1 if zlib_depth else 0))
+    cc = {None: 0, "png": 1, "jpeg": 2}[color_codec]
+    out.append(struct.pack("<ii", cc, 1 if zlib_depth else 0))
     out.append(struct.pack("<IIIIfQ", w, h, w, h, shift, F))
     for f in range(F):
         col = np.ascontiguousarray(rgbx[f, ..., :3]).tobytes()
+        if color_codec is not None:
+            import io as _io
+
+            from PIL import Image
+            b = _io.BytesIO()
+            im = Image.fromarray(np.ascontiguousarray(rgbx[f, ..., :3]))
+            im.save(b, "JPEG", quality=jpeg_quality) if color_codec == "jpeg" else im.save(b, "PNG")
+            col = b.getvalue()
         dep = depth[f].astype("<u2").tobytes()
         if zlib_depth:
             dep = zlib.compress(dep)
