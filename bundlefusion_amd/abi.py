@@ -163,7 +163,15 @@ PAIR_STATS = 28  # doubles per image pair of the assembled normal equations (bf_
 class BFSolveResult(C.Structure):
     _fields_ = [("gnIterations", C.c_uint32), ("pcgIterations", C.c_uint32), ("maxResidual", C.c_float),
                 ("maxResidualIndex", C.c_int32), ("energy", C.c_float), ("highResidualCount", C.c_uint32),
-                ("numDensePairs", C.c_uint32), ("error", C.c_uint32)]
+                ("numDensePairs", C.c_uint32), ("error", C.c_uint32), ("skipped", C.c_uint32),
+                ("verifyUsed", C.c_uint32), ("verifyOk", C.c_uint32)]
+
+
+class BFVerifyOptions(C.Structure):  # include/bf/bf.h: local-submap verification thresholds (0 = default)
+    _fields_ = [("projCorrDistThresh", C.c_float), ("projCorrNormalThresh", C.c_float),
+                ("verifyOptErrThresh", C.c_float), ("verifyOptCorrThresh", C.c_float),
+                ("verifyOptPercentThresh", C.c_float), ("sensorDepthMin", C.c_float), ("sensorDepthMax", C.c_float),
+                ("always", C.c_int32)]
 
 
 class BFSensInfo(C.Structure):  # include/bf/types.h, mLib SensorData v4 header
@@ -214,7 +222,7 @@ class BFReconOptions(C.Structure):
                 ("maxGlobalCorr", C.c_uint32), ("maxResidualThresh", C.c_float), ("useLocalDense", C.c_int32),
                 ("cacheWidth", C.c_uint32), ("cacheHeight", C.c_uint32), ("cacheIntrinsics", C.c_float * 4),
                 ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("asyncBundling", C.c_int32),
-                ("solver", BFSolverOptions)]
+                ("solver", BFSolverOptions), ("disableLocalVerify", C.c_int32), ("verify", BFVerifyOptions)]
 
 
 class BFReconStats(C.Structure):
@@ -223,4 +231,5 @@ class BFReconStats(C.Structure):
         "globalGnIterations", "globalPcgIterations", "localGnIterations", "localPcgIterations",
         "removedPairs", "integrateLaunches")] + [
         ("integrateKernelMs", C.c_double), ("localSolveMs", C.c_double), ("globalSolveMs", C.c_double),
-        ("reintegrateLaunches", C.c_uint64), ("reintegrateKernelMs", C.c_double)]
+        ("reintegrateLaunches", C.c_uint64), ("reintegrateKernelMs", C.c_double),
+        ("localVerifications", C.c_uint64), ("invalidLocals", C.c_uint64), ("endSolves", C.c_uint64)]

@@ -475,6 +475,28 @@ int bf_solver_result(bf_solver* s, BFSolveResult* out) {
     out->highResidualCount = r.highResidualCount;
     out->numDensePairs = r.numDensePairs;
     out->error = r.error;
+    out->skipped = r.skipped;
+    out->verifyUsed = r.verifyUsed;
+    out->verifyOk = r.verifyOk;
+    BF_CATCH
+}
+int bf_solver_verify_trajectory(bf_solver* s, const float* T, const int* valid, uint32_t nImages, uint32_t nCorr,
+                                const BFCachedFrame* cache, uint32_t cacheW, uint32_t cacheH, const float intrinsics[4],
+                                const BFVerifyOptions* o, float* pairStats, int* validOut) {
+    BF_TRY
+    BF_REQUIRE(s && T && valid && cache && intrinsics, BF_ERR_ARG, "null argument");
+    VerifyParams p = verify_params(o);
+    p.T = T; p.valid = valid; p.numImages = nImages; p.numCorr = nCorr; p.cache = cache;
+    p.cacheW = cacheW; p.cacheH = cacheH;
+    std::memcpy(p.intrinsics, intrinsics, 16);
+    p.pairStats = pairStats;
+    s->solver->verify(p);
+    if (validOut) {
+        int v = 0;
+        BF_HIP(hipMemcpyAsync(&v, s->solver->verifyFlag(), 4, hipMemcpyDeviceToHost, s->stream));
+        BF_HIP(hipStreamSynchronize(s->stream));
+        *validOut = v;
+    }
     BF_CATCH
 }
 int bf_solver_num_entries_per_row(bf_solver* s, const int** dptr) {
@@ -649,6 +671,32 @@ int bf_recon_finish(bf_recon* r) {
     BF_TRY
     BF_REQUIRE(r, BF_ERR_ARG, "null recon");
     r->r->finish();
+    BF_CATCH
+}
+int bf_recon_end_solve(bf_recon* r, float denseDepthWeight, BFSolveResult* out, float* ms) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    BF_REQUIRE(denseDepthWeight >= 0.0f, BF_ERR_ARG, "negative dense weight");
+    const SolveResult res = r->r->endSolve(denseDepthWeight, ms);
+    if (out) {
+        *out = BFSolveResult{};
+        out->gnIterations = res.gnIterations;
+        out->pcgIterations = res.pcgIterations;
+        out->maxResidual = res.maxResidual;
+        out->maxResidualIndex = res.maxResidualIndex;
+        out->energy = res.energy;
+        out->highResidualCount = res.highResidualCount;
+        out->numDensePairs = res.numDensePairs;
+        out->error = res.error;
+        out->skipped = res.skipped;
+    }
+    BF_CATCH
+}
+int bf_recon_submap_poses(bf_recon* r, uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal,
+                          uint32_t* numKeyframes, int32_t* localValid) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->submapPoses(s, local, global, valid, numLocal, numKeyframes, localValid);
     BF_CATCH
 }
 int bf_recon_reintegrate(bf_recon* r) {

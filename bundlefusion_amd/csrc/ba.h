@@ -59,6 +59,31 @@ struct SolveArgs {
     bool rebuildJT;
     bool findMaxResidual;
     uint32_t pairBound = 0;  // host-known upper bound on image pairs (sharded solves; 0: read it back)
+    // device int read when the solve starts: 0 skips the whole solve (no pose change, no residual
+    // analysis, so no max-residual removal). The reconstruction loop gates a submap's global solve on
+    // its local verification (OnlineBundler.cpp:351-360, :399-405: an invalid local is not solved).
+    const int* gate = nullptr;
+};
+
+// Local-submap verification: CUDASolverBundling::useVerification (CUDASolverBundling.cpp:454-476)
+// -> Bundler::optimize (Bundler.cpp:259-274) -> SIFTImageManager::VerifyTrajectoryCU
+// (SiftGPU/SIFTImageManager.cu:1036-1159), defaults of zParametersBundlingDefault.txt:55-64.
+struct VerifyParams {
+    const float* T;              // device float4x4[n] camera -> world (the solved trajectory)
+    const int* valid;            // device int[n]
+    uint32_t numImages;
+    const BFCachedFrame* cache;  // device array [n]
+    uint32_t cacheW, cacheH;
+    float intrinsics[4];         // fx fy mx my of the cache frames
+    float distThresh = 0.15f;    // s_projCorrDistThres
+    float normalThresh = 0.97f;  // s_projCorrNormalThres
+    float errThresh = 0.05f;     // s_verifyOptErrThresh
+    float corrThresh = 0.001f;   // s_verifyOptCorrThresh
+    float percentThresh = 0.05f; // m_verifyOptPercentThresh (CUDASolverBundling.cpp:36)
+    float depthMin = 0.1f, depthMax = 3.0f;  // Bundler.cpp:267
+    uint32_t numCorr = 0;        // the solve's correspondence count (useVerification's denominator)
+    bool always = false;         // true: skip useVerification and check every pair
+    float* pairStats = nullptr;  // optional device float[n*n*3]: {sum residual, sum weight, #corr} per pair i < j
 };
 
 struct SolveResult {
@@ -71,6 +96,9 @@ struct SolveResult {
     uint32_t numDensePairs;
     uint32_t error;
     uint32_t removedI = 0xFFFFFFFFu, removedJ = 0xFFFFFFFFu;  // pair invalidated by removeMaxResidualAsync
+    uint32_t skipped = 0;      // the solve's gate was 0
+    uint32_t verifyUsed = 0;   // the last verify ran its pair check
+    uint32_t verifyOk = 0;     // ... and its outcome (1 valid)
 };
 
 class Solver {
@@ -80,12 +108,16 @@ public:
     void solve(const SolveArgs& a);       // async
     SolveResult result();                 // synchronizes
     // async variants for the reconstruction loop: copy the result words into pinned host memory
-    // (K_COUNT = 16 words) and decode them once the stream has passed that point
+    // (kResultWords words) and decode them once the stream has passed that point
     void resultAsync(uint32_t* pinnedCtrl);
     static SolveResult decodeResult(const uint32_t* ctrl);
-    static constexpr uint32_t kResultWords = 16;
+    static constexpr uint32_t kResultWords = 19;
     // device-side SBA::removeMaxResidualCUDA after a solve with findMaxResidual
     void removeMaxResidualAsync(BFEntryJ* corr, uint32_t n, int* valid, uint32_t numImages, float thresh);
+    // async local verification after a solve with findMaxResidual (its high-residual count decides
+    // whether the pair check runs); the outcome is the device int verifyFlag() (1 valid, 0 invalid)
+    void verify(const VerifyParams& p);
+    const int* verifyFlag() const;
     const int* numEntriesPerRow() const { return rowCount_.p; }  // getVarToCorrNumEntriesPerRow
     hipStream_t stream() const { return stream_; }
     const SolverConfig& config() const { return cfg_; }
@@ -140,10 +172,16 @@ private:
 };
 
 SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* opts);
+VerifyParams verify_params(const BFVerifyOptions* o);  // defaults for fields left 0
 
-// initNextGlobalTransformCU: rot/trans[s+1] = log(exp(rot/trans[s]) * exp(localRot/Trans[last]))
+// initNextGlobalTransformCU: rot/trans[s+1] = log(exp(rot/trans[s]) * exp(localRot/Trans[last])), or
+// rot/trans[s] when the device int *gate is 0 (invalid local submap, Bundler.h:75-79)
 void seed_keyframe(const float* localRot, const float* localTrans, uint32_t last, float* rot, float* trans, uint32_t s,
-                   hipStream_t st);
+                   hipStream_t st, const int* gate = nullptr);
+// *gate = *src (1 when src is null), on the stream
+void set_gate(int* gate, const int* src, hipStream_t st);
+// *gate == 0: keyframe s invalid and every correspondence with image s invalidated (OnlineBundler.cpp:351-360)
+void invalidate_local(const int* gate, uint32_t s, int* valid, BFEntryJ* corr, uint32_t n, hipStream_t st);
 
 // SBA.cu:75-119 — float4x4 <-> (rot, trans) for valid images
 void matrices_to_poses(const float* T, uint32_t n, float* rot, float* trans, const int* valid, hipStream_t s);

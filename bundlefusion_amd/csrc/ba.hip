@@ -33,10 +33,15 @@ constexpr int CPL = CH / 64;   // chunk entries per lane
 enum VecField { V_DELTA = 0, V_R, V_Z, V_P, V_AP, V_M, V_NUM };
 enum CtrlWord {
     K_TICKET = 0, K_PCG_DONE, K_GN_DONE, K_GN_ITERS, K_PCG_ITERS, K_RDOTZ, K_NPAIRS, K_LAST_W,
-    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J, K_COUNT = 16,
+    K_MAXRES, K_MAXIDX, K_ENERGY, K_HIGHCOUNT, K_ERROR, K_USE_DENSE, K_RM_I, K_RM_J,
+    K_SKIPPED,      // the solve's gate was 0: nothing ran (an invalidated local submap's global solve)
+    K_VERIFY_USED,  // useVerification said yes: the dense pair check ran
+    K_VERIFY_OK,    // VerifyTrajectoryCU's d_validOpt (1 unless a pair failed)
+    K_COUNT,
     K_NCHUNK = K_COUNT, K_NPAIRS_A,
     K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
 };
+static_assert(K_COUNT == Solver::kResultWords, "result words");
 
 struct BA {
     BFEntryJ* corr;
@@ -1537,6 +1542,7 @@ __global__ __launch_bounds__(WG) void k_residuals(BA a) {
     __shared__ int shi[WG];
     __shared__ float she[WG];
     __shared__ int shc[WG];
+    if (a.ctrl[K_SKIPPED]) return;  // gated-off solve: no residual analysis, hence no removal
     const float w = ctrlf(a.ctrl, K_LAST_W);
     float best = 0.0f, e = 0.0f;
     int bi = 0x7FFFFFFF, cnt = 0;
@@ -1603,9 +1609,110 @@ __global__ __launch_bounds__(WG) void k_residuals(BA a) {
     }
 }
 
-__global__ void k_solve_begin(uint32_t* ctrl) {
-    if (threadIdx.x < K_COUNT && threadIdx.x != K_ERROR)
-        ctrl[threadIdx.x] = (threadIdx.x == K_RM_I || threadIdx.x == K_RM_J) ? BF_INVALID_IMAGE : 0u;
+__global__ void k_solve_begin(uint32_t* ctrl, const int* gate) {
+    const uint32_t off = (gate && *gate == 0) ? 1u : 0u;
+    const uint32_t t = threadIdx.x;
+    if (t < K_COUNT && t != K_ERROR)
+        ctrl[t] = (t == K_RM_I || t == K_RM_J) ? BF_INVALID_IMAGE : (t == K_GN_DONE || t == K_SKIPPED) ? off : 0u;
+}
+
+// ---- local-submap verification (SBA.cpp:106-109 -> CUDASolverBundling::useVerification,
+// CUDASolverBundling.cpp:454-476 -> Bundler::optimize, Bundler.cpp:259-274) ----------------------
+struct VerifyArgs {
+    const float* T;
+    const int* valid;
+    uint32_t N;
+    const BFCachedFrame* cache;
+    uint32_t W, H;
+    float K[16];  // cache intrinsics as the reference's float4x4 (MatrixConversion::toCUDA(getIntrinsics()))
+    float distT, normT, errT, corrT, dmin, dmax, percentT;
+    uint32_t nCorr, always;
+    uint32_t* ctrl;
+    float* stats;
+};
+// useVerification: the pair check runs when the solve left >= 5 % of its correspondences with a
+// max-norm residual above verifyOptDistThresh (K_HIGHCOUNT, counted by k_residuals)
+__global__ void k_verify_begin(VerifyArgs v) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const bool used = v.always || ((float)v.ctrl[K_HIGHCOUNT] / (float)v.nCorr >= v.percentT);
+    v.ctrl[K_VERIFY_USED] = used ? 1u : 0u;
+    v.ctrl[K_VERIFY_OK] = 1u;
+}
+__device__ __forceinline__ float4 m4x4(const m4& m, float4 p) {  // float4x4 * float4 (cuda_SimpleMatrixUtil.h:925-933)
+    const float* e = m.e;
+    return make_float4(e[0] * p.x + e[1] * p.y + e[2] * p.z + e[3] * p.w, e[4] * p.x + e[5] * p.y + e[6] * p.z + e[7] * p.w,
+                       e[8] * p.x + e[9] * p.y + e[10] * p.z + e[11] * p.w, e[12] * p.x + e[13] * p.y + e[14] * p.z + e[15] * p.w);
+}
+// computeProjError, CUDACACHE_FLOAT_NORMALS branch (SIFTImageManager.cu:418-487; CUDACacheUtil.h:7-8
+// defines both normal formats, the float one is the branch compiled): {residual, weight, 1} of input
+// pixel idx carried by `tr` into the model frame, or 0
+__device__ f3 proj_error(const VerifyArgs& v, uint32_t idx, const m4& tr, const BFCachedFrame& in, const BFCachedFrame& model) {
+    const float4 pIn = reinterpret_cast<const float4*>(in.campos)[idx];
+    float4 nIn = reinterpret_cast<const float4*>(in.normals)[idx];
+    nIn.w = 0.0f;
+    const float dIn = in.depth[idx];
+    if (!(pIn.x != -INFINITY && nIn.x != -INFINITY && dIn >= v.dmin && dIn <= v.dmax)) return mk3(0, 0, 0);
+    const float4 pT = m4x4(tr, pIn), nT = m4x4(tr, nIn);
+    const float* K = v.K;
+    const f3 q = mk3(K[0] * pT.x + K[1] * pT.y + K[2] * pT.z + K[3] * 1.0f, K[4] * pT.x + K[5] * pT.y + K[6] * pT.z + K[7] * 1.0f,
+                     K[8] * pT.x + K[9] * pT.y + K[10] * pT.z + K[11] * 1.0f);
+    const int sx = f2i(roundf(q.x / q.z)), sy = f2i(roundf(q.y / q.z));
+    if (!(sx >= 0 && sy >= 0 && sx < (int)v.W && sy < (int)v.H)) return mk3(0, 0, 0);
+    const uint32_t t = (uint32_t)sy * v.W + (uint32_t)sx;
+    const float4 pTg = reinterpret_cast<const float4*>(model.campos)[t];
+    const float4 nTg = reinterpret_cast<const float4*>(model.normals)[t];
+    if (!(pTg.x != -INFINITY && nTg.x != -INFINITY)) return mk3(0, 0, 0);
+    const float dx = pT.x - pTg.x, dy = pT.y - pTg.y, dz = pT.z - pTg.z, dw = pT.w - pTg.w;
+    const float d = sqrtf(dx * dx + dy * dy + dz * dz + dw * dw);  // length(float4)
+    const float dN = nT.x * nTg.x + nT.y * nTg.y + nT.z * nTg.z;
+    const float tgtDepth = model.depth[t];
+    if (!(tgtDepth >= v.dmin && tgtDepth <= v.dmax)) return mk3(0, 0, 0);
+    const bool bad = (tgtDepth != -INFINITY && pT.z < tgtDepth) && d > v.distT;  // known bad match
+    if (!((dN >= v.normT && d <= v.distT) || bad)) return mk3(0, 0, 0);
+    const float camZ = (pT.z - v.dmin) / (v.dmax - v.dmin);
+    const float w = fmaxf(0.0f, 0.5f * ((1.0f - d / v.distT) + (1.0f - camZ)));
+    return mk3(d, w, 1.0f);
+}
+// VerifyTrajectoryCU_Kernel (SIFTImageManager.cu:1036-1127): one workgroup per image pair i < j,
+// both directions of every cache pixel. Sums per thread in pixel order (t, t + 256, ...), then a fixed
+// tree per wave and the 4 waves in order (the reference's warp sums + shared float atomics have no
+// fixed order; the oracle restates this one).
+__global__ __launch_bounds__(WG) void k_verify_pairs(VerifyArgs v) {
+    __shared__ float sh[3][WG / 64];
+    if (!v.ctrl[K_VERIFY_USED]) return;
+    const uint32_t i = blockIdx.x / v.N, j = blockIdx.x % v.N;
+    if (i >= j) return;
+    if (v.valid[i] == 0 || v.valid[j] == 0) return;
+    const m4 tr = mul44(inverse44(loadm4(v.T + (size_t)j * 16)), loadm4(v.T + (size_t)i * 16));
+    const m4 trInv = inverse44(tr);
+    const BFCachedFrame in = v.cache[i], model = v.cache[j];
+    float sr = 0.0f, sw = 0.0f, sn = 0.0f;
+    for (uint32_t idx = threadIdx.x; idx < v.W * v.H; idx += WG) {
+        const f3 a = proj_error(v, idx, tr, in, model);
+        const f3 b = proj_error(v, idx, trInv, model, in);
+        sr += a.x + b.x;
+        sw += a.y + b.y;
+        sn += a.z + b.z;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sr += __shfl_down(sr, off);
+        sw += __shfl_down(sw, off);
+        sn += __shfl_down(sn, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        sh[0][threadIdx.x >> 6] = sr;
+        sh[1][threadIdx.x >> 6] = sw;
+        sh[2][threadIdx.x >> 6] = sn;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float s[3];
+    for (int q = 0; q < 3; q++) s[q] = ((sh[q][0] + sh[q][1]) + sh[q][2]) + sh[q][3];
+    if (v.stats)
+        for (int q = 0; q < 3; q++) v.stats[((size_t)i * v.N + j) * 3 + q] = s[q];
+    const float err = s[0] / s[1];
+    const float corr = 0.5f * s[2] / (float)(v.W * v.H);
+    if (corr < v.corrT || err > v.errT || isnan(err)) v.ctrl[K_VERIFY_OK] = 0u;  // every failing pair writes 0
 }
 
 // ---- SBA.cu / SIFTImageManager.cu helpers ----
@@ -1645,10 +1752,16 @@ __global__ void k_check_frames(const int* numEntries, int* valid, uint32_t numIm
     }
 }
 
-// initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 = global[s] * local[last]
+// initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 = global[s] * local[last]; when the
+// submap's gate is 0 (invalid local) Bundler::initializeNextTransformUnknown instead (Bundler.h:75-79,
+// via addInvalidFrame, Bundler.cpp:362-368): keyframe s+1 = keyframe s
 __global__ void k_seed_keyframe(const float* localRot, const float* localTrans, uint32_t last, float* rot, float* trans,
-                                uint32_t s) {
+                                uint32_t s, const int* gate) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (gate && *gate == 0) {
+        for (int k = 0; k < 3; k++) { rot[3 * (s + 1) + k] = rot[3 * s + k]; trans[3 * (s + 1) + k] = trans[3 * s + k]; }
+        return;
+    }
     const m4 G = pose_to_matrix(mk3(rot[3 * s], rot[3 * s + 1], rot[3 * s + 2]), mk3(trans[3 * s], trans[3 * s + 1], trans[3 * s + 2]));
     const m4 L = pose_to_matrix(mk3(localRot[3 * last], localRot[3 * last + 1], localRot[3 * last + 2]),
                                 mk3(localTrans[3 * last], localTrans[3 * last + 1], localTrans[3 * last + 2]));
@@ -1656,6 +1769,19 @@ __global__ void k_seed_keyframe(const float* localRot, const float* localTrans, 
     matrix_to_pose(mul44(G, L), r, t);
     rot[3 * (s + 1)] = r.x; rot[3 * (s + 1) + 1] = r.y; rot[3 * (s + 1) + 2] = r.z;
     trans[3 * (s + 1)] = t.x; trans[3 * (s + 1) + 1] = t.y; trans[3 * (s + 1) + 2] = t.z;
+}
+__global__ void k_set_gate(int* gate, const int* src) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *gate = src ? *src : 1;
+}
+// An invalidated local submap becomes an invalid global frame with no features
+// (OnlineBundler.cpp:351-360: addInvalidFrame; :399-401: invalidateLastFrame): its keyframe is marked
+// invalid and no correspondence of the global list may reference it (the reference's matcher finds
+// none for a frame with 0 SIFT keys; here the list is an input, so its entries are invalidated)
+__global__ void k_invalidate_local(const int* gate, uint32_t s, int* valid, BFEntryJ* corr, uint32_t n) {
+    if (*gate != 0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) valid[s] = 0;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+        if (corr[c].imgIdx_i == s || corr[c].imgIdx_j == s) { corr[c].imgIdx_i = BF_INVALID_IMAGE; corr[c].imgIdx_j = BF_INVALID_IMAGE; }
 }
 
 // SBA::removeMaxResidualCUDA (SBA.cpp:164-203) + getMaxResidual (CUDASolverBundling.cpp:429-452) on
@@ -1706,6 +1832,20 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.earlyOut = !(o && o->disableEarlyOut);
     if (const char* e = getenv("BF_NORMAL_EQUATIONS"); e && (!o || o->normalEquations == 0)) cfg.normalEquations = atoi(e);
     return cfg;
+}
+
+VerifyParams verify_params(const BFVerifyOptions* o) {
+    VerifyParams p{};
+    if (!o) return p;
+    if (o->projCorrDistThresh > 0) p.distThresh = o->projCorrDistThresh;
+    if (o->projCorrNormalThresh > 0) p.normalThresh = o->projCorrNormalThresh;
+    if (o->verifyOptErrThresh > 0) p.errThresh = o->verifyOptErrThresh;
+    if (o->verifyOptCorrThresh > 0) p.corrThresh = o->verifyOptCorrThresh;
+    if (o->verifyOptPercentThresh > 0) p.percentThresh = o->verifyOptPercentThresh;
+    if (o->sensorDepthMin > 0) p.depthMin = o->sensorDepthMin;
+    if (o->sensorDepthMax > 0) p.depthMax = o->sensorDepthMax;
+    p.always = o->always != 0;
+    return p;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1845,7 +1985,7 @@ void Solver::solve(const SolveArgs& s) {
     const unsigned rowGrid = std::max(1u, std::min(div_up(chunkBound, (size_t)(WG / 64)), (unsigned)numCUs_ * 4));
     const bool timed = solveClock_.enabled();
     if (timed) solveClock_.start(stream_);
-    k_solve_begin<<<1, 64, 0, stream_>>>(ctrl_.p);
+    k_solve_begin<<<1, 64, 0, stream_>>>(ctrl_.p, s.gate);
     BF_LAUNCH_CHECK();
     if (s.rebuildJT) {
         const size_t lds = sizeof(int) * s.numImages;
@@ -1970,12 +2110,42 @@ SolveResult Solver::decodeResult(const uint32_t* c) {
     r.error = c[K_ERROR];
     r.removedI = c[K_RM_I];
     r.removedJ = c[K_RM_J];
+    r.skipped = c[K_SKIPPED];
+    r.verifyUsed = c[K_VERIFY_USED];
+    r.verifyOk = c[K_VERIFY_OK];
     return r;
 }
 
+void Solver::verify(const VerifyParams& p) {
+    BF_REQUIRE(p.numImages >= 1 && p.numImages <= cfg_.maxImages, BF_ERR_ARG, "verify: numImages out of range");
+    BF_REQUIRE(p.cache && p.T && p.valid, BF_ERR_ARG, "verify: trajectory, valid flags and cache frames are required");
+    VerifyArgs v{};
+    v.T = p.T; v.valid = p.valid; v.N = p.numImages; v.cache = p.cache; v.W = p.cacheW; v.H = p.cacheH;
+    for (int k = 0; k < 16; k++) v.K[k] = 0.0f;  // mat4f intrinsics of the cache (CUDACache.cpp:20-24)
+    v.K[0] = p.intrinsics[0]; v.K[2] = p.intrinsics[2];
+    v.K[5] = p.intrinsics[1]; v.K[6] = p.intrinsics[3];
+    v.K[10] = 1.0f; v.K[15] = 1.0f;
+    v.distT = p.distThresh; v.normT = p.normalThresh; v.errT = p.errThresh; v.corrT = p.corrThresh;
+    v.dmin = p.depthMin; v.dmax = p.depthMax; v.percentT = p.percentThresh;
+    v.nCorr = p.numCorr; v.always = p.always ? 1u : 0u; v.ctrl = ctrl_.p; v.stats = p.pairStats;
+    k_verify_begin<<<1, 64, 0, stream_>>>(v);
+    if (p.numImages >= 2) k_verify_pairs<<<p.numImages * p.numImages, WG, 0, stream_>>>(v);
+    BF_LAUNCH_CHECK();
+}
+
+const int* Solver::verifyFlag() const { return reinterpret_cast<const int*>(ctrl_.p + K_VERIFY_OK); }
+
 void seed_keyframe(const float* localRot, const float* localTrans, uint32_t last, float* rot, float* trans, uint32_t s,
-                   hipStream_t st) {
-    k_seed_keyframe<<<1, 64, 0, st>>>(localRot, localTrans, last, rot, trans, s);
+                   hipStream_t st, const int* gate) {
+    k_seed_keyframe<<<1, 64, 0, st>>>(localRot, localTrans, last, rot, trans, s, gate);
+    BF_LAUNCH_CHECK();
+}
+void set_gate(int* gate, const int* src, hipStream_t st) {
+    k_set_gate<<<1, 64, 0, st>>>(gate, src);
+    BF_LAUNCH_CHECK();
+}
+void invalidate_local(const int* gate, uint32_t s, int* valid, BFEntryJ* corr, uint32_t n, hipStream_t st) {
+    k_invalidate_local<<<std::max(1u, std::min(div_up(n, 256), 1024u)), 256, 0, st>>>(gate, s, valid, corr, n);
     BF_LAUNCH_CHECK();
 }
 

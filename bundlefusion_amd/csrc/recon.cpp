@@ -95,8 +95,10 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     globalValid_.assign(K, 1);
     complete_.resize(opt_.maxFrames);
 
-    dLocalRot_.alloc(6 * L);
+    dLocalRot_.alloc(6 * L + 1);
     dLocalTrans_ = dLocalRot_.p + 3 * L;
+    dGate_ = reinterpret_cast<int*>(dLocalRot_.p + 6 * L);
+    dGlobalCache_.alloc(K);
     dLocalT_.alloc(16 * L);
     dLocalValid_.alloc(L);
     dLocalCache_.alloc(L);
@@ -110,6 +112,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     BF_HIP(hipMemcpyAsync(dLocalValid_.p, ones.data(), 4 * L, hipMemcpyHostToDevice, baStream_));
     BF_HIP(hipMemcpyAsync(dGlobalValid_.p, ones.data(), 4 * K, hipMemcpyHostToDevice, baStream_));
     BF_HIP(hipMemcpyAsync(dOne_.p, ones.data(), 4, hipMemcpyHostToDevice, baStream_));
+    BF_HIP(hipMemcpyAsync(dGate_, ones.data(), 4, hipMemcpyHostToDevice, baStream_));
     BF_HIP(hipMemsetAsync(dGlobalRot_.p, 0, dGlobalRot_.bytes(), baStream_));
     BF_HIP(hipMemsetAsync(dGlobalTrans_.p, 0, dGlobalTrans_.bytes(), baStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
@@ -126,6 +129,8 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
         p.ctrl = pinned<uint32_t>(2 * Solver::kResultWords);
         p.localInit = pinned<float>(16 * L);
         p.cacheTable = pinned<BFCachedFrame>(L);
+        p.gate = pinned<int>(1);
+        *p.gate = 1;
     }
 }
 
@@ -143,7 +148,7 @@ Recon::~Recon() {
     for (Pending& p : ring_) {
         if (p.done) (void)hipEventDestroy(p.done);
         for (void* q : {(void*)p.localT, (void*)p.globalT, (void*)p.valid, (void*)p.ctrl, (void*)p.localInit,
-                        (void*)p.cacheTable})
+                        (void*)p.cacheTable, (void*)p.gate})
             if (q) (void)hipHostFree(q);
     }
     scene_.reset();
@@ -339,6 +344,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     P.submap = s;
     P.numLocal = n;
     P.localSolved = P.globalSolved = false;
+    P.endSolve = false;
 
     // ---- local solve over frames base .. base+n-1 (first frame fixed) ----------------------
     bool haveCache = opt_.useLocalDense != 0;
@@ -366,15 +372,19 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
 void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache,
                         std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk) {
     Pending& P = ring_[slot];
+    const uint32_t L = S + 1;
     BF_HIP(hipMemcpyAsync(dLocalT_.p, P.localInit, 64 * n, hipMemcpyHostToDevice, baStream_));
     matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_, dLocalValid_.p, baStream_);
     // multi-GPU: submap s's local solve runs on rank s % R only (the submaps are independent units,
-    // SURVEY.md §8(e)2); its poses are then broadcast so that every rank continues identically
+    // SURVEY.md §8(e)2); its poses and verification outcome are then broadcast so that every rank
+    // continues identically
     const bool shardLocal = comm_ && comm_->size() > 1;
     const int localOwner = shardLocal ? (int)(s % (uint32_t)comm_->size()) : 0;
     const bool solveHere = !shardLocal || localOwner == comm_->rank();
+    const bool verify = opt_.disableLocalVerify == 0;
+    const size_t bcast = 6 * (size_t)L + 1;  // [rot | trans | gate]
     if (n >= 2 && lc.first && lc.second > 0 && !solveHere) {
-        comm_->broadcast(dLocalRot_.p, 6 * (size_t)(S + 1), localOwner, baStream_);
+        comm_->broadcast(dLocalRot_.p, bcast, localOwner, baStream_);
         poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
         BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
     } else if (n >= 2 && lc.first && lc.second > 0) {
@@ -399,17 +409,41 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
         a.rot = dLocalRot_.p;
         a.trans = dLocalTrans_;
         a.rebuildJT = true;
-        a.findMaxResidual = false;  // optimizeLocal: no max residual removal (OnlineBundler.cpp:255)
+        // optimizeLocal removes no max residual (OnlineBundler.cpp:255-256); the residual analysis
+        // only counts the high residuals useVerification asks for
+        a.findMaxResidual = verify;
         local_->solve(a);
+        poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
+        // SBA::align :106-109 -> Bundler::optimize :259-274 (needs the submap's cache frames)
+        const bool check = verify && haveCache;
+        if (check) {
+            VerifyParams vp = verify_params(&opt_.verify);
+            vp.T = dLocalT_.p;
+            vp.valid = dLocalValid_.p;
+            vp.numImages = n;
+            vp.cache = dLocalCache_.p;
+            vp.cacheW = opt_.cacheWidth;
+            vp.cacheH = opt_.cacheHeight;
+            std::memcpy(vp.intrinsics, opt_.cacheIntrinsics, sizeof(vp.intrinsics));
+            vp.numCorr = lc.second;
+            local_->verify(vp);
+        }
+        set_gate(dGate_, check ? local_->verifyFlag() : nullptr, baStream_);
         local_->resultAsync(P.ctrl);
         P.localSolved = true;
-        if (shardLocal) comm_->broadcast(dLocalRot_.p, 6 * (size_t)(S + 1), localOwner, baStream_);
-        poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
+        if (shardLocal) comm_->broadcast(dLocalRot_.p, bcast, localOwner, baStream_);
         BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
     } else {
+        set_gate(dGate_, nullptr, baStream_);
         std::memcpy(P.localT, P.localInit, 64 * n);
     }
     // ---- global solve over keyframes 0..s ---------------------------------------------------
+    // an invalid local submap (gate 0) becomes an invalid keyframe without correspondences and its
+    // global solve is skipped (processGlobal / optimizeGlobal INVALIDATE, OnlineBundler.cpp:351-360,
+    // 399-405). Keyframe 0 is never invalidated (the reference exits on an invalid first chunk,
+    // Bundler.cpp:377-384).
+    const int* gate = (verify && s > 0) ? dGate_ : nullptr;
+    if (gate && globalCorr_) invalidate_local(gate, s, dGlobalValid_.p, globalCorr_, globalCorrN_, baStream_);
     const uint32_t ncorr = (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_;
     if (nk >= 2 && globalCorr_ && ncorr > 0) {
         std::vector<float> ws(opt_.globalNonLin, 1.0f), wz(opt_.globalNonLin, 0.0f);  // SBA.cpp:34-39, dense off
@@ -427,6 +461,7 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
         a.trans = dGlobalTrans_.p;
         a.rebuildJT = true;
         a.findMaxResidual = true;
+        a.gate = gate;
         if (comm_ && s < pairBound_.size()) a.pairBound = std::max(pairBound_[s], 1u);
         global_->solve(a);
         // removeMaxResidualCUDA with getMaxResidual's (0, <10) exemption, on the device
@@ -437,9 +472,110 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
     poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
     BF_HIP(hipMemcpyAsync(P.globalT, dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
     BF_HIP(hipMemcpyAsync(P.valid, dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
+    BF_HIP(hipMemcpyAsync(P.gate, dGate_, 4, hipMemcpyDeviceToHost, baStream_));
     // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
-    if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_);
+    if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_, gate);
     BF_HIP(hipEventRecord(P.done, baStream_));
+}
+
+// One end-of-sequence global solve (OnlineBundler.cpp:171-197 + optimizeGlobal with isSequenceDone,
+// :373-398): every keyframe and correspondence, max-residual removal, optionally the dense depth term
+// of USE_GLOBAL_DENSE_AT_END (:177-189) over the keyframes' cache frames.
+void Recon::issueEndSolve(uint32_t slot, uint32_t nk, uint32_t ncorr, float wDense, hipEvent_t t0, hipEvent_t t1) {
+    Pending& P = ring_[slot];
+    std::vector<float> ws(opt_.globalNonLin, 1.0f), wd(opt_.globalNonLin, wDense), wc(opt_.globalNonLin, 0.0f);
+    SolveArgs a{};
+    a.corr = globalCorr_;
+    a.numCorr = ncorr;
+    a.valid = dGlobalValid_.p;
+    a.numImages = nk;
+    a.nNonLin = opt_.globalNonLin;
+    a.nLin = opt_.globalLin;
+    a.wSparse = ws.data();
+    a.wDenseDepth = wd.data();
+    a.wDenseColor = wc.data();
+    a.cache = wDense > 0.0f ? dGlobalCache_.p : nullptr;
+    a.cacheW = opt_.cacheWidth;
+    a.cacheH = opt_.cacheHeight;
+    std::memcpy(a.intrinsics, opt_.cacheIntrinsics, sizeof(a.intrinsics));
+    a.rot = dGlobalRot_.p;
+    a.trans = dGlobalTrans_.p;
+    a.rebuildJT = true;
+    a.findMaxResidual = true;
+    const uint32_t last = nk - 1;
+    if (comm_ && last < pairBound_.size()) a.pairBound = std::max(pairBound_[last], 1u);
+    BF_HIP(hipEventRecord(t0, baStream_));
+    global_->solve(a);
+    BF_HIP(hipEventRecord(t1, baStream_));
+    global_->removeMaxResidualAsync(globalCorr_, ncorr, dGlobalValid_.p, nk, opt_.maxResidualThresh);
+    global_->resultAsync(P.ctrl + Solver::kResultWords);
+    P.globalSolved = true;
+    poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
+    BF_HIP(hipMemcpyAsync(P.globalT, dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
+    BF_HIP(hipMemcpyAsync(P.valid, dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
+    BF_HIP(hipEventRecord(P.done, baStream_));
+}
+
+SolveResult Recon::endSolve(float wDense, float* ms) {
+    synchronize();  // every submap result applied: the ring is empty
+    const uint32_t S = opt_.submapSize;
+    BF_REQUIRE(numFrames_ > 0, BF_ERR_STATE, "end solve before the first frame");
+    const uint32_t last = (numFrames_ - 1) / S, nk = last + 1;
+    const uint32_t ncorr = (last < globalPrefix_.size()) ? globalPrefix_[last] : globalCorrN_;
+    SolveResult res{};
+    res.skipped = 1;
+    if (ms) *ms = 0.0f;
+    if (nk < 2 || !globalCorr_ || ncorr == 0) return res;
+    if (wDense > 0.0f) {
+        std::vector<BFCachedFrame> tab(nk);
+        for (uint32_t k = 0; k < nk; k++) {
+            tab[k] = frames_[k * S].cache;  // Bundler::fuseToGlobal keeps the submap's first frame
+            BF_REQUIRE(tab[k].depth, BF_ERR_STATE, "dense end solve: a keyframe has no cache frame");
+        }
+        BF_HIP(hipMemcpyAsync(dGlobalCache_.p, tab.data(), sizeof(BFCachedFrame) * nk, hipMemcpyHostToDevice, baStream_));
+        BF_HIP(hipStreamSynchronize(baStream_));
+    }
+    const uint32_t slot = ringNext_;
+    ringNext_ = (ringNext_ + 1) % RING;
+    Pending& P = ring_[slot];
+    P.submap = last;
+    P.numLocal = 0;
+    P.numKeyframes = nk;
+    P.localSolved = P.globalSolved = false;
+    P.endSolve = true;
+    *P.gate = 1;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    BF_HIP(hipEventCreate(&t0));
+    BF_HIP(hipEventCreate(&t1));
+    try {
+        baPost([this, slot, nk, ncorr, wDense, t0, t1]() { issueEndSolve(slot, nk, ncorr, wDense, t0, t1); });
+        P.job = lastJob_;
+        baWaitFor(P.job);
+        BF_HIP(hipEventSynchronize(P.done));
+        if (ms) BF_HIP(hipEventElapsedTime(ms, t0, t1));
+    } catch (...) {
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+        throw;
+    }
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    apply(P);
+    st_.endSolves++;
+    return Solver::decodeResult(P.ctrl + Solver::kResultWords);
+}
+
+void Recon::submapPoses(uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal, uint32_t* numKeyframes,
+                        int32_t* localValid) const {
+    BF_REQUIRE(opt_.recordOps, BF_ERR_STATE, "submap history needs recordOps");
+    BF_REQUIRE(s < history_.size() && !history_[s].local.empty(), BF_ERR_ARG, "no record of this submap");
+    const SubmapRecord& r = history_[s];
+    if (local) std::memcpy(local, r.local.data(), 64 * r.local.size());
+    if (global) std::memcpy(global, r.global.data(), 64 * r.global.size());
+    if (valid) std::memcpy(valid, r.valid.data(), 4 * r.valid.size());
+    if (numLocal) *numLocal = (uint32_t)r.local.size();
+    if (numKeyframes) *numKeyframes = (uint32_t)r.global.size();
+    if (localValid) *localValid = r.localOk;
 }
 
 void Recon::baPost(std::function<void()> job) {
@@ -516,10 +652,13 @@ void Recon::applyPending(bool block) {
 // updateTrajectoryCU (OnlineBundler.cu:73-110) + TrajectoryManager::updateOptimizedTransform
 void Recon::apply(Pending& P) {
     const uint32_t S = opt_.submapSize, s = P.submap, n = P.numLocal, nk = P.numKeyframes;
+    const bool localOk = *P.gate != 0;
     std::vector<BFMat4>& traj = localTraj_[s];
-    traj.resize(n);
-    std::memcpy(traj.data(), P.localT, 64 * n);
-    localKnown_[s] = 1;
+    if (!P.endSolve) {
+        traj.resize(n);
+        std::memcpy(traj.data(), P.localT, 64 * n);
+        localKnown_[s] = 1;
+    }
     std::memcpy(globalValid_.data(), P.valid, 4 * nk);
     for (uint32_t k = 0; k < nk; k++) {
         if (!globalValid_[k]) continue;
@@ -527,7 +666,9 @@ void Recon::apply(Pending& P) {
         kf_[k] = globalT_[k];
         kfSolved_[k] = 1;
     }
-    if (n == S + 1 && globalValid_[s]) {
+    // keyframe s+1 from the solver's seed; after an invalid local the reference copies keyframe s
+    // (initializeNextTransformUnknown), which the front end's dead reckoning here improves on
+    if (!P.endSolve && n == S + 1 && globalValid_[s] && localOk) {
         kf_[s + 1] = mat4_mul(globalT_[s], traj[S]);
         kfSolved_[s + 1] = 1;
     }
@@ -536,15 +677,30 @@ void Recon::apply(Pending& P) {
         st_.localSolves++;
         st_.localGnIterations += r.gnIterations;
         st_.localPcgIterations += r.pcgIterations;
+        if (r.verifyUsed) st_.localVerifications++;
     }
+    if (!P.endSolve && !localOk) st_.invalidLocals++;
     if (P.globalSolved) {
         const SolveResult r = Solver::decodeResult(P.ctrl + Solver::kResultWords);
-        st_.globalSolves++;
-        st_.globalGnIterations += r.gnIterations;
-        st_.globalPcgIterations += r.pcgIterations;
-        if (r.removedI != BF_INVALID_IMAGE) st_.removedPairs++;
+        if (!r.skipped) {
+            st_.globalSolves++;
+            st_.globalGnIterations += r.gnIterations;
+            st_.globalPcgIterations += r.pcgIterations;
+            if (r.removedI != BF_INVALID_IMAGE) st_.removedPairs++;
+        }
     }
-    const uint32_t optimized = std::min(S * s + std::min(n, S), numFrames_);
+    if (opt_.recordOps && !P.endSolve) {
+        if (history_.size() <= s) history_.resize(s + 1);
+        SubmapRecord& rec = history_[s];
+        rec.local = traj;
+        rec.global.resize(nk);
+        std::memcpy(rec.global.data(), P.globalT, 64 * nk);
+        rec.valid.assign(P.valid, P.valid + nk);
+        rec.localOk = localOk ? 1 : 0;
+    }
+    // frames of invalid keyframes (and of invalidated local submaps) get -inf transforms: the queue
+    // de-integrates them (invalidateImages + updateTrajectoryCU, OnlineBundler.cpp:317-320, 387-394)
+    const uint32_t optimized = P.endSolve ? numFrames_ : std::min(S * s + std::min(n, S), numFrames_);
     for (uint32_t g = 0; g < optimized; g++) {
         const uint32_t k = g / S;
         complete_[g] = (globalValid_[k] && localKnown_[k]) ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();

@@ -51,6 +51,11 @@ public:
     void finish();       // end of sequence: solve the last (partial) submap and wait for all results
     void reintegrate();  // one render-loop iteration without a new frame: apply results, fix ops, GC
     void synchronize();  // drain both streams and apply every pending bundling result
+    // one end-of-sequence global solve over every keyframe (dense depth weight wDense when > 0); waits
+    SolveResult endSolve(float wDense, float* ms);
+    // recordOps history: submap s's local trajectory and the keyframe poses after its global solve
+    void submapPoses(uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal, uint32_t* numKeyframes,
+                     int32_t* localValid) const;
 
     BFReconStats stats();
     void resetStats();
@@ -67,7 +72,9 @@ private:
         uint32_t submap = 0, numLocal = 0, numKeyframes = 0;
         uint64_t job = 0;  // bundling-thread job that enqueues this submap's work (see baPost)
         bool localSolved = false, globalSolved = false;
+        bool endSolve = false;      // an end-of-sequence global solve (no local part)
         hipEvent_t done = nullptr;
+        int* gate = nullptr;        // pinned: the submap's verification outcome (1 valid)
         float* localT = nullptr;    // pinned [S+1][16]
         float* globalT = nullptr;   // pinned [maxKeyframes][16]
         int* valid = nullptr;       // pinned [maxKeyframes]
@@ -78,6 +85,7 @@ private:
     void endSubmap(uint32_t s, uint32_t numFrames);
     void issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache, std::pair<BFEntryJ*, uint32_t> lc,
                      uint32_t nk);
+    void issueEndSolve(uint32_t slot, uint32_t nk, uint32_t ncorr, float wDense, hipEvent_t t0, hipEvent_t t1);
     void applyPending(bool block);
     void apply(Pending& p);
     void runReintegrate();
@@ -157,8 +165,16 @@ private:
     std::atomic<uint64_t> baDone_{0};  // jobs issued
     std::exception_ptr baErr_;
 
-    DevBuf<float> dLocalRot_, dLocalT_;  // dLocalRot_ holds [rot 3L | trans 3L] (one broadcast)
+    DevBuf<float> dLocalRot_, dLocalT_;  // dLocalRot_ holds [rot 3L | trans 3L | gate] (one broadcast)
     float* dLocalTrans_ = nullptr;
+    int* dGate_ = nullptr;               // the submap's verification outcome, read by the gated global solve
+    DevBuf<BFCachedFrame> dGlobalCache_; // keyframe k's cache frame (frame k * S), for the end-of-sequence dense solve
+    struct SubmapRecord {  // recordOps history
+        std::vector<BFMat4> local, global;
+        std::vector<int> valid;
+        int localOk = 1;
+    };
+    std::vector<SubmapRecord> history_;
     DevBuf<int> dLocalValid_;
     DevBuf<BFCachedFrame> dLocalCache_;
     DevBuf<float> dGlobalRot_, dGlobalTrans_, dGlobalT_;

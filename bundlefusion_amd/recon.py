@@ -8,7 +8,7 @@ import ctypes as C
 import numpy as np
 
 from . import check, lib
-from .abi import BFFixOp, BFReconOptions, BFReconStats, BFTsdfStats
+from .abi import BFFixOp, BFReconOptions, BFReconStats, BFSolveResult, BFTsdfStats
 
 FIX_DEINTEGRATE, FIX_INTEGRATE, FIX_REINTEGRATE, OP_GC = 1, 2, 3, 4
 
@@ -124,6 +124,25 @@ class Recon:
 
     def reintegrate(self):
         check(lib().bf_recon_reintegrate(self.h))
+
+    def end_solve(self, dense_depth_weight: float = 0.0):
+        """One end-of-sequence global solve (OnlineBundler.cpp:171-197, 373-398); 15 = the
+        USE_GLOBAL_DENSE_AT_END solve. Returns (result dict, device ms)."""
+        r = BFSolveResult()
+        ms = C.c_float()
+        check(lib().bf_recon_end_solve(self.h, C.c_float(dense_depth_weight), C.byref(r), C.byref(ms)))
+        return {k: getattr(r, k) for k, _ in BFSolveResult._fields_}, ms.value
+
+    def submap_poses(self, s: int, max_keyframes: int, submap_size: int = 10):
+        """recordOps history of submap s: (local float32[n,4,4], global float32[k,4,4], valid int32[k], local_ok)."""
+        loc = np.zeros((submap_size + 1, 4, 4), np.float32)
+        glo = np.zeros((max_keyframes, 4, 4), np.float32)
+        val = np.zeros(max_keyframes, np.int32)
+        nl, nk, ok = C.c_uint32(), C.c_uint32(), C.c_int32()
+        check(lib().bf_recon_submap_poses(self.h, C.c_uint32(s), loc.ctypes.data_as(C.c_void_p),
+                                          glo.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p), C.byref(nl),
+                                          C.byref(nk), C.byref(ok)))
+        return loc[:nl.value], glo[:nk.value], val[:nk.value], bool(ok.value)
 
     def synchronize(self):
         check(lib().bf_recon_synchronize(self.h))

@@ -7,7 +7,7 @@ import ctypes as C
 import numpy as np
 
 from . import DeviceArray, abi, check, lib
-from .abi import ENTRYJ_DTYPE, BFCachedFrame, BFSolveResult, BFSolverOptions
+from .abi import ENTRYJ_DTYPE, BFCachedFrame, BFSolveResult, BFSolverOptions, BFVerifyOptions
 
 # SBA weight schedules (Source/SBA.cpp:28-39), indexed by GN iteration
 LOCAL_WEIGHTS = dict(sparse=[1.0, 1.0, 1.0], dense_depth=[1.0, 2.0, 3.0], dense_color=[0.0, 0.0, 0.0])
@@ -61,6 +61,22 @@ class SolverBundling:
 
     def synchronize(self):
         check(lib().bf_solver_synchronize(self.h))
+
+    def verify_trajectory(self, T: DeviceArray, valid: DeviceArray, n_images: int, n_corr: int, cache: DeviceArray,
+                          cache_w: int, cache_h: int, intrinsics, always=False, pair_stats: DeviceArray | None = None,
+                          **thresholds) -> bool:
+        """useVerification + VerifyTrajectoryCU after the last solve (CUDASolverBundling.cpp:454-476,
+        Bundler.cpp:259-274): True when the submap is accepted."""
+        o = BFVerifyOptions()
+        for k, v in thresholds.items():
+            setattr(o, k, v)
+        o.always = int(always)
+        intr = (C.c_float * 4)(*[float(x) for x in intrinsics])
+        ok = C.c_int()
+        check(lib().bf_solver_verify_trajectory(self.h, T.ptr, valid.ptr, C.c_uint32(n_images), C.c_uint32(n_corr),
+                                                cache.ptr, C.c_uint32(cache_w), C.c_uint32(cache_h), intr, C.byref(o),
+                                                pair_stats.ptr if pair_stats is not None else None, C.byref(ok)))
+        return bool(ok.value)
 
     def set_shard(self, count: int, index: int, comm=None):
         """Build only the pair blocks p % count == index; comm (bundlefusion_amd.dist.Comm) sums them."""

@@ -179,6 +179,29 @@ int bf_solver_invalidate_image_pair(bf_solver* s, BFEntryJ* corr, uint32_t nCorr
 int bf_solver_check_invalid_frames(bf_solver* s, int* valid, uint32_t nImages, BFEntryJ* corr, uint32_t nCorr,
                                    int comprehensive);
 
+/* Local-submap verification after a solve (SBA::align, SBA.cpp:106-109):
+ * CUDASolverBundling::useVerification (Solver/CUDASolverBundling.cpp:454-476) — the dense check runs only
+ * when >= percentThresh of the last solve's nCorr correspondences kept a max-norm residual above
+ * verifyOptDistThresh (the solve must have run with findMaxResidual, which counts them) or when
+ * `always` is set — then SIFTImageManager::VerifyTrajectoryCU (SiftGPU/SIFTImageManager.cu:1036-1159) over
+ * every valid image pair i < j of the trajectory T (DEVICE float4x4[nImages], camera -> world) with the
+ * cache frames (DEVICE BFCachedFrame[nImages]). Fields left 0 take the defaults of
+ * zParametersBundlingDefault.txt:55-64 / Bundler.cpp:267. *valid (may be NULL; synchronizes) = 1 when the
+ * submap is accepted; pairStats (DEVICE float[nImages^2 * 3] or NULL) receives {sum residual, sum
+ * weight, #correspondences} per pair (i * nImages + j). The outcome is also in bf_solver_result. */
+typedef struct BFVerifyOptions {
+    float projCorrDistThresh;      /* s_projCorrDistThres = 0.15 */
+    float projCorrNormalThresh;    /* s_projCorrNormalThres = 0.97 */
+    float verifyOptErrThresh;      /* s_verifyOptErrThresh = 0.05 */
+    float verifyOptCorrThresh;     /* s_verifyOptCorrThresh = 0.001 */
+    float verifyOptPercentThresh;  /* m_verifyOptPercentThresh = 0.05 (CUDASolverBundling.cpp:36) */
+    float sensorDepthMin, sensorDepthMax;  /* 0.1 / 3.0 (Bundler.cpp:267) */
+    int32_t always;                /* 1: skip useVerification, check every pair */
+} BFVerifyOptions;
+int bf_solver_verify_trajectory(bf_solver* s, const float* T, const int* valid, uint32_t nImages, uint32_t nCorr,
+                                const BFCachedFrame* cache, uint32_t cacheW, uint32_t cacheH, const float intrinsics[4],
+                                const BFVerifyOptions* opts, float* pairStats, int* validOut);
+
 /* ---- multi-GPU: RCCL communicator for the global normal equations ----------
  * One process per GPU. Rank 0 draws the id (bf_comm_unique_id), the host hands it to every rank,
  * every rank calls bf_comm_create (collective). A sharded solver builds the normal-equation blocks
@@ -235,12 +258,6 @@ int bf_synth_cache_frame(const BFSynthScene* scene, const float T[16], const BFD
  * TrajectoryManager (TrajectoryManager.cpp:8-200) and the OnlineBundler local->global
  * hierarchy (OnlineBundler.cpp:242-416). Frames are borrowed device pointers that must stay
  * resident (the CUDAImageManager frame store); correspondences are EntryJ inputs. */
-typedef struct BFFixOp {
-    int32_t kind;     /* 1 de-integrate (oldT), 2 integrate (newT), 3 re-integrate (oldT -> newT) */
-    uint32_t frame;
-    float oldT[16];
-    float newT[16];
-} BFFixOp;
 
 typedef struct BFReconOptions {
     uint32_t maxFrames;          /* frame-store / trajectory capacity */
@@ -263,6 +280,10 @@ typedef struct BFReconOptions {
                                     by the frame loop when ready (the reference's bundling thread);
                                     0: the loop waits for each submap's solves (deterministic) */
     BFSolverOptions solver;
+    int32_t disableLocalVerify;  /* 0: s_useLocalVerify = true (zParametersBundlingDefault.txt:62): after each local
+                                    solve useVerification + VerifyTrajectoryCU; a failing submap is invalidated
+                                    (OnlineBundler.cpp:145-159, 255-261, 351-360, 399-405) */
+    BFVerifyOptions verify;      /* its thresholds (0 = defaults) */
 } BFReconOptions;
 
 typedef struct BFReconStats {
@@ -279,6 +300,9 @@ typedef struct BFReconStats {
     double localSolveMs, globalSolveMs;  /* summed device time of the solves */
     uint64_t reintegrateLaunches;  /* timed k_reintegrate launches (fused de-/re-integration) */
     double reintegrateKernelMs;
+    uint64_t localVerifications; /* local solves whose dense verification ran (useVerification) */
+    uint64_t invalidLocals;      /* local submaps invalidated by it */
+    uint64_t endSolves;          /* end-of-sequence global solves (bf_recon_end_solve) */
 } BFReconStats;
 
 typedef struct bf_recon bf_recon;
@@ -297,6 +321,19 @@ int bf_recon_set_global_correspondences(bf_recon* r, BFEntryJ* corr, uint32_t n,
 int bf_recon_set_initial_pose(bf_recon* r, const float T0[16]);
 int bf_recon_process_frame(bf_recon* r, uint32_t f);
 int bf_recon_finish(bf_recon* r);
+/* One end-of-sequence global solve (OnlineBundler::processInput past the last frame, OnlineBundler.cpp:171-197,
+ * then optimizeGlobal with isSequenceDone, :373-398): all keyframes, every global correspondence, max-residual
+ * removal; the reference's bundling thread runs s_numSolveFramesBeforeExit (30) of them and, with
+ * USE_GLOBAL_DENSE_AT_END (GlobalBundlingState.h:9), the last with dense depth weight 15 (:177-189) — pass
+ * denseDepthWeight 15 for that one (0: sparse only). The dense term reads each keyframe's cache frame (the
+ * submap's first frame, Bundler::fuseToGlobal's copy). Waits for the solve; the new poses go to the
+ * trajectory (the queue picks them up). out / ms (device time) may be NULL. */
+int bf_recon_end_solve(bf_recon* r, float denseDepthWeight, BFSolveResult* out, float* ms);
+/* with recordOps: submap s's local trajectory (HOST float[16 * (submapSize + 1)]) and the global keyframe poses
+ * and valid flags after its global solve (HOST float[16 * maxKeyframes], int[maxKeyframes]); *numLocal /
+ * *numKeyframes = entries written, *localValid = its verification outcome. Any output may be NULL. */
+int bf_recon_submap_poses(bf_recon* r, uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal,
+                          uint32_t* numKeyframes, int32_t* localValid);
 /* a loop iteration without a new frame (the reference keeps calling reintegrate() from its render
  * loop after scanning ends): pick up results, run up to maxFrameFixes queue ops, GC */
 int bf_recon_reintegrate(bf_recon* r);
@@ -400,8 +437,8 @@ int bf_mesh_save_ply(const char* path, const BFMcTriangle* tris, uint32_t n, con
                      uint32_t* numVertices, uint32_t* numFaces);
 
 /* .sens reader (mLib SensorData v4 as SensorDataReader.cpp:38-116 uses it; format restated in
- * SURVEY.md Appendix B). Frames are read on demand. Depth: raw or zlib ushort; colour: raw RGB
- * (png / jpeg and occi return BF_ERR_ARG: no decoder in this build). */
+ * SURVEY.md Appendix B). Frames are read on demand. Depth: raw or zlib ushort; colour: raw RGB, PNG or
+ * baseline/progressive JPEG (bf_image_decode); occi depth returns BF_ERR_ARG. */
 typedef struct bf_sens bf_sens;
 int bf_sens_open(const char* path, bf_sens** out);
 int bf_sens_close(bf_sens* s);

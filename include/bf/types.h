@@ -115,6 +115,15 @@ typedef struct BFCachedFrame {
     const float* intensityDeriv; /* d_intensityDerivsDownsampled, float2 per pixel */
 } BFCachedFrame;
 
+/* One scene call of the re-integration queue / reconstruction loop log (reintegrate(),
+ * DepthSensing.cpp:854-902). */
+typedef struct BFFixOp {
+    int32_t kind;     /* 1 de-integrate (oldT), 2 integrate (newT), 3 re-integrate (oldT -> newT) */
+    uint32_t frame;
+    float oldT[16];
+    float newT[16];
+} BFFixOp;
+
 /* Outcome of one bundle-adjustment solve (CUDASolverBundling::solve + computeMaxResidual). */
 typedef struct BFSolveResult {
     uint32_t gnIterations;       /* Gauss-Newton iterations executed (early exit at max|delta| < 0.005) */
@@ -125,6 +134,9 @@ typedef struct BFSolveResult {
     uint32_t highResidualCount;  /* correspondences with max residual > verifyOptDistThresh */
     uint32_t numDensePairs;      /* overlapping image pairs found by the dense term (last GN iter) */
     uint32_t error;              /* bit 1: a row exceeded the sort capacity */
+    uint32_t skipped;            /* the solve was gated off (an invalidated local submap's global solve) */
+    uint32_t verifyUsed;         /* the last verification ran its dense pair check (useVerification) */
+    uint32_t verifyOk;           /* ... and passed (VerifyTrajectoryCU's d_validOpt) */
 } BFSolveResult;
 
 /* Device-side counters used by the bench to compute algorithmic bytes. */

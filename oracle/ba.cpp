@@ -599,4 +599,103 @@ void or_ba_dense_system(const int* validImages, const ORSolveParams* p, const fl
     if (pairsOut) *pairsOut = S.densePairs;
 }
 
+uint32_t or_ba_count_high_residuals(const BFEntryJ* corr, uint32_t n, const float* rot, const float* trans, float w,
+                                    float thresh) {
+    uint32_t cnt = 0;
+    for (uint32_t c = 0; c < n; c++) {
+        const BFEntryJ& e = corr[c];
+        if (e.imgIdx_i == BF_INVALID_IMAGE) continue;
+        const m4 TI = poseToMatrix(ld3(rot + 3 * e.imgIdx_i), ld3(trans + 3 * e.imgIdx_i));
+        const m4 TJ = poseToMatrix(ld3(rot + 3 * e.imgIdx_j), ld3(trans + 3 * e.imgIdx_j));
+        const f3 d = w * fabs3(xform(TI, ld3(e.pos_i)) - xform(TJ, ld3(e.pos_j)));
+        if (std::max(d.z, std::max(d.x, d.y)) > thresh) cnt++;
+    }
+    return cnt;
+}
+
+// VerifyTrajectoryCU_Kernel (SiftGPU/SIFTImageManager.cu:1036-1127) / computeProjError (:418-487)
+int or_verify_trajectory(const int* valid, const float* Tall, const BFCachedFrame* cache, const ORVerifyParams* p,
+                         float* pairStats) {
+    const uint32_t N = p->numImages, W = p->width, H = p->height;
+    if (N < 2) return 0;  // VerifyTrajectoryCU: numImages < 2 -> 0
+    m4 K{};
+    for (float& x : K.e) x = 0.0f;
+    K.e[0] = p->intrinsics[0]; K.e[2] = p->intrinsics[2]; K.e[5] = p->intrinsics[1]; K.e[6] = p->intrinsics[3];
+    K.e[10] = 1.0f; K.e[15] = 1.0f;
+    auto mv4 = [](const m4& m, const float* v, float* o) {  // float4x4 * float4 (cuda_SimpleMatrixUtil.h:925-933)
+        const float* e = m.e;
+        for (int r = 0; r < 4; r++) o[r] = e[4 * r] * v[0] + e[4 * r + 1] * v[1] + e[4 * r + 2] * v[2] + e[4 * r + 3] * v[3];
+    };
+    auto projErr = [&](uint32_t idx, const m4& tr, const BFCachedFrame& in, const BFCachedFrame& model, float out[3]) {
+        out[0] = out[1] = out[2] = 0.0f;
+        const float* pIn = in.campos + 4 * (size_t)idx;
+        float nIn[4] = {in.normals[4 * idx], in.normals[4 * idx + 1], in.normals[4 * idx + 2], 0.0f};
+        const float dIn = in.depth[idx];
+        if (!(pIn[0] != MINF && nIn[0] != MINF && dIn >= p->depthMin && dIn <= p->depthMax)) return;
+        float pT[4], nT[4];
+        mv4(tr, pIn, pT);
+        mv4(tr, nIn, nT);
+        const f3 q = xform(K, f3{pT[0], pT[1], pT[2]});
+        const int sx = f2i(std::round(q.x / q.z)), sy = f2i(std::round(q.y / q.z));
+        if (!(sx >= 0 && sy >= 0 && sx < (int)W && sy < (int)H)) return;
+        const size_t t = (size_t)sy * W + (size_t)sx;
+        const float* pTg = model.campos + 4 * t;
+        const float* nTg = model.normals + 4 * t;
+        if (!(pTg[0] != MINF && nTg[0] != MINF)) return;
+        const float dx = pT[0] - pTg[0], dy = pT[1] - pTg[1], dz = pT[2] - pTg[2], dw = pT[3] - pTg[3];
+        const float d = std::sqrt(dx * dx + dy * dy + dz * dz + dw * dw);
+        const float dN = nT[0] * nTg[0] + nT[1] * nTg[1] + nT[2] * nTg[2];
+        const float tgtDepth = model.depth[t];
+        if (!(tgtDepth >= p->depthMin && tgtDepth <= p->depthMax)) return;
+        const bool bad = (tgtDepth != MINF && pT[2] < tgtDepth) && d > p->distThresh;
+        if (!((dN >= p->normalThresh && d <= p->distThresh) || bad)) return;
+        const float camZ = (pT[2] - p->depthMin) / (p->depthMax - p->depthMin);
+        out[0] = d;
+        out[1] = std::max(0.0f, 0.5f * ((1.0f - d / p->distThresh) + (1.0f - camZ)));
+        out[2] = 1.0f;
+    };
+    int ok = 1;
+    constexpr uint32_t WGS = 256;
+    std::vector<float> part(3 * WGS);
+    for (uint32_t i = 0; i < N; i++)
+        for (uint32_t j = i + 1; j < N; j++) {
+            if (valid[i] == 0 || valid[j] == 0) continue;
+            m4 Ti, Tj;
+            std::memcpy(Ti.e, Tall + 16 * (size_t)i, 64);
+            std::memcpy(Tj.e, Tall + 16 * (size_t)j, 64);
+            const m4 tr = matmul(inverse(Tj), Ti);  // d_trajectory[img1].getInverse() * d_trajectory[img0]
+            const m4 trInv = inverse(tr);
+            for (uint32_t t = 0; t < WGS; t++) {
+                float sr = 0, sw = 0, sn = 0;
+                for (uint32_t idx = t; idx < W * H; idx += WGS) {
+                    float a[3], b[3];
+                    projErr(idx, tr, cache[i], cache[j], a);
+                    projErr(idx, trInv, cache[j], cache[i], b);
+                    sr += a[0] + b[0];
+                    sw += a[1] + b[1];
+                    sn += a[2] + b[2];
+                }
+                part[3 * t] = sr; part[3 * t + 1] = sw; part[3 * t + 2] = sn;
+            }
+            float s[3];
+            for (int q = 0; q < 3; q++) {
+                float wv[4];
+                for (uint32_t w = 0; w < 4; w++) {  // shfl_down tree: lane 0 of each wave
+                    float v[64];
+                    for (int l = 0; l < 64; l++) v[l] = part[3 * (64 * w + l) + q];
+                    for (int off = 32; off > 0; off >>= 1)
+                        for (int l = 0; l < off; l++) v[l] += v[l + off];
+                    wv[w] = v[0];
+                }
+                s[q] = ((wv[0] + wv[1]) + wv[2]) + wv[3];
+            }
+            if (pairStats)
+                for (int q = 0; q < 3; q++) pairStats[((size_t)i * N + j) * 3 + q] = s[q];
+            const float err = s[0] / s[1];
+            const float corr = 0.5f * s[2] / (float)(W * H);
+            if (corr < p->corrThresh || err > p->errThresh || std::isnan(err)) ok = 0;
+        }
+    return ok;
+}
+
 }  // extern "C"

@@ -105,6 +105,22 @@ void or_ba_solve(BFEntryJ* corr, const int* validImages, const ORSolveParams* p,
 void or_ba_dense_system(const int* validImages, const ORSolveParams* p, const float* rot, const float* trans,
                         float* jtjOut, float* jtrOut, double* energyOut, uint32_t* pairsOut);
 
+/* CountHighResidualsDevice (SolverBundling.cu:657-687) at poses rot/trans with weight w: correspondences
+ * whose evalAbsMaxResidualDevice (SolverBundlingEquationsLie.h:27-40) exceeds thresh */
+uint32_t or_ba_count_high_residuals(const BFEntryJ* corr, uint32_t n, const float* rot, const float* trans, float w,
+                                    float thresh);
+/* VerifyTrajectoryCU (SiftGPU/SIFTImageManager.cu:1036-1159) with computeProjError's float-normal branch
+ * (:418-487): T = camera->world float4x4[numImages] (host), cache = host frames; returns 1 (valid) / 0.
+ * Sums in the order of the gfx950 kernel (thread t of 256 takes pixels t, t+256, ...; a tree per 64
+ * threads; the 4 partials in order). pairStats (may be NULL): float[numImages^2 * 3]. */
+typedef struct ORVerifyParams {
+    uint32_t numImages, width, height;
+    float intrinsics[4];
+    float distThresh, normalThresh, errThresh, corrThresh, depthMin, depthMax;
+} ORVerifyParams;
+int or_verify_trajectory(const int* valid, const float* T, const BFCachedFrame* cache, const ORVerifyParams* p,
+                         float* pairStats);
+
 /* TrajectoryManager + reintegrate() list logic (traj.cpp) */
 void or_pose_helper_matrix_to_pose(const float* T, float out[6]);
 void* or_traj_create(unsigned maxFrames, unsigned topN, float minDist);
@@ -113,6 +129,46 @@ void or_traj_add_frame(void* h, int type, const float* T, unsigned idx);
 void or_traj_update_optimized(void* h, const float* T, unsigned numFrames);
 unsigned or_traj_next_fixes(void* h, unsigned maxFixes, int* kinds, unsigned* frames, float* oldT, float* newT);
 void or_traj_frame_info(void* h, unsigned idx, int* type, float* dist);
+
+void or_traj_integrated(void* h, unsigned idx, float* T);
+
+/* ---- bundling side of the reconstruction loop (recon.cpp): OnlineBundler local -> global state
+ * machine + TrajectoryManager, in the order of the product's synchronous mode ----------------- */
+typedef struct ORReconParams {
+    uint32_t maxFrames, submapSize, maxFrameFixes, topNActive;
+    float minPoseDistSqrt;
+    uint32_t localNonLin, localLin, globalNonLin, globalLin;
+    uint32_t maxKeyframes;
+    uint32_t maxCorrPerImageLocal, maxCorrPerImageGlobal;  /* clamp(maxCorr / maxImages, 1000, 4000) */
+    float maxResidualThresh;
+    int32_t useLocalDense;
+    uint32_t cacheWidth, cacheHeight;
+    float cacheIntrinsics[4];
+    uint32_t disableEarlyOut;
+    int32_t disableLocalVerify;
+    float verifyOptDistThresh, verifyOptPercentThresh;
+    float projCorrDistThresh, projCorrNormalThresh, verifyOptErrThresh, verifyOptCorrThresh;
+} ORReconParams;
+typedef struct ORReconStats {
+    uint64_t localSolves, globalSolves, localPcgIterations, globalPcgIterations, removedPairs;
+    uint64_t localVerifications, invalidLocals, endSolves;
+} ORReconStats;
+typedef struct ORRecon ORRecon;
+ORRecon* or_recon_create(const ORReconParams* p, const float T0[16]);
+void or_recon_destroy(ORRecon* r);
+/* cache: HOST BFCachedFrame of host pointers (or NULL) */
+void or_recon_set_frame(ORRecon* r, uint32_t f, const float Tinc[16], const BFCachedFrame* cache);
+void or_recon_set_local_corr(ORRecon* r, uint32_t s, const BFEntryJ* corr, uint32_t n);
+void or_recon_set_global_corr(ORRecon* r, const BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes);
+void or_recon_process_frame(ORRecon* r, uint32_t f);
+void or_recon_finish(ORRecon* r);
+void or_recon_reintegrate(ORRecon* r);
+void or_recon_end_solve(ORRecon* r, float denseDepthWeight);
+uint32_t or_recon_op_log(const ORRecon* r, BFFixOp* out, uint32_t cap);
+int or_recon_submap_poses(const ORRecon* r, uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal,
+                          uint32_t* numKeyframes, int32_t* localValid);
+void or_recon_trajectory(const ORRecon* r, float* T, uint32_t n);
+void or_recon_stats(const ORRecon* r, ORReconStats* out);
 
 /* ---- input preprocessing (CUDAImageManager::process) ---------------------- */
 void or_preprocess(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh,

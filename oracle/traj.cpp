@@ -271,6 +271,10 @@ unsigned or_traj_next_fixes(void* h, unsigned maxFixes, int* kinds, unsigned* fr
     return n;
 }
 
+void or_traj_integrated(void* h, unsigned idx, float* T) {
+    std::memcpy(T, static_cast<TM*>(h)->frames[idx].integrated, 64);
+}
+
 void or_traj_frame_info(void* h, unsigned idx, int* type, float* dist) {
     TM* tm = static_cast<TM*>(h);
     *type = tm->frames[idx].type;

@@ -126,6 +126,41 @@ def dense_system(valid, rot, trans, cache, intrinsics, w_depth=1.0, w_color=0.0,
     return jtj, jtr, e.value, npairs.value
 
 
+class ORVerifyParams(C.Structure):
+    _fields_ = [("numImages", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32), ("intrinsics", C.c_float * 4),
+                ("distThresh", C.c_float), ("normalThresh", C.c_float), ("errThresh", C.c_float),
+                ("corrThresh", C.c_float), ("depthMin", C.c_float), ("depthMax", C.c_float)]
+
+
+def verify_trajectory(valid, T, cache: dict, intrinsics, dist=0.15, normal=0.97, err=0.05, corr=0.001, dmin=0.1, dmax=3.0):
+    """Oracle VerifyTrajectoryCU: (valid flag, pair stats float32[N, N, 3])."""
+    valid = np.ascontiguousarray(valid, np.int32)
+    N = valid.shape[0]
+    T = np.ascontiguousarray(np.asarray(T, np.float32).reshape(N, 16))
+    keep = []
+    p = _params(N, 0, 1, 1, [1.0], None, None, cache, intrinsics, 4000, None, keep)
+    v = ORVerifyParams()
+    v.numImages, v.width, v.height = N, p.cacheW, p.cacheH
+    v.intrinsics[:] = [float(x) for x in intrinsics]
+    v.distThresh, v.normalThresh, v.errThresh, v.corrThresh, v.depthMin, v.depthMax = dist, normal, err, corr, dmin, dmax
+    stats = np.zeros((N, N, 3), np.float32)
+    L = _lib()
+    L.or_verify_trajectory.argtypes = [C.c_void_p] * 5
+    L.or_verify_trajectory.restype = C.c_int
+    ok = L.or_verify_trajectory(valid.ctypes.data, T.ctypes.data, p.cache, C.addressof(v), stats.ctypes.data)
+    return bool(ok), stats
+
+
+def count_high_residuals(corr: np.ndarray, rot, trans, w=1.0, thresh=0.02) -> int:
+    corr = np.ascontiguousarray(corr)
+    rot = np.ascontiguousarray(rot, np.float32)
+    trans = np.ascontiguousarray(trans, np.float32)
+    L = _lib()
+    L.or_ba_count_high_residuals.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_float, C.c_float]
+    L.or_ba_count_high_residuals.restype = C.c_uint32
+    return int(L.or_ba_count_high_residuals(corr.ctypes.data, len(corr), rot.ctypes.data, trans.ctypes.data, w, thresh))
+
+
 def rotation_angle(R1: np.ndarray, R2: np.ndarray) -> float:
     c = (np.trace(R1[:3, :3].T @ R2[:3, :3]) - 1.0) / 2.0
     return float(np.arccos(np.clip(c, -1.0, 1.0)))

@@ -140,3 +140,39 @@ def test_dense_plus_sparse_local_solve():
                                [1000, 1000, 1000], [0, 0, 0], cache=prob["cache"], intrinsics=prob["intrinsics"])
     er, et = pose_errors(rot, trans, prob["gt"])
     assert er < 3e-3 and et < 5e-3, (er, et)
+
+
+def test_oracle_verify_trajectory_known_answers():
+    """VerifyTrajectoryCU restated (SIFTImageManager.cu:1036-1127): the ground-truth trajectory of an
+    11-frame submap passes with every pair overlapping; one frame moved by 6 deg / 8 cm fails."""
+    from oracle_ba import verify_trajectory
+    prob = make_problem(K=11, stride=1, outliers=0.0, with_cache=True, max_per_pair=10, drift=(0.2, 0.004))
+    ok, st = verify_trajectory(prob["valid"], prob["gt"], prob["cache"], prob["intrinsics"])
+    iu = np.triu_indices(11, 1)
+    assert ok and np.all(st[iu][:, 2] > 0)
+    err = st[iu][:, 0] / st[iu][:, 1]
+    assert np.all(err < 0.05)
+    T = prob["gt"].copy()
+    D = np.eye(4)
+    D[:3, :3] = rodrigues(np.array([0.3, -0.8, 0.5]) / np.linalg.norm([0.3, -0.8, 0.5]) * np.deg2rad(6.0))
+    D[:3, 3] = [0.08, -0.08, 0.04]
+    T[6] = (T[6].astype(np.float64) @ D).astype(np.float32)
+    ok2, st2 = verify_trajectory(prob["valid"], T, prob["cache"], prob["intrinsics"])
+    assert not ok2
+    # pairs without frame 6 are unchanged
+    for i, j in zip(*iu):
+        if 6 not in (i, j):
+            np.testing.assert_array_equal(st2[i, j], st[i, j])
+
+
+def test_oracle_count_high_residuals():
+    from oracle_ba import count_high_residuals
+    prob = make_problem(K=6, outliers=0.3, max_per_pair=20)
+    gt_rot = np.zeros((6, 3), np.float32)
+    gt_trans = np.zeros((6, 3), np.float32)
+    for k in range(6):
+        gt_rot[k], gt_trans[k] = matrix_to_pose(prob["gt"][k])
+    n = count_high_residuals(prob["corr"], gt_rot, gt_trans, 1.0, 0.02)
+    # at the ground truth only the 0.1-0.3 m outliers exceed 2 cm
+    assert 0.2 * len(prob["corr"]) < n < 0.4 * len(prob["corr"])
+    assert count_high_residuals(prob["corr"], gt_rot, gt_trans, 1.0, 1.0) == 0
