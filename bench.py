@@ -426,6 +426,13 @@ def main():
                  "heap_free": rc.heap_free_count(),
                  "allocated_blocks_scanned_per_compactify": ss["scanned"] / max(1, ss["integrateOps"])},
     }
+    # multi-GPU TSDF sharding: how evenly 1 m chunk ownership spreads the final
+    # scene's blocks and the timed frames' in-frustum blocks over G = 2 / 4 / 8 ranks (host mirror)
+    if world == 1:
+        from bundlefusion_amd.dist import shard_balance
+        blk = rc.export_blocks()
+        blk = blk[blk[:, 3] != 0]
+        out["shard_balance"] = shard_balance(blk[:, :3], args.voxel, stream.gt[fill:frames_total:10], stream.cam)
     # raycast (visualizeFrame's render, reported beside the metric): 20 renders from the last pose
     W_, H_ = args.width, args.height
     rpr = bfa.raycast_params(W_, H_, fx=stream.cam.fx, fy=stream.cam.fy)

@@ -327,6 +327,12 @@ int bf_scene_export(bf_scene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* he
     s->scene->exportState(hash, heap, heapCounter, voxels);
     BF_CATCH
 }
+int bf_scene_export_blocks(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(s && n && (out4 || cap == 0), BF_ERR_ARG, "null argument");
+    *n = s->scene->exportBlocks(reinterpret_cast<int4*>(out4), cap);
+    BF_CATCH
+}
 int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n) {
     BF_TRY
     BF_REQUIRE(s && out4 && n, BF_ERR_ARG, "null argument");
@@ -748,6 +754,13 @@ int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* he
     BF_REQUIRE(r, BF_ERR_ARG, "null recon");
     r->r->synchronize();
     r->r->scene().exportState(hash, heap, heapCounter, voxels);
+    BF_CATCH
+}
+int bf_recon_export_blocks(bf_recon* r, int32_t* out4, uint32_t cap, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(r && n && (out4 || cap == 0), BF_ERR_ARG, "null argument");
+    r->r->synchronize();
+    *n = r->r->scene().exportBlocks(reinterpret_cast<int4*>(out4), cap);
     BF_CATCH
 }
 int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, float* depth, float* depth4, float* normals,

@@ -800,6 +800,36 @@ __device__ __forceinline__ void voxel_deintegrate(float& s0, float& w0, uint32_t
     if (w0 <= 0.001f) { s0 = 0.0f; col = 0u; w0 = 0.0f; }
 }
 
+// The running-average quotient num / den of the voxel update, den = an integral weight in [0, 1024]:
+// rcp, product, one fma residual and one fma correction. Checked bit-identical to the IEEE division
+// for every float numerator in [2^-100, 2^100] (both signs) and every divisor 1..1024 on the GPU (the
+// update's numerators are 0 or far above 2^-100: sdf and s0 * w0 are multiples of ~1e-9 m); den = 0
+// only when a de-integration empties the voxel, whose sdf is then reset to 0.
+__device__ __forceinline__ float div_weight(float num, float den) {
+    const float r = __builtin_amdgcn_rcpf(den);
+    const float q = num * r;
+    const float e = __builtin_fmaf(-q, den, num);
+    return __builtin_fmaf(e, r, q);
+}
+__device__ __forceinline__ void voxel_integrate_f(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
+    col = blend_color(c, col, w0 == 0.0f);
+    s0 = div_weight(sdf * 1.0f + s0 * w0, 1.0f + w0);
+    w0 = fminf(weightMax, 1.0f + w0);
+}
+__device__ __forceinline__ void voxel_deintegrate_f(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c) {
+    const float wUpd = 1.0f;
+    const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
+    const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
+    const float den = w0 - wUpd, rden = __builtin_amdgcn_rcpf(den);
+    float r0 = fmaxf(0.0f, fminf(round_quot(oc0 * w0 - cu0 * wUpd, den, rden), 254.5f));
+    float r1 = fmaxf(0.0f, fminf(round_quot(oc1 * w0 - cu1 * wUpd, den, rden), 254.5f));
+    float r2 = fmaxf(0.0f, fminf(round_quot(oc2 * w0 - cu2 * wUpd, den, rden), 254.5f));
+    col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+    s0 = div_weight(s0 * w0 - sdf * wUpd, den);
+    w0 = fmaxf(0.0f, w0 - wUpd);
+    if (w0 <= 0.001f) { s0 = 0.0f; col = 0u; w0 = 0.0f; }
+}
+
 // Two voxels of one lane column, (x, y, z) and (x, y, z + 1), projected together: every float
 // operation is the scalar path's (xform's ((e0 x + e1 y) + e2 z) + e3, then fx * x, the rcp quotient,
 // + m, + 0.5), done elementwise on 2-wide vectors so that it issues as packed-FP32 instructions
@@ -816,15 +846,13 @@ __device__ __forceinline__ int proj_fix(float num, float den, float qa, float m,
     }
     return f2i(t);
 }
-__device__ __forceinline__ void voxel_pixel2(const BFDepthCameraParams& cam, const BFMat4& T, float wx, float wy, f2v wz,
-                                             bool haveColor, uint32_t& pix0, uint32_t& pix1, f2v& pz) {
+// b_r = e[4r] wx + e[4r+1] wy: the (x, y) part of every row, computed once per lane column and op
+__device__ __forceinline__ void voxel_pixel2b(const BFDepthCameraParams& cam, const BFMat4& T, const float* b, f2v wz,
+                                              bool haveColor, uint32_t& pix0, uint32_t& pix1, f2v& pz) {
     const float* e = T.m;
     f2v p[3];
 #pragma unroll
-    for (int r = 0; r < 3; r++) {
-        const float b = e[4 * r] * wx + e[4 * r + 1] * wy;
-        p[r] = (f2v{b, b} + f2v{e[4 * r + 2], e[4 * r + 2]} * wz) + f2v{e[4 * r + 3], e[4 * r + 3]};
-    }
+    for (int r = 0; r < 3; r++) p[r] = (f2v{b[r], b[r]} + f2v{e[4 * r + 2], e[4 * r + 2]} * wz) + f2v{e[4 * r + 3], e[4 * r + 3]};
     const f2v nx = p[0] * f2v{cam.fx, cam.fx}, ny = p[1] * f2v{cam.fy, cam.fy};
     const f2v rz = f2v{__builtin_amdgcn_rcpf(p[2].x), __builtin_amdgcn_rcpf(p[2].y)};
     const f2v qx = nx * rz, qy = ny * rz;
@@ -1094,135 +1122,99 @@ __device__ __forceinline__ bool work_slot(const uint32_t* ctrl, WorkCursor& c, u
     slot = (size_t)c.bin * binCap + (g - c.lo);
     return true;
 }
-// k_apply_ops: the memory round trips of an op batched. The ZC voxels of the lane are loaded
-// once at the start of the round (whether or not an op reaches them: +12 B per untouched voxel, but
-// no dependent load in the op loop), and the ops of the block's mask are taken two at a time —
-// both projections, then the depth AND colour gathers of both issued back to back, then the band
-// tests and updates of the first op followed by the second (sequence order, on the register copy).
-// Per pair of ops one gather round trip instead of ~4. Same arithmetic, same results.
-template <int ZC>
-__device__ __forceinline__ void apply_project(const HashArgs& A, const BFDepthCameraParams& cam, const OpTable& ops,
-                                              uint32_t k, float wx, float wy, const float* wz, uint32_t* pix, float* pz,
-                                              float* d, uint32_t* cc) {
-    const BFMat4 Ti = op_mat(ops.tinv[k]);
-    const uint2* dcImg = ops.dc[k];
-#pragma unroll
-    for (int zi = 0; zi < ZC; zi += 2) {
-        f2v pz2;
-        voxel_pixel2(cam, Ti, wx, wy, f2v{wz[zi], wz[zi + 1]}, ops.color[k] != nullptr, pix[zi], pix[zi + 1], pz2);
-        pz[zi] = pz2.x;
-        pz[zi + 1] = pz2.y;
-    }
-#pragma unroll
-    for (int zi = 0; zi < ZC; zi++) {
-        const bool on = pix[zi] != 0xFFFFFFFFu;
-        const uint2 v = on ? dcImg[pix[zi]] : make_uint2(0xFF800000u, 0u);  // off-screen: depth -inf
-        d[zi] = __uint_as_float(v.x);
-        cc[zi] = v.y;
-    }
-}
-#ifdef BF_APPLY_DIAG
-// diagnostic build only (-DBF_APPLY_DIAG): where the voxel-op evaluations of the batch pass go
-__device__ unsigned long long g_diag[8];  // 0 off-screen, 1 invalid depth, 2 outside band, 3 updates, 4 wave-rounds, 5 dead wave-rounds
-#endif
-template <int ZC>
-__device__ __forceinline__ uint32_t apply_update(const HashArgs& A, bool deint, const float* d, const float* pz,
-                                                 const uint32_t* cc, float* vs, float* vw, uint32_t* vc) {
-    uint32_t in = 0;
-#ifdef BF_APPLY_DIAG
-    {
-        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-        for (int zi = 0; zi < ZC; zi++) {
-            float sd;
-            const bool ib = voxel_in_band(A, d[zi], pz[zi], sd);
-            if (ib) c3++;
-            else if (d[zi] == -INFINITY && cc[zi] == 0u) c0++;
-            else if (d[zi] == -INFINITY || d[zi] >= A.maxIntegrationDistance) c1++;
-            else c2++;
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            c0 += __shfl_xor(c0, off); c1 += __shfl_xor(c1, off); c2 += __shfl_xor(c2, off); c3 += __shfl_xor(c3, off);
-        }
-        if (lane_id() == 0) {
-            atomicAdd(&g_diag[0], (unsigned long long)c0); atomicAdd(&g_diag[1], (unsigned long long)c1);
-            atomicAdd(&g_diag[2], (unsigned long long)c2); atomicAdd(&g_diag[3], (unsigned long long)c3);
-            atomicAdd(&g_diag[4], 1ull);
-            if (c3 == 0) atomicAdd(&g_diag[5], 1ull);
-        }
-    }
-#endif
-#pragma unroll
-    for (int zi = 0; zi < ZC; zi++) {
-        float sd;
-        if (!voxel_in_band(A, d[zi], pz[zi], sd)) continue;
-        in |= 1u << zi;
-        if (deint) voxel_deintegrate(vs[zi], vw[zi], vc[zi], sd, cc[zi]);
-        else voxel_integrate(vs[zi], vw[zi], vc[zi], sd, cc[zi], A.weightMax);
-    }
-    return in;
-}
-// ZC = 2 z-slices per round at 8 waves per SIMD (measured best: 4 slices 941 us, 7 waves 860 us vs
-// 824 us per launch at the bench workload)
-template <int ZC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_apply_ops(
+// k_apply_ops, the batch's voxel pass: one wave per work-list block, lane = (x, y) column. The lane's
+// voxels of ZR z-slices stay in registers while the ops of the block's mask run over them in sequence
+// order (the outer loop), ZC z-slices per step (the inner one): project, gather {depth, colour}, band
+// test, then the integrate / de-integrate update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:
+// 420-521) on the register copy; each touched voxel is stored once. An op's z-slices project to nearly
+// the same pixels, so its gathers follow each other and hit the lines the previous slice fetched (the
+// z-round-outer order re-fetched every op's footprint once per round: 888 -> 856 us per launch at the
+// bench workload); the op's pose and the (x, y) part of its projection are taken once per ZR slices.
+// ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us).
+template <int ZR, int ZC, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks, uint32_t binCap) {
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const int lx = lane & 7, ly = lane >> 3;
-    unsigned long long updated = 0, rmw = 0;
+    uint32_t updated = 0, rmw = 0;  // per lane and launch: < 2^32
     WorkCursor cur = work_begin(A.ctrl, ops.n);
     size_t b;
     for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
-        const int4 e = A.band[b];
+        const int4 ev = A.band[b];  // wave-uniform: keep the block's coordinates and base in SGPRs
+        const int4 e = make_int4(__builtin_amdgcn_readfirstlane(ev.x), __builtin_amdgcn_readfirstlane(ev.y),
+                                 __builtin_amdgcn_readfirstlane(ev.z), __builtin_amdgcn_readfirstlane(ev.w));
         const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);  // wave-uniform: op table reads stay scalar
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
+        Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w) + lane;
         int dcount = 0;
         uint32_t nupd = 0, nrmw = 0;
 #pragma unroll
-        for (int z0 = 0; z0 < BF_SDF_BLOCK_SIZE; z0 += ZC) {
-            float vs[ZC], vw[ZC], w0[ZC], wz[ZC];
-            uint32_t vc[ZC];
+        for (int h = 0; h < BF_SDF_BLOCK_SIZE; h += ZR) {
+            float vs[ZR], vw[ZR];
+            uint32_t vc[ZR], pos0 = 0;
 #pragma unroll
-            for (int zi = 0; zi < ZC; zi++) {
-                wz[zi] = (float)(bz + z0 + zi) * A.voxelSize;  // vvox_to_world z
-                const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane));
-                vs[zi] = __uint_as_float(v.a);
-                vw[zi] = __uint_as_float(v.b);
-                vc[zi] = v.c;
-                w0[zi] = vw[zi];
+            for (int z = 0; z < ZR; z++) {
+                const Vox3 v = vp[(h + z) * 64];
+                vs[z] = __uint_as_float(v.a);
+                vw[z] = __uint_as_float(v.b);
+                vc[z] = v.c;
+                pos0 |= (uint32_t)(vw[z] >= 1.0f) << z;
             }
             uint32_t touched = 0;
             for (uint32_t mk = mask; mk;) {
-                const uint32_t k1 = (uint32_t)__builtin_ctz(mk);
+                const uint32_t k = (uint32_t)__builtin_ctz(mk);
                 mk &= mk - 1;
-                const bool two = mk != 0;
-                const uint32_t k2 = two ? (uint32_t)__builtin_ctz(mk) : k1;
-                if (two) mk &= mk - 1;
-                float d1[ZC], p1[ZC], d2[ZC], p2[ZC];
-                uint32_t x1[ZC], c1[ZC], x2[ZC], c2[ZC];
-                apply_project<ZC>(A, cam, ops, k1, wx, wy, wz, x1, p1, d1, c1);
-                if (two) apply_project<ZC>(A, cam, ops, k2, wx, wy, wz, x2, p2, d2, c2);
-                uint32_t in = apply_update<ZC>(A, (ops.deintMask >> k1) & 1u, d1, p1, c1, vs, vw, vc);
-                nupd += (uint32_t)__popc(in);
-                touched |= in;
-                if (two) {
-                    in = apply_update<ZC>(A, (ops.deintMask >> k2) & 1u, d2, p2, c2, vs, vw, vc);
-                    nupd += (uint32_t)__popc(in);
-                    touched |= in;
+                const BFMat4 Ti = op_mat(ops.tinv[k]);
+                const float bxy[3] = {Ti.m[0] * wx + Ti.m[1] * wy, Ti.m[4] * wx + Ti.m[5] * wy, Ti.m[8] * wx + Ti.m[9] * wy};
+                // the op's {depth, colour} image through a buffer descriptor: 32-bit offsets, and an
+                // off-screen lane's out-of-range offset reads 0 without a branch
+                const __amdgpu_buffer_rsrc_t dcRsrc =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)ops.dc[k], (short)0, (int)(cam.imageWidth * cam.imageHeight * 8u), 0x00020000);
+                const bool haveColor = ops.color[k] != nullptr;
+                const bool deint = (ops.deintMask >> k) & 1u;
+#pragma unroll
+                for (int z0 = 0; z0 < ZR; z0 += ZC) {
+                    uint32_t pix[ZC], cc[ZC];
+                    float pz[ZC], d[ZC];
+#pragma unroll
+                    for (int zi = 0; zi < ZC; zi += 2) {
+                        const f2v wz = f2v{(float)(bz + h + z0 + zi), (float)(bz + h + z0 + zi + 1)} * f2v{A.voxelSize, A.voxelSize};
+                        f2v pz2;
+                        voxel_pixel2b(cam, Ti, bxy, wz, haveColor, pix[zi], pix[zi + 1], pz2);
+                        pz[zi] = pz2.x;
+                        pz[zi + 1] = pz2.y;
+                    }
+#pragma unroll
+                    for (int zi = 0; zi < ZC; zi++) {
+                        const bool on = pix[zi] != 0xFFFFFFFFu;
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b64(dcRsrc, on ? pix[zi] * 8u : 0xFFFFFFFFu, 0, 0);
+                        d[zi] = on ? __uint_as_float(v[0]) : -INFINITY;  // off-screen: depth -inf, colour 0
+                        cc[zi] = on ? v[1] : 0u;
+                    }
+#pragma unroll
+                    for (int zi = 0; zi < ZC; zi++) {
+                        float sd;
+                        if (!voxel_in_band(A, d[zi], pz[zi], sd)) continue;
+                        touched |= 1u << (z0 + zi);
+                        nupd++;
+                        if (deint) voxel_deintegrate_f(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi]);
+                        else voxel_integrate_f(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi], A.weightMax);
+                    }
                 }
             }
 #pragma unroll
-            for (int zi = 0; zi < ZC; zi++) {
-                if (!((touched >> zi) & 1u)) continue;
+            for (int z = 0; z < ZR; z++) {
+                if (!((touched >> z) & 1u)) continue;
                 Vox3 nv;
-                nv.a = __float_as_uint(vs[zi]);
-                nv.b = __float_as_uint(vw[zi]);
-                nv.c = vc[zi];
-                *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)((z0 + zi) * 64 + lane)) = nv;
-                dcount += (int)(vw[zi] >= 1.0f) - (int)(w0[zi] >= 1.0f);
+                nv.a = __float_as_uint(vs[z]);
+                nv.b = __float_as_uint(vw[z]);
+                nv.c = vc[z];
+                vp[(h + z) * 64] = nv;
+                dcount += (int)(vw[z] >= 1.0f) - (int)((pos0 >> z) & 1u);
                 nrmw++;
             }
         }
@@ -1442,7 +1434,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int occ0 = 0, occ1 = 0, occA = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<2>, 256, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, 4, 8>, 256, 0));
     applyGrid_ = (unsigned)std::max(1, occA) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
@@ -1639,7 +1631,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    hipExtLaunchKernelGGL(k_apply_ops<2>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
+    hipExtLaunchKernelGGL(k_apply_ops<4, 4, 8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;
@@ -1685,14 +1677,6 @@ uint32_t Scene::errorFlags() {
 }
 
 BFTsdfStats Scene::stats() {
-#ifdef BF_APPLY_DIAG
-    {
-        unsigned long long d[8];
-        BF_HIP(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_diag), sizeof(d)));
-        fprintf(stderr, "APPLY_DIAG offscreen %llu invalid_depth %llu outside_band %llu updates %llu wave_rounds %llu dead_wave_rounds %llu\n",
-                d[0], d[1], d[2], d[3], d[4], d[5]);
-    }
-#endif
     std::vector<unsigned long long> h(STAT_SLOTS * STAT_FIELDS);
     BF_HIP(hipMemcpyAsync(h.data(), stats_.p, stats_.bytes(), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
@@ -1713,6 +1697,16 @@ void Scene::exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter
     if (heapCounter) BF_HIP(hipMemcpyAsync(heapCounter, ctrl_.p + C_HEAP, 4, hipMemcpyDeviceToHost, stream_));
     if (voxels) BF_HIP(hipMemcpyAsync(voxels, voxels_.p, voxels_.bytes(), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
+}
+
+uint32_t Scene::exportBlocks(int4* out, uint32_t cap) {
+    uint32_t hw = 0;
+    BF_HIP(hipMemcpyAsync(&hw, ctrl_.p + C_HIGHWATER, 4, hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    const uint32_t n = std::min(hw, cap);
+    if (n && out) BF_HIP(hipMemcpyAsync(out, blockPos_.p, n * sizeof(int4), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    return hw;
 }
 
 uint32_t Scene::exportVisible(int4* out, uint32_t cap) {

@@ -95,6 +95,51 @@ class Comm:
             self.h = None
 
 
+def chunk_owner_array(blocks, voxel_size: float, shard_count: int, chunk: float = 1.0):
+    """chunk_owner over an int array of block coordinates [n, 3] (same float32 / int32 arithmetic)."""
+    import numpy as np
+    b = np.asarray(blocks, np.int64)[:, :3]
+    w = (b * 8).astype(np.float32) * np.float32(voxel_size)
+    q = (w / np.float32(chunk)).astype(np.float32)
+    c = np.trunc((q + np.sign(q).astype(np.float32) * np.float32(0.5)).astype(np.float32)).astype(np.int64)
+    h = ((c[:, 0] * 73856093) ^ (c[:, 1] * 19349669) ^ (c[:, 2] * 83492791)) & 0xFFFFFFFF
+    h = np.where(h >= (1 << 31), h - (1 << 32), h)
+    r = np.abs(h) % shard_count
+    r = np.where(h < 0, -r, r)
+    return np.where(r < 0, r + shard_count, r).astype(np.int32)
+
+
+def shard_balance(blocks, voxel_size: float, poses, cam, shard_counts=(2, 4, 8)) -> dict:
+    """Load balance of the chunk-ownership TSDF sharding for a final scene: per shard
+    count G, the allocated blocks each rank stores and, over the given camera poses, the in-frustum
+    allocated blocks each rank scans and updates (the per-frame voxel work, isInCameraFrustumApprox at
+    the block centre, DepthCameraUtil.h:95-107); max / mean over ranks."""
+    import numpy as np
+    b = np.asarray(blocks, np.int64)[:, :3]
+    ctr = (b * 8).astype(np.float64) * voxel_size + voxel_size * 0.5 * 7.0
+    vis = np.zeros(len(b), np.int64)
+    for T in poses:
+        Ti = np.linalg.inv(np.asarray(T, np.float64))
+        p = ctr @ Ti[:3, :3].T + Ti[:3, 3]
+        z = p[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = p[:, 0] * cam.fx / z + cam.mx
+            v = p[:, 1] * cam.fy / z + cam.my
+        nx = (2.0 * u - (cam.imageWidth - 1.0)) / (cam.imageWidth - 1.0) * 0.95
+        ny = ((cam.imageHeight - 1.0) - 2.0 * v) / (cam.imageHeight - 1.0) * 0.95
+        nz = (z - cam.sensorDepthWorldMin) / (cam.sensorDepthWorldMax - cam.sensorDepthWorldMin) * 0.95
+        vis += ((z > 0) & (np.abs(nx) <= 1) & (np.abs(ny) <= 1) & (nz >= 0) & (nz <= 1)).astype(np.int64)
+    out = {"blocks": int(len(b)), "frames": len(poses)}
+    for G in shard_counts:
+        own = chunk_owner_array(b, voxel_size, G)
+        stored = np.bincount(own, minlength=G)
+        work = np.bincount(own, weights=vis, minlength=G)
+        out[f"G{G}"] = {"stored_max_over_mean": float(stored.max() / max(stored.mean(), 1e-9)),
+                        "visible_max_over_mean": float(work.max() / max(work.mean(), 1e-9)),
+                        "stored": stored.tolist(), "visible_block_frames": work.astype(int).tolist()}
+    return out
+
+
 def chunk_owner(bx: int, by: int, bz: int, voxel_size: float, shard_count: int, chunk: float = 1.0) -> int:
     """Shard owning block (bx, by, bz): computeHashPos of its 1 m chunk (worldToChunks rounding,
     CUDASceneRepHashSDF.cu:136-150) mod shard_count — the host mirror of owned() in csrc/tsdf.hip."""

@@ -200,6 +200,14 @@ class Recon:
                                     C.byref(hc), vox.ctypes.data_as(C.c_void_p)))
         return hash_, heap, hc.value, vox
 
+    def export_blocks(self) -> np.ndarray:
+        """int32 [n, 4] {x, y, z, allocated} of heap blocks [0, highWater) (bf_recon_export_blocks)."""
+        n = C.c_uint32()
+        check(lib().bf_recon_export_blocks(self.h, None, C.c_uint32(0), C.byref(n)))
+        out = np.zeros((max(1, n.value), 4), np.int32)
+        check(lib().bf_recon_export_blocks(self.h, out.ctypes.data_as(C.c_void_p), C.c_uint32(n.value), C.byref(n)))
+        return out[:n.value]
+
     def op_log(self):
         n = C.c_uint32()
         check(lib().bf_recon_op_log(self.h, None, C.c_uint32(0), C.byref(n)))

@@ -104,6 +104,9 @@ int bf_scene_reset_stats(bf_scene* s);
 /* debugHash-style dump to HOST memory (CUDASceneRepHashSDF.h:179-314): any pointer may be NULL.
  * hash: BFHashEntry[4*numBuckets], heap: uint32[numSDFBlocks], voxels: BFVoxel[numSDFBlocks*512] */
 int bf_scene_export(bf_scene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
+/* heap blocks [0, highWater) to HOST: int32 {x, y, z, allocated} per block (heap order); min(cap, n) written,
+ * *n = highWater (the allocated prefix compactify streams) */
+int bf_scene_export_blocks(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n);
 /* visible list of the last compactify to HOST: int32 {x,y,z,ptr} x n */
 int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n);
 /* CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) preceded by setLastRigidTransformAndCompactify
@@ -354,6 +357,8 @@ int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTrian
                           uint32_t* totalTriangles);
 /* summed device time / count of the renderKernel launches since the first call (enables the clock) */
 int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches);
+/* bf_scene_export_blocks on the loop's scene */
+int bf_recon_export_blocks(bf_recon* r, int32_t* out4, uint32_t cap, uint32_t* n);
 /* debugHash-style dump of the loop's scene (same layout as bf_scene_export) */
 int bf_recon_export(bf_recon* r, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
 /* with recordOps: the scene calls issued so far, in order (kind 1 de-integrate with oldT,

@@ -121,3 +121,26 @@ def test_gloo_world2_pair_shard_exchange_is_exact():
         assert p.exitcode == 0
     for r in range(world):
         np.testing.assert_array_equal(res[r][0], res[r][1])
+
+
+def test_chunk_owner_array_matches_scalar_mirror():
+    from bundlefusion_amd.dist import chunk_owner_array
+    rng = np.random.default_rng(1)
+    b = rng.integers(-2000, 2000, (3000, 3))
+    for G in (2, 4, 8):
+        got = chunk_owner_array(b, 0.004, G)
+        want = [chunk_owner(int(x), int(y), int(z), 0.004, G) for x, y, z in b]
+        np.testing.assert_array_equal(got, want)
+
+
+def test_shard_balance_report_shape():
+    from types import SimpleNamespace
+    from bundlefusion_amd.dist import shard_balance
+    rng = np.random.default_rng(2)
+    b = rng.integers(-100, 100, (5000, 3))
+    cam = SimpleNamespace(fx=577.87, fy=577.87, mx=319.5, my=239.5, imageWidth=640, imageHeight=480,
+                          sensorDepthWorldMin=0.1, sensorDepthWorldMax=4.0)
+    T = np.eye(4)
+    r = shard_balance(b, 0.004, [T], cam, (2, 4))
+    assert r["blocks"] == 5000 and sum(r["G2"]["stored"]) == 5000 and sum(r["G4"]["stored"]) == 5000
+    assert r["G2"]["stored_max_over_mean"] >= 1.0
