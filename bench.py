@@ -247,17 +247,26 @@ def main():
                     help="stream length (BASELINE north star: 5000 frames); independent of --steps")
     ap.add_argument("--steps", type=int, default=50, help="timed submaps (10 frames each) at the stream's tail")
     ap.add_argument("--warmup", type=int, default=5, help="untimed submaps right before the timed ones")
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--voxel", type=float, default=0.004)
-    ap.add_argument("--buckets", type=int, default=1 << 23)
-    ap.add_argument("--blocks", type=int, default=1 << 21)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--voxel", type=float, default=None)
+    ap.add_argument("--buckets", type=int, default=None)
+    ap.add_argument("--blocks", type=int, default=None)
+    ap.add_argument("--preset", choices=["config1", "config5"], default="config1",
+                    help="config1: BASELINE north star (640x480, 4 mm, 2^23 buckets, 2^21 blocks); config5: "
+                         "1280x960 depth at 2 mm voxels (2^24 buckets, 2^23 blocks: a heap beyond the "
+                         "reference's 2^22-block int32 voxel index); explicit size flags override")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "apply_pass_pmc.json"),
                     help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
                          "tools/profile_bench.sh (committed under profiles/); used only when its "
                          "workload equals this run's, else traffic is null")
     args = ap.parse_args()
+    preset = {"config1": dict(width=640, height=480, voxel=0.004, buckets=1 << 23, blocks=1 << 21),
+              "config5": dict(width=1280, height=960, voxel=0.002, buckets=1 << 24, blocks=1 << 23)}[args.preset]
+    for k, v in preset.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     from bundlefusion_amd.dist import HostGroup, env_rank
     rank, world, local_rank = env_rank()
@@ -374,7 +383,7 @@ def main():
                  "note": "bf_recon_end_solve(15): sparse weight 1 + dense depth 15 (3 x 150 GN x PCG), every keyframe's "
                          "80x60 cache frame; untimed, after the timed tail"}
     out = {
-        "metric": "frames/s integrate+global-BA on 640x480 @4mm voxels",
+        "metric": f"frames/s integrate+global-BA on {args.width}x{args.height} @{args.voxel * 1000:g}mm voxels",
         "value": frames / dt,
         "unit": "frames/s",
         "n_gpus": world,

@@ -255,6 +255,20 @@ class SceneRepHashSDF:
             np.zeros((0, 3, 6), np.float32)
         return tris, total.value
 
+    def export_blocks(self) -> np.ndarray:
+        """int32 [n, 4] {x, y, z, allocated} of heap blocks [0, highWater) (bf_scene_export_blocks)."""
+        n = C.c_uint32()
+        check(lib().bf_scene_export_blocks(self.h, None, C.c_uint32(0), C.byref(n)))
+        out = np.empty((max(n.value, 1), 4), np.int32)
+        check(lib().bf_scene_export_blocks(self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), C.c_uint32(n.value), C.byref(n)))
+        return out[: n.value].copy()
+
+    def export_block_voxels(self, first: int, count: int) -> np.ndarray:
+        """voxels of heap blocks [first, first + count): VOXEL_DTYPE [count, 512] (bf_scene_export_block_voxels)."""
+        out = np.empty((max(count, 1), 512), VOXEL_DTYPE)
+        check(lib().bf_scene_export_block_voxels(self.h, C.c_uint32(first), C.c_uint32(count), out.ctypes.data_as(C.c_void_p)))
+        return out[:count]
+
     def export_visible(self) -> np.ndarray:
         cap = self.params.numSDFBlocks
         out = np.empty((cap, 4), np.int32)

@@ -339,6 +339,12 @@ int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* 
     *n = s->scene->exportVisible(reinterpret_cast<int4*>(out4), cap);
     BF_CATCH
 }
+int bf_scene_export_block_voxels(bf_scene* s, uint32_t first, uint32_t count, BFVoxel* out) {
+    BF_TRY
+    BF_REQUIRE(s && (out || count == 0), BF_ERR_ARG, "null argument");
+    s->scene->exportBlockVoxels(first, count, out);
+    BF_CATCH
+}
 int bf_scene_raycast(bf_scene* s, const float T[16], const BFDepthCameraParams* cam, const BFRayCastParams* rp, float* depth,
                      float* depth4, float* normals, float* colors, float* rayMin, float* rayMax) {
     BF_TRY

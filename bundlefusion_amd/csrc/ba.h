@@ -157,7 +157,11 @@ private:
     DevBuf<float> pairBlk_;  // [maxPairs][36]
     DevBuf<float> diag_;     // [N][36]
     DevBuf<float> jtr_;      // [N][6]
-    DevBuf<float> apDense_;  // [N][8]
+    DevBuf<uint32_t> pairFlag_;  // [N][N]
+    DevBuf<float> pairAcc_;      // [maxPairs][54]
+    DevBuf<float> pairProd_;     // [maxPairs][12]
+    DevBuf<uint32_t> imgPairs_;  // [N][N]
+    DevBuf<uint32_t> imgPairN_;  // [N]
     // assembled (pair) normal equations
     uint32_t maxPairsA_ = 0;
     uint32_t shardCount_ = 1, shardIndex_ = 0;

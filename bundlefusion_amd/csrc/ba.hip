@@ -69,7 +69,12 @@ struct BA {
     float* pairBlk;
     float* diag;
     float* jtr;
-    float* apDense;
+    // dense term in a fixed order (no float atomics, so two solves of one problem agree bit for bit):
+    uint32_t* pairFlag;  // [N][N] overlap flag of (i, j), i < j (k_dense_overlap)
+    float* pairAcc;      // [maxPairs][54] a pair's J_i^T J_i | J_j^T J_j upper triangles (21 + 21), J_i^T r | J_j^T r
+    float* pairProd;     // [maxPairs][12] per PCG iteration: B p_i (image j's rows) | B^T p_j (image i's rows)
+    uint32_t* imgPairs;  // [N][N] pairs of image v in pair order: k << 1 | (v is the pair's j)
+    uint32_t* imgPairN;  // [N]
     uint32_t maxPairs;
     const BFCachedFrame* cache;
     uint32_t cw, ch;
@@ -648,9 +653,6 @@ __global__ void k_transforms(BA a, float wSparse, int useDense, int gated, int s
             t[r] = make_float4(T.e[r * 4], T.e[r * 4 + 1], T.e[r * 4 + 2], T.e[r * 4 + 3]);
             ti[r] = make_float4(Ti.e[r * 4], Ti.e[r * 4 + 1], Ti.e[r * 4 + 2], Ti.e[r * 4 + 3]);
         }
-        float4* ad = reinterpret_cast<float4*>(a.apDense + (size_t)v * 8);
-        ad[0] = make_float4(0, 0, 0, 0);
-        ad[1] = make_float4(0, 0, 0, 0);
     }
     if (setState && blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctrl[K_PCG_DONE] = 0;
@@ -851,12 +853,15 @@ __device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, in
         }
         aT = aT + mk3(o6[0], o6[1], o6[2]);
         aR = aR + mk3(o6[3], o6[4], o6[5]);
-        float4* ad = reinterpret_cast<float4*>(a.apDense + (size_t)v * 8);
-        const float4 x = ld_wt(ad), y = ld_wt(ad + 1);  // agent-scope atomics of this launch
-        aR = aR + mk3(x.x, x.y, x.z);
-        aT = aT + mk3(y.x, y.y, y.z);
-        ad[0] = make_float4(0, 0, 0, 0);
-        ad[1] = make_float4(0, 0, 0, 0);
+        // off-diagonal blocks: the row's pair products of this launch (write-through), in pair order
+        const uint32_t* L = a.imgPairs + (size_t)v * a.maxN;
+        const uint32_t nL = a.imgPairN[v];
+        for (uint32_t q = 0; q < nL; q++) {
+            const uint32_t e = L[q];
+            const float* pp = a.pairProd + (size_t)(e >> 1) * 12 + ((e & 1u) ? 0u : 6u);
+            aT = aT + mk3(ld_wtf(pp), ld_wtf(pp + 1), ld_wtf(pp + 2));
+            aR = aR + mk3(ld_wtf(pp + 3), ld_wtf(pp + 4), ld_wtf(pp + 5));
+        }
     }
 }
 
@@ -918,7 +923,8 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
     return rDotzNew;
 }
 
-// dense off-diagonal blocks: Ap_j += B p_i, Ap_i += B^T p_j (B rows: image j), agent-scope atomics
+// dense off-diagonal blocks: per pair B p_i (for image j) and B^T p_j (for image i), [trans | rot] rows,
+// stored write-through for the finisher, which sums each row's pairs in pair order (pcg_ap)
 __device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
     const uint32_t lane = lane_id();
     const uint32_t np = a.ctrl[K_NPAIRS];
@@ -932,13 +938,13 @@ __device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
             vload(a, V_P, pr.x, r, t);
             const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
             for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
-            if (pr.y > 0) atomicAdd(&a.apDense[(size_t)pr.y * 8 + (lane < 3 ? 4 + lane : lane - 3)], o);
+            st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)k * 12 + lane, __float_as_uint(o));
         } else if (lane < 12) {
             vload(a, V_P, pr.y, r, t);
             const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
             const int c0 = lane - 6;
             for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
-            if (pr.x > 0) atomicAdd(&a.apDense[(size_t)pr.x * 8 + (c0 < 3 ? 4 + c0 : c0 - 3)], o);
+            st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)k * 12 + lane, __float_as_uint(o));
         }
     }
 }
@@ -1338,9 +1344,7 @@ __device__ __forceinline__ void bilinear(const BA& a, float x, float y, const fl
 
 __global__ void k_dense_reset(BA a) {
     if (a.ctrl[K_GN_DONE]) return;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.N * 36; k += gridDim.x * blockDim.x) a.diag[k] = 0.0f;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.N * 6; k += gridDim.x * blockDim.x) a.jtr[k] = 0.0f;
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctrl[K_NPAIRS] = 0;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.N * a.N; k += gridDim.x * blockDim.x) a.pairFlag[k] = 0u;
 }
 
 // FindImageImageCorr_Kernel<true> (SolverBundling.cu:29-79), one wave per (i, j), i < j
@@ -1372,10 +1376,32 @@ __global__ void k_dense_overlap(BA a) {
         if (length3(s2t - ct) <= a.distT) found++;
     }
     for (int off = 32; off > 0; off >>= 1) found += __shfl_xor(found, off);
-    if (threadIdx.x == 0 && found > 10) {
-        const uint32_t k = atomicAdd(&a.ctrl[K_NPAIRS], 1u);
-        if (k < a.maxPairs) a.pairs[k] = make_uint2(i, j);
+    if (threadIdx.x == 0 && found > 10) a.pairFlag[(size_t)i * a.N + j] = 1u;
+}
+
+// The overlapping pairs in (i, j) order (the reference appends them at atomic offsets): one workgroup
+// compacts the flag matrix with wave ballots; K_NPAIRS = all pairs found, the first maxPairs are kept.
+__global__ __launch_bounds__(1024) void k_dense_compact(BA a) {
+    __shared__ uint32_t sCnt[16], sBase;
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, NN = a.N * a.N;
+    if (threadIdx.x == 0) sBase = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < NN; b0 += 1024) {
+        const uint32_t idx = b0 + threadIdx.x;
+        const bool f = idx < NN && a.pairFlag[idx] != 0u;
+        const unsigned long long m = __ballot(f);
+        if (lane == 0) sCnt[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t off = sBase;
+        for (uint32_t w = 0; w < wv; w++) off += sCnt[w];
+        off += (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (f && off < a.maxPairs) a.pairs[off] = make_uint2(idx / a.N, idx % a.N);
+        __syncthreads();
+        if (threadIdx.x == 0) for (uint32_t w = 0; w < 16; w++) sBase += sCnt[w];
+        __syncthreads();
     }
+    if (threadIdx.x == 0) a.ctrl[K_NPAIRS] = sBase;
 }
 
 // FindDenseCorrespondences_Kernel (:92-160, uchar4-normal variant :152-184) + WeightDenseCorrespondences (:162-180)
@@ -1516,23 +1542,55 @@ __global__ __launch_bounds__(WG) void k_dense_build(BA a, float wDepth, float wC
             float s = 0.0f;
             for (uint32_t wv = 0; wv < blockDim.x / 64; wv++) s += red[wv][threadIdx.x];
             const int q = threadIdx.x;
-            if (q < 42) {  // symmetric diagonal block entry (r, c), r <= c -> both halves
-                const int qq = q < 21 ? q : q - 21;
-                int r = 0, c = 0, t2 = 0;
-                for (r = 0; r < 6; r++) { if (qq < t2 + (6 - r)) { c = r + (qq - t2); break; } t2 += 6 - r; }
-                float* D = a.diag + (size_t)(q < 21 ? i : j) * 36;
-                atomicAdd(&D[r * 6 + c], s);
-                if (r != c) atomicAdd(&D[c * 6 + r], s);
+            if (q < 42) {  // diagonal-block upper triangles of images i (q < 21) and j: summed per image by k_dense_lists
+                a.pairAcc[(size_t)k * 54 + q] = s;
             } else if (q < 78) {  // B(row j-index c, col i-index r) = (J_i^T W J_j)^T
                 const int r = (q - 42) / 6, c = (q - 42) % 6;
                 a.pairBlk[(size_t)k * 36 + c * 6 + r] = s;
-            } else if (q < 84) {
-                atomicAdd(&a.jtr[(size_t)i * 6 + (q - 78)], s);
-            } else {
-                atomicAdd(&a.jtr[(size_t)j * 6 + (q - 84)], s);
+            } else {  // J_i^T r (q < 84), J_j^T r
+                a.pairAcc[(size_t)k * 54 + 42 + (q - 78)] = s;
             }
         }
         __syncthreads();
+    }
+}
+
+// Per image v (one wave): its pairs in pair order (pairW != 0), and its dense diagonal block and J^T r
+// summed over them in that order (the reference adds them with float atomics in arrival order).
+__global__ __launch_bounds__(64) void k_dense_lists(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t v = blockIdx.x, lane = lane_id();
+    const uint32_t np = min(a.ctrl[K_NPAIRS], a.maxPairs);
+    uint32_t* L = a.imgPairs + (size_t)v * a.maxN;
+    uint32_t n = 0;
+    float s = 0.0f;  // lane < 21: upper-triangle entry of the diagonal block, 21..26: J^T r
+    for (uint32_t b0 = 0; b0 < np; b0 += 64) {
+        const uint32_t k = b0 + lane;
+        uint32_t e = 0;
+        bool in = false;
+        if (k < np && a.pairW[k] != 0.0f) {
+            const uint2 pr = a.pairs[k];
+            in = pr.x == v || pr.y == v;
+            e = (k << 1) | (pr.y == v ? 1u : 0u);
+        }
+        const unsigned long long m = __ballot(in);
+        if (in) L[n + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = e;
+        n += (uint32_t)__popcll(m);
+        for (unsigned long long mm = m; mm; mm &= mm - 1ull) {  // this chunk's pairs of v, ascending
+            const uint32_t ek = (uint32_t)__shfl((int)e, (int)__builtin_ctzll(mm));
+            const float* acc = a.pairAcc + (size_t)(ek >> 1) * 54;
+            if (lane < 21) s += acc[((ek & 1u) ? 21 : 0) + lane];
+            else if (lane < 27) s += acc[42 + ((ek & 1u) ? 6 : 0) + (lane - 21)];
+        }
+    }
+    if (lane == 0) a.imgPairN[v] = n;
+    if (lane < 21) {
+        int r = 0, c = 0, t2 = 0;
+        for (r = 0; r < 6; r++) { if ((int)lane < t2 + (6 - r)) { c = r + ((int)lane - t2); break; } t2 += 6 - r; }
+        a.diag[(size_t)v * 36 + r * 6 + c] = s;
+        a.diag[(size_t)v * 36 + c * 6 + r] = s;
+    } else if (lane < 27) {
+        a.jtr[(size_t)v * 6 + (lane - 21)] = s;
     }
 }
 
@@ -1830,7 +1888,6 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
     cfg.normalEquations = o ? o->normalEquations : 0;
     cfg.earlyOut = !(o && o->disableEarlyOut);
-    if (const char* e = getenv("BF_NORMAL_EQUATIONS"); e && (!o || o->normalEquations == 0)) cfg.normalEquations = atoi(e);
     return cfg;
 }
 
@@ -1881,7 +1938,11 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     pairBlk_.alloc((size_t)maxPairs_ * 36);
     diag_.alloc((size_t)N * 36);
     jtr_.alloc((size_t)N * 6);
-    apDense_.alloc((size_t)N * 8);
+    pairFlag_.alloc((size_t)N * N);
+    pairAcc_.alloc((size_t)maxPairs_ * 54);
+    pairProd_.alloc((size_t)maxPairs_ * 12);
+    imgPairs_.alloc((size_t)N * N);
+    imgPairN_.alloc(N);
     // assembled normal equations: a pair has >= 1 correspondence, so pairs <= min(N(N-1)/2, maxCorr)
     maxPairsA_ = (uint32_t)std::min<size_t>((size_t)N * (N - 1) / 2, (size_t)cfg.maxCorr);
     rowSorted_.alloc(2 * (size_t)cfg.maxCorr + 1);
@@ -1907,7 +1968,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
-    BF_HIP(hipMemsetAsync(apDense_.p, 0, apDense_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(imgPairN_.p, 0, imgPairN_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
 }
 
@@ -1953,7 +2014,8 @@ void Solver::solve(const SolveArgs& s) {
     a.rowCount = rowCount_.p; a.rowStart = rowStart_.p; a.rowLen = rowLen_.p; a.rowTmp = rowTmp_.p; a.rowIdx = rowIdx_.p;
     a.entries = entries_.p; a.vec = vec_.p; a.img = img_.p; a.T = T_.p; a.Tinv = Tinv_.p; a.ctrl = ctrl_.p;
     a.part = part_.p; a.partIdx = partIdx_.p; a.rot = s.rot; a.trans = s.trans;
-    a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p; a.apDense = apDense_.p;
+    a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p;
+    a.pairFlag = pairFlag_.p; a.pairAcc = pairAcc_.p; a.pairProd = pairProd_.p; a.imgPairs = imgPairs_.p; a.imgPairN = imgPairN_.p;
     a.maxPairs = s.numImages * (s.numImages - 1) / 2;
     a.tileCnt = tileCnt_.p; a.nTiles = div_up(s.numCorr, TILE);
     a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.sync = sync_.p;
@@ -2036,8 +2098,10 @@ void Solver::solve(const SolveArgs& s) {
             if (dense) {
                 k_dense_reset<<<64, WG, 0, stream_>>>(a);
                 k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);
+                k_dense_compact<<<1, 1024, 0, stream_>>>(a);
                 k_dense_count<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 8), WG, 0, stream_>>>(a);
                 k_dense_build<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 4), WG, 0, stream_>>>(a, wD, wC);
+                k_dense_lists<<<s.numImages, 64, 0, stream_>>>(a);
                 BF_LAUNCH_CHECK();
             }
             k_pair_stats<<<(unsigned)numCUs_ * 4, WG, 0, stream_>>>(a);
@@ -2057,8 +2121,10 @@ void Solver::solve(const SolveArgs& s) {
         if (dense) {
             k_dense_reset<<<64, WG, 0, stream_>>>(a);
             k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);
+            k_dense_compact<<<1, 1024, 0, stream_>>>(a);
             k_dense_count<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 8), WG, 0, stream_>>>(a);
             k_dense_build<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 4), WG, 0, stream_>>>(a, wD, wC);
+            k_dense_lists<<<s.numImages, 64, 0, stream_>>>(a);
             BF_LAUNCH_CHECK();
         }
         k_entries<<<rowGrid, WG, 0, stream_>>>(a);

@@ -66,7 +66,7 @@ __device__ __forceinline__ void mc_voxel(const McArgs& A, const Nbhd& nb, f3 pos
     if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
     if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
     if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
-    const BFVoxel* vp = A.voxels + ptr + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+    const BFVoxel* vp = A.voxels + (size_t)ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
     sdf = vp->sdf;
     weight = vp->weight;
     color = *reinterpret_cast<const uint32_t*>(vp->color);

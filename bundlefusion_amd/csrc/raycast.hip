@@ -138,7 +138,7 @@ __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 po
     if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
     if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
     if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
-    const BFVoxel* vp = R.voxels + c.ptr + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+    const BFVoxel* vp = R.voxels + (size_t)c.ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
     sdf = vp->sdf;
     weight = vp->weight;
     color = *reinterpret_cast<const uint32_t*>(vp->color);

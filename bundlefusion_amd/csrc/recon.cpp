@@ -117,8 +117,9 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     BF_HIP(hipMemsetAsync(dGlobalTrans_.p, 0, dGlobalTrans_.bytes(), baStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
 
-    const char* btEnv = std::getenv("BF_BA_THREAD");
-    baThreaded_ = btEnv && std::atoi(btEnv) == 1;  // measured: no gain in the bench (the scene stream stays fed)
+    // asyncBundling 2: the solves are issued from a bundling thread (measured: no gain in the bench, the
+    // scene stream stays fed either way)
+    baThreaded_ = opt_.asyncBundling == 2;
     if (baThreaded_) baThread_ = std::thread([this] { baLoop(); });
     ring_.resize(RING);
     for (Pending& p : ring_) {

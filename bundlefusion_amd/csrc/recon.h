@@ -146,7 +146,7 @@ private:
     std::deque<uint32_t> inflight_;     // ring indices in submap order
     uint32_t ringNext_ = 0;
 
-    // Bundling thread (the reference's bundling thread, OnlineBundler), BF_BA_THREAD=1: a submap's
+    // Bundling thread (the reference's bundling thread, OnlineBundler), asyncBundling = 2: a submap's
     // local + global solves are ~450 kernel launches; the frame loop posts them as one job and this
     // thread issues them on baStream_ in post order, so the loop never spends the launch time. Off by
     // default (jobs run inline): without a profiler the host issues them faster than the scene stream

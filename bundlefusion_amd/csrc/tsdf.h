@@ -99,6 +99,7 @@ public:
     void resetStats();
     void exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
     uint32_t exportVisible(int4* out, uint32_t cap);
+    void exportBlockVoxels(uint32_t first, uint32_t count, BFVoxel* out);
     uint32_t exportBlocks(int4* out, uint32_t cap);  // blockPos[0, highWater): {x, y, z, allocated}
 
     const SceneConfig& config() const { return cfg_; }

@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) void k_alloc_birth(HashArgs A, const unsigned 
         const i3 b = key_block(cand[i]);
         const int ptr = lookup_ptr(A, b.x, b.y, b.z);
         if (ptr == BF_FREE_ENTRY) continue;  // not inserted (hash / heap full: flagged in ctrl)
-        atomicMax(&birth[(uint32_t)ptr / BF_VOXELS_PER_BLOCK], (epoch << 8) | (255u - candOp[i]));
+        atomicMax(&birth[(uint32_t)ptr], (epoch << 8) | (255u - candOp[i]));
     }
 }
 
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256) void k_alloc_insert(HashArgs A, const unsigned
                 if (ok) {
                     const uint32_t blk = A.heap[old - rank];
                     e[1] = make_int4(0, 0, 0, 0);
-                    e[0] = make_int4(p.x, p.y, p.z, (int)(blk * BF_VOXELS_PER_BLOCK));
+                    e[0] = make_int4(p.x, p.y, p.z, (int)blk);
                     A.blockPos[blk] = make_int4(p.x, p.y, p.z, 1);
                     atomicMax(&A.ctrl[C_HIGHWATER], blk + 1);
                     allocated++;
@@ -649,7 +649,7 @@ __device__ void alloc_overflow_serial(const HashArgs& A, const unsigned long lon
             newOffset = (uint32_t)offset;
         }
         (void)newOffset;
-        e.ptr = (int)(blk * BF_VOXELS_PER_BLOCK);
+        e.ptr = (int)blk;
         A.blockPos[blk] = make_int4(pos.x, pos.y, pos.z, 1);
         if (blk + 1 > A.ctrl[C_HIGHWATER]) A.ctrl[C_HIGHWATER] = blk + 1;
         A.stats[S_ALLOC]++;
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(256) void k_compactify(HashArgs A, BFDepthCameraPar
             off0 += s_cnt[0][k];
             off1 += s_cnt[1][k];
         }
-        const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
+        const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)i);
         if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
         if (inb) A.band[off1 + __popcll(m1 & lanemask_lt())] = ent;
         scanned += alloc ? 1 : 0;
@@ -836,19 +836,18 @@ __device__ __forceinline__ void voxel_deintegrate_f(float& s0, float& w0, uint32
 // (v_pk_mul_f32 / v_pk_add_f32: two IEEE results per instruction, no contraction). The exactness
 // check and the IEEE fallback of proj_coord follow per element.
 typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ int proj_fix(float num, float den, float qa, float m, float t) {
-    const float eps = (fabsf(qa) + 2.0f * fabsf(t) + 2.0f) * 0x1p-21f;
-    const bool need = !(fabsf(t - rintf(t)) > eps);
-    if (__builtin_amdgcn_ballot_w64(need)) {
-        asm volatile("" ::: "memory");
-        const float te = (num / den + m) + 0.5f;
-        t = need ? te : t;
-    }
-    return f2i(t);
-}
-// b_r = e[4r] wx + e[4r+1] wy: the (x, y) part of every row, computed once per lane column and op
+// Exactness test of a rounded screen coordinate t = (num * rcp(den) + m) + 0.5 against a bound that
+// is constant per launch: eps_c = (3 (max(W, H) + 2) + max(|mx|, |my|) + 3) 2^-21 is at least
+// proj_coord's per-lane bound (|qa| + 2 |t| + 2) 2^-21 for every lane with |t| <= max(W, H) + 2.
+// Lanes beyond that are off-screen for the fast and the exact quotient alike (their distance to the
+// screen exceeds the quotient error), so the pixel decision is the IEEE one everywhere.
+__device__ __forceinline__ bool proj_needs_exact(float t, float epsc) { return !(fabsf(t - rintf(t)) > epsc); }
+// b_r = e[4r] wx + e[4r+1] wy: the (x, y) part of every row, computed once per lane column and op.
+// Outputs the byte offsets of the two voxels' pixels in the op's {depth, colour} image, or
+// 0xFFFFFFFF off-screen (wc = 0 forces every pixel off-screen: an op without colour, :441-448);
+// uy * W + ux in 24-bit multiplies (the image is far below 2^24 pixels a side).
 __device__ __forceinline__ void voxel_pixel2b(const BFDepthCameraParams& cam, const BFMat4& T, const float* b, f2v wz,
-                                              bool haveColor, uint32_t& pix0, uint32_t& pix1, f2v& pz) {
+                                              uint32_t wc, float epsc, uint32_t& off0, uint32_t& off1, f2v& pz) {
     const float* e = T.m;
     f2v p[3];
 #pragma unroll
@@ -856,15 +855,23 @@ __device__ __forceinline__ void voxel_pixel2b(const BFDepthCameraParams& cam, co
     const f2v nx = p[0] * f2v{cam.fx, cam.fx}, ny = p[1] * f2v{cam.fy, cam.fy};
     const f2v rz = f2v{__builtin_amdgcn_rcpf(p[2].x), __builtin_amdgcn_rcpf(p[2].y)};
     const f2v qx = nx * rz, qy = ny * rz;
-    const f2v tx = (qx + f2v{cam.mx, cam.mx}) + f2v{0.5f, 0.5f};
-    const f2v ty = (qy + f2v{cam.my, cam.my}) + f2v{0.5f, 0.5f};
-    const uint32_t ux0 = (uint32_t)proj_fix(nx.x, p[2].x, qx.x, cam.mx, tx.x);
-    const uint32_t ux1 = (uint32_t)proj_fix(nx.y, p[2].y, qx.y, cam.mx, tx.y);
-    const uint32_t uy0 = (uint32_t)proj_fix(ny.x, p[2].x, qy.x, cam.my, ty.x);
-    const uint32_t uy1 = (uint32_t)proj_fix(ny.y, p[2].y, qy.y, cam.my, ty.y);
+    f2v tx = (qx + f2v{cam.mx, cam.mx}) + f2v{0.5f, 0.5f};
+    f2v ty = (qy + f2v{cam.my, cam.my}) + f2v{0.5f, 0.5f};
+    const bool nx0 = proj_needs_exact(tx.x, epsc), nx1 = proj_needs_exact(tx.y, epsc);
+    const bool ny0 = proj_needs_exact(ty.x, epsc), ny1 = proj_needs_exact(ty.y, epsc);
+    if (__builtin_amdgcn_ballot_w64(nx0 | nx1 | ny0 | ny1)) {  // ~1e-4 of lanes: the IEEE quotients
+        asm volatile("" ::: "memory");
+        if (nx0) tx.x = (nx.x / p[2].x + cam.mx) + 0.5f;
+        if (nx1) tx.y = (nx.y / p[2].y + cam.mx) + 0.5f;
+        if (ny0) ty.x = (ny.x / p[2].x + cam.my) + 0.5f;
+        if (ny1) ty.y = (ny.y / p[2].y + cam.my) + 0.5f;
+    }
+    const uint32_t ux0 = (uint32_t)f2i(tx.x), ux1 = (uint32_t)f2i(tx.y);
+    const uint32_t uy0 = (uint32_t)f2i(ty.x), uy1 = (uint32_t)f2i(ty.y);
+    const uint32_t W8 = cam.imageWidth * 8u;
     pz = p[2];
-    pix0 = (ux0 < cam.imageWidth && uy0 < cam.imageHeight && haveColor) ? uy0 * cam.imageWidth + ux0 : 0xFFFFFFFFu;
-    pix1 = (ux1 < cam.imageWidth && uy1 < cam.imageHeight && haveColor) ? uy1 * cam.imageWidth + ux1 : 0xFFFFFFFFu;
+    off0 = ((ux0 < wc) & (uy0 < cam.imageHeight)) ? __umul24(uy0, W8) + (ux0 << 3) : 0xFFFFFFFFu;
+    off1 = ((ux1 < wc) & (uy1 < cam.imageHeight)) ? __umul24(uy1, W8) + (ux1 << 3) : 0xFFFFFFFFu;
 }
 
 // Band test of one voxel for one pose (CUDASceneRepHashSDF.cu:449-466): sdf clamped to +-truncation.
@@ -929,7 +936,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             if (in) {
                 band |= 1u << zi;
                 // one 12-B load per voxel (global_load_dwordx3) instead of three dword loads
-                const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane));
+                const Vox3 v = *reinterpret_cast<const Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK + (uint32_t)(z * 64 + lane));
                 osdf[zi] = __uint_as_float(v.a);
                 ow[zi] = __uint_as_float(v.b);
                 oc[zi] = v.c;
@@ -966,7 +973,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             nv.a = __float_as_uint(nsdf);
             nv.b = __float_as_uint(nw);
             nv.c = ncol;
-            *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w + (uint32_t)(z * 64 + lane)) = nv;  // dwordx3 store
+            *reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK + (uint32_t)(z * 64 + lane)) = nv;  // dwordx3 store
             // per-block count of voxels with (uint)weight != 0 (GC decision, :606/:625)
             dcount += (int)(nw >= 1.0f) - (int)(w0 >= 1.0f);
             nupd++;
@@ -975,7 +982,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         const unsigned long long anyChange = __ballot(dcount != 0);
         if (anyChange) {
             for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
-            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[(uint32_t)e.w / BF_VOXELS_PER_BLOCK], (uint32_t)dcount);
+            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[(uint32_t)e.w], (uint32_t)dcount);
         }
         updated += nupd;
     }
@@ -1075,7 +1082,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         __syncthreads();
         uint32_t off0 = s_base;
         for (uint32_t k = 0; k < wv; k++) off0 += s_cnt[k];
-        const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)(i * BF_VOXELS_PER_BLOCK));
+        const int4 ent = make_int4(bp.x, bp.y, bp.z, (int)i);
         if (keepVis) A.visible[off0 + __popcll(m0 & lanemask_lt())] = ent;
         if (inb) {
             const size_t k = (size_t)bin * binCap + s_bbase[bin] + local;
@@ -1135,9 +1142,10 @@ template <int ZR, int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks, uint32_t binCap) {
     const uint32_t lane = lane_id();
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lx = lane & 7, ly = lane >> 3;
+    const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
     uint32_t updated = 0, rmw = 0;  // per lane and launch: < 2^32
     WorkCursor cur = work_begin(A.ctrl, ops.n);
     size_t b;
@@ -1145,11 +1153,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int4 ev = A.band[b];  // wave-uniform: keep the block's coordinates and base in SGPRs
         const int4 e = make_int4(__builtin_amdgcn_readfirstlane(ev.x), __builtin_amdgcn_readfirstlane(ev.y),
                                  __builtin_amdgcn_readfirstlane(ev.z), __builtin_amdgcn_readfirstlane(ev.w));
-        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
+        const uint32_t blk = (uint32_t)e.w;
         const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
-        Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w) + lane;
+        Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK) + lane;
         int dcount = 0;
         uint32_t nupd = 0, nrmw = 0;
 #pragma unroll
@@ -1174,7 +1182,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 // off-screen lane's out-of-range offset reads 0 without a branch
                 const __amdgpu_buffer_rsrc_t dcRsrc =
                     __builtin_amdgcn_make_buffer_rsrc((void*)ops.dc[k], (short)0, (int)(cam.imageWidth * cam.imageHeight * 8u), 0x00020000);
-                const bool haveColor = ops.color[k] != nullptr;
+                const uint32_t wc = ops.color[k] != nullptr ? cam.imageWidth : 0u;
                 const bool deint = (ops.deintMask >> k) & 1u;
 #pragma unroll
                 for (int z0 = 0; z0 < ZR; z0 += ZC) {
@@ -1184,16 +1192,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     for (int zi = 0; zi < ZC; zi += 2) {
                         const f2v wz = f2v{(float)(bz + h + z0 + zi), (float)(bz + h + z0 + zi + 1)} * f2v{A.voxelSize, A.voxelSize};
                         f2v pz2;
-                        voxel_pixel2b(cam, Ti, bxy, wz, haveColor, pix[zi], pix[zi + 1], pz2);
+                        voxel_pixel2b(cam, Ti, bxy, wz, wc, epsc, pix[zi], pix[zi + 1], pz2);
                         pz[zi] = pz2.x;
                         pz[zi + 1] = pz2.y;
                     }
 #pragma unroll
                     for (int zi = 0; zi < ZC; zi++) {
-                        const bool on = pix[zi] != 0xFFFFFFFFu;
-                        const auto v = __builtin_amdgcn_raw_buffer_load_b64(dcRsrc, on ? pix[zi] * 8u : 0xFFFFFFFFu, 0, 0);
-                        d[zi] = on ? __uint_as_float(v[0]) : -INFINITY;  // off-screen: depth -inf, colour 0
-                        cc[zi] = on ? v[1] : 0u;
+                        // off-screen lanes read past the descriptor's range: {0, 0}, depth set to -inf
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b64(dcRsrc, pix[zi], 0, 0);
+                        d[zi] = pix[zi] != 0xFFFFFFFFu ? __uint_as_float(v[0]) : -INFINITY;
+                        cc[zi] = v[1];
                     }
 #pragma unroll
                     for (int zi = 0; zi < ZC; zi++) {
@@ -1239,7 +1247,7 @@ __global__ __launch_bounds__(256) void k_gc_identify(HashArgs A, int4* simple, u
     const uint32_t nvis = A.ctrl[C_VISIBLE];
     for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nvis; b += gridDim.x * blockDim.x) {
         const int4 e = A.visible[b];
-        const uint32_t blk = (uint32_t)e.w / BF_VOXELS_PER_BLOCK;
+        const uint32_t blk = (uint32_t)e.w;
         if (A.blockCount[blk] != 0) continue;
         if (A.blockPos[blk].w == 0) continue;  // already freed by an earlier GC on this list
         const uint32_t h = hash_bucket(e.x, e.y, e.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
@@ -1269,7 +1277,7 @@ __global__ __launch_bounds__(256) void k_gc_free_simple(HashArgs A, const int4* 
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t k = wave; k < n; k += nwaves) {
         const int4 v = simple[k];
-        const uint32_t blk = (uint32_t)v.y / BF_VOXELS_PER_BLOCK;
+        const uint32_t blk = (uint32_t)v.y;
         if (lane == 0) {
             int4* e = reinterpret_cast<int4*>(A.hash + v.x);
             e[0] = make_int4(0, 0, 0, BF_FREE_ENTRY);
@@ -1349,7 +1357,7 @@ __global__ void k_gc_free_list(HashArgs A, unsigned long long* listV) {
             }
         }
         if (delPtr >= 0) {
-            const uint32_t blk = (uint32_t)delPtr / BF_VOXELS_PER_BLOCK;
+            const uint32_t blk = (uint32_t)delPtr;
             const uint32_t addr = A.ctrl[C_HEAP]++;
             A.heap[addr + 1] = blk;
             A.blockPos[blk] = make_int4(0, 0, 0, 0);
@@ -1396,7 +1404,10 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
 
 Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
     BF_REQUIRE(cfg.hp.hashNumBuckets > 0 && cfg.hp.numSDFBlocks > 0, BF_ERR_ARG, "empty hash/heap");
-    BF_REQUIRE(cfg.hp.numSDFBlocks <= (1u << 22), BF_ERR_CAPACITY, "numSDFBlocks exceeds the int ptr range (4194304 blocks)");
+    // HashEntry.ptr holds the heap block index inside the scene (voxel address = ptr * 512 in 64 bits):
+    // the reference's int32 voxel index (ptr = block * 512, VoxelUtilHashSDF.h:60,609) stops at 2^22
+    // blocks (25.8 GB of voxels); block indices reach 2^31 - 1, beyond what one GPU's HBM holds
+    BF_REQUIRE(cfg.hp.numSDFBlocks < (1u << 31), BF_ERR_CAPACITY, "numSDFBlocks exceeds the int block-index range");
     BF_REQUIRE((uint64_t)cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE < (1ull << 31), BF_ERR_CAPACITY, "hash too large");
     BF_REQUIRE(cfg.hp.virtualVoxelSize > 0, BF_ERR_ARG, "voxel size");
     E_ = cfg.hp.hashNumBuckets * BF_HASH_BUCKET_SIZE;
@@ -1691,12 +1702,21 @@ BFTsdfStats Scene::stats() {
 
 void Scene::resetStats() { BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_)); }
 
+// Dumps use the reference's units: ptr = heap block * 512 (the voxel index of the block's first
+// voxel), which an int32 holds up to 2^22 blocks; larger scenes dump blocks and voxels by heap block
+// (exportBlocks, exportBlockVoxels).
+static inline int32_t ref_ptr(int32_t blk) { return blk >= 0 ? blk * BF_VOXELS_PER_BLOCK : blk; }
+
 void Scene::exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels) {
+    BF_REQUIRE(hash == nullptr || (uint64_t)B_ <= (1ull << 22), BF_ERR_CAPACITY,
+               "hash dump in the reference's voxel-index ptr needs numSDFBlocks <= 2^22 (use bf_scene_export_blocks)");
     if (hash) BF_HIP(hipMemcpyAsync(hash, hash_.p, hash_.bytes(), hipMemcpyDeviceToHost, stream_));
     if (heap) BF_HIP(hipMemcpyAsync(heap, heap_.p, heap_.bytes(), hipMemcpyDeviceToHost, stream_));
     if (heapCounter) BF_HIP(hipMemcpyAsync(heapCounter, ctrl_.p + C_HEAP, 4, hipMemcpyDeviceToHost, stream_));
     if (voxels) BF_HIP(hipMemcpyAsync(voxels, voxels_.p, voxels_.bytes(), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
+    if (hash)
+        for (uint32_t i = 0; i < E_; i++) hash[i].ptr = ref_ptr(hash[i].ptr);
 }
 
 uint32_t Scene::exportBlocks(int4* out, uint32_t cap) {
@@ -1710,11 +1730,21 @@ uint32_t Scene::exportBlocks(int4* out, uint32_t cap) {
 }
 
 uint32_t Scene::exportVisible(int4* out, uint32_t cap) {
+    BF_REQUIRE((uint64_t)B_ <= (1ull << 22), BF_ERR_CAPACITY, "visible dump in voxel-index ptr needs numSDFBlocks <= 2^22");
     uint32_t n = numVisible();
     n = std::min(n, cap);
     if (n) BF_HIP(hipMemcpyAsync(out, visible_.p, n * sizeof(int4), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
+    for (uint32_t i = 0; i < n; i++) out[i].w = ref_ptr(out[i].w);
     return n;
+}
+
+void Scene::exportBlockVoxels(uint32_t first, uint32_t count, BFVoxel* out) {
+    BF_REQUIRE((uint64_t)first + count <= B_, BF_ERR_ARG, "heap block range out of bounds");
+    if (count)
+        BF_HIP(hipMemcpyAsync(out, voxels_.p + (size_t)first * BF_VOXELS_PER_BLOCK, (size_t)count * BF_VOXELS_PER_BLOCK * sizeof(BFVoxel),
+                              hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
 }
 
 }  // namespace bf

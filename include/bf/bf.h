@@ -102,13 +102,18 @@ int bf_scene_error_flags(bf_scene* s, uint32_t* flags);
 int bf_scene_get_stats(bf_scene* s, BFTsdfStats* out);
 int bf_scene_reset_stats(bf_scene* s);
 /* debugHash-style dump to HOST memory (CUDASceneRepHashSDF.h:179-314): any pointer may be NULL.
- * hash: BFHashEntry[4*numBuckets], heap: uint32[numSDFBlocks], voxels: BFVoxel[numSDFBlocks*512] */
+ * hash: BFHashEntry[4*numBuckets], heap: uint32[numSDFBlocks], voxels: BFVoxel[numSDFBlocks*512].
+ * Entries carry the reference's ptr (heap block * 512), so a hash dump needs numSDFBlocks <= 2^22
+ * (BF_ERR_CAPACITY otherwise); larger scenes dump with bf_scene_export_blocks / _block_voxels. */
 int bf_scene_export(bf_scene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
 /* heap blocks [0, highWater) to HOST: int32 {x, y, z, allocated} per block (heap order); min(cap, n) written,
  * *n = highWater (the allocated prefix compactify streams) */
 int bf_scene_export_blocks(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n);
 /* visible list of the last compactify to HOST: int32 {x,y,z,ptr} x n */
 int bf_scene_export_visible(bf_scene* s, int32_t* out4, uint32_t cap, uint32_t* n);
+/* voxels of heap blocks [first, first + count) to HOST: BFVoxel[count * 512] (block i's run is the
+ * voxels at voxel index i * 512, VoxelUtilHashSDF.h:609); the dump of scenes above 2^22 blocks */
+int bf_scene_export_block_voxels(bf_scene* s, uint32_t first, uint32_t count, BFVoxel* out);
 /* CUDARayCastSDF::render (CUDARayCastSDF.cpp:38-72) preceded by setLastRigidTransformAndCompactify
  * (CUDASceneRepHashSDF.h:128-139): camera->world T, frustum camera params cam (render depth range),
  * ray-cast params rp (intrinsics, size, minDepth/maxDepth, rayIncrement, thresholds, useGradients;
@@ -281,7 +286,8 @@ typedef struct BFReconOptions {
     int32_t recordOps;           /* keep a log of every scene call (parity replay in tests) */
     int32_t asyncBundling;       /* 1: solves run on their own stream and their poses are picked up
                                     by the frame loop when ready (the reference's bundling thread);
-                                    0: the loop waits for each submap's solves (deterministic) */
+                                    0: the loop waits for each submap's solves (deterministic);
+                                    2: as 1, with the solves issued from a separate host thread */
     BFSolverOptions solver;
     int32_t disableLocalVerify;  /* 0: s_useLocalVerify = true (zParametersBundlingDefault.txt:62): after each local
                                     solve useVerification + VerifyTrajectoryCU; a failing submap is invalidated

@@ -40,7 +40,9 @@ typedef struct BFInt3 { int32_t x, y, z; } BFInt3;
 
 typedef struct __attribute__((aligned(16))) BFHashEntry {
     int32_t x, y, z;   /* SDF block coordinate (lower-left corner / 8) */
-    int32_t ptr;       /* voxel index of the block's first voxel (= heap block * 512), or FREE/LOCK */
+    int32_t ptr;       /* dumps: voxel index of the block's first voxel (= heap block * 512, the reference's
+                          unit), or FREE/LOCK; on the device the scene keeps the heap block index here so
+                          that more than 2^22 blocks fit (bf_scene_export converts) */
     uint32_t offset;   /* collision-list offset relative to the bucket's last slot */
     int32_t pad[3];
 } BFHashEntry;

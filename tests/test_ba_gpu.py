@@ -359,6 +359,24 @@ def test_solve_bit_deterministic(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("K", [6, 72])
+def test_dense_solve_bit_deterministic(mode, K):
+    """The dense term in a fixed order: overlapping pairs compacted in (i, j) order, each image's
+    diagonal block, J^T r and off-diagonal products summed over its pairs in pair order (the
+    reference adds them with float atomics). Two dense solves of one problem agree bit for bit, both
+    through the one-workgroup PCG (K = 6) and the grid-wide PCG with the per-pair products handed to
+    the finisher (K = 72)."""
+    prob = make_problem(K=K, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
+    args = (2, 40, [1, 1], [1000, 1000], [0, 0])
+    a = gpu_solve(prob, *args, use_cache=True, mode=mode)
+    b = gpu_solve(prob, *args, use_cache=True, mode=mode)
+    assert a[3]["numDensePairs"] > (0 if K == 6 else 20)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_many_images_multipass_finisher(mode):
     """More than 2 x 256 images: the PCG finisher takes its multi-pass path (rows do not fit the
     register-resident form); one GN step with a few PCG iterations tracks the oracle tightly."""

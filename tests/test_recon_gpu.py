@@ -39,7 +39,7 @@ def run_loop(F=40, W=160, H=120, voxel=0.01, record=True, drift=(0.05, 0.002), a
     return st, params, rc
 
 
-@pytest.fixture(scope="module", params=[0, 1], ids=["sync", "async"])
+@pytest.fixture(scope="module", params=[0, 1, 2], ids=["sync", "async", "thread"])
 def loop(request):
     return run_loop(async_ba=request.param)
 
