@@ -918,7 +918,7 @@ int bf_cache_create(const BFCacheOptions* o, bf_cache** out) {
     try {
         h->c = new Cache(cfg, h->stream);
     } catch (...) {
-        hipStreamDestroy(h->stream);
+        (void)hipStreamDestroy(h->stream);
         throw;
     }
     *out = h.release();
@@ -927,9 +927,9 @@ int bf_cache_create(const BFCacheOptions* o, bf_cache** out) {
 int bf_cache_destroy(bf_cache* c) {
     BF_TRY
     if (!c) return 0;
-    hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream);
     delete c->c;
-    hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->stream);
     delete c;
     BF_CATCH
 }

@@ -1381,13 +1381,13 @@ __global__ void k_dense_overlap(BA a) {
 
 // The overlapping pairs in (i, j) order (the reference appends them at atomic offsets): one workgroup
 // compacts the flag matrix with wave ballots; K_NPAIRS = all pairs found, the first maxPairs are kept.
-__global__ __launch_bounds__(1024) void k_dense_compact(BA a) {
-    __shared__ uint32_t sCnt[16], sBase;
+__global__ __launch_bounds__(256) void k_dense_compact(BA a) {
+    __shared__ uint32_t sCnt[4], sBase;
     if (a.ctrl[K_GN_DONE]) return;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, NN = a.N * a.N;
     if (threadIdx.x == 0) sBase = 0;
     __syncthreads();
-    for (uint32_t b0 = 0; b0 < NN; b0 += 1024) {
+    for (uint32_t b0 = 0; b0 < NN; b0 += 256) {
         const uint32_t idx = b0 + threadIdx.x;
         const bool f = idx < NN && a.pairFlag[idx] != 0u;
         const unsigned long long m = __ballot(f);
@@ -1398,7 +1398,7 @@ __global__ __launch_bounds__(1024) void k_dense_compact(BA a) {
         off += (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         if (f && off < a.maxPairs) a.pairs[off] = make_uint2(idx / a.N, idx % a.N);
         __syncthreads();
-        if (threadIdx.x == 0) for (uint32_t w = 0; w < 16; w++) sBase += sCnt[w];
+        if (threadIdx.x == 0) for (uint32_t w = 0; w < 4; w++) sBase += sCnt[w];
         __syncthreads();
     }
     if (threadIdx.x == 0) a.ctrl[K_NPAIRS] = sBase;
@@ -2098,7 +2098,7 @@ void Solver::solve(const SolveArgs& s) {
             if (dense) {
                 k_dense_reset<<<64, WG, 0, stream_>>>(a);
                 k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);
-                k_dense_compact<<<1, 1024, 0, stream_>>>(a);
+                k_dense_compact<<<1, 256, 0, stream_>>>(a);
                 k_dense_count<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 8), WG, 0, stream_>>>(a);
                 k_dense_build<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 4), WG, 0, stream_>>>(a, wD, wC);
                 k_dense_lists<<<s.numImages, 64, 0, stream_>>>(a);
@@ -2121,7 +2121,7 @@ void Solver::solve(const SolveArgs& s) {
         if (dense) {
             k_dense_reset<<<64, WG, 0, stream_>>>(a);
             k_dense_overlap<<<dim3(s.numImages, s.numImages), 64, 0, stream_>>>(a);
-            k_dense_compact<<<1, 1024, 0, stream_>>>(a);
+            k_dense_compact<<<1, 256, 0, stream_>>>(a);
             k_dense_count<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 8), WG, 0, stream_>>>(a);
             k_dense_build<<<std::min(a.maxPairs, (uint32_t)numCUs_ * 4), WG, 0, stream_>>>(a, wD, wC);
             k_dense_lists<<<s.numImages, 64, 0, stream_>>>(a);

@@ -56,6 +56,11 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
 
     BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
     BF_HIP(hipStreamCreateWithFlags(&baStream_, hipStreamNonBlocking));
+    BF_HIP(hipStreamCreateWithFlags(&localStream_, hipStreamNonBlocking));
+    for (int b = 0; b < 2; b++) {
+        BF_HIP(hipEventCreateWithFlags(&localDone_[b], hipEventDisableTiming));
+        BF_HIP(hipEventCreateWithFlags(&globalDone_[b], hipEventDisableTiming));
+    }
     SceneConfig sc{};
     sc.hp = hp;
     if (so) {
@@ -74,7 +79,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
         frameTiles_.alloc(tileStride_ * opt_.maxFrames);
         frameDC_.alloc(framePixels_ * opt_.maxFrames);
     }
-    local_.reset(new Solver(make_solver_config(S + 1, opt_.maxLocalCorr, &opt_.solver), baStream_));
+    local_.reset(new Solver(make_solver_config(S + 1, opt_.maxLocalCorr, &opt_.solver), localStream_));
     global_.reset(new Solver(make_solver_config(opt_.maxKeyframes, opt_.maxGlobalCorr, &opt_.solver), baStream_));
     tm_.reset(new TrajectoryManager(opt_.maxFrames, opt_.topNActive, opt_.minPoseDistSqrt));
     if (opt_.enableTiming) {
@@ -95,13 +100,15 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     globalValid_.assign(K, 1);
     complete_.resize(opt_.maxFrames);
 
-    dLocalRot_.alloc(6 * L + 1);
-    dLocalTrans_ = dLocalRot_.p + 3 * L;
-    dGate_ = reinterpret_cast<int*>(dLocalRot_.p + 6 * L);
+    for (LocalSet& b : ls_) {
+        b.rot.alloc(6 * L + 1);
+        b.trans = b.rot.p + 3 * L;
+        b.gate = reinterpret_cast<int*>(b.rot.p + 6 * L);
+        b.T.alloc(16 * L);
+        b.valid.alloc(L);
+        b.cache.alloc(L);
+    }
     dGlobalCache_.alloc(K);
-    dLocalT_.alloc(16 * L);
-    dLocalValid_.alloc(L);
-    dLocalCache_.alloc(L);
     dGlobalRot_.alloc(3 * K);
     dGlobalTrans_.alloc(3 * K);
     dGlobalT_.alloc(16 * K);
@@ -109,10 +116,12 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     dSeedT_.alloc(16);
     dOne_.alloc(1);
     std::vector<int> ones(std::max(L, K), 1);
-    BF_HIP(hipMemcpyAsync(dLocalValid_.p, ones.data(), 4 * L, hipMemcpyHostToDevice, baStream_));
+    for (LocalSet& b : ls_) {
+        BF_HIP(hipMemcpyAsync(b.valid.p, ones.data(), 4 * L, hipMemcpyHostToDevice, baStream_));
+        BF_HIP(hipMemcpyAsync(b.gate, ones.data(), 4, hipMemcpyHostToDevice, baStream_));
+    }
     BF_HIP(hipMemcpyAsync(dGlobalValid_.p, ones.data(), 4 * K, hipMemcpyHostToDevice, baStream_));
     BF_HIP(hipMemcpyAsync(dOne_.p, ones.data(), 4, hipMemcpyHostToDevice, baStream_));
-    BF_HIP(hipMemcpyAsync(dGate_, ones.data(), 4, hipMemcpyHostToDevice, baStream_));
     BF_HIP(hipMemsetAsync(dGlobalRot_.p, 0, dGlobalRot_.bytes(), baStream_));
     BF_HIP(hipMemsetAsync(dGlobalTrans_.p, 0, dGlobalTrans_.bytes(), baStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
@@ -146,6 +155,11 @@ Recon::~Recon() {
     }
     if (sceneStream_) (void)hipStreamSynchronize(sceneStream_);
     if (baStream_) (void)hipStreamSynchronize(baStream_);
+    if (localStream_) (void)hipStreamSynchronize(localStream_);
+    for (int b = 0; b < 2; b++) {
+        if (localDone_[b]) (void)hipEventDestroy(localDone_[b]);
+        if (globalDone_[b]) (void)hipEventDestroy(globalDone_[b]);
+    }
     for (Pending& p : ring_) {
         if (p.done) (void)hipEventDestroy(p.done);
         for (void* q : {(void*)p.localT, (void*)p.globalT, (void*)p.valid, (void*)p.ctrl, (void*)p.localInit,
@@ -157,6 +171,7 @@ Recon::~Recon() {
     global_.reset();
     if (sceneStream_) (void)hipStreamDestroy(sceneStream_);
     if (baStream_) (void)hipStreamDestroy(baStream_);
+    if (localStream_) (void)hipStreamDestroy(localStream_);
 }
 
 void Recon::setFrame(uint32_t f, const float* depth, const uint8_t* color, const BFCachedFrame* cache, const BFMat4& Tinc) {
@@ -374,76 +389,86 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
                         std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk) {
     Pending& P = ring_[slot];
     const uint32_t L = S + 1;
-    BF_HIP(hipMemcpyAsync(dLocalT_.p, P.localInit, 64 * n, hipMemcpyHostToDevice, baStream_));
-    matrices_to_poses(dLocalT_.p, n, dLocalRot_.p, dLocalTrans_, dLocalValid_.p, baStream_);
+    const int bi = (int)(s & 1u);
+    LocalSet& B = ls_[bi];
+    // ---- local solve over frames base .. base+n-1 (first frame fixed), on the local stream ----------
+    // set bi was last read by global solve s - 2
+    BF_HIP(hipStreamWaitEvent(localStream_, globalDone_[bi], 0));
+    BF_HIP(hipMemcpyAsync(B.T.p, P.localInit, 64 * n, hipMemcpyHostToDevice, localStream_));
+    matrices_to_poses(B.T.p, n, B.rot.p, B.trans, B.valid.p, localStream_);
     // multi-GPU: submap s's local solve runs on rank s % R only (the submaps are independent units,
     // SURVEY.md §8(e)2); its poses and verification outcome are then broadcast so that every rank
-    // continues identically
+    // continues identically. The broadcast goes on the BA stream (the communicator's one order on
+    // every rank), after the owner's solve; the solve itself overlaps the previous global solve.
     const bool shardLocal = comm_ && comm_->size() > 1;
     const int localOwner = shardLocal ? (int)(s % (uint32_t)comm_->size()) : 0;
     const bool solveHere = !shardLocal || localOwner == comm_->rank();
     const bool verify = opt_.disableLocalVerify == 0;
     const size_t bcast = 6 * (size_t)L + 1;  // [rot | trans | gate]
-    if (n >= 2 && lc.first && lc.second > 0 && !solveHere) {
-        comm_->broadcast(dLocalRot_.p, bcast, localOwner, baStream_);
-        poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
-        BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
-    } else if (n >= 2 && lc.first && lc.second > 0) {
+    const bool haveLocal = n >= 2 && lc.first && lc.second > 0;
+    if (haveLocal && solveHere) {
         if (haveCache)
-            BF_HIP(hipMemcpyAsync(dLocalCache_.p, P.cacheTable, sizeof(BFCachedFrame) * n, hipMemcpyHostToDevice, baStream_));
+            BF_HIP(hipMemcpyAsync(B.cache.p, P.cacheTable, sizeof(BFCachedFrame) * n, hipMemcpyHostToDevice, localStream_));
         std::vector<float> ws(opt_.localNonLin, 1.0f), wd(opt_.localNonLin), wc(opt_.localNonLin, 0.0f);
         for (uint32_t i = 0; i < opt_.localNonLin; i++) wd[i] = haveCache ? (float)(i + 1) : 0.0f;  // SBA.cpp:28-31
         SolveArgs a{};
         a.corr = lc.first;
         a.numCorr = lc.second;
-        a.valid = dLocalValid_.p;
+        a.valid = B.valid.p;
         a.numImages = n;
         a.nNonLin = opt_.localNonLin;
         a.nLin = opt_.localLin;
         a.wSparse = ws.data();
         a.wDenseDepth = wd.data();
         a.wDenseColor = wc.data();
-        a.cache = haveCache ? dLocalCache_.p : nullptr;
+        a.cache = haveCache ? B.cache.p : nullptr;
         a.cacheW = opt_.cacheWidth;
         a.cacheH = opt_.cacheHeight;
         std::memcpy(a.intrinsics, opt_.cacheIntrinsics, sizeof(a.intrinsics));
-        a.rot = dLocalRot_.p;
-        a.trans = dLocalTrans_;
+        a.rot = B.rot.p;
+        a.trans = B.trans;
         a.rebuildJT = true;
         // optimizeLocal removes no max residual (OnlineBundler.cpp:255-256); the residual analysis
         // only counts the high residuals useVerification asks for
         a.findMaxResidual = verify;
         local_->solve(a);
-        poses_to_matrices(dLocalRot_.p, dLocalTrans_, n, dLocalT_.p, dLocalValid_.p, baStream_);
+        poses_to_matrices(B.rot.p, B.trans, n, B.T.p, B.valid.p, localStream_);
         // SBA::align :106-109 -> Bundler::optimize :259-274 (needs the submap's cache frames)
         const bool check = verify && haveCache;
         if (check) {
             VerifyParams vp = verify_params(&opt_.verify);
-            vp.T = dLocalT_.p;
-            vp.valid = dLocalValid_.p;
+            vp.T = B.T.p;
+            vp.valid = B.valid.p;
             vp.numImages = n;
-            vp.cache = dLocalCache_.p;
+            vp.cache = B.cache.p;
             vp.cacheW = opt_.cacheWidth;
             vp.cacheH = opt_.cacheHeight;
             std::memcpy(vp.intrinsics, opt_.cacheIntrinsics, sizeof(vp.intrinsics));
             vp.numCorr = lc.second;
             local_->verify(vp);
         }
-        set_gate(dGate_, check ? local_->verifyFlag() : nullptr, baStream_);
+        set_gate(B.gate, check ? local_->verifyFlag() : nullptr, localStream_);
         local_->resultAsync(P.ctrl);
         P.localSolved = true;
-        if (shardLocal) comm_->broadcast(dLocalRot_.p, bcast, localOwner, baStream_);
-        BF_HIP(hipMemcpyAsync(P.localT, dLocalT_.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
-    } else {
-        set_gate(dGate_, nullptr, baStream_);
+    } else if (!haveLocal) {
+        set_gate(B.gate, nullptr, localStream_);
         std::memcpy(P.localT, P.localInit, 64 * n);
+    }
+    BF_HIP(hipEventRecord(localDone_[bi], localStream_));
+    BF_HIP(hipStreamWaitEvent(baStream_, localDone_[bi], 0));
+    if (haveLocal) {
+        if (shardLocal) {
+            comm_->broadcast(B.rot.p, bcast, localOwner, baStream_);
+            if (!solveHere) poses_to_matrices(B.rot.p, B.trans, n, B.T.p, B.valid.p, baStream_);
+        }
+        BF_HIP(hipMemcpyAsync(P.localT, B.T.p, 64 * n, hipMemcpyDeviceToHost, baStream_));
     }
     // ---- global solve over keyframes 0..s ---------------------------------------------------
     // an invalid local submap (gate 0) becomes an invalid keyframe without correspondences and its
     // global solve is skipped (processGlobal / optimizeGlobal INVALIDATE, OnlineBundler.cpp:351-360,
     // 399-405). Keyframe 0 is never invalidated (the reference exits on an invalid first chunk,
     // Bundler.cpp:377-384).
-    const int* gate = (verify && s > 0) ? dGate_ : nullptr;
+    const int* gate = (verify && s > 0) ? B.gate : nullptr;
     if (gate && globalCorr_) invalidate_local(gate, s, dGlobalValid_.p, globalCorr_, globalCorrN_, baStream_);
     const uint32_t ncorr = (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_;
     if (nk >= 2 && globalCorr_ && ncorr > 0) {
@@ -473,9 +498,10 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
     poses_to_matrices(dGlobalRot_.p, dGlobalTrans_.p, nk, dGlobalT_.p, dGlobalValid_.p, baStream_);
     BF_HIP(hipMemcpyAsync(P.globalT, dGlobalT_.p, 64 * nk, hipMemcpyDeviceToHost, baStream_));
     BF_HIP(hipMemcpyAsync(P.valid, dGlobalValid_.p, 4 * nk, hipMemcpyDeviceToHost, baStream_));
-    BF_HIP(hipMemcpyAsync(P.gate, dGate_, 4, hipMemcpyDeviceToHost, baStream_));
+    BF_HIP(hipMemcpyAsync(P.gate, B.gate, 4, hipMemcpyDeviceToHost, baStream_));
     // ---- initNextGlobalTransformCU (OnlineBundler.cu:112-140): keyframe s+1 from the last local
-    if (n == S + 1) seed_keyframe(dLocalRot_.p, dLocalTrans_, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_, gate);
+    if (n == S + 1) seed_keyframe(B.rot.p, B.trans, S, dGlobalRot_.p, dGlobalTrans_.p, s, baStream_, gate);
+    BF_HIP(hipEventRecord(globalDone_[bi], baStream_));
     BF_HIP(hipEventRecord(P.done, baStream_));
 }
 
@@ -713,6 +739,7 @@ void Recon::synchronize() {
     flushIntegrate();
     baDrain();
     BF_HIP(hipStreamSynchronize(sceneStream_));
+    BF_HIP(hipStreamSynchronize(localStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
     applyPending(true);
 }

@@ -93,7 +93,10 @@ private:
 
     BFReconOptions opt_;
     BFDepthCameraParams cam_;
-    hipStream_t sceneStream_ = nullptr, baStream_ = nullptr;
+    // baStream_: global solves (and the multi-GPU exchanges, in one order on every rank); localStream_:
+    // local solves, which depend only on their submap's frames, so submap s+1's local solve runs while
+    // submap s's global solve is still in flight
+    hipStream_t sceneStream_ = nullptr, baStream_ = nullptr, localStream_ = nullptr;
     std::unique_ptr<Scene> scene_;
     std::unique_ptr<Solver> local_, global_;
     std::unique_ptr<TrajectoryManager> tm_;
@@ -165,9 +168,17 @@ private:
     std::atomic<uint64_t> baDone_{0};  // jobs issued
     std::exception_ptr baErr_;
 
-    DevBuf<float> dLocalRot_, dLocalT_;  // dLocalRot_ holds [rot 3L | trans 3L | gate] (one broadcast)
-    float* dLocalTrans_ = nullptr;
-    int* dGate_ = nullptr;               // the submap's verification outcome, read by the gated global solve
+    // per-submap local state, double-buffered by submap parity: set s & 1 is written by local solve s
+    // and read by global solve s (gate, keyframe seed); local solve s + 2 waits for globalDone_[s & 1]
+    struct LocalSet {
+        DevBuf<float> rot, T;     // rot holds [rot 3L | trans 3L | gate] (one broadcast)
+        float* trans = nullptr;
+        int* gate = nullptr;      // the submap's verification outcome, read by the gated global solve
+        DevBuf<int> valid;
+        DevBuf<BFCachedFrame> cache;
+    };
+    LocalSet ls_[2];
+    hipEvent_t localDone_[2] = {nullptr, nullptr}, globalDone_[2] = {nullptr, nullptr};
     DevBuf<BFCachedFrame> dGlobalCache_; // keyframe k's cache frame (frame k * S), for the end-of-sequence dense solve
     struct SubmapRecord {  // recordOps history
         std::vector<BFMat4> local, global;
@@ -175,8 +186,6 @@ private:
         int localOk = 1;
     };
     std::vector<SubmapRecord> history_;
-    DevBuf<int> dLocalValid_;
-    DevBuf<BFCachedFrame> dLocalCache_;
     DevBuf<float> dGlobalRot_, dGlobalTrans_, dGlobalT_;
     DevBuf<int> dGlobalValid_;
     DevBuf<float> dSeedT_;
