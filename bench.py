@@ -460,7 +460,7 @@ def main():
     rdepth = routs[0].download()
     out["raycast"] = {"ms_per_render": t_r * 1e3, "k_render_us": (ms1 - ms0) / max(1, n1 - n0) * 1e3,
                       "valid_fraction": float(np.isfinite(rdepth).mean()),
-                      "note": "compactify + interval splat + renderKernel + computeNormals at 640x480 from the last pose"}
+                      "note": f"compactify + interval splat + renderKernel + computeNormals at {W_}x{H_} from the last pose"}
     # marching cubes over the final scene (StopScanningAndExtractIsoSurfaceMC, reported beside the metric)
     mcp = bfa.mc_params(params.virtualVoxelSize)
     mbuf = bfa.DeviceArray((mcp.maxNumTriangles, 3, 6), np.float32)
