@@ -75,6 +75,7 @@ def host_info() -> dict:
             "host_mem_copy_GBps": gbs}
 
 
+SHARD_CHUNK = 1.0  # metres: edge of the ownership chunks of the multi-GPU TSDF sharding
 PREFIX_FRAMES = 40  # the loop prefix the CPU oracle runs in full (and the GPU's time for it, untimed region)
 
 
@@ -293,7 +294,7 @@ def main():
     opts = recon_options(F, enableTiming=1, asyncBundling=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
                          maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2))
     so = BFSceneOptions()
-    so.shardCount, so.shardIndex, so.shardChunk = world, rank, 1.0
+    so.shardCount, so.shardIndex, so.shardChunk = world, rank, SHARD_CHUNK
     rc = Recon(params, stream.cam, opts, so)
     comm = None
     if world > 1 and os.environ.get("BF_BA_SHARD", "1") != "0":
@@ -441,7 +442,14 @@ def main():
         from bundlefusion_amd.dist import shard_balance
         blk = rc.export_blocks()
         blk = blk[blk[:, 3] != 0]
-        out["shard_balance"] = shard_balance(blk[:, :3], args.voxel, stream.gt[fill:frames_total:10], stream.cam)
+        poses_t = stream.gt[fill:frames_total:10]
+        out["shard_balance"] = shard_balance(blk[:, :3], args.voxel, poses_t, stream.cam, chunk=SHARD_CHUNK)
+        # max / mean over ranks of (stored blocks, in-frustum block-frames) for other ownership chunk sizes
+        out["shard_balance"]["by_chunk"] = {
+            f"{c:g}m": {g: [round(v["stored_max_over_mean"], 3), round(v["visible_max_over_mean"], 3)]
+                        for g, v in shard_balance(blk[:, :3], args.voxel, poses_t, stream.cam, chunk=c).items()
+                        if g.startswith("G")}
+            for c in (1.0, 0.5, 0.25, 0.125)}
     # raycast (visualizeFrame's render, reported beside the metric): 20 renders from the last pose
     W_, H_ = args.width, args.height
     rpr = bfa.raycast_params(W_, H_, fx=stream.cam.fx, fy=stream.cam.fy)

@@ -998,7 +998,12 @@ __device__ __forceinline__ void pack_dc(const OpTable& ops, uint32_t k, uint32_t
     const float* __restrict__ d = ops.depth[k];
     const uint32_t* __restrict__ c = ops.color[k];
     uint2* __restrict__ o = ops.dc[k];
-    for (uint32_t i = i0; i < P; i += stride) o[i] = make_uint2(__float_as_uint(d[i]), c[i]);
+    // a depth of +0.0 is stored as -0.0 (equal in every comparison and sum the voxel update makes), so
+    // the all-zero word a buffer load returns past the image's range marks "off-screen" by itself
+    for (uint32_t i = i0; i < P; i += stride) {
+        const uint32_t db = __float_as_uint(d[i]);
+        o[i] = make_uint2(db == 0u ? 0x80000000u : db, c[i]);
+    }
 }
 // per-op 8x8-tile depth bounds and dc image (blockIdx.y = op; workgroups [0, tileBlocks) build the
 // tiles, the rest the dc image) + the per-batch counter reset (ops whose frame already has both,
@@ -1198,9 +1203,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     }
 #pragma unroll
                     for (int zi = 0; zi < ZC; zi++) {
-                        // off-screen lanes read past the descriptor's range: {0, 0}, depth set to -inf
+                        // off-screen lanes read past the descriptor's range: {0, 0}, depth -> -inf
                         const auto v = __builtin_amdgcn_raw_buffer_load_b64(dcRsrc, pix[zi], 0, 0);
-                        d[zi] = pix[zi] != 0xFFFFFFFFu ? __uint_as_float(v[0]) : -INFINITY;
+                        d[zi] = v[0] != 0u ? __uint_as_float(v[0]) : -INFINITY;
                         cc[zi] = v[1];
                     }
 #pragma unroll

@@ -109,7 +109,7 @@ def chunk_owner_array(blocks, voxel_size: float, shard_count: int, chunk: float 
     return np.where(r < 0, r + shard_count, r).astype(np.int32)
 
 
-def shard_balance(blocks, voxel_size: float, poses, cam, shard_counts=(2, 4, 8)) -> dict:
+def shard_balance(blocks, voxel_size: float, poses, cam, shard_counts=(2, 4, 8), chunk: float = 1.0) -> dict:
     """Load balance of the chunk-ownership TSDF sharding for a final scene: per shard
     count G, the allocated blocks each rank stores and, over the given camera poses, the in-frustum
     allocated blocks each rank scans and updates (the per-frame voxel work, isInCameraFrustumApprox at
@@ -129,9 +129,9 @@ def shard_balance(blocks, voxel_size: float, poses, cam, shard_counts=(2, 4, 8))
         ny = ((cam.imageHeight - 1.0) - 2.0 * v) / (cam.imageHeight - 1.0) * 0.95
         nz = (z - cam.sensorDepthWorldMin) / (cam.sensorDepthWorldMax - cam.sensorDepthWorldMin) * 0.95
         vis += ((z > 0) & (np.abs(nx) <= 1) & (np.abs(ny) <= 1) & (nz >= 0) & (nz <= 1)).astype(np.int64)
-    out = {"blocks": int(len(b)), "frames": len(poses)}
+    out = {"blocks": int(len(b)), "frames": len(poses), "chunk_m": chunk}
     for G in shard_counts:
-        own = chunk_owner_array(b, voxel_size, G)
+        own = chunk_owner_array(b, voxel_size, G, chunk=chunk)
         stored = np.bincount(own, minlength=G)
         work = np.bincount(own, weights=vis, minlength=G)
         out[f"G{G}"] = {"stored_max_over_mean": float(stored.max() / max(stored.mean(), 1e-9)),
