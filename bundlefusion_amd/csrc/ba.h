@@ -20,6 +20,7 @@
 // are evaluated on the device, so there is no host round trip inside solve (the reference
 // copies scanAlpha to the host every PCG iteration, SolverBundling.cu:1089).
 #pragma once
+#include <vector>
 #include "../../include/bf/bf.h"
 #include "bf_math.h"
 #include "bf_runtime.h"
@@ -159,7 +160,7 @@ private:
     DevBuf<float> jtr_;      // [N][6]
     DevBuf<uint32_t> pairFlag_;  // [N][N]
     DevBuf<float> pairAcc_;      // [maxPairs][54]
-    DevBuf<float> pairProd_;     // [maxPairs][12]
+    DevBuf<float> pairProd_;     // [N][8]
     DevBuf<uint32_t> imgPairs_;  // [N][N]
     DevBuf<uint32_t> imgPairN_;  // [N]
     // assembled (pair) normal equations

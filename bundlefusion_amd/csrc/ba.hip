@@ -72,7 +72,7 @@ struct BA {
     // dense term in a fixed order (no float atomics, so two solves of one problem agree bit for bit):
     uint32_t* pairFlag;  // [N][N] overlap flag of (i, j), i < j (k_dense_overlap)
     float* pairAcc;      // [maxPairs][54] a pair's J_i^T J_i | J_j^T J_j upper triangles (21 + 21), J_i^T r | J_j^T r
-    float* pairProd;     // [maxPairs][12] per PCG iteration: B p_i (image j's rows) | B^T p_j (image i's rows)
+    float* pairProd;     // [N][8] per PCG iteration: image v's dense off-diagonal Ap rows [trans | rot]
     uint32_t* imgPairs;  // [N][N] pairs of image v in pair order: k << 1 | (v is the pair's j)
     uint32_t* imgPairN;  // [N]
     uint32_t maxPairs;
@@ -853,15 +853,10 @@ __device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, in
         }
         aT = aT + mk3(o6[0], o6[1], o6[2]);
         aR = aR + mk3(o6[3], o6[4], o6[5]);
-        // off-diagonal blocks: the row's pair products of this launch (write-through), in pair order
-        const uint32_t* L = a.imgPairs + (size_t)v * a.maxN;
-        const uint32_t nL = a.imgPairN[v];
-        for (uint32_t q = 0; q < nL; q++) {
-            const uint32_t e = L[q];
-            const float* pp = a.pairProd + (size_t)(e >> 1) * 12 + ((e & 1u) ? 0u : 6u);
-            aT = aT + mk3(ld_wtf(pp), ld_wtf(pp + 1), ld_wtf(pp + 2));
-            aR = aR + mk3(ld_wtf(pp + 3), ld_wtf(pp + 4), ld_wtf(pp + 5));
-        }
+        // off-diagonal blocks: the row's sum over its pairs of this launch (pcg_dense_offdiag, write-through)
+        const float* pp = a.pairProd + (size_t)v * 8;
+        aT = aT + mk3(ld_wtf(pp), ld_wtf(pp + 1), ld_wtf(pp + 2));
+        aR = aR + mk3(ld_wtf(pp + 3), ld_wtf(pp + 4), ld_wtf(pp + 5));
     }
 }
 
@@ -923,29 +918,34 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
     return rDotzNew;
 }
 
-// dense off-diagonal blocks: per pair B p_i (for image j) and B^T p_j (for image i), [trans | rot] rows,
-// stored write-through for the finisher, which sums each row's pairs in pair order (pcg_ap)
+// dense off-diagonal blocks, per image v (one wave each): Σ over v's pairs, in pair order, of B p_i
+// (v = the pair's j) or B^T p_j (v = its i), [trans | rot] rows. Lanes form 10 groups of 6 (one lane
+// per output row); group g takes the list entries g, g + 10, ...; the groups' partial sums are then
+// added in group order, so the sum is the same on every run. Stored write-through for the finisher.
 __device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
     const uint32_t lane = lane_id();
-    const uint32_t np = a.ctrl[K_NPAIRS];
-    for (uint32_t k = wave; k < np; k += nw) {
-        if (a.pairW[k] == 0.0f) continue;
-        const uint2 pr = a.pairs[k];
-        const float* Bk = a.pairBlk + (size_t)k * 36;
-        f3 r, t;
+    const uint32_t grp = lane / 6, row = lane % 6;
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+        const uint32_t* L = a.imgPairs + (size_t)v * a.maxN;
+        const uint32_t nL = a.imgPairN[v];
         float o = 0.0f;
-        if (lane < 6) {
-            vload(a, V_P, pr.x, r, t);
-            const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-            for (int c = 0; c < 6; c++) o += Bk[lane * 6 + c] * pv[c];
-            st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)k * 12 + lane, __float_as_uint(o));
-        } else if (lane < 12) {
-            vload(a, V_P, pr.y, r, t);
-            const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-            const int c0 = lane - 6;
-            for (int rr = 0; rr < 6; rr++) o += Bk[rr * 6 + c0] * pv[rr];
-            st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)k * 12 + lane, __float_as_uint(o));
+        if (grp < 10) {
+            for (uint32_t q = grp; q < nL; q += 10) {
+                const uint32_t e = L[q], k = e >> 1;
+                const uint2 pr = a.pairs[k];
+                const float* Bk = a.pairBlk + (size_t)k * 36;  // rows: image pr.y, columns: image pr.x
+                f3 r, t;
+                vload(a, V_P, (e & 1u) ? pr.x : pr.y, r, t);
+                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+                float s = 0.0f;
+                if (e & 1u) { for (int c = 0; c < 6; c++) s += Bk[row * 6 + c] * pv[c]; }
+                else { for (int rr = 0; rr < 6; rr++) s += Bk[rr * 6 + row] * pv[rr]; }
+                if ((e & 1u) ? pr.x > 0 : pr.y > 0) o += s;  // p_0 = 0 (image 0 fixed)
+            }
         }
+        float tot = 0.0f;
+        for (uint32_t g = 0; g < 10; g++) tot += __shfl(o, (int)(g * 6 + row));
+        if (lane < 6) st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)v * 8 + lane, __float_as_uint(tot));
     }
 }
 
@@ -1940,7 +1940,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     jtr_.alloc((size_t)N * 6);
     pairFlag_.alloc((size_t)N * N);
     pairAcc_.alloc((size_t)maxPairs_ * 54);
-    pairProd_.alloc((size_t)maxPairs_ * 12);
+    pairProd_.alloc((size_t)N * 8);
     imgPairs_.alloc((size_t)N * N);
     imgPairN_.alloc(N);
     // assembled normal equations: a pair has >= 1 correspondence, so pairs <= min(N(N-1)/2, maxCorr)
