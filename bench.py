@@ -257,6 +257,9 @@ def main():
                     help="config1: BASELINE north star (640x480, 4 mm, 2^23 buckets, 2^21 blocks); config5: "
                          "1280x960 depth at 2 mm voxels (2^24 buckets, 2^23 blocks: a heap beyond the "
                          "reference's 2^22-block int32 voxel index); explicit size flags override")
+    ap.add_argument("--rehearse-shards", type=int, default=0,
+                    help="single process: run rank 0's share of a G-way TSDF-sharded job (scene chunk shard 0 "
+                         "of G, bundling replicated) to measure one rank's per-frame cost without G GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "apply_pass_pmc.json"),
                     help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
@@ -278,7 +281,9 @@ def main():
     from bundlefusion_amd.recon import Recon, recon_options
     from bundlefusion_amd.stream import SyntheticStream
 
-    bfa.check(bfa.lib().bf_set_device(local_rank))
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the multi-rank path on a smaller box)
+    # share them round-robin
+    bfa.check(bfa.lib().bf_set_device(local_rank % max(1, bfa.device_count())))
     S = 10
     # The stream is the BASELINE workload whatever --steps says: `frames` frames (+1 so that the
     # last submap has its S+1-th local frame). The untimed prefix ("fill": everything before the
@@ -295,6 +300,8 @@ def main():
                          maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2))
     so = BFSceneOptions()
     so.shardCount, so.shardIndex, so.shardChunk = world, rank, SHARD_CHUNK
+    if world == 1 and args.rehearse_shards > 1:
+        so.shardCount, so.shardIndex = args.rehearse_shards, 0
     rc = Recon(params, stream.cam, opts, so)
     comm = None
     if world > 1 and os.environ.get("BF_BA_SHARD", "1") != "0":
@@ -400,7 +407,9 @@ def main():
         "config": {"workload": workload, "frames": frames_total, "frames_fill": fill, "frames_timed": frames,
                    "keyframes_final": K,
                    "parallelism": (f"tsdf-chunk-shard{world}+ba-pair-shard{world}-rccl" if comm is not None
-                                   else f"tsdf-chunk-shard{world}+ba-replicated") if world > 1 else "single"},
+                                   else f"tsdf-chunk-shard{world}+ba-replicated") if world > 1 else
+                                  (f"rehearsal: rank 0 of tsdf-chunk-shard{args.rehearse_shards}, ba-replicated"
+                                   if args.rehearse_shards > 1 else "single")},
         "stream": {"frames_per_s_whole_stream": frames_total / (t_fill + dt), "fill_s": t_fill, "timed_s": dt,
                    "fill_frames_per_s": fill / t_fill if fill else None,
                    "fill_global_gn_iters": fill_stats["globalGnIterations"],

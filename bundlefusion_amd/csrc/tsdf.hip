@@ -137,6 +137,22 @@ __device__ __forceinline__ bool owned(const HashArgs& A, int bx, int by, int bz)
     return hash_bucket(cx, cy, cz, A.shardCount) == A.shardIndex;
 }
 
+// Does this rank own a chunk of any block in the box spanned by blocks b0 and b1? Same float
+// arithmetic as owned() at the box's corners; at most 4 chunks per axis are tested (a truncation
+// band is far shorter than a chunk), beyond that the walk runs.
+__device__ __forceinline__ bool segment_may_own(const HashArgs& A, i3 b0, i3 b1) {
+    const f3 wl = block_to_world(min(b0.x, b1.x), min(b0.y, b1.y), min(b0.z, b1.z), A.voxelSize) / A.shardChunk;
+    const f3 wh = block_to_world(max(b0.x, b1.x), max(b0.y, b1.y), max(b0.z, b1.z), A.voxelSize) / A.shardChunk;
+    const int x0 = f2i(wl.x + (float)sgn(wl.x) * 0.5f), y0 = f2i(wl.y + (float)sgn(wl.y) * 0.5f), z0 = f2i(wl.z + (float)sgn(wl.z) * 0.5f);
+    const int x1 = f2i(wh.x + (float)sgn(wh.x) * 0.5f), y1 = f2i(wh.y + (float)sgn(wh.y) * 0.5f), z1 = f2i(wh.z + (float)sgn(wh.z) * 0.5f);
+    if (x1 - x0 > 3 || y1 - y0 > 3 || z1 - z0 > 3) return true;
+    for (int cz = z0; cz <= z1; cz++)
+        for (int cy = y0; cy <= y1; cy++)
+            for (int cx = x0; cx <= x1; cx++)
+                if (hash_bucket(cx, cy, cz, A.shardCount) == A.shardIndex) return true;
+    return false;
+}
+
 // isSDFBlockStreamedOut, CUDASceneRepHashSDF.cu:152-163
 __device__ __forceinline__ bool streamed_out(const HashArgs& A, int bx, int by, int bz) {
     if (!A.bitMask) return false;
@@ -367,6 +383,10 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         if (bp.y - rayMin.y == 0.0f) { tMax.y = INFINITY; tDelta.y = INFINITY; }
         if (rayDir.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
         if (bp.z - rayMin.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
+        // multi-GPU: the walk visits only blocks inside the box of its first and last block; when no
+        // chunk of that box belongs to this rank, none of its blocks can be emitted, so skip the walk
+        // (chunk indices are monotone in the block coordinate: the box's corners bound them)
+        if (A.shardCount > 1) active = segment_may_own(A, id, idEnd);
     }
 
     // phase 1: walk the ray's blocks and collect the tile's distinct blocks in the LDS set (compute
