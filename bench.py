@@ -75,7 +75,7 @@ def host_info() -> dict:
             "host_mem_copy_GBps": gbs}
 
 
-SHARD_CHUNK = 1.0  # metres: edge of the ownership chunks of the multi-GPU TSDF sharding
+SHARD_CHUNK = 0.25  # metres: edge of the ownership chunks of the multi-GPU TSDF sharding (balance: DESIGN §6)
 PREFIX_FRAMES = 40  # the loop prefix the CPU oracle runs in full (and the GPU's time for it, untimed region)
 
 
@@ -260,6 +260,10 @@ def main():
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="single process: run rank 0's share of a G-way TSDF-sharded job (scene chunk shard 0 "
                          "of G, bundling replicated) to measure one rank's per-frame cost without G GPUs")
+    ap.add_argument("--shard-chunk", type=float, default=SHARD_CHUNK,
+                    help="edge (m) of the TSDF ownership chunks when sharded over ranks")
+    ap.add_argument("--async-bundling", type=int, default=1, choices=[1, 2],
+                    help="1: solves issued from the frame loop onto their own streams; 2: from a bundling thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "apply_pass_pmc.json"),
                     help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
@@ -296,10 +300,10 @@ def main():
     stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log)
     params = bfa.hash_params(voxel_size=args.voxel, num_buckets=args.buckets, num_blocks=args.blocks)
     K = stream.K
-    opts = recon_options(F, enableTiming=1, asyncBundling=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
+    opts = recon_options(F, enableTiming=1, asyncBundling=args.async_bundling, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
                          maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2))
     so = BFSceneOptions()
-    so.shardCount, so.shardIndex, so.shardChunk = world, rank, SHARD_CHUNK
+    so.shardCount, so.shardIndex, so.shardChunk = world, rank, args.shard_chunk
     if world == 1 and args.rehearse_shards > 1:
         so.shardCount, so.shardIndex = args.rehearse_shards, 0
     rc = Recon(params, stream.cam, opts, so)
@@ -452,7 +456,7 @@ def main():
         blk = rc.export_blocks()
         blk = blk[blk[:, 3] != 0]
         poses_t = stream.gt[fill:frames_total:10]
-        out["shard_balance"] = shard_balance(blk[:, :3], args.voxel, poses_t, stream.cam, chunk=SHARD_CHUNK)
+        out["shard_balance"] = shard_balance(blk[:, :3], args.voxel, poses_t, stream.cam, chunk=args.shard_chunk)
         # max / mean over ranks of (stored blocks, in-frustum block-frames) for other ownership chunk sizes
         out["shard_balance"]["by_chunk"] = {
             f"{c:g}m": {g: [round(v["stored_max_over_mean"], 3), round(v["visible_max_over_mean"], 3)]

@@ -346,9 +346,6 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
                                               unsigned long long* __restrict__ cand, uint32_t candCap,
                                               uint8_t* __restrict__ candOp = nullptr, uint8_t opIdx = 0) {
     __shared__ unsigned long long set[LDS_SET];
-    for (int k = threadIdx.x; k < LDS_SET; k += blockDim.x) set[k] = EMPTY_KEY;
-    __syncthreads();
-
     const uint32_t x = blockIdx.x * ALLOC_TILE + (threadIdx.x % ALLOC_TILE);
     const uint32_t y = blockIdx.y * ALLOC_TILE + (threadIdx.x / ALLOC_TILE);
     bool active = x < cam.imageWidth && y < cam.imageHeight;
@@ -388,6 +385,13 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         // (chunk indices are monotone in the block coordinate: the box's corners bound them)
         if (A.shardCount > 1) active = segment_may_own(A, id, idEnd);
     }
+    // a tile none of whose rays walks (no valid depth, or, sharded, no ray near an owned chunk) ends here
+    if (!__syncthreads_or(active ? 1 : 0)) {
+        flush_stats2(A.stats, S_CAND, 0ull, S_PIXELS, (x < cam.imageWidth && y < cam.imageHeight) ? 1ull : 0ull);
+        return;
+    }
+    for (int k = threadIdx.x; k < LDS_SET; k += blockDim.x) set[k] = EMPTY_KEY;
+    __syncthreads();
 
     // phase 1: walk the ray's blocks and collect the tile's distinct blocks in the LDS set (compute
     // only, no global memory on the DDA's critical path). The per-block tests (frustum, ownership,
