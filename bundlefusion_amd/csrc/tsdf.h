@@ -139,6 +139,7 @@ private:
     DevBuf<BFHashEntry> hash_;
     DevBuf<uint32_t> heap_;
     DevBuf<BFVoxel> voxels_;
+    uint64_t hostPixels_ = 0;  // BFTsdfStats.pixels: W x H per alloc walk, counted at launch
     DevBuf<int4> blockPos_;
     DevBuf<int4> visible_;
     DevBuf<int4> band_;

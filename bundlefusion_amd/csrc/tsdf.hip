@@ -386,10 +386,7 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         if (A.shardCount > 1) active = segment_may_own(A, id, idEnd);
     }
     // a tile none of whose rays walks (no valid depth, or, sharded, no ray near an owned chunk) ends here
-    if (!__syncthreads_or(active ? 1 : 0)) {
-        flush_stats2(A.stats, S_CAND, 0ull, S_PIXELS, (x < cam.imageWidth && y < cam.imageHeight) ? 1ull : 0ull);
-        return;
-    }
+    if (!__syncthreads_or(active ? 1 : 0)) return;
     for (int k = threadIdx.x; k < LDS_SET; k += blockDim.x) set[k] = EMPTY_KEY;
     __syncthreads();
 
@@ -495,8 +492,10 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
             emitted++;
         }
     }
-    const bool inImage = x < cam.imageWidth && y < cam.imageHeight;
-    flush_stats2(A.stats, S_CAND, emitted, S_PIXELS, inImage ? 1ull : 0ull);
+    // pixels are counted on the host (W x H per walk); candidates are rare in steady state, so the
+    // workgroup adds its count only when it emitted some (every workgroup adding to a few counters
+    // serialised ~10^5 atomics per frame on them)
+    if (__syncthreads_or(emitted != 0 ? 1 : 0)) flush_stats2(A.stats, S_CAND, emitted, -1, 0);
 }
 __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* __restrict__ depthImg,
                                                        BFDepthCameraParams cam, BFMat4 T, BFMat4 Tinv,
@@ -1528,6 +1527,7 @@ void Scene::alloc(const float* depth, const BFDepthCameraParams& cam, const uint
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
     dim3 g(div_up(cam.imageWidth, ALLOC_TILE), div_up(cam.imageHeight, ALLOC_TILE));
     k_alloc_collect<<<g, 256, 0, stream_>>>(A, depth, cam, T_, Tinv_, cand_.p, cfg_.candCapacity);
+    hostPixels_ += (uint64_t)cam.imageWidth * cam.imageHeight;
     BF_LAUNCH_CHECK();
     // few candidates per op in steady state: a small grid keeps the last-workgroup ticket cheap
     const unsigned grid = 64;
@@ -1653,6 +1653,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     if (tab.nInt) {
         dim3 g(div_up(cam.imageWidth, ALLOC_TILE), div_up(cam.imageHeight, ALLOC_TILE), tab.nInt);
         k_alloc_collect_ops<<<g, 256, 0, stream_>>>(A, cam, tab, cand_.p, cfg_.candCapacity, candOp_.p);
+        hostPixels_ += (uint64_t)cam.imageWidth * cam.imageHeight * tab.nInt;
         BF_LAUNCH_CHECK();
         k_alloc_insert<<<64, 256, 0, stream_>>>(A, cand_.p, cfg_.candCapacity, candSet_.p, candSetMask_, candSlot_.p, ovf_.p);
         BF_LAUNCH_CHECK();
@@ -1726,10 +1727,14 @@ BFTsdfStats Scene::stats() {
     BFTsdfStats s;
     static_assert(sizeof(BFTsdfStats) == 17 * 8 && sizeof(BFTsdfStats) <= STAT_FIELDS * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
+    s.pixels += hostPixels_;
     return s;
 }
 
-void Scene::resetStats() { BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_)); }
+void Scene::resetStats() {
+    BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
+    hostPixels_ = 0;
+}
 
 // Dumps use the reference's units: ptr = heap block * 512 (the voxel index of the block's first
 // voxel), which an int32 holds up to 2^22 blocks; larger scenes dump blocks and voxels by heap block
