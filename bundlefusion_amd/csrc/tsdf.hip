@@ -1068,6 +1068,20 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         }
     }
     __shared__ uint32_t s_cnt[4], s_base, s_bcnt[Scene::kMaxOps], s_bbase[Scene::kMaxOps];
+    // the band cull runs on the (block, op) pairs that passed the frustum test, compacted per wave:
+    // run per lane over its ops, it had every lane of a wave execute it whenever one lane's block
+    // passed (the wave's 64 blocks almost always include one), ~3x the VALU of the compacted form
+    __shared__ int4 s_bp[256];
+    __shared__ uint32_t s_mask[256];
+    __shared__ uint16_t s_q[4][64 * Scene::kMaxOps];  // per wave: lane << 5 | op
+    __shared__ float s_tinv[Scene::kMaxOps][12];
+    __shared__ const float2* s_tiles[2][Scene::kMaxOps];
+    for (uint32_t q = threadIdx.x; q < ops.n * 12; q += blockDim.x) s_tinv[q / 12][q % 12] = ops.tinv[q / 12][q % 12];
+    if (threadIdx.x < ops.n) {
+        s_tiles[0][threadIdx.x] = ops.tiles[threadIdx.x];
+        s_tiles[1][threadIdx.x] = ops.tiles2[threadIdx.x];
+    }
+    __syncthreads();
     const uint32_t hw = A.ctrl[C_HIGHWATER];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const BFMat4 TinvLast = op_mat(ops.tinv[ops.n - 1]);
@@ -1078,20 +1092,37 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
         const bool keepVis = alloc && block_in_frustum_fast(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
-        uint32_t mask = 0;
+        uint32_t fr = 0;  // ops whose frustum holds the block
         if (alloc) {
             const uint32_t bi = birth[i];
             // a block born in this batch at op j exists for ops j.. only (ops before it see no block)
             const uint32_t first = (bi >> 8) == epoch ? 255u - (bi & 255u) : 0u;
-            // k runs over every op in every lane (a wave-uniform loop keeps the op's pose and tile
-            // pointers in scalar loads; a per-lane start made them per-lane loads of the op table)
+            // k runs over every op in every lane (a wave-uniform loop keeps the op's pose in scalar loads)
             for (uint32_t k = 0; k < ops.n; k++) {
                 const BFMat4 Ti = op_mat(ops.tinv[k]);
-                if (k >= first && block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize) &&
-                    block_may_update(A, cam, Ti, bp.x, bp.y, bp.z, ops.tiles[k], ops.tiles2[k]))
-                    mask |= 1u << k;
+                if (k >= first && block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize)) fr |= 1u << k;
             }
         }
+        // queue the wave's (block, op) pairs, then every lane takes one pair per round for the band cull
+        s_bp[threadIdx.x] = bp;
+        s_mask[threadIdx.x] = 0u;
+        uint32_t qoff = (uint32_t)__popc(fr), qtot = qoff;
+        for (int off = 1; off < 64; off <<= 1) {  // inclusive wave scan of the pair counts
+            const uint32_t v = (uint32_t)__shfl_up((int)qoff, off);
+            if ((int)lane >= off) qoff += v;
+        }
+        qtot = (uint32_t)__shfl((int)qoff, 63);
+        qoff -= (uint32_t)__popc(fr);
+        for (uint32_t m = fr; m; m &= m - 1) s_q[wv][qoff++] = (uint16_t)((lane << 5) | (uint32_t)__builtin_ctz(m));
+        __syncthreads();
+        for (uint32_t r = lane; r < qtot; r += 64) {
+            const uint32_t e = s_q[wv][r], src = wv * 64 + (e >> 5), k = e & 31u;
+            const int4 b = s_bp[src];
+            if (block_may_update(A, cam, op_mat(s_tinv[k]), b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]))
+                atomicOr(&s_mask[src], 1u << k);
+        }
+        __syncthreads();
+        const uint32_t mask = s_mask[threadIdx.x];
         const bool inb = mask != 0;
         // work list: one bin per op count, so the voxel pass can hand out the costliest blocks first
         // (entry order inside a bin is free: every block is applied by exactly one wave)
