@@ -164,7 +164,7 @@ private:
     unsigned integrateGrid_[2] = {0, 0};
     KernelClock integrateClock_;
     KernelClock renderClock_;
-    DevBuf<uint32_t> blockMask_;  // per work-list entry of an op batch: which ops may update it
+    DevBuf<uint2> blockMask_;  // per work-list entry of an op batch: which ops may update each z-half
     DevBuf<uint32_t> blockBirth_;  // per heap block: epoch << 8 | (255 - first op) of the batch that allocated it
     DevBuf<uint8_t> candOp_;       // per alloc candidate of a batch: the integrate op that emitted it
     uint32_t batchEpoch_ = 0;

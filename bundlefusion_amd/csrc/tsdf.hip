@@ -267,14 +267,17 @@ __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned
 // changes no voxel. The corner projections use rcp (1 ulp, far inside the one-pixel growth);
 // footprints within 3x3 fine (8-pixel) tiles read those tiles, wider ones up to 3x3 coarse
 // (16-pixel) tiles, all loads independent.
+// z0 / z1: the voxel z-range (offsets in the block) the test covers; a half-block test covers 0..3
+// or 4..7, the block test 0..7
 __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx, int by,
-                                 int bz, const float2* __restrict__ tiles, const float2* __restrict__ tiles2) {
-    const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
-    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
+                                 int bz, const float2* __restrict__ tiles, const float2* __restrict__ tiles2, int z0 = 0,
+                                 int z1 = BF_SDF_BLOCK_SIZE - 1) {
+    const f3 c0 = block_to_world(bx, by, bz, A.voxelSize) + mk3(0.0f, 0.0f, A.voxelSize * (float)z0);
+    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1), extz = A.voxelSize * (float)(z1 - z0);
     float zlo = INFINITY, zhi = -INFINITY, xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
+        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? extz : 0.0f);
         const f3 p = xform(Tinv, w);
         if (!(p.z > 1e-3f)) return true;  // straddles the camera plane: keep
         const float rz = __builtin_amdgcn_rcpf(p.z);
@@ -316,6 +319,76 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
     if (dlo * (1.0f - A.truncScale) >= zhi + A.truncation + slack) return false;  // surface far behind
     if (dhi * (1.0f + A.truncScale) <= zlo - A.truncation - slack) return false;  // surface far in front
     return true;
+}
+
+// block_may_update for the two z-halves of the block at once (bit h: half h, voxel z 4h..4h+3, may
+// hold an in-band voxel): the screen footprint and its depth bounds are the whole block's (a superset
+// of each half's pixels: still conservative), the depth range is each half's own, from the corners at
+// z offsets 0, 3 and 4, 7 (only the depth row of the transform for the inner two levels).
+__device__ uint32_t block_may_update_halves(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx,
+                                            int by, int bz, const float2* __restrict__ tiles,
+                                            const float2* __restrict__ tiles2) {
+    const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
+    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
+    float zlo[2] = {INFINITY, INFINITY}, zhi[2] = {-INFINITY, -INFINITY};
+    float xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
+        const f3 p = xform(Tinv, w);
+        if (!(p.z > 1e-3f)) return 3u;  // straddles the camera plane: keep
+        const float rz = __builtin_amdgcn_rcpf(p.z);
+        const float sx = p.x * cam.fx * rz + cam.mx, sy = p.y * cam.fy * rz + cam.my;
+        const int hh = (k & 4) ? 1 : 0;
+        zlo[hh] = fminf(zlo[hh], p.z); zhi[hh] = fmaxf(zhi[hh], p.z);
+        xlo = fminf(xlo, sx); xhi = fmaxf(xhi, sx);
+        ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {  // the inner levels: z offset 3 (half 0) and 4 (half 1)
+        const int hh = (k & 4) ? 1 : 0;
+        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, A.voxelSize * (float)(3 + hh));
+        const float pz = ((Tinv.m[8] * w.x + Tinv.m[9] * w.y) + Tinv.m[10] * w.z) + Tinv.m[11];
+        if (!(pz > 1e-3f)) return 3u;
+        zlo[hh] = fminf(zlo[hh], pz); zhi[hh] = fmaxf(zhi[hh], pz);
+    }
+    const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
+    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
+    if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) return 0u;  // every voxel off-screen
+    const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
+    const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
+    const int tx0 = x0 / DEPTH_TILE, tx1 = x1 / DEPTH_TILE, ty0 = y0 / DEPTH_TILE, ty1 = y1 / DEPTH_TILE;
+    float dlo = INFINITY, dhi = -INFINITY;
+    if (tx1 - tx0 <= 2 && ty1 - ty0 <= 2) {
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float2 t = tiles[min(ty0 + j, ty1) * A.tilesW + min(tx0 + i, tx1)];
+                dlo = fminf(dlo, t.x);
+                dhi = fmaxf(dhi, t.y);
+            }
+    } else {
+        const int cx0 = x0 / DEPTH_TILE2, cx1 = x1 / DEPTH_TILE2, cy0 = y0 / DEPTH_TILE2, cy1 = y1 / DEPTH_TILE2;
+        if (cx1 - cx0 > 2 || cy1 - cy0 > 2) return 3u;  // very close block: keep
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float2 t = tiles2[min(cy0 + j, cy1) * A.tiles2W + min(cx0 + i, cx1)];
+                dlo = fminf(dlo, t.x);
+                dhi = fmaxf(dhi, t.y);
+            }
+    }
+    if (!(dlo <= dhi)) return 0u;  // no integrable depth under the block
+    const float slack = 0.001f;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++)
+        if (!(dlo * (1.0f - A.truncScale) >= zhi[hh] + A.truncation + slack) &&
+            !(dhi * (1.0f + A.truncScale) <= zlo[hh] - A.truncation - slack))
+            bits |= 1u << hh;
+    return bits;
 }
 
 // isSDFBlockInCameraFrustumApprox (VoxelUtilHashSDF.h:322-326, DepthCameraUtil.h:95-107) with the
@@ -1058,7 +1131,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
 // releases the batch's alloc dedup-set slots.
 __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
-                                                        uint32_t* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
+                                                        uint2* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
                                                         uint32_t binCap) {
     {
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
@@ -1072,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
     // run per lane over its ops, it had every lane of a wave execute it whenever one lane's block
     // passed (the wave's 64 blocks almost always include one), ~3x the VALU of the compacted form
     __shared__ int4 s_bp[256];
-    __shared__ uint32_t s_mask[256];
+    __shared__ uint32_t s_mask[2][256];  // per z-half of the block (voxel z 0..3 / 4..7)
     __shared__ uint16_t s_q[4][64 * Scene::kMaxOps];  // per wave: lane << 5 | op
     __shared__ float s_tinv[Scene::kMaxOps][12];
     __shared__ const float2* s_tiles[2][Scene::kMaxOps];
@@ -1105,7 +1178,8 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         }
         // queue the wave's (block, op) pairs, then every lane takes one pair per round for the band cull
         s_bp[threadIdx.x] = bp;
-        s_mask[threadIdx.x] = 0u;
+        s_mask[0][threadIdx.x] = 0u;
+        s_mask[1][threadIdx.x] = 0u;
         uint32_t qoff = (uint32_t)__popc(fr), qtot = qoff;
         for (int off = 1; off < 64; off <<= 1) {  // inclusive wave scan of the pair counts
             const uint32_t v = (uint32_t)__shfl_up((int)qoff, off);
@@ -1118,15 +1192,20 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         for (uint32_t r = lane; r < qtot; r += 64) {
             const uint32_t e = s_q[wv][r], src = wv * 64 + (e >> 5), k = e & 31u;
             const int4 b = s_bp[src];
-            if (block_may_update(A, cam, op_mat(s_tinv[k]), b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]))
-                atomicOr(&s_mask[src], 1u << k);
+            const BFMat4 Ti = op_mat(s_tinv[k]);
+            // the voxel pass applies an op to a block half by half (4 z-slices per round)
+            const uint32_t hb = block_may_update_halves(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
+            if (hb & 1u) atomicOr(&s_mask[0][src], 1u << k);
+            if (hb & 2u) atomicOr(&s_mask[1][src], 1u << k);
         }
         __syncthreads();
-        const uint32_t mask = s_mask[threadIdx.x];
+        const uint2 hm = make_uint2(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x]);
+        const uint32_t mask = hm.x | hm.y;
+        const uint32_t cost = (uint32_t)(__popc(hm.x) + __popc(hm.y));  // op-halves to apply
         const bool inb = mask != 0;
-        // work list: one bin per op count, so the voxel pass can hand out the costliest blocks first
-        // (entry order inside a bin is free: every block is applied by exactly one wave)
-        const uint32_t bin = inb ? (uint32_t)__popc(mask) - 1u : 0u;
+        // work list: one bin per cost (op-halves, two per bin), so the voxel pass can hand out the
+        // costliest blocks first (entry order inside a bin is free: every block is applied by one wave)
+        const uint32_t bin = inb ? (cost + 1u) / 2u - 1u : 0u;
         const unsigned long long m0 = __ballot(keepVis);
         if (threadIdx.x < Scene::kMaxOps) s_bcnt[threadIdx.x] = 0;
         if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(m0);
@@ -1146,19 +1225,19 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         if (inb) {
             const size_t k = (size_t)bin * binCap + s_bbase[bin] + local;
             A.band[k] = ent;
-            masks[k] = mask;
+            masks[k] = hm;
         }
         scanned += alloc ? 1 : 0;
         vis += keepVis ? 1 : 0;
         band += inb ? 1 : 0;
-        evals += (unsigned long long)__popc(mask);
+        evals += (unsigned long long)cost;
         __syncthreads();
     }
     flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
     __syncthreads();
     flush_stats2(A.stats, S_BAND, band, S_BBLOCKS, band);
     __syncthreads();
-    flush_stats2(A.stats, S_BEVAL, evals * BF_VOXELS_PER_BLOCK, -1, 0);
+    flush_stats2(A.stats, S_BEVAL, evals * (BF_VOXELS_PER_BLOCK / 2), -1, 0);
 }
 
 // The batch's voxel pass: one wave per work-list block, lane = (x, y), ZC z-slices per round. For
@@ -1199,7 +1278,8 @@ __device__ __forceinline__ bool work_slot(const uint32_t* ctrl, WorkCursor& c, u
 // ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us).
 template <int ZR, int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
-    HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint32_t* __restrict__ masks, uint32_t binCap) {
+    HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint2* __restrict__ masks, uint32_t binCap) {
+    static_assert(ZR * 2 == BF_SDF_BLOCK_SIZE, "one op mask per z-half of the block");
     const uint32_t lane = lane_id();
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1213,7 +1293,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int4 e = make_int4(__builtin_amdgcn_readfirstlane(ev.x), __builtin_amdgcn_readfirstlane(ev.y),
                                  __builtin_amdgcn_readfirstlane(ev.z), __builtin_amdgcn_readfirstlane(ev.w));
         const uint32_t blk = (uint32_t)e.w;
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(masks[b]);
+        const uint2 mh = masks[b];
+        const uint32_t maskH[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(mh.x), (uint32_t)__builtin_amdgcn_readfirstlane(mh.y)};
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
         Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK) + lane;
@@ -1232,7 +1313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 pos0 |= (uint32_t)(vw[z] >= 1.0f) << z;
             }
             uint32_t touched = 0;
-            for (uint32_t mk = mask; mk;) {
+            for (uint32_t mk = maskH[h / ZR]; mk;) {
                 const uint32_t k = (uint32_t)__builtin_ctz(mk);
                 mk &= mk - 1;
                 const BFMat4 Ti = op_mat(ops.tinv[k]);
