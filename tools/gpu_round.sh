@@ -17,7 +17,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 for v in $V; do
   run bench_$v 300 python -u bench.py --no-cpu-baseline "$@"
-  python3 -c "import json; d=json.loads(open('$O/bench_$v.log').read().strip().splitlines()[-1]); r=d['roofline']; print('variant $v', 'fps %.1f' % d['value'], 'apply_us %.1f' % r['avg_launch_us'], 'gn_ms %.3f' % d['ms_per_gn_iter'], 'gn_loop_ms %.3f' % d['global_solve']['ms_per_gn_iter_in_loop'], 'dense_end_ms %.2f' % d['global_dense_end_solve']['ms'])"
+  python3 -c "import json; d=json.loads(open('$O/bench_$v.log').read().strip().splitlines()[-1]); r=d['roofline']; print('variant $v', 'fps %.1f' % d['value'], 'apply_us %.1f' % r['avg_launch_us'], 'gn_ms %.3f' % d['ms_per_gn_iter'], 'gn_loop_ms %.3f' % d['global_solve']['ms_per_gn_iter_in_loop'], 'dense_end_ms %.2f' % d['global_dense_end_solve']['ms'], 'evals %.1fM' % (r['per_launch']['voxel_op_evaluations'] / 1e6), 'blocks %.0fk' % (r['per_launch']['work_list_blocks'] / 1e3))"
 done
 if [ -z "$SKIP_LARGE" ]; then
   run large 300 python -u -m pytest -s tests/test_large_scene_gpu.py -x -v --timeout 280 --timeout-method thread
