@@ -53,16 +53,20 @@ __device__ float filtered_at(const GeomArgs& A, int x, int y) {
     const int R = A.g.radius;
     float sum = 0.0f, sumWeight = 0.0f;
     if (depthCenter != -INFINITY) {
-        for (int m = x - R; m <= x + R; m++)
-            for (int n = y - R; n <= y + R; n++)
+        // loops over the offsets (same m-outer / n-inner order), so the weight index is wave-uniform
+        // and the weights come through scalar loads instead of one vector load per tap
+        for (int dm = -R; dm <= R; dm++)
+            for (int dn = -R; dn <= R; dn++) {
+                const int m = x + dm, n = y + dn;
                 if (m >= 0 && n >= 0 && m < W && n < H) {
                     const float currentDepth = A.depth[n * W + m];
                     if (currentDepth != -INFINITY && fabsf(depthCenter - currentDepth) < A.sigmaR) {
-                        const float weight = A.g.w[(n - y + R) * (2 * R + 1) + (m - x + R)];
+                        const float weight = A.g.w[(dn + R) * (2 * R + 1) + (dm + R)];
                         sumWeight += weight;
                         sum += weight * currentDepth;
                     }
                 }
+            }
     }
     return sumWeight > 0.0f ? sum / sumWeight : -INFINITY;
 }
@@ -170,13 +174,15 @@ __global__ __launch_bounds__(256) void k_cache_intensity(IntArgs A) {
             out = I[(gy - y0) * E + (gx - x0)];
             if (A.useGauss) {
                 float sum = 0.0f, sumWeight = 0.0f;
-                for (int m = gx - R; m <= gx + R; m++)
-                    for (int q = gy - R; q <= gy + R; q++)
+                for (int dm = -R; dm <= R; dm++)  // offsets: wave-uniform weight index (scalar loads)
+                    for (int dq = -R; dq <= R; dq++) {
+                        const int m = gx + dm, q = gy + dq;
                         if (m >= 0 && q >= 0 && m < W && q < H) {
-                            const float weight = A.g.w[(q - gy + R) * (2 * R + 1) + (m - gx + R)];
+                            const float weight = A.g.w[(dq + R) * (2 * R + 1) + (dm + R)];
                             sumWeight += weight;
                             sum += weight * I[(q - y0) * E + (m - x0)];
                         }
+                    }
                 if (sumWeight > 0.0f) out = sum / sumWeight;
             }
             const int lx = gx - blockIdx.x * IT, ly = gy - blockIdx.y * IT;
