@@ -53,7 +53,7 @@ struct BA {
     uint32_t nTiles;
     int *rowChunk, *chunkRow;  // chunks of row v: [rowChunk[v], rowChunk[v+1]); chunk -> row
     float4* chunkPart;         // [chunk][3] per-chunk partial sums
-    uint32_t* sync;            // k_pcg_loop: 8 shard counters + top counter + 8 flag replicas, 64 B apart
+    uint32_t* sync;            // last_block_sharded: 8 shard counters + top counter (+ flag words), 64 B apart
     float4* entries;
     float* vec;
     float* img;
@@ -781,7 +781,7 @@ __global__ __launch_bounds__(WG) void k_init(BA a, float wSparse) {
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(s);
         a.ctrl[K_TICKET] = 0;
-        for (int w = 0; w < SYNC_WORDS; w += SYNC_LINE) a.sync[w] = 0;  // k_pcg_loop's counters and flags
+        for (int w = 0; w < SYNC_WORDS; w += SYNC_LINE) a.sync[w] = 0;  // the PCG launches' arrival counters
         vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
     }
 }
