@@ -493,7 +493,8 @@ def main():
                    "allocated_blocks": int(params.numSDFBlocks - rc.heap_free_count()),
                    "note": "marching cubes over every allocated block (count + scan + emit), 3M-triangle cap"}
     del mbuf
-    if rank == 0 and not args.no_cpu_baseline and args.preset == "config1":  # the metric's config only
+    # the metric's config, rank 0 of a one-GPU run only (the multi-GPU lines carry no CPU leg)
+    if world == 1 and rank == 0 and not args.no_cpu_baseline and args.preset == "config1":
         gpu = {"keyframes": K - 1, "global_corr": solo["correspondences"],
                "gn_per_solve": st["globalGnIterations"] / max(1, st["globalSolves"]),
                "pcg_per_solve": st["globalPcgIterations"] / max(1, st["globalSolves"]),
