@@ -950,10 +950,11 @@ __device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
 }
 
 // PCG finisher (one workgroup): Kernel1b, Kernel2, the host early-out test, Kernel3
+template <int RB = 2>
 __device__ void pcg_finisher(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, float& rDotzNew,
                              bool& last) {
-    if (a.N <= 2 * WG + 1) {
-        rDotzNew = pcg_finish_regs<2, false>(a, sh, nch, useDense, iter, nLin, last);
+    if (a.N <= RB * WG + 1) {
+        rDotzNew = pcg_finish_regs<RB, false>(a, sh, nch, useDense, iter, nLin, last);
     } else {
         float d = 0.0f;
         for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
@@ -1097,6 +1098,9 @@ __global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
 // Pair mode PCG iteration: one wave per row v >= 1, Ap_v = w (D_v p_v - sum_u B_vu p_u) in fp64 over
 // the row's pairs (the same operator as applyJ / applyJT; no second w, SolverBundlingEquationsLie.h:
 // 154-228), handed to the finisher write-through; then the finisher of k_pcg.
+// RB: image rows per finisher thread held in registers (2: up to 513 images; 8: up to 2 049, the
+// host picks it from the solve's image count; beyond, the finisher's multi-pass form)
+template <int RB>
 __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter, int nLin) {
     __shared__ float sh[WG];
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
@@ -1137,7 +1141,7 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
     if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
     float rDotzNew;
     bool last;
-    pcg_finisher(a, sh, 0u, useDense, iter, nLin, rDotzNew, last);
+    pcg_finisher<RB>(a, sh, 0u, useDense, iter, nLin, rDotzNew, last);
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
         a.ctrl[K_PCG_ITERS]++;
@@ -2111,7 +2115,11 @@ void Solver::solve(const SolveArgs& s) {
             if (s.numImages <= (uint32_t)SMALL_N) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
-                for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+                if (s.numImages <= 2u * WG + 1u) {
+                    for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<2><<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+                } else {
+                    for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<8><<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+                }
             }
             BF_LAUNCH_CHECK();
             k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);

@@ -211,6 +211,24 @@ def test_global_schedule_bench_scale(mode, early_out):
     assert g[3]["maxResidualIndex"] == o[3]["maxResidualIndex"]
 
 
+def test_global_schedule_wide_finisher():
+    """Above 513 images the assembled-mode PCG finisher holds 8 image rows per thread in registers
+    (k_pcg_pairs<8>, up to 2 049 images: config 4's stream reaches 2 001 keyframes) instead of 2: same
+    per-thread row order and reductions, so the same parity bar against the oracle as at K = 400
+    (1e-3 rad / 1 mm per pose) and the same integer outcomes."""
+    prob = make_problem(K=600, stride=10, max_per_pair=25, outliers=0.02, drift=(0.05, 0.002), seed=3)
+    g = gpu_solve(prob, 3, 150, [1, 1, 1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED, early_out=True)
+    o = oracle_solve(prob, 3, 150, [1, 1, 1], early_out=True)
+    assert g[3]["gnIterations"] == o[3]["gnIterations"]
+    er, et = pose_diff(g[0], g[1], o[0], o[1])
+    assert er <= 1e-3 and et <= 1e-3, (er, et)
+    np.testing.assert_array_equal(g[2]["i"] == INVALID, o[2]["i"] == INVALID)
+    assert g[3]["maxResidualIndex"] == o[3]["maxResidualIndex"]
+    # run to run bit-identical
+    g2 = gpu_solve(prob, 3, 150, [1, 1, 1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED, early_out=True)
+    assert np.array_equal(g[0], g2[0]) and np.array_equal(g[1], g2[1])
+
+
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("K,seed,out", [(12, 2, 0.0), (16, 5, 0.02)])
 def test_fixed_schedule_chain_parity(mode, K, seed, out):
