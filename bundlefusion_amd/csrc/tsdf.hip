@@ -473,37 +473,11 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
     // keys: a lane whose left (same pixel row) or upper neighbour pixel reaches the same block in
     // the same step leaves the insert to it (the chain ends at a lane that inserts or emits it), so
     // the LDS set sees far fewer same-address CAS. The emitted set is unchanged.
-    for (uint32_t iter = 0; iter < 1024; iter++) {
-        if (!__any(active)) break;
-        const unsigned long long myKey = active ? block_key(id.x, id.y, id.z) : EMPTY_KEY;
-        const unsigned long long left = __shfl_up(myKey, 1, ALLOC_TILE), up = __shfl_up(myKey, ALLOC_TILE);
-        const bool dup = ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
-        if (active && !dup) {
-            const unsigned long long key = myKey;
-            // slot from the low coordinate bits (3 + 4 + 3 = 10 bits = LDS_SET): the blocks one 16x16-pixel
-            // tile reaches span a few blocks per axis, so they land in distinct slots without a mixing hash
-            uint32_t h = ((uint32_t)id.x & 7u) | (((uint32_t)id.y & 15u) << 3) | (((uint32_t)id.z & 7u) << 7);
-            bool placed = false;
-            for (int p = 0; p < 16; p++) {
-                const unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
-                if (old == EMPTY_KEY || old == key) { placed = true; break; }
-                h = (h + 1) & (LDS_SET - 1);
-            }
-            // congested tile set (rare): test and look the block up right here, emit it if absent
-            // (duplicates are removed by the global dedup in k_alloc_insert)
-            if (!placed && block_in_frustum(cam, Tinv, id.x, id.y, id.z, A.voxelSize) && owned(A, id.x, id.y, id.z) &&
-                !streamed_out(A, id.x, id.y, id.z) && lookup_ptr(A, id.x, id.y, id.z) == BF_FREE_ENTRY) {
-                const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
-                if (k < candCap) {
-                    cand[k] = key;
-                    if (candOp) candOp[k] = opIdx;
-                }
-                else atomicOr(&A.ctrl[C_ERR], 1u);
-                emitted++;
-            }
-        }
-        // traverse (CUDASceneRepHashSDF.cu:231-246)
-        if (!active) continue;
+    // Two DDA steps per trip: both steps' first-probe CAS are issued back to back, so a walk pays one
+    // LDS round trip per two blocks (probing past a taken slot, rare, follows per step). Which lane
+    // inserts a key and in what order changes nothing: the set ends up holding the same keys, and a
+    // key that finds no slot is tested and emitted directly (the global dedup removes repeats).
+    auto advance = [&]() {  // traverse (CUDASceneRepHashSDF.cu:231-246)
         if (tMax.x < tMax.y && tMax.x < tMax.z) {
             id.x = f2i((float)id.x + step.x);
             if (id.x == idBound.x) active = false;
@@ -517,6 +491,50 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
             if (id.y == idBound.y) active = false;
             tMax.y += tDelta.y;
         }
+    };
+    auto is_dup = [&](unsigned long long myKey) {
+        const unsigned long long left = __shfl_up(myKey, 1, ALLOC_TILE), up = __shfl_up(myKey, ALLOC_TILE);
+        return ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
+    };
+    // slot from the low coordinate bits (3 + 4 + 3 = 10 bits = LDS_SET): the blocks one 16x16-pixel
+    // tile reaches span a few blocks per axis, so they land in distinct slots without a mixing hash
+    auto slot_of = [](i3 b) { return ((uint32_t)b.x & 7u) | (((uint32_t)b.y & 15u) << 3) | (((uint32_t)b.z & 7u) << 7); };
+    auto finish_insert = [&](unsigned long long key, i3 b, uint32_t h) {  // probes 2..16, then the direct path
+        bool placed = false;
+        for (int p = 1; p < 16; p++) {
+            h = (h + 1) & (LDS_SET - 1);
+            const unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
+            if (old == EMPTY_KEY || old == key) { placed = true; break; }
+        }
+        // congested tile set (rare): test and look the block up right here, emit it if absent
+        // (duplicates are removed by the global dedup in k_alloc_insert)
+        if (!placed && block_in_frustum(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
+            !streamed_out(A, b.x, b.y, b.z) && lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY) {
+            const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
+            if (k < candCap) {
+                cand[k] = key;
+                if (candOp) candOp[k] = opIdx;
+            }
+            else atomicOr(&A.ctrl[C_ERR], 1u);
+            emitted++;
+        }
+    };
+    for (uint32_t iter = 0; iter < 512; iter++) {
+        if (!__any(active)) break;
+        const bool actA = active;
+        const i3 idA = id;
+        if (active) advance();
+        const bool actB = active;
+        const i3 idB = id;
+        if (active) advance();
+        const unsigned long long keyA = actA ? block_key(idA.x, idA.y, idA.z) : EMPTY_KEY;
+        const unsigned long long keyB = actB ? block_key(idB.x, idB.y, idB.z) : EMPTY_KEY;
+        const bool doA = actA && !is_dup(keyA), doB = actB && !is_dup(keyB);
+        const uint32_t hA = slot_of(idA), hB = slot_of(idB);
+        const unsigned long long oldA = doA ? atomicCAS(&set[hA], EMPTY_KEY, keyA) : EMPTY_KEY;
+        const unsigned long long oldB = doB ? atomicCAS(&set[hB], EMPTY_KEY, keyB) : EMPTY_KEY;
+        if (doA && oldA != EMPTY_KEY && oldA != keyA) finish_insert(keyA, idA, hA);
+        if (doB && oldB != EMPTY_KEY && oldB != keyB) finish_insert(keyB, idB, hB);
     }
     // phase 2: compact the distinct blocks to the front of the set, then every thread checks one of
     // them against the hash (one round of parallel lookups per 256 distinct blocks — a tile reaches
