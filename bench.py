@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import glob
 import json
 import os
 import sys
@@ -265,10 +266,11 @@ def main():
     ap.add_argument("--async-bundling", type=int, default=1, choices=[1, 2],
                     help="1: solves issued from the frame loop onto their own streams; 2: from a bundling thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "apply_pass_pmc.json"),
+    ap.add_argument("--traffic", default=None,
                     help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
                          "tools/profile_bench.sh (committed under profiles/); used only when its "
-                         "workload equals this run's, else traffic is null")
+                         "workload equals this run's, else traffic is null. Default: the first "
+                         "profiles/apply_pass_pmc*.json whose workload matches")
     args = ap.parse_args()
     preset = {"config1": dict(width=640, height=480, voxel=0.004, buckets=1 << 23, blocks=1 << 21),
               "config5": dict(width=1280, height=960, voxel=0.002, buckets=1 << 24, blocks=1 << 23)}[args.preset]
@@ -372,7 +374,14 @@ def main():
     traffic = None
     valu = None
     traffic_src = None
-    tj = json.load(open(args.traffic)) if args.traffic and os.path.exists(args.traffic) else {}
+    cands = [args.traffic] if args.traffic else sorted(glob.glob(os.path.join(REPO, "profiles", "apply_pass_pmc*.json")))
+    tj = {}
+    for c in cands:
+        if c and os.path.exists(c):
+            tj = json.load(open(c))
+            if tj.get("workload") == workload:
+                args.traffic = c
+                break
     # counters are taken only from a profile of this same workload (tools/profile_bench.sh records
     # the workload string of the bench run it profiled and averages over its timed launches)
     if tj.get("workload") == workload and world == 1:
