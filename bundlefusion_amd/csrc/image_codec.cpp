@@ -150,37 +150,37 @@ constexpr int CONST_BITS = 13, PASS1_BITS = 2;
 constexpr int32_t F_0_298631336 = 2446, F_0_390180644 = 3196, F_0_541196100 = 4433, F_0_765366865 = 6270,
                   F_0_899976223 = 7373, F_1_175875602 = 9633, F_1_501321110 = 12299, F_1_847759065 = 15137,
                   F_1_961570560 = 16069, F_2_053119869 = 16819, F_2_562915447 = 20995, F_3_072711026 = 25172;
-inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+inline int64_t descale(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
 
 void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, size_t stride) {
-    int32_t ws[64];
+    int64_t ws[64];
     for (int c = 0; c < 8; c++) {
         const int16_t* in = coef + c;
         const uint16_t* qq = q + c;
-        int32_t* w = ws + c;
+        int64_t* w = ws + c;
         if (in[8] == 0 && in[16] == 0 && in[24] == 0 && in[32] == 0 && in[40] == 0 && in[48] == 0 && in[56] == 0) {
-            const int32_t dc = ((int32_t)in[0] * qq[0]) * (1 << PASS1_BITS);
+            const int64_t dc = ((int64_t)in[0] * qq[0]) * (1 << PASS1_BITS);
             for (int r = 0; r < 8; r++) w[8 * r] = dc;
             continue;
         }
-        int32_t z2 = (int32_t)in[16] * qq[16], z3 = (int32_t)in[48] * qq[48];
-        int32_t z1 = (z2 + z3) * F_0_541196100;
-        int32_t tmp2 = z1 + z3 * (-F_1_847759065);
-        int32_t tmp3 = z1 + z2 * F_0_765366865;
-        z2 = (int32_t)in[0] * qq[0];
-        z3 = (int32_t)in[32] * qq[32];
-        int32_t tmp0 = (z2 + z3) * (1 << CONST_BITS);
-        int32_t tmp1 = (z2 - z3) * (1 << CONST_BITS);
-        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
-        tmp0 = (int32_t)in[56] * qq[56];
-        tmp1 = (int32_t)in[40] * qq[40];
-        tmp2 = (int32_t)in[24] * qq[24];
-        tmp3 = (int32_t)in[8] * qq[8];
+        int64_t z2 = (int64_t)in[16] * qq[16], z3 = (int64_t)in[48] * qq[48];
+        int64_t z1 = (z2 + z3) * F_0_541196100;
+        int64_t tmp2 = z1 + z3 * (-F_1_847759065);
+        int64_t tmp3 = z1 + z2 * F_0_765366865;
+        z2 = (int64_t)in[0] * qq[0];
+        z3 = (int64_t)in[32] * qq[32];
+        int64_t tmp0 = (z2 + z3) * (1 << CONST_BITS);
+        int64_t tmp1 = (z2 - z3) * (1 << CONST_BITS);
+        const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        tmp0 = (int64_t)in[56] * qq[56];
+        tmp1 = (int64_t)in[40] * qq[40];
+        tmp2 = (int64_t)in[24] * qq[24];
+        tmp3 = (int64_t)in[8] * qq[8];
         z1 = tmp0 + tmp3;
         z2 = tmp1 + tmp2;
         z3 = tmp0 + tmp2;
-        int32_t z4 = tmp1 + tmp3;
-        const int32_t z5 = (z3 + z4) * F_1_175875602;
+        int64_t z4 = tmp1 + tmp3;
+        const int64_t z5 = (z3 + z4) * F_1_175875602;
         tmp0 *= F_0_298631336;
         tmp1 *= F_2_053119869;
         tmp2 *= F_3_072711026;
@@ -206,21 +206,21 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, size_t str
         w[32] = descale(tmp13 - tmp0, S);
     }
     for (int r = 0; r < 8; r++) {
-        const int32_t* w = ws + 8 * r;
+        const int64_t* w = ws + 8 * r;
         uint8_t* o = out + (size_t)r * stride;
         constexpr int S = CONST_BITS + PASS1_BITS + 3;
         if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
-            const uint8_t v = idct_limit(descale(w[0], PASS1_BITS + 3));
+            const uint8_t v = idct_limit((int32_t)descale(w[0], PASS1_BITS + 3));
             for (int c = 0; c < 8; c++) o[c] = v;
             continue;
         }
-        int32_t z2 = w[2], z3 = w[6];
-        int32_t z1 = (z2 + z3) * F_0_541196100;
-        int32_t tmp2 = z1 + z3 * (-F_1_847759065);
-        int32_t tmp3 = z1 + z2 * F_0_765366865;
-        int32_t tmp0 = (w[0] + w[4]) * (1 << CONST_BITS);
-        int32_t tmp1 = (w[0] - w[4]) * (1 << CONST_BITS);
-        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        int64_t z2 = w[2], z3 = w[6];
+        int64_t z1 = (z2 + z3) * F_0_541196100;
+        int64_t tmp2 = z1 + z3 * (-F_1_847759065);
+        int64_t tmp3 = z1 + z2 * F_0_765366865;
+        int64_t tmp0 = (w[0] + w[4]) * (1 << CONST_BITS);
+        int64_t tmp1 = (w[0] - w[4]) * (1 << CONST_BITS);
+        const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
         tmp0 = w[7];
         tmp1 = w[5];
         tmp2 = w[3];
@@ -228,8 +228,8 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, size_t str
         z1 = tmp0 + tmp3;
         z2 = tmp1 + tmp2;
         z3 = tmp0 + tmp2;
-        int32_t z4 = tmp1 + tmp3;
-        const int32_t z5 = (z3 + z4) * F_1_175875602;
+        int64_t z4 = tmp1 + tmp3;
+        const int64_t z5 = (z3 + z4) * F_1_175875602;
         tmp0 *= F_0_298631336;
         tmp1 *= F_2_053119869;
         tmp2 *= F_3_072711026;
@@ -244,14 +244,14 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, size_t str
         tmp1 += z2 + z4;
         tmp2 += z2 + z3;
         tmp3 += z1 + z4;
-        o[0] = idct_limit(descale(tmp10 + tmp3, S));
-        o[7] = idct_limit(descale(tmp10 - tmp3, S));
-        o[1] = idct_limit(descale(tmp11 + tmp2, S));
-        o[6] = idct_limit(descale(tmp11 - tmp2, S));
-        o[2] = idct_limit(descale(tmp12 + tmp1, S));
-        o[5] = idct_limit(descale(tmp12 - tmp1, S));
-        o[3] = idct_limit(descale(tmp13 + tmp0, S));
-        o[4] = idct_limit(descale(tmp13 - tmp0, S));
+        o[0] = idct_limit((int32_t)descale(tmp10 + tmp3, S));
+        o[7] = idct_limit((int32_t)descale(tmp10 - tmp3, S));
+        o[1] = idct_limit((int32_t)descale(tmp11 + tmp2, S));
+        o[6] = idct_limit((int32_t)descale(tmp11 - tmp2, S));
+        o[2] = idct_limit((int32_t)descale(tmp12 + tmp1, S));
+        o[5] = idct_limit((int32_t)descale(tmp12 - tmp1, S));
+        o[3] = idct_limit((int32_t)descale(tmp13 + tmp0, S));
+        o[4] = idct_limit((int32_t)descale(tmp13 - tmp0, S));
     }
 }
 
@@ -357,7 +357,7 @@ inline uint8_t clamp255(int v) { return (uint8_t)std::min(255, std::max(0, v)); 
 
 }  // namespace
 
-DecodedImage jpeg_decode(const uint8_t* data, size_t n) {
+DecodedImage jpeg_decode(const uint8_t* data, size_t n, uint32_t expectW, uint32_t expectH) {
     if (n < 4 || data[0] != 0xFF || data[1] != 0xD8) corrupt("missing SOI");
     uint16_t q[4][64];  // natural order
     bool qdef[4] = {false, false, false, false};
@@ -421,6 +421,8 @@ DecodedImage jpeg_decode(const uint8_t* data, size_t n) {
             W = be16(s + 3);
             const int nc = s[5];
             if (W == 0 || H == 0) throw Error(BF_ERR_ARG, "JPEG: DNL-defined height is not supported");
+            if ((uint64_t)W * H > kMaxImagePixels) throw Error(BF_ERR_ARG, "JPEG: image dimensions exceed the decoder's limit");
+            if ((expectW && W != expectW) || (expectH && H != expectH)) corrupt("frame size differs from the container's");
             if ((nc != 1 && nc != 3) || slen < 6 + 3 * (size_t)nc) throw Error(BF_ERR_ARG, "JPEG: 1 or 3 components supported");
             comp.resize(nc);
             for (int c = 0; c < nc; c++) {
@@ -449,6 +451,7 @@ DecodedImage jpeg_decode(const uint8_t* data, size_t n) {
             throw Error(BF_ERR_ARG, "JPEG: progressive / lossless / arithmetic-coded streams are not supported");
         } else if (m == 0xDA) {  // SOS + entropy-coded data
             if (!frame) corrupt("scan before frame");
+            if (slen < 1) corrupt("bad SOS");
             const int ns = s[0];
             if (ns < 1 || ns > (int)comp.size() || slen < 1 + 2 * (size_t)ns + 3) corrupt("bad SOS");
             std::vector<Component*> sc;
@@ -577,7 +580,7 @@ inline uint8_t paeth(int a, int b, int c) {
 }
 }  // namespace
 
-DecodedImage png_decode(const uint8_t* data, size_t n) {
+DecodedImage png_decode(const uint8_t* data, size_t n, uint32_t expectW, uint32_t expectH) {
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
     if (n < 8 || std::memcmp(data, sig, 8) != 0) png_corrupt("bad signature");
     uint32_t W = 0, H = 0;
@@ -608,6 +611,11 @@ DecodedImage png_decode(const uint8_t* data, size_t n) {
         pos += 12 + len;
     }
     if (W == 0 || H == 0 || ctype < 0) png_corrupt("missing IHDR");
+    // ISO/IEC 15948 caps each dimension at 2^31 - 1; the pixel cap keeps (stride + 1) * H and the
+    // RGBX size far from size_t overflow whatever the file claims
+    if (W > 0x7FFFFFFFu || H > 0x7FFFFFFFu || (uint64_t)W * H > kMaxImagePixels)
+        throw Error(BF_ERR_ARG, "PNG: image dimensions exceed the decoder's limit");
+    if ((expectW && W != expectW) || (expectH && H != expectH)) png_corrupt("image size differs from the container's");
     if (depth != 8) throw Error(BF_ERR_ARG, "PNG: only 8-bit channels are supported");
     if (interlace != 0) throw Error(BF_ERR_ARG, "PNG: interlaced images are not supported");
     int ch = 0;

@@ -23,8 +23,14 @@ struct DecodedImage {
     std::vector<uint8_t> rgbx;  // width * height * 4
 };
 
-// Throws bf::Error (BF_ERR_IO for corrupt data, BF_ERR_ARG for unsupported variants).
-DecodedImage jpeg_decode(const uint8_t* data, size_t n);
-DecodedImage png_decode(const uint8_t* data, size_t n);
+// Largest image either decoder accepts (2^28 pixels = 1 GiB of RGBX; a VGA frame is 2^18.3): a
+// header claiming more is refused before anything is allocated.
+constexpr uint64_t kMaxImagePixels = 1ull << 28;
+
+// Throws bf::Error (BF_ERR_IO for corrupt data, BF_ERR_ARG for unsupported variants). expectW /
+// expectH (0 = any): the size the caller's container header states (the .sens colour size); a stream
+// whose own header disagrees is refused before its planes are allocated.
+DecodedImage jpeg_decode(const uint8_t* data, size_t n, uint32_t expectW = 0, uint32_t expectH = 0);
+DecodedImage png_decode(const uint8_t* data, size_t n, uint32_t expectW = 0, uint32_t expectH = 0);
 
 }  // namespace bf

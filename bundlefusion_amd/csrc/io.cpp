@@ -133,8 +133,9 @@ void SensReader::colorRGBX(uint64_t i, uint8_t* out) {
     }
     BF_REQUIRE(info_.colorCompression == 1 || info_.colorCompression == 2, BF_ERR_ARG,
                "unsupported colour compression " + std::to_string(info_.colorCompression));
-    const DecodedImage img = info_.colorCompression == 2 ? jpeg_decode(buf_.data(), buf_.size())
-                                                         : png_decode(buf_.data(), buf_.size());
+    const uint32_t cw = info_.colorWidth, ch = info_.colorHeight;
+    const DecodedImage img = info_.colorCompression == 2 ? jpeg_decode(buf_.data(), buf_.size(), cw, ch)
+                                                         : png_decode(buf_.data(), buf_.size(), cw, ch);
     BF_REQUIRE(img.width == info_.colorWidth && img.height == info_.colorHeight, BF_ERR_IO,
                "decoded colour frame size differs from the header");
     std::memcpy(out, img.rgbx.data(), 4 * n);

@@ -61,11 +61,15 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     // free, Scene::Scene). Measured on one GPU as one rank's share (--rehearse-shards G): +7 % at G = 4,
     // +11 % at G = 8, neutral at G = 2; unsharded it costs 3 % (the scene stream is the bound there),
     // so the streams keep the default priority (profiles/r3n_late_experiments.txt).
-    int prLeast = 0, prGreatest = 0;
-    BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
-    const int baPriority = (so && so->shardCount > 1) ? prGreatest : prLeast;
-    BF_HIP(hipStreamCreateWithPriority(&baStream_, hipStreamNonBlocking, baPriority));
-    BF_HIP(hipStreamCreateWithPriority(&localStream_, hipStreamNonBlocking, baPriority));
+    if (so && so->shardCount > 1) {
+        int prLeast = 0, prGreatest = 0;
+        BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
+        BF_HIP(hipStreamCreateWithPriority(&baStream_, hipStreamNonBlocking, prGreatest));
+        BF_HIP(hipStreamCreateWithPriority(&localStream_, hipStreamNonBlocking, prGreatest));
+    } else {  // normal priority, as the scene stream (ROCm's "least" priority is below normal)
+        BF_HIP(hipStreamCreateWithFlags(&baStream_, hipStreamNonBlocking));
+        BF_HIP(hipStreamCreateWithFlags(&localStream_, hipStreamNonBlocking));
+    }
     for (int b = 0; b < 2; b++) {
         BF_HIP(hipEventCreateWithFlags(&localDone_[b], hipEventDisableTiming));
         BF_HIP(hipEventCreateWithFlags(&globalDone_[b], hipEventDisableTiming));

@@ -449,7 +449,7 @@ int bf_mesh_save_ply(const char* path, const BFMcTriangle* tris, uint32_t n, con
 
 /* .sens reader (mLib SensorData v4 as SensorDataReader.cpp:38-116 uses it; format restated in
  * SURVEY.md Appendix B). Frames are read on demand. Depth: raw or zlib ushort; colour: raw RGB, PNG or
- * baseline/progressive JPEG (bf_image_decode); occi depth returns BF_ERR_ARG. */
+ * baseline / extended-sequential Huffman JPEG (SOF0 / SOF1, 8-bit; bf_image_decode; progressive is refused); occi depth returns BF_ERR_ARG. */
 typedef struct bf_sens bf_sens;
 int bf_sens_open(const char* path, bf_sens** out);
 int bf_sens_close(bf_sens* s);

@@ -95,3 +95,32 @@ def test_unsupported_and_corrupt_streams():
         bio.decode_image(b"\x89PNG\r\n\x1a\n" + struct.pack(">I", 13) + b"IHDR" + b"\x00" * 17, 1)
     with pytest.raises(bfa.BFError):
         bio.decode_image(png[:40], 1)
+
+
+def _png_chunk(kind: bytes, body: bytes) -> bytes:
+    import zlib
+    return struct.pack(">I", len(body)) + kind + body + struct.pack(">I", zlib.crc32(kind + body) & 0xFFFFFFFF)
+
+
+def test_hostile_headers_refused_before_allocation():
+    """Crafted headers: a PNG whose IHDR claims 2^16 x 2^16 or 2^31 x 1 pixels (so that
+    (stride + 1) * H or W * H * 4 would wrap a small zlib stream past the size check), and a JPEG SOS
+    segment of length 0 at the end of the buffer, are rejected with an error, never decoded."""
+    import zlib
+    for w, h in ((1 << 16, 1 << 16), (1 << 31, 1), (0xFFFFFFFF, 0xFFFFFFFF)):
+        ihdr = struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)
+        png = (b"\x89PNG\r\n\x1a\n" + _png_chunk(b"IHDR", ihdr) + _png_chunk(b"IDAT", zlib.compress(b"\x00" * 64))
+               + _png_chunk(b"IEND", b""))
+        with pytest.raises(bfa.BFError, match="limit"):
+            bio.decode_image(png, 1)
+    d, _ = _fixtures()
+    good = d["jpeg_64x48_s2_q90_r0__bytes"].tobytes()
+    sos = good.index(b"\xff\xda")
+    with pytest.raises(bfa.BFError):
+        bio.decode_image(good[:sos] + b"\xff\xda\x00\x02", 2)  # SOS with an empty body at the buffer's end
+    # a SOF0 claiming 65535 x 65535 (4.3 G pixels) is refused before its planes are allocated
+    sof = good.index(b"\xff\xc0")
+    big = bytearray(good)
+    big[sof + 5:sof + 9] = b"\xff\xff\xff\xff"
+    with pytest.raises(bfa.BFError, match="limit"):
+        bio.decode_image(bytes(big), 2)
