@@ -199,7 +199,8 @@ class BFCacheOptions(C.Structure):  # include/bf/types.h
 class BFCorrOptions(C.Structure):  # include/bf/types.h
     _fields_ = [("intrinsics", C.c_float * 4), ("intrinsicsInv", C.c_float * 16), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("stride", C.c_uint32), ("maxPerPair", C.c_uint32), ("minDepth", C.c_float),
-                ("maxDepth", C.c_float), ("depthThresh", C.c_float)]
+                ("maxDepth", C.c_float), ("depthThresh", C.c_float),
+                ("minPerPair", C.c_uint32)]
 
 
 class BFVoxelOp(C.Structure):  # include/bf/bf.h
@@ -223,6 +224,47 @@ class BFReconOptions(C.Structure):
                 ("cacheWidth", C.c_uint32), ("cacheHeight", C.c_uint32), ("cacheIntrinsics", C.c_float * 4),
                 ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("asyncBundling", C.c_int32),
                 ("solver", BFSolverOptions), ("disableLocalVerify", C.c_int32), ("verify", BFVerifyOptions)]
+
+
+class BFEndSequenceOptions(C.Structure):  # include/bf/bf.h: the render loop past the last frame
+    _fields_ = [("numSolveFramesBeforeExit", C.c_int32), ("disableDenseAtEnd", C.c_int32),
+                ("denseFrameLimit", C.c_uint32), ("denseDepthWeight", C.c_float), ("maxPastEndFrames", C.c_uint32)]
+
+
+class BFEndSequenceResult(C.Structure):
+    _fields_ = [("pastEndFrames", C.c_uint32), ("globalSolves", C.c_uint32), ("localSolved", C.c_uint32),
+                ("denseSolve", C.c_uint32), ("queueDrained", C.c_uint32), ("denseSolveMs", C.c_float),
+                ("last", BFSolveResult)]
+
+
+class BFQueueEvent(C.Structure):  # include/bf/bf.h: one TrajectoryManager call of the loop (recordOps)
+    _fields_ = [("kind", C.c_int32), ("frame", C.c_uint32), ("count", C.c_uint32), ("offset", C.c_uint32)]
+
+
+class BFAppOptions(C.Structure):  # include/bf/bf.h: the FriedLiver application (bf_app_*)
+    _fields_ = [("sensFile", C.c_char_p), ("outputDir", C.c_char_p), ("overwriteSens", C.c_int32),
+                ("skipOutputs", C.c_int32), ("asyncBundling", C.c_int32), ("recordOps", C.c_int32),
+                ("enableTiming", C.c_int32), ("maxFrames", C.c_uint32), ("frontEndDriftRad", C.c_float),
+                ("frontEndDriftM", C.c_float), ("frontEndSeed", C.c_uint32), ("noFrontEndDrift", C.c_int32),
+                ("corrStride", C.c_uint32), ("corrDepthThresh", C.c_float), ("prefetchFrames", C.c_uint32),
+                ("decodeThreads", C.c_uint32), ("numSolveFramesBeforeExit", C.c_int32)]
+
+
+class BFAppInfo(C.Structure):
+    _fields_ = [("hashParams", BFHashParams), ("integrationCamera", BFDepthCameraParams), ("numFrames", C.c_uint32),
+                ("sensorDepthWidth", C.c_uint32), ("sensorDepthHeight", C.c_uint32), ("sensorColorWidth", C.c_uint32),
+                ("sensorColorHeight", C.c_uint32),
+                ("preprocess", BFPreprocessOptions), ("cache", BFCacheOptions), ("corr", BFCorrOptions),
+                ("cacheIntrinsics", C.c_float * 4), ("submapSize", C.c_uint32), ("maxKeyframes", C.c_uint32),
+                ("maxLocalCorr", C.c_uint32), ("maxGlobalCorr", C.c_uint32), ("numSolveFramesBeforeExit", C.c_int32),
+                ("reserved", C.c_uint32 * 2)]
+
+
+class BFAppResult(C.Structure):
+    _fields_ = [("frames", C.c_uint32), ("loopSeconds", C.c_double), ("endSeconds", C.c_double),
+                ("end", BFEndSequenceResult), ("heapFreeCount", C.c_uint32), ("numTransforms", C.c_uint32),
+                ("numValidTransforms", C.c_uint32), ("valid", C.c_int32), ("meshTriangles", C.c_uint32),
+                ("meshVertices", C.c_uint32), ("meshFaces", C.c_uint32)]
 
 
 class BFReconStats(C.Structure):

@@ -12,7 +12,7 @@ from .abi import ENTRYJ_DTYPE, BFCorrOptions
 
 
 def corr_options(width, height, fx, fy, cx, cy, stride=16, max_per_pair=25, min_depth=0.1, max_depth=3.0,
-                 depth_thresh=0.02) -> BFCorrOptions:
+                 depth_thresh=0.02, min_per_pair=1) -> BFCorrOptions:
     o = BFCorrOptions()
     o.intrinsics[:] = [fx, fy, cx, cy]
     K = np.eye(4, dtype=np.float64)
@@ -20,6 +20,7 @@ def corr_options(width, height, fx, fy, cx, cy, stride=16, max_per_pair=25, min_
     o.intrinsicsInv[:] = np.linalg.inv(K).astype(np.float32).ravel().tolist()
     o.width, o.height, o.stride, o.maxPerPair = width, height, stride, max_per_pair
     o.minDepth, o.maxDepth, o.depthThresh = min_depth, max_depth, depth_thresh
+    o.minPerPair = min_per_pair
     return o
 
 

@@ -11,6 +11,8 @@
 #include "io.h"
 #include "cache.h"
 #include "frames.h"
+#include "app.h"
+#include "frontend.h"
 
 #include <cstring>
 #include <memory>
@@ -137,6 +139,50 @@ struct bf_preproc {
 extern "C" {
 
 int bf_abi_version(void) { return BF_ABI_VERSION; }
+int bf_abi_struct_size(const char* name, size_t* out) {
+    BF_TRY
+    BF_REQUIRE(name && out, BF_ERR_ARG, "null argument");
+    static const struct {
+        const char* n;
+        size_t s;
+    } kSizes[] = {
+        {"BFHashParams", sizeof(BFHashParams)},
+        {"BFDepthCameraParams", sizeof(BFDepthCameraParams)},
+        {"BFRayCastParams", sizeof(BFRayCastParams)},
+        {"BFHashEntry", sizeof(BFHashEntry)},
+        {"BFVoxel", sizeof(BFVoxel)},
+        {"BFEntryJ", sizeof(BFEntryJ)},
+        {"BFFixOp", sizeof(BFFixOp)},
+        {"BFSolveResult", sizeof(BFSolveResult)},
+        {"BFTsdfStats", sizeof(BFTsdfStats)},
+        {"BFSensInfo", sizeof(BFSensInfo)},
+        {"BFPreprocessOptions", sizeof(BFPreprocessOptions)},
+        {"BFMarchingCubesParams", sizeof(BFMarchingCubesParams)},
+        {"BFCacheOptions", sizeof(BFCacheOptions)},
+        {"BFCorrOptions", sizeof(BFCorrOptions)},
+        {"BFCachedFrame", sizeof(BFCachedFrame)},
+        {"BFSceneOptions", sizeof(BFSceneOptions)},
+        {"BFVoxelOp", sizeof(BFVoxelOp)},
+        {"BFSolverOptions", sizeof(BFSolverOptions)},
+        {"BFVerifyOptions", sizeof(BFVerifyOptions)},
+        {"BFReconOptions", sizeof(BFReconOptions)},
+        {"BFReconStats", sizeof(BFReconStats)},
+        {"BFEndSequenceOptions", sizeof(BFEndSequenceOptions)},
+        {"BFEndSequenceResult", sizeof(BFEndSequenceResult)},
+        {"BFQueueEvent", sizeof(BFQueueEvent)},
+        {"BFAppOptions", sizeof(BFAppOptions)},
+        {"BFAppInfo", sizeof(BFAppInfo)},
+        {"BFAppResult", sizeof(BFAppResult)},
+        {"BFMcTriangle", sizeof(BFMcTriangle)},
+        {"BFSynthScene", sizeof(BFSynthScene)}};
+    for (const auto& e : kSizes)
+        if (std::strcmp(e.n, name) == 0) {
+            *out = e.s;
+            return 0;
+        }
+    throw Error(BF_ERR_ARG, std::string("unknown struct ") + name);
+    BF_CATCH
+}
 const char* bf_last_error(void) { return g_lastError.c_str(); }
 
 int bf_device_count(int* count) {
@@ -801,12 +847,131 @@ int bf_recon_set_comm(bf_recon* r, bf_comm* c) {
     r->r->setComm(c ? c->c : nullptr);
     BF_CATCH
 }
+int bf_recon_attach_cache(bf_recon* r, bf_cache* c) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->attachCache(c ? c->c : nullptr);
+    BF_CATCH
+}
+int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW,
+                              uint32_t colorH) {
+    BF_TRY
+    BF_REQUIRE(r && depth && color, BF_ERR_ARG, "null argument");
+    r->r->setFrameSource(f, depth, color, colorW, colorH);
+    BF_CATCH
+}
+int bf_recon_end_sequence(bf_recon* r, const BFEndSequenceOptions* o, BFEndSequenceResult* out) {
+    BF_TRY
+    BF_REQUIRE(r && o, BF_ERR_ARG, "null argument");
+    const BFEndSequenceResult res = r->r->endSequence(*o);
+    if (out) *out = res;
+    BF_CATCH
+}
+int bf_recon_optimized_trajectory(bf_recon* r, float* T, uint32_t cap, uint32_t* n) {
+    BF_TRY
+    BF_REQUIRE(r && n && (T || cap == 0), BF_ERR_ARG, "null argument");
+    r->r->synchronize();
+    *n = r->r->optimizedTrajectory(reinterpret_cast<BFMat4*>(T), cap);
+    BF_CATCH
+}
+int bf_recon_queue_trace(bf_recon* r, BFQueueEvent* events, uint32_t capEvents, uint32_t* nEvents, float* transforms,
+                         uint32_t capTransforms, uint32_t* nTransforms, BFFixOp* fixes, uint32_t capFixes, uint32_t* nFixes) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    BF_REQUIRE((events || capEvents == 0) && (transforms || capTransforms == 0) && (fixes || capFixes == 0), BF_ERR_ARG,
+               "null output with a capacity");
+    const auto& ev = r->r->queueEvents();
+    const auto& tr = r->r->queueTransforms();
+    const auto& fx = r->r->queueFixes();
+    if (nEvents) *nEvents = (uint32_t)ev.size();
+    if (nTransforms) *nTransforms = (uint32_t)tr.size();
+    if (nFixes) *nFixes = (uint32_t)fx.size();
+    for (uint32_t i = 0; i < capEvents && i < ev.size(); i++) events[i] = ev[i];
+    for (uint32_t i = 0; i < capTransforms && i < tr.size(); i++) std::memcpy(transforms + 16 * (size_t)i, tr[i].m, 64);
+    for (uint32_t i = 0; i < capFixes && i < fx.size(); i++) fixes[i] = fx[i];
+    BF_CATCH
+}
 int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n) {
     BF_TRY
     BF_REQUIRE(r && n && (out || cap == 0), BF_ERR_ARG, "null argument");
     const auto& log = r->r->opLog();
     *n = (uint32_t)log.size();
     for (uint32_t i = 0; i < cap && i < log.size(); i++) out[i] = log[i];
+    BF_CATCH
+}
+
+// ---- the FriedLiver application ---------------------------------------------------------------
+struct bf_app {
+    App* a = nullptr;
+    bf_recon recon;  // borrowed view of the app's loop
+};
+
+int bf_app_create(const char* appParams, const char* bundlingParams, const BFAppOptions* o, bf_app** out) {
+    BF_TRY
+    BF_REQUIRE(appParams && bundlingParams && out, BF_ERR_ARG, "null argument");
+    *out = nullptr;
+    BFAppOptions def{};
+    def.asyncBundling = 1;
+    std::unique_ptr<bf_app> h(new bf_app);
+    h->a = new App(appParams, bundlingParams, o ? *o : def);
+    h->recon.r = &h->a->recon();
+    *out = h.release();
+    BF_CATCH
+}
+int bf_app_destroy(bf_app* a) {
+    BF_TRY
+    if (a) {
+        delete a->a;
+        delete a;
+    }
+    BF_CATCH
+}
+int bf_app_info(const bf_app* a, BFAppInfo* out) {
+    BF_TRY
+    BF_REQUIRE(a && out, BF_ERR_ARG, "null argument");
+    *out = a->a->info();
+    BF_CATCH
+}
+int bf_app_step(bf_app* a, int* gotFrame) {
+    BF_TRY
+    BF_REQUIRE(a, BF_ERR_ARG, "null app");
+    const bool got = a->a->step();
+    if (gotFrame) *gotFrame = got ? 1 : 0;
+    BF_CATCH
+}
+int bf_app_finish(bf_app* a, BFAppResult* out) {
+    BF_TRY
+    BF_REQUIRE(a, BF_ERR_ARG, "null app");
+    const BFAppResult r = a->a->finish();
+    if (out) *out = r;
+    BF_CATCH
+}
+int bf_app_run(bf_app* a, BFAppResult* out) {
+    BF_TRY
+    BF_REQUIRE(a, BF_ERR_ARG, "null app");
+    const BFAppResult r = a->a->run();
+    if (out) *out = r;
+    BF_CATCH
+}
+int bf_app_recon(bf_app* a, bf_recon** out) {
+    BF_TRY
+    BF_REQUIRE(a && out, BF_ERR_ARG, "null argument");
+    *out = &a->recon;
+    BF_CATCH
+}
+int bf_front_end_tinc(const float prev[16], const float cur[16], uint32_t frame, uint32_t seed, float driftRad, float driftM,
+                      float Tinc[16]) {
+    BF_TRY
+    BF_REQUIRE(prev && cur && Tinc, BF_ERR_ARG, "null argument");
+    const BFMat4 T = front_end_tinc(prev, cur, frame, seed, driftRad, driftM);
+    std::memcpy(Tinc, T.m, 64);
+    BF_CATCH
+}
+int bf_app_front_end_pose(const bf_app* a, uint32_t f, float Tinc[16]) {
+    BF_TRY
+    BF_REQUIRE(a && Tinc, BF_ERR_ARG, "null argument");
+    const BFMat4 T = a->a->frontEndPose(f);
+    std::memcpy(Tinc, T.m, 64);
     BF_CATCH
 }
 
@@ -1090,6 +1255,19 @@ int bf_sens_writer_add_frame(bf_sens_writer* w, const float camToWorld[16], uint
     w->w->addFrame(camToWorld, tsColor, tsDepth, depth, rgbx);
     BF_CATCH
 }
+int bf_sens_save_trajectory(const char* in, const char* out, const float* T, uint64_t n) {
+    BF_TRY
+    BF_REQUIRE(in && out && (T || n == 0), BF_ERR_ARG, "null argument");
+    sens_save_with_trajectory(in, out, reinterpret_cast<const BFMat4*>(T), n);
+    BF_CATCH
+}
+int bf_sens_writer_add_compressed_frame(bf_sens_writer* w, const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth,
+                                        const uint8_t* color, uint64_t colorBytes, const uint8_t* depth, uint64_t depthBytes) {
+    BF_TRY
+    BF_REQUIRE(w && camToWorld, BF_ERR_ARG, "null argument");
+    w->w->addCompressedFrame(camToWorld, tsColor, tsDepth, color, colorBytes, depth, depthBytes);
+    BF_CATCH
+}
 int bf_sens_writer_close(bf_sens_writer* w) {
     BF_TRY
     if (w) {
@@ -1154,66 +1332,19 @@ int bf_params_get_bool(const bf_params* p, const char* key, int* out) {
 int bf_params_hash_params(const bf_params* p, BFHashParams* o) {
     BF_TRY
     BF_REQUIRE(p && o, BF_ERR_ARG, "null argument");
-    const ParamFile& f = p->f;
-    std::memset(o, 0, sizeof(*o));
-    for (int i = 0; i < 16; i += 5) { o->rigidTransform.m[i] = 1.0f; o->rigidTransformInverse.m[i] = 1.0f; }
-    o->hashNumBuckets = (uint32_t)f.number("s_hashNumBuckets");
-    o->hashBucketSize = BF_HASH_BUCKET_SIZE;
-    o->hashMaxCollisionLinkedListSize = (uint32_t)f.number("s_hashMaxCollisionLinkedListSize");
-    o->numSDFBlocks = (uint32_t)f.number("s_hashNumSDFBlocks");
-    o->SDFBlockSize = BF_SDF_BLOCK_SIZE;
-    o->virtualVoxelSize = (float)f.floats("s_SDFVoxelSize").at(0);
-    o->maxIntegrationDistance = f.floats("s_SDFMaxIntegrationDistance").at(0);
-    o->truncation = f.floats("s_SDFTruncation").at(0);
-    o->truncScale = f.floats("s_SDFTruncationScale").at(0);
-    o->integrationWeightSample = (uint32_t)f.number("s_SDFIntegrationWeightSample");
-    o->integrationWeightMax = (uint32_t)f.number("s_SDFIntegrationWeightMax");
-    const std::vector<float> ext = f.floats("s_streamingVoxelExtents"), dims = f.floats("s_streamingGridDimensions"),
-                             minp = f.floats("s_streamingMinGridPos");
-    BF_REQUIRE(ext.size() == 3 && dims.size() == 3 && minp.size() == 3, BF_ERR_ARG, "streaming vectors need 3 values");
-    o->streamingVoxelExtents = BFFloat3{ext[0], ext[1], ext[2]};
-    o->streamingGridDimensions = BFInt3{(int)dims[0], (int)dims[1], (int)dims[2]};
-    o->streamingMinGridPos = BFInt3{(int)minp[0], (int)minp[1], (int)minp[2]};
-    o->streamingInitialChunkListSize = (uint32_t)f.number("s_streamingInitialChunkListSize");
+    *o = hash_params_from(p->f);
     BF_CATCH
 }
 int bf_params_raycast_params(const bf_params* p, float fx, float fy, float mx, float my, BFRayCastParams* o) {
     BF_TRY
     BF_REQUIRE(p && o, BF_ERR_ARG, "null argument");
-    const ParamFile& f = p->f;
-    const uint32_t rw = (uint32_t)f.number("s_rayCastWidth"), rh = (uint32_t)f.number("s_rayCastHeight");
-    const uint32_t iw = (uint32_t)f.number("s_integrationWidth"), ih = (uint32_t)f.number("s_integrationHeight");
-    if (rw != iw || rh != ih) {  // adapt intrinsics (CUDARayCastSDF.h:26-32)
-        fx *= (float)rw / (float)iw;
-        fy *= (float)rh / (float)ih;
-        mx *= (float)(rw - 1) / (float)(iw - 1);
-        my *= (float)(rh - 1) / (float)(ih - 1);
-    }
-    std::memset(o, 0, sizeof(*o));
-    o->width = rw;
-    o->height = rh;
-    o->fx = fx; o->fy = fy; o->mx = mx; o->my = my;
-    o->minDepth = f.floats("s_renderDepthMin").at(0);
-    o->maxDepth = f.floats("s_renderDepthMax").at(0);
-    o->rayIncrement = f.floats("s_SDFRayIncrementFactor").at(0) * f.floats("s_SDFTruncation").at(0);
-    o->thresSampleDist = f.floats("s_SDFRayThresSampleDistFactor").at(0) * o->rayIncrement;
-    o->thresDist = f.floats("s_SDFRayThresDistFactor").at(0) * o->rayIncrement;
-    o->useGradients = f.boolean("s_SDFUseGradients") ? 1 : 0;
-    o->maxNumVertices = (uint32_t)f.number("s_hashNumSDFBlocks") * 6;
+    *o = raycast_params_from(p->f, fx, fy, mx, my);
     BF_CATCH
 }
 int bf_params_preprocess_options(const bf_params* p, float depthShift, BFPreprocessOptions* o) {
     BF_TRY
     BF_REQUIRE(p && o, BF_ERR_ARG, "null argument");
-    const ParamFile& f = p->f;
-    o->erode = f.boolean("s_erodeSIFTdepth") ? 1 : 0;
-    o->erodeStructureSize = 3;      // CUDAImageManager.cpp:95-103
-    o->erodeDepthThresh = 0.05f;
-    o->erodeFraction = 0.3f;
-    o->depthFilter = f.boolean("s_depthFilter") ? 1 : 0;
-    o->sigmaD = f.floats("s_depthSigmaD").at(0);
-    o->sigmaR = f.floats("s_depthSigmaR").at(0);
-    o->depthShift = depthShift;
+    *o = preprocess_options_from(p->f, depthShift);
     BF_CATCH
 }
 

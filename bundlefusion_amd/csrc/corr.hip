@@ -112,9 +112,10 @@ __global__ __launch_bounds__(CORR_WG) void k_corr_pairs(CorrArgs A) {
 }
 
 // pair order: exclusive scan of the counts (one workgroup), then each thread copies its pair's slots
+// (a pair with fewer than minPerPair matches contributes none: the matcher's s_minNumMatches filter)
 __global__ __launch_bounds__(1024) void k_corr_pack(const BFEntryJ* __restrict__ slots, const uint32_t* __restrict__ counts,
-                                                    uint32_t pairs, uint32_t maxPerPair, BFEntryJ* out, uint32_t cap,
-                                                    uint32_t* total) {
+                                                    uint32_t pairs, uint32_t maxPerPair, uint32_t minPerPair, BFEntryJ* out,
+                                                    uint32_t cap, uint32_t* total) {
     __shared__ uint32_t sWave[16];
     __shared__ uint32_t carry;
     if (threadIdx.x == 0) carry = 0;
@@ -122,7 +123,8 @@ __global__ __launch_bounds__(1024) void k_corr_pack(const BFEntryJ* __restrict__
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t r = 0; r < pairs; r += 1024) {
         const uint32_t p = r + threadIdx.x;
-        const uint32_t c = p < pairs ? counts[p] : 0u;
+        uint32_t c = p < pairs ? counts[p] : 0u;
+        if (c < minPerPair) c = 0;
         uint32_t incl = c;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t t = __shfl_up(incl, o);
@@ -181,7 +183,7 @@ uint32_t corr_from_depth(const float* const* depth, const float* T, const float*
     hipStream_t s = nullptr;
     k_corr_pairs<<<pairs, CORR_WG, 0, s>>>(A);
     BF_LAUNCH_CHECK();
-    k_corr_pack<<<1, 1024, 0, s>>>(slots.p, counts.p, pairs, o.maxPerPair, out, cap, tot.p);
+    k_corr_pack<<<1, 1024, 0, s>>>(slots.p, counts.p, pairs, o.maxPerPair, o.minPerPair, out, cap, tot.p);
     BF_LAUNCH_CHECK();
     uint32_t t = 0;
     BF_HIP(hipMemcpyAsync(&t, tot.p, 4, hipMemcpyDeviceToHost, s));

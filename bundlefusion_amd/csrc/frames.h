@@ -21,6 +21,11 @@ public:
     // device pointers; queued on the stream
     void run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut);
     hipStream_t stream() const { return stream_; }
+    // the sensor-size images of the last run that CUDAImageManager::copyToBundling hands the bundler
+    // (CUDAImageManager.h:223-227): d_depthInputRaw (the two erosion passes end in it) and
+    // d_depthInputFiltered (the bilateral filter's output; the raw image when the filter is off)
+    const float* rawDepth() const { return a_.p; }
+    const float* filteredDepth() const { return opt_.depthFilter ? b_.p : a_.p; }
 
 private:
     uint32_t dw_, dh_, cw_, ch_, iw_, ih_;

@@ -143,8 +143,8 @@ void SensReader::colorRGBX(uint64_t i, uint8_t* out) {
 
 // ---- writer ------------------------------------------------------------------------------------
 SensWriter::SensWriter(const std::string& path, const BFSensInfo& info) : info_(info) {
-    BF_REQUIRE(info.colorCompression == 0 && (info.depthCompression == 0 || info.depthCompression == 1), BF_ERR_ARG,
-               "writer supports raw colour and raw / zlib depth");
+    BF_REQUIRE(info.colorCompression >= 0 && info.colorCompression <= 2 && info.depthCompression >= 0 && info.depthCompression <= 2,
+               BF_ERR_ARG, "unknown compression type");
     f_ = std::fopen(path.c_str(), "wb");
     BF_REQUIRE(f_ != nullptr, BF_ERR_IO, "cannot create " + path);
     const uint32_t version = 4;
@@ -176,9 +176,25 @@ SensWriter::~SensWriter() {
     }
 }
 
+void SensWriter::addCompressedFrame(const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth, const uint8_t* color,
+                                    uint64_t colorBytes, const uint8_t* depth, uint64_t depthBytes) {
+    BF_REQUIRE(f_ != nullptr, BF_ERR_STATE, "writer closed");
+    BF_REQUIRE((color || colorBytes == 0) && (depth || depthBytes == 0), BF_ERR_ARG, "null frame payload");
+    wr(f_, camToWorld, 16);
+    wr(f_, &tsColor);
+    wr(f_, &tsDepth);
+    wr(f_, &colorBytes);
+    wr(f_, &depthBytes);
+    if (colorBytes) wr(f_, color, colorBytes);
+    if (depthBytes) wr(f_, depth, depthBytes);
+    numFrames_++;
+}
+
 void SensWriter::addFrame(const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth, const uint16_t* depth,
                           const uint8_t* rgbx) {
     BF_REQUIRE(f_ != nullptr, BF_ERR_STATE, "writer closed");
+    BF_REQUIRE(info_.colorCompression == 0 && (info_.depthCompression == 0 || info_.depthCompression == 1), BF_ERR_ARG,
+               "addFrame encodes raw colour and raw / zlib depth (add pre-compressed streams with addCompressedFrame)");
     const uint64_t nd = (uint64_t)info_.depthWidth * info_.depthHeight, nc = (uint64_t)info_.colorWidth * info_.colorHeight;
     std::vector<uint8_t> rgb(3 * nc);
     for (uint64_t p = 0; p < nc; p++) {
@@ -214,6 +230,41 @@ void SensWriter::close() {
     wr(f_, &numFrames_);
     std::fclose(f_);
     f_ = nullptr;
+}
+
+void sens_save_with_trajectory(const std::string& in, const std::string& out, const BFMat4* T, uint64_t n) {
+    std::vector<uint64_t> offsets;
+    {
+        SensReader r(in);
+        offsets.resize(r.info().numFrames);
+        for (uint64_t i = 0; i < offsets.size(); i++) offsets[i] = r.poseOffset(i);
+    }
+    if (out != in) {
+        FILE* src = std::fopen(in.c_str(), "rb");
+        BF_REQUIRE(src != nullptr, BF_ERR_IO, "cannot open " + in);
+        FILE* dst = std::fopen(out.c_str(), "wb");
+        if (!dst) {
+            std::fclose(src);
+            throw Error(BF_ERR_IO, "cannot create " + out);
+        }
+        std::vector<uint8_t> buf(1 << 24);
+        bool ok = true;
+        for (size_t k; ok && (k = std::fread(buf.data(), 1, buf.size(), src)) > 0;) ok = std::fwrite(buf.data(), 1, k, dst) == k;
+        ok = ok && !std::ferror(src);
+        std::fclose(src);
+        ok = (std::fclose(dst) == 0) && ok;
+        BF_REQUIRE(ok, BF_ERR_IO, "copy " + in + " -> " + out + " failed");
+    }
+    FILE* f = std::fopen(out.c_str(), "r+b");
+    BF_REQUIRE(f != nullptr, BF_ERR_IO, "cannot open " + out);
+    float ninf[16];
+    for (float& v : ninf) v = -std::numeric_limits<float>::infinity();
+    bool ok = true;
+    for (uint64_t i = 0; ok && i < offsets.size(); i++) {
+        ok = fseeko(f, (off_t)offsets[i], SEEK_SET) == 0 && std::fwrite(i < n ? T[i].m : ninf, 4, 16, f) == 16;
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    BF_REQUIRE(ok, BF_ERR_IO, "writing the trajectory into " + out + " failed");
 }
 
 // ---- zParameters: `name = value;`, `//` comments outside quotes, values up to ';' ------------
@@ -404,6 +455,72 @@ uint64_t corr_load(const std::string& path, BFEntryJ* corr, uint64_t cap) {
     std::fclose(f);
     BF_REQUIRE(ok, BF_ERR_IO, "truncated correspondence file " + path);
     return n;
+}
+
+// CUDASceneRepHashSDF::parametersFromGlobalAppState (CUDASceneRepHashSDF.h:39-59)
+BFHashParams hash_params_from(const ParamFile& f) {
+    BFHashParams out;
+    BFHashParams* o = &out;
+    std::memset(o, 0, sizeof(*o));
+    for (int i = 0; i < 16; i += 5) { o->rigidTransform.m[i] = 1.0f; o->rigidTransformInverse.m[i] = 1.0f; }
+    o->hashNumBuckets = (uint32_t)f.number("s_hashNumBuckets");
+    o->hashBucketSize = BF_HASH_BUCKET_SIZE;
+    o->hashMaxCollisionLinkedListSize = (uint32_t)f.number("s_hashMaxCollisionLinkedListSize");
+    o->numSDFBlocks = (uint32_t)f.number("s_hashNumSDFBlocks");
+    o->SDFBlockSize = BF_SDF_BLOCK_SIZE;
+    o->virtualVoxelSize = (float)f.floats("s_SDFVoxelSize").at(0);
+    o->maxIntegrationDistance = f.floats("s_SDFMaxIntegrationDistance").at(0);
+    o->truncation = f.floats("s_SDFTruncation").at(0);
+    o->truncScale = f.floats("s_SDFTruncationScale").at(0);
+    o->integrationWeightSample = (uint32_t)f.number("s_SDFIntegrationWeightSample");
+    o->integrationWeightMax = (uint32_t)f.number("s_SDFIntegrationWeightMax");
+    const std::vector<float> ext = f.floats("s_streamingVoxelExtents"), dims = f.floats("s_streamingGridDimensions"),
+                             minp = f.floats("s_streamingMinGridPos");
+    BF_REQUIRE(ext.size() == 3 && dims.size() == 3 && minp.size() == 3, BF_ERR_ARG, "streaming vectors need 3 values");
+    o->streamingVoxelExtents = BFFloat3{ext[0], ext[1], ext[2]};
+    o->streamingGridDimensions = BFInt3{(int)dims[0], (int)dims[1], (int)dims[2]};
+    o->streamingMinGridPos = BFInt3{(int)minp[0], (int)minp[1], (int)minp[2]};
+    o->streamingInitialChunkListSize = (uint32_t)f.number("s_streamingInitialChunkListSize");
+    return out;
+}
+// CUDARayCastSDF::parametersFromGlobalAppState (CUDARayCastSDF.h:24-51)
+BFRayCastParams raycast_params_from(const ParamFile& f, float fx, float fy, float mx, float my) {
+    BFRayCastParams out;
+    BFRayCastParams* o = &out;
+    const uint32_t rw = (uint32_t)f.number("s_rayCastWidth"), rh = (uint32_t)f.number("s_rayCastHeight");
+    const uint32_t iw = (uint32_t)f.number("s_integrationWidth"), ih = (uint32_t)f.number("s_integrationHeight");
+    if (rw != iw || rh != ih) {  // adapt intrinsics (CUDARayCastSDF.h:26-32)
+        fx *= (float)rw / (float)iw;
+        fy *= (float)rh / (float)ih;
+        mx *= (float)(rw - 1) / (float)(iw - 1);
+        my *= (float)(rh - 1) / (float)(ih - 1);
+    }
+    std::memset(o, 0, sizeof(*o));
+    o->width = rw;
+    o->height = rh;
+    o->fx = fx; o->fy = fy; o->mx = mx; o->my = my;
+    o->minDepth = f.floats("s_renderDepthMin").at(0);
+    o->maxDepth = f.floats("s_renderDepthMax").at(0);
+    o->rayIncrement = f.floats("s_SDFRayIncrementFactor").at(0) * f.floats("s_SDFTruncation").at(0);
+    o->thresSampleDist = f.floats("s_SDFRayThresSampleDistFactor").at(0) * o->rayIncrement;
+    o->thresDist = f.floats("s_SDFRayThresDistFactor").at(0) * o->rayIncrement;
+    o->useGradients = f.boolean("s_SDFUseGradients") ? 1 : 0;
+    o->maxNumVertices = (uint32_t)f.number("s_hashNumSDFBlocks") * 6;
+    return out;
+}
+// CUDAImageManager::process options from the bundling parameters
+BFPreprocessOptions preprocess_options_from(const ParamFile& f, float depthShift) {
+    BFPreprocessOptions out{};
+    BFPreprocessOptions* o = &out;
+    o->erode = f.boolean("s_erodeSIFTdepth") ? 1 : 0;
+    o->erodeStructureSize = 3;      // CUDAImageManager.cpp:95-103
+    o->erodeDepthThresh = 0.05f;
+    o->erodeFraction = 0.3f;
+    o->depthFilter = f.boolean("s_depthFilter") ? 1 : 0;
+    o->sigmaD = f.floats("s_depthSigmaD").at(0);
+    o->sigmaR = f.floats("s_depthSigmaR").at(0);
+    o->depthShift = depthShift;
+    return out;
 }
 
 }  // namespace bf

@@ -25,6 +25,8 @@ public:
     void timestamps(uint64_t frame, uint64_t* tsColor, uint64_t* tsDepth) const;
     void depthU16(uint64_t frame, uint16_t* out);
     void colorRGBX(uint64_t frame, uint8_t* out);
+    // file offset of frame i's camToWorld matrix (the 64 B before its timestamps and sizes)
+    uint64_t poseOffset(uint64_t frame) const { return this->frame(frame).colorOffset - 32 - 64; }
 
 private:
     struct Frame {
@@ -44,6 +46,9 @@ public:
     SensWriter(const std::string& path, const BFSensInfo& info);
     ~SensWriter();
     void addFrame(const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth, const uint16_t* depth, const uint8_t* rgbx);
+    // streams already compressed as the header's colorCompression / depthCompression say (e.g. JPEG colour)
+    void addCompressedFrame(const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth, const uint8_t* color,
+                            uint64_t colorBytes, const uint8_t* depth, uint64_t depthBytes);
     void close();
 
 private:
@@ -53,6 +58,11 @@ private:
     uint64_t numFrames_ = 0;
     std::vector<uint8_t> buf_;
 };
+
+// SensorDataReader::saveToFile (SensorDataReader.cpp:153-166): the input file with frame i's camToWorld
+// replaced by T[i] for i < n and by -inf for the rest; every other byte (compressed colour / depth, IMU
+// records) as read. out == in patches the file in place (the reference overwrites its input).
+void sens_save_with_trajectory(const std::string& in, const std::string& out, const BFMat4* T, uint64_t n);
 
 // Indexed mesh of CUDAMarchingCubesHashSDF::saveMesh (CUDAMarchingCubesHashSDF.cpp:71-100)
 struct Mesh {
@@ -84,5 +94,10 @@ public:
 private:
     std::map<std::string, std::string> kv_;
 };
+
+// zParameters -> the structs the path reads (the bf_params_* getters)
+BFHashParams hash_params_from(const ParamFile& f);
+BFRayCastParams raycast_params_from(const ParamFile& f, float fx, float fy, float mx, float my);
+BFPreprocessOptions preprocess_options_from(const ParamFile& f, float depthShift);
 
 }  // namespace bf

@@ -27,6 +27,21 @@ BFMat4 identity() {
 }
 template <class T>
 T or_default(T v, T d) { return v ? v : d; }
+BFSolveResult to_abi(const SolveResult& r) {
+    BFSolveResult o{};
+    o.gnIterations = r.gnIterations;
+    o.pcgIterations = r.pcgIterations;
+    o.maxResidual = r.maxResidual;
+    o.maxResidualIndex = r.maxResidualIndex;
+    o.energy = r.energy;
+    o.highResidualCount = r.highResidualCount;
+    o.numDensePairs = r.numDensePairs;
+    o.error = r.error;
+    o.skipped = r.skipped;
+    o.verifyUsed = r.verifyUsed;
+    o.verifyOk = r.verifyOk;
+    return o;
+}
 template <class T>
 T* pinned(size_t n) {
     void* p = nullptr;
@@ -173,6 +188,7 @@ Recon::~Recon() {
         if (localDone_[b]) (void)hipEventDestroy(localDone_[b]);
         if (globalDone_[b]) (void)hipEventDestroy(globalDone_[b]);
     }
+    if (cacheEv_) (void)hipEventDestroy(cacheEv_);
     for (Pending& p : ring_) {
         if (p.done) (void)hipEventDestroy(p.done);
         for (void* q : {(void*)p.localT, (void*)p.globalT, (void*)p.valid, (void*)p.ctrl, (void*)p.localInit,
@@ -276,6 +292,7 @@ void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
 // (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls).
 void Recon::runReintegrate() {
     tm_->nextFixes(opt_.maxFrameFixes, ops_);
+    traceQueue(2, 0, (uint32_t)ops_.size(), nullptr, &ops_);
     std::vector<VoxelOp>& batch = batch_;
     batch.clear();
     if (pendingInt_) {  // the previous frame's integration, in its place in the call sequence
@@ -314,6 +331,9 @@ void Recon::processFrame(uint32_t f) {
     BF_REQUIRE(f < opt_.maxFrames && frames_[f].set, BF_ERR_STATE, "frame not in the frame store");
     const uint32_t S = opt_.submapSize;
     const uint32_t s = f / S;
+    // processInput -> storeCachedFrame before anything reads the frame's cache (the submap ending at
+    // this frame includes it as its overlap frame)
+    if (cache_) storeCacheFrame(f);
     applyPending(false);
     FrameRef& fr = frames_[f];
     if (f % S == 0 && f > 0) {
@@ -332,6 +352,7 @@ void Recon::processFrame(uint32_t f) {
     logOp(2, f, &T);
     st_.integrations++;
     tm_->addFrame(FrameType::Integrated, T, f);
+    traceQueue(0, f, 1, &T, nullptr);
     numFrames_++;
     st_.frames++;
 }
@@ -350,8 +371,10 @@ void Recon::flushIntegrate() {
 void Recon::finish() {
     const uint32_t S = opt_.submapSize;
     if (numFrames_ == 0) return;
-    const uint32_t s = (numFrames_ - 1) / S;
-    if (s != lastSubmapEnqueued_) endSubmap(s, numFrames_ - s * S);
+    const uint32_t s = (numFrames_ - 1) / S, n = numFrames_ - s * S;
+    // a last submap of one frame is only the previous submap's overlap frame, solved with it
+    // (isLastLocalFrame skips prepareLocalSolve for it, OnlineBundler.cpp:170-172, OnlineBundler.h:42)
+    if (s != lastSubmapEnqueued_ && n >= 2) endSubmap(s, n);
     synchronize();
 }
 
@@ -396,6 +419,8 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     P.job = lastJob_;
     inflight_.push_back(slot);
     lastSubmapEnqueued_ = s;
+    // m_totalNumOptLocalFrames (OnlineBundler.cpp:268): the frames the complete trajectory covers
+    optimizedFrames_ = S * s + std::min(n, S);
 }
 
 void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache,
@@ -407,6 +432,7 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
     // ---- local solve over frames base .. base+n-1 (first frame fixed), on the local stream ----------
     // set bi was last read by global solve s - 2
     BF_HIP(hipStreamWaitEvent(localStream_, globalDone_[bi], 0));
+    if (cacheEv_) BF_HIP(hipStreamWaitEvent(localStream_, cacheEv_, 0));  // the submap's cache frames
     BF_HIP(hipMemcpyAsync(B.T.p, P.localInit, 64 * n, hipMemcpyHostToDevice, localStream_));
     matrices_to_poses(B.T.p, n, B.rot.p, B.trans, B.valid.p, localStream_);
     // multi-GPU: submap s's local solve runs on rank s % R only (the submaps are independent units,
@@ -542,6 +568,7 @@ void Recon::issueEndSolve(uint32_t slot, uint32_t nk, uint32_t ncorr, float wDen
     a.trans = dGlobalTrans_.p;
     a.rebuildJT = true;
     a.findMaxResidual = true;
+    if (cacheEv_ && wDense > 0.0f) BF_HIP(hipStreamWaitEvent(baStream_, cacheEv_, 0));
     const uint32_t last = nk - 1;
     if (comm_ && last < pairBound_.size()) a.pairBound = std::max(pairBound_[last], 1u);
     BF_HIP(hipEventRecord(t0, baStream_));
@@ -560,7 +587,14 @@ SolveResult Recon::endSolve(float wDense, float* ms) {
     synchronize();  // every submap result applied: the ring is empty
     const uint32_t S = opt_.submapSize;
     BF_REQUIRE(numFrames_ > 0, BF_ERR_STATE, "end solve before the first frame");
-    const uint32_t last = (numFrames_ - 1) / S, nk = last + 1;
+    // the global problem holds one keyframe per solved submap (fuseToGlobal, OnlineBundler.cpp:298)
+    if (lastSubmapEnqueued_ == 0xFFFFFFFFu) {
+        SolveResult none{};
+        none.skipped = 1;
+        if (ms) *ms = 0.0f;
+        return none;
+    }
+    const uint32_t last = lastSubmapEnqueued_, nk = last + 1;
     const uint32_t ncorr = (last < globalPrefix_.size()) ? globalPrefix_[last] : globalCorrN_;
     SolveResult res{};
     res.skipped = 1;
@@ -722,6 +756,7 @@ void Recon::apply(Pending& P) {
     if (!P.endSolve && !localOk) st_.invalidLocals++;
     if (P.globalSolved) {
         const SolveResult r = Solver::decodeResult(P.ctrl + Solver::kResultWords);
+        lastGlobalResult_ = r;
         if (!r.skipped) {
             st_.globalSolves++;
             st_.globalGnIterations += r.gnIterations;
@@ -740,12 +775,13 @@ void Recon::apply(Pending& P) {
     }
     // frames of invalid keyframes (and of invalidated local submaps) get -inf transforms: the queue
     // de-integrates them (invalidateImages + updateTrajectoryCU, OnlineBundler.cpp:317-320, 387-394)
-    const uint32_t optimized = P.endSolve ? numFrames_ : std::min(S * s + std::min(n, S), numFrames_);
+    const uint32_t optimized = P.endSolve ? std::min(optimizedFrames_, numFrames_) : std::min(S * s + std::min(n, S), numFrames_);
     for (uint32_t g = 0; g < optimized; g++) {
         const uint32_t k = g / S;
         complete_[g] = (globalValid_[k] && localKnown_[k]) ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();
     }
     tm_->updateOptimizedTransforms(complete_.data(), optimized);
+    traceQueue(1, 0, optimized, complete_.data(), nullptr);
 }
 
 void Recon::synchronize() {
@@ -779,6 +815,122 @@ void Recon::resetStats() {
     scene_->applyClock().reset();
     local_->solveClock().reset();
     global_->solveClock().reset();
+}
+
+void Recon::attachCache(Cache* c) {
+    BF_REQUIRE(numFrames_ == 0, BF_ERR_STATE, "attach the cache before the first frame");
+    BF_REQUIRE(!c || c->config().width == opt_.cacheWidth && c->config().height == opt_.cacheHeight, BF_ERR_ARG,
+               "cache size differs from the loop's cacheWidth x cacheHeight");
+    cache_ = c;
+    if (c && !cacheEv_) BF_HIP(hipEventCreateWithFlags(&cacheEv_, hipEventDisableTiming));
+}
+
+void Recon::setFrameSource(uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH) {
+    BF_REQUIRE(f < opt_.maxFrames, BF_ERR_CAPACITY, "frame index beyond maxFrames");
+    FrameRef& r = frames_[f];
+    r.srcDepth = depth;
+    r.srcColor = color;
+    r.srcW = colorW;
+    r.srcH = colorH;
+}
+
+// Bundler::storeCachedFrame (Bundler.cpp:278-281) for frame f, on the cache's stream
+void Recon::storeCacheFrame(uint32_t f) {
+    FrameRef& fr = frames_[f];
+    BF_REQUIRE(cache_->numFrames() == f, BF_ERR_STATE, "attached cache must hold exactly the frames before this one");
+    const float* d = fr.srcDepth ? fr.srcDepth : fr.depth;
+    const uint8_t* c = fr.srcDepth ? fr.srcColor : fr.color;
+    const uint32_t w = fr.srcDepth ? fr.srcW : cam_.imageWidth, h = fr.srcDepth ? fr.srcH : cam_.imageHeight;
+    cache_->storeFrame(d, c, w, h);
+    fr.cache = cache_->frame(f);
+    BF_HIP(hipEventRecord(cacheEv_, cache_->stream()));
+}
+
+BFEndSequenceResult Recon::endSequence(const BFEndSequenceOptions& o) {
+    BFEndSequenceResult res{};
+    synchronize();
+    if (numFrames_ == 0) return res;
+    const int32_t N = o.numSolveFramesBeforeExit;
+    const uint32_t cap = o.maxPastEndFrames ? o.maxPastEndFrames : 100000u;
+    const uint32_t denseLimit = o.denseFrameLimit ? o.denseFrameLimit : 10000u;
+    const float wDense = o.denseDepthWeight > 0.0f ? o.denseDepthWeight : 15.0f;
+    const uint32_t S = opt_.submapSize, last = (numFrames_ - 1) / S, n = numFrames_ - last * S;
+    auto keyframeCaches = [&]() {
+        if (lastSubmapEnqueued_ == 0xFFFFFFFFu) return false;
+        for (uint32_t k = 0; k <= lastSubmapEnqueued_; k++)
+            if (!frames_[k * S].cache.depth) return false;
+        return true;
+    };
+    for (uint32_t p = 0; p < cap; p++) {
+        res.pastEndFrames = p + 1;
+        if (N < 0 || (int64_t)p <= (int64_t)N) {
+            if (p == 0 && last != lastSubmapEnqueued_ && n >= 2) {
+                // prepareLocalSolve(curFrame, true) at the first past-the-end processInput, then process():
+                // the partial submap's local solve, fuseToGlobal and the global solve
+                const uint64_t before = st_.globalSolves;
+                endSubmap(last, n);
+                synchronize();
+                res.localSolved = 1;
+                res.globalSolves += (uint32_t)(st_.globalSolves - before);
+                res.last = to_abi(lastGlobalResult_);
+            } else {
+                // setSolveWeights(sparse 1, dense depth 15, colour 0) at numFramesPastEnd == N (:177-189)
+                const bool dense = N >= 0 && (int64_t)p == (int64_t)N && !o.disableDenseAtEnd &&
+                                   numFrames_ - 1 < denseLimit && keyframeCaches();
+                float ms = 0.0f;
+                const SolveResult r = endSolve(dense ? wDense : 0.0f, &ms);
+                if (!r.skipped) res.globalSolves++;
+                if (dense) {
+                    res.denseSolve = 1;
+                    res.denseSolveMs = ms;
+                }
+                res.last = to_abi(r);
+            }
+        }
+        reintegrate();
+        // exit check (DepthSensing.cpp:1116-1123) once the solves are done
+        if (N < 0 || (int64_t)p >= (int64_t)N) {
+            tm_->generateUpdateLists();
+            const uint32_t active = tm_->numActiveOperations();
+            traceQueue(3, 0, active, nullptr, nullptr);
+            if (active == 0) {
+                res.queueDrained = 1;
+                break;
+            }
+        }
+    }
+    synchronize();
+    return res;
+}
+
+uint32_t Recon::optimizedTrajectory(BFMat4* out, uint32_t cap) const {
+    const uint32_t n = std::min(tm_->numAddedFrames(), tm_->numOptimizedFrames());
+    for (uint32_t i = 0; i < n && i < cap; i++)
+        out[i] = tm_->type(i) == FrameType::Invalid ? ninf_mat() : tm_->optimized(i);
+    return n;
+}
+
+void Recon::traceQueue(int32_t kind, uint32_t frame, uint32_t count, const BFMat4* T, const std::vector<FixOp>* fixes) {
+    if (!opt_.recordOps) return;
+    BFQueueEvent e{};
+    e.kind = kind;
+    e.frame = frame;
+    e.count = count;
+    if (kind == 0 || kind == 1) {
+        e.offset = (uint32_t)qT_.size();
+        qT_.insert(qT_.end(), T, T + count);
+    } else if (kind == 2) {
+        e.offset = (uint32_t)qFixes_.size();
+        for (const FixOp& op : *fixes) {
+            BFFixOp b{};
+            b.kind = (int32_t)op.kind;
+            b.frame = op.frame;
+            std::memcpy(b.oldT, op.oldT.m, 64);
+            std::memcpy(b.newT, op.newT.m, 64);
+            qFixes_.push_back(b);
+        }
+    }
+    qEvents_.push_back(e);
 }
 
 void Recon::trajectory(BFMat4* out, uint32_t n) const {

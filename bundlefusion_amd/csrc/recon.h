@@ -31,6 +31,7 @@
 
 #include "../../include/bf/bf.h"
 #include "ba.h"
+#include "cache.h"
 #include "trajectory.h"
 #include "tsdf.h"
 
@@ -53,6 +54,18 @@ public:
     void synchronize();  // drain both streams and apply every pending bundling result
     // one end-of-sequence global solve over every keyframe (dense depth weight wDense when > 0); waits
     SolveResult endSolve(float wDense, float* ms);
+    // the render loop past the last frame (bf_recon_end_sequence: OnlineBundler.cpp:167-196, 373-408,
+    // DepthSensing.cpp:1114-1126)
+    BFEndSequenceResult endSequence(const BFEndSequenceOptions& o);
+    // per-frame CUDACache::storeFrame inside processFrame (OnlineBundler.cpp:199-204); c is borrowed
+    void attachCache(Cache* c);
+    void setFrameSource(uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH);
+    // TrajectoryManager::getOptimizedTransforms (TrajectoryManager.h:50-68)
+    uint32_t optimizedTrajectory(BFMat4* out, uint32_t cap) const;
+    // recordOps: the TrajectoryManager call sequence (bf_recon_queue_trace)
+    const std::vector<BFQueueEvent>& queueEvents() const { return qEvents_; }
+    const std::vector<BFMat4>& queueTransforms() const { return qT_; }
+    const std::vector<BFFixOp>& queueFixes() const { return qFixes_; }
     // recordOps history: submap s's local trajectory and the keyframe poses after its global solve
     void submapPoses(uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal, uint32_t* numKeyframes,
                      int32_t* localValid) const;
@@ -107,6 +120,9 @@ private:
         BFCachedFrame cache{};
         BFMat4 Tinc{};    // front-end estimate: camera f in camera f-1 coordinates
         BFMat4 Tlocal{};  // chained estimate relative to the submap's first frame
+        const float* srcDepth = nullptr;   // cache source images (setFrameSource; null: the frame store's)
+        const uint8_t* srcColor = nullptr;
+        uint32_t srcW = 0, srcH = 0;
         bool set = false;
         bool tilesReady = false;  // its band-cull depth tiles and dc image are in frameTiles_ / frameDC_
     };
@@ -143,6 +159,8 @@ private:
     VoxelOp pendingOp_{};
     void flushIntegrate();
     uint32_t lastSubmapEnqueued_ = 0xFFFFFFFFu;
+    uint32_t optimizedFrames_ = 0;      // frames covered by the complete trajectory (m_totalNumOptLocalFrames)
+    SolveResult lastGlobalResult_{};
     uint32_t numFrames_ = 0;
 
     std::vector<Pending> ring_;
@@ -193,6 +211,16 @@ private:
 
     BFReconStats st_{};
     std::vector<BFFixOp> log_;
+
+    Cache* cache_ = nullptr;            // attached frame cache (borrowed)
+    hipEvent_t cacheEv_ = nullptr;      // the last storeFrame on the cache's stream
+    void storeCacheFrame(uint32_t f);
+
+    // recordOps: TrajectoryManager call trace
+    std::vector<BFQueueEvent> qEvents_;
+    std::vector<BFMat4> qT_;
+    std::vector<BFFixOp> qFixes_;
+    void traceQueue(int32_t kind, uint32_t frame, uint32_t count, const BFMat4* T, const std::vector<FixOp>* fixes);
 };
 
 }  // namespace bf

@@ -116,6 +116,56 @@ def write_sens(path: str, depth_u16, rgbx, poses, depth_intrinsic, color_intrins
         check(lib().bf_sens_writer_close(w))
 
 
+class SensWriter:
+    """bf_sens_writer_*: frames encoded here (raw RGB, raw / zlib depth) or passed pre-compressed (e.g. JPEG
+    colour + zlib depth: the copyroom / apt0 layout)."""
+
+    def __init__(self, path: str, info: BFSensInfo):
+        self.h = C.c_void_p()
+        check(lib().bf_sens_writer_create(path.encode(), C.byref(info), C.byref(self.h)))
+
+    def add_frame(self, pose, depth_u16: np.ndarray, rgbx: np.ndarray, ts=(0, 0)):
+        d = np.ascontiguousarray(depth_u16, np.uint16)
+        c = np.ascontiguousarray(rgbx, np.uint8)
+        check(lib().bf_sens_writer_add_frame(self.h, _mat(pose), C.c_uint64(ts[0]), C.c_uint64(ts[1]),
+                                             d.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p)))
+
+    def add_compressed_frame(self, pose, color: bytes, depth: bytes, ts=(0, 0)):
+        cb = (C.c_uint8 * max(1, len(color))).from_buffer_copy(color or b"\0")
+        db = (C.c_uint8 * max(1, len(depth))).from_buffer_copy(depth or b"\0")
+        check(lib().bf_sens_writer_add_compressed_frame(self.h, _mat(pose), C.c_uint64(ts[0]), C.c_uint64(ts[1]), cb,
+                                                        C.c_uint64(len(color)), db, C.c_uint64(len(depth))))
+
+    def close(self):
+        if self.h:
+            check(lib().bf_sens_writer_close(self.h))
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def sens_info(depth_wh, color_wh, depth_intrinsic, color_intrinsic=None, color_compression=0, depth_compression=1,
+              depth_shift=1000.0, name="bundlefusion_amd synthetic") -> BFSensInfo:
+    info = BFSensInfo()
+    info.version = 4
+    info.sensorName = name.encode()[:255]
+    ident = np.eye(4, dtype=np.float32).reshape(16)
+    info.depthIntrinsic[:] = np.asarray(depth_intrinsic, np.float32).reshape(16)
+    info.colorIntrinsic[:] = np.asarray(color_intrinsic if color_intrinsic is not None else depth_intrinsic,
+                                        np.float32).reshape(16)
+    info.depthExtrinsic[:] = ident
+    info.colorExtrinsic[:] = ident
+    info.colorCompression, info.depthCompression = color_compression, depth_compression
+    info.depthWidth, info.depthHeight = depth_wh
+    info.colorWidth, info.colorHeight = color_wh
+    info.depthShift = depth_shift
+    return info
+
+
 class ParameterFile:
     """zParameters*.txt; later loads override earlier keys."""
 

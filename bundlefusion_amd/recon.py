@@ -8,7 +8,8 @@ import ctypes as C
 import numpy as np
 
 from . import check, lib
-from .abi import BFFixOp, BFReconOptions, BFReconStats, BFSolveResult, BFTsdfStats
+from .abi import (BFEndSequenceOptions, BFEndSequenceResult, BFFixOp, BFQueueEvent, BFReconOptions, BFReconStats,
+                  BFSolveResult, BFTsdfStats)
 
 FIX_DEINTEGRATE, FIX_INTEGRATE, FIX_REINTEGRATE, OP_GC = 1, 2, 3, 4
 
@@ -84,10 +85,17 @@ class Recon:
         check(lib().bf_recon_create(C.byref(params), C.byref(scene_opts) if scene_opts is not None else None,
                                     C.byref(cam), C.byref(opts), C.byref(self.h)))
 
+    @classmethod
+    def borrowed(cls, handle: C.c_void_p, params, cam, owner=None):
+        """A view of a loop owned elsewhere (bf_app_recon): never destroyed through this object."""
+        r = cls.__new__(cls)
+        r.h, r.params, r.cam, r._borrowed, r._owner = handle, params, cam, True, owner
+        return r
+
     def close(self):
-        if self.h:
+        if self.h and not getattr(self, "_borrowed", False):
             lib().bf_recon_destroy(self.h)
-            self.h = C.c_void_p()
+        self.h = C.c_void_p()
 
     def __del__(self):
         try:
@@ -132,6 +140,60 @@ class Recon:
         ms = C.c_float()
         check(lib().bf_recon_end_solve(self.h, C.c_float(dense_depth_weight), C.byref(r), C.byref(ms)))
         return {k: getattr(r, k) for k, _ in BFSolveResult._fields_}, ms.value
+
+    def end_sequence(self, num_solve_frames_before_exit: int = 30, dense_at_end: bool = True,
+                     dense_frame_limit: int = 10000, dense_depth_weight: float = 15.0, max_past_end_frames: int = 0):
+        """The render loop past the last frame (bf_recon_end_sequence: OnlineBundler.cpp:167-196, 373-408;
+        DepthSensing.cpp:1114-1126): the last submap, s_numSolveFramesBeforeExit global solves (the last with
+        the dense term), then re-integration until the queue is empty. Returns the result as a dict."""
+        o = BFEndSequenceOptions(int(num_solve_frames_before_exit), 0 if dense_at_end else 1, int(dense_frame_limit),
+                                 float(dense_depth_weight), int(max_past_end_frames))
+        r = BFEndSequenceResult()
+        check(lib().bf_recon_end_sequence(self.h, C.byref(o), C.byref(r)))
+        out = {k: getattr(r, k) for k, _ in BFEndSequenceResult._fields_ if k != "last"}
+        out["last"] = {k: getattr(r.last, k) for k, _ in BFSolveResult._fields_}
+        return out
+
+    def attach_cache(self, cache):
+        """CUDACache::storeFrame per processed frame (OnlineBundler.cpp:199-204); cache: cache.CUDACache."""
+        self._cache = cache
+        check(lib().bf_recon_attach_cache(self.h, cache.h if cache is not None else None))
+
+    def set_frame_source(self, f: int, depth_ptr: int, color_ptr: int, color_w: int, color_h: int):
+        check(lib().bf_recon_set_frame_source(self.h, C.c_uint32(f), C.c_void_p(depth_ptr), C.c_void_p(color_ptr),
+                                              C.c_uint32(color_w), C.c_uint32(color_h)))
+
+    def optimized_trajectory(self) -> np.ndarray:
+        """TrajectoryManager::getOptimizedTransforms: the trajectory StopScanningAndExit saves."""
+        n = C.c_uint32()
+        check(lib().bf_recon_optimized_trajectory(self.h, None, C.c_uint32(0), C.byref(n)))
+        T = np.zeros((max(1, n.value), 4, 4), np.float32)
+        check(lib().bf_recon_optimized_trajectory(self.h, T.ctypes.data_as(C.c_void_p), C.c_uint32(n.value), C.byref(n)))
+        return T[:n.value]
+
+    def queue_trace(self):
+        """recordOps: the TrajectoryManager call sequence as a list of (kind, frame, payload):
+        0 addFrame -> 4x4 T; 1 updateOptimizedTransform -> [count,4,4]; 2 fix loop -> list of
+        (kind, frame, oldT, newT); 3 exit check -> active op count."""
+        ne, nt, nf = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().bf_recon_queue_trace(self.h, None, 0, C.byref(ne), None, 0, C.byref(nt), None, 0, C.byref(nf)))
+        ev = (BFQueueEvent * max(1, ne.value))()
+        T = np.zeros((max(1, nt.value), 4, 4), np.float32)
+        fx = (BFFixOp * max(1, nf.value))()
+        check(lib().bf_recon_queue_trace(self.h, ev, ne.value, C.byref(ne), T.ctypes.data_as(C.c_void_p), nt.value,
+                                         C.byref(nt), fx, nf.value, C.byref(nf)))
+        out = []
+        for e in ev[:ne.value]:
+            if e.kind == 0:
+                out.append((0, e.frame, T[e.offset]))
+            elif e.kind == 1:
+                out.append((1, e.count, T[e.offset:e.offset + e.count]))
+            elif e.kind == 2:
+                out.append((2, e.count, [(fx[i].kind, fx[i].frame, np.array(fx[i].oldT[:], np.float32),
+                                          np.array(fx[i].newT[:], np.float32)) for i in range(e.offset, e.offset + e.count)]))
+            else:
+                out.append((3, e.count, None))
+        return out
 
     def submap_poses(self, s: int, max_keyframes: int, submap_size: int = 10):
         """recordOps history of submap s: (local float32[n,4,4], global float32[k,4,4], valid int32[k], local_ok)."""

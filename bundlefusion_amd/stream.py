@@ -124,3 +124,50 @@ class SyntheticStream:
                 recon.set_local_correspondences(s, self.local_corr.ptr.value + 32 * self.local_off[s], self.local_n[s])
         recon.set_global_correspondences(self.global_corr.ptr.value, len(self.global_host), self.global_prefix)
         recon.set_initial_pose(self.gt[0])
+
+
+def write_synthetic_sens(path: str, num_frames: int, width: int = 640, height: int = 480, seed: int = 0,
+                         color_codec: str = "jpeg", jpeg_quality: int = 90, device: bool = True, log=None):
+    """A `.sens` of the seeded synthetic room (SURVEY.md §8(d) inputs) in the copyroom / apt0 layout: JPEG
+    (or PNG / raw) colour, zlib ushort depth in millimetres, the ground-truth camera trajectory, the depth
+    camera's intrinsics. Frames are rendered on the GPU (device=True) or with the host renderer, and the
+    colour is compressed with PIL (the image library mLib's SensorData uses for its colour streams)."""
+    import io as _io
+    import zlib
+
+    from .io import SensWriter, sens_info
+    f = 577.87 * width / 640.0
+    cam = depth_camera(width, height, fx=f, fy=f)
+    K = np.eye(4, dtype=np.float32)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = cam.fx, cam.fy, cam.mx, cam.my
+    cc = {"raw": 0, "png": 1, "jpeg": 2}[color_codec]
+    scene = synth_scene(seed)
+    if color_codec != "raw":
+        from PIL import Image
+    if device:
+        dd = DeviceArray((height, width), np.float32)
+        dc = DeviceArray((height, width, 4), np.uint8)
+    t0 = time.perf_counter()
+    with SensWriter(path, sens_info((width, height), (width, height), K, color_compression=cc)) as w:
+        for i in range(num_frames):
+            T = synth_pose(i)
+            if device:
+                check(lib().bf_synth_render(C.byref(scene), abi.mat(T), C.byref(cam), C.c_uint32(1), C.c_uint32(i),
+                                            dd.ptr, dc.ptr))
+                d, c = dd.download(), dc.download()
+            else:
+                from . import synth_render_host
+                d, c = synth_render_host(scene, T, cam, 1, i)
+            # the renderer quantises to 1 mm (the .sens convention, SensorDataReader.cpp:104-107)
+            du = np.where(np.isfinite(d) & (d > 0), np.rint(d * 1000.0), 0).astype(np.uint16)
+            rgb = np.ascontiguousarray(c[..., :3])
+            if cc == 0:
+                col = rgb.tobytes()
+            else:
+                b = _io.BytesIO()
+                Image.fromarray(rgb).save(b, "JPEG", quality=jpeg_quality) if cc == 2 else Image.fromarray(rgb).save(b, "PNG")
+                col = b.getvalue()
+            w.add_compressed_frame(T, col, zlib.compress(du.tobytes(), 1), ts=(i, i))
+    if log:
+        log(f"wrote {num_frames} frames {width}x{height} ({color_codec}) to {path} in {time.perf_counter() - t0:.1f}s")
+    return cam

@@ -27,6 +27,8 @@ extern "C" {
 
 /* ---- runtime ------------------------------------------------------------- */
 int bf_abi_version(void);
+/* sizeof of a struct of types.h / bf.h by name (bindings check their layouts against it) */
+int bf_abi_struct_size(const char* name, size_t* out);
 const char* bf_last_error(void);
 int bf_device_count(int* count);
 int bf_set_device(int device);
@@ -375,6 +377,70 @@ int bf_recon_op_log(bf_recon* r, BFFixOp* out, uint32_t cap, uint32_t* n);
  * the image pairs of each keyframe prefix of the global correspondences (computed when they are set). */
 int bf_recon_set_comm(bf_recon* r, bf_comm* c);
 
+/* Per-frame dense-term cache construction inside the loop (OnlineBundler::processInput ->
+ * Bundler::storeCachedFrame -> CUDACache::storeFrame, OnlineBundler.cpp:199-204). With a cache attached,
+ * bf_recon_process_frame(f) first stores frame f into it (slot f: the cache must hold exactly f frames at
+ * that point) from the frame's source images — those of bf_recon_set_frame_source, else the frame store's
+ * depth and colour at the integration size — and the local solves read those cache frames (ordered after
+ * the cache's stream by an event). The cache is borrowed: it must outlive the loop. */
+typedef struct bf_cache bf_cache;
+int bf_recon_attach_cache(bf_recon* r, bf_cache* c);
+int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW,
+                              uint32_t colorH);
+
+/* The end of the sequence (the render loop past the last input frame): OnlineBundler::processInput's
+ * past-the-end branch (OnlineBundler.cpp:167-196), process() -> optimizeGlobal with isSequenceDone (:373-408)
+ * and the exit check of OnD3D11FrameRender (DepthSensing/DepthSensing.cpp:1114-1126), in the single-threaded
+ * order (the reference's bundling thread races the render loop; this is its RUN_MULTITHREADED-off schedule).
+ * Past-the-end iteration p = 0, 1, ...:
+ *   p = 0: the last (partial) submap's local solve + a global solve (prepareLocalSolve(curFrame, true)), or a
+ *          global solve alone when the last submap was already solved;
+ *   1 <= p < N: a global solve over every keyframe (sparse, max-residual removal: s_numOptPerResidualRemoval 1);
+ *   p == N: the same with dense depth weight denseDepthWeight (15) when USE_GLOBAL_DENSE_AT_END applies
+ *          (fewer than denseFrameLimit frames, every keyframe has a cache frame), else sparse;
+ *   then reintegrate(); from p >= N on, the loop stops when generateUpdateLists leaves no active op.
+ * N = numSolveFramesBeforeExit (s_numSolveFramesBeforeExit, 30). N < 0 (the reference's -1: never stop
+ * solving) solves every iteration and checks the queue from p = 0 on. maxPastEndFrames caps the iterations
+ * (0 = 100000). Waits for every solve (deterministic). */
+typedef struct BFEndSequenceOptions {
+    int32_t numSolveFramesBeforeExit;  /* [30] */
+    int32_t disableDenseAtEnd;         /* 1: no USE_GLOBAL_DENSE_AT_END switch */
+    uint32_t denseFrameLimit;          /* [10000] m_lastFrameProcessed < 10000 (OnlineBundler.cpp:179); 0 = default */
+    float denseDepthWeight;            /* [15] (0 = default) */
+    uint32_t maxPastEndFrames;         /* [100000] */
+} BFEndSequenceOptions;
+typedef struct BFEndSequenceResult {
+    uint32_t pastEndFrames;   /* render-loop iterations past the last frame */
+    uint32_t globalSolves;    /* global solves issued past the end (incl. the last submap's) */
+    uint32_t localSolved;     /* 1 if p = 0 solved a last partial submap */
+    uint32_t denseSolve;      /* 1 if the USE_GLOBAL_DENSE_AT_END solve ran with the dense term */
+    uint32_t queueDrained;    /* 1 if the loop stopped with no re-integration op left (0: hit the cap) */
+    float denseSolveMs;       /* device time of that solve */
+    BFSolveResult last;       /* the last global solve */
+} BFEndSequenceResult;
+int bf_recon_end_sequence(bf_recon* r, const BFEndSequenceOptions* o, BFEndSequenceResult* out);
+
+/* TrajectoryManager::getOptimizedTransforms (TrajectoryManager.h:50-68): min(#added, #optimized) frames,
+ * -inf for Invalid frames; the trajectory StopScanningAndExit writes (DepthSensing.cpp:921-934). HOST
+ * T[16 * cap]; *n = frame count (min(cap, n) written). */
+int bf_recon_optimized_trajectory(bf_recon* r, float* T, uint32_t cap, uint32_t* n);
+
+/* With recordOps: every TrajectoryManager call the loop made, in order, so a test can drive a second
+ * TrajectoryManager through the identical call sequence (the queue checked apart from BA float drift):
+ *   kind 0 addFrame(Integrated, T, frame)            T = transforms[offset]
+ *   kind 1 updateOptimizedTransform(count frames)    transforms[offset .. offset + count)
+ *   kind 2 reintegrate()'s fix loop: count ops       fixes[offset .. offset + count) (kind 1/2/3 BFFixOp)
+ *   kind 3 generateUpdateLists + getNumActiveOperations (the exit check), count = the result
+ * Any output may be NULL with cap 0; *n* = totals. */
+typedef struct BFQueueEvent {
+    int32_t kind;
+    uint32_t frame;
+    uint32_t count;
+    uint32_t offset;
+} BFQueueEvent;
+int bf_recon_queue_trace(bf_recon* r, BFQueueEvent* events, uint32_t capEvents, uint32_t* nEvents, float* transforms,
+                         uint32_t capTransforms, uint32_t* nTransforms, BFFixOp* fixes, uint32_t capFixes, uint32_t* nFixes);
+
 /* ---- re-integration queue alone (host; TrajectoryManager.h:6-118) ---------------------- */
 typedef struct bf_traj bf_traj;
 
@@ -395,7 +461,6 @@ int bf_pose_helper_matrix_to_pose(const float T[16], float out[6]);
  * its Sobel derivatives (the CUDACachedFrame the dense term reads). Device storage is owned by the
  * cache; bf_cache_frame hands out a BFCachedFrame of device pointers for bf_solver_solve /
  * bf_recon_set_frame. Work is queued on the cache's own stream. */
-typedef struct bf_cache bf_cache;
 int bf_cache_create(const BFCacheOptions* o, bf_cache** out);
 int bf_cache_destroy(bf_cache* c);
 /* storeFrame (CUDACache.cpp:45-94): device depth (inputWidth x inputHeight float metres, -inf invalid,
@@ -460,12 +525,21 @@ int bf_sens_read_depth_u16(bf_sens* s, uint64_t frame, uint16_t* out);      /* h
 /* SensorDataReader::processDepth (:104-107): d / depthShift, 0 -> -inf */
 int bf_sens_read_depth(bf_sens* s, uint64_t frame, float* out);             /* host, depthW*depthH */
 int bf_sens_read_color(bf_sens* s, uint64_t frame, uint8_t* rgbx);           /* host, colorW*colorH*4, X = 255 */
-/* writer (SensorData::saveToFile layout; numFrames patched on close): raw RGB colour, raw or zlib depth */
+/* writer (SensorData::saveToFile layout; numFrames patched on close): bf_sens_writer_add_frame encodes raw RGB
+ * colour and raw or zlib depth; any compression with pre-compressed frames */
 typedef struct bf_sens_writer bf_sens_writer;
 int bf_sens_writer_create(const char* path, const BFSensInfo* info, bf_sens_writer** out);
 int bf_sens_writer_add_frame(bf_sens_writer* w, const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth,
                              const uint16_t* depth, const uint8_t* rgbx);
+/* a frame whose colour / depth streams are already compressed as the header says (JPEG / PNG colour, zlib
+ * depth): written as given (SensorData::saveToFile keeps the compressed streams) */
+int bf_sens_writer_add_compressed_frame(bf_sens_writer* w, const float camToWorld[16], uint64_t tsColor, uint64_t tsDepth,
+                                        const uint8_t* color, uint64_t colorBytes, const uint8_t* depth, uint64_t depthBytes);
 int bf_sens_writer_close(bf_sens_writer* w);
+/* SensorDataReader::saveToFile (SensorDataReader.cpp:153-166) as StopScanningAndExit uses it: the input .sens
+ * with frame i's camToWorld = T[i] (HOST float[16 n]) for i < n and -inf after, every other byte unchanged;
+ * out == in rewrites the file in place (the reference overwrites its input). */
+int bf_sens_save_trajectory(const char* in, const char* out, const float* T, uint64_t n);
 /* The colour-stream decoders behind bf_sens_read_color (colorCompression 1 = PNG, 2 = JPEG; the
  * reference decodes through mLib, SensorDataReader.cpp:98-116): data[n] -> RGBX (X = 255). Call with
  * rgbx = NULL to get the size; otherwise rgbx holds cap bytes (>= 4 * width * height). */
@@ -501,6 +575,85 @@ int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_
 int bf_preproc_destroy(bf_preproc* p);
 int bf_preproc_run(bf_preproc* p, const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut);
 int bf_preproc_synchronize(bf_preproc* p);
+
+/* ---- the FriedLiver application over the path: main() + the render loop --------
+ * FriedLiver.cpp:184-320 reads two parameter files (argv[1] zParametersDefault.txt -> GlobalAppState,
+ * argv[2] zParametersBundlingDefault.txt -> GlobalBundlingState; argv[3] overrides s_binaryDumpSensorFile,
+ * :228-250), opens the .sens (SensorDataReader::createFirstConnected, SensorDataReader.cpp:38-79) and runs
+ * OnD3D11FrameRender per input frame (DepthSensing.cpp:966-1129). Per frame here:
+ *   CUDAImageManager::process (CUDAImageManager.cpp:22-158): read + decode the frame (prefetch threads),
+ *     H2D, erode x2, bilateral filter, resample into the device-resident frame store;
+ *   OnlineBundler::processInput (OnlineBundler.cpp:167-227): CUDACache::storeFrame from the sensor-size
+ *     eroded depth + colour; the SiftGPU stand-in: bf_corr_from_depth EntryJ between the frames of each
+ *     submap and between keyframes (matched with the .sens trajectory, s_minNumMatches filter), and the
+ *     front end's frame-to-frame estimate (see bundlefusion_amd/csrc/frontend.h);
+ *   the loop (bf_recon_process_frame): re-integration queue + integrate, local/global BA per submap.
+ * At the end of the input: bf_recon_end_sequence (s_numSolveFramesBeforeExit), then StopScanningAndExit
+ * (DepthSensing.cpp:904-953): the optimized trajectory into a .sens (SensorDataReader::saveToFile,
+ * SensorDataReader.cpp:153-166), marching cubes into <sens stem>.ply, processed.txt. */
+typedef struct bf_app bf_app;
+typedef struct BFAppOptions {
+    const char* sensFile;       /* argv[3]: overrides s_binaryDumpSensorFile (NULL: the parameter) */
+    const char* outputDir;      /* directory of the exit outputs (NULL: the .sens file's, as the reference) */
+    int32_t overwriteSens;      /* 1: the trajectory goes into the input .sens (the reference overwrites it);
+                                   0: into <outputDir>/<stem>.optimized.sens */
+    int32_t skipOutputs;        /* 1: no .sens / .ply / processed.txt */
+    int32_t asyncBundling;      /* BFReconOptions.asyncBundling (the app default is 1) */
+    int32_t recordOps;          /* BFReconOptions.recordOps (tests) */
+    int32_t enableTiming;       /* BFReconOptions.enableTiming */
+    uint32_t maxFrames;         /* read at most this many frames (0: all; CUDAImageManager also stops at
+                                   s_maxNumImages * s_submapSize) */
+    float frontEndDriftRad;     /* front-end error per frame (rotation sigma, rad) [0.000873 = 0.05 deg] */
+    float frontEndDriftM;       /* (translation sigma, m) [0.002] */
+    uint32_t frontEndSeed;      /* [1] */
+    int32_t noFrontEndDrift;    /* 1: the .sens relative motion exactly */
+    uint32_t corrStride;        /* EntryJ producer sampling grid, pixels [16] */
+    float corrDepthThresh;      /* depth agreement, m [0.02] */
+    uint32_t prefetchFrames;    /* decoded frames ahead [16] */
+    uint32_t decodeThreads;     /* [4] */
+    int32_t numSolveFramesBeforeExit; /* overrides s_numSolveFramesBeforeExit when != 0 (-2: run no past-end phase) */
+} BFAppOptions;
+typedef struct BFAppInfo {      /* what the app derived from the parameters and the .sens header */
+    BFHashParams hashParams;    /* (the 16-byte aligned members first) */
+    BFDepthCameraParams integrationCamera; /* the depth intrinsics scaled to the integration size (CUDAImageManager.h:160-166) */
+    uint32_t numFrames;         /* frames it will process */
+    uint32_t sensorDepthWidth, sensorDepthHeight, sensorColorWidth, sensorColorHeight;
+    BFPreprocessOptions preprocess;
+    BFCacheOptions cache;
+    BFCorrOptions corr;         /* EntryJ producer: sensor depth size and intrinsics */
+    float cacheIntrinsics[4];
+    uint32_t submapSize, maxKeyframes, maxLocalCorr, maxGlobalCorr;
+    int32_t numSolveFramesBeforeExit;
+    uint32_t reserved[2];       /* (size a multiple of 16) */
+} BFAppInfo;
+typedef struct BFAppResult {
+    uint32_t frames;            /* input frames processed */
+    double loopSeconds;         /* wall time of the frame loop (input decode overlapped) */
+    double endSeconds;          /* wall time of the end-of-sequence phase */
+    BFEndSequenceResult end;
+    uint32_t heapFreeCount;     /* getHeapFreeCount at exit */
+    uint32_t numTransforms, numValidTransforms;  /* of the optimized trajectory (PoseHelper::countNumValidTransforms) */
+    int32_t valid;              /* processed.txt's verdict: heap free >= 800 and >= half the transforms valid */
+    uint32_t meshTriangles, meshVertices, meshFaces;
+} BFAppResult;
+int bf_app_create(const char* appParams, const char* bundlingParams, const BFAppOptions* o, bf_app** out);
+int bf_app_destroy(bf_app* a);
+int bf_app_info(const bf_app* a, BFAppInfo* out);
+/* one input frame through the loop; *gotFrame = 0 once the input has ended (nothing done) */
+int bf_app_step(bf_app* a, int* gotFrame);
+/* end of sequence + StopScanningAndExit outputs (after the last step) */
+int bf_app_finish(bf_app* a, BFAppResult* out);
+/* FriedLiver main: every frame, then finish */
+int bf_app_run(bf_app* a, BFAppResult* out);
+/* the app's loop (borrowed: do not destroy) for the bf_recon_* queries (op log, submap poses, trajectory) */
+int bf_app_recon(bf_app* a, bf_recon** out);
+/* The stand-in front end's frame-to-frame estimate (computeSiftTransformCU's role, OnlineBundler.cu:6-71;
+ * bundlefusion_amd/csrc/frontend.h): inv(prev) * cur * a seeded error step (rotation sigma driftRad, translation
+ * sigma driftM; both 0: the exact relative motion), identity when a pose is not finite. Host only. */
+int bf_front_end_tinc(const float prev[16], const float cur[16], uint32_t frame, uint32_t seed, float driftRad, float driftM,
+                      float Tinc[16]);
+/* inputs the app handed the loop for frame f (tests): Tinc (HOST float[16]) */
+int bf_app_front_end_pose(const bf_app* a, uint32_t f, float Tinc[16]);
 
 #ifdef __cplusplus
 }

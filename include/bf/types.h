@@ -232,6 +232,7 @@ typedef struct BFCorrOptions {
     uint32_t maxPerPair;       /* MAX_MATCHES_PER_IMAGE_PAIR_FILTERED [25], <= 64 */
     float minDepth, maxDepth;  /* accepted depth range (metres) */
     float depthThresh;         /* |depth_cur - z| agreement (metres) */
+    uint32_t minPerPair;       /* a pair with fewer matches keeps none (s_minNumMatchesLocal / Global [5]); 0 = 1 */
 } BFCorrOptions;
 
 #ifdef __cplusplus

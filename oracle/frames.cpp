@@ -91,9 +91,22 @@ void gaussIntensity(float* out, const float* in, float sigmaD, int W, int H) {  
 
 }  // namespace
 
+extern "C" void or_preprocess2(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh,
+                               const uint8_t* rgbx, uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, float* depthOut,
+                               uint8_t* colorOut, float* rawOut, float* filteredOut);
+
 extern "C" void or_preprocess(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh,
                               const uint8_t* rgbx, uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, float* depthOut,
                               uint8_t* colorOut) {
+    or_preprocess2(o, depthU16, dw, dh, rgbx, cw, ch, iw, ih, depthOut, colorOut, nullptr, nullptr);
+}
+
+// ... plus the sensor-size images CUDAImageManager::copyToBundling hands the bundler
+// (CUDAImageManager.h:223-227): d_depthInputRaw (after the two erosion passes, which end in it) and
+// d_depthInputFiltered (the bilateral filter's output, or the raw copy without it); either may be NULL
+extern "C" void or_preprocess2(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh,
+                               const uint8_t* rgbx, uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, float* depthOut,
+                               uint8_t* colorOut, float* rawOut, float* filteredOut) {
     const size_t n = (size_t)dw * dh;
     std::vector<float> raw(n), filtered(n);
     for (size_t i = 0; i < n; i++) raw[i] = depthU16[i] == 0 ? MINF : (float)depthU16[i] / o->depthShift;
@@ -108,6 +121,8 @@ extern "C" void or_preprocess(const BFPreprocessOptions* o, const uint16_t* dept
         gauss(filtered.data(), raw.data(), o->sigmaD, o->sigmaR, (int)dw, (int)dh);
         result = filtered.data();
     }
+    if (rawOut) std::memcpy(rawOut, raw.data(), sizeof(float) * n);
+    if (filteredOut) std::memcpy(filteredOut, result, sizeof(float) * n);
     if (dw == iw && dh == ih) std::memcpy(depthOut, result, sizeof(float) * n);
     else resample(depthOut, iw, ih, result, dw, dh);
     if (rgbx && colorOut) {
@@ -265,9 +280,74 @@ extern "C" void or_corr_from_depth(const float* const* depth, const float* T, co
             all.push_back(e);
             taken++;
         }
+        if (taken < o->minPerPair) all.resize(all.size() - taken);  // s_minNumMatches: the pair is dropped
     }
     const uint32_t m = (uint32_t)std::min<size_t>(all.size(), cap);
     if (m) std::memcpy(out, all.data(), sizeof(BFEntryJ) * m);
     if (n) *n = m;
     if (total) *total = (uint32_t)all.size();
+}
+
+// The app's stand-in front end (bundlefusion_amd/csrc/frontend.h, restated): Tinc(f) = inv(T[f-1]) T[f]
+// [R(w) | t] with w, t normal (sigma driftRad, driftM) from splitmix64 + Box-Muller, in double, one final
+// rounding; identity when a pose is not finite.
+namespace {
+uint64_t or_splitmix(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+double or_fe_uniform(uint32_t seed, uint32_t frame, uint32_t k) {
+    const uint64_t key = ((uint64_t)seed << 32) ^ ((uint64_t)frame << 3) ^ (uint64_t)k;
+    return ((double)(or_splitmix(key) >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+}
+}  // namespace
+
+extern "C" void or_front_end_tinc(const float* prev, const float* cur, uint32_t frame, uint32_t seed, float driftRad,
+                                  float driftM, float* out) {
+    for (int k = 0; k < 16; k++) out[k] = (k % 5 == 0) ? 1.0f : 0.0f;
+    for (int k = 0; k < 16; k++)
+        if (!std::isfinite(prev[k]) || !std::isfinite(cur[k])) return;
+    double Pinv[16] = {0};  // [R^T | -R^T t]
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Pinv[4 * r + c] = (double)prev[4 * c + r];
+        Pinv[4 * r + 3] = -((double)prev[r] * prev[3] + (double)prev[4 + r] * prev[7] + (double)prev[8 + r] * prev[11]);
+    }
+    Pinv[15] = 1.0;
+    double rel[16];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; k++) acc += Pinv[4 * r + k] * (double)cur[4 * k + c];
+            rel[4 * r + c] = acc;
+        }
+    double g[6];
+    for (int p = 0; p < 3; p++) {
+        const double u1 = or_fe_uniform(seed, frame, 2 * p), u2 = or_fe_uniform(seed, frame, 2 * p + 1);
+        const double rad = std::sqrt(-2.0 * std::log(u1)), ang = 6.283185307179586 * u2;
+        g[2 * p] = rad * std::cos(ang);
+        g[2 * p + 1] = rad * std::sin(ang);
+    }
+    const double w0 = g[0] * driftRad, w1 = g[1] * driftRad, w2 = g[2] * driftRad;
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const double th = std::sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    if (th > 1e-12) {
+        const double a = w0 / th, b = w1 / th, c = w2 / th;
+        const double K[9] = {0, -c, b, c, 0, -a, -b, a, 0};
+        const double s = std::sin(th), v = 1.0 - std::cos(th);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                const double k2 = K[3 * i] * K[j] + K[3 * i + 1] * K[3 + j] + K[3 * i + 2] * K[6 + j];
+                R[3 * i + j] += s * K[3 * i + j] + v * k2;
+            }
+    }
+    double step[16] = {R[0], R[1], R[2], g[3] * driftM, R[3], R[4], R[5], g[4] * driftM, R[6], R[7], R[8], g[5] * driftM,
+                       0, 0, 0, 1};
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; k++) acc += rel[4 * r + k] * step[4 * k + c];
+            out[4 * r + c] = (float)acc;
+        }
 }

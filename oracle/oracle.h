@@ -36,6 +36,7 @@ uint32_t or_scene_num_occupied(const ORScene* s);
 /* full dump (debugHash): hash[E], heap[B], voxels[B*512] */
 void or_scene_export(const ORScene* s, BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter,
                      BFVoxel* voxels);
+void or_scene_import(ORScene* o, const BFHashEntry* hash, const uint32_t* heap, uint32_t heapCounter, const BFVoxel* voxels);
 /* occupied (visible) list of the last compactify: entries[numOccupied] */
 void or_scene_export_visible(const ORScene* s, BFHashEntry* out);
 void or_scene_get_stats(const ORScene* s, BFTsdfStats* out);
@@ -131,6 +132,8 @@ unsigned or_traj_next_fixes(void* h, unsigned maxFixes, int* kinds, unsigned* fr
 void or_traj_frame_info(void* h, unsigned idx, int* type, float* dist);
 
 void or_traj_integrated(void* h, unsigned idx, float* T);
+/* generateUpdateLists + getNumActiveOperations (the past-the-end exit check, DepthSensing.cpp:1116-1123) */
+unsigned or_traj_generate_and_count(void* h);
 
 /* ---- bundling side of the reconstruction loop (recon.cpp): OnlineBundler local -> global state
  * machine + TrajectoryManager, in the order of the product's synchronous mode ----------------- */
@@ -160,10 +163,13 @@ void or_recon_destroy(ORRecon* r);
 void or_recon_set_frame(ORRecon* r, uint32_t f, const float Tinc[16], const BFCachedFrame* cache);
 void or_recon_set_local_corr(ORRecon* r, uint32_t s, const BFEntryJ* corr, uint32_t n);
 void or_recon_set_global_corr(ORRecon* r, const BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes);
+void or_recon_append_global_corr(ORRecon* r, const BFEntryJ* corr, uint32_t n);
 void or_recon_process_frame(ORRecon* r, uint32_t f);
 void or_recon_finish(ORRecon* r);
 void or_recon_reintegrate(ORRecon* r);
 void or_recon_end_solve(ORRecon* r, float denseDepthWeight);
+void or_recon_end_sequence(ORRecon* r, int32_t numSolveFramesBeforeExit, int32_t disableDense, uint32_t denseFrameLimit,
+                           float denseDepthWeight, uint32_t maxPastEndFrames, uint32_t* out5);
 uint32_t or_recon_op_log(const ORRecon* r, BFFixOp* out, uint32_t cap);
 int or_recon_submap_poses(const ORRecon* r, uint32_t s, float* local, float* global, int32_t* valid, uint32_t* numLocal,
                           uint32_t* numKeyframes, int32_t* localValid);
@@ -174,6 +180,14 @@ void or_recon_stats(const ORRecon* r, ORReconStats* out);
 void or_preprocess(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh,
                    const uint8_t* rgbx, uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, float* depthOut,
                    uint8_t* colorOut);
+/* ... also returning the sensor-size raw (eroded) and filtered depth (CUDAImageManager::copyToBundling) */
+void or_preprocess2(const BFPreprocessOptions* o, const uint16_t* depthU16, uint32_t dw, uint32_t dh, const uint8_t* rgbx,
+                    uint32_t cw, uint32_t ch, uint32_t iw, uint32_t ih, float* depthOut, uint8_t* colorOut, float* rawOut,
+                    float* filteredOut);
+
+/* the app's front-end estimate (bundlefusion_amd/csrc/frontend.h), restated */
+void or_front_end_tinc(const float* prev, const float* cur, uint32_t frame, uint32_t seed, float driftRad, float driftM,
+                       float* out);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,7 @@ struct Recon {
     std::vector<m4> gMat;                        // dGlobalT_: matrices of the valid keyframes
     void* tm = nullptr;
     uint32_t numFrames = 0, lastSubmapEnqueued = 0xFFFFFFFFu;
+    uint32_t optimizedFrames = 0;  // m_totalNumOptLocalFrames (OnlineBundler.cpp:268)
     std::vector<BFFixOp> log;
     std::vector<Rec> history;
     ORReconStats st{};
@@ -239,6 +240,7 @@ struct Recon {
             }
         }
         lastSubmapEnqueued = s;
+        optimizedFrames = S * s + std::min(n, S);
         // ---- the loop picks the results up (Recon::apply) -----------------------------------------
         localTraj[s] = traj;
         localKnown[s] = 1;
@@ -367,23 +369,33 @@ void or_recon_set_global_corr(ORRecon* h, const BFEntryJ* corr, uint32_t n, cons
     r->prefix.assign(prefix, prefix + numKeyframes);
 }
 
+// the app's incremental form: keyframe k's correspondences appended (earlier entries keep the in-place
+// invalidations of the solves so far), prefix[k] = the new length
+void or_recon_append_global_corr(ORRecon* h, const BFEntryJ* corr, uint32_t n) {
+    Recon* r = reinterpret_cast<Recon*>(h);
+    r->globalCorr.insert(r->globalCorr.end(), corr, corr + n);
+    r->prefix.push_back((uint32_t)r->globalCorr.size());
+}
+
 void or_recon_process_frame(ORRecon* h, uint32_t f) { reinterpret_cast<Recon*>(h)->processFrame(f); }
 
 void or_recon_finish(ORRecon* h) {
     Recon* r = reinterpret_cast<Recon*>(h);
     if (r->numFrames == 0) return;
-    const uint32_t s = (r->numFrames - 1) / r->S;
-    if (s != r->lastSubmapEnqueued) r->endSubmap(s, r->numFrames - s * r->S);
+    const uint32_t s = (r->numFrames - 1) / r->S, n = r->numFrames - s * r->S;
+    // a one-frame last submap is the previous submap's overlap frame (isLastLocalFrame, OnlineBundler.h:42)
+    if (s != r->lastSubmapEnqueued && n >= 2) r->endSubmap(s, n);
 }
 
 void or_recon_reintegrate(ORRecon* h) { reinterpret_cast<Recon*>(h)->runReintegrate(); }
 
-void or_recon_end_solve(ORRecon* h, float denseDepthWeight) {
-    Recon* r = reinterpret_cast<Recon*>(h);
-    if (r->numFrames == 0) return;
-    const uint32_t last = (r->numFrames - 1) / r->S, nk = last + 1;
+// one past-the-end global solve over the keyframes of the solved submaps (fuseToGlobal adds one per
+// submap, OnlineBundler.cpp:298); returns 1 if it ran
+static int end_solve(Recon* r, float denseDepthWeight) {
+    if (r->numFrames == 0 || r->lastSubmapEnqueued == 0xFFFFFFFFu) return 0;
+    const uint32_t last = r->lastSubmapEnqueued, nk = last + 1;
     const uint32_t ncorr = (last < r->prefix.size()) ? r->prefix[last] : (uint32_t)r->globalCorr.size();
-    if (nk < 2 || r->globalCorr.empty() || ncorr == 0) return;
+    if (nk < 2 || r->globalCorr.empty() || ncorr == 0) return 0;
     r->globalSolve(nk, ncorr, denseDepthWeight);
     r->globalToMatrices(nk);
     for (uint32_t k = 0; k < nk; k++) {
@@ -392,8 +404,51 @@ void or_recon_end_solve(ORRecon* h, float denseDepthWeight) {
         r->kf[k] = r->globalT[k];
         r->kfSolved[k] = 1;
     }
-    r->updateTrajectory(r->numFrames);
+    r->updateTrajectory(std::min(r->optimizedFrames, r->numFrames));
     r->st.endSolves++;
+    return 1;
+}
+
+void or_recon_end_solve(ORRecon* h, float denseDepthWeight) { end_solve(reinterpret_cast<Recon*>(h), denseDepthWeight); }
+
+// The render loop past the last frame, the product's Recon::endSequence (bf_recon_end_sequence):
+// OnlineBundler::processInput's past-the-end branch (OnlineBundler.cpp:167-196), optimizeGlobal with
+// isSequenceDone (:373-408), the exit check of OnD3D11FrameRender (DepthSensing.cpp:1114-1126).
+// out[5] = {pastEndFrames, globalSolves, localSolved, denseSolve, queueDrained}.
+void or_recon_end_sequence(ORRecon* h, int32_t N, int32_t disableDense, uint32_t denseLimit, float wDense, uint32_t cap,
+                           uint32_t* out) {
+    Recon* r = reinterpret_cast<Recon*>(h);
+    for (int i = 0; i < 5; i++) out[i] = 0;
+    if (r->numFrames == 0) return;
+    const uint32_t S = r->S, last = (r->numFrames - 1) / S, n = r->numFrames - last * S;
+    if (!cap) cap = 100000u;
+    if (!denseLimit) denseLimit = 10000u;
+    if (!(wDense > 0.0f)) wDense = 15.0f;
+    for (uint32_t p = 0; p < cap; p++) {
+        out[0] = p + 1;
+        if (N < 0 || (int64_t)p <= (int64_t)N) {
+            if (p == 0 && last != r->lastSubmapEnqueued && n >= 2) {
+                const uint64_t before = r->st.globalSolves;
+                r->endSubmap(last, n);
+                out[1] += (uint32_t)(r->st.globalSolves - before);
+                out[2] = 1;
+            } else {
+                bool caches = r->lastSubmapEnqueued != 0xFFFFFFFFu;
+                for (uint32_t k = 0; caches && k <= r->lastSubmapEnqueued; k++)
+                    if (!r->cache[k * S].depth) caches = false;
+                const bool dense = N >= 0 && (int64_t)p == (int64_t)N && !disableDense && r->numFrames - 1 < denseLimit && caches;
+                out[1] += (uint32_t)end_solve(r, dense ? wDense : 0.0f);
+                if (dense) out[3] = 1;
+            }
+        }
+        r->runReintegrate();
+        if (N < 0 || (int64_t)p >= (int64_t)N) {
+            if (or_traj_generate_and_count(r->tm) == 0) {
+                out[4] = 1;
+                break;
+            }
+        }
+    }
 }
 
 uint32_t or_recon_op_log(const ORRecon* h, BFFixOp* out, uint32_t cap) {

@@ -271,6 +271,14 @@ unsigned or_traj_next_fixes(void* h, unsigned maxFixes, int* kinds, unsigned* fr
     return n;
 }
 
+// the exit check of the render loop past the end (DepthSensing.cpp:1116-1123): generateUpdateLists,
+// then getNumActiveOperations
+unsigned or_traj_generate_and_count(void* h) {
+    TM* tm = static_cast<TM*>(h);
+    generate(tm);
+    return (unsigned)(tm->deint.size() + tm->integ.size() + tm->reint.size());
+}
+
 void or_traj_integrated(void* h, unsigned idx, float* T) {
     std::memcpy(T, static_cast<TM*>(h)->frames[idx].integrated, 64);
 }

@@ -247,8 +247,10 @@ f3 depthToSkeleton(const BFDepthCameraParams& c, uint32_t ux, uint32_t uy, float
     return mk(depth * x, depth * y, depth);
 }
 
-// allocKernel, CUDASceneRepHashSDF.cu:165-251, one pixel
-void allocPixel(Scene& s, const float* depth, uint32_t x, uint32_t y, const uint32_t* bitMask, bool count) {
+// allocKernel, CUDASceneRepHashSDF.cu:165-251, one pixel: the DDA walk. The blocks it would test
+// (in the frustum, in walk order) are appended to `out`; the hash lookups and inserts happen in
+// allocPass, in pixel order, because their outcome depends on what earlier threads inserted.
+void allocPixelWalk(const Scene& s, const float* depth, uint32_t x, uint32_t y, std::vector<i3>& out) {
     const BFDepthCameraParams& c = s.cam;
     float d = depth[y * c.imageWidth + x];
     if (d == MINF || d == 0.0f) return;
@@ -275,13 +277,9 @@ void allocPixel(Scene& s, const float* depth, uint32_t x, uint32_t y, const uint
     if (boundaryPos.y - rayMin.y == 0.0f) { tMax.y = PINF; tDelta.y = PINF; }
     if (rayDir.z == 0.0f) { tMax.z = PINF; tDelta.z = PINF; }
     if (boundaryPos.z - rayMin.z == 0.0f) { tMax.z = PINF; tDelta.z = PINF; }
-    (void)bitMask;  // chunk streaming bitmask: streaming is disabled (zParametersDefault.txt:100)
+    // (the chunk-streaming bitmask test is disabled with streaming, zParametersDefault.txt:100)
     for (uint32_t iter = 0; iter < 1024; iter++) {
-        if (blockInFrustum(s, id)) {
-            // count a candidate lookup only for blocks that are absent (what the HIP alloc emits)
-            BFHashEntry e = getHashEntryForSDFBlockPos(s, id);
-            if (e.ptr == BF_FREE_ENTRY) { if (count) s.stats.candidates++; allocBlock(s, id); }
-        }
+        if (blockInFrustum(s, id)) out.push_back(id);
         if (tMax.x < tMax.y && tMax.x < tMax.z) {
             id.x = f2i((float)id.x + step.x);
             if (id.x == idBound.x) return;
@@ -298,17 +296,77 @@ void allocPixel(Scene& s, const float* depth, uint32_t x, uint32_t y, const uint
     }
 }
 
+// Open-addressing set of block coordinates seen in one alloc pass, with the outcome of their first
+// test (absent after it: 1).
+struct SeenSet {
+    std::vector<uint64_t> key;
+    std::vector<uint8_t> absent;
+    uint64_t mask = 0;
+    void reset(size_t n) {
+        size_t cap = 1024;
+        while (cap < 2 * n) cap <<= 1;
+        key.assign(cap, ~0ull);
+        absent.assign(cap, 0);
+        mask = cap - 1;
+    }
+    static uint64_t pack(i3 p) {
+        return ((uint64_t)(uint32_t)(p.x & 0x1FFFFF) << 42) | ((uint64_t)(uint32_t)(p.y & 0x1FFFFF) << 21) |
+               (uint64_t)(uint32_t)(p.z & 0x1FFFFF);
+    }
+    // returns the slot; *found = already present
+    size_t find(uint64_t k, bool* found) const {
+        size_t h = (size_t)((k * 0x9E3779B97F4A7C15ull) >> 20) & mask;
+        while (key[h] != ~0ull && key[h] != k) h = (h + 1) & mask;
+        *found = key[h] == k;
+        return h;
+    }
+};
+
+// One alloc pass over the walks' block lists in pixel order (thread order of a serial schedule). A
+// repeated block inside a pass is a no-op whatever its first test did (found: found again; inserted:
+// found; failed on a locked bucket / full list / empty heap: fails again, the locks stay set for the
+// pass), so only its first occurrence runs; the candidate count still counts every absent test.
+void allocPass(Scene& s, const std::vector<i3>& walk, SeenSet& seen, bool count) {
+    seen.reset(walk.size());
+    for (const i3& id : walk) {
+        bool found = false;
+        const size_t slot = seen.find(SeenSet::pack(id), &found);
+        if (found) {
+            if (count && seen.absent[slot]) s.stats.candidates++;
+            continue;
+        }
+        seen.key[slot] = SeenSet::pack(id);
+        BFHashEntry e = getHashEntryForSDFBlockPos(s, id);
+        if (e.ptr == BF_FREE_ENTRY) {
+            if (count) s.stats.candidates++;
+            seen.absent[slot] = allocBlock(s, id) ? 0 : 1;
+        }
+    }
+}
+
 // compactifyHashAllInOneKernel :324-366 (order: table order; the HIP build's order differs,
 // consumers are order-independent)
 uint32_t compactify(Scene& s) {
     s.numOccupied = 0;
     const uint32_t E = numEntries(s);
-    for (uint32_t i = 0; i < E; i++) {
-        const BFHashEntry& e = s.hash[i];
-        if (e.ptr != BF_FREE_ENTRY) {
-            s.stats.scanned++;
-            if (blockInFrustum(s, {e.x, e.y, e.z})) s.compact[s.numOccupied++] = e;
+    // table order, evaluated in parallel chunks and concatenated in chunk order
+    const uint32_t chunk = 1u << 16, nChunks = (E + chunk - 1) / chunk;
+    std::vector<std::vector<BFHashEntry>> part(nChunks);
+    std::vector<uint64_t> scanned(nChunks, 0);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long c = 0; c < (long)nChunks; c++) {
+        const uint32_t lo = (uint32_t)c * chunk, hi = std::min(E, lo + chunk);
+        for (uint32_t i = lo; i < hi; i++) {
+            const BFHashEntry& e = s.hash[i];
+            if (e.ptr != BF_FREE_ENTRY) {
+                scanned[c]++;
+                if (blockInFrustum(s, {e.x, e.y, e.z})) part[c].push_back(e);
+            }
         }
+    }
+    for (uint32_t c = 0; c < nChunks; c++) {
+        s.stats.scanned += scanned[c];
+        for (const BFHashEntry& e : part[c]) s.compact[s.numOccupied++] = e;
     }
     s.stats.visible += s.numOccupied;
     s.hp.numOccupiedBlocks = s.numOccupied;
@@ -430,11 +488,25 @@ void or_scene_integrate(ORScene* o, const float T[16], const float* depth, const
         // count is unchanged. Serially, a pass inserts at most one block per bucket (the
         // bucket stays locked for the rest of the pass, VoxelUtilHashSDF.h:604-611).
         s.stats.pixels += (uint64_t)cam->imageWidth * cam->imageHeight;
+        (void)bitMask;
+        // the walks depend on the pose and the depth only: computed once, in parallel by row, and
+        // concatenated in pixel order
+        const uint32_t W = cam->imageWidth, H = cam->imageHeight;
+        std::vector<std::vector<i3>> rows(H);
+#pragma omp parallel for schedule(dynamic, 4)
+        for (long y = 0; y < (long)H; y++)
+            for (uint32_t x = 0; x < W; x++) allocPixelWalk(s, depth, x, (uint32_t)y, rows[y]);
+        std::vector<i3> walk;
+        size_t total = 0;
+        for (const auto& r : rows) total += r.size();
+        walk.reserve(total);
+        for (const auto& r : rows) walk.insert(walk.end(), r.begin(), r.end());
+        rows.clear();
+        SeenSet seen;
         uint32_t prevFree = s.heapCounter + 1;
         for (int pass = 0;; pass++) {
             resetMutex(s);
-            for (uint32_t y = 0; y < cam->imageHeight; y++)
-                for (uint32_t x = 0; x < cam->imageWidth; x++) allocPixel(s, depth, x, y, bitMask, pass == 0);
+            allocPass(s, walk, seen, pass == 0);
             uint32_t currFree = s.heapCounter + 1;
             if (currFree == prevFree) break;
             prevFree = currFree;
@@ -494,6 +566,18 @@ void or_scene_export(const ORScene* o, BFHashEntry* hash, uint32_t* heap, uint32
     if (heap) std::memcpy(heap, s.heap.data(), s.heap.size() * sizeof(uint32_t));
     if (heapCounter) *heapCounter = s.heapCounter;
     if (voxels) std::memcpy(voxels, s.voxels.data(), s.voxels.size() * sizeof(BFVoxel));
+}
+
+// the inverse of or_scene_export: a scene state (e.g. a GPU dump, bf_scene_export's layout) to continue
+// from; the compacted list is empty until the next compactify
+void or_scene_import(ORScene* o, const BFHashEntry* hash, const uint32_t* heap, uint32_t heapCounter, const BFVoxel* voxels) {
+    Scene& s = o->s;
+    std::memcpy(s.hash.data(), hash, s.hash.size() * sizeof(BFHashEntry));
+    std::memcpy(s.heap.data(), heap, s.heap.size() * sizeof(uint32_t));
+    s.heapCounter = heapCounter;
+    std::memcpy(s.voxels.data(), voxels, s.voxels.size() * sizeof(BFVoxel));
+    s.numOccupied = 0;
+    resetMutex(s);
 }
 
 void or_scene_export_visible(const ORScene* o, BFHashEntry* out) {

@@ -44,6 +44,8 @@ def lib() -> C.CDLL:
         L.or_scene_export.argtypes = [C.c_void_p] * 5
         L.or_scene_export.restype = None
         L.or_scene_export_visible.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_scene_import.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+        L.or_scene_import.restype = None
         L.or_scene_export_visible.restype = None
         L.or_scene_get_stats.argtypes = [C.c_void_p, C.c_void_p]
         L.or_scene_get_stats.restype = None
@@ -175,6 +177,15 @@ class OracleScene:
         vox = np.empty(B * 512, abi.VOXEL_DTYPE)
         lib().or_scene_export(self.h, h.ctypes.data, heap.ctypes.data, C.addressof(hc), vox.ctypes.data)
         return h, heap, hc.value, vox
+
+    def import_state(self, hash_, heap, heap_counter, voxels):
+        """Continue from a dumped state (e.g. the GPU loop's, bf_recon_export); compactify before a GC."""
+        h = np.ascontiguousarray(hash_)
+        hp = np.ascontiguousarray(heap, np.uint32)
+        v = np.ascontiguousarray(voxels)
+        assert len(h) == self.params.hashNumBuckets * 4 and len(hp) == self.params.numSDFBlocks
+        assert len(v) == self.params.numSDFBlocks * 512
+        lib().or_scene_import(self.h, h.ctypes.data, hp.ctypes.data, C.c_uint32(heap_counter), v.ctypes.data)
 
     def export_visible(self) -> np.ndarray:
         n = self.numOccupied()

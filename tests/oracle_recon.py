@@ -43,11 +43,14 @@ class OracleRecon:
                 ("or_recon_set_local_corr", None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
                 ("or_recon_set_global_corr", None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
                 ("or_recon_process_frame", None, [C.c_void_p, C.c_uint32]), ("or_recon_finish", None, [C.c_void_p]),
+                ("or_recon_append_global_corr", None, [C.c_void_p, C.c_void_p, C.c_uint32]),
                 ("or_recon_reintegrate", None, [C.c_void_p]), ("or_recon_end_solve", None, [C.c_void_p, C.c_float]),
                 ("or_recon_op_log", C.c_uint32, [C.c_void_p, C.c_void_p, C.c_uint32]),
                 ("or_recon_submap_poses", C.c_int, [C.c_void_p, C.c_uint32] + [C.c_void_p] * 6),
                 ("or_recon_trajectory", None, [C.c_void_p, C.c_void_p, C.c_uint32]),
-                ("or_recon_stats", None, [C.c_void_p, C.c_void_p])):
+                ("or_recon_stats", None, [C.c_void_p, C.c_void_p]),
+                ("or_recon_end_sequence", None, [C.c_void_p, C.c_int32, C.c_int32, C.c_uint32, C.c_float, C.c_uint32,
+                                                 C.c_void_p])):
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -106,6 +109,11 @@ class OracleRecon:
         prefix = np.ascontiguousarray(prefix, np.uint32)
         self.L.or_recon_set_global_corr(self.h, corr.ctypes.data, len(corr), prefix.ctypes.data, len(prefix))
 
+    def append_global_corr(self, corr: np.ndarray):
+        """keyframe k's entries appended; prefix[k] = the new total (the app's incremental list)"""
+        corr = np.ascontiguousarray(corr)
+        self.L.or_recon_append_global_corr(self.h, corr.ctypes.data if len(corr) else None, len(corr))
+
     def process_frame(self, f):
         self.L.or_recon_process_frame(self.h, f)
 
@@ -117,6 +125,13 @@ class OracleRecon:
 
     def end_solve(self, dense_depth_weight=0.0):
         self.L.or_recon_end_solve(self.h, dense_depth_weight)
+
+    def end_sequence(self, num_solve_frames_before_exit=30, dense_at_end=True, dense_frame_limit=10000,
+                     dense_depth_weight=15.0, max_past_end_frames=0):
+        out = np.zeros(5, np.uint32)
+        self.L.or_recon_end_sequence(self.h, num_solve_frames_before_exit, 0 if dense_at_end else 1, dense_frame_limit,
+                                     dense_depth_weight, max_past_end_frames, out.ctypes.data)
+        return dict(zip(("pastEndFrames", "globalSolves", "localSolved", "denseSolve", "queueDrained"), map(int, out)))
 
     def op_log(self):
         n = self.L.or_recon_op_log(self.h, None, 0)

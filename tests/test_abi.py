@@ -38,6 +38,24 @@ def test_struct_layouts():
     assert abi.ENTRYJ_DTYPE.itemsize == 32
 
 
+def test_struct_sizes_match_the_library():
+    """Every ctypes mirror has the size the C++ compiler gives the struct (bf_abi_struct_size)."""
+    import bundlefusion_amd as bfa
+    L = bfa.lib()
+    checked = 0
+    for name in dir(abi):
+        cls = getattr(abi, name)
+        if not (name.startswith("BF") and isinstance(cls, type) and issubclass(cls, C.Structure)):
+            continue
+        n = C.c_size_t()
+        rc = L.bf_abi_struct_size(name.encode(), C.byref(n))
+        if rc != 0:
+            continue  # a Python-only helper struct
+        assert C.sizeof(cls) == n.value, (name, C.sizeof(cls), n.value)
+        checked += 1
+    assert checked >= 20
+
+
 def test_error_path_without_device():
     """A null handle returns an error status and a message instead of crashing."""
     rc = bfa.lib().bf_scene_reset(None)

@@ -31,11 +31,10 @@ def test_two_shard_loops_partition_the_unsharded_loop():
     K = st.K
     loops = []
     for (count, index), sti in zip([(1, 0), (2, 0), (2, 1)], streams):
-        # local solves without the dense term: its per-image sums use float atomics (as the reference's
-        # do), so two replicated solves may differ in the last bit; the sparse solves are bit-deterministic
+        # the default bundling config, dense local term included: every BA reduction is a fixed-order sum
+        # (no float atomics), so replicated solves on every rank are bit-identical
         opts = recon_options(F, recordOps=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=st.cache_intrinsics,
-                             maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2), maxKeyframes=K + 1, asyncBundling=0,
-                             useLocalDense=0)
+                             maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2), maxKeyframes=K + 1, asyncBundling=0)
         so = BFSceneOptions()
         so.shardCount, so.shardIndex, so.shardChunk = count, index, CHUNK
         rc = Recon(params, st.cam, opts, so)
@@ -44,10 +43,10 @@ def test_two_shard_loops_partition_the_unsharded_loop():
     for f in range(F):
         for rc in loops:
             rc.process_frame(f)
+    ends = [rc.end_sequence() for rc in loops]  # the past-the-end phase, dense solve included
+    keys = ("pastEndFrames", "globalSolves", "localSolved", "denseSolve", "queueDrained")
+    assert ends[0]["denseSolve"] == 1 and all([e[k] for k in keys] == [ends[0][k] for k in keys] for e in ends[1:])
     for rc in loops:
-        rc.finish()
-        for _ in range(10):
-            rc.reintegrate()
         rc.synchronize()
     full, s0, s1 = loops
     # identical queue op lists and trajectories on every rank

@@ -26,6 +26,8 @@ class OracleTM:
         L.or_traj_frame_info.argtypes = [C.c_void_p, C.c_uint, C.c_void_p, C.c_void_p]
         L.or_traj_destroy.argtypes = [C.c_void_p]
         L.or_pose_helper_matrix_to_pose.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_traj_generate_and_count.argtypes = [C.c_void_p]
+        L.or_traj_generate_and_count.restype = C.c_uint
         self.L = L
         self.h = L.or_traj_create(max_frames, top_n, min_dist)
 
@@ -48,6 +50,10 @@ class OracleTM:
         n = self.L.or_traj_next_fixes(self.h, max_fixes, kinds.ctypes.data, frames.ctypes.data, old.ctypes.data,
                                       new.ctypes.data)
         return [(int(kinds[i]), int(frames[i]), old[i], new[i]) for i in range(n)]
+
+    def generate_and_count(self):
+        """generateUpdateLists + getNumActiveOperations (the past-the-end exit check)"""
+        return self.L.or_traj_generate_and_count(self.h)
 
     def frame_info(self, idx):
         t = C.c_int()
@@ -148,3 +154,30 @@ def test_queue_semantics_by_hand():
     ops = tm.next_fixes(10)
     assert [(k, f) for k, f, _, _ in ops] == [(2, 4)]
     assert tm.next_fixes(10) == []
+
+
+def replay_queue_trace(trace, max_frames, max_fixes=10, top_n=30, min_dist=0.0):
+    """Drive the oracle TrajectoryManager through a loop's recorded call sequence (bf_recon_queue_trace)
+    and require every fix list and exit-check count to be identical, transforms bit for bit. Returns the
+    number of fix-loop calls checked and of ops compared."""
+    tm = OracleTM(max_frames, top_n, min_dist)
+    calls = ops = 0
+    for kind, a, payload in trace:
+        if kind == 0:
+            tm.add_frame(0, payload, a)
+        elif kind == 1:
+            tm.update_optimized(payload)
+        elif kind == 2:
+            got = tm.next_fixes(max_fixes)
+            assert len(got) == len(payload), (calls, len(got), len(payload))
+            for (k1, f1, o1, n1), (k2, f2, o2, n2) in zip(got, payload):
+                assert (k1, f1) == (k2, f2), (calls, (k1, f1), (k2, f2))
+                if k1 in (1, 3):
+                    assert o1.tobytes() == o2.tobytes(), (calls, f1, "oldT")
+                if k1 in (2, 3):
+                    assert n1.tobytes() == n2.tobytes(), (calls, f1, "newT")
+                ops += 1
+            calls += 1
+        elif kind == 3:
+            assert tm.generate_and_count() == a
+    return calls, ops
