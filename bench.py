@@ -242,6 +242,55 @@ def global_solve_timing(stream, K, reps=3):
             "gn_iters": gn_tot / reps, "pcg_iters": pcg_tot / reps, "ms_per_solve": ms_tot / reps}
 
 
+def sens_main(args):
+    """FriedLiver over a .sens (BASELINE configs 2 / 3 when copyroom.sens / apt0.sens are present): one GPU."""
+    import tempfile
+
+    import bundlefusion_amd as bfa
+    from bundlefusion_amd.app import FriedLiver
+    from bundlefusion_amd.io import SensorData
+    from bundlefusion_amd.params import NORTH_STAR_APP, write_parameter_files
+    from bundlefusion_amd.dist import env_rank
+    rank, world, local_rank = env_rank()
+    if world > 1:
+        raise SystemExit("--sens runs on one GPU (the application is single-process)")
+    bfa.check(bfa.lib().bf_set_device(0))
+    tmp = tempfile.mkdtemp(prefix="bf_sens_")
+    pa, pb = args.app_params, args.bundling_params
+    n = len(SensorData(args.sens))
+    if not (pa and pb):
+        pa, pb = write_parameter_files(tmp, NORTH_STAR_APP, {"s_maxNumImages": max(1200, n // 10 + 2)}, sens=args.sens)
+    app = FriedLiver(pa, pb, args.sens, output_dir=tmp, skip_outputs=True, enable_timing=True)
+    log(f"{args.sens}: {app.num_frames} frames")
+    t0 = time.perf_counter()
+    done, last = 0, t0
+    while app.step():
+        done += 1
+        if time.perf_counter() - last > 20.0:
+            log(f"  frame {done}")
+            last = time.perf_counter()
+    rc = app.recon
+    rc.synchronize()
+    dt = time.perf_counter() - t0
+    st = rc.stats()
+    res = app.finish()
+    out = {"metric": f"frames/s FriedLiver pipeline on {os.path.basename(args.sens)}", "value": done / dt,
+           "unit": "frames/s", "n_gpus": 1, "steps": done, "warmup": 0, "ms_per_step": dt / max(1, done) * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": f"{args.sens} (.sens input; EntryJ from the stand-in producer)",
+           "config": {"workload": f"FriedLiver over {os.path.basename(args.sens)}: {done} frames, parameters {pa}, {pb}",
+                      "note": "whole pipeline per frame: .sens decode (prefetch threads), H2D, preprocessing, cache, "
+                              "EntryJ stand-in, re-integration queue + integrate, local/global BA; not HBM-resident"},
+           "loop": {k: st[k] for k in ("frames", "integrations", "deintegrations", "localSolves", "globalSolves",
+                                       "globalGnIterations", "globalPcgIterations", "removedPairs", "invalidLocals")},
+           "end_phase": {k: res["end"][k] for k in ("pastEndFrames", "globalSolves", "localSolved", "denseSolve",
+                                                     "queueDrained", "denseSolveMs")},
+           "end_phase_s": res["endSeconds"], "heap_free": res["heapFreeCount"],
+           "valid_transforms": [res["numValidTransforms"], res["numTransforms"]], "mesh_triangles": res["meshTriangles"]}
+    print(json.dumps(out), flush=True)
+    app.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +314,13 @@ def main():
                     help="edge (m) of the TSDF ownership chunks when sharded over ranks")
     ap.add_argument("--async-bundling", type=int, default=1, choices=[1, 2],
                     help="1: solves issued from the frame loop onto their own streams; 2: from a bundling thread")
+    ap.add_argument("--sens", default=None,
+                    help="run the FriedLiver application (bf_app_*) over this .sens instead of the synthetic stream "
+                         "(copyroom / apt0: BASELINE configs 2 and 3): decode, preprocessing, cache, EntryJ stand-in, "
+                         "the loop, the end-of-sequence phase; frames/s of the whole pipeline")
+    ap.add_argument("--app-params", default=None, help="with --sens: zParametersDefault.txt-style file (default: the "
+                    "reference defaults at the north-star 640x480 / 4 mm, 2^23 buckets, 2^21 blocks)")
+    ap.add_argument("--bundling-params", default=None, help="with --sens: zParametersBundlingDefault.txt-style file")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None,
                     help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
@@ -277,6 +333,9 @@ def main():
     for k, v in preset.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
+
+    if args.sens:
+        return sens_main(args)
 
     from bundlefusion_amd.dist import HostGroup, env_rank
     rank, world, local_rank = env_rank()
@@ -299,7 +358,10 @@ def main():
     F = frames_total + 1
     fill = frames_total - S * args.steps
     t_setup = time.perf_counter()
-    stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log)
+    # the dense-term cache frames are built inside the loop as each frame is processed
+    # (Bundler::storeCachedFrame in OnlineBundler::processInput, OnlineBundler.cpp:199-204), so the
+    # timed region includes CUDACache::storeFrame
+    stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log, cache_source="loop")
     params = bfa.hash_params(voxel_size=args.voxel, num_buckets=args.buckets, num_blocks=args.blocks)
     K = stream.K
     opts = recon_options(F, enableTiming=1, asyncBundling=args.async_bundling, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
@@ -356,7 +418,14 @@ def main():
     P = args.width * args.height
     workload = (f"{frames_total}-frame {args.width}x{args.height} stream, {args.voxel * 1000:.0f} mm voxels, "
                 f"2^{args.buckets.bit_length() - 1} buckets, 2^{args.blocks.bit_length() - 1} blocks; "
-                f"local 2x100 + global 3x150 GN x PCG per submap; timed: last {args.steps} submaps")
+                f"local 2x100 + global 3x150 GN x PCG per submap; cache frames built in the loop; "
+                f"timed: last {args.steps} submaps")
+    # a profile's counters describe one scheduling: a sharded rehearsal or another bundling mode is a
+    # different workload (a rehearsal must not pick up the unsharded profile's counters)
+    if world > 1 or args.rehearse_shards > 1:
+        workload += f"; tsdf shard {so.shardIndex} of {so.shardCount} (chunk {so.shardChunk:g} m)"
+    if args.async_bundling != 1:
+        workload += f"; asyncBundling {args.async_bundling}"
     # dominant kernel: k_apply_ops, the op-batch voxel pass that applies a frame's re-integration
     # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Per launch, from the
     # device counters of the same launches:
@@ -384,7 +453,7 @@ def main():
                 break
     # counters are taken only from a profile of this same workload (tools/profile_bench.sh records
     # the workload string of the bench run it profiled and averages over its timed launches)
-    if tj.get("workload") == workload and world == 1:
+    if tj.get("workload") == workload and world == 1 and args.rehearse_shards <= 1:
         traffic = tj.get("bytes_per_launch")
         traffic_src = os.path.relpath(args.traffic, REPO)
         if "valu_insts_per_launch" in tj:  # VALU-issue bound of the same kernel (SQ_INSTS_VALU pass)
@@ -395,14 +464,23 @@ def main():
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
     solo = global_solve_timing(stream, K - 1)
-    # end of sequence (after the timed region): one global solve with the dense depth term at weight 15
-    # over every keyframe (USE_GLOBAL_DENSE_AT_END, OnlineBundler.cpp:177-189)
-    rc.finish()
-    dres, dms = rc.end_solve(15.0)
-    dense_end = {"ms": dms, "keyframes": K, "dense_pairs": dres["numDensePairs"], "gn_iters": dres["gnIterations"],
-                 "pcg_iters": dres["pcgIterations"], "ms_per_gn_iter": dms / max(1, dres["gnIterations"]),
-                 "note": "bf_recon_end_solve(15): sparse weight 1 + dense depth 15 (3 x 150 GN x PCG), every keyframe's "
-                         "80x60 cache frame; untimed, after the timed tail"}
+    # end of sequence (after the timed region): the render loop past the last frame — the last submap,
+    # s_numSolveFramesBeforeExit (30) global solves, the last with the dense depth term at weight 15
+    # (USE_GLOBAL_DENSE_AT_END, OnlineBundler.cpp:167-196), re-integration until the queue is empty
+    # (DepthSensing.cpp:1114-1126)
+    t_end = time.perf_counter()
+    end = rc.end_sequence(30)
+    t_end = time.perf_counter() - t_end
+    dres = end["last"]
+    dense_end = {"ms": end["denseSolveMs"], "keyframes": K - 1, "dense_pairs": dres["numDensePairs"],
+                 "gn_iters": dres["gnIterations"], "pcg_iters": dres["pcgIterations"],
+                 "ms_per_gn_iter": end["denseSolveMs"] / max(1, dres["gnIterations"]),
+                 "end_phase": {k: end[k] for k in ("pastEndFrames", "globalSolves", "localSolved", "denseSolve",
+                                                   "queueDrained")},
+                 "end_phase_s": t_end,
+                 "note": "bf_recon_end_sequence(30): 31 past-the-end global solves, the last with sparse weight 1 + "
+                         "dense depth 15 (3 x 150 GN x PCG) over every keyframe's 80x60 cache frame, then re-integration "
+                         "until the queue drains; untimed, after the timed tail"}
     out = {
         "metric": f"frames/s integrate+global-BA on {args.width}x{args.height} @{args.voxel * 1000:g}mm voxels",
         "value": frames / dt,

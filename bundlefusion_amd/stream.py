@@ -64,10 +64,17 @@ class SyntheticStream:
 
         # dense-term cache frames (80x60): "frames" builds them from the rendered frames with the
         # reference's pipeline (CUDACache::storeFrame, called by Bundler::storeCachedFrame per input
-        # frame); "synth" renders them analytically at 80x60 (no filtering)
+        # frame); "loop": the same, but inside the loop as each frame is processed (attach_cache);
+        # "synth" renders them analytically at 80x60 (no filtering)
         t1 = time.perf_counter()
         self.cache = []
-        if cache_source == "frames":
+        self.cache_source = cache_source
+        if cache_source == "loop":
+            from .cache import CUDACache, cache_options
+            self.cache_store = CUDACache(cache_options(width, height, f, f, self.cam.mx, self.cam.my, num_frames,
+                                                       width=cache_w, height=cache_h))
+            self.cache = [None] * num_frames
+        elif cache_source == "frames":
             from .cache import CUDACache, cache_options
             self.cache_store = CUDACache(cache_options(width, height, f, f, self.cam.mx, self.cam.my, num_frames,
                                                        width=cache_w, height=cache_h))
@@ -124,6 +131,8 @@ class SyntheticStream:
                 recon.set_local_correspondences(s, self.local_corr.ptr.value + 32 * self.local_off[s], self.local_n[s])
         recon.set_global_correspondences(self.global_corr.ptr.value, len(self.global_host), self.global_prefix)
         recon.set_initial_pose(self.gt[0])
+        if self.cache_source == "loop":  # storeFrame of every frame inside process_frame (the frame store is the source)
+            recon.attach_cache(self.cache_store)
 
 
 def write_synthetic_sens(path: str, num_frames: int, width: int = 640, height: int = 480, seed: int = 0,

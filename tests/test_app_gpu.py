@@ -32,8 +32,8 @@ from tsdf_compare import compare_states
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
-F = 165            # 16 full submaps + a 5-frame partial one
-SNAP, WINDOW = 120, 6
+F = 205            # 20 full submaps + a 5-frame partial one
+SNAP, WINDOW = 140, 30
 ROT_TOL, TRANS_TOL = 1e-3, 1e-3
 DRIFT = (float(np.deg2rad(0.05)), 0.002)
 APP = dict(NORTH_STAR_APP, s_hashNumBuckets=1 << 20, s_hashNumSDFBlocks=1 << 18)
@@ -65,6 +65,7 @@ def run(tmp_path_factory):
     assert not app.step()
     res = app.finish()
     ores = ora.finish(APP_DEFAULTS["s_numSolveFramesBeforeExit"])
+    snaps["end"] = (rc.export(), len(rc.op_log()))
     return dict(dir=d, sens=sens, app=app, rc=rc, ora=ora, res=res, ores=ores, snaps=snaps)
 
 
@@ -164,6 +165,28 @@ def test_tsdf_window_replay(run):
     blocks = compare_states(params, _Snapshot(s1), sc)
     print(f"TSDF window frames {SNAP + 1}..{SNAP + WINDOW}: {n} scene ops replayed, {blocks} blocks bit-identical")
     assert n >= 4 * WINDOW
+
+
+def test_tsdf_full_replay(run):
+    """Every scene call of the run — the frames, the re-integration queue, the end-of-sequence phase —
+    through the oracle TSDF from an empty scene: the GPU loop's final scene, bit for bit."""
+    import time
+    rc, ora = run["rc"], run["ora"]
+    final, n_ops = run["snaps"]["end"]
+    log = rc.op_log()
+    assert len(log) == n_ops
+    sc = OracleScene(rc.params)
+    t0 = time.perf_counter()
+    n = 0
+    for kind, f, oldT, newT in log:
+        if kind == 4:
+            sc.garbageCollect()
+            continue
+        d, c = ora.integration_image(f)
+        sc.integrate((oldT if kind == 1 else newT).reshape(4, 4), d, c, ora.cam, deintegrate=(kind == 1))
+        n += 1
+    blocks = compare_states(rc.params, _Snapshot(final), sc)
+    print(f"TSDF full replay: {n} scene ops in {time.perf_counter() - t0:.0f} s, {blocks} blocks bit-identical")
 
 
 def test_outputs(run):
