@@ -339,10 +339,15 @@ struct Solver {
     }
 
     // evalMinusJTFDevice (SolverBundlingEquationsLie.h:63-148) + PCGInit_Kernel1 (SolverBundling.cu:755-787)
+    // OpenMP over images / correspondences: every per-image sum keeps its serial order and every
+    // cross-image reduction is summed afterwards in image order, so the result equals the serial run's
     void init() {
         scanAlpha[0] = 0.0f;
         const uint32_t cap = P.maxCorrPerImage;
-        for (uint32_t x = 1; x < N; x++) {
+        std::vector<float> part(N, 0.0f);
+#pragma omp parallel for schedule(dynamic, 8)
+        for (long xl = 1; xl < (long)N; xl++) {
+            const uint32_t x = (uint32_t)xl;
             f3 rR{0, 0, 0}, rT{0, 0, 0}, pR{0, 0, 0}, pT{0, 0, 0};
             dRot[x] = dTrans[x] = {0, 0, 0};
             const int n = std::min(numEntries[x], (int)cap);
@@ -376,9 +381,10 @@ struct Solver {
             rTrans[x] = resT;
             pRot[x] = orc::mul(mRot[x], resR);
             pTrans[x] = orc::mul(mTrans[x], resT);
-            scanAlpha[0] += dot(resR, pRot[x]) + dot(resT, pTrans[x]);
+            part[x] = dot(resR, pRot[x]) + dot(resT, pTrans[x]);
             apRot[x] = apTrans[x] = {0, 0, 0};
         }
+        for (uint32_t x = 1; x < N; x++) scanAlpha[0] += part[x];
         for (uint32_t x = 1; x < N; x++) rDotzOld[x] = scanAlpha[0];  // PCGInit_Kernel2 (:789-794)
     }
 
@@ -405,8 +411,11 @@ struct Solver {
         const uint32_t cap = P.maxCorrPerImage;
         if (useSparse) {
             std::vector<f3> Jp(Nc);
-            for (uint32_t c = 0; c < Nc; c++) Jp[c] = applyJ(corr[c]);  // PCGStep_Kernel0
-            for (uint32_t x = 1; x < N; x++) {                          // PCGStep_Kernel1a / applyJTDevice
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < (long)Nc; c++) Jp[c] = applyJ(corr[c]);  // PCGStep_Kernel0
+#pragma omp parallel for schedule(dynamic, 8)
+            for (long xl = 1; xl < (long)N; xl++) {                      // PCGStep_Kernel1a / applyJTDevice
+                const uint32_t x = (uint32_t)xl;
                 f3 oR{0, 0, 0}, oT{0, 0, 0};
                 const int n = std::min(numEntries[x], (int)cap);
                 for (int k = 0; k < n; k++) {
@@ -428,7 +437,9 @@ struct Solver {
         }
         if (useDense) {  // PCGStep_Kernel_Dense / applyJTJDenseDevice (SolverBundlingDenseUtil.h:371-411)
             const uint32_t dim = 6 * N;
-            for (uint32_t x = 1; x < N; x++) {
+#pragma omp parallel for schedule(dynamic, 8)
+            for (long xl = 1; xl < (long)N; xl++) {
+                const uint32_t x = (uint32_t)xl;
                 f3 oR{0, 0, 0}, oT{0, 0, 0};
                 const uint32_t bv = x * 6;
                 for (uint32_t i = 1; i < N; i++) {
@@ -459,7 +470,7 @@ struct Solver {
             zRot[x] = orc::mul(mRot[x], rRot[x]);
             zTrans[x] = orc::mul(mTrans[x], rTrans[x]);
             scanAlpha[1] += dot(zRot[x], rRot[x]) + dot(zTrans[x], rTrans[x]);
-        }
+        }  // (N-long: serial)
         if (!P.disableEarlyOut && std::fabs(scanAlpha[0]) < 5e-7) last = true;  // ENABLE_EARLY_OUT (:1088-1093)
         for (uint32_t x = 1; x < N; x++) {  // Kernel3
             const float rDotzNew = scanAlpha[1];
@@ -497,28 +508,48 @@ struct Solver {
         mr = 0.0f;
         mi = 0;
         if (!(wSparse > 0.0f)) return;
-        for (uint32_t c = 0; c < Nc; c++) {
-            const BFEntryJ& e = corr[c];
-            float r = 0.0f;
-            if (corrValid(e)) {
-                const m4 TI = poseToMatrix(xRot[e.imgIdx_i], xTrans[e.imgIdx_i]);
-                const m4 TJ = poseToMatrix(xRot[e.imgIdx_j], xTrans[e.imgIdx_j]);
-                f3 d = wSparse * fabs3(xform(TI, ld3(e.pos_i)) - xform(TJ, ld3(e.pos_j)));
-                r = std::max(d.z, std::max(d.x, d.y));
+        std::vector<m4> Tm(N);
+        for (uint32_t i = 0; i < N; i++) Tm[i] = poseToMatrix(xRot[i], xTrans[i]);
+        // per chunk: the first maximum; chunks combined in order (strict >: the lowest index wins ties)
+        const uint32_t chunk = 1u << 16, nChunks = (Nc + chunk - 1) / chunk;
+        std::vector<float> cm(nChunks, 0.0f);
+        std::vector<int> ci(nChunks, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (long k = 0; k < (long)nChunks; k++) {
+            float m = 0.0f;
+            int idx = 0;
+            const uint32_t lo = (uint32_t)k * chunk, hi = std::min(Nc, lo + chunk);
+            for (uint32_t c = lo; c < hi; c++) {
+                const BFEntryJ& e = corr[c];
+                float r = 0.0f;
+                if (corrValid(e)) {
+                    f3 d = wSparse * fabs3(xform(Tm[e.imgIdx_i], ld3(e.pos_i)) - xform(Tm[e.imgIdx_j], ld3(e.pos_j)));
+                    r = std::max(d.z, std::max(d.x, d.y));
+                }
+                if (m < r) { m = r; idx = (int)c; }
             }
-            if (mr < r) { mr = r; mi = (int)c; }
+            cm[k] = m;
+            ci[k] = idx;
         }
+        for (uint32_t k = 0; k < nChunks; k++)
+            if (mr < cm[k]) { mr = cm[k]; mi = ci[k]; }
     }
 
-    float energy() const {  // EvalResidual (:570-614): sum of w * |r|^2
-        float s = 0.0f;
-        for (uint32_t c = 0; c < Nc; c++) {
+    float energy() const {  // EvalResidual (:570-614): sum of w * |r|^2 (serial float sum, as before)
+        std::vector<m4> Tm(N);
+        for (uint32_t i = 0; i < N; i++) Tm[i] = poseToMatrix(xRot[i], xTrans[i]);
+        std::vector<float> term(Nc, 0.0f);
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < (long)Nc; c++) {
             const BFEntryJ& e = corr[c];
             if (!corrValid(e)) continue;
-            const m4 TI = poseToMatrix(xRot[e.imgIdx_i], xTrans[e.imgIdx_i]);
-            const m4 TJ = poseToMatrix(xRot[e.imgIdx_j], xTrans[e.imgIdx_j]);
-            f3 r = xform(TI, ld3(e.pos_i)) - xform(TJ, ld3(e.pos_j));
-            s += wSparse * dot(r, r);
+            f3 r = xform(Tm[e.imgIdx_i], ld3(e.pos_i)) - xform(Tm[e.imgIdx_j], ld3(e.pos_j));
+            term[c] = wSparse * dot(r, r);
+        }
+        float s = 0.0f;
+        for (uint32_t c = 0; c < Nc; c++) {
+            if (!corrValid(corr[c])) continue;
+            s += term[c];
         }
         return s;
     }

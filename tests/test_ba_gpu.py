@@ -242,6 +242,31 @@ def test_fixed_schedule_chain_parity(mode, K, seed, out):
     assert_parity(g, o, energy_rtol=1e-3)
 
 
+@pytest.mark.timeout(900)
+def test_global_schedule_config4_scale():
+    """BASELINE config 4's global problem at its full size: 2 001 keyframes (a 20 010-frame stream, every
+    10th frame), <= 25 correspondences per co-visible pair with 2 % outliers: 9.2 M correspondences, the
+    reference's global schedule (3 GN x 150 PCG) with its early exits, in the assembled mode the loop uses.
+    Same bar as K = 400 (1e-3 rad / 1 mm per pose); integer outcomes exact."""
+    import time
+    t0 = time.perf_counter()
+    prob = make_problem(K=2001, stride=10, max_per_pair=25, outliers=0.02, drift=(0.05, 0.002), seed=3)
+    assert len(prob["corr"]) > 9_000_000
+    t1 = time.perf_counter()
+    g = gpu_solve(prob, 3, 150, [1, 1, 1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED, early_out=True)
+    t2 = time.perf_counter()
+    o = oracle_solve(prob, 3, 150, [1, 1, 1], early_out=True)
+    t3 = time.perf_counter()
+    print(f"K=2001, Nc={len(prob['corr'])}: problem {t1 - t0:.0f} s, GPU {t2 - t1:.1f} s (incl. transfers), "
+          f"oracle {t3 - t2:.0f} s; gn {g[3]['gnIterations']} pcg {g[3]['pcgIterations']}")
+    assert g[3]["gnIterations"] == o[3]["gnIterations"]
+    er, et = pose_diff(g[0], g[1], o[0], o[1])
+    print(f"max pose difference rot {er:.2e} trans {et:.2e}")
+    assert er <= 1e-3 and et <= 1e-3, (er, et)
+    np.testing.assert_array_equal(g[2]["i"] == INVALID, o[2]["i"] == INVALID)
+    assert g[3]["maxResidualIndex"] == o[3]["maxResidualIndex"]
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_per_image_cap_invalidation_exact(mode):
     """BuildVariablesToCorrespondencesTableDevice (SolverBundling.cu:1226-1248) with cap 1000."""
