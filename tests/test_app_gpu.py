@@ -12,8 +12,9 @@ frame by frame. Bars:
     counts, the end-of-sequence outcome: exact;
   * the re-integration queue: the loop's recorded TrajectoryManager call sequence replayed through the
     oracle TrajectoryManager gives every fix list bit for bit (queue logic separated from BA float drift);
-  * the voxels: the GPU loop's scene calls over a window of frames, replayed through the oracle TSDF from the
-    GPU's own state at the window's start, give a bit-identical scene;
+  * the voxels: the GPU loop's scene calls over three windows — frames 0..50 from an empty scene, frames
+    141..170 and the whole end-of-sequence phase from the GPU's own state at the window's start — replayed
+    through the oracle TSDF give a bit-identical scene;
   * the outputs: the trajectory .sens carries the optimized trajectory, processed.txt its verdict."""
 import os
 
@@ -28,11 +29,12 @@ from oracle_app import OracleFriedLiver
 from oracle_lib import OracleScene
 from test_recon_parity_gpu import mat_diff
 from test_traj import replay_queue_trace
-from tsdf_compare import compare_states
+from tsdf_compare import compare_states, replay_ops
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
 F = 205            # 20 full submaps + a 5-frame partial one
+START = 50         # the first window: frames 0..START from an empty scene
 SNAP, WINDOW = 140, 30
 ROT_TOL, TRANS_TOL = 1e-3, 1e-3
 DRIFT = (float(np.deg2rad(0.05)), 0.002)
@@ -60,7 +62,7 @@ def run(tmp_path_factory):
     for f in range(F):
         assert app.step()
         ora.step()
-        if f in (SNAP, SNAP + WINDOW):
+        if f in (START, SNAP, SNAP + WINDOW, F - 1):
             snaps[f] = (rc.export(), len(rc.op_log()))
     assert not app.step()
     res = app.finish()
@@ -154,39 +156,36 @@ def test_tsdf_window_replay(run):
     sc = OracleScene(params)
     sc.import_state(*s0)
     sc.compactify(newT.reshape(4, 4), ora.cam)  # the last op's frustum list (what the next GC walks)
-    n = 0
-    for kind, f, oldT, newT in log[i0:i1]:
-        if kind == 4:
-            sc.garbageCollect()
-            continue
-        d, c = ora.integration_image(f)
-        sc.integrate((oldT if kind == 1 else newT).reshape(4, 4), d, c, ora.cam, deintegrate=(kind == 1))
-        n += 1
+    n = replay_ops(sc, log[i0:i1], ora.integration_image, ora.cam, "window")
     blocks = compare_states(params, _Snapshot(s1), sc)
     print(f"TSDF window frames {SNAP + 1}..{SNAP + WINDOW}: {n} scene ops replayed, {blocks} blocks bit-identical")
     assert n >= 4 * WINDOW
 
 
-def test_tsdf_full_replay(run):
-    """Every scene call of the run — the frames, the re-integration queue, the end-of-sequence phase —
-    through the oracle TSDF from an empty scene: the GPU loop's final scene, bit for bit."""
-    import time
+def test_tsdf_first_frames_replay(run):
+    """The scene calls of frames 0..START through the oracle TSDF from an empty scene: bit for bit."""
     rc, ora = run["rc"], run["ora"]
-    final, n_ops = run["snaps"]["end"]
-    log = rc.op_log()
-    assert len(log) == n_ops
+    s1, i1 = run["snaps"][START]
     sc = OracleScene(rc.params)
-    t0 = time.perf_counter()
-    n = 0
-    for kind, f, oldT, newT in log:
-        if kind == 4:
-            sc.garbageCollect()
-            continue
-        d, c = ora.integration_image(f)
-        sc.integrate((oldT if kind == 1 else newT).reshape(4, 4), d, c, ora.cam, deintegrate=(kind == 1))
-        n += 1
-    blocks = compare_states(rc.params, _Snapshot(final), sc)
-    print(f"TSDF full replay: {n} scene ops in {time.perf_counter() - t0:.0f} s, {blocks} blocks bit-identical")
+    n = replay_ops(sc, rc.op_log()[:i1], ora.integration_image, ora.cam, "first frames")
+    blocks = compare_states(rc.params, _Snapshot(s1), sc)
+    print(f"TSDF frames 0..{START} from empty: {n} scene ops, {blocks} blocks bit-identical")
+
+
+def test_tsdf_end_phase_replay(run):
+    """The end-of-sequence phase's scene calls (the last submap's and 30 more solves' re-integrations
+    until the queue drains) from the GPU's state after the last frame: bit for bit."""
+    rc, ora = run["rc"], run["ora"]
+    (s0, i0), (s1, i1) = run["snaps"][F - 1], run["snaps"]["end"]
+    log = rc.op_log()
+    assert len(log) == i1 and log[i0 - 1][0] == 2 and log[i0 - 1][1] == F - 1
+    sc = OracleScene(rc.params)
+    sc.import_state(*s0)
+    sc.compactify(log[i0 - 1][3].reshape(4, 4), ora.cam)
+    n = replay_ops(sc, log[i0:i1], ora.integration_image, ora.cam, "end phase")
+    blocks = compare_states(rc.params, _Snapshot(s1), sc)
+    print(f"TSDF end phase: {n} scene ops, {blocks} blocks bit-identical")
+    assert n > 100
 
 
 def test_outputs(run):

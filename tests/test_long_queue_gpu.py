@@ -18,7 +18,7 @@ from bundlefusion_amd.recon import Recon, recon_options
 from bundlefusion_amd.stream import SyntheticStream
 from oracle_lib import OracleScene, check_hash_invariants
 from test_traj import replay_queue_trace
-from tsdf_compare import compare_states
+from tsdf_compare import compare_states, replay_ops
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
 
@@ -46,8 +46,11 @@ def test_long_stream_queue_heap_voxels():
     st.attach(rc)
     t1 = time.perf_counter()
     snaps = {}
+    import sys
     for f in range(F):
         rc.process_frame(f)
+        if f % 250 == 0:
+            print(f"  frame {f}", file=sys.stderr, flush=True)
         if f in (SNAP, SNAP + WINDOW):
             snaps[f] = (rc.export(), len(rc.op_log()))
     end = rc.end_sequence(30)
@@ -81,15 +84,11 @@ def test_long_stream_queue_heap_voxels():
     sc.compactify(newT.reshape(4, 4), st.cam)
     P = st.cam.imageWidth * st.cam.imageHeight
     H = st.cam.imageHeight
-    n = 0
-    for kind, f, oldT, newT in log[i0:i1]:
-        if kind == 4:
-            sc.garbageCollect()
-            continue
+    def image(f):
         d = st.depth.download_range(f * P * 4, P * 4).view(np.float32).reshape(H, -1)
-        c = st.color.download_range(f * P * 4, P * 4).reshape(H, -1, 4)
-        sc.integrate((oldT if kind == 1 else newT).reshape(4, 4), d, c, st.cam, deintegrate=(kind == 1))
-        n += 1
+        return d, st.color.download_range(f * P * 4, P * 4).reshape(H, -1, 4)
+
+    n = replay_ops(sc, log[i0:i1], image, st.cam, "window")
     blocks = compare_states(params, _Snapshot(s1), sc)
     print(f"TSDF window frames {SNAP + 1}..{SNAP + WINDOW}: {n} scene ops, {blocks} blocks bit-identical")
     assert n >= 10 * WINDOW

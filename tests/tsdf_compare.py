@@ -90,3 +90,23 @@ class Pair:
 
     def compare(self, **kw):
         return compare_states(self.params, self.gpu, self.ora, **kw)
+
+
+def replay_ops(scene, ops, image, cam, label="replay"):
+    """Apply a loop's op log (kind 1 de-integrate oldT, 2 integrate newT, 4 GC) to an oracle scene;
+    image(f) -> (depth, colour). Prints a progress line every 30 s (long replays must not look hung).
+    Returns the number of integrate / de-integrate calls."""
+    import sys
+    import time
+    n, t0, last = 0, time.perf_counter(), time.perf_counter()
+    for kind, f, oldT, newT in ops:
+        if kind == 4:
+            scene.garbageCollect()
+            continue
+        d, c = image(f)
+        scene.integrate((oldT if kind == 1 else newT).reshape(4, 4), d, c, cam, deintegrate=(kind == 1))
+        n += 1
+        if time.perf_counter() - last > 30.0:
+            last = time.perf_counter()
+            print(f"  {label}: {n} ops in {last - t0:.0f} s", file=sys.stderr, flush=True)
+    return n
