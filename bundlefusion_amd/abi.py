@@ -14,7 +14,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_HERE, "libbf_hip.so")
+# BF_HIP_LIB: an alternative build of the same library (A/B timing of kernel variants, tools/gpu_ab.sh)
+LIB_PATH = os.environ.get("BF_HIP_LIB") or os.path.join(_HERE, "libbf_hip.so")
 HEADER_PATH = os.path.join(REPO, "include", "bf", "bf.h")
 
 FREE_ENTRY = -2

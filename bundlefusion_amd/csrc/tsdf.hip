@@ -98,17 +98,48 @@ constexpr int DEPTH_TILE2 = 16;  // coarse level: 16x16 pixels
 constexpr int STAT_SLOTS = 64;
 constexpr int STAT_FIELDS = 32;  // counters per slot (BFTsdfStats uses the first sizeof/8)
 
-// Workgroup-level counter flush: wave shuffle-reduce, LDS add, then one global atomic per
-// workgroup into one of 64 slots (no single hot word; summed on the host at query time).
-// Every thread of the workgroup must call it (it contains a barrier).
+// The lane index, re-read where it is used: an asm statement the compiler cannot hoist, so a long
+// kernel does not keep lane-derived values live (or spilled) across its loops.
+__device__ __forceinline__ unsigned lane_id_here() {
+    unsigned l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+// Sum over the 64 lanes of a fully active wave through DPP row permutes (no LDS addresses to keep
+// live): pairs, quads, half rows, rows, then the four row sums read into scalars.
+__device__ __forceinline__ uint32_t dpp_row_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);  // row_mirror
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+    const uint32_t r = dpp_row_sum((uint32_t)v);
+    return (int)(__builtin_amdgcn_readlane(r, 0) + __builtin_amdgcn_readlane(r, 16) + __builtin_amdgcn_readlane(r, 32) +
+                 __builtin_amdgcn_readlane(r, 48));
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    // 16-bit limbs: every partial sum of 64 lanes stays below 2^22, so no carries are lost
+    unsigned long long s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t r = dpp_row_sum((uint32_t)(v >> (16 * k)) & 0xFFFFu);
+        s += (unsigned long long)(__builtin_amdgcn_readlane(r, 0) + __builtin_amdgcn_readlane(r, 16) +
+                                  __builtin_amdgcn_readlane(r, 32) + __builtin_amdgcn_readlane(r, 48)) << (16 * k);
+    }
+    return s;
+}
+
+// Workgroup-level counter flush: wave sum, LDS add, then one global atomic per workgroup into one
+// of 64 slots (no single hot word; summed on the host at query time). Every thread of the workgroup
+// must call it (it contains a barrier).
 __device__ void flush_stats2(unsigned long long* stats, int f0, unsigned long long v0, int f1, unsigned long long v1) {
     __shared__ unsigned long long s_st[2];
     if (threadIdx.x < 2) s_st[threadIdx.x] = 0;
     __syncthreads();
-    for (int off = 32; off > 0; off >>= 1) {
-        v0 += __shfl_xor(v0, off);
-        v1 += __shfl_xor(v1, off);
-    }
+    v0 = wave_sum_u64(v0);
+    v1 = wave_sum_u64(v1);
     if ((threadIdx.x & 63) == 0) {
         if (v0) atomicAdd(&s_st[0], v0);
         if (v1) atomicAdd(&s_st[1], v1);
@@ -930,15 +961,36 @@ __device__ __forceinline__ void voxel_integrate_f(float& s0, float& w0, uint32_t
     s0 = div_weight(sdf * 1.0f + s0 * w0, 1.0f + w0);
     w0 = fminf(weightMax, 1.0f + w0);
 }
+// De-integrate colour of one channel, u8(clamp(roundf((oc w - cu) / (w - 1)), 0, 254.5)), for an
+// integral weight w >= 2 (every weight the update produces: +-1 steps from 0, capped by the integral
+// weightMax). With d = w - 1 and delta = oc - cu the quotient is oc + delta / d, so the result is
+// oc + floor((2 delta + d) / (2 d)), clamped to [0, 254]; for d > 510 the floor is 0 (|delta| <= 255),
+// otherwise the quotient's distance to an integer is 0 or >= 1 / (2 d) >= 1 / 1020, far above the
+// rcp product's error (<= 5e-5), so floor(q + 5e-4) is exact. 9.3e9 cases (w 2..140000 with rcp +-1
+// ulp, sampled up to 1e8, every oc, cu) checked equal to the IEEE expression (tools/check_deint_color.c).
+// rc = rcp(2 d), or 0 when d > 510.
+__device__ __forceinline__ float deint_channel(float oc, float cu, float d, float rc) {
+    const float num = __builtin_fmaf(oc - cu, 2.0f, d);
+    const float k = floorf(num * rc + 5e-4f);
+    return fminf(fmaxf(oc + k, 0.0f), 254.0f);
+}
 __device__ __forceinline__ void voxel_deintegrate_f(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c) {
     const float wUpd = 1.0f;
     const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
     const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
-    const float den = w0 - wUpd, rden = __builtin_amdgcn_rcpf(den);
-    float r0 = fmaxf(0.0f, fminf(round_quot(oc0 * w0 - cu0 * wUpd, den, rden), 254.5f));
-    float r1 = fmaxf(0.0f, fminf(round_quot(oc1 * w0 - cu1 * wUpd, den, rden), 254.5f));
-    float r2 = fmaxf(0.0f, fminf(round_quot(oc2 * w0 - cu2 * wUpd, den, rden), 254.5f));
-    col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+    const float den = w0 - wUpd;
+    if (__builtin_amdgcn_ballot_w64(w0 != rintf(w0))) {
+        // a non-integral weight (only from an imported scene): the reference expression
+        asm volatile("" ::: "memory");
+        float r0 = fmaxf(0.0f, fminf(roundf((oc0 * w0 - cu0 * wUpd) / den), 254.5f));
+        float r1 = fmaxf(0.0f, fminf(roundf((oc1 * w0 - cu1 * wUpd) / den), 254.5f));
+        float r2 = fmaxf(0.0f, fminf(roundf((oc2 * w0 - cu2 * wUpd) / den), 254.5f));
+        col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+    } else {
+        const float rc = den > 510.0f ? 0.0f : __builtin_amdgcn_rcpf(2.0f * den);
+        col = (uint32_t)deint_channel(oc0, cu0, den, rc) | ((uint32_t)deint_channel(oc1, cu1, den, rc) << 8) |
+              ((uint32_t)deint_channel(oc2, cu2, den, rc) << 16) | (255u << 24);
+    }
     s0 = div_weight(s0 * w0 - sdf * wUpd, den);
     w0 = fmaxf(0.0f, w0 - wUpd);
     if (w0 <= 0.001f) { s0 = 0.0f; col = 0u; w0 = 0.0f; }
@@ -1298,10 +1350,8 @@ template <int ZR, int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint2* __restrict__ masks, uint32_t binCap) {
     static_assert(ZR * 2 == BF_SDF_BLOCK_SIZE, "one op mask per z-half of the block");
-    const uint32_t lane = lane_id();
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lx = lane & 7, ly = lane >> 3;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
     uint32_t updated = 0, rmw = 0;  // per lane and launch: < 2^32
     WorkCursor cur = work_begin(A.ctrl, ops.n);
@@ -1311,6 +1361,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int4 e = make_int4(__builtin_amdgcn_readfirstlane(ev.x), __builtin_amdgcn_readfirstlane(ev.y),
                                  __builtin_amdgcn_readfirstlane(ev.z), __builtin_amdgcn_readfirstlane(ev.w));
         const uint32_t blk = (uint32_t)e.w;
+        const uint32_t lane = lane_id_here();
+        const int lx = lane & 7, ly = lane >> 3;
         const uint2 mh = masks[b];
         const uint32_t maskH[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(mh.x), (uint32_t)__builtin_amdgcn_readfirstlane(mh.y)};
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
@@ -1384,10 +1436,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 nrmw++;
             }
         }
-        const unsigned long long anyChange = __ballot(dcount != 0);
-        if (anyChange) {
-            for (int off = 32; off > 0; off >>= 1) dcount += __shfl_xor(dcount, off);
-            if (lane == 0 && dcount != 0) atomicAdd(&A.blockCount[blk], (uint32_t)dcount);
+        if (__ballot(dcount != 0)) {
+            const int total = wave_sum(dcount);
+            if (lane_id_here() == 0 && total != 0) atomicAdd(&A.blockCount[blk], (uint32_t)total);
         }
         updated += nupd;
         rmw += nrmw;

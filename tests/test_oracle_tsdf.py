@@ -202,3 +202,40 @@ def test_integer_colour_blend_is_exact():
     ci, oi = np.arange(256)[:, None], np.arange(256)[None, :]
     alt = np.minimum(((2 * ci + 8 * oi + 5) * 6554) >> 16, 254)
     np.testing.assert_array_equal(ref, alt)
+
+
+def test_deintegrate_colour_shortcut_is_exact():
+    """csrc/tsdf.hip deint_channel: the de-integrate colour update u8(clamp(roundf((oc w - cu) / (w - 1)),
+    0, 254.5)) (float32, CUDASceneRepHashSDF.cu:420-521) equals med3(oc + floor((2 (oc - cu) + d) * rcp(2 d)
+    + 5e-4), 0, 254), d = w - 1, rcp forced to 0 for d > 510 — for every (oc, cu), every integral weight
+    2..700 with the rcp exactly rounded and 1 ulp either side (v_rcp_f32's bound), and sampled weights up to
+    the default weightMax (tools/check_deint_color.c runs the 9.3e9-case sweep)."""
+    import numpy as np
+    f32 = np.float32
+    o = np.arange(256, dtype=f32)[:, None]
+    c = np.arange(256, dtype=f32)[None, :]
+
+    def ref(w):
+        x = (o * w).astype(f32) - c
+        q = (x / (w - f32(1))).astype(f32)
+        a = np.abs(q)
+        t = np.floor(a)
+        r = np.copysign(t + ((a - t) >= f32(0.5)), q)
+        return np.maximum(f32(0), np.minimum(r, f32(254.5))).astype(np.uint8)
+
+    def fast(w, rc):
+        d = w - f32(1)
+        num = ((o - c) * f32(2)).astype(f32) + d  # exact: small integers
+        k = np.floor((num * rc).astype(f32) + f32(5e-4))
+        return np.minimum(np.maximum(o + k, f32(0)), f32(254)).astype(np.uint8)
+
+    with np.errstate(all="ignore"):
+        for wi in list(range(2, 701)) + [int(x) for x in np.geomspace(701, 99999999, 300)]:
+            w = f32(wi)
+            d = w - f32(1)
+            r0 = ref(w)
+            rcs = [f32(0)] if d > 510 else [f32(1) / (f32(2) * d)]
+            if d <= 510:
+                rcs += [np.nextafter(rcs[0], f32(np.inf)), np.nextafter(rcs[0], f32(0))]
+            for rc in rcs:
+                np.testing.assert_array_equal(fast(w, rc), r0, err_msg=f"w={wi} rc={rc!r}")
