@@ -974,26 +974,24 @@ __device__ __forceinline__ float deint_channel(float oc, float cu, float d, floa
     const float k = floorf(num * rc + 5e-4f);
     return fminf(fmaxf(oc + k, 0.0f), 254.0f);
 }
-__device__ __forceinline__ void voxel_deintegrate_f(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c) {
+// The de-integrate colour of the batch pass: deint_channel for integral weights, the reference
+// expression otherwise (only an imported scene can hold those).
+__device__ __forceinline__ void voxel_deint_color(float w0, uint32_t col, uint32_t c, uint32_t& out) {
     const float wUpd = 1.0f;
     const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
     const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
     const float den = w0 - wUpd;
     if (__builtin_amdgcn_ballot_w64(w0 != rintf(w0))) {
-        // a non-integral weight (only from an imported scene): the reference expression
         asm volatile("" ::: "memory");
         float r0 = fmaxf(0.0f, fminf(roundf((oc0 * w0 - cu0 * wUpd) / den), 254.5f));
         float r1 = fmaxf(0.0f, fminf(roundf((oc1 * w0 - cu1 * wUpd) / den), 254.5f));
         float r2 = fmaxf(0.0f, fminf(roundf((oc2 * w0 - cu2 * wUpd) / den), 254.5f));
-        col = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
+        out = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
     } else {
         const float rc = den > 510.0f ? 0.0f : __builtin_amdgcn_rcpf(2.0f * den);
-        col = (uint32_t)deint_channel(oc0, cu0, den, rc) | ((uint32_t)deint_channel(oc1, cu1, den, rc) << 8) |
+        out = (uint32_t)deint_channel(oc0, cu0, den, rc) | ((uint32_t)deint_channel(oc1, cu1, den, rc) << 8) |
               ((uint32_t)deint_channel(oc2, cu2, den, rc) << 16) | (255u << 24);
     }
-    s0 = div_weight(s0 * w0 - sdf * wUpd, den);
-    w0 = fmaxf(0.0f, w0 - wUpd);
-    if (w0 <= 0.001f) { s0 = 0.0f; col = 0u; w0 = 0.0f; }
 }
 
 // Two voxels of one lane column, (x, y, z) and (x, y, z + 1), projected together: every float
@@ -1156,20 +1154,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 }
 
 // ---- op batches (Scene::applyOps) ---------------------------------------------------------------
+// The batch pass's {depth, colour} image stores depth as bits(d) ^ 0xFF800000 for the depths
+// integrateDepthMapKernel accepts (d != MINF, d < maxIntegrationDistance, CUDASceneRepHashSDF.cu:
+// 449-452) and 0 for the rest: a decoded invalid depth, like the all-zero word a buffer load returns
+// past the image's range, is -inf, for which |d - z| < truncation + truncScale * d is false. The band
+// test is then that one comparison, and the clamp of sdf to +-truncation (:458-462) is the identity
+// inside the band.
+constexpr uint32_t DC_DEPTH_KEY = 0xFF800000u;
+// k_apply_ops's inner step and occupancy (overridable for A/B builds of kernel variants)
+#ifndef BF_APPLY_ZC
+#define BF_APPLY_ZC 4
+#endif
+#ifndef BF_APPLY_WPE
+#define BF_APPLY_WPE 8
+#endif
+__device__ __forceinline__ uint32_t dc_depth_word(float d, float maxDist) {
+    return (d != -INFINITY && d < maxDist) ? (__float_as_uint(d) ^ DC_DEPTH_KEY) : 0u;
+}
+
 // per-op interleaved {depth, colour} image: the voxel pass gathers both values of a pixel with one
 // dwordx2 load from one cache line (two dword gathers from two images before). Ops without colour
 // never gather (their pixels are off-screen to integrateDepthMapKernel, :441-448).
-__device__ __forceinline__ void pack_dc(const OpTable& ops, uint32_t k, uint32_t i0, uint32_t stride, uint32_t P) {
+__device__ __forceinline__ void pack_dc(const OpTable& ops, uint32_t k, uint32_t i0, uint32_t stride, uint32_t P, float maxDist) {
     if (ops.color[k] == nullptr) return;
     const float* __restrict__ d = ops.depth[k];
     const uint32_t* __restrict__ c = ops.color[k];
     uint2* __restrict__ o = ops.dc[k];
-    // a depth of +0.0 is stored as -0.0 (equal in every comparison and sum the voxel update makes), so
-    // the all-zero word a buffer load returns past the image's range marks "off-screen" by itself
-    for (uint32_t i = i0; i < P; i += stride) {
-        const uint32_t db = __float_as_uint(d[i]);
-        o[i] = make_uint2(db == 0u ? 0x80000000u : db, c[i]);
-    }
+    for (uint32_t i = i0; i < P; i += stride) o[i] = make_uint2(dc_depth_word(d[i], maxDist), c[i]);
 }
 // per-op 8x8-tile depth bounds and dc image (blockIdx.y = op; workgroups [0, tileBlocks) build the
 // tiles, the rest the dc image) + the per-batch counter reset (ops whose frame already has both,
@@ -1189,7 +1200,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
     if (blockIdx.y >= ops.nTile) return;  // a batch whose frames are all cached launches one workgroup
     const uint32_t k = ops.tileIdx[blockIdx.y];
     if (blockIdx.x >= tileBlocks) {
-        pack_dc(ops, k, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H);
+        pack_dc(ops, k, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H, maxDist);
         return;
     }
     depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[k], W, H, tilesW, tilesH, tiles2W, tiles2H,
@@ -1346,6 +1357,76 @@ __device__ __forceinline__ bool work_slot(const uint32_t* ctrl, WorkCursor& c, u
 // z-round-outer order re-fetched every op's footprint once per round: 888 -> 856 us per launch at the
 // bench workload); the op's pose and the (x, y) part of its projection are taken once per ZR slices.
 // ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us).
+// Voxel updates of the batch pass (integrateDepthMapKernel, :467-514, weightUpdate = 1) on register
+// copies, for in-band voxels (sdf unclamped: see above). Weights are non-negative floats here, whose
+// bit patterns order like the values: min(1 + w, weightMax) is an integer min of the bits.
+__device__ __forceinline__ void batch_integrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
+    col = blend_color(c, col, w0 == 0.0f);
+    s0 = div_weight(sdf * 1.0f + s0 * w0, 1.0f + w0);
+    w0 = __uint_as_float(min(__float_as_uint(1.0f + w0), __float_as_uint(weightMax)));
+}
+__device__ __forceinline__ void batch_deintegrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c) {
+    uint32_t ncol;
+    voxel_deint_color(w0, col, c, ncol);
+    const float den = w0 - 1.0f;
+    const float ns = div_weight(s0 * w0 - sdf * 1.0f, den);
+    // fmaxf(0, w - 1) <= 0.001 exactly when w - 1 <= 0.001: the emptied voxel is reset
+    const bool empty = den <= 0.001f;
+    s0 = empty ? 0.0f : ns;
+    col = empty ? 0u : ncol;
+    w0 = empty ? 0.0f : den;
+}
+
+// One op over the lane's ZR register voxels (see k_apply_ops); deint: the op's direction (wave-
+// uniform; a template split of the op body into two directions measured spills at 64 VGPRs).
+template <int ZR, int ZC>
+__device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Ti,
+                                                const float* bxy, __amdgpu_buffer_rsrc_t dcRsrc, uint32_t wc, float epsc,
+                                                int bzh, float* vs, float* vw, uint32_t* vc, uint32_t& touched,
+                                                uint32_t& nupd) {
+#pragma unroll
+    for (int z0 = 0; z0 < ZR; z0 += ZC) {
+        uint32_t pix[ZC], cc[ZC];
+        float pz[ZC], d[ZC];
+#pragma unroll
+        for (int zi = 0; zi < ZC; zi += 2) {
+            const f2v wz = f2v{(float)(bzh + z0 + zi), (float)(bzh + z0 + zi + 1)} * f2v{A.voxelSize, A.voxelSize};
+            f2v pz2;
+            voxel_pixel2b(cam, Ti, bxy, wz, wc, epsc, pix[zi], pix[zi + 1], pz2);
+            pz[zi] = pz2.x;
+            pz[zi + 1] = pz2.y;
+        }
+#pragma unroll
+        for (int zi = 0; zi < ZC; zi++) {
+            // off-screen lanes read past the descriptor's range: {0, 0}
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(dcRsrc, pix[zi], 0, 0);
+            d[zi] = __uint_as_float(v[0] ^ DC_DEPTH_KEY);
+            cc[zi] = v[1];
+        }
+#pragma unroll
+        for (int zi = 0; zi < ZC; zi++) {
+            const float sd = d[zi] - pz[zi];
+            const float tr = A.truncation + A.truncScale * d[zi];
+            if (!(fabsf(sd) < tr)) continue;
+            touched |= 1u << (z0 + zi);
+            nupd += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(true));  // the wave's in-band lanes (SALU)
+            if (deint) batch_deintegrate(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi]);
+            else batch_integrate(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi], A.weightMax);
+        }
+    }
+}
+
+// k_apply_ops, the batch's voxel pass: one wave per work-list block, lane = (x, y) column. The lane's
+// voxels of ZR z-slices stay in registers while the ops of the block's mask run over them in sequence
+// order (the outer loop), ZC z-slices per step (the inner one): project, gather {depth, colour}, band
+// test, then the integrate / de-integrate update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:
+// 420-521) on the register copy; each touched voxel is stored once. An op's z-slices project to nearly
+// the same pixels, so its gathers follow each other and hit the lines the previous slice fetched (the
+// z-round-outer order re-fetched every op's footprint once per round: 888 -> 856 us per launch at the
+// bench workload); the op's pose and the (x, y) part of its projection are taken once per ZR slices.
+// ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us).
+// The kernel is VALU-issue bound (~95% of the VALU issue rate at the bench workload): lane-derived
+// values are re-read per block instead of kept live (no spills), counters are scalar.
 template <int ZR, int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint2* __restrict__ masks, uint32_t binCap) {
@@ -1353,7 +1434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
-    uint32_t updated = 0, rmw = 0;  // per lane and launch: < 2^32
+    uint32_t updated = 0, rmw = 0;  // per wave and launch: < 2^32
     WorkCursor cur = work_begin(A.ctrl, ops.n);
     size_t b;
     for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
@@ -1393,36 +1474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const __amdgpu_buffer_rsrc_t dcRsrc =
                     __builtin_amdgcn_make_buffer_rsrc((void*)ops.dc[k], (short)0, (int)(cam.imageWidth * cam.imageHeight * 8u), 0x00020000);
                 const uint32_t wc = ops.color[k] != nullptr ? cam.imageWidth : 0u;
-                const bool deint = (ops.deintMask >> k) & 1u;
-#pragma unroll
-                for (int z0 = 0; z0 < ZR; z0 += ZC) {
-                    uint32_t pix[ZC], cc[ZC];
-                    float pz[ZC], d[ZC];
-#pragma unroll
-                    for (int zi = 0; zi < ZC; zi += 2) {
-                        const f2v wz = f2v{(float)(bz + h + z0 + zi), (float)(bz + h + z0 + zi + 1)} * f2v{A.voxelSize, A.voxelSize};
-                        f2v pz2;
-                        voxel_pixel2b(cam, Ti, bxy, wz, wc, epsc, pix[zi], pix[zi + 1], pz2);
-                        pz[zi] = pz2.x;
-                        pz[zi + 1] = pz2.y;
-                    }
-#pragma unroll
-                    for (int zi = 0; zi < ZC; zi++) {
-                        // off-screen lanes read past the descriptor's range: {0, 0}, depth -> -inf
-                        const auto v = __builtin_amdgcn_raw_buffer_load_b64(dcRsrc, pix[zi], 0, 0);
-                        d[zi] = v[0] != 0u ? __uint_as_float(v[0]) : -INFINITY;
-                        cc[zi] = v[1];
-                    }
-#pragma unroll
-                    for (int zi = 0; zi < ZC; zi++) {
-                        float sd;
-                        if (!voxel_in_band(A, d[zi], pz[zi], sd)) continue;
-                        touched |= 1u << (z0 + zi);
-                        nupd++;
-                        if (deint) voxel_deintegrate_f(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi]);
-                        else voxel_integrate_f(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi], A.weightMax);
-                    }
-                }
+                apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, vs, vw, vc, touched, nupd);
             }
 #pragma unroll
             for (int z = 0; z < ZR; z++) {
@@ -1443,9 +1495,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         updated += nupd;
         rmw += nrmw;
     }
-    flush_stats2(A.stats, S_VOXELS, updated, S_RMW, rmw);
+    // updated is the wave's total (scalar), rmw per lane
+    flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);
     __syncthreads();
-    flush_stats2(A.stats, S_BUPD, updated, S_BRMW, rmw);
+    flush_stats2(A.stats, S_BUPD, lane_id_here() == 0 ? updated : 0u, S_BRMW, rmw);
 }
 
 // garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
@@ -1654,7 +1707,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int occ0 = 0, occ1 = 0, occA = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, 4, 8>, 256, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, 256, 0));
     // sharded: one workgroup slot per CU stays free for the bundling streams' launches (Recon::Recon)
     applyGrid_ = (unsigned)std::max(1, occA - (cfg_.shardCount > 1 ? 1 : 0)) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
@@ -1854,7 +1907,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    hipExtLaunchKernelGGL(k_apply_ops<4, 4, 8>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
+    hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;
