@@ -77,14 +77,32 @@ def host_info() -> dict:
 
 
 SHARD_CHUNK = 0.25  # metres: edge of the ownership chunks of the multi-GPU TSDF sharding (balance: DESIGN §6)
-PREFIX_FRAMES = 40  # the loop prefix the CPU oracle runs in full (and the GPU's time for it, untimed region)
+# The CPU oracle's loop prefix (500 frames): it runs whole 10-frame steps until
+# PREFIX_FRAMES frames or the time budget, whichever comes first. At the north-star shape the oracle
+# costs ~2 s per steady-state frame on the box's 16-thread CPU share (21 TSDF ops of 640x480 per frame),
+# so 500 frames take ~15 min: the default bench caps the prefix by --cpu-prefix-budget (the bench must
+# finish within minutes); `--cpu-prefix-budget 0` runs all 500. The GPU's time for the same prefix
+# comes from synchronized checkpoints every PREFIX_STEP frames of the (untimed) fill.
+PREFIX_FRAMES = 500
+PREFIX_STEP = 10
+PREFIX_BUDGET_S = 45.0
 
 
-def cpu_loop_prefix(stream, params, n_frames=PREFIX_FRAMES):
+def oracle_threads() -> tuple[int, str]:
+    """The thread count the CPU oracle runs with, set explicitly: the CPU share the pool gives this
+    process (OMP_NUM_THREADS, which the GPU boxes export as their share), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.strip().isdigit() and int(env) > 0:
+        return int(env), "OMP_NUM_THREADS (the box's CPU share)"
+    return len(os.sched_getaffinity(0)), "sched_getaffinity"
+
+
+def cpu_loop_prefix(stream, params, n_frames=PREFIX_FRAMES, budget_s=PREFIX_BUDGET_S):
     """The CPU oracle running the reconstruction loop itself on the stream's first frames: the
     OnlineBundler state machine + TrajectoryManager restatement (oracle/recon.cpp: local solves with the
     dense term, verification, global solves, max-residual removal, queue) with every scene call it
-    issues applied to the oracle TSDF (integrate / de-integrate / GC, OpenMP), over the first n_frames."""
+    issues applied to the oracle TSDF (integrate / de-integrate / GC, OpenMP), over the first n_frames
+    or the whole PREFIX_STEP-frame steps that fit in budget_s (0: no budget)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_lib import OracleScene
     from oracle_recon import OracleRecon
@@ -111,7 +129,13 @@ def cpu_loop_prefix(stream, params, n_frames=PREFIX_FRAMES):
         ora.set_frame(f, stream.tinc[f], stream.cache_store.download(f))
     done, ops = 0, 0
     t0 = time.perf_counter()
+    last = t0
     while done < n_max:
+        if budget_s > 0 and done % PREFIX_STEP == 0 and done > 0 and time.perf_counter() - t0 > budget_s:
+            break
+        if time.perf_counter() - last > 20.0:
+            log(f"  cpu oracle loop frame {done}")
+            last = time.perf_counter()
         ora.process_frame(done)
         log_ = ora.op_log()
         for kind, f, oldT, newT in log_[ops:]:
@@ -127,10 +151,14 @@ def cpu_loop_prefix(stream, params, n_frames=PREFIX_FRAMES):
     st = ora.stats()
     n_tsdf = sum(1 for k, *_ in ora.op_log() if k in (1, 2))
     return {"frames": done, "s": t, "frames_per_s": done / t, "tsdf_ops": n_tsdf, "ops_per_frame": n_tsdf / done,
-            "local_solves": st["localSolves"], "global_solves": st["globalSolves"]}
+            "local_solves": st["localSolves"], "global_solves": st["globalSolves"], "frame_cap": n_max,
+            "budget_s": budget_s,
+            "cap_reason": None if done >= n_max else
+            f"time budget {budget_s:.0f} s (the bench must finish within minutes; 500 frames take ~15 min of "
+            f"oracle time on this CPU share; run bench.py --cpu-prefix-budget 0 for all {n_max})"}
 
 
-def cpu_baseline(stream, params, gpu, budget_s=20.0):
+def cpu_baseline(stream, params, gpu, prefix_frames=PREFIX_FRAMES, prefix_budget_s=PREFIX_BUDGET_S):
     """The CPU oracle (oracle/, C++ restatement built -O3 -fopenmp) on the box's host cores: TSDF
     integrate / de-integrate / GC on frames of the same stream, and one full global GN iteration
     (150 PCG iterations, the reference's global schedule) at the same (K, Nc) as the GPU's global
@@ -140,9 +168,18 @@ def cpu_baseline(stream, params, gpu, budget_s=20.0):
     from oracle_ba import matrix_to_pose, max_corr_per_image, solve
     from oracle_lib import OracleScene
 
+    from oracle_lib import lib as olib
+    nthr, thr_src = oracle_threads()
+    L = olib()
+    L.or_set_threads.restype = C.c_int
+    L.or_set_threads.argtypes = [C.c_int]
+    threads = L.or_set_threads(nthr)
     hi = host_info()
     t_start = time.perf_counter()
-    prefix = cpu_loop_prefix(stream, params)
+    prefix = cpu_loop_prefix(stream, params, prefix_frames, prefix_budget_s)
+    gpu_t = gpu.get("prefix_times", {}).get(prefix["frames"])
+    prefix["gpu_s"] = gpu_t
+    prefix["gpu_frames_per_s"] = prefix["frames"] / gpu_t if gpu_t else None
     P = stream.cam.imageWidth * stream.cam.imageHeight
     ora = OracleScene(params)
     n = min(6, stream.F)
@@ -178,18 +215,22 @@ def cpu_baseline(stream, params, gpu, budget_s=20.0):
     ops_per_frame = gpu["ops_per_frame"]
     frame_s = ops_per_frame * (t_int + t_deint) / 2.0 + t_gc + per_solve / stream.S
     sample = (f"the oracle loop (bundling state machine + queue + TSDF, oracle/recon.cpp + tsdf.cpp) over the "
-              f"stream's first {prefix['frames']} frames ({prefix['ops_per_frame']:.1f} TSDF ops/frame): "
-              f"{prefix['frames_per_s']:.3f} frames/s = value; steady-state estimate: oracle TSDF: {n} integrates + 2 de-integrates + 1 GC at {stream.cam.imageWidth}x"
+              f"stream's first {prefix['frames']} frames ({prefix['ops_per_frame']:.1f} TSDF ops/frame, "
+              f"{'cap: ' + prefix['cap_reason'] if prefix['cap_reason'] else 'uncapped'}): "
+              f"{prefix['frames_per_s']:.3f} frames/s = value; the GPU loop over the same prefix: "
+              f"{(prefix['gpu_frames_per_s'] or 0):.0f} frames/s; steady-state estimate: oracle TSDF: {n} integrates + 2 de-integrates + 1 GC at {stream.cam.imageWidth}x"
               f"{stream.cam.imageHeight} @ {params.virtualVoxelSize * 1000:.0f} mm ({t_int * 1e3:.0f} / "
               f"{t_deint * 1e3:.0f} / {t_gc * 1e3:.0f} ms per call); oracle global GN iteration at K={K}, "
               f"Nc={ncorr}: {t_gn * 1e3:.0f} ms for {res['pcgIterations']} PCG iterations; frames/s at the GPU "
               f"run's {ops_per_frame:.2f} ops/frame and {gpu['pcg_per_solve']:.1f} PCG iterations per global solve "
               f"(local solves not counted); {time.perf_counter() - t_start:.0f} s of CPU work")
-    return {"value": prefix["frames_per_s"], "unit": "frames/s", "cores": hi["omp_threads"], "kind": "port",
+    return {"value": prefix["frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": sample, "loop_prefix": prefix, "steady_state_frames_per_s": 1.0 / frame_s,
-            "gpu_prefix_frames_per_s": gpu.get("prefix_frames_per_s"),
-            "ms_per_gn_iter": t_gn * 1e3, "host": hi,
-            "threading": "TSDF integrate: OpenMP over visible blocks; BA: serial (1 core)"}
+            "gpu_prefix_frames_per_s": prefix["gpu_frames_per_s"],
+            "ms_per_gn_iter": t_gn * 1e3, "host": hi, "threads": threads, "threads_source": thr_src,
+            "threading": "set explicitly (or_set_threads); TSDF integrate / de-integrate / GC: OpenMP over "
+                         "blocks; BA: OpenMP over correspondences and images with order-preserving reductions "
+                         "(bit-identical to the serial oracle)"}
 
 
 def global_solve_timing(stream, K, reps=3):
@@ -322,6 +363,10 @@ def main():
                     "reference defaults at the north-star 640x480 / 4 mm, 2^23 buckets, 2^21 blocks)")
     ap.add_argument("--bundling-params", default=None, help="with --sens: zParametersBundlingDefault.txt-style file")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-prefix-frames", type=int, default=PREFIX_FRAMES,
+                    help="cpu_baseline: frames of the oracle loop prefix (SURVEY.md §8(d): 500)")
+    ap.add_argument("--cpu-prefix-budget", type=float, default=PREFIX_BUDGET_S,
+                    help="cpu_baseline: seconds after which the oracle prefix stops at a 10-frame boundary (0: none)")
     ap.add_argument("--traffic", default=None,
                     help="JSON with per-launch HBM bytes of k_apply_ops from the PMC passes of "
                          "tools/profile_bench.sh (committed under profiles/); used only when its "
@@ -388,13 +433,13 @@ def main():
     barrier()
     t_fill = time.perf_counter()
     last = t_fill
-    prefix_n = min(fill, PREFIX_FRAMES)
-    t_prefix = None
+    prefix_times = {}
     for f in range(fill):
         rc.process_frame(f)
-        if f + 1 == prefix_n:  # the same prefix the CPU loop baseline runs (untimed region)
+        if (f + 1) % PREFIX_STEP == 0 and f + 1 <= PREFIX_FRAMES:
+            # the prefixes the CPU loop baseline may run (untimed region): synchronized checkpoints
             rc.synchronize()
-            t_prefix = time.perf_counter() - t_fill
+            prefix_times[f + 1] = time.perf_counter() - t_fill
         if time.perf_counter() - last > 20.0:
             log(f"  fill frame {f}")
             last = time.perf_counter()
@@ -586,9 +631,9 @@ def main():
                "gn_per_solve": st["globalGnIterations"] / max(1, st["globalSolves"]),
                "pcg_per_solve": st["globalPcgIterations"] / max(1, st["globalSolves"]),
                "ops_per_frame": out["loop"]["ops_per_frame"],
-               "prefix_frames_per_s": prefix_n / t_prefix if t_prefix else None}
+               "prefix_times": prefix_times}
         try:
-            out["cpu_baseline"] = cpu_baseline(stream, params, gpu)
+            out["cpu_baseline"] = cpu_baseline(stream, params, gpu, args.cpu_prefix_frames, args.cpu_prefix_budget)
         except Exception as e:  # the baseline is reported, not the target: keep the GPU line
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

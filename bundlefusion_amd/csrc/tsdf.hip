@@ -966,31 +966,39 @@ __device__ __forceinline__ void voxel_integrate_f(float& s0, float& w0, uint32_t
 // weightMax). With d = w - 1 and delta = oc - cu the quotient is oc + delta / d, so the result is
 // oc + floor((2 delta + d) / (2 d)), clamped to [0, 254]; for d > 510 the floor is 0 (|delta| <= 255),
 // otherwise the quotient's distance to an integer is 0 or >= 1 / (2 d) >= 1 / 1020, far above the
-// rcp product's error (<= 5e-5), so floor(q + 5e-4) is exact. 9.3e9 cases (w 2..140000 with rcp +-1
-// ulp, sampled up to 1e8, every oc, cu) checked equal to the IEEE expression (tools/check_deint_color.c).
-// rc = rcp(2 d), or 0 when d > 510.
-__device__ __forceinline__ float deint_channel(float oc, float cu, float d, float rc) {
-    const float num = __builtin_fmaf(oc - cu, 2.0f, d);
-    const float k = floorf(num * rc + 5e-4f);
-    return fminf(fmaxf(oc + k, 0.0f), 254.0f);
+// rcp product's error (<= 5e-5), so floor(fma(2 delta + d, rcp(2 d), 5e-4)) is exact. 9.3e9 cases
+// (w 2..140000 with rcp +-1 ulp, sampled up to 1e8, every oc, cu; the fused and the unfused form)
+// checked equal to the IEEE expression (tools/check_deint_color.c). Integer bytes in and out:
+// delta and oc + k are 32-bit integer ops, floor + convert is one v_cvt_flr_i32_f32.
+// rc = rcp(2 d), or 0 when d > 510; di = (int)d.
+__device__ __forceinline__ int cvt_flr(float v) {
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));  // floor, saturate, NaN -> 0 (no UB)
+    return r;
+}
+__device__ __forceinline__ uint32_t deint_channel(int oc, int cu, int di, float rc) {
+    const int k = cvt_flr(__builtin_fmaf((float)(2 * (oc - cu) + di), rc, 5e-4f));
+    return (uint32_t)min(max(oc + k, 0), 254);
 }
 // The de-integrate colour of the batch pass: deint_channel for integral weights, the reference
 // expression otherwise (only an imported scene can hold those).
 __device__ __forceinline__ void voxel_deint_color(float w0, uint32_t col, uint32_t c, uint32_t& out) {
-    const float wUpd = 1.0f;
-    const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
-    const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
-    const float den = w0 - wUpd;
+    const float den = w0 - 1.0f;
     if (__builtin_amdgcn_ballot_w64(w0 != rintf(w0))) {
         asm volatile("" ::: "memory");
+        const float wUpd = 1.0f;
+        const float cu0 = (float)(c & 0xFF), cu1 = (float)((c >> 8) & 0xFF), cu2 = (float)((c >> 16) & 0xFF);
+        const float oc0 = (float)(col & 0xFF), oc1 = (float)((col >> 8) & 0xFF), oc2 = (float)((col >> 16) & 0xFF);
         float r0 = fmaxf(0.0f, fminf(roundf((oc0 * w0 - cu0 * wUpd) / den), 254.5f));
         float r1 = fmaxf(0.0f, fminf(roundf((oc1 * w0 - cu1 * wUpd) / den), 254.5f));
         float r2 = fmaxf(0.0f, fminf(roundf((oc2 * w0 - cu2 * wUpd) / den), 254.5f));
         out = (uint32_t)(uint8_t)r0 | ((uint32_t)(uint8_t)r1 << 8) | ((uint32_t)(uint8_t)r2 << 16) | (255u << 24);
     } else {
         const float rc = den > 510.0f ? 0.0f : __builtin_amdgcn_rcpf(2.0f * den);
-        out = (uint32_t)deint_channel(oc0, cu0, den, rc) | ((uint32_t)deint_channel(oc1, cu1, den, rc) << 8) |
-              ((uint32_t)deint_channel(oc2, cu2, den, rc) << 16) | (255u << 24);
+        const int di = cvt_flr(den);  // den is integral (w0 >= 0 here: no saturation matters)
+        out = deint_channel((int)(col & 0xFF), (int)(c & 0xFF), di, rc) |
+              (deint_channel((int)((col >> 8) & 0xFF), (int)((c >> 8) & 0xFF), di, rc) << 8) |
+              (deint_channel((int)((col >> 16) & 0xFF), (int)((c >> 16) & 0xFF), di, rc) << 16) | (255u << 24);
     }
 }
 
@@ -1377,13 +1385,19 @@ __device__ __forceinline__ void batch_deintegrate(float& s0, float& w0, uint32_t
     w0 = empty ? 0.0f : den;
 }
 
+// A voxel's register copy in the batch pass: an array of these (not three arrays of floats, which the
+// compiler promotes to vectors whose one-element updates cost whole-vector register copies)
+struct RegVox {
+    float s, w;
+    uint32_t c;
+};
 // One op over the lane's ZR register voxels (see k_apply_ops); deint: the op's direction (wave-
 // uniform; a template split of the op body into two directions measured spills at 64 VGPRs).
 template <int ZR, int ZC>
 __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Ti,
                                                 const float* bxy, __amdgpu_buffer_rsrc_t dcRsrc, uint32_t wc, float epsc,
-                                                int bzh, float* vs, float* vw, uint32_t* vc, uint32_t& touched,
-                                                uint32_t& nupd) {
+                                                int bzh, RegVox* rv, uint32_t& touched,
+                                                uint32_t& nupd, uint32_t& nwav) {
 #pragma unroll
     for (int z0 = 0; z0 < ZR; z0 += ZC) {
         uint32_t pix[ZC], cc[ZC];
@@ -1407,11 +1421,18 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
         for (int zi = 0; zi < ZC; zi++) {
             const float sd = d[zi] - pz[zi];
             const float tr = A.truncation + A.truncScale * d[zi];
-            if (!(fabsf(sd) < tr)) continue;
+            const bool in = fabsf(sd) < tr;
+            // the wave's in-band lanes, counted in uniform control flow (a scalar add inside the
+            // divergent branch below would be per lane)
+            nupd += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(in));
+#ifdef BF_APPLY_COUNT_WAVES
+            nwav += __builtin_amdgcn_ballot_w64(in) ? 64u : 0u;  // measurement build: update executions x 64 as voxels_rmw
+#endif
+            if (!in) continue;
             touched |= 1u << (z0 + zi);
-            nupd += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(true));  // the wave's in-band lanes (SALU)
-            if (deint) batch_deintegrate(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi]);
-            else batch_integrate(vs[z0 + zi], vw[z0 + zi], vc[z0 + zi], sd, cc[zi], A.weightMax);
+            RegVox& v = rv[z0 + zi];
+            if (deint) batch_deintegrate(v.s, v.w, v.c, sd, cc[zi]);
+            else batch_integrate(v.s, v.w, v.c, sd, cc[zi], A.weightMax);
         }
     }
 }
@@ -1450,18 +1471,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
         Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK) + lane;
         int dcount = 0;
-        uint32_t nupd = 0, nrmw = 0;
+        uint32_t nupd = 0, nrmw = 0, nwav = 0;
 #pragma unroll
         for (int h = 0; h < BF_SDF_BLOCK_SIZE; h += ZR) {
-            float vs[ZR], vw[ZR];
-            uint32_t vc[ZR], pos0 = 0;
+            RegVox rv[ZR];
+            uint32_t pos0 = 0;
 #pragma unroll
             for (int z = 0; z < ZR; z++) {
                 const Vox3 v = vp[(h + z) * 64];
-                vs[z] = __uint_as_float(v.a);
-                vw[z] = __uint_as_float(v.b);
-                vc[z] = v.c;
-                pos0 |= (uint32_t)(vw[z] >= 1.0f) << z;
+                rv[z] = RegVox{__uint_as_float(v.a), __uint_as_float(v.b), v.c};
+                pos0 |= (uint32_t)(rv[z].w >= 1.0f) << z;
             }
             uint32_t touched = 0;
             for (uint32_t mk = maskH[h / ZR]; mk;) {
@@ -1474,17 +1493,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const __amdgpu_buffer_rsrc_t dcRsrc =
                     __builtin_amdgcn_make_buffer_rsrc((void*)ops.dc[k], (short)0, (int)(cam.imageWidth * cam.imageHeight * 8u), 0x00020000);
                 const uint32_t wc = ops.color[k] != nullptr ? cam.imageWidth : 0u;
-                apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, vs, vw, vc, touched, nupd);
+                apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
             }
 #pragma unroll
             for (int z = 0; z < ZR; z++) {
                 if (!((touched >> z) & 1u)) continue;
                 Vox3 nv;
-                nv.a = __float_as_uint(vs[z]);
-                nv.b = __float_as_uint(vw[z]);
-                nv.c = vc[z];
+                nv.a = __float_as_uint(rv[z].s);
+                nv.b = __float_as_uint(rv[z].w);
+                nv.c = rv[z].c;
                 vp[(h + z) * 64] = nv;
-                dcount += (int)(vw[z] >= 1.0f) - (int)((pos0 >> z) & 1u);
+                dcount += (int)(rv[z].w >= 1.0f) - (int)((pos0 >> z) & 1u);
                 nrmw++;
             }
         }
@@ -1493,7 +1512,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (lane_id_here() == 0 && total != 0) atomicAdd(&A.blockCount[blk], (uint32_t)total);
         }
         updated += nupd;
+#ifdef BF_APPLY_COUNT_WAVES
+        rmw += lane_id_here() == 0 ? nwav : 0u;
+#else
         rmw += nrmw;
+#endif
     }
     // updated is the wave's total (scalar), rmw per lane
     flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);

@@ -68,3 +68,10 @@ extern "C" double or_host_membw(size_t bytes, int reps, int* threadsOut) {
     delete[] b;
     return best;
 }
+
+// The oracle's OpenMP thread count, set explicitly by bench.py's cpu_baseline (returns the count in
+// effect afterwards).
+extern "C" int or_set_threads(int n) {
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+}
