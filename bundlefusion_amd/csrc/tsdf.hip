@@ -1397,7 +1397,11 @@ template <int ZR, int ZC>
 __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Ti,
                                                 const float* bxy, __amdgpu_buffer_rsrc_t dcRsrc, uint32_t wc, float epsc,
                                                 int bzh, RegVox* rv, uint32_t& touched,
-                                                uint32_t& nupd, uint32_t& nwav) {
+                                                uint32_t& nupd, uint32_t& nwav
+#ifdef BF_APPLY_DIAG
+                                                , uint32_t* diag
+#endif
+                                                ) {
 #pragma unroll
     for (int z0 = 0; z0 < ZR; z0 += ZC) {
         uint32_t pix[ZC], cc[ZC];
@@ -1422,6 +1426,15 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
             const float sd = d[zi] - pz[zi];
             const float tr = A.truncation + A.truncScale * d[zi];
             const bool in = fabsf(sd) < tr;
+#ifdef BF_APPLY_DIAG
+            {  // measurement build: where the evaluations go (per lane)
+                const bool off = pix[zi] == 0xFFFFFFFFu, inval = !off && d[zi] == -INFINITY;
+                diag[0] += off;
+                diag[1] += inval;
+                diag[2] += !off && !inval && sd >= tr;
+                diag[3] += !off && !inval && sd <= -tr;
+            }
+#endif
             // the wave's in-band lanes, counted in uniform control flow (a scalar add inside the
             // divergent branch below would be per lane)
             nupd += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(in));
@@ -1456,6 +1469,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
     uint32_t updated = 0, rmw = 0;  // per wave and launch: < 2^32
+#ifdef BF_APPLY_DIAG
+    uint32_t diag[4] = {0, 0, 0, 0}, diagPairs = 0, diagEmpty = 0;
+#endif
     WorkCursor cur = work_begin(A.ctrl, ops.n);
     size_t b;
     for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
@@ -1493,7 +1509,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const __amdgpu_buffer_rsrc_t dcRsrc =
                     __builtin_amdgcn_make_buffer_rsrc((void*)ops.dc[k], (short)0, (int)(cam.imageWidth * cam.imageHeight * 8u), 0x00020000);
                 const uint32_t wc = ops.color[k] != nullptr ? cam.imageWidth : 0u;
+#ifdef BF_APPLY_DIAG
+                const uint32_t before = nupd;
+                apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav, diag);
+                diagPairs++;
+                diagEmpty += nupd == before;
+#else
                 apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
+#endif
             }
 #pragma unroll
             for (int z = 0; z < ZR; z++) {
@@ -1522,6 +1545,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);
     __syncthreads();
     flush_stats2(A.stats, S_BUPD, lane_id_here() == 0 ? updated : 0u, S_BRMW, rmw);
+#ifdef BF_APPLY_DIAG
+    __syncthreads();
+    flush_stats2(A.stats, 20, diag[0], 21, diag[1]);
+    __syncthreads();
+    flush_stats2(A.stats, 22, diag[2], 23, diag[3]);
+    __syncthreads();
+    flush_stats2(A.stats, 24, lane_id_here() == 0 ? diagPairs : 0u, 25, lane_id_here() == 0 ? diagEmpty : 0u);
+#endif
 }
 
 // garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
@@ -1986,6 +2017,11 @@ BFTsdfStats Scene::stats() {
     static_assert(sizeof(BFTsdfStats) == 17 * 8 && sizeof(BFTsdfStats) <= STAT_FIELDS * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
     s.pixels += hostPixels_;
+#ifdef BF_APPLY_DIAG
+    fprintf(stderr, "apply diag: offscreen %llu invalid %llu front %llu behind %llu (half,op) pairs %llu empty %llu\n",
+            (unsigned long long)sum[20], (unsigned long long)sum[21], (unsigned long long)sum[22], (unsigned long long)sum[23],
+            (unsigned long long)sum[24], (unsigned long long)sum[25]);
+#endif
     return s;
 }
 
