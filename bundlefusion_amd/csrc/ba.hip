@@ -949,6 +949,12 @@ __device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
     }
 }
 
+#ifdef BF_PCG_TIMING
+// measurement build: per PCG launch (iteration index mod 1024) the earliest workgroup start, the
+// latest phase-A end, the finisher's start and end (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_pcgT[1024][4];
+__device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+#endif
 // PCG finisher (one workgroup): Kernel1b, Kernel2, the host early-out test, Kernel3
 template <int RB = 2>
 __device__ void pcg_finisher(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, float& rDotzNew,
@@ -1104,6 +1110,9 @@ template <int RB>
 __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter, int nLin) {
     __shared__ float sh[WG];
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+#ifdef BF_PCG_TIMING
+    const unsigned long long tStart = rtc();
+#endif
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t v = 1 + wave; v < a.N; v += nw) {
@@ -1137,11 +1146,24 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
     }
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     if (useDense) pcg_dense_offdiag(a, wave, nw);
+#ifdef BF_PCG_TIMING
+    if (threadIdx.x == 0) {
+        atomicMin(&g_pcgT[iter & 1023][0], tStart);
+        atomicMax(&g_pcgT[iter & 1023][1], rtc());
+    }
+#endif
     if (!last_block_sharded(a.sync, 1u)) return;
+#ifdef BF_PCG_TIMING
+    if (threadIdx.x == 0) g_pcgT[iter & 1023][2] = rtc();
+#endif
     if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
     float rDotzNew;
     bool last;
     pcg_finisher<RB>(a, sh, 0u, useDense, iter, nLin, rDotzNew, last);
+#ifdef BF_PCG_TIMING
+    __syncthreads();
+    if (threadIdx.x == 0) g_pcgT[iter & 1023][3] = rtc();
+#endif
     if (threadIdx.x == 0) {
         a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
         a.ctrl[K_PCG_ITERS]++;
@@ -2116,7 +2138,31 @@ void Solver::solve(const SolveArgs& s) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
                 if (s.numImages <= 2u * WG + 1u) {
+#ifdef BF_PCG_TIMING
+                    {
+                        std::vector<unsigned long long> init(1024 * 4);
+                        for (int q = 0; q < 1024; q++) { init[q * 4] = ~0ull; init[q * 4 + 1] = 0; init[q * 4 + 2] = 0; init[q * 4 + 3] = 0; }
+                        BF_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_pcgT), init.data(), init.size() * 8, 0, hipMemcpyHostToDevice, stream_));
+                    }
+#endif
                     for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<2><<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
+#ifdef BF_PCG_TIMING
+                    {
+                        std::vector<unsigned long long> t(1024 * 4);
+                        BF_HIP(hipMemcpyFromSymbolAsync(t.data(), HIP_SYMBOL(g_pcgT), t.size() * 8, 0, hipMemcpyDeviceToHost, stream_));
+                        BF_HIP(hipStreamSynchronize(stream_));
+                        double sA = 0, sW = 0, sF = 0, sAll = 0; int n = 0;
+                        for (uint32_t q = 1; q + 1 < s.nLin && q < 1024; q++) {
+                            const unsigned long long* r = &t[q * 4];
+                            const unsigned long long* nx = &t[(q + 1) * 4];
+                            if (!r[3] || !nx[3] || r[0] == ~0ull) continue;
+                            sA += (double)(r[1] - r[0]); sW += (double)(r[2] - r[1]); sF += (double)(r[3] - r[2]);
+                            sAll += (double)(nx[0] - r[0]); n++;
+                        }
+                        if (n) fprintf(stderr, "pcg timing (us, mean over %d launches): phase A %.2f  arrival %.2f  finisher %.2f  start-to-next-start %.2f\n",
+                                       n, sA / n / 100.0, sW / n / 100.0, sF / n / 100.0, sAll / n / 100.0);
+                    }
+#endif
                 } else {
                     for (uint32_t li = 0; li < s.nLin; li++) k_pcg_pairs<8><<<pairRowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
                 }

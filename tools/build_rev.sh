@@ -9,6 +9,6 @@ SRC=bundlefusion_amd/csrc/tsdf_rev_$NAME.hip
 git show $REV:bundlefusion_amd/csrc/tsdf.hip > $SRC
 trap 'rm -f $SRC' EXIT
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -munsafe-fp-atomics -x hip -c $SRC -o build/hip/tsdf_rev_$NAME.o
-OBJS=$(ls build/hip/*.o | grep -v '/tsdf')
+OBJS=$(ls build/hip/*.o | grep -v "/tsdf[._]" | grep -v "_var_\|_rev_")
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -Wl,-rpath,/opt/rocm/lib -lz -o bundlefusion_amd/libbf_hip_$NAME.so $OBJS build/hip/tsdf_rev_$NAME.o -L/opt/rocm/lib -lrccl
 echo bundlefusion_amd/libbf_hip_$NAME.so
