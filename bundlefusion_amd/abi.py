@@ -155,7 +155,8 @@ class BFSolverOptions(C.Structure):
     _fields_ = [("denseDistThresh", C.c_float), ("denseNormalThresh", C.c_float), ("denseColorThresh", C.c_float),
                 ("denseColorGradientMin", C.c_float), ("denseDepthMin", C.c_float), ("denseDepthMax", C.c_float),
                 ("denseOverlapSubsample", C.c_uint32), ("verifyOptDistThresh", C.c_float),
-                ("normalEquations", C.c_int32), ("disableEarlyOut", C.c_int32)]
+                ("normalEquations", C.c_int32), ("disableEarlyOut", C.c_int32),
+                ("pcgLaunch", C.c_int32)]
 
 NORMAL_EQ_AUTO, NORMAL_EQ_MATRIX_FREE, NORMAL_EQ_ASSEMBLED = 0, 1, 2
 PAIR_STATS = 28  # doubles per image pair of the assembled normal equations (bf_solver_export_pairs)

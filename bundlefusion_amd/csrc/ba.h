@@ -41,6 +41,7 @@ struct SolverConfig {
     float verifyOptDistThresh;    // 0.02 (CUDASolverBundling.cpp:34)
     int normalEquations;          // 0 auto (assembled for sparse-only solves), 1 matrix-free, 2 assembled
     bool earlyOut = true;         // the reference's ENABLE_EARLY_OUT build (SolverBundling.cu:7)
+    int pcgLaunch = 0;            // 0 auto (persistent PCG launch when it fits), 1 one launch per iteration
 };
 
 struct SolveArgs {
@@ -138,6 +139,7 @@ private:
     uint32_t maxCorrPerImage_;
     uint32_t maxPairs_;
     int numCUs_;
+    unsigned persistCapacity_ = 0;  // co-resident workgroups of k_pcg_persist (occupancy query x CUs)
     uint32_t maxTiles_;
     size_t maxChunks_;
     DevBuf<int> rowCount_, rowStart_, rowLen_;
@@ -174,6 +176,8 @@ private:
     DevBuf<int2> pairCorr_, rowPair_;
     DevBuf<double> pstat_, dstat_;
     DevBuf<float> apPair_, rzPart_;
+    DevBuf<uint2> aGran_;           // k_pcg_persist: Ap rows as {value, tag} granules
+    uint32_t pcgEpoch_ = 0;          // tag base of the next persistent launch
 };
 
 SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSolverOptions* opts);

@@ -86,6 +86,7 @@ struct BA {
     int2 *pairCorr, *rowPair;
     double *pstat, *dstat;
     float *apPair, *rzPart;
+    uint2* aGran;  // [2][maxN][6] {value bits, tag}: k_pcg_persist's Ap hand-off
     uint32_t pairMode, shardCount, shardIndex, pairBound;
     uint32_t earlyOut;  // ENABLE_EARLY_OUT (SolverBundling.cu:7): PCG |p.Ap| < 5e-7 and GN max|delta| < 0.005 exits
 };
@@ -103,9 +104,29 @@ __device__ __forceinline__ void vstore(const BA& a, int field, uint32_t v, f3 r,
     p[0] = make_float4(r.x, r.y, r.z, 0.0f);
     p[1] = make_float4(t.x, t.y, t.z, 0.0f);
 }
+// Fixed-order wave sums (all 64 lanes active): adjacent lanes, quads, half rows and rows through DPP
+// (after each step every lane of the group holds the same value, so the mirrors pair groups exactly as
+// an xor butterfly would), then the four row sums as (r0 + r1) + (r2 + r3), read into scalars. Every
+// lane returns the same value; no LDS round trips.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true)); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
 __device__ __forceinline__ float wave_sum(float v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
+    v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);  // row_half_mirror
+    v += dpp_f<0x140>(v);  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 __device__ __forceinline__ float ctrlf(const uint32_t* c, int k) { return __uint_as_float(c[k]); }
 __device__ __forceinline__ m4 loadm4(const float* p) {
@@ -414,9 +435,18 @@ constexpr uint32_t SORT_MAX = 4096;  // >= maxCorrPerImage (4000)
 constexpr uint32_t ROW_POS_BITS = 12;
 constexpr uint32_t PAIR_A_FLAG = 0x80000000u;
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {  // wave_sum's order in fp64
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
 // per row v: the row's entries ordered by (other image, position) — position order is ascending
@@ -922,38 +952,91 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
 // (v = the pair's j) or B^T p_j (v = its i), [trans | rot] rows. Lanes form 10 groups of 6 (one lane
 // per output row); group g takes the list entries g, g + 10, ...; the groups' partial sums are then
 // added in group order, so the sum is the same on every run. Stored write-through for the finisher.
-__device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
+__device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+constexpr unsigned long long PP_SPIN_TICKS = 200000000ull;  // 2 s at 100 MHz
+__device__ __forceinline__ bool pp_timed_out(unsigned long long t0) { return rtc() - t0 > PP_SPIN_TICKS; }
+// Data-tagged granules for k_pcg_persist's Ap hand-off (MI355X_MICROARCH.md's handoff-1to1 row): one
+// 8-B {value, tag} per float, written by ONE 8-B agent-scope atomic store and read by 8-B agent-scope
+// atomic loads, so a granule is never torn and its tag says which iteration wrote it; the consumer
+// polls the granules themselves (no drain, no arrival counter). Tags are epoch * 256 + iteration + 1:
+// the epoch counts persistent launches on this solver, so no granule of an earlier launch matches.
+// (Moving p to the workers the same way — 500 waves polling their partners' granules — ran 2x
+// slower than the polled flag: the polls' load traffic swamps the hand-off.)
+__device__ __forceinline__ void gran_store(uint2* g, float v, uint32_t tag) {
+    __hip_atomic_store((gu64*)g, ((uint64_t)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t gran_load(const uint2* g) {
+    return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Waits until the granules g[i][0..5] (i < n, null rows skipped) all carry `tag`; every load of every
+// row is in flight at once, stale ones are reloaded after a short sleep. Returns 1, or -1 on timeout.
+template <int NR>
+__device__ __forceinline__ int gran_rows(const uint2* const* g, uint32_t tag, float out[][6], unsigned long long t0) {
+    uint64_t x[NR][6];
+#pragma unroll
+    for (int r = 0; r < NR; r++)
+#pragma unroll
+        for (int q = 0; q < 6; q++) x[r][q] = g[r] ? gran_load(g[r] + q) : ((uint64_t)tag << 32);
+    for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+#pragma unroll
+            for (int q = 0; q < 6; q++) all = all && (uint32_t)(x[r][q] >> 32) == tag;
+        if (all) break;
+        if (pp_timed_out(t0)) return -1;
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+#pragma unroll
+            for (int q = 0; q < 6; q++)
+                if ((uint32_t)(x[r][q] >> 32) != tag) x[r][q] = gran_load(g[r] + q);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; r++)
+#pragma unroll
+        for (int q = 0; q < 6; q++) out[r][q] = __uint_as_float((uint32_t)x[r][q]);
+    return 1;
+}
+
+// granTag != 0 (k_pcg_persist): the products go out as Ap granules of that tag
+template <bool WT>
+__device__ void pcg_dense_offdiag_row(const BA& a, uint32_t v, uint32_t granTag = 0) {
     const uint32_t lane = lane_id();
     const uint32_t grp = lane / 6, row = lane % 6;
-    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
-        const uint32_t* L = a.imgPairs + (size_t)v * a.maxN;
-        const uint32_t nL = a.imgPairN[v];
-        float o = 0.0f;
-        if (grp < 10) {
-            for (uint32_t q = grp; q < nL; q += 10) {
-                const uint32_t e = L[q], k = e >> 1;
-                const uint2 pr = a.pairs[k];
-                const float* Bk = a.pairBlk + (size_t)k * 36;  // rows: image pr.y, columns: image pr.x
-                f3 r, t;
-                vload(a, V_P, (e & 1u) ? pr.x : pr.y, r, t);
-                const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
-                float s = 0.0f;
-                if (e & 1u) { for (int c = 0; c < 6; c++) s += Bk[row * 6 + c] * pv[c]; }
-                else { for (int rr = 0; rr < 6; rr++) s += Bk[rr * 6 + row] * pv[rr]; }
-                if ((e & 1u) ? pr.x > 0 : pr.y > 0) o += s;  // p_0 = 0 (image 0 fixed)
-            }
+    const uint32_t* L = a.imgPairs + (size_t)v * a.maxN;
+    const uint32_t nL = a.imgPairN[v];
+    float o = 0.0f;
+    if (grp < 10) {
+        for (uint32_t q = grp; q < nL; q += 10) {
+            const uint32_t e = L[q], k = e >> 1;
+            const uint2 pr = a.pairs[k];
+            const float* Bk = a.pairBlk + (size_t)k * 36;  // rows: image pr.y, columns: image pr.x
+            f3 r, t;
+            vload_t<WT>(a, V_P, (e & 1u) ? pr.x : pr.y, r, t);
+            const float pv[6] = {t.x, t.y, t.z, r.x, r.y, r.z};
+            float s = 0.0f;
+            if (e & 1u) { for (int c = 0; c < 6; c++) s += Bk[row * 6 + c] * pv[c]; }
+            else { for (int rr = 0; rr < 6; rr++) s += Bk[rr * 6 + row] * pv[rr]; }
+            if ((e & 1u) ? pr.x > 0 : pr.y > 0) o += s;  // p_0 = 0 (image 0 fixed)
         }
-        float tot = 0.0f;
-        for (uint32_t g = 0; g < 10; g++) tot += __shfl(o, (int)(g * 6 + row));
-        if (lane < 6) st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)v * 8 + lane, __float_as_uint(tot));
     }
+    float tot = 0.0f;
+    for (uint32_t g = 0; g < 10; g++) tot += __shfl(o, (int)(g * 6 + row));
+    if (lane < 6) {
+        if (granTag) gran_store(a.aGran + ((size_t)a.maxN + v) * 6 + lane, tot, granTag);  // k_pcg_persist
+        else st_wt(reinterpret_cast<uint32_t*>(a.pairProd) + (size_t)v * 8 + lane, __float_as_uint(tot));
+    }
+}
+__device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) pcg_dense_offdiag_row<false>(a, v);
 }
 
 #ifdef BF_PCG_TIMING
 // measurement build: per PCG launch (iteration index mod 1024) the earliest workgroup start, the
 // latest phase-A end, the finisher's start and end (s_memrealtime, 100 MHz)
 __device__ unsigned long long g_pcgT[1024][4];
-__device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ unsigned long long g_pcgS[1024][6];  // the last-arriving workgroup's stage stamps (wave 0)
 #endif
 // PCG finisher (one workgroup): Kernel1b, Kernel2, the host early-out test, Kernel3
 template <int RB = 2>
@@ -1112,32 +1195,68 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
 #ifdef BF_PCG_TIMING
     const unsigned long long tStart = rtc();
+    unsigned long long stg[3] = {0, 0, 0};
 #endif
     const uint32_t lane = lane_id();
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t v = 1 + wave; v < a.N; v += nw) {
         const int e0 = a.rowPairStart[v], e1 = a.rowPairStart[v + 1];
-        double o[6] = {0, 0, 0, 0, 0, 0};
-        for (int k = e0 + (int)lane; k < e1; k += 64) {
-            const int2 rp = a.rowPair[k];
-            const uint32_t u = (uint32_t)rp.y & ~PAIR_A_FLAG;
-            if (u == 0) continue;  // p_0 = 0 (image 0 fixed)
-            f3 pr, pt;
-            vload(a, V_P, u, pr, pt);
-            const double w[3] = {pr.x, pr.y, pr.z}, t[3] = {pt.x, pt.y, pt.z};
-            double b[6];
-            pair_block_apply(a.pstat + (size_t)rp.x * PSTAT, ((uint32_t)rp.y & PAIR_A_FLAG) != 0, w, t, b);
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); stg[0] = rtc() + (unsigned long long)(e0 & 0); }
+#endif
+        // the row's own p and image statistics, loaded beside the pair loop (lane 0 uses them)
+        f3 pvR, pvT;
+        vload(a, V_P, v, pvR, pvT);
+        double dst[DSTAT];
 #pragma unroll
-            for (int q = 0; q < 6; q++) o[q] += b[q];
+        for (int q = 0; q < DSTAT; q++) dst[q] = a.dstat[(size_t)v * DSTAT + q];
+        double o[6] = {0, 0, 0, 0, 0, 0};
+        // two entries per lane per round (k and k + 64), every load of both issued before either is
+        // used: one round of dependent loads (entry, then partner p + pair statistics) per 128 entries;
+        // each lane still adds its entries in ascending k, so the sums equal the one-entry loop's
+        for (int kb = e0; kb < e1; kb += 128) {
+            const int k0 = kb + (int)lane, k1 = k0 + 64;
+            const int2 rp0 = a.rowPair[min(k0, e1 - 1)], rp1 = a.rowPair[min(k1, e1 - 1)];
+            const uint32_t u0 = (uint32_t)rp0.y & ~PAIR_A_FLAG, u1 = (uint32_t)rp1.y & ~PAIR_A_FLAG;
+            f3 pr0, pt0, pr1, pt1;
+            vload(a, V_P, u0, pr0, pt0);
+            vload(a, V_P, u1, pr1, pt1);
+            double st0[16], st1[16];
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                const double2 x0 = *reinterpret_cast<const double2*>(a.pstat + (size_t)rp0.x * PSTAT + q);
+                const double2 x1 = *reinterpret_cast<const double2*>(a.pstat + (size_t)rp1.x * PSTAT + q);
+                st0[q] = x0.x; st0[q + 1] = x0.y;
+                st1[q] = x1.x; st1[q + 1] = x1.y;
+            }
+            if (k0 < e1 && u0 != 0) {  // p_0 = 0 (image 0 fixed)
+                const double w[3] = {pr0.x, pr0.y, pr0.z}, t[3] = {pt0.x, pt0.y, pt0.z};
+                double b[6];
+                pair_block_apply(st0, ((uint32_t)rp0.y & PAIR_A_FLAG) != 0, w, t, b);
+#pragma unroll
+                for (int q = 0; q < 6; q++) o[q] += b[q];
+            }
+            if (k1 < e1 && u1 != 0) {
+                const double w[3] = {pr1.x, pr1.y, pr1.z}, t[3] = {pt1.x, pt1.y, pt1.z};
+                double b[6];
+                pair_block_apply(st1, ((uint32_t)rp1.y & PAIR_A_FLAG) != 0, w, t, b);
+#pragma unroll
+                for (int q = 0; q < 6; q++) o[q] += b[q];
+            }
         }
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) stg[1] = rtc() + (unsigned long long)(o[0] != o[0]);
+#endif
 #pragma unroll
         for (int q = 0; q < 6; q++) o[q] = wave_sum_d(o[q]);
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) stg[2] = rtc() + (unsigned long long)(o[5] != o[5]);
+#endif
         if (lane == 0) {
-            f3 pr, pt;
-            vload(a, V_P, v, pr, pt);
+            const f3 pr = pvR, pt = pvT;
             const double w[3] = {pr.x, pr.y, pr.z}, t[3] = {pt.x, pt.y, pt.z};
             double dp[6];
-            diag_apply(a.dstat + (size_t)v * DSTAT, w, t, dp);
+            diag_apply(dst, w, t, dp);
             const double ws = wSparse;
             float4* q = reinterpret_cast<float4*>(a.apPair + (size_t)v * 8);
             st_wt(q, make_float4((float)(ws * (dp[0] - o[0])), (float)(ws * (dp[1] - o[1])), (float)(ws * (dp[2] - o[2])), 0.0f));
@@ -1154,7 +1273,11 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
 #endif
     if (!last_block_sharded(a.sync, 1u)) return;
 #ifdef BF_PCG_TIMING
-    if (threadIdx.x == 0) g_pcgT[iter & 1023][2] = rtc();
+    if (threadIdx.x == 0) {
+        g_pcgT[iter & 1023][2] = rtc();
+        unsigned long long* S = g_pcgS[iter & 1023];
+        S[0] = tStart; S[1] = stg[0]; S[2] = stg[1]; S[3] = stg[2]; S[4] = g_pcgT[iter & 1023][2];
+    }
 #endif
     if (threadIdx.x < 9) a.sync[threadIdx.x * SYNC_LINE] = 0;  // counters of the next launch
     float rDotzNew;
@@ -1169,6 +1292,255 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
         a.ctrl[K_PCG_ITERS]++;
         if (last) a.ctrl[K_PCG_DONE] = 1;
         a.ctrl[K_TICKET] = 0;
+    }
+}
+
+// Pair mode, all PCG iterations of one GN step in ONE launch (64 < N <= 2 WG + 1 images): the
+// same arithmetic as k_pcg_pairs<2> + pcg_finish_regs<2> (bit-identical results), without a launch
+// per iteration. Workgroup 0 is the finisher: its threads keep their rows' delta, r, M and p in
+// registers across iterations. Workgroups 1.. are workers, one wave per image row, each holding its
+// row's first PP_CPL x 64 pair entries and their pair statistics in registers across iterations.
+// Per iteration the workers gather the partners' p (sc1 loads), apply the pair blocks in fp64 in the
+// order of k_pcg_pairs, hand Ap_v over write-through (sc1, drained) and add to their shard's arrival
+// counter; the finisher polls the 8 shards, runs Kernel1b / 2 / 3 (SolverBundling.cu:930-1022), stores
+// p write-through (drained) and publishes the iteration on a flag word the workers poll: two hand-offs
+// per iteration of MI355X_MICROARCH.md's first valid form, instead of a kernel boundary plus a
+// last-workgroup election and two reloads of every vector. Every wait is bounded (2 s of s_memrealtime):
+// a timeout sets result error bit 3 and releases every workgroup. The grid must be co-resident: the
+// host launches it only when the occupancy query admits it with room to spare.
+#ifndef BF_PCG_PERSISTENT
+#define BF_PCG_PERSISTENT 1  // 0: one k_pcg_pairs launch per PCG iteration (A/B builds)
+#endif
+constexpr int PP_CPL = 3;                 // cached entries per lane: rows up to 192 partner pairs stay in registers
+constexpr uint32_t PP_DONE = 0x80000000u; // flag bit: the PCG loop ended (last iteration or timeout)
+constexpr uint32_t PP_ERR_TIMEOUT = 8u;   // K_ERROR bit 3
+
+__global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLin, uint32_t epoch) {
+    __shared__ float sh[WG];
+    __shared__ uint32_t sFlag;
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;  // uniform over the grid (set by earlier launches)
+    const uint32_t lane = lane_id();
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    const unsigned long long t0 = rtc();
+    uint32_t* flag = &a.sync[SYNC_FLAG];
+    const uint32_t tagBase = epoch << 8;  // iteration it's Ap granules carry tagBase + it + 1
+    if (blockIdx.x == 0) {
+        // ---- finisher ----
+        constexpr int R = 2;
+        f3 pR[R], pT[R], dR[R], dT[R], rR[R], rT[R], mR[R], mT[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = 1 + threadIdx.x + q * WG;
+            if (v < a.N) {
+                vload(a, V_P, v, pR[q], pT[q]);
+                vload(a, V_DELTA, v, dR[q], dT[q]);
+                vload(a, V_R, v, rR[q], rT[q]);
+                vload(a, V_M, v, mR[q], mT[q]);
+            }
+        }
+        float rz = ctrlf(a.ctrl, K_RDOTZ);
+        int it = 0;
+        bool last = false;
+        for (;; it++) {
+            // the rows' Ap granules (sparse part, then the dense off-diagonal products), all polled at once
+            const uint2* g[2 * R];
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const uint32_t v = 1 + threadIdx.x + q * WG;
+                g[q] = v < a.N ? a.aGran + (size_t)v * 6 : nullptr;
+                g[R + q] = v < a.N && useDense ? a.aGran + ((size_t)a.maxN + v) * 6 : nullptr;
+            }
+            float x[2 * R][6];
+            const int ok = gran_rows<2 * R>(g, tagBase + (uint32_t)it + 1u, x, t0);
+#ifdef BF_PCG_TIMING
+            if (threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
+#endif
+            if (__syncthreads_and(ok > 0) == 0) break;  // timeout: released below
+            float d = 0.0f;
+            f3 aR[R], aT[R];
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const uint32_t v = 1 + threadIdx.x + q * WG;
+                if (v < a.N) {  // pcg_ap's order of additions
+                    aR[q] = mk3(x[q][0], x[q][1], x[q][2]);
+                    aT[q] = mk3(x[q][3], x[q][4], x[q][5]);
+                    if (useDense) {  // diagonal block [trans | rot] x [pTrans | pRot], then the off-diagonal products
+                        const float* D = a.diag + (size_t)v * 36;
+                        const float pv[6] = {pT[q].x, pT[q].y, pT[q].z, pR[q].x, pR[q].y, pR[q].z};
+                        float o6[6];
+                        for (int r = 0; r < 6; r++) {
+                            float sm = 0.0f;
+                            for (int c = 0; c < 6; c++) sm += D[r * 6 + c] * pv[c];
+                            o6[r] = sm;
+                        }
+                        aT[q] = aT[q] + mk3(o6[0], o6[1], o6[2]);
+                        aR[q] = aR[q] + mk3(o6[3], o6[4], o6[5]);
+                        aT[q] = aT[q] + mk3(x[R + q][0], x[R + q][1], x[R + q][2]);
+                        aR[q] = aR[q] + mk3(x[R + q][3], x[R + q][4], x[R + q][5]);
+                    }
+                    d += dot3(pR[q], aR[q]) + dot3(pT[q], aT[q]);
+                }
+            }
+            const float pAp = block_sum(d, sh);
+            const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
+            float b = 0.0f;
+            f3 zR[R], zT[R];
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                if (1 + threadIdx.x + q * WG < a.N) {
+                    dR[q] = dR[q] + alpha * pR[q];
+                    dT[q] = dT[q] + alpha * pT[q];
+                    rR[q] = rR[q] - alpha * aR[q];
+                    rT[q] = rT[q] - alpha * aT[q];
+                    zR[q] = mul3(mR[q], rR[q]);
+                    zT[q] = mul3(mT[q], rT[q]);
+                    b += dot3(zR[q], rR[q]) + dot3(zT[q], rT[q]);
+                }
+            }
+            const float rzNew = block_sum(b, sh);
+            last = (it == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
+            const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const uint32_t v = 1 + threadIdx.x + q * WG;
+                if (v < a.N) {
+                    pR[q] = zR[q] + beta * pR[q];
+                    pT[q] = zT[q] + beta * pT[q];
+                    if (!last) vstore_t<true>(a, V_P, v, pR[q], pT[q]);  // the workers' next gathers
+                }
+            }
+            rz = rzNew;
+            if (last) break;
+            // p is read by ~N x 92 gathers: published write-through, drained, then one flag word
+            // (p as polled granules ran 20 % slower: the workers' polls swamp the hand-off)
+            drain_stores();
+            __syncthreads();
+            if (threadIdx.x == 0) st_wt(flag, (uint32_t)(it + 1));
+#ifdef BF_PCG_TIMING
+            if (threadIdx.x == 0) g_pcgT[it & 1023][3] = rtc();
+#endif
+        }
+        // final state (later launches read it plainly across the kernel boundary)
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = 1 + threadIdx.x + q * WG;
+            if (v < a.N) {
+                vstore(a, V_DELTA, v, dR[q], dT[q]);
+                vstore(a, V_R, v, rR[q], rT[q]);
+                vstore(a, V_P, v, pR[q], pT[q]);
+                if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
+                    f3 nr, nt;
+                    lie_update(dR[q], dT[q], mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                               mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
+                    a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
+                    a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+                }
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (!last) atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT);
+            a.ctrl[K_RDOTZ] = __float_as_uint(rz);
+            a.ctrl[K_PCG_ITERS] += (uint32_t)(it + (last ? 1 : 0));
+            a.ctrl[K_PCG_DONE] = 1;
+            st_wt(flag, PP_DONE);  // releases the workers
+        }
+        return;
+    }
+    // ---- workers: one wave per row ----
+    const uint32_t v = 1 + (blockIdx.x - 1) * (WG / 64) + (threadIdx.x >> 6);
+    const bool hasRow = v < a.N;
+    int e0 = 0, e1 = 0;
+    int2 rp[PP_CPL];
+    double st[PP_CPL][16];
+    double dst[DSTAT];
+    if (hasRow) {
+        e0 = a.rowPairStart[v];
+        e1 = a.rowPairStart[v + 1];
+#pragma unroll
+        for (int c = 0; c < PP_CPL; c++) {
+            const int k = e0 + (int)lane + 64 * c;
+            rp[c] = k < e1 ? a.rowPair[k] : make_int2(0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < PP_CPL; c++) {
+            const bool ok = e0 + (int)lane + 64 * c < e1;
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                const double2 x = ok ? *reinterpret_cast<const double2*>(a.pstat + (size_t)rp[c].x * PSTAT + q) : make_double2(0.0, 0.0);
+                st[c][q] = x.x;
+                st[c][q + 1] = x.y;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < DSTAT; q++) dst[q] = a.dstat[(size_t)v * DSTAT + q];
+    }
+    for (uint32_t it = 0;; it++) {
+        int state = 1;
+        if (hasRow) {
+            // p of iteration it (the previous launch's, or the finisher's write-through stores)
+            f3 pr[PP_CPL], pt[PP_CPL], pvR, pvT;
+            const uint32_t tag = tagBase + it + 1u;
+#pragma unroll
+            for (int c = 0; c < PP_CPL; c++) vload_t<true>(a, V_P, (uint32_t)rp[c].y & ~PAIR_A_FLAG, pr[c], pt[c]);
+            vload_t<true>(a, V_P, v, pvR, pvT);
+            double o[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int c = 0; c < PP_CPL; c++) {
+                const uint32_t u = (uint32_t)rp[c].y & ~PAIR_A_FLAG;
+                if (e0 + (int)lane + 64 * c < e1 && u != 0) {  // p_0 = 0 (image 0 fixed)
+                    const double w[3] = {pr[c].x, pr[c].y, pr[c].z}, t[3] = {pt[c].x, pt[c].y, pt[c].z};
+                    double bb[6];
+                    pair_block_apply(st[c], ((uint32_t)rp[c].y & PAIR_A_FLAG) != 0, w, t, bb);
+#pragma unroll
+                    for (int q = 0; q < 6; q++) o[q] += bb[q];
+                }
+            }
+            // entries beyond the cached ones (rows with more than PP_CPL x 64 partners), from memory
+            for (int k = e0 + (int)lane + 64 * PP_CPL; k < e1; k += 64) {
+                const int2 r2 = a.rowPair[k];
+                const uint32_t u = (uint32_t)r2.y & ~PAIR_A_FLAG;
+                if (u == 0) continue;
+                f3 qr, qt;
+                vload_t<true>(a, V_P, u, qr, qt);
+                const double w[3] = {qr.x, qr.y, qr.z}, t[3] = {qt.x, qt.y, qt.z};
+                double bb[6];
+                pair_block_apply(a.pstat + (size_t)r2.x * PSTAT, ((uint32_t)r2.y & PAIR_A_FLAG) != 0, w, t, bb);
+#pragma unroll
+                for (int q = 0; q < 6; q++) o[q] += bb[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 6; q++) o[q] = wave_sum_d(o[q]);
+            if (lane < 6) {  // Ap_v = w (D_v p_v - sum_u B_vu p_u): one granule per lane, [rot | trans]
+                const double w[3] = {pvR.x, pvR.y, pvR.z}, t[3] = {pvT.x, pvT.y, pvT.z};
+                double dp[6];
+                diag_apply(dst, w, t, dp);
+                const double ws = wSparse;
+                float y = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 6; q++)
+                    if ((int)lane == q) y = (float)(ws * (dp[q] - o[q]));
+                gran_store(a.aGran + (size_t)v * 6 + lane, y, tag);
+            }
+            if (useDense) pcg_dense_offdiag_row<true>(a, v, tag);
+        }
+        if (threadIdx.x == 0) {
+#ifdef BF_PCG_TIMING
+            atomicMax(&g_pcgT[it & 1023][1], rtc());
+#endif
+            uint32_t f;
+            for (;;) {
+                f = ld_wt(flag);
+                if ((f & PP_DONE) || f >= it + 1) break;
+                if (pp_timed_out(t0)) { f = PP_DONE; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            sFlag = f;
+#ifdef BF_PCG_TIMING
+            if (!(f & PP_DONE)) atomicMax(&g_pcgT[(it + 1) & 1023][0], rtc());  // the latest worker to see the flag
+#endif
+        }
+        __syncthreads();
+        if ((sFlag & PP_DONE) || __syncthreads_or(state < 1)) return;
     }
 }
 
@@ -1914,6 +2286,7 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.verifyOptDistThresh = (o && o->verifyOptDistThresh > 0) ? o->verifyOptDistThresh : 0.02f;
     cfg.normalEquations = o ? o->normalEquations : 0;
     cfg.earlyOut = !(o && o->disableEarlyOut);
+    cfg.pcgLaunch = o ? o->pcgLaunch : 0;
     return cfg;
 }
 
@@ -1985,15 +2358,20 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     pstat_.alloc(((size_t)maxPairsA_ + 1) * PSTAT);
     dstat_.alloc((size_t)N * DSTAT);
     apPair_.alloc((size_t)N * 8);
+    aGran_.alloc((size_t)N * 12);  // [2][N][6]: sparse Ap rows, then the dense off-diagonal products
     rzPart_.alloc(N);
     int dev = 0;
     hipDeviceProp_t prop;
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
+    int occP = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP, k_pcg_persist, WG, 0));
+    persistCapacity_ = (unsigned)std::max(occP, 0) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
+    BF_HIP(hipMemsetAsync(aGran_.p, 0, aGran_.bytes(), stream_));  // tag 0 is never awaited
     BF_HIP(hipMemsetAsync(imgPairN_.p, 0, imgPairN_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
 }
@@ -2055,6 +2433,7 @@ void Solver::solve(const SolveArgs& s) {
     a.pairStart = pairStart_.p; a.rowPairStart = rowPairStart_.p; a.pairA = pairA_.p; a.pairB = pairB_.p;
     a.pairCorr = pairCorr_.p; a.rowPair = rowPair_.p; a.pstat = pstat_.p; a.dstat = dstat_.p;
     a.apPair = apPair_.p; a.rzPart = rzPart_.p;
+    a.aGran = aGran_.p;
     a.shardCount = shardCount_; a.shardIndex = shardIndex_; a.pairBound = 0;
     a.earlyOut = cfg_.earlyOut ? 1u : 0u;
     // assembled normal equations for sparse-only solves (auto) unless the matrix-free path is forced
@@ -2137,7 +2516,40 @@ void Solver::solve(const SolveArgs& s) {
             if (s.numImages <= (uint32_t)SMALL_N) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
-                if (s.numImages <= 2u * WG + 1u) {
+                const unsigned persistGrid = 1u + div_up(s.numImages - 1u, (unsigned)(WG / 64));
+                if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.numImages <= 2u * WG + 1u && s.nLin < 255u &&
+                    persistGrid * 2u <= persistCapacity_) {
+                    // one launch for the GN step's PCG loop (its grid is co-resident with room to spare)
+#ifdef BF_PCG_TIMING
+                    {
+                        std::vector<unsigned long long> z(1024 * 4, 0ull);
+                        BF_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_pcgT), z.data(), z.size() * 8, 0, hipMemcpyHostToDevice, stream_));
+                    }
+#endif
+                    if (s.nLin) {
+                        k_pcg_persist<<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
+                        pcgEpoch_ = (pcgEpoch_ + 1) & 0xFFFFFFu;
+                    }
+#ifdef BF_PCG_TIMING
+                    {
+                        std::vector<unsigned long long> t(1024 * 4);
+                        BF_HIP(hipMemcpyFromSymbolAsync(t.data(), HIP_SYMBOL(g_pcgT), t.size() * 8, 0, hipMemcpyDeviceToHost, stream_));
+                        BF_HIP(hipStreamSynchronize(stream_));
+                        // per iteration q: [0] latest worker saw the flag of q, [1] latest worker arrival of q,
+                        // [2] finisher saw all arrivals of q, [3] finisher published q + 1
+                        double w = 0, ar = 0, fi = 0, bc = 0; int n = 0;
+                        for (uint32_t q = 1; q + 2 < s.nLin && q < 1023; q++) {
+                            const unsigned long long* r = &t[q * 4];
+                            const unsigned long long* nx = &t[(q + 1) * 4];
+                            if (!r[0] || !r[1] || !r[2] || !r[3] || !nx[0]) continue;
+                            w += (double)r[1] - (double)r[0]; ar += (double)r[2] - (double)r[1];
+                            fi += (double)r[3] - (double)r[2]; bc += (double)nx[0] - (double)r[3]; n++;
+                        }
+                        if (n) fprintf(stderr, "persistent pcg (us, mean over %d iterations): workers flag->arrive %.2f  arrival->finisher %.2f  finisher %.2f  flag->last worker %.2f  total %.2f\n",
+                                       n, w / n / 100, ar / n / 100, fi / n / 100, bc / n / 100, (w + ar + fi + bc) / n / 100);
+                    }
+#endif
+                } else if (s.numImages <= 2u * WG + 1u) {
 #ifdef BF_PCG_TIMING
                     {
                         std::vector<unsigned long long> init(1024 * 4);
@@ -2161,6 +2573,17 @@ void Solver::solve(const SolveArgs& s) {
                         }
                         if (n) fprintf(stderr, "pcg timing (us, mean over %d launches): phase A %.2f  arrival %.2f  finisher %.2f  start-to-next-start %.2f\n",
                                        n, sA / n / 100.0, sW / n / 100.0, sF / n / 100.0, sAll / n / 100.0);
+                        std::vector<unsigned long long> g(1024 * 6);
+                        BF_HIP(hipMemcpyFromSymbol(g.data(), HIP_SYMBOL(g_pcgS), g.size() * 8));
+                        double d0 = 0, d1 = 0, d2 = 0, d3 = 0, sk = 0; int m = 0;
+                        for (uint32_t q = 1; q + 1 < s.nLin && q < 1024; q++) {
+                            const unsigned long long* G = &g[q * 6];
+                            if (!G[4] || !G[1] || !G[2] || !G[3]) continue;
+                            sk += (double)(G[0] - t[q * 4]); d0 += (double)(G[1] - G[0]); d1 += (double)(G[2] - G[1]);
+                            d2 += (double)(G[3] - G[2]); d3 += (double)(G[4] - G[3]); m++;
+                        }
+                        if (m) fprintf(stderr, "  last WG (us): start skew %.2f  row start loads %.2f  pair loop %.2f  wave sums %.2f  diag+store+arrival %.2f\n",
+                                       sk / m / 100.0, d0 / m / 100.0, d1 / m / 100.0, d2 / m / 100.0, d3 / m / 100.0);
                     }
 #endif
                 } else {

@@ -158,6 +158,9 @@ typedef struct BFSolverOptions {   /* zParametersBundlingDefault.txt defaults wh
                                       a PCG step with |p.Ap| < 5e-7 is the last, and the GN loop stops when
                                       max|delta| < 0.005, :1088-1093, :1204-1210); 1: built without it, fixed
                                       nNonLin x nLin schedules */
+    int32_t pcgLaunch;             /* 0 auto: a pair-mode GN step of 65..513 images runs its whole PCG loop in
+                                      one persistent launch (when the grid fits co-resident); 1: one launch
+                                      per PCG iteration. Bit-identical results either way */
 } BFSolverOptions;
 
 /* ctor (CUDASolverBundling.cpp:24-136): capacity maxImages x maxCorr residuals */

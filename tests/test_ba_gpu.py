@@ -23,13 +23,14 @@ MODES = [bfa.abi.NORMAL_EQ_MATRIX_FREE, bfa.abi.NORMAL_EQ_ASSEMBLED]
 
 
 def gpu_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_corr=None, corr=None, mode=None,
-              shard=None, export=False, early_out=True):
-    """mode: normal equations (None = auto: assembled for sparse-only solves); shard = (count, index)."""
+              shard=None, export=False, early_out=True, pcg_launch=0):
+    """mode: normal equations (None = auto: assembled for sparse-only solves); shard = (count, index);
+    pcg_launch: 0 auto (one persistent PCG launch per GN step where it fits), 1 one launch per iteration."""
     from bundlefusion_amd.solver import DeviceCache, SolverBundling
     K = prob["K"]
     corr = prob["corr"] if corr is None else corr
     max_corr = max_corr or max(K * 4000, len(corr))
-    S = SolverBundling(K, max_corr, normal_equations=mode, early_out=early_out)
+    S = SolverBundling(K, max_corr, normal_equations=mode, early_out=early_out, pcg_launch=pcg_launch)
     if shard is not None:
         S.set_shard(*shard)
     d_corr = bfa.DeviceArray.from_host(corr if len(corr) else np.zeros(1, corr.dtype))
@@ -414,6 +415,30 @@ def test_dense_solve_bit_deterministic(mode, K):
     a = gpu_solve(prob, *args, use_cache=True, mode=mode)
     b = gpu_solve(prob, *args, use_cache=True, mode=mode)
     assert a[3]["numDensePairs"] > (0 if K == 6 else 20)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("early_out", [False, True])
+def test_persistent_pcg_bit_identical(early_out):
+    """The persistent pair-mode PCG (all iterations of a GN step in one launch: register-resident rows,
+    write-through hand-offs and a polled flag, k_pcg_persist) and one launch per iteration (k_pcg_pairs)
+    compute the same arithmetic in the same order: the solves agree bit for bit, with and without the
+    early exits, sparse and with the dense term."""
+    prob = k400_problem()
+    a = gpu_solve(prob, 3, 150, [1, 1, 1], early_out=early_out, pcg_launch=0)
+    b = gpu_solve(prob, 3, 150, [1, 1, 1], early_out=early_out, pcg_launch=1)
+    assert a[3]["error"] == 0 and b[3]["error"] == 0
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert a[3] == b[3]
+    prob = make_problem(K=72, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
+    args = (2, 40, [1, 1], [1000, 1000], [0, 0])
+    m = bfa.abi.NORMAL_EQ_ASSEMBLED
+    a = gpu_solve(prob, *args, use_cache=True, mode=m, early_out=early_out, pcg_launch=0)
+    b = gpu_solve(prob, *args, use_cache=True, mode=m, early_out=early_out, pcg_launch=1)
+    assert a[3]["numDensePairs"] > 20 and a[3]["error"] == 0
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     assert a[3] == b[3]
