@@ -1315,6 +1315,150 @@ constexpr int PP_CPL = 3;                 // cached entries per lane: rows up to
 constexpr uint32_t PP_DONE = 0x80000000u; // flag bit: the PCG loop ended (last iteration or timeout)
 constexpr uint32_t PP_ERR_TIMEOUT = 8u;   // K_ERROR bit 3
 
+// The finisher workgroup of k_pcg_persist: R image rows per thread (R = 2: up to 513 images, every
+// vector in registers; R = 8: up to 2 049, p and r in registers, delta and M read and written in
+// memory by the thread that owns the row, z recomputed from M r where it is needed again: the same
+// operations in the same order, so the result matches the per-launch finisher's bit for bit). The
+// dense term is taken by R = 2 only (the host routes larger dense steps to one launch per iteration).
+template <int R>
+__device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int nLin, uint32_t tagBase, uint32_t* flag,
+                                     unsigned long long t0) {
+    constexpr bool REGS = R <= 2;
+    f3 pR[R], pT[R], rR[R], rT[R];
+    f3 dR[REGS ? R : 1], dT[REGS ? R : 1], mR[REGS ? R : 1], mT[REGS ? R : 1];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        const uint32_t v = 1 + threadIdx.x + q * WG;
+        if (v < a.N) {
+            vload(a, V_P, v, pR[q], pT[q]);
+            vload(a, V_R, v, rR[q], rT[q]);
+            if (REGS) {
+                vload(a, V_DELTA, v, dR[REGS ? q : 0], dT[REGS ? q : 0]);
+                vload(a, V_M, v, mR[REGS ? q : 0], mT[REGS ? q : 0]);
+            }
+        }
+    }
+    float rz = ctrlf(a.ctrl, K_RDOTZ);
+    int it = 0;
+    bool last = false;
+    for (;; it++) {
+        // the rows' Ap granules (sparse part, then the dense off-diagonal products), all polled at once
+        constexpr int NG = REGS ? 2 * R : R;
+        const uint2* g[NG];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = 1 + threadIdx.x + q * WG;
+            g[q] = v < a.N ? a.aGran + (size_t)v * 6 : nullptr;
+            if (REGS) g[(R + q) % NG] = v < a.N && useDense ? a.aGran + ((size_t)a.maxN + v) * 6 : nullptr;
+        }
+        float x[NG][6];
+        const int ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0);
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
+#endif
+        if (__syncthreads_and(ok > 0) == 0) break;  // timeout: released below
+        float d = 0.0f;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = 1 + threadIdx.x + q * WG;
+            if (v < a.N) {  // pcg_ap's order of additions; x[q] becomes Ap of the row
+                f3 aR = mk3(x[q][0], x[q][1], x[q][2]), aT = mk3(x[q][3], x[q][4], x[q][5]);
+                if (REGS && useDense) {  // diagonal block [trans | rot] x [pTrans | pRot], then the off-diagonal products
+                    const float* D = a.diag + (size_t)v * 36;
+                    const float pv[6] = {pT[q].x, pT[q].y, pT[q].z, pR[q].x, pR[q].y, pR[q].z};
+                    float o6[6];
+                    for (int r = 0; r < 6; r++) {
+                        float sm = 0.0f;
+                        for (int c = 0; c < 6; c++) sm += D[r * 6 + c] * pv[c];
+                        o6[r] = sm;
+                    }
+                    aT = aT + mk3(o6[0], o6[1], o6[2]);
+                    aR = aR + mk3(o6[3], o6[4], o6[5]);
+                    aT = aT + mk3(x[(R + q) % NG][0], x[(R + q) % NG][1], x[(R + q) % NG][2]);
+                    aR = aR + mk3(x[(R + q) % NG][3], x[(R + q) % NG][4], x[(R + q) % NG][5]);
+                }
+                x[q][0] = aR.x; x[q][1] = aR.y; x[q][2] = aR.z;
+                x[q][3] = aT.x; x[q][4] = aT.y; x[q][5] = aT.z;
+                d += dot3(pR[q], aR) + dot3(pT[q], aT);
+            }
+        }
+        const float pAp = block_sum(d, sh);
+        const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
+        float b = 0.0f;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = 1 + threadIdx.x + q * WG;
+            if (v < a.N) {
+                const f3 aR = mk3(x[q][0], x[q][1], x[q][2]), aT = mk3(x[q][3], x[q][4], x[q][5]);
+                f3 dr, dt, mr, mt;
+                if (REGS) { dr = dR[REGS ? q : 0]; dt = dT[REGS ? q : 0]; mr = mR[REGS ? q : 0]; mt = mT[REGS ? q : 0]; }
+                else { vload(a, V_DELTA, v, dr, dt); vload(a, V_M, v, mr, mt); }
+                dr = dr + alpha * pR[q];
+                dt = dt + alpha * pT[q];
+                if (REGS) { dR[REGS ? q : 0] = dr; dT[REGS ? q : 0] = dt; }
+                else vstore(a, V_DELTA, v, dr, dt);
+                rR[q] = rR[q] - alpha * aR;
+                rT[q] = rT[q] - alpha * aT;
+                const f3 zR = mul3(mr, rR[q]), zT = mul3(mt, rT[q]);
+                b += dot3(zR, rR[q]) + dot3(zT, rT[q]);
+            }
+        }
+        const float rzNew = block_sum(b, sh);
+        last = (it == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
+        const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = 1 + threadIdx.x + q * WG;
+            if (v < a.N) {
+                f3 mr, mt;
+                if (REGS) { mr = mR[REGS ? q : 0]; mt = mT[REGS ? q : 0]; }
+                else vload(a, V_M, v, mr, mt);
+                const f3 zR = mul3(mr, rR[q]), zT = mul3(mt, rT[q]);
+                pR[q] = zR + beta * pR[q];
+                pT[q] = zT + beta * pT[q];
+                if (!last) vstore_t<true>(a, V_P, v, pR[q], pT[q]);  // the workers' next gathers
+            }
+        }
+        rz = rzNew;
+        if (last) break;
+        // p is read by ~N x 92 gathers: published write-through, drained, then one flag word
+        // (p as polled granules ran 20 % slower: the workers' polls swamp the hand-off)
+        drain_stores();
+        __syncthreads();
+        if (threadIdx.x == 0) st_wt(flag, (uint32_t)(it + 1));
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) g_pcgT[it & 1023][3] = rtc();
+#endif
+    }
+    // final state (later launches read it plainly across the kernel boundary)
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        const uint32_t v = 1 + threadIdx.x + q * WG;
+        if (v < a.N) {
+            f3 dr, dt;
+            if (REGS) { dr = dR[REGS ? q : 0]; dt = dT[REGS ? q : 0]; vstore(a, V_DELTA, v, dr, dt); }
+            else vload(a, V_DELTA, v, dr, dt);
+            vstore(a, V_R, v, rR[q], rT[q]);
+            vstore(a, V_P, v, pR[q], pT[q]);
+            if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
+                f3 nr, nt;
+                lie_update(dr, dt, mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                           mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
+                a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
+                a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (!last) atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT);
+        a.ctrl[K_RDOTZ] = __float_as_uint(rz);
+        a.ctrl[K_PCG_ITERS] += (uint32_t)(it + (last ? 1 : 0));
+        a.ctrl[K_PCG_DONE] = 1;
+        st_wt(flag, PP_DONE);  // releases the workers
+    }
+}
+
+template <int R>
 __global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLin, uint32_t epoch) {
     __shared__ float sh[WG];
     __shared__ uint32_t sFlag;
@@ -1325,125 +1469,7 @@ __global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLi
     uint32_t* flag = &a.sync[SYNC_FLAG];
     const uint32_t tagBase = epoch << 8;  // iteration it's Ap granules carry tagBase + it + 1
     if (blockIdx.x == 0) {
-        // ---- finisher ----
-        constexpr int R = 2;
-        f3 pR[R], pT[R], dR[R], dT[R], rR[R], rT[R], mR[R], mT[R];
-#pragma unroll
-        for (int q = 0; q < R; q++) {
-            const uint32_t v = 1 + threadIdx.x + q * WG;
-            if (v < a.N) {
-                vload(a, V_P, v, pR[q], pT[q]);
-                vload(a, V_DELTA, v, dR[q], dT[q]);
-                vload(a, V_R, v, rR[q], rT[q]);
-                vload(a, V_M, v, mR[q], mT[q]);
-            }
-        }
-        float rz = ctrlf(a.ctrl, K_RDOTZ);
-        int it = 0;
-        bool last = false;
-        for (;; it++) {
-            // the rows' Ap granules (sparse part, then the dense off-diagonal products), all polled at once
-            const uint2* g[2 * R];
-#pragma unroll
-            for (int q = 0; q < R; q++) {
-                const uint32_t v = 1 + threadIdx.x + q * WG;
-                g[q] = v < a.N ? a.aGran + (size_t)v * 6 : nullptr;
-                g[R + q] = v < a.N && useDense ? a.aGran + ((size_t)a.maxN + v) * 6 : nullptr;
-            }
-            float x[2 * R][6];
-            const int ok = gran_rows<2 * R>(g, tagBase + (uint32_t)it + 1u, x, t0);
-#ifdef BF_PCG_TIMING
-            if (threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
-#endif
-            if (__syncthreads_and(ok > 0) == 0) break;  // timeout: released below
-            float d = 0.0f;
-            f3 aR[R], aT[R];
-#pragma unroll
-            for (int q = 0; q < R; q++) {
-                const uint32_t v = 1 + threadIdx.x + q * WG;
-                if (v < a.N) {  // pcg_ap's order of additions
-                    aR[q] = mk3(x[q][0], x[q][1], x[q][2]);
-                    aT[q] = mk3(x[q][3], x[q][4], x[q][5]);
-                    if (useDense) {  // diagonal block [trans | rot] x [pTrans | pRot], then the off-diagonal products
-                        const float* D = a.diag + (size_t)v * 36;
-                        const float pv[6] = {pT[q].x, pT[q].y, pT[q].z, pR[q].x, pR[q].y, pR[q].z};
-                        float o6[6];
-                        for (int r = 0; r < 6; r++) {
-                            float sm = 0.0f;
-                            for (int c = 0; c < 6; c++) sm += D[r * 6 + c] * pv[c];
-                            o6[r] = sm;
-                        }
-                        aT[q] = aT[q] + mk3(o6[0], o6[1], o6[2]);
-                        aR[q] = aR[q] + mk3(o6[3], o6[4], o6[5]);
-                        aT[q] = aT[q] + mk3(x[R + q][0], x[R + q][1], x[R + q][2]);
-                        aR[q] = aR[q] + mk3(x[R + q][3], x[R + q][4], x[R + q][5]);
-                    }
-                    d += dot3(pR[q], aR[q]) + dot3(pT[q], aT[q]);
-                }
-            }
-            const float pAp = block_sum(d, sh);
-            const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
-            float b = 0.0f;
-            f3 zR[R], zT[R];
-#pragma unroll
-            for (int q = 0; q < R; q++) {
-                if (1 + threadIdx.x + q * WG < a.N) {
-                    dR[q] = dR[q] + alpha * pR[q];
-                    dT[q] = dT[q] + alpha * pT[q];
-                    rR[q] = rR[q] - alpha * aR[q];
-                    rT[q] = rT[q] - alpha * aT[q];
-                    zR[q] = mul3(mR[q], rR[q]);
-                    zT[q] = mul3(mT[q], rT[q]);
-                    b += dot3(zR[q], rR[q]) + dot3(zT[q], rT[q]);
-                }
-            }
-            const float rzNew = block_sum(b, sh);
-            last = (it == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
-            const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
-#pragma unroll
-            for (int q = 0; q < R; q++) {
-                const uint32_t v = 1 + threadIdx.x + q * WG;
-                if (v < a.N) {
-                    pR[q] = zR[q] + beta * pR[q];
-                    pT[q] = zT[q] + beta * pT[q];
-                    if (!last) vstore_t<true>(a, V_P, v, pR[q], pT[q]);  // the workers' next gathers
-                }
-            }
-            rz = rzNew;
-            if (last) break;
-            // p is read by ~N x 92 gathers: published write-through, drained, then one flag word
-            // (p as polled granules ran 20 % slower: the workers' polls swamp the hand-off)
-            drain_stores();
-            __syncthreads();
-            if (threadIdx.x == 0) st_wt(flag, (uint32_t)(it + 1));
-#ifdef BF_PCG_TIMING
-            if (threadIdx.x == 0) g_pcgT[it & 1023][3] = rtc();
-#endif
-        }
-        // final state (later launches read it plainly across the kernel boundary)
-#pragma unroll
-        for (int q = 0; q < R; q++) {
-            const uint32_t v = 1 + threadIdx.x + q * WG;
-            if (v < a.N) {
-                vstore(a, V_DELTA, v, dR[q], dT[q]);
-                vstore(a, V_R, v, rR[q], rT[q]);
-                vstore(a, V_P, v, pR[q], pT[q]);
-                if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
-                    f3 nr, nt;
-                    lie_update(dR[q], dT[q], mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
-                               mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
-                    a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
-                    a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
-                }
-            }
-        }
-        if (threadIdx.x == 0) {
-            if (!last) atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT);
-            a.ctrl[K_RDOTZ] = __float_as_uint(rz);
-            a.ctrl[K_PCG_ITERS] += (uint32_t)(it + (last ? 1 : 0));
-            a.ctrl[K_PCG_DONE] = 1;
-            st_wt(flag, PP_DONE);  // releases the workers
-        }
+        pcg_persist_finisher<R>(a, sh, useDense, nLin, tagBase, flag, t0);
         return;
     }
     // ---- workers: one wave per row ----
@@ -2365,9 +2391,10 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
-    int occP = 0;
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP, k_pcg_persist, WG, 0));
-    persistCapacity_ = (unsigned)std::max(occP, 0) * (unsigned)numCUs_;
+    int occP = 0, occP8 = 0;
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP, k_pcg_persist<2>, WG, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP8, k_pcg_persist<8>, WG, 0));
+    persistCapacity_ = (unsigned)std::max(std::min(occP, occP8), 0) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
@@ -2517,9 +2544,12 @@ void Solver::solve(const SolveArgs& s) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
                 const unsigned persistGrid = 1u + div_up(s.numImages - 1u, (unsigned)(WG / 64));
-                if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.numImages <= 2u * WG + 1u && s.nLin < 255u &&
-                    persistGrid * 2u <= persistCapacity_) {
-                    // one launch for the GN step's PCG loop (its grid is co-resident with room to spare)
+                // one launch for the GN step's PCG loop when its grid is co-resident: up to 513 images
+                // (finisher rows in registers, dense term included) with room to spare, up to 2 049
+                // sparse-only (config 4's 2 001 keyframes) within the occupancy query's capacity
+                const bool small = s.numImages <= 2u * WG + 1u && persistGrid * 2u <= persistCapacity_;
+                const bool wide = !small && !dense && s.numImages <= 8u * WG + 1u && persistGrid <= persistCapacity_;
+                if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.nLin < 255u && (small || wide)) {
 #ifdef BF_PCG_TIMING
                     {
                         std::vector<unsigned long long> z(1024 * 4, 0ull);
@@ -2527,7 +2557,8 @@ void Solver::solve(const SolveArgs& s) {
                     }
 #endif
                     if (s.nLin) {
-                        k_pcg_persist<<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
+                        if (small) k_pcg_persist<2><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
+                        else k_pcg_persist<8><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
                         pcgEpoch_ = (pcgEpoch_ + 1) & 0xFFFFFFu;
                     }
 #ifdef BF_PCG_TIMING

@@ -423,9 +423,10 @@ def test_dense_solve_bit_deterministic(mode, K):
 @pytest.mark.parametrize("early_out", [False, True])
 def test_persistent_pcg_bit_identical(early_out):
     """The persistent pair-mode PCG (all iterations of a GN step in one launch: register-resident rows,
-    write-through hand-offs and a polled flag, k_pcg_persist) and one launch per iteration (k_pcg_pairs)
-    compute the same arithmetic in the same order: the solves agree bit for bit, with and without the
-    early exits, sparse and with the dense term."""
+    Ap as tagged granules, p write-through behind a polled flag, k_pcg_persist) and one launch per
+    iteration (k_pcg_pairs) compute the same arithmetic in the same order: the solves agree bit for bit,
+    with and without the early exits, sparse and with the dense term, and above 513 images (the wide
+    finisher of config 4's 2 001 keyframes)."""
     prob = k400_problem()
     a = gpu_solve(prob, 3, 150, [1, 1, 1], early_out=early_out, pcg_launch=0)
     b = gpu_solve(prob, 3, 150, [1, 1, 1], early_out=early_out, pcg_launch=1)
@@ -439,6 +440,14 @@ def test_persistent_pcg_bit_identical(early_out):
     a = gpu_solve(prob, *args, use_cache=True, mode=m, early_out=early_out, pcg_launch=0)
     b = gpu_solve(prob, *args, use_cache=True, mode=m, early_out=early_out, pcg_launch=1)
     assert a[3]["numDensePairs"] > 20 and a[3]["error"] == 0
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert a[3] == b[3]
+    # above 513 images: the wide finisher (8 rows per thread, delta and M in memory), sparse only
+    prob = make_problem(K=700, stride=1, max_per_pair=4, outliers=0.0, drift=(0.05, 0.002))
+    a = gpu_solve(prob, 2, 30, [1, 1], early_out=early_out, pcg_launch=0)
+    b = gpu_solve(prob, 2, 30, [1, 1], early_out=early_out, pcg_launch=1)
+    assert a[3]["error"] == 0 and a[3]["pcgIterations"] > 10
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     assert a[3] == b[3]
