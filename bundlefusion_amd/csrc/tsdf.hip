@@ -1421,6 +1421,16 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
             d[zi] = __uint_as_float(v[0] ^ DC_DEPTH_KEY);
             cc[zi] = v[1];
         }
+#ifdef BF_APPLY_DIAG
+        {  // (slice pair, op) wave-slots with no lane in band, and all of them (counted on lane 0)
+            unsigned long long b[ZC];
+#pragma unroll
+            for (int zi = 0; zi < ZC; zi++) b[zi] = __builtin_amdgcn_ballot_w64(fabsf(d[zi] - pz[zi]) < A.truncation + A.truncScale * d[zi]);
+            if (lane_id_here() == 0)
+#pragma unroll
+                for (int zi = 0; zi < ZC; zi += 2) { diag[4] += (b[zi] | b[zi + 1]) == 0; diag[5] += 1; }
+        }
+#endif
 #pragma unroll
         for (int zi = 0; zi < ZC; zi++) {
             const float sd = d[zi] - pz[zi];
@@ -1470,7 +1480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
     uint32_t updated = 0, rmw = 0;  // per wave and launch: < 2^32
 #ifdef BF_APPLY_DIAG
-    uint32_t diag[4] = {0, 0, 0, 0}, diagPairs = 0, diagEmpty = 0;
+    uint32_t diag[6] = {0, 0, 0, 0, 0, 0}, diagPairs = 0, diagEmpty = 0;
 #endif
     WorkCursor cur = work_begin(A.ctrl, ops.n);
     size_t b;
@@ -1552,6 +1562,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     flush_stats2(A.stats, 22, diag[2], 23, diag[3]);
     __syncthreads();
     flush_stats2(A.stats, 24, lane_id_here() == 0 ? diagPairs : 0u, 25, lane_id_here() == 0 ? diagEmpty : 0u);
+    __syncthreads();
+    flush_stats2(A.stats, 26, diag[4], 27, diag[5]);
 #endif
 }
 
@@ -2018,9 +2030,9 @@ BFTsdfStats Scene::stats() {
     std::memcpy(&s, sum, sizeof(s));
     s.pixels += hostPixels_;
 #ifdef BF_APPLY_DIAG
-    fprintf(stderr, "apply diag: offscreen %llu invalid %llu front %llu behind %llu (half,op) pairs %llu empty %llu\n",
+    fprintf(stderr, "apply diag: offscreen %llu invalid %llu front %llu behind %llu (half,op) pairs %llu empty %llu (slice pair,op) %llu empty %llu\n",
             (unsigned long long)sum[20], (unsigned long long)sum[21], (unsigned long long)sum[22], (unsigned long long)sum[23],
-            (unsigned long long)sum[24], (unsigned long long)sum[25]);
+            (unsigned long long)sum[24], (unsigned long long)sum[25], (unsigned long long)sum[27], (unsigned long long)sum[26]);
 #endif
     return s;
 }
