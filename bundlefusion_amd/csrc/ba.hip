@@ -26,7 +26,10 @@ namespace {
 
 constexpr float FLOAT_EPSILON = 0.000001f;  // Source/SolverUtil.h:9
 constexpr int WG = 256;
-constexpr uint32_t TILE = 256;  // correspondences per table-build tile
+constexpr uint32_t TILE = 256;  // correspondences per table-build tile, per 256 images (a.tile)
+// tile size for n images: the [n][nTiles] count matrix stays ~nCorr entries at any image count (a
+// fixed 256 made it 8 x nCorr at 2 001 images: 955 us of strided count writes per solve)
+__host__ __device__ constexpr uint32_t tile_for(uint32_t n) { return TILE * (n > 256u ? (n + 255u) / 256u : 1u); }
 constexpr int CH = 512;        // row entries per chunk: the work unit of one wave in the GN/PCG kernels
 constexpr int CPL = CH / 64;   // chunk entries per lane
 
@@ -50,7 +53,7 @@ struct BA {
     uint32_t N, maxN, cap;
     int *rowCount, *rowStart, *rowLen, *rowTmp, *rowIdx;
     int* tileCnt;  // [N][nTiles]
-    uint32_t nTiles;
+    uint32_t nTiles, tile;
     int *rowChunk, *chunkRow;  // chunks of row v: [rowChunk[v], rowChunk[v+1]); chunk -> row
     float4* chunkPart;         // [chunk][3] per-chunk partial sums
     uint32_t* sync;            // last_block_sharded: 8 shard counters + top counter (+ flag words), 64 B apart
@@ -208,7 +211,12 @@ __device__ bool last_block(uint32_t* ticket) {
 // not depend on it); a shard's last arriver adds to the top counter. Counters grow monotonically
 // within a launch, so round `epoch` (1-based) completes at epoch * arrivers.
 constexpr int SYNC_LINE = 16;  // words per 64-B line
-constexpr int SYNC_TOP = 8 * SYNC_LINE, SYNC_FLAG = 9 * SYNC_LINE, SYNC_WORDS = 17 * SYNC_LINE;
+constexpr int SYNC_TOP = 8 * SYNC_LINE, SYNC_FLAG = 9 * SYNC_LINE, SYNC_ALPHA = 17 * SYNC_LINE;  // alpha: 256 words
+// k_pcg_persist's flag in PP_NFLAG replicas 256 B apart (one per 64-word stride): 500 workgroups polling
+// one word took 5.9 us from the finisher's store to the last of them seeing it (1.0 at 126)
+constexpr int PP_NFLAG = 16, PP_FLAG_STRIDE = 64;
+constexpr int SYNC_FLAGR = SYNC_ALPHA + 256;
+constexpr int SYNC_WORDS = SYNC_FLAGR + PP_NFLAG * PP_FLAG_STRIDE + SYNC_LINE;
 __device__ bool last_block_sharded(uint32_t* sync, uint32_t epoch) {
     __shared__ int isLast;
     drain_stores();
@@ -253,8 +261,8 @@ __global__ __launch_bounds__(64) void k_tile_count(BA a) {
     const uint32_t t = blockIdx.x;
     for (uint32_t r = threadIdx.x; r < a.N; r += 64) hist[r] = 0;
     __syncthreads();
-    const uint32_t c1 = min((t + 1) * TILE, a.nCorr);
-    for (uint32_t c = t * TILE + threadIdx.x; c < c1; c += 64) {
+    const uint32_t c1 = min((t + 1) * a.tile, a.nCorr);
+    for (uint32_t c = t * a.tile + threadIdx.x; c < c1; c += 64) {
         uint32_t i, j;
         if (!corr_rows(a, c, i, j)) continue;
         atomicAdd(&hist[i], 1);
@@ -316,8 +324,8 @@ __global__ __launch_bounds__(64) void k_tile_fill(BA a) {
     for (uint32_t r = lane; r < a.N; r += 64) run[r] = 0;
     __syncthreads();
     const uint64_t lower = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t c1 = min((t + 1) * TILE, a.nCorr);
-    for (uint32_t c0 = t * TILE; c0 < c1; c0 += 64) {
+    const uint32_t c1 = min((t + 1) * a.tile, a.nCorr);
+    for (uint32_t c0 = t * a.tile; c0 < c1; c0 += 64) {
         const uint32_t c = c0 + lane;
         uint32_t i = BF_INVALID_IMAGE, j = BF_INVALID_IMAGE;
         const bool ok = c < c1 && corr_rows(a, c, i, j);
@@ -968,16 +976,18 @@ __device__ __forceinline__ void gran_store(uint2* g, float v, uint32_t tag) {
 __device__ __forceinline__ uint64_t gran_load(const uint2* g) {
     return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Waits until the granules g[i][0..5] (i < n, null rows skipped) all carry `tag`; every load of every
-// row is in flight at once, stale ones are reloaded after a short sleep. Returns 1, or -1 on timeout.
+// Waits until the granules g[i][0..5] (i < NR) all carry `tag`: every load of every row in flight at
+// once, and all of them reloaded after a short sleep while any is stale (no per-granule branches, so
+// the loaded values do not multiply into merge copies). Every pointer must be valid and written with
+// this tag (a lane without a row of its own polls a row that is). Returns 1, or -1 on timeout.
 template <int NR>
 __device__ __forceinline__ int gran_rows(const uint2* const* g, uint32_t tag, float out[][6], unsigned long long t0) {
     uint64_t x[NR][6];
-#pragma unroll
-    for (int r = 0; r < NR; r++)
-#pragma unroll
-        for (int q = 0; q < 6; q++) x[r][q] = g[r] ? gran_load(g[r] + q) : ((uint64_t)tag << 32);
     for (;;) {
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+#pragma unroll
+            for (int q = 0; q < 6; q++) x[r][q] = gran_load(g[r] + q);
         bool all = true;
 #pragma unroll
         for (int r = 0; r < NR; r++)
@@ -986,11 +996,6 @@ __device__ __forceinline__ int gran_rows(const uint2* const* g, uint32_t tag, fl
         if (all) break;
         if (pp_timed_out(t0)) return -1;
         __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (int r = 0; r < NR; r++)
-#pragma unroll
-            for (int q = 0; q < 6; q++)
-                if ((uint32_t)(x[r][q] >> 32) != tag) x[r][q] = gran_load(g[r] + q);
     }
 #pragma unroll
     for (int r = 0; r < NR; r++)
@@ -1037,6 +1042,7 @@ __device__ void pcg_dense_offdiag(const BA& a, uint32_t wave, uint32_t nw) {
 // latest phase-A end, the finisher's start and end (s_memrealtime, 100 MHz)
 __device__ unsigned long long g_pcgT[1024][4];
 __device__ unsigned long long g_pcgS[1024][6];  // the last-arriving workgroup's stage stamps (wave 0)
+__device__ unsigned long long g_pcgW[64][1024][2];  // k_pcg_persist: per iteration (< 64) and worker WG: flag seen, arrival
 #endif
 // PCG finisher (one workgroup): Kernel1b, Kernel2, the host early-out test, Kernel3
 template <int RB = 2>
@@ -1312,33 +1318,81 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
 #define BF_PCG_PERSISTENT 1  // 0: one k_pcg_pairs launch per PCG iteration (A/B builds)
 #endif
 constexpr int PP_CPL = 3;                 // cached entries per lane: rows up to 192 partner pairs stay in registers
+constexpr uint32_t PP_SHADOW = 256;       // the workgroup without rows (see the workers)
+constexpr int PP_OV = 4;                  // further entries per lane whose pair refs stay in registers (rows up to 448)
 constexpr uint32_t PP_DONE = 0x80000000u; // flag bit: the PCG loop ended (last iteration or timeout)
 constexpr uint32_t PP_ERR_TIMEOUT = 8u;   // K_ERROR bit 3
 
 // The finisher workgroup of k_pcg_persist: R image rows per thread (R = 2: up to 513 images, every
-// vector in registers; R = 8: up to 2 049, p and r in registers, delta and M read and written in
-// memory by the thread that owns the row, z recomputed from M r where it is needed again: the same
-// operations in the same order, so the result matches the per-launch finisher's bit for bit). The
+// vector in registers; R = 8: up to 2 049, p and r in registers, the preconditioner M in LDS (sM,
+// [6][8 WG] floats), delta read and written in memory by the thread that owns the row and z recomputed
+// from M r: the same operations in the same order, so the result matches the per-launch finisher's bit
+// for bit; the kernel stays within 256 VGPRs, i.e. two workgroups per CU for a 501-workgroup grid). The
 // dense term is taken by R = 2 only (the host routes larger dense steps to one launch per iteration).
+// The workers' gathers of p: two 16-B buffer loads per row with the sc1 (agent-coherent) cache policy
+// — the policy of the agent-scope atomic loads in vload_t<true>, at half the L2 requests (four 8-B
+// atomics per row). Tearing cannot matter: p is complete (drained, then flagged) before any gather.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p_rsrc(const BA& a) {
+    return __builtin_amdgcn_make_buffer_rsrc(a.vec + (size_t)V_P * a.maxN * 8, (short)0, (int)(a.maxN * 32u), 0x00020000);
+}
+__device__ __forceinline__ void pload_coh(__amdgpu_buffer_rsrc_t rs, uint32_t u, f3& r, f3& t) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, u * 32u, 0, 16);  // 16: sc1
+    const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, u * 32u + 16u, 0, 16);
+    r = mk3(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]));
+    t = mk3(__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]));
+}
+// the finisher's publication of p: 16-B write-through (sc1) stores, [r | 0][t | 0] (the
+// MI355X_MICROARCH.md hand-off table: 16-B sc1 stores ~ plain, 8-B ones 2.7x the time per byte)
+__device__ __forceinline__ void pstore_coh(__amdgpu_buffer_rsrc_t rs, uint32_t u, f3 r, f3 t) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const u4 x = {__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), 0u};
+    const u4 y = {__float_as_uint(t.x), __float_as_uint(t.y), __float_as_uint(t.z), 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, u * 32u, 0, 16);  // 16: sc1
+    __builtin_amdgcn_raw_buffer_store_b128(y, rs, u * 32u + 16u, 0, 16);
+}
+
+// Row q of this finisher thread, opaque to the compiler at every use: otherwise the addresses of all
+// R rows in all five vectors are hoisted out of the PCG loop and held in registers (R = 8: ~100 VGPRs).
+__device__ __forceinline__ uint32_t fin_row(int q) {
+    uint32_t v = 1 + threadIdx.x + q * WG;
+    asm volatile("" : "+v"(v));
+    return v;
+}
 template <int R>
-__device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int nLin, uint32_t tagBase, uint32_t* flag,
-                                     unsigned long long t0) {
+__device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useDense, int nLin, uint32_t tagBase,
+                                     uint32_t* flag, unsigned long long t0) {
     constexpr bool REGS = R <= 2;
+    constexpr int SMR = R * WG;  // sM row stride (R > 2)
     f3 pR[R], pT[R], rR[R], rT[R];
-    f3 dR[REGS ? R : 1], dT[REGS ? R : 1], mR[REGS ? R : 1], mT[REGS ? R : 1];
+    f3 mR[REGS ? R : 1], mT[REGS ? R : 1];
 #pragma unroll
     for (int q = 0; q < R; q++) {
-        const uint32_t v = 1 + threadIdx.x + q * WG;
+        const uint32_t v = fin_row(q);
         if (v < a.N) {
             vload(a, V_P, v, pR[q], pT[q]);
             vload(a, V_R, v, rR[q], rT[q]);
             if (REGS) {
-                vload(a, V_DELTA, v, dR[REGS ? q : 0], dT[REGS ? q : 0]);
                 vload(a, V_M, v, mR[REGS ? q : 0], mT[REGS ? q : 0]);
+            } else {
+                f3 mr, mt;
+                vload(a, V_M, v, mr, mt);
+                const int i = (int)threadIdx.x + q * WG;
+                sM[i] = mr.x; sM[SMR + i] = mr.y; sM[2 * SMR + i] = mr.z;
+                sM[3 * SMR + i] = mt.x; sM[4 * SMR + i] = mt.y; sM[5 * SMR + i] = mt.z;
             }
         }
     }
+    // M of row q (registers, or this thread's own LDS slots)
+    auto getM = [&](int q, f3& mr, f3& mt) {
+        if (REGS) { mr = mR[REGS ? q : 0]; mt = mT[REGS ? q : 0]; }
+        else {
+            const int i = (int)threadIdx.x + q * WG;
+            mr = mk3(sM[i], sM[SMR + i], sM[2 * SMR + i]);
+            mt = mk3(sM[3 * SMR + i], sM[4 * SMR + i], sM[5 * SMR + i]);
+        }
+    };
     float rz = ctrlf(a.ctrl, K_RDOTZ);
+    const __amdgpu_buffer_rsrc_t prs = p_rsrc(a);
     int it = 0;
     bool last = false;
     for (;; it++) {
@@ -1347,12 +1401,19 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int n
         const uint2* g[NG];
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            const uint32_t v = 1 + threadIdx.x + q * WG;
-            g[q] = v < a.N ? a.aGran + (size_t)v * 6 : nullptr;
-            if (REGS) g[(R + q) % NG] = v < a.N && useDense ? a.aGran + ((size_t)a.maxN + v) * 6 : nullptr;
+            const uint32_t v = fin_row(q);
+            const uint32_t vv = v < a.N ? v : 1u;  // image 1's granules: written every iteration (N >= 2)
+            g[q] = a.aGran + (size_t)vv * 6;
+            if (REGS) g[(R + q) % NG] = useDense ? a.aGran + ((size_t)a.maxN + vv) * 6 : g[q];
         }
         float x[NG][6];
-        const int ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0);
+        int ok;
+        if (REGS) ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0);
+        else {  // R = 8: two halves of four rows (half the in-flight registers)
+            constexpr int H = NG / 2 > 0 ? NG / 2 : 1;
+            ok = gran_rows<H>(g, tagBase + (uint32_t)it + 1u, x, t0);
+            if (ok > 0) ok = gran_rows<H>(g + H, tagBase + (uint32_t)it + 1u, x + H, t0);
+        }
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
 #endif
@@ -1360,7 +1421,7 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int n
         float d = 0.0f;
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            const uint32_t v = 1 + threadIdx.x + q * WG;
+            const uint32_t v = fin_row(q);
             if (v < a.N) {  // pcg_ap's order of additions; x[q] becomes Ap of the row
                 f3 aR = mk3(x[q][0], x[q][1], x[q][2]), aT = mk3(x[q][3], x[q][4], x[q][5]);
                 if (REGS && useDense) {  // diagonal block [trans | rot] x [pTrans | pRot], then the off-diagonal products
@@ -1383,20 +1444,21 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int n
             }
         }
         const float pAp = block_sum(d, sh);
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) g_pcgS[it & 1023][0] = rtc();
+#endif
         const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
+        // delta += alpha p is the workers' (each on its own row, from the p it gathered): alpha goes out
+        // with the flag
+        if (threadIdx.x == 0) st_wt(&a.sync[SYNC_ALPHA + it], __float_as_uint(alpha));
         float b = 0.0f;
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            const uint32_t v = 1 + threadIdx.x + q * WG;
+            const uint32_t v = fin_row(q);
             if (v < a.N) {
                 const f3 aR = mk3(x[q][0], x[q][1], x[q][2]), aT = mk3(x[q][3], x[q][4], x[q][5]);
-                f3 dr, dt, mr, mt;
-                if (REGS) { dr = dR[REGS ? q : 0]; dt = dT[REGS ? q : 0]; mr = mR[REGS ? q : 0]; mt = mT[REGS ? q : 0]; }
-                else { vload(a, V_DELTA, v, dr, dt); vload(a, V_M, v, mr, mt); }
-                dr = dr + alpha * pR[q];
-                dt = dt + alpha * pT[q];
-                if (REGS) { dR[REGS ? q : 0] = dr; dT[REGS ? q : 0] = dt; }
-                else vstore(a, V_DELTA, v, dr, dt);
+                f3 mr, mt;
+                getM(q, mr, mt);
                 rR[q] = rR[q] - alpha * aR;
                 rT[q] = rT[q] - alpha * aT;
                 const f3 zR = mul3(mr, rR[q]), zT = mul3(mt, rT[q]);
@@ -1404,49 +1466,45 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int n
             }
         }
         const float rzNew = block_sum(b, sh);
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) g_pcgS[it & 1023][1] = rtc();
+#endif
         last = (it == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
         const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            const uint32_t v = 1 + threadIdx.x + q * WG;
+            const uint32_t v = fin_row(q);
             if (v < a.N) {
                 f3 mr, mt;
-                if (REGS) { mr = mR[REGS ? q : 0]; mt = mT[REGS ? q : 0]; }
-                else vload(a, V_M, v, mr, mt);
+                getM(q, mr, mt);
                 const f3 zR = mul3(mr, rR[q]), zT = mul3(mt, rT[q]);
                 pR[q] = zR + beta * pR[q];
                 pT[q] = zT + beta * pT[q];
-                if (!last) vstore_t<true>(a, V_P, v, pR[q], pT[q]);  // the workers' next gathers
+                if (!last) pstore_coh(prs, v, pR[q], pT[q]);  // the workers' next gathers
             }
         }
         rz = rzNew;
         if (last) break;
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0) g_pcgS[it & 1023][2] = rtc();
+#endif
         // p is read by ~N x 92 gathers: published write-through, drained, then one flag word
         // (p as polled granules ran 20 % slower: the workers' polls swamp the hand-off)
         drain_stores();
         __syncthreads();
-        if (threadIdx.x == 0) st_wt(flag, (uint32_t)(it + 1));
+        if (threadIdx.x < PP_NFLAG) st_wt(flag + threadIdx.x * PP_FLAG_STRIDE, (uint32_t)(it + 1));  // one instruction
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) g_pcgT[it & 1023][3] = rtc();
 #endif
     }
-    // final state (later launches read it plainly across the kernel boundary)
+    // final state (later launches read it plainly across the kernel boundary); delta and the Lie
+    // update are the workers'
 #pragma unroll
     for (int q = 0; q < R; q++) {
-        const uint32_t v = 1 + threadIdx.x + q * WG;
+        const uint32_t v = fin_row(q);
         if (v < a.N) {
-            f3 dr, dt;
-            if (REGS) { dr = dR[REGS ? q : 0]; dt = dT[REGS ? q : 0]; vstore(a, V_DELTA, v, dr, dt); }
-            else vload(a, V_DELTA, v, dr, dt);
             vstore(a, V_R, v, rR[q], rT[q]);
             vstore(a, V_P, v, pR[q], pT[q]);
-            if (last) {  // computeLieUpdate (LieDerivUtil.h:301-307)
-                f3 nr, nt;
-                lie_update(dr, dt, mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
-                           mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
-                a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
-                a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
-            }
         }
     }
     if (threadIdx.x == 0) {
@@ -1454,38 +1512,55 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, int useDense, int n
         a.ctrl[K_RDOTZ] = __float_as_uint(rz);
         a.ctrl[K_PCG_ITERS] += (uint32_t)(it + (last ? 1 : 0));
         a.ctrl[K_PCG_DONE] = 1;
-        st_wt(flag, PP_DONE);  // releases the workers
+    }
+    if (threadIdx.x < 64) {  // wave 0: lane 0's alpha of the last iteration drained before the release
+        drain_stores();
+        if (threadIdx.x < PP_NFLAG)
+            st_wt(flag + threadIdx.x * PP_FLAG_STRIDE, PP_DONE | (uint32_t)(it + (last ? 1 : 0)));  // alphas written
     }
 }
 
 template <int R>
-__global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLin, uint32_t epoch) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_pcg_persist(BA a, float wSparse, int nLin, uint32_t epoch) {
     __shared__ float sh[WG];
+    __shared__ float sM[R > 2 ? 6 * R * WG : 1];  // the R = 8 finisher's preconditioner (48 KB)
+    __shared__ double sD[WG / 64][DSTAT];          // each worker wave's image statistics
     __shared__ uint32_t sFlag;
+    __shared__ float sAlpha;
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;  // uniform over the grid (set by earlier launches)
     const uint32_t lane = lane_id();
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     const unsigned long long t0 = rtc();
-    uint32_t* flag = &a.sync[SYNC_FLAG];
+    uint32_t* flag = &a.sync[SYNC_FLAGR];
     const uint32_t tagBase = epoch << 8;  // iteration it's Ap granules carry tagBase + it + 1
     if (blockIdx.x == 0) {
-        pcg_persist_finisher<R>(a, sh, useDense, nLin, tagBase, flag, t0);
+        pcg_persist_finisher<R>(a, sh, sM, useDense, nLin, tagBase, flag, t0);
         return;
     }
+    const uint32_t* myFlag = flag + (blockIdx.x % PP_NFLAG) * PP_FLAG_STRIDE;
     // ---- workers: one wave per row ----
-    const uint32_t v = 1 + (blockIdx.x - 1) * (WG / 64) + (threadIdx.x >> 6);
-    const bool hasRow = v < a.N;
+    // Workgroup PP_SHADOW is dispatched onto the finisher's CU (256 CUs, round-robin) and holds no rows:
+    // there, the finisher's granule polls held its rows' gathers up 2.4x (8 us of the 3.4 us others took)
+    const uint32_t wb = blockIdx.x < PP_SHADOW ? blockIdx.x : blockIdx.x - 1;
+    const uint32_t v = 1 + (wb - 1) * (WG / 64) + (threadIdx.x >> 6);
+    const bool hasRow = blockIdx.x != PP_SHADOW && v < a.N;
+    f3 dlR = mk3(0, 0, 0), dlT = dlR, pvR = dlR, pvT = dlR;  // the row's delta (every lane), the p it gathered
     int e0 = 0, e1 = 0;
-    int2 rp[PP_CPL];
+    int2 rp[PP_CPL], rq[PP_OV];
     double st[PP_CPL][16];
-    double dst[DSTAT];
+    double* dst = sD[threadIdx.x >> 6];
     if (hasRow) {
         e0 = a.rowPairStart[v];
         e1 = a.rowPairStart[v + 1];
 #pragma unroll
         for (int c = 0; c < PP_CPL; c++) {
             const int k = e0 + (int)lane + 64 * c;
-            rp[c] = k < e1 ? a.rowPair[k] : make_int2(0, 0);
+            rp[c] = k < e1 ? a.rowPair[k] : make_int2(0, (int)v);  // idle lanes gather the wave's own row, not one hot row 0
+        }
+#pragma unroll
+        for (int c = 0; c < PP_OV; c++) {
+            const int k = e0 + (int)lane + 64 * (PP_CPL + c);
+            rq[c] = k < e1 ? a.rowPair[k] : make_int2(0, (int)v);
         }
 #pragma unroll
         for (int c = 0; c < PP_CPL; c++) {
@@ -1497,18 +1572,20 @@ __global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLi
                 st[c][q + 1] = x.y;
             }
         }
-#pragma unroll
-        for (int q = 0; q < DSTAT; q++) dst[q] = a.dstat[(size_t)v * DSTAT + q];
+        if (lane < DSTAT) dst[lane] = a.dstat[(size_t)v * DSTAT + lane];
+        vload(a, V_DELTA, v, dlR, dlT);
     }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t prs = p_rsrc(a);
     for (uint32_t it = 0;; it++) {
         int state = 1;
         if (hasRow) {
             // p of iteration it (the previous launch's, or the finisher's write-through stores)
-            f3 pr[PP_CPL], pt[PP_CPL], pvR, pvT;
+            f3 pr[PP_CPL], pt[PP_CPL];
             const uint32_t tag = tagBase + it + 1u;
 #pragma unroll
-            for (int c = 0; c < PP_CPL; c++) vload_t<true>(a, V_P, (uint32_t)rp[c].y & ~PAIR_A_FLAG, pr[c], pt[c]);
-            vload_t<true>(a, V_P, v, pvR, pvT);
+            for (int c = 0; c < PP_CPL; c++) pload_coh(prs, (uint32_t)rp[c].y & ~PAIR_A_FLAG, pr[c], pt[c]);
+            pload_coh(prs, v, pvR, pvT);
             double o[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
             for (int c = 0; c < PP_CPL; c++) {
@@ -1521,13 +1598,27 @@ __global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLi
                     for (int q = 0; q < 6; q++) o[q] += bb[q];
                 }
             }
-            // entries beyond the cached ones (rows with more than PP_CPL x 64 partners), from memory
-            for (int k = e0 + (int)lane + 64 * PP_CPL; k < e1; k += 64) {
+            // entries beyond the cached ones (rows with more than PP_CPL x 64 partners): the next PP_OV
+            // per lane with their pair refs in registers (one dependent load round fewer), then from memory
+#pragma unroll
+            for (int c = 0; c < PP_OV; c++) {
+                if (e0 + (int)lane + 64 * (PP_CPL + c) >= e1) break;
+                const uint32_t u = (uint32_t)rq[c].y & ~PAIR_A_FLAG;
+                if (u == 0) continue;
+                f3 qr, qt;
+                pload_coh(prs, u, qr, qt);
+                const double w[3] = {qr.x, qr.y, qr.z}, t[3] = {qt.x, qt.y, qt.z};
+                double bb[6];
+                pair_block_apply(a.pstat + (size_t)rq[c].x * PSTAT, ((uint32_t)rq[c].y & PAIR_A_FLAG) != 0, w, t, bb);
+#pragma unroll
+                for (int q = 0; q < 6; q++) o[q] += bb[q];
+            }
+            for (int k = e0 + (int)lane + 64 * (PP_CPL + PP_OV); k < e1; k += 64) {
                 const int2 r2 = a.rowPair[k];
                 const uint32_t u = (uint32_t)r2.y & ~PAIR_A_FLAG;
                 if (u == 0) continue;
                 f3 qr, qt;
-                vload_t<true>(a, V_P, u, qr, qt);
+                pload_coh(prs, u, qr, qt);
                 const double w[3] = {qr.x, qr.y, qr.z}, t[3] = {qt.x, qt.y, qt.z};
                 double bb[6];
                 pair_block_apply(a.pstat + (size_t)r2.x * PSTAT, ((uint32_t)r2.y & PAIR_A_FLAG) != 0, w, t, bb);
@@ -1551,22 +1642,43 @@ __global__ __launch_bounds__(WG) void k_pcg_persist(BA a, float wSparse, int nLi
         }
         if (threadIdx.x == 0) {
 #ifdef BF_PCG_TIMING
-            atomicMax(&g_pcgT[it & 1023][1], rtc());
+            if (it < 64 && blockIdx.x < 1024) g_pcgW[it][blockIdx.x][1] = rtc();  // plain per-WG stamps: no fan-in
 #endif
             uint32_t f;
             for (;;) {
-                f = ld_wt(flag);
+                f = ld_wt(myFlag);
                 if ((f & PP_DONE) || f >= it + 1) break;
                 if (pp_timed_out(t0)) { f = PP_DONE; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
+            // alpha of this iteration, published before the flag (PP_DONE carries how many were)
+            if (!(f & PP_DONE) || (f & ~PP_DONE) > it) sAlpha = __uint_as_float(ld_wt(&a.sync[SYNC_ALPHA + it]));
             sFlag = f;
 #ifdef BF_PCG_TIMING
-            if (!(f & PP_DONE)) atomicMax(&g_pcgT[(it + 1) & 1023][0], rtc());  // the latest worker to see the flag
+            if (!(f & PP_DONE) && it + 1 < 64 && blockIdx.x < 1024) g_pcgW[it + 1][blockIdx.x][0] = rtc();
 #endif
         }
         __syncthreads();
-        if ((sFlag & PP_DONE) || __syncthreads_or(state < 1)) return;
+        const uint32_t f = sFlag;
+        const bool haveAlpha = !(f & PP_DONE) || (f & ~PP_DONE) > it;
+        if (hasRow && haveAlpha) {  // delta += alpha p (the finisher's order of operations)
+            const float alpha = sAlpha;
+            dlR = dlR + alpha * pvR;
+            dlT = dlT + alpha * pvT;
+        }
+        if ((f & PP_DONE) || __syncthreads_or(state < 1)) {
+            if (hasRow && lane == 0) {
+                vstore(a, V_DELTA, v, dlR, dlT);
+                if (haveAlpha && (f & PP_DONE)) {  // the PCG loop ended normally: computeLieUpdate (LieDerivUtil.h:301-307)
+                    f3 nr, nt;
+                    lie_update(dlR, dlT, mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
+                               mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]), nr, nt);
+                    a.rot[3 * v] = nr.x; a.rot[3 * v + 1] = nr.y; a.rot[3 * v + 2] = nr.z;
+                    a.trans[3 * v] = nt.x; a.trans[3 * v + 1] = nt.y; a.trans[3 * v + 2] = nt.z;
+                }
+            }
+            return;
+        }
     }
 }
 
@@ -2341,9 +2453,9 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     rowStart_.alloc(N + 1);
     rowLen_.alloc(N + 1);
     BF_REQUIRE(cfg.maxImages <= 16384, BF_ERR_CAPACITY, "maxImages > 16384 (LDS row histograms)");
-    maxTiles_ = div_up(cfg.maxCorr, TILE);
+    maxTiles_ = div_up(cfg.maxCorr, TILE);  // tiles at <= 256 images; tileCnt_ holds any n x div_up(nCorr, tile_for(n))
     maxChunks_ = div_up(2 * (size_t)cfg.maxCorr, (size_t)CH) + N;
-    tileCnt_.alloc((size_t)maxTiles_ * N + 1);
+    tileCnt_.alloc((size_t)maxTiles_ * std::min(N, 256u) + (size_t)cfg.maxCorr + N + TILE + 1);
     rowChunk_.alloc(N + 1);
     chunkRow_.alloc(maxChunks_ + 1);
     chunkPart_.alloc(3 * (size_t)maxChunks_ + 3);
@@ -2395,6 +2507,9 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP, k_pcg_persist<2>, WG, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP8, k_pcg_persist<8>, WG, 0));
     persistCapacity_ = (unsigned)std::max(std::min(occP, occP8), 0) * (unsigned)numCUs_;
+#ifdef BF_PCG_TIMING
+    fprintf(stderr, "k_pcg_persist occupancy: <2> %d, <8> %d workgroups per CU, %d CUs\n", occP, occP8, numCUs_);
+#endif
     BF_HIP(hipMemsetAsync(vec_.p, 0, vec_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
@@ -2448,7 +2563,7 @@ void Solver::solve(const SolveArgs& s) {
     a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p;
     a.pairFlag = pairFlag_.p; a.pairAcc = pairAcc_.p; a.pairProd = pairProd_.p; a.imgPairs = imgPairs_.p; a.imgPairN = imgPairN_.p;
     a.maxPairs = s.numImages * (s.numImages - 1) / 2;
-    a.tileCnt = tileCnt_.p; a.nTiles = div_up(s.numCorr, TILE);
+    a.tileCnt = tileCnt_.p; a.tile = tile_for(s.numImages); a.nTiles = div_up(s.numCorr, a.tile);
     a.rowChunk = rowChunk_.p; a.chunkRow = chunkRow_.p; a.chunkPart = chunkPart_.p; a.sync = sync_.p;
     a.cache = s.cache; a.cw = s.cacheW; a.ch = s.cacheH;
     a.fx = s.intrinsics[0]; a.fy = s.intrinsics[1]; a.mx = s.intrinsics[2]; a.my = s.intrinsics[3];
@@ -2543,13 +2658,14 @@ void Solver::solve(const SolveArgs& s) {
             if (s.numImages <= (uint32_t)SMALL_N) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
-                const unsigned persistGrid = 1u + div_up(s.numImages - 1u, (unsigned)(WG / 64));
+                unsigned persistGrid = 1u + div_up(s.numImages - 1u, (unsigned)(WG / 64));
+                if (persistGrid > PP_SHADOW) persistGrid++;  // the row-less workgroup on the finisher's CU
                 // one launch for the GN step's PCG loop when its grid is co-resident: up to 513 images
                 // (finisher rows in registers, dense term included) with room to spare, up to 2 049
                 // sparse-only (config 4's 2 001 keyframes) within the occupancy query's capacity
                 const bool small = s.numImages <= 2u * WG + 1u && persistGrid * 2u <= persistCapacity_;
                 const bool wide = !small && !dense && s.numImages <= 8u * WG + 1u && persistGrid <= persistCapacity_;
-                if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.nLin < 255u && (small || wide)) {
+                if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.nLin < 255u && s.numImages >= 2u && (small || wide)) {
 #ifdef BF_PCG_TIMING
                     {
                         std::vector<unsigned long long> z(1024 * 4, 0ull);
@@ -2566,6 +2682,53 @@ void Solver::solve(const SolveArgs& s) {
                         std::vector<unsigned long long> t(1024 * 4);
                         BF_HIP(hipMemcpyFromSymbolAsync(t.data(), HIP_SYMBOL(g_pcgT), t.size() * 8, 0, hipMemcpyDeviceToHost, stream_));
                         BF_HIP(hipStreamSynchronize(stream_));
+                        {   // per-WG stamps (iterations < 64): maxima into t[.][0..1]; spread and per-WG work time
+                            std::vector<unsigned long long> W(64 * 1024 * 2);
+                            BF_HIP(hipMemcpyFromSymbol(W.data(), HIP_SYMBOL(g_pcgW), W.size() * 8));
+                            double spreadSeen = 0, spreadArr = 0, meanWork = 0, maxWork = 0; int nq = 0;
+                            for (uint32_t q = 1; q < 63 && q + 2 < s.nLin; q++) {
+                                unsigned long long s0 = ~0ull, s1 = 0, a0 = ~0ull, a1 = 0; double wsum = 0, wmax = 0; int nw = 0, bmax = 0;
+                                for (uint32_t b = 1; b < persistGrid && b < 1024; b++) {
+                                    if (b == PP_SHADOW) continue;  // no rows
+                                    const unsigned long long fs = W[(q * 1024 + b) * 2], ar = W[(q * 1024 + b) * 2 + 1];
+                                    if (!fs || !ar) continue;
+                                    s0 = std::min(s0, fs); s1 = std::max(s1, fs); a0 = std::min(a0, ar); a1 = std::max(a1, ar);
+                                    if ((double)ar - (double)fs > wmax) bmax = (int)b;
+                                    wsum += (double)ar - (double)fs; wmax = std::max(wmax, (double)ar - (double)fs); nw++;
+                                }
+                                if (!nw) continue;
+                                if (q < 6) {  // the slowest workgroups of a few iterations
+                                    std::vector<std::pair<double, int>> v;
+                                    for (uint32_t b = 1; b < persistGrid && b < 1024; b++) {
+                                    if (b == PP_SHADOW) continue;  // no rows
+                                        const unsigned long long fs = W[(q * 1024 + b) * 2], ar = W[(q * 1024 + b) * 2 + 1];
+                                        if (fs && ar) v.push_back({((double)ar - (double)fs) / 100, (int)b});
+                                    }
+                                    std::sort(v.rbegin(), v.rend());
+                                    fprintf(stderr, "  iteration %u slowest WGs (us:block):", q);
+                                    for (size_t k = 0; k < v.size() && k < 8; k++) fprintf(stderr, " %.2f:%d", v[k].first, v[k].second);
+                                    fprintf(stderr, "\n");
+                                    std::vector<std::pair<double, int>> fsv;
+                                    for (uint32_t b = 1; b < persistGrid && b < 1024; b++) {
+                                    if (b == PP_SHADOW) continue;  // no rows
+                                        const unsigned long long fs = W[(q * 1024 + b) * 2];
+                                        if (fs) fsv.push_back({((double)fs - (double)s0) / 100, (int)b});
+                                    }
+                                    std::sort(fsv.rbegin(), fsv.rend());
+                                    fprintf(stderr, "  iteration %u latest flag-seen WGs (us after first:block):", q);
+                                    for (size_t k = 0; k < fsv.size() && k < 12; k++) fprintf(stderr, " %.2f:%d", fsv[k].first, fsv[k].second);
+                                    int late = 0;
+                                    for (auto& e : fsv) late += e.first > 2.0;
+                                    fprintf(stderr, "  (%d WGs > 2 us)\n", late);
+                                }
+                                (void)bmax;
+                                t[q * 4] = s1; t[q * 4 + 1] = a1;
+                                spreadSeen += (double)(s1 - s0); spreadArr += (double)(a1 - a0); meanWork += wsum / nw; maxWork += wmax; nq++;
+                            }
+                            for (uint32_t q = 64; q < 1024; q++) t[q * 4] = t[q * 4 + 1] = 0;
+                            if (nq) fprintf(stderr, "  workers (us, iterations 1-62): flag-seen spread %.2f  arrival spread %.2f  per-WG work mean %.2f  max %.2f\n",
+                                            spreadSeen / nq / 100, spreadArr / nq / 100, meanWork / nq / 100, maxWork / nq / 100);
+                        }
                         // per iteration q: [0] latest worker saw the flag of q, [1] latest worker arrival of q,
                         // [2] finisher saw all arrivals of q, [3] finisher published q + 1
                         double w = 0, ar = 0, fi = 0, bc = 0; int n = 0;
@@ -2578,6 +2741,27 @@ void Solver::solve(const SolveArgs& s) {
                         }
                         if (n) fprintf(stderr, "persistent pcg (us, mean over %d iterations): workers flag->arrive %.2f  arrival->finisher %.2f  finisher %.2f  flag->last worker %.2f  total %.2f\n",
                                        n, w / n / 100, ar / n / 100, fi / n / 100, bc / n / 100, (w + ar + fi + bc) / n / 100);
+                        std::vector<unsigned long long> g(1024 * 6);
+                        BF_HIP(hipMemcpyFromSymbol(g.data(), HIP_SYMBOL(g_pcgS), g.size() * 8));
+                        double f0 = 0, f1 = 0, f2 = 0, f3v = 0; int m = 0;
+                        for (uint32_t q = 1; q + 2 < s.nLin && q < 1023; q++) {
+                            const unsigned long long* r = &t[q * 4];
+                            const unsigned long long* G = &g[q * 6];
+                            if (!r[2] || !r[3] || !G[0] || !G[1] || !G[2]) continue;
+                            f0 += (double)G[0] - (double)r[2]; f1 += (double)G[1] - (double)G[0];
+                            f2 += (double)G[2] - (double)G[1]; f3v += (double)r[3] - (double)G[2]; m++;
+                        }
+                        if (m) fprintf(stderr, "  finisher (us): Ap + pAp sum %.2f  delta/r/z + rz sum %.2f  p + stores %.2f  drain + flag %.2f\n",
+                                       f0 / m / 100, f1 / m / 100, f2 / m / 100, f3v / m / 100);
+                        std::vector<int> rps(s.numImages + 1);
+                        BF_HIP(hipMemcpy(rps.data(), rowPairStart_.p, rps.size() * 4, hipMemcpyDeviceToHost));
+                        int dmax = 0, over192 = 0, over448 = 0;
+                        for (uint32_t q = 1; q < s.numImages; q++) {
+                            const int dg = rps[q + 1] - rps[q];
+                            dmax = std::max(dmax, dg); over192 += dg > 192; over448 += dg > 448;
+                        }
+                        fprintf(stderr, "  row degrees: mean %.1f  max %d  rows > 192: %d  > 448: %d\n",
+                                (double)(rps[s.numImages] - rps[1]) / (s.numImages - 1), dmax, over192, over448);
                     }
 #endif
                 } else if (s.numImages <= 2u * WG + 1u) {

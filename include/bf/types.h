@@ -135,7 +135,9 @@ typedef struct BFSolveResult {
     float energy;                /* sum_c w |r_c|^2 (EvalResidual) */
     uint32_t highResidualCount;  /* correspondences with max residual > verifyOptDistThresh */
     uint32_t numDensePairs;      /* overlapping image pairs found by the dense term (last GN iter) */
-    uint32_t error;              /* bit 1: a row exceeded the sort capacity */
+    uint32_t error;              /* bit 1: a row exceeded the sort capacity; bit 2: more image pairs than
+                                    the pair bound; bit 3: the persistent PCG launch timed out waiting
+                                    for a hand-off (2 s; the result is the last completed iteration) */
     uint32_t skipped;            /* the solve was gated off (an invalidated local submap's global solve) */
     uint32_t verifyUsed;         /* the last verification ran its dense pair check (useVerification) */
     uint32_t verifyOk;           /* ... and passed (VerifyTrajectoryCU's d_validOpt) */
