@@ -1417,7 +1417,6 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
 #endif
-        if (__syncthreads_and(ok > 0) == 0) break;  // timeout: released below
         float d = 0.0f;
 #pragma unroll
         for (int q = 0; q < R; q++) {
@@ -1443,7 +1442,20 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
                 d += dot3(pR[q], aR) + dot3(pT[q], aT);
             }
         }
-        const float pAp = block_sum(d, sh);
+        // pAp and the timeout vote in one reduction (block_sum's order; the vote rides in the same pass)
+        float pAp;
+        {
+            const float wsum = wave_sum(d);
+            const bool wok = __all(ok > 0);
+            if ((threadIdx.x & 63) == 0) { sh[threadIdx.x >> 6] = wsum; sh[WG / 64 + (threadIdx.x >> 6)] = wok ? 1.0f : 0.0f; }
+            __syncthreads();
+            float r = 0.0f;
+            bool all = true;
+            for (uint32_t w = 0; w < WG / 64; w++) { r += sh[w]; all = all && sh[WG / 64 + w] != 0.0f; }
+            // no trailing barrier: sh[0, 8) is rewritten next iteration, after every wave passed the rz barrier
+            if (!all) break;  // timeout: released below
+            pAp = r;
+        }
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) g_pcgS[it & 1023][0] = rtc();
 #endif
@@ -1465,7 +1477,15 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
                 b += dot3(zR, rR[q]) + dot3(zT, rT[q]);
             }
         }
-        const float rzNew = block_sum(b, sh);
+        float rzNew;
+        {   // block_sum's order in sh[16, 20): its next writer is behind the next iteration's pAp barrier
+            const float wsum = wave_sum(b);
+            if ((threadIdx.x & 63) == 0) sh[2 * (WG / 64) + (threadIdx.x >> 6)] = wsum;
+            __syncthreads();
+            float r = 0.0f;
+            for (uint32_t w = 0; w < WG / 64; w++) r += sh[2 * (WG / 64) + w];
+            rzNew = r;
+        }
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) g_pcgS[it & 1023][1] = rtc();
 #endif
@@ -1525,8 +1545,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
     __shared__ float sh[WG];
     __shared__ float sM[R > 2 ? 6 * R * WG : 1];  // the R = 8 finisher's preconditioner (48 KB)
     __shared__ double sD[WG / 64][DSTAT];          // each worker wave's image statistics
-    __shared__ uint32_t sFlag;
-    __shared__ float sAlpha;
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;  // uniform over the grid (set by earlier launches)
     const uint32_t lane = lane_id();
     const int useDense = (int)a.ctrl[K_USE_DENSE];
@@ -1537,7 +1555,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
         pcg_persist_finisher<R>(a, sh, sM, useDense, nLin, tagBase, flag, t0);
         return;
     }
-    const uint32_t* myFlag = flag + (blockIdx.x % PP_NFLAG) * PP_FLAG_STRIDE;
+    const uint32_t* myFlag = flag + ((blockIdx.x * (WG / 64) + (threadIdx.x >> 6)) % PP_NFLAG) * PP_FLAG_STRIDE;
     // ---- workers: one wave per row ----
     // Workgroup PP_SHADOW is dispatched onto the finisher's CU (256 CUs, round-robin) and holds no rows:
     // there, the finisher's granule polls held its rows' gathers up 2.4x (8 us of the 3.4 us others took)
@@ -1576,9 +1594,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
         vload(a, V_DELTA, v, dlR, dlT);
     }
     __syncthreads();
+    if (!hasRow) return;  // the row-less waves (the shadow workgroup, rows past N) have nothing to wait for
     const __amdgpu_buffer_rsrc_t prs = p_rsrc(a);
     for (uint32_t it = 0;; it++) {
-        int state = 1;
         if (hasRow) {
             // p of iteration it (the previous launch's, or the finisher's write-through stores)
             f3 pr[PP_CPL], pt[PP_CPL];
@@ -1640,33 +1658,28 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
             }
             if (useDense) pcg_dense_offdiag_row<true>(a, v, tag);
         }
-        if (threadIdx.x == 0) {
+        // every wave polls its own flag replica (no workgroup barrier per iteration): one load per poll
 #ifdef BF_PCG_TIMING
-            if (it < 64 && blockIdx.x < 1024) g_pcgW[it][blockIdx.x][1] = rtc();  // plain per-WG stamps: no fan-in
+        if (threadIdx.x == 0 && it < 64 && blockIdx.x < 1024) g_pcgW[it][blockIdx.x][1] = rtc();  // plain per-WG stamps
 #endif
-            uint32_t f;
-            for (;;) {
-                f = ld_wt(myFlag);
-                if ((f & PP_DONE) || f >= it + 1) break;
-                if (pp_timed_out(t0)) { f = PP_DONE; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            // alpha of this iteration, published before the flag (PP_DONE carries how many were)
-            if (!(f & PP_DONE) || (f & ~PP_DONE) > it) sAlpha = __uint_as_float(ld_wt(&a.sync[SYNC_ALPHA + it]));
-            sFlag = f;
-#ifdef BF_PCG_TIMING
-            if (!(f & PP_DONE) && it + 1 < 64 && blockIdx.x < 1024) g_pcgW[it + 1][blockIdx.x][0] = rtc();
-#endif
+        uint32_t f;
+        for (;;) {
+            f = __builtin_amdgcn_readfirstlane(ld_wt(myFlag));
+            if ((f & PP_DONE) || f >= it + 1) break;
+            if (pp_timed_out(t0)) { f = PP_DONE; break; }
+            __builtin_amdgcn_s_sleep(1);
         }
-        __syncthreads();
-        const uint32_t f = sFlag;
+#ifdef BF_PCG_TIMING
+        if (threadIdx.x == 0 && !(f & PP_DONE) && it + 1 < 64 && blockIdx.x < 1024) g_pcgW[it + 1][blockIdx.x][0] = rtc();
+#endif
+        // alpha of this iteration, published before the flag (PP_DONE carries how many were)
         const bool haveAlpha = !(f & PP_DONE) || (f & ~PP_DONE) > it;
         if (hasRow && haveAlpha) {  // delta += alpha p (the finisher's order of operations)
-            const float alpha = sAlpha;
+            const float alpha = __uint_as_float(__builtin_amdgcn_readfirstlane(ld_wt(&a.sync[SYNC_ALPHA + it])));
             dlR = dlR + alpha * pvR;
             dlT = dlT + alpha * pvT;
         }
-        if ((f & PP_DONE) || __syncthreads_or(state < 1)) {
+        if (f & PP_DONE) {
             if (hasRow && lane == 0) {
                 vstore(a, V_DELTA, v, dlR, dlT);
                 if (haveAlpha && (f & PP_DONE)) {  // the PCG loop ended normally: computeLieUpdate (LieDerivUtil.h:301-307)
