@@ -87,6 +87,7 @@ struct BA {
     // assembled normal equations (pair mode)
     int *rowSorted, *rowOther, *rowSeg, *rowDeg, *rowNA, *pairStart, *rowPairStart, *pairA, *pairB;
     int2 *pairCorr, *rowPair;
+    uint32_t entTail;  // float4 offset of k_pair_gather's float2 tail in entries (2 maxCorr + 1)
     double *pstat, *dstat;
     float *apPair, *rzPart;
     uint2* aGran;  // [2][maxN][6] {value bits, tag}: k_pcg_persist's Ap hand-off
@@ -580,6 +581,30 @@ __device__ void pair_segments(const BA& a, uint32_t v) {
 __global__ __launch_bounds__(64) void k_pair_fill(BA a) { pair_segments<true>(a, blockIdx.x); }
 __global__ __launch_bounds__(64) void k_pair_rows(BA a) { pair_segments<false>(a, blockIdx.x); }
 
+// once per solve (pair mode): each pair's correspondence points, oriented (a, b), copied into the
+// pair's run order — k_pair_stats then streams them contiguously on every GN iteration instead of
+// gathering 48-B EntryJ records through rowSorted three times (the entries buffer is free in pair mode)
+__global__ __launch_bounds__(WG) void k_pair_gather(BA a) {
+    if (a.ctrl[K_GN_DONE]) return;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t np = a.ctrl[K_NPAIRS_A];
+    float2* tail = reinterpret_cast<float2*>(a.entries + a.entTail);
+    for (uint32_t p = wave; p < np; p += nw) {
+        if (p % a.shardCount != a.shardIndex) continue;
+        const uint32_t pa = (uint32_t)a.pairA[p];
+        const int2 run = a.pairCorr[p];
+        for (int k = (int)lane; k < run.y; k += 64) {
+            const BFEntryJ e = a.corr[a.rowSorted[run.x + k]];
+            const bool aIsI = e.imgIdx_i == pa;
+            const f3 pA = aIsI ? mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z) : mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z);
+            const f3 pB = aIsI ? mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z) : mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z);
+            a.entries[run.x + k] = make_float4(pA.x, pA.y, pA.z, pB.x);
+            tail[run.x + k] = make_float2(pB.y, pB.z);
+        }
+    }
+}
+
 // per GN iteration: the sufficient statistics of every pair of this shard (one wave per pair,
 // lanes over its correspondences in ascending index order, fixed butterfly); pairs of other shards
 // and slots in [nPairs, pairBound) are written as zeros
@@ -601,11 +626,11 @@ __global__ __launch_bounds__(WG) void k_pair_stats(BA a) {
         const m4 Ta = loadm4(a.T + (size_t)pa * 16), Tb = loadm4(a.T + (size_t)pb * 16);
         double M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, sa[3] = {0, 0, 0}, sb[3] = {0, 0, 0}, cnt = 0.0;
         double qa[6] = {0, 0, 0, 0, 0, 0}, qb[6] = {0, 0, 0, 0, 0, 0};
+        const float2* tail = reinterpret_cast<const float2*>(a.entries + a.entTail);
         for (int k = (int)lane; k < run.y; k += 64) {
-            const BFEntryJ e = a.corr[a.rowSorted[run.x + k]];
-            const bool aIsI = e.imgIdx_i == pa;
-            const f3 pA = aIsI ? mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z) : mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z);
-            const f3 pB = aIsI ? mk3(e.pos_j.x, e.pos_j.y, e.pos_j.z) : mk3(e.pos_i.x, e.pos_i.y, e.pos_i.z);
+            const float4 x = a.entries[run.x + k];  // k_pair_gather's copy, contiguous per pair
+            const float2 y = tail[run.x + k];
+            const f3 pA = mk3(x.x, x.y, x.z), pB = mk3(x.w, y.x, y.y);
             const f3 A3 = xf(Ta, pA), B3 = xf(Tb, pB);  // the world points of k_entries
             const double A[3] = {A3.x, A3.y, A3.z}, B[3] = {B3.x, B3.y, B3.z};
 #pragma unroll
@@ -1408,7 +1433,8 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
         }
         float x[NG][6];
         int ok;
-        if (REGS) ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0);
+        if (REGS && useDense) ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0);
+        else if (REGS) ok = gran_rows<R>(g, tagBase + (uint32_t)it + 1u, x, t0);  // no dense granules to poll
         else {  // R = 8: two halves of four rows (half the in-flight registers)
             constexpr int H = NG / 2 > 0 ? NG / 2 : 1;
             ok = gran_rows<H>(g, tagBase + (uint32_t)it + 1u, x, t0);
@@ -2571,7 +2597,7 @@ void Solver::solve(const SolveArgs& s) {
     BA a{};
     a.corr = s.corr; a.nCorr = s.numCorr; a.valid = s.valid; a.N = s.numImages; a.maxN = cfg_.maxImages; a.cap = maxCorrPerImage_;
     a.rowCount = rowCount_.p; a.rowStart = rowStart_.p; a.rowLen = rowLen_.p; a.rowTmp = rowTmp_.p; a.rowIdx = rowIdx_.p;
-    a.entries = entries_.p; a.vec = vec_.p; a.img = img_.p; a.T = T_.p; a.Tinv = Tinv_.p; a.ctrl = ctrl_.p;
+    a.entries = entries_.p; a.entTail = 2u * cfg_.maxCorr + 1u; a.vec = vec_.p; a.img = img_.p; a.T = T_.p; a.Tinv = Tinv_.p; a.ctrl = ctrl_.p;
     a.part = part_.p; a.partIdx = partIdx_.p; a.rot = s.rot; a.trans = s.trans;
     a.pairs = pairs_.p; a.pairW = pairW_.p; a.pairBlk = pairBlk_.p; a.diag = diag_.p; a.jtr = jtr_.p;
     a.pairFlag = pairFlag_.p; a.pairAcc = pairAcc_.p; a.pairProd = pairProd_.p; a.imgPairs = imgPairs_.p; a.imgPairN = imgPairN_.p;
@@ -2647,6 +2673,7 @@ void Solver::solve(const SolveArgs& s) {
             a.pairBound = bound;
         }
     }
+    if (pairMode) k_pair_gather<<<(unsigned)numCUs_ * 4, WG, 0, stream_>>>(a);
     const unsigned pairRowGrid = std::max(1u, std::min(div_up(s.numImages, WG / 64), (unsigned)numCUs_ * 4));
     for (uint32_t it = 0; it < s.nNonLin; it++) {
         const float wS = s.wSparse[it];
