@@ -1,0 +1,6 @@
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+L=bundlefusion_amd; mkdir -p gpurun_out
+BF_HIP_LIB=$PWD/$L/libbf_hip_lazy.so timeout -k 10 600 python -u -m pytest tests/test_tsdf_gpu.py tests/test_recon_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r7d_lazy_tests.log 2>&1 || { tail -30 gpurun_out/r7d_lazy_tests.log; exit 1; }
+tail -1 gpurun_out/r7d_lazy_tests.log
+SKIP_TESTS=1 bash tools/gpu_abn.sh r7d "cur=$L/libbf_hip_cur.so skiphalf=$L/libbf_hip_skiphalf.so lazy=$L/libbf_hip_lazy.so cur=$L/libbf_hip_cur.so skiphalf=$L/libbf_hip_skiphalf.so lazy=$L/libbf_hip_lazy.so" --steps 20 --warmup 5 || exit 1
+bash tools/gpu_fetch_ab.sh r7d "cur=$L/libbf_hip_cur.so skiphalf=$L/libbf_hip_skiphalf.so lazy=$L/libbf_hip_lazy.so" --steps 20 --warmup 5
