@@ -924,6 +924,24 @@ __device__ __forceinline__ uint32_t blend_color(uint32_t c, uint32_t col, bool e
     return blend_channel(c & 0xFF, col & 0xFF, empty) | (blend_channel((c >> 8) & 0xFF, (col >> 8) & 0xFF, empty) << 8) |
            (blend_channel((c >> 16) & 0xFF, (col >> 16) & 0xFF, empty) << 16) | (255u << 24);
 }
+// blend_color with packed FP32 arithmetic (BF_BLEND_F, the batch pass): (cu + 4 oc) / 5 as (4 oc + cu)
+// x 0.2f (operands exact integers, product within 1e-5 of the quotient, whose fraction is a multiple of
+// 0.2), rounded by rintf (never a tie), min 254, and packed by v_cvt_pk_u8_f32 (an exact conversion of
+// an integral value). An empty voxel takes oc = cu, for which the quotient is cu. Same bytes as
+// blend_color for every (cu, oc, empty).
+#ifndef BF_BLEND_F
+#define BF_BLEND_F 0
+#endif
+__device__ __forceinline__ uint32_t blend_color_f(uint32_t c, uint32_t col, bool empty) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const uint32_t o = empty ? c : col;
+    const f2 cu = {(float)(c & 0xFF), (float)((c >> 8) & 0xFF)}, oc = {(float)(o & 0xFF), (float)((o >> 8) & 0xFF)};
+    const f2 t = __builtin_elementwise_fma(oc, f2{4.0f, 4.0f}, cu) * f2{0.2f, 0.2f};
+    const float t2 = __builtin_fmaf((float)((o >> 16) & 0xFF), 4.0f, (float)((c >> 16) & 0xFF)) * 0.2f;
+    uint32_t r = __builtin_amdgcn_cvt_pk_u8_f32(fminf(rintf(t.x), 254.0f), 0u, 0xFF000000u);
+    r = __builtin_amdgcn_cvt_pk_u8_f32(fminf(rintf(t.y), 254.0f), 1u, r);
+    return __builtin_amdgcn_cvt_pk_u8_f32(fminf(rintf(t2), 254.0f), 2u, r);
+}
 // Voxel update of integrateDepthMapKernel (CUDASceneRepHashSDF.cu:486-514), weightUpdate = 1.
 __device__ __forceinline__ void voxel_integrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
     const float wUpd = 1.0f;
@@ -1369,7 +1387,7 @@ __device__ __forceinline__ bool work_slot(const uint32_t* ctrl, WorkCursor& c, u
 // copies, for in-band voxels (sdf unclamped: see above). Weights are non-negative floats here, whose
 // bit patterns order like the values: min(1 + w, weightMax) is an integer min of the bits.
 __device__ __forceinline__ void batch_integrate(float& s0, float& w0, uint32_t& col, float sdf, uint32_t c, float weightMax) {
-    col = blend_color(c, col, w0 == 0.0f);
+    col = BF_BLEND_F ? blend_color_f(c, col, w0 == 0.0f) : blend_color(c, col, w0 == 0.0f);
     s0 = div_weight(sdf * 1.0f + s0 * w0, 1.0f + w0);
     w0 = __uint_as_float(min(__float_as_uint(1.0f + w0), __float_as_uint(weightMax)));
 }
