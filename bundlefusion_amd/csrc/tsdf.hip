@@ -924,13 +924,15 @@ __device__ __forceinline__ uint32_t blend_color(uint32_t c, uint32_t col, bool e
     return blend_channel(c & 0xFF, col & 0xFF, empty) | (blend_channel((c >> 8) & 0xFF, (col >> 8) & 0xFF, empty) << 8) |
            (blend_channel((c >> 16) & 0xFF, (col >> 16) & 0xFF, empty) << 16) | (255u << 24);
 }
-// blend_color with packed FP32 arithmetic (BF_BLEND_F, the batch pass): (cu + 4 oc) / 5 as (4 oc + cu)
+// blend_color with packed FP32 arithmetic (the batch pass; BF_BLEND_F=0 builds the integer form:
+// 4 VALU fewer per integrate update, k_apply_ops 619 / 618 -> 593 / 596 us, A/B pairs in
+// profiles/r5_apply_experiments.txt): (cu + 4 oc) / 5 as (4 oc + cu)
 // x 0.2f (operands exact integers, product within 1e-5 of the quotient, whose fraction is a multiple of
 // 0.2), rounded by rintf (never a tie), min 254, and packed by v_cvt_pk_u8_f32 (an exact conversion of
 // an integral value). An empty voxel takes oc = cu, for which the quotient is cu. Same bytes as
 // blend_color for every (cu, oc, empty).
 #ifndef BF_BLEND_F
-#define BF_BLEND_F 0
+#define BF_BLEND_F 1
 #endif
 __device__ __forceinline__ uint32_t blend_color_f(uint32_t c, uint32_t col, bool empty) {
     typedef float f2 __attribute__((ext_vector_type(2)));
