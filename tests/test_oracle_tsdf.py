@@ -204,6 +204,28 @@ def test_integer_colour_blend_is_exact():
     np.testing.assert_array_equal(ref, alt)
 
 
+def test_packed_float_colour_blend_is_exact():
+    """csrc/tsdf.hip blend_color_f (the batch pass's integrate colour): min(rint((4 oc + cu) * 0.2f), 254)
+    in float32 (4 oc + cu an exact integer, one rounded multiply, round-to-nearest-even; v_cvt_pk_u8_f32
+    then converts an integral value) equals the reference byte for all 65536 (cu, oc), and an empty voxel
+    (oc := cu) gives min(cu, 254) as the reference's new-colour branch clamped like blend_channel."""
+    import numpy as np
+    f32 = np.float32
+    cu = np.arange(256, dtype=f32)[:, None]
+    oc = np.arange(256, dtype=f32)[None, :]
+    r = (np.float32(0.2) * cu).astype(f32) + (np.float32(0.8) * oc).astype(f32)
+    t = np.trunc(r)
+    ref = np.minimum(np.maximum(t + ((r - t) >= f32(0.5)), 0), 254.5).astype(np.uint8)
+    a = (oc * f32(4.0) + cu).astype(f32)
+    q = (a * f32(0.2)).astype(f32)
+    assert q.dtype == f32
+    packed = np.minimum(np.rint(q), f32(254.0)).astype(np.uint8)
+    np.testing.assert_array_equal(packed, ref)
+    c1 = np.arange(256, dtype=f32)
+    empty = np.minimum(np.rint((c1 * f32(4.0) + c1).astype(f32) * f32(0.2)), f32(254.0)).astype(np.uint8)
+    np.testing.assert_array_equal(empty, np.minimum(np.arange(256), 254).astype(np.uint8))
+
+
 def test_deintegrate_colour_shortcut_is_exact():
     """csrc/tsdf.hip deint_channel: the de-integrate colour update u8(clamp(roundf((oc w - cu) / (w - 1)),
     0, 254.5)) (float32, CUDASceneRepHashSDF.cu:420-521) equals med3(oc + floor((2 (oc - cu) + d) * rcp(2 d)
