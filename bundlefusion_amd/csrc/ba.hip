@@ -1410,7 +1410,7 @@ __device__ __forceinline__ bool pload_tag(__amdgpu_buffer_rsrc_t rs, uint32_t u,
 __device__ __forceinline__ void pload_wait(const BA& a, __amdgpu_buffer_rsrc_t rs, uint32_t u, f3& r, f3& t, uint32_t tag, bool check,
                                            unsigned long long t0) {
     while (!pload_tag(rs, u, r, t, tag) && check) {
-        if (pp_timed_out(t0)) { atomicOr(&a.ctrl[K_ERROR], 8u); break; }
+        if (pp_timed_out(t0)) { atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT); break; }
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
                         ok = (pload_tag(prs, u, pr[c], pt[c], tag) || !chk || u == 0) && ok;
                     }
                     if (ok) break;
-                    if (pp_timed_out(t0)) { atomicOr(&a.ctrl[K_ERROR], 8u); break; }
+                    if (pp_timed_out(t0)) { atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT); break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
