@@ -38,6 +38,8 @@ def lib() -> C.CDLL:
         for name in abi.header_functions():
             fn = getattr(L, name)
             fn.restype = C.c_char_p if name == "bf_last_error" else C.c_int
+        if L.bf_abi_version() != abi.ABI_VERSION:
+            raise ImportError(f"{abi.LIB_PATH}: ABI version {L.bf_abi_version()}, the binding expects {abi.ABI_VERSION}")
         _lib = L
     return _lib
 

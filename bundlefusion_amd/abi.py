@@ -156,7 +156,11 @@ class BFSolverOptions(C.Structure):
                 ("denseColorGradientMin", C.c_float), ("denseDepthMin", C.c_float), ("denseDepthMax", C.c_float),
                 ("denseOverlapSubsample", C.c_uint32), ("verifyOptDistThresh", C.c_float),
                 ("normalEquations", C.c_int32), ("disableEarlyOut", C.c_int32),
-                ("pcgLaunch", C.c_int32)]
+                ("pcgLaunch", C.c_int32), ("pcgSpinLimitUs", C.c_uint32)]
+
+ABI_VERSION = 2  # include/bf/bf.h BF_ABI_VERSION: the struct layouts above
+SOLVE_ERR_PAIR_BOUND, SOLVE_ERR_PCG_TIMEOUT, SOLVE_PCG_RECOVERED = 4, 8, 16  # BFSolveResult.error bits
+SOLVE_ERR_FATAL = 0xFFFFFFFF & ~SOLVE_PCG_RECOVERED
 
 NORMAL_EQ_AUTO, NORMAL_EQ_MATRIX_FREE, NORMAL_EQ_ASSEMBLED = 0, 1, 2
 PAIR_STATS = 28  # doubles per image pair of the assembled normal equations (bf_solver_export_pairs)
@@ -276,4 +280,5 @@ class BFReconStats(C.Structure):
         "removedPairs", "integrateLaunches")] + [
         ("integrateKernelMs", C.c_double), ("localSolveMs", C.c_double), ("globalSolveMs", C.c_double),
         ("reintegrateLaunches", C.c_uint64), ("reintegrateKernelMs", C.c_double),
-        ("localVerifications", C.c_uint64), ("invalidLocals", C.c_uint64), ("endSolves", C.c_uint64)]
+        ("localVerifications", C.c_uint64), ("invalidLocals", C.c_uint64), ("endSolves", C.c_uint64),
+        ("pcgRecoveries", C.c_uint64)]

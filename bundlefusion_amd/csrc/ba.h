@@ -42,6 +42,7 @@ struct SolverConfig {
     int normalEquations;          // 0 auto (assembled for sparse-only solves), 1 matrix-free, 2 assembled
     bool earlyOut = true;         // the reference's ENABLE_EARLY_OUT build (SolverBundling.cu:7)
     int pcgLaunch = 0;            // 0 auto (persistent PCG launch when it fits), 1 one launch per iteration
+    uint32_t pcgSpinLimitUs = 0;  // bound of each persistent-PCG wait (0: 2 s); tests force the recovery path with it
 };
 
 struct SolveArgs {
@@ -175,7 +176,7 @@ private:
     DevBuf<int> rowSorted_, rowOther_, rowSeg_, rowDeg_, rowNA_, pairStart_, rowPairStart_, pairA_, pairB_;
     DevBuf<int2> pairCorr_, rowPair_;
     DevBuf<double> pstat_, dstat_;
-    DevBuf<float> apPair_, rzPart_;
+    DevBuf<float> apPair_, rzPart_, poseBak_;
     DevBuf<uint2> aGran_;           // k_pcg_persist: Ap rows as {value, tag} granules
     uint32_t pcgEpoch_ = 0;          // tag base of the next persistent launch
 };

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 namespace bf {
@@ -42,6 +43,7 @@ enum CtrlWord {
     K_VERIFY_OK,    // VerifyTrajectoryCU's d_validOpt (1 unless a pair failed)
     K_COUNT,
     K_NCHUNK = K_COUNT, K_NPAIRS_A,
+    K_PCG_ITERS0,  // K_PCG_ITERS before the GN step's PCG (k_pair_init): k_pcg_recover restarts from it
     K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
 };
 static_assert(K_COUNT == Solver::kResultWords, "result words");
@@ -93,6 +95,8 @@ struct BA {
     uint2* aGran;  // [2][maxN][6] {value bits, tag}: k_pcg_persist's Ap hand-off
     uint32_t pairMode, shardCount, shardIndex, pairBound;
     uint32_t earlyOut;  // ENABLE_EARLY_OUT (SolverBundling.cu:7): PCG |p.Ap| < 5e-7 and GN max|delta| < 0.005 exits
+    float* poseBak;     // [maxN][6] rot | trans at the GN step's start (k_pair_init), for k_pcg_recover
+    unsigned long long spinTicks;  // bound of every k_pcg_persist wait (s_memrealtime ticks, 100 MHz)
 };
 
 __device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -992,8 +996,8 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
 // per output row); group g takes the list entries g, g + 10, ...; the groups' partial sums are then
 // added in group order, so the sum is the same on every run. Stored write-through for the finisher.
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
-constexpr unsigned long long PP_SPIN_TICKS = 200000000ull;  // 2 s at 100 MHz
-__device__ __forceinline__ bool pp_timed_out(unsigned long long t0) { return rtc() - t0 > PP_SPIN_TICKS; }
+constexpr unsigned long long PP_SPIN_TICKS = 200000000ull;  // 2 s at 100 MHz (BFSolverOptions.pcgSpinLimitUs = 0)
+__device__ __forceinline__ bool pp_timed_out(unsigned long long t0, unsigned long long lim) { return rtc() - t0 > lim; }
 // Data-tagged granules for k_pcg_persist's Ap hand-off (MI355X_MICROARCH.md's handoff-1to1 row): one
 // 8-B {value, tag} per float, written by ONE 8-B agent-scope atomic store and read by 8-B agent-scope
 // atomic loads, so a granule is never torn and its tag says which iteration wrote it; the consumer
@@ -1012,7 +1016,8 @@ __device__ __forceinline__ uint64_t gran_load(const uint2* g) {
 // the loaded values do not multiply into merge copies). Every pointer must be valid and written with
 // this tag (a lane without a row of its own polls a row that is). Returns 1, or -1 on timeout.
 template <int NR>
-__device__ __forceinline__ int gran_rows(const uint2* const* g, uint32_t tag, float out[][6], unsigned long long t0) {
+__device__ __forceinline__ int gran_rows(const uint2* const* g, uint32_t tag, float out[][6], unsigned long long t0,
+                                         unsigned long long lim) {
     uint64_t x[NR][6];
     for (;;) {
 #pragma unroll
@@ -1025,7 +1030,7 @@ __device__ __forceinline__ int gran_rows(const uint2* const* g, uint32_t tag, fl
 #pragma unroll
             for (int q = 0; q < 6; q++) all = all && (uint32_t)(x[r][q] >> 32) == tag;
         if (all) break;
-        if (pp_timed_out(t0)) return -1;
+        if (pp_timed_out(t0, lim)) return -1;
         __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
@@ -1166,12 +1171,11 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
 // pairs (in partner order) into D_v (the diagonal block statistics), J^T F and the Jacobi
 // preconditioner, then initialises the row as PCGInit does (evalMinusJTFDevice + PCGInit_Kernel1,
 // SolverBundlingEquationsLie.h:63-148, SolverBundling.cu:755-794); the last workgroup sums r.z.
-__global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
-    __shared__ float sh[WG];
-    if (a.ctrl[K_GN_DONE]) return;
+// Row v (one wave); lane 0 also keeps the row's pose as it was before the GN step (a.poseBak, the
+// state k_pcg_recover restarts from)
+__device__ void pair_init_row(const BA& a, float wSparse, uint32_t v, bool backup) {
     const uint32_t lane = lane_id();
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+    {
         const int e0 = a.rowPairStart[v], e1 = a.rowPairStart[v + 1];
         double d[DSTAT + 6];
 #pragma unroll
@@ -1208,8 +1212,11 @@ __global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
             const f3 pr = mk3((float)(d[3] + d[5]), (float)(d[0] + d[5]), (float)(d[0] + d[3]));
             st_wt(&a.rzPart[v], init_row_cnt(a, v, rr, rt, pr, (float)d[9], wSparse, (int)a.ctrl[K_USE_DENSE]));
         }
+        if (backup && lane < 6) a.poseBak[(size_t)v * 6 + lane] = lane < 3 ? a.rot[3 * v + lane] : a.trans[3 * v + lane - 3];
     }
-    if (!last_block(&a.ctrl[K_TICKET])) return;
+}
+// r.z summed over the rows by one workgroup (k_pair_init's last), PCG counters reset, p_0 = 0
+__device__ void pair_init_finish(const BA& a, float* sh) {
     float s = 0.0f;
     for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) s += ld_wtf(&a.rzPart[v]);
     s = block_sum(s, sh);
@@ -1220,23 +1227,21 @@ __global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
         vstore(a, V_P, 0, mk3(0, 0, 0), mk3(0, 0, 0));  // image 0 is fixed: its p stays 0
     }
 }
-
-// Pair mode PCG iteration: one wave per row v >= 1, Ap_v = w (D_v p_v - sum_u B_vu p_u) in fp64 over
-// the row's pairs (the same operator as applyJ / applyJT; no second w, SolverBundlingEquationsLie.h:
-// 154-228), handed to the finisher write-through; then the finisher of k_pcg.
-// RB: image rows per finisher thread held in registers (2: up to 513 images; 8: up to 2 049, the
-// host picks it from the solve's image count; beyond, the finisher's multi-pass form)
-template <int RB>
-__global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter, int nLin) {
+__global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
     __shared__ float sh[WG];
-    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
-#ifdef BF_PCG_TIMING
-    const unsigned long long tStart = rtc();
-    unsigned long long stg[3] = {0, 0, 0};
-#endif
-    const uint32_t lane = lane_id();
+    if (a.ctrl[K_GN_DONE]) return;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) pair_init_row(a, wSparse, v, true);
+    if (!last_block(&a.ctrl[K_TICKET])) return;
+    if (threadIdx.x == 0) a.ctrl[K_PCG_ITERS0] = a.ctrl[K_PCG_ITERS];
+    pair_init_finish(a, sh);
+}
+
+// Ap of row v (one wave), handed to the finisher write-through: k_pcg_pairs and k_pcg_recover
+__device__ void pair_row_ap(const BA& a, float wSparse, uint32_t v, unsigned long long* stg) {
+    const uint32_t lane = lane_id();
+    (void)stg;
+    {
         const int e0 = a.rowPairStart[v], e1 = a.rowPairStart[v + 1];
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); stg[0] = rtc() + (unsigned long long)(e0 & 0); }
@@ -1300,6 +1305,30 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
             st_wt(q + 1, make_float4((float)(ws * (dp[3] - o[3])), (float)(ws * (dp[4] - o[4])), (float)(ws * (dp[5] - o[5])), 0.0f));
         }
     }
+}
+
+// Pair mode PCG iteration: one wave per row v >= 1, Ap_v = w (D_v p_v - sum_u B_vu p_u) in fp64 over
+// the row's pairs (the same operator as applyJ / applyJT; no second w, SolverBundlingEquationsLie.h:
+// 154-228), handed to the finisher write-through; then the finisher of k_pcg.
+// RB: image rows per finisher thread held in registers (2: up to 513 images; 8: up to 2 049, the
+// host picks it from the solve's image count; beyond, the finisher's multi-pass form)
+template <int RB>
+__global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter, int nLin) {
+    __shared__ float sh[WG];
+    if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
+#ifdef BF_PCG_TIMING
+    const unsigned long long tStart = rtc();
+    unsigned long long stg[3] = {0, 0, 0};
+#endif
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) {
+#ifdef BF_PCG_TIMING
+        pair_row_ap(a, wSparse, v, stg);
+#else
+        pair_row_ap(a, wSparse, v, nullptr);
+#endif
+    }
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     if (useDense) pcg_dense_offdiag(a, wave, nw);
 #ifdef BF_PCG_TIMING
@@ -1352,7 +1381,8 @@ constexpr int PP_CPL = 3;                 // cached entries per lane: rows up to
 constexpr uint32_t PP_SHADOW = 256;       // the workgroup without rows (see the workers)
 constexpr int PP_OV = 4;                  // further entries per lane whose pair refs stay in registers (rows up to 448)
 constexpr uint32_t PP_DONE = 0x80000000u; // flag bit: the PCG loop ended (last iteration or timeout)
-constexpr uint32_t PP_ERR_TIMEOUT = 8u;   // K_ERROR bit 3
+constexpr uint32_t PP_ERR_TIMEOUT = 8u;   // K_ERROR bit 3 (BF_SOLVE_ERR_PCG_TIMEOUT)
+constexpr uint32_t PP_RECOVERED = 16u;    // K_ERROR bit 4 (BF_SOLVE_PCG_RECOVERED): k_pcg_recover redid the step
 
 // The finisher workgroup of k_pcg_persist: R image rows per thread (R = 2: up to 513 images, every
 // vector in registers; R = 8: up to 2 049, p and r in registers, the preconditioner M in LDS (sM,
@@ -1410,7 +1440,7 @@ __device__ __forceinline__ bool pload_tag(__amdgpu_buffer_rsrc_t rs, uint32_t u,
 __device__ __forceinline__ void pload_wait(const BA& a, __amdgpu_buffer_rsrc_t rs, uint32_t u, f3& r, f3& t, uint32_t tag, bool check,
                                            unsigned long long t0) {
     while (!pload_tag(rs, u, r, t, tag) && check) {
-        if (pp_timed_out(t0)) { atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT); break; }
+        if (pp_timed_out(t0, a.spinTicks)) { atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT); break; }
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -1472,12 +1502,12 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
         }
         float x[NG][6];
         int ok;
-        if (REGS && useDense) ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0);
-        else if (REGS) ok = gran_rows<R>(g, tagBase + (uint32_t)it + 1u, x, t0);  // no dense granules to poll
+        if (REGS && useDense) ok = gran_rows<NG>(g, tagBase + (uint32_t)it + 1u, x, t0, a.spinTicks);
+        else if (REGS) ok = gran_rows<R>(g, tagBase + (uint32_t)it + 1u, x, t0, a.spinTicks);  // no dense granules to poll
         else {  // R = 8: two halves of four rows (half the in-flight registers)
             constexpr int H = NG / 2 > 0 ? NG / 2 : 1;
-            ok = gran_rows<H>(g, tagBase + (uint32_t)it + 1u, x, t0);
-            if (ok > 0) ok = gran_rows<H>(g + H, tagBase + (uint32_t)it + 1u, x + H, t0);
+            ok = gran_rows<H>(g, tagBase + (uint32_t)it + 1u, x, t0, a.spinTicks);
+            if (ok > 0) ok = gran_rows<H>(g + H, tagBase + (uint32_t)it + 1u, x + H, t0, a.spinTicks);
         }
 #ifdef BF_PCG_TIMING
         if (threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
@@ -1684,7 +1714,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
                         ok = (pload_tag(prs, u, pr[c], pt[c], tag) || !chk || u == 0) && ok;
                     }
                     if (ok) break;
-                    if (pp_timed_out(t0)) { atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT); break; }
+                    if (pp_timed_out(t0, a.spinTicks)) { atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT); break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
@@ -1765,7 +1795,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
             f = __builtin_amdgcn_readfirstlane((uint32_t)fw);
             fa = __builtin_amdgcn_readfirstlane((uint32_t)(fw >> 32));
             if ((f & PP_DONE) || f >= it + 1) break;
-            if (pp_timed_out(t0)) { f = PP_DONE; break; }
+            if (pp_timed_out(t0, a.spinTicks)) { f = PP_DONE; break; }
             __builtin_amdgcn_s_sleep(1);
         }
 #ifdef BF_PCG_TIMING
@@ -1793,6 +1823,52 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
             return;
         }
     }
+}
+
+// After every k_pcg_persist launch, in stream order (one workgroup, returns at once unless the launch
+// timed out): a persistent launch that timed out (a hand-off never arrived, e.g. the grid was not
+// co-resident) redoes the GN step's PCG here, from the state k_pair_init left: the poses it saved are
+// restored (the timed-out launch may have applied a partial Lie update), the rows are initialised
+// again, and every PCG iteration runs as k_pcg_pairs<RB> + its finisher would, in one workgroup (the
+// row order of the per-row work does not enter any sum, and the finisher is the same code), so the
+// step's result is bit-identical to BFSolverOptions.pcgLaunch = 1. Bit 3 of the result's error word is
+// then cleared and bit 4 set: the solve's result is valid and says that it took this path.
+template <int RB>
+__global__ __launch_bounds__(WG) void k_pcg_recover(BA a, float wSparse, int nLin) {
+    __shared__ float sh[WG];
+    if (!(a.ctrl[K_ERROR] & PP_ERR_TIMEOUT)) return;  // uniform
+    const uint32_t wave = threadIdx.x >> 6, nw = WG / 64;
+    for (uint32_t v = 1 + threadIdx.x; v < a.N; v += WG) {
+        const float* b = a.poseBak + (size_t)v * 6;
+        a.rot[3 * v] = b[0]; a.rot[3 * v + 1] = b[1]; a.rot[3 * v + 2] = b[2];
+        a.trans[3 * v] = b[3]; a.trans[3 * v + 1] = b[4]; a.trans[3 * v + 2] = b[5];
+    }
+    __syncthreads();
+    for (uint32_t v = 1 + wave; v < a.N; v += nw) pair_init_row(a, wSparse, v, false);
+    __syncthreads();
+    pair_init_finish(a, sh);
+    if (threadIdx.x == 0) {
+        a.ctrl[K_PCG_DONE] = 0;
+        a.ctrl[K_PCG_ITERS] = a.ctrl[K_PCG_ITERS0];
+    }
+    __syncthreads();
+    const int useDense = (int)a.ctrl[K_USE_DENSE];
+    for (int iter = 0; iter < nLin; iter++) {
+        for (uint32_t v = 1 + wave; v < a.N; v += nw) pair_row_ap(a, wSparse, v, nullptr);
+        if (useDense) pcg_dense_offdiag(a, wave, nw);
+        __syncthreads();
+        float rDotzNew;
+        bool last;
+        pcg_finisher<RB>(a, sh, 0u, useDense, iter, nLin, rDotzNew, last);
+        if (threadIdx.x == 0) {
+            a.ctrl[K_RDOTZ] = __float_as_uint(rDotzNew);
+            a.ctrl[K_PCG_ITERS]++;
+            if (last) a.ctrl[K_PCG_DONE] = 1;
+        }
+        __syncthreads();
+        if (last) break;  // uniform: from block sums
+    }
+    if (threadIdx.x == 0) a.ctrl[K_ERROR] = (a.ctrl[K_ERROR] & ~PP_ERR_TIMEOUT) | PP_RECOVERED;
 }
 
 // Small solves (N <= 64 images: the 11-frame local submaps, early global solves): every PCG
@@ -2319,7 +2395,7 @@ __global__ __launch_bounds__(WG) void k_residuals(BA a) {
 __global__ void k_solve_begin(uint32_t* ctrl, const int* gate) {
     const uint32_t off = (gate && *gate == 0) ? 1u : 0u;
     const uint32_t t = threadIdx.x;
-    if (t < K_COUNT && t != K_ERROR)
+    if (t < K_COUNT)  // the error word too: every solve reports its own
         ctrl[t] = (t == K_RM_I || t == K_RM_J) ? BF_INVALID_IMAGE : (t == K_GN_DONE || t == K_SKIPPED) ? off : 0u;
 }
 
@@ -2520,6 +2596,19 @@ __global__ void k_check_frames_if_removed(const uint32_t* ctrl, const int* numEn
     if (t < numImages && numEntries[t] == 0) valid[t] = 0;
 }
 
+// one per device: orders the persistent PCG launches of all solvers on it (Solver::solve)
+struct PersistGate {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+    hipStream_t stream = nullptr;
+};
+PersistGate& persist_gate() {
+    static PersistGate gates[64];
+    int dev = 0;
+    BF_HIP(hipGetDevice(&dev));
+    return gates[dev & 63];
+}
+
 }  // namespace
 
 // zParametersBundlingDefault.txt defaults for every option left 0
@@ -2538,6 +2627,7 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.normalEquations = o ? o->normalEquations : 0;
     cfg.earlyOut = !(o && o->disableEarlyOut);
     cfg.pcgLaunch = o ? o->pcgLaunch : 0;
+    cfg.pcgSpinLimitUs = o ? o->pcgSpinLimitUs : 0u;
     return cfg;
 }
 
@@ -2611,6 +2701,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     apPair_.alloc((size_t)N * 8);
     aGran_.alloc((size_t)N * 12);  // [2][N][6]: sparse Ap rows, then the dense off-diagonal products
     rzPart_.alloc(N);
+    poseBak_.alloc((size_t)N * 6);
     int dev = 0;
     hipDeviceProp_t prop;
     BF_HIP(hipGetDevice(&dev));
@@ -2691,6 +2782,8 @@ void Solver::solve(const SolveArgs& s) {
     a.aGran = aGran_.p;
     a.shardCount = shardCount_; a.shardIndex = shardIndex_; a.pairBound = 0;
     a.earlyOut = cfg_.earlyOut ? 1u : 0u;
+    a.poseBak = poseBak_.p;
+    a.spinTicks = cfg_.pcgSpinLimitUs ? 100ull * cfg_.pcgSpinLimitUs : PP_SPIN_TICKS;
     // assembled normal equations for sparse-only solves (auto) unless the matrix-free path is forced
     bool denseAny = false;
     for (uint32_t it = 0; it < s.nNonLin && s.cache; it++)
@@ -2787,9 +2880,20 @@ void Solver::solve(const SolveArgs& s) {
                     }
 #endif
                     if (s.nLin) {
+                        // persistent launches of every solver on this device run one at a time: two
+                        // partly resident persistent grids could each wait on the other's workgroups
+                        PersistGate& pg = persist_gate();
+                        std::lock_guard<std::mutex> lk(pg.mu);
+                        if (pg.ev && pg.stream != stream_) BF_HIP(hipStreamWaitEvent(stream_, pg.ev, 0));
                         if (small) k_pcg_persist<2><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
                         else k_pcg_persist<8><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
+                        if (!pg.ev) BF_HIP(hipEventCreateWithFlags(&pg.ev, hipEventDisableTiming));
+                        BF_HIP(hipEventRecord(pg.ev, stream_));
+                        pg.stream = stream_;
                         pcgEpoch_ = (pcgEpoch_ + 1) & 0xFFFFFFu;
+                        // a launch that timed out is redone in one workgroup (no-op otherwise)
+                        if (s.numImages <= 2u * WG + 1u) k_pcg_recover<2><<<1, WG, 0, stream_>>>(a, wS, (int)s.nLin);
+                        else k_pcg_recover<8><<<1, WG, 0, stream_>>>(a, wS, (int)s.nLin);
                     }
 #ifdef BF_PCG_TIMING
                     {

@@ -1,6 +1,7 @@
 // io.cpp — `.sens` reader / writer and `zParameters*.txt` parser (see io.h).
 #include "io.h"
 
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -239,7 +240,12 @@ void sens_save_with_trajectory(const std::string& in, const std::string& out, co
         offsets.resize(r.info().numFrames);
         for (uint64_t i = 0; i < offsets.size(); i++) offsets[i] = r.poseOffset(i);
     }
-    if (out != in) {
+    // the same file under another spelling (./a.sens, a symlink, a hard link) is patched in place: a
+    // copy would truncate the input before reading it
+    struct stat si{}, so{};
+    const bool same = out == in || (::stat(in.c_str(), &si) == 0 && ::stat(out.c_str(), &so) == 0 && si.st_dev == so.st_dev &&
+                                    si.st_ino == so.st_ino);
+    if (!same) {
         FILE* src = std::fopen(in.c_str(), "rb");
         BF_REQUIRE(src != nullptr, BF_ERR_IO, "cannot open " + in);
         FILE* dst = std::fopen(out.c_str(), "wb");

@@ -726,6 +726,16 @@ void Recon::applyPending(bool block) {
 // updateTrajectoryCU (OnlineBundler.cu:73-110) + TrajectoryManager::updateOptimizedTransform
 void Recon::apply(Pending& P) {
     const uint32_t S = opt_.submapSize, s = P.submap, n = P.numLocal, nk = P.numKeyframes;
+    // a solve whose result is not a valid solve is never consumed: the loop fails instead (a timed-out
+    // persistent PCG launch is redone on the device and flagged BF_SOLVE_PCG_RECOVERED, which is valid)
+    for (int which = 0; which < 2; which++) {
+        if (!(which ? P.globalSolved : P.localSolved)) continue;
+        const SolveResult r = Solver::decodeResult(P.ctrl + (which ? Solver::kResultWords : 0));
+        BF_REQUIRE(!(r.error & BF_SOLVE_ERR_FATAL), BF_ERR_INTERNAL,
+                   which ? "global solve failed (BFSolveResult.error has a BF_SOLVE_ERR_FATAL bit)"
+                         : "local solve failed (BFSolveResult.error has a BF_SOLVE_ERR_FATAL bit)");
+        if (r.error & BF_SOLVE_PCG_RECOVERED) st_.pcgRecoveries++;
+    }
     const bool localOk = *P.gate != 0;
     std::vector<BFMat4>& traj = localTraj_[s];
     if (!P.endSolve) {
@@ -841,6 +851,10 @@ void Recon::storeCacheFrame(uint32_t f) {
     const float* d = fr.srcDepth ? fr.srcDepth : fr.depth;
     const uint8_t* c = fr.srcDepth ? fr.srcColor : fr.color;
     const uint32_t w = fr.srcDepth ? fr.srcW : cam_.imageWidth, h = fr.srcDepth ? fr.srcH : cam_.imageHeight;
+    // k_cache_geometry reads the depth as the cache's input size: without a frame source the frame
+    // store's integration-size depth must be that size
+    BF_REQUIRE(fr.srcDepth || (cache_->config().inputWidth == cam_.imageWidth && cache_->config().inputHeight == cam_.imageHeight),
+               BF_ERR_ARG, "the attached cache's input size differs from the integration size: set a frame source (bf_recon_set_frame_source)");
     cache_->storeFrame(d, c, w, h);
     fr.cache = cache_->frame(f);
     BF_HIP(hipEventRecord(cacheEv_, cache_->stream()));
@@ -889,7 +903,7 @@ BFEndSequenceResult Recon::endSequence(const BFEndSequenceOptions& o) {
         }
         reintegrate();
         // exit check (DepthSensing.cpp:1116-1123) once the solves are done
-        if (N < 0 || (int64_t)p >= (int64_t)N) {
+        if (N >= 0 && (int64_t)p >= (int64_t)N) {  // N < 0 (the reference's -1) never exits: maxPastEndFrames bounds it
             tm_->generateUpdateLists();
             const uint32_t active = tm_->numActiveOperations();
             traceQueue(3, 0, active, nullptr, nullptr);

@@ -19,14 +19,16 @@ class SolverBundling:
     """CUDASolverBundling over bf_solver_* (all buffers device-resident)."""
 
     def __init__(self, max_images: int, max_corr: int, opts: BFSolverOptions | None = None,
-                 normal_equations: int | None = None, early_out: bool = True, pcg_launch: int = 0):
-        if normal_equations is not None or not early_out or pcg_launch:
+                 normal_equations: int | None = None, early_out: bool = True, pcg_launch: int = 0,
+                 pcg_spin_limit_us: int = 0):
+        if normal_equations is not None or not early_out or pcg_launch or pcg_spin_limit_us:
             opts = opts if opts is not None else BFSolverOptions()
             if normal_equations is not None:
                 opts.normalEquations = normal_equations
             opts.disableEarlyOut = 0 if early_out else 1
             if pcg_launch:
                 opts.pcgLaunch = pcg_launch
+            opts.pcgSpinLimitUs = pcg_spin_limit_us
         self.h = C.c_void_p()
         check(lib().bf_solver_create(C.c_uint32(max_images), C.c_uint32(max_corr),
                                      C.byref(opts) if opts is not None else None, C.byref(self.h)))

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BF_ABI_VERSION 1
+#define BF_ABI_VERSION 2  /* 2: BFSolverOptions.pcgSpinLimitUs, BFCorrOptions.minPerPair */
 
 /* ---- runtime ------------------------------------------------------------- */
 int bf_abi_version(void);
@@ -161,6 +161,10 @@ typedef struct BFSolverOptions {   /* zParametersBundlingDefault.txt defaults wh
     int32_t pcgLaunch;             /* 0 auto: a pair-mode GN step of 65..513 images runs its whole PCG loop in
                                       one persistent launch (when the grid fits co-resident); 1: one launch
                                       per PCG iteration. Bit-identical results either way */
+    uint32_t pcgSpinLimitUs;       /* bound of every wait inside the persistent PCG launch, in microseconds
+                                      (0: 2 s). A launch that times out is redone in stream order with the
+                                      per-iteration arithmetic (result error bit BF_SOLVE_PCG_RECOVERED);
+                                      a small value forces that path (tests) */
 } BFSolverOptions;
 
 /* ctor (CUDASolverBundling.cpp:24-136): capacity maxImages x maxCorr residuals */
@@ -317,6 +321,8 @@ typedef struct BFReconStats {
     uint64_t localVerifications; /* local solves whose dense verification ran (useVerification) */
     uint64_t invalidLocals;      /* local submaps invalidated by it */
     uint64_t endSolves;          /* end-of-sequence global solves (bf_recon_end_solve) */
+    uint64_t pcgRecoveries;      /* solves whose persistent PCG timed out and was redone (BF_SOLVE_PCG_RECOVERED);
+                                    a solve with a BF_SOLVE_ERR_FATAL bit fails the call with BF_ERR_INTERNAL */
 } BFReconStats;
 
 typedef struct bf_recon bf_recon;
@@ -402,9 +408,9 @@ int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const
  *   p == N: the same with dense depth weight denseDepthWeight (15) when USE_GLOBAL_DENSE_AT_END applies
  *          (fewer than denseFrameLimit frames, every keyframe has a cache frame), else sparse;
  *   then reintegrate(); from p >= N on, the loop stops when generateUpdateLists leaves no active op.
- * N = numSolveFramesBeforeExit (s_numSolveFramesBeforeExit, 30). N < 0 (the reference's -1: never stop
- * solving) solves every iteration and checks the queue from p = 0 on. maxPastEndFrames caps the iterations
- * (0 = 100000). Waits for every solve (deterministic). */
+ * N = numSolveFramesBeforeExit (s_numSolveFramesBeforeExit, 30). N < 0 is the reference's -1: a global solve
+ * every iteration and no exit check (OnlineBundler.cpp:175, DepthSensing.cpp:1116), so only maxPastEndFrames
+ * ends the phase. maxPastEndFrames caps the iterations (0 = 100000). Waits for every solve (deterministic). */
 typedef struct BFEndSequenceOptions {
     int32_t numSolveFramesBeforeExit;  /* [30] */
     int32_t disableDenseAtEnd;         /* 1: no USE_GLOBAL_DENSE_AT_END switch */

@@ -127,6 +127,14 @@ typedef struct BFFixOp {
 } BFFixOp;
 
 /* Outcome of one bundle-adjustment solve (CUDASolverBundling::solve + computeMaxResidual). */
+/* BFSolveResult.error bits */
+#define BF_SOLVE_ERR_PAIR_BOUND 4u   /* more image pairs than the all-reduce's pair bound (sharded solves) */
+#define BF_SOLVE_ERR_PCG_TIMEOUT 8u  /* a persistent PCG launch timed out and was not redone */
+#define BF_SOLVE_PCG_RECOVERED 16u   /* a persistent PCG launch timed out and its GN step was redone with the
+                                        per-iteration arithmetic: the result is valid (bit-identical to
+                                        BFSolverOptions.pcgLaunch = 1) */
+#define BF_SOLVE_ERR_FATAL (~BF_SOLVE_PCG_RECOVERED)
+
 typedef struct BFSolveResult {
     uint32_t gnIterations;       /* Gauss-Newton iterations executed (early exit at max|delta| < 0.005) */
     uint32_t pcgIterations;      /* PCG iterations executed over all GN iterations */
@@ -135,9 +143,8 @@ typedef struct BFSolveResult {
     float energy;                /* sum_c w |r_c|^2 (EvalResidual) */
     uint32_t highResidualCount;  /* correspondences with max residual > verifyOptDistThresh */
     uint32_t numDensePairs;      /* overlapping image pairs found by the dense term (last GN iter) */
-    uint32_t error;              /* bit 1: a row exceeded the sort capacity; bit 2: more image pairs than
-                                    the pair bound; bit 3: the persistent PCG launch timed out waiting
-                                    for a hand-off (2 s; the result is the last completed iteration) */
+    uint32_t error;              /* BF_SOLVE_ERR_* bits: nonzero under BF_SOLVE_ERR_FATAL means the poses
+                                    are not a valid solve (the loop fails the call with BF_ERR_INTERNAL) */
     uint32_t skipped;            /* the solve was gated off (an invalidated local submap's global solve) */
     uint32_t verifyUsed;         /* the last verification ran its dense pair check (useVerification) */
     uint32_t verifyOk;           /* ... and passed (VerifyTrajectoryCU's d_validOpt) */

@@ -442,7 +442,7 @@ void or_recon_end_sequence(ORRecon* h, int32_t N, int32_t disableDense, uint32_t
             }
         }
         r->runReintegrate();
-        if (N < 0 || (int64_t)p >= (int64_t)N) {
+        if (N >= 0 && (int64_t)p >= (int64_t)N) {  // N < 0 (the reference's -1) never exits: maxPastEndFrames bounds it
             if (or_traj_generate_and_count(r->tm) == 0) {
                 out[4] = 1;
                 break;

@@ -23,14 +23,15 @@ MODES = [bfa.abi.NORMAL_EQ_MATRIX_FREE, bfa.abi.NORMAL_EQ_ASSEMBLED]
 
 
 def gpu_solve(prob, n_nonlin, n_lin, ws, wd=None, wc=None, use_cache=False, max_corr=None, corr=None, mode=None,
-              shard=None, export=False, early_out=True, pcg_launch=0):
+              shard=None, export=False, early_out=True, pcg_launch=0, pcg_spin_limit_us=0):
     """mode: normal equations (None = auto: assembled for sparse-only solves); shard = (count, index);
     pcg_launch: 0 auto (one persistent PCG launch per GN step where it fits), 1 one launch per iteration."""
     from bundlefusion_amd.solver import DeviceCache, SolverBundling
     K = prob["K"]
     corr = prob["corr"] if corr is None else corr
     max_corr = max_corr or max(K * 4000, len(corr))
-    S = SolverBundling(K, max_corr, normal_equations=mode, early_out=early_out, pcg_launch=pcg_launch)
+    S = SolverBundling(K, max_corr, normal_equations=mode, early_out=early_out, pcg_launch=pcg_launch,
+                       pcg_spin_limit_us=pcg_spin_limit_us)
     if shard is not None:
         S.set_shard(*shard)
     d_corr = bfa.DeviceArray.from_host(corr if len(corr) else np.zeros(1, corr.dtype))
@@ -451,6 +452,37 @@ def test_persistent_pcg_bit_identical(early_out):
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("case", ["k400", "dense72", "wide700"])
+def test_persistent_pcg_timeout_is_redone(case):
+    """A persistent PCG launch whose hand-offs time out (forced: every wait bounded by 1 us through
+    BFSolverOptions.pcgSpinLimitUs) must not hand back its partial result. k_pcg_recover redoes the GN
+    step from the state k_pair_init saved, with the per-iteration arithmetic: the error word says so
+    (BF_SOLVE_PCG_RECOVERED, no fatal bit) and the poses, residual analysis and iteration counts are bit
+    for bit those of one launch per PCG iteration (pcgLaunch = 1), on both persistent routes (<= 513 images,
+    sparse and dense; the wide finisher above 513)."""
+    A = bfa.abi
+    if case == "k400":
+        prob, args, kw = k400_problem(), (3, 150, [1, 1, 1]), {}
+    elif case == "dense72":
+        prob = make_problem(K=72, stride=2, max_per_pair=10, outliers=0.0, with_cache=True, drift=(0.2, 0.005))
+        args, kw = (2, 40, [1, 1], [1000, 1000], [0, 0]), dict(use_cache=True, mode=A.NORMAL_EQ_ASSEMBLED)
+    else:
+        prob = make_problem(K=700, stride=1, max_per_pair=4, outliers=0.0, drift=(0.05, 0.002))
+        args, kw = (2, 30, [1, 1]), {}
+    a = gpu_solve(prob, *args, pcg_launch=0, pcg_spin_limit_us=1, **kw)
+    b = gpu_solve(prob, *args, pcg_launch=1, **kw)
+    assert b[3]["error"] == 0
+    assert a[3]["error"] == A.SOLVE_PCG_RECOVERED, a[3]["error"]
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    a[3]["error"] = 0
+    assert a[3] == b[3]
+    # the default bound on the same solver path: no timeout, and the same result again
+    c = gpu_solve(prob, *args, pcg_launch=0, **kw)
+    assert c[3]["error"] == 0
+    np.testing.assert_array_equal(c[0], b[0])
 
 
 @pytest.mark.parametrize("mode", MODES)

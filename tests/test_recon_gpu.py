@@ -93,3 +93,44 @@ def test_loop_corrects_drift(loop):
     err_loop = np.array([np.linalg.norm(traj[f][:3, 3] - st.gt[f][:3, 3]) for f in range(st.F)])
     settled = st.F
     assert np.mean(err_loop[:settled]) < 0.5 * np.mean(err_dr[:settled]), (err_loop[:settled], err_dr[:settled])
+
+
+def test_loop_redoes_timed_out_persistent_pcg():
+    """The loop never consumes a timed-out persistent PCG solve. With every wait of the persistent launch
+    bounded by 1 us (BFSolverOptions.pcgSpinLimitUs) each global solve above 64 keyframes times out and
+    its GN steps are redone in stream order (k_pcg_recover): the loop counts them (pcgRecoveries) and its
+    scene calls, trajectory and submap poses are bit-identical to a loop that runs one launch per PCG
+    iteration (pcgLaunch = 1)."""
+    F, S = 216, 3  # 72 keyframes: the global solves from keyframe 65 on take the persistent route
+    st = SyntheticStream(F, width=80, height=60, submap=S, drift=(0.05, 0.002), outliers=0.0, cache_w=40,
+                         cache_h=30)
+    params = bfa.hash_params(voxel_size=0.02, num_buckets=1 << 14, num_blocks=1 << 13)
+    K = st.K
+    runs = []
+    for launch, spin in ((1, 0), (0, 1)):
+        opts = recon_options(F, recordOps=1, submapSize=S, cacheWidth=40, cacheHeight=30,
+                             cacheIntrinsics=st.cache_intrinsics, maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2),
+                             maxKeyframes=K + 1, asyncBundling=0)
+        opts.solver.pcgLaunch = launch
+        opts.solver.pcgSpinLimitUs = spin
+        rc = Recon(params, st.cam, opts)
+        st.attach(rc)
+        for f in range(F):
+            rc.process_frame(f)
+        rc.finish()
+        rc.synchronize()
+        runs.append((rc.stats(), rc.trajectory(F), rc.op_log(),
+                     [rc.submap_poses(s, K + 1, S)[1] for s in range(st.num_submaps - 1)]))
+        rc.close()
+    (s1, t1, o1, g1), (s0, t0, o0, g0) = runs
+    assert s1["pcgRecoveries"] == 0
+    assert s0["pcgRecoveries"] >= K - 66, s0["pcgRecoveries"]  # every global solve above 64 keyframes
+    assert s0["globalSolves"] == s1["globalSolves"] and s0["globalPcgIterations"] == s1["globalPcgIterations"]
+    np.testing.assert_array_equal(t0, t1)
+    assert len(o0) == len(o1)
+    for a, b in zip(o0, o1):
+        assert a[0] == b[0] and a[1] == b[1]
+        np.testing.assert_array_equal(a[2], b[2])
+        np.testing.assert_array_equal(a[3], b[3])
+    for a, b in zip(g0, g1):
+        np.testing.assert_array_equal(a, b)
