@@ -119,10 +119,22 @@ def cpu_loop_prefix(stream, params, n_frames=PREFIX_FRAMES, budget_s=PREFIX_BUDG
     scene = OracleScene(params)
     depth, color = {}, {}
 
+    raw = getattr(stream, "raw_input", False)
+    if raw:
+        from oracle_lib import preprocess
+        from bundlefusion_amd.io import preprocess_options
+        popt = preprocess_options()
+        W = stream.cam.imageWidth
+
     def frame(f):
         if f not in depth:
-            depth[f] = stream.depth.download_range(f * P * 4, P * 4).view(np.float32).reshape(H, -1)
-            color[f] = stream.color.download_range(f * P * 4, P * 4).reshape(H, -1, 4)
+            if raw:  # the loop's per-frame CUDAImageManager::process, restated by the oracle (oracle/frames.cpp)
+                du = stream.depth_u16.download_range(f * P * 2, P * 2).view(np.uint16).reshape(H, -1)
+                cx = stream.rgbx.download_range(f * P * 4, P * 4).reshape(H, -1, 4)
+                depth[f], color[f] = preprocess(popt, du, cx, (W, H))
+            else:
+                depth[f] = stream.depth.download_range(f * P * 4, P * 4).view(np.float32).reshape(H, -1)
+                color[f] = stream.color.download_range(f * P * 4, P * 4).reshape(H, -1, 4)
         return depth[f], color[f]
 
     for f in range(n_max + 1):
@@ -136,6 +148,8 @@ def cpu_loop_prefix(stream, params, n_frames=PREFIX_FRAMES, budget_s=PREFIX_BUDG
         if time.perf_counter() - last > 20.0:
             log(f"  cpu oracle loop frame {done}")
             last = time.perf_counter()
+        if raw:
+            frame(done)  # preprocessing of the frame the loop takes in
         ora.process_frame(done)
         log_ = ora.op_log()
         for kind, f, oldT, newT in log_[ops:]:
@@ -379,6 +393,14 @@ def main():
                     help="edge (m) of the TSDF ownership chunks when sharded over ranks")
     ap.add_argument("--async-bundling", type=int, default=1, choices=[1, 2],
                     help="1: solves issued from the frame loop onto their own streams; 2: from a bundling thread")
+    ap.add_argument("--no-preprocess", action="store_true",
+                    help="feed the rendered float depth straight into the loop instead of raw sensor frames "
+                         "(ushort depth, RGBX) preprocessed per frame inside it (CUDAImageManager::process: erode x2, "
+                         "bilateral filter, resample; DepthSensing.cpp:986)")
+    ap.add_argument("--result-lag", type=int, default=10,
+                    help="frames after its issue at which a submap's solved poses are applied (waiting if needed): "
+                         "the run's op sequence is then repeatable; 0: picked up by polling as soon as done "
+                         "(timing-dependent, like the reference's bundling thread)")
     ap.add_argument("--sens", default=None,
                     help="run the FriedLiver application (bf_app_*) over this .sens instead of the synthetic stream "
                          "(copyroom / apt0: BASELINE configs 2 and 3): decode, preprocessing, cache, EntryJ stand-in, "
@@ -430,11 +452,12 @@ def main():
     # the dense-term cache frames are built inside the loop as each frame is processed
     # (Bundler::storeCachedFrame in OnlineBundler::processInput, OnlineBundler.cpp:199-204), so the
     # timed region includes CUDACache::storeFrame
-    stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log, cache_source="loop")
+    stream = SyntheticStream(F, width=args.width, height=args.height, submap=S, log=log, cache_source="loop",
+                             raw_input=not args.no_preprocess)
     params = bfa.hash_params(voxel_size=args.voxel, num_buckets=args.buckets, num_blocks=args.blocks)
     K = stream.K
     opts = recon_options(F, enableTiming=1, asyncBundling=args.async_bundling, cacheWidth=80, cacheHeight=60, cacheIntrinsics=stream.cache_intrinsics,
-                         maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2))
+                         maxKeyframes=K + 1, maxGlobalCorr=max(1000, 25 * (K + 1) * K // 2), resultLag=args.result_lag)
     so = BFSceneOptions()
     so.shardCount, so.shardIndex, so.shardChunk = world, rank, args.shard_chunk
     if world == 1 and args.rehearse_shards > 1:
@@ -488,6 +511,7 @@ def main():
     workload = (f"{frames_total}-frame {args.width}x{args.height} stream, {args.voxel * 1000:.0f} mm voxels, "
                 f"2^{args.buckets.bit_length() - 1} buckets, 2^{args.blocks.bit_length() - 1} blocks; "
                 f"local 2x100 + global 3x150 GN x PCG per submap; cache frames built in the loop; "
+                f"{'rendered depth fed directly' if args.no_preprocess else 'raw frames preprocessed in the loop'}; "
                 f"timed: last {args.steps} submaps")
     # a profile's counters describe one scheduling: a sharded rehearsal or another bundling mode is a
     # different workload (a rehearsal must not pick up the unsharded profile's counters)
@@ -495,6 +519,8 @@ def main():
         workload += f"; tsdf shard {so.shardIndex} of {so.shardCount} (chunk {so.shardChunk:g} m)"
     if args.async_bundling != 1:
         workload += f"; asyncBundling {args.async_bundling}"
+    workload += (f"; solved poses applied {args.result_lag} frames after issue" if args.result_lag
+                 else "; solved poses applied when polled ready (timing-dependent)")
     # dominant kernel: k_apply_ops, the op-batch voxel pass that applies a frame's re-integration
     # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Per launch, from the
     # device counters of the same launches:
@@ -629,15 +655,41 @@ def main():
     rc.raycast_device(Tlast, rpr, routs)
     rc.synchronize()
     ms0, n0 = rc.render_time()
+    rs0 = rc.render_stats()
     t_r = time.perf_counter()
     for _ in range(20):
         rc.raycast_device(Tlast, rpr, routs)
     rc.synchronize()
     t_r = (time.perf_counter() - t_r) / 20
     ms1, n1 = rc.render_time()
+    rs1 = rc.render_stats()
     rdepth = routs[0].download()
-    out["raycast"] = {"ms_per_render": t_r * 1e3, "k_render_us": (ms1 - ms0) / max(1, n1 - n0) * 1e3,
+    # SURVEY.md §8(d) raycast bytes: 96 B per trilinear sample (8 corner voxels x 12 B) + 52 B of output per
+    # pixel (depth 4 + depth4 16 + normal 16 + colour 16), from the device counters of the same 20 renders
+    nr = max(1, rs1["renders"] - rs0["renders"])
+    samples = (rs1["samples"] - rs0["samples"]) / nr
+    loads = (rs1["voxelLoads"] - rs0["voxelLoads"]) / nr
+    k_render_us = (ms1 - ms0) / max(1, n1 - n0) * 1e3
+    splat_us = (rs1["splatMs"] - rs0["splatMs"]) / max(1, rs1["timedRenders"] - rs0["timedRenders"]) * 1e3
+    rbytes = 96.0 * samples + 52.0 * W_ * H_
+    atomics = (rs1["splatAtomics"] - rs0["splatAtomics"]) / nr
+    out["raycast"] = {"ms_per_render": t_r * 1e3, "k_render_us": k_render_us,
                       "valid_fraction": float(np.isfinite(rdepth).mean()),
+                      "per_render": {"samples": samples, "voxel_loads": loads,
+                                     "hash_probes": (rs1["hashProbes"] - rs0["hashProbes"]) / nr,
+                                     "rays": (rs1["rays"] - rs0["rays"]) / nr,
+                                     "splat_blocks": (rs1["splatBlocks"] - rs0["splatBlocks"]) / nr,
+                                     "splat_atomics": atomics, "k_splat_us": splat_us},
+                      "roofline": {"bound": "latency", "kernel": "k_render (renderKernel)", "unit": "GB/s",
+                                   "alg_bytes_per_render": rbytes, "achieved": rbytes / (k_render_us * 1e-6) / 1e9,
+                                   "peak": HBM_PEAK_GBS, "frac": rbytes / (k_render_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                                   "loaded_bytes_per_render": 12.0 * loads + 52.0 * W_ * H_,
+                                   "note": "SURVEY 8(d): 96 B per trilinear sample + 52 B per pixel; a sample's voxels "
+                                           "are dependent loads of one ray (hash probe -> 8 corners -> next step), so "
+                                           "the march is bound by load latency, not bandwidth"},
+                      "splat_roofline": {"kernel": "k_splat (ray-interval splat)", "atomics_per_render": atomics,
+                                         "atomics_per_us": atomics / max(1e-9, splat_us),
+                                         "note": "one 4-B atomic min/max per covered pixel per pass"},
                       "note": f"compactify + interval splat + renderKernel + computeNormals at {W_}x{H_} from the last pose"}
     # marching cubes over the final scene (StopScanningAndExtractIsoSurfaceMC, reported beside the metric)
     mcp = bfa.mc_params(params.virtualVoxelSize)

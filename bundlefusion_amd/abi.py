@@ -229,7 +229,14 @@ class BFReconOptions(C.Structure):
                 ("maxGlobalCorr", C.c_uint32), ("maxResidualThresh", C.c_float), ("useLocalDense", C.c_int32),
                 ("cacheWidth", C.c_uint32), ("cacheHeight", C.c_uint32), ("cacheIntrinsics", C.c_float * 4),
                 ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("asyncBundling", C.c_int32),
-                ("solver", BFSolverOptions), ("disableLocalVerify", C.c_int32), ("verify", BFVerifyOptions)]
+                ("solver", BFSolverOptions), ("disableLocalVerify", C.c_int32), ("verify", BFVerifyOptions),
+                ("resultLag", C.c_uint32)]
+
+
+class BFRenderStats(C.Structure):  # include/bf/bf.h
+    _fields_ = [(n, C.c_uint64) for n in ("samples", "voxelLoads", "hashProbes", "rays", "splatBlocks", "splatAtomics",
+                                          "renders", "pixels", "timedRenders")] + [
+        ("renderMs", C.c_double), ("splatMs", C.c_double)]
 
 
 class BFEndSequenceOptions(C.Structure):  # include/bf/bf.h: the render loop past the last frame

@@ -29,6 +29,8 @@ void synth_render_device(const BFSynthScene& sc, const BFMat4& T, const BFDepthC
 void synth_render_host(const BFSynthScene& sc, const BFMat4& T, const BFDepthCameraParams& cam, uint32_t noiseSeed,
                        uint32_t frame, float* depth, uint8_t* color);
 void synth_scene_default(uint32_t seed, BFSynthScene* out);
+void synth_to_raw(const float* depth, const uint8_t* color, uint32_t n, float shift, uint16_t* du, uint8_t* rgbx,
+                  hipStream_t stream);
 uint32_t synth_correspondences(const BFSynthScene& sc, const float* poses, uint32_t K, const BFDepthCameraParams& cam,
                                uint32_t maxPerPair, float minCovis, float noise, float outlierFrac, uint32_t seed,
                                BFEntryJ* out, uint32_t cap);
@@ -454,6 +456,14 @@ int bf_synth_render(const BFSynthScene* scene, const float T[16], const BFDepthC
     BF_HIP(hipStreamSynchronize(nullptr));
     BF_CATCH
 }
+int bf_synth_to_raw(const float* d_depth, const uint8_t* d_color, uint32_t numPixels, float depthShift,
+                    uint16_t* d_depthU16, uint8_t* d_rgbx) {
+    BF_TRY
+    BF_REQUIRE(d_depth && d_color && d_depthU16 && d_rgbx && depthShift > 0.0f, BF_ERR_ARG, "null argument");
+    synth_to_raw(d_depth, d_color, numPixels, depthShift, d_depthU16, d_rgbx, nullptr);
+    BF_HIP(hipStreamSynchronize(nullptr));
+    BF_CATCH
+}
 int bf_synth_render_host(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam, uint32_t noiseSeed,
                          uint32_t frame, float* depth, uint8_t* color) {
     BF_TRY
@@ -831,6 +841,13 @@ int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTrian
     *numTriangles = r->r->scene().extractMesh(*p, tris, tris ? p->maxNumTriangles : 0u, totalTriangles);
     BF_CATCH
 }
+int bf_recon_render_stats(bf_recon* r, BFRenderStats* out) {
+    BF_TRY
+    BF_REQUIRE(r && out, BF_ERR_ARG, "null argument");
+    r->r->synchronize();
+    r->r->scene().renderStats(*out);
+    BF_CATCH
+}
 int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches) {
     BF_TRY
     BF_REQUIRE(r && ms && launches, BF_ERR_ARG, "null argument");
@@ -858,6 +875,18 @@ int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const
     BF_TRY
     BF_REQUIRE(r && depth && color, BF_ERR_ARG, "null argument");
     r->r->setFrameSource(f, depth, color, colorW, colorH);
+    BF_CATCH
+}
+int bf_recon_attach_preproc(bf_recon* r, bf_preproc* p) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null recon");
+    r->r->attachPreproc(p ? p->p : nullptr);
+    BF_CATCH
+}
+int bf_recon_set_frame_raw(bf_recon* r, uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx) {
+    BF_TRY
+    BF_REQUIRE(r && depthU16 && rgbx, BF_ERR_ARG, "null argument");
+    r->r->setFrameRaw(f, depthU16, rgbx);
     BF_CATCH
 }
 int bf_recon_end_sequence(bf_recon* r, const BFEndSequenceOptions* o, BFEndSequenceResult* out) {

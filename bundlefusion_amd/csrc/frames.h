@@ -21,6 +21,10 @@ public:
     // device pointers; queued on the stream
     void run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut);
     hipStream_t stream() const { return stream_; }
+    uint32_t integrationWidth() const { return iw_; }
+    uint32_t integrationHeight() const { return ih_; }
+    uint32_t colorWidth() const { return cw_; }
+    uint32_t colorHeight() const { return ch_; }
     // the sensor-size images of the last run that CUDAImageManager::copyToBundling hands the bundler
     // (CUDAImageManager.h:223-227): d_depthInputRaw (the two erosion passes end in it) and
     // d_depthInputFiltered (the bilateral filter's output; the raw image when the filter is off)

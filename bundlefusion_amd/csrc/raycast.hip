@@ -26,6 +26,7 @@ BFMat4 mat4_inverse(const BFMat4& M);  // api.cpp
 namespace {
 
 const float MINF_F = -__builtin_inff();
+enum RenderStat { RS_SAMPLES = 0, RS_LOADS, RS_PROBES, RS_RAYS, RS_QUADS, RS_ATOMICS, RS_RENDERS, RS_PIXELS };
 
 __device__ __forceinline__ uint32_t enc_f(float f) {  // monotone float -> uint32
     const uint32_t b = __float_as_uint(f);
@@ -69,8 +70,10 @@ __global__ void k_splat_clear(uint32_t* smin, uint32_t* smax, uint32_t n) {
 
 // rayIntervalSplatKernel (CUDARayCastSDF.cu:101-190) for both passes + the raster of its quads
 __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible, const uint32_t* ctrl, float voxelSize,
-                                               BFDepthCameraParams cam, BFRayCastParams rp, uint32_t* smin, uint32_t* smax) {
+                                               BFDepthCameraParams cam, BFRayCastParams rp, uint32_t* smin, uint32_t* smax,
+                                               unsigned long long* stats) {
     const uint32_t n = ctrl[C_VISIBLE];
+    uint32_t quads = 0, atoms = 0;  // per wave (uniform): rasterised blocks, atomic depth updates
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -111,17 +114,24 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
         if (x1 < x0 || y1 < y0) continue;
         const uint32_t w = (uint32_t)(x1 - x0 + 1), npx = w * (uint32_t)(y1 - y0 + 1);
         const uint32_t emin = enc_f(dwMin), emax = enc_f(dwMax);
+        quads++;
+        atoms += npx * ((minOk ? 1u : 0u) + (maxOk ? 1u : 0u));
         for (uint32_t k = lane; k < npx; k += 64) {
             const uint32_t idx = (uint32_t)(y0 + (int)(k / w)) * rp.width + (uint32_t)(x0 + (int)(k % w));
             if (minOk) atomicMin(&smin[idx], emin);
             if (maxOk) atomicMax(&smax[idx], emax);
         }
     }
+    if (lane == 0 && quads) {
+        atomicAdd(&stats[RS_QUADS], (unsigned long long)quads);
+        atomicAdd(&stats[RS_ATOMICS], (unsigned long long)atoms);
+    }
 }
 
 // getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417) with a one-entry per-thread block cache
 struct BlockCache {
     int bx = INT_MIN, by = 0, bz = 0, ptr = BF_FREE_ENTRY;
+    uint32_t samples = 0, loads = 0, probes = 0;  // render statistics (trilinear samples, voxel loads, hash probes)
 };
 __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 pos, float& sdf, float& weight, uint32_t& color) {
     const i3 v = world_to_vvox(pos, R.voxelSize);
@@ -129,6 +139,7 @@ __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 po
     if (b.x != c.bx || b.y != c.by || b.z != c.bz) {
         c.bx = b.x; c.by = b.y; c.bz = b.z;
         c.ptr = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
+        c.probes++;
     }
     if (c.ptr == BF_FREE_ENTRY) {  // deleteVoxel
         sdf = 0.0f; weight = 0.0f; color = 0u;
@@ -139,6 +150,7 @@ __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 po
     if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
     if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
     const BFVoxel* vp = R.voxels + (size_t)c.ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+    c.loads++;
     sdf = vp->sdf;
     weight = vp->weight;
     color = *reinterpret_cast<const uint32_t*>(vp->color);
@@ -152,6 +164,7 @@ __device__ bool trilinear(const RayArgs& R, BlockCache& c, f3 pos, float& dist, 
     const float oSet = R.voxelSize;
     const f3 posDual = pos - mk3(oSet / 2.0f, oSet / 2.0f, oSet / 2.0f);
     const f3 vv = pos / R.voxelSize;
+    c.samples++;
     const f3 weight = mk3(frac1(vv.x), frac1(vv.y), frac1(vv.z));
     dist = 0.0f;
     f3 colorFloat = mk3(0.0f, 0.0f, 0.0f);
@@ -195,11 +208,9 @@ __device__ f3 gradient_for_point(const RayArgs& R, BlockCache& c, f3 pos) {
 }
 
 // renderKernel (CUDARayCastSDF.cu:17-57) + traverseCoarseGridSimpleSampleAll (RayCastSDFUtil.h:224-290)
-__global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
-                                                const uint32_t* __restrict__ smax, float* d_depth, float4* d_depth4,
-                                                float4* d_normals, float4* d_colors, float* outMin, float* outMax) {
-    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= rp.width || y >= rp.height) return;
+__device__ void render_pixel(const RayArgs& R, const BFRayCastParams& rp, BlockCache& cache, uint32_t x, uint32_t y,
+                             const uint32_t* __restrict__ smin, const uint32_t* __restrict__ smax, float* d_depth,
+                             float4* d_depth4, float4* d_normals, float4* d_colors, float* outMin, float* outMax, bool& rayed) {
     const uint32_t pix = y * rp.width + x;
     const float MINF = -__builtin_inff();
     d_depth[pix] = MINF;
@@ -221,8 +232,8 @@ __global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, c
     if (maxInterval == 0.0f || maxInterval == MINF) return;
     minInterval = fmaxf(minInterval, rp.minDepth);
     maxInterval = fminf(maxInterval, rp.maxDepth);
+    rayed = true;
 
-    BlockCache cache;
     float lastSdf = 0.0f, lastAlpha = 0.0f;
     int lastWeight = 0;
     const float depthToRayLength = 1.0f / camDir.z;
@@ -274,6 +285,34 @@ __global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, c
         }
     }
 }
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+// stats: [RS_SAMPLES] trilinear samples, [RS_LOADS] voxel loads, [RS_PROBES] hash probes, [RS_RAYS] marched rays
+__global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
+                                                const uint32_t* __restrict__ smax, float* d_depth, float4* d_depth4,
+                                                float4* d_normals, float4* d_colors, float* outMin, float* outMax,
+                                                unsigned long long* stats) {
+    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    BlockCache cache;
+    bool rayed = false;
+    if (x < rp.width && y < rp.height)
+        render_pixel(R, rp, cache, x, y, smin, smax, d_depth, d_depth4, d_normals, d_colors, outMin, outMax, rayed);
+    const uint32_t s = wave_sum_u32(cache.samples), l = wave_sum_u32(cache.loads), p = wave_sum_u32(cache.probes);
+    const uint32_t r = wave_sum_u32(rayed ? 1u : 0u);
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+        atomicAdd(&stats[RS_RENDERS], 1ull);
+        atomicAdd(&stats[RS_PIXELS], (unsigned long long)rp.width * rp.height);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&stats[RS_SAMPLES], (unsigned long long)s);
+        atomicAdd(&stats[RS_LOADS], (unsigned long long)l);
+        atomicAdd(&stats[RS_PROBES], (unsigned long long)p);
+        atomicAdd(&stats[RS_RAYS], (unsigned long long)r);
+    }
+}
 
 // computeNormalsDevice (CameraUtil.cu:665-692)
 __global__ void k_normals(float4* out, const float4* in, uint32_t W, uint32_t H) {
@@ -295,6 +334,17 @@ __global__ void k_normals(float4* out, const float4* in, uint32_t W, uint32_t H)
 
 }  // namespace
 
+void Scene::renderStats(BFRenderStats& out) {
+    uint64_t c[8];
+    BF_HIP(hipMemcpyAsync(c, renderStats_.p, sizeof(c), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    out.samples = c[RS_SAMPLES]; out.voxelLoads = c[RS_LOADS]; out.hashProbes = c[RS_PROBES]; out.rays = c[RS_RAYS];
+    out.splatBlocks = c[RS_QUADS]; out.splatAtomics = c[RS_ATOMICS]; out.renders = c[RS_RENDERS]; out.pixels = c[RS_PIXELS];
+    out.timedRenders = renderClock_.enabled() ? renderClock_.launches() : 0;
+    out.renderMs = renderClock_.enabled() ? renderClock_.totalMs() : 0.0;
+    out.splatMs = splatClock_.enabled() ? splatClock_.totalMs() : 0.0;
+}
+
 void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRayCastParams& rpIn, float* depth, float4* depth4,
                     float4* normals, float4* colors, float* rayMin, float* rayMax) {
     BF_REQUIRE(depth && depth4 && normals && colors, BF_ERR_ARG, "raycast outputs");
@@ -311,9 +361,15 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
     }
     k_splat_clear<<<std::max(1u, std::min(div_up(P, 256), 2048u)), 256, 0, stream_>>>(splatMin_.p, splatMax_.p, (uint32_t)P);
     BF_LAUNCH_CHECK();
+    const bool timed = renderClock_.enabled();
+    if (timed) {
+        if (!splatClock_.enabled()) splatClock_.enable(true);
+        splatClock_.start(stream_);
+    }
     k_splat<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp, splatMin_.p,
-                                                          splatMax_.p);
+                                                          splatMax_.p, renderStats_.p);
     BF_LAUNCH_CHECK();
+    if (timed) splatClock_.stop(stream_);
     RayArgs R;
     R.hash = hash_.p;
     R.voxels = voxels_.p;
@@ -322,9 +378,9 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
     R.maxList = cfg_.hp.hashMaxCollisionLinkedListSize;
     R.voxelSize = cfg_.hp.virtualVoxelSize;
     const dim3 g(div_up(rp.width, 16), div_up(rp.height, 16));
-    const bool timed = renderClock_.enabled();
     if (timed) renderClock_.start(stream_);
-    k_render<<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax);
+    k_render<<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
+                                     renderStats_.p);
     BF_LAUNCH_CHECK();
     if (timed) renderClock_.stop(stream_);
     if (!rp.useGradients) {

@@ -189,6 +189,7 @@ Recon::~Recon() {
         if (globalDone_[b]) (void)hipEventDestroy(globalDone_[b]);
     }
     if (cacheEv_) (void)hipEventDestroy(cacheEv_);
+    if (preEv_) (void)hipEventDestroy(preEv_);
     for (Pending& p : ring_) {
         if (p.done) (void)hipEventDestroy(p.done);
         for (void* q : {(void*)p.localT, (void*)p.globalT, (void*)p.valid, (void*)p.ctrl, (void*)p.localInit,
@@ -331,6 +332,10 @@ void Recon::processFrame(uint32_t f) {
     BF_REQUIRE(f < opt_.maxFrames && frames_[f].set, BF_ERR_STATE, "frame not in the frame store");
     const uint32_t S = opt_.submapSize;
     const uint32_t s = f / S;
+    // CUDAImageManager::process (DepthSensing.cpp:986 -> CUDAImageManager.cpp:22-158): the raw sensor
+    // frame into its frame-store slot; the scene stream (which integrates it with the next frame's batch)
+    // and the cache (which reads the raw depth) are ordered after it by an event
+    if (preproc_ && frames_[f].rawDepth) preprocessFrame(f);
     // processInput -> storeCachedFrame before anything reads the frame's cache (the submap ending at
     // this frame includes it as its overlap frame)
     if (cache_) storeCacheFrame(f);
@@ -397,6 +402,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     P.numLocal = n;
     P.localSolved = P.globalSolved = false;
     P.endSolve = false;
+    P.issueFrame = numFrames_;
 
     // ---- local solve over frames base .. base+n-1 (first frame fixed) ----------------------
     bool haveCache = opt_.useLocalDense != 0;
@@ -707,6 +713,18 @@ void Recon::baWaitFor(uint64_t job) {
 void Recon::baDrain() { baWaitFor(lastJob_); }
 
 void Recon::applyPending(bool block) {
+    if (!block && opt_.asyncBundling && opt_.resultLag) {
+        // repeatable hand-off: submap results are applied exactly resultLag frames after their issue
+        while (!inflight_.empty()) {
+            Pending& P = ring_[inflight_.front()];
+            if (numFrames_ < P.issueFrame + opt_.resultLag) break;
+            baWaitFor(P.job);
+            BF_HIP(hipEventSynchronize(P.done));
+            apply(P);
+            inflight_.pop_front();
+        }
+        return;
+    }
     while (!inflight_.empty()) {
         Pending& P = ring_[inflight_.front()];
         if (!block && baDone_.load(std::memory_order_acquire) < P.job) break;  // not issued yet
@@ -844,9 +862,40 @@ void Recon::setFrameSource(uint32_t f, const float* depth, const uint8_t* color,
     r.srcH = colorH;
 }
 
+void Recon::attachPreproc(Preproc* p) {
+    BF_REQUIRE(numFrames_ == 0, BF_ERR_STATE, "attach the preprocessing before the first frame");
+    BF_REQUIRE(!p || (p->integrationWidth() == cam_.imageWidth && p->integrationHeight() == cam_.imageHeight), BF_ERR_ARG,
+               "preprocessing output size differs from the integration size");
+    preproc_ = p;
+    if (p && !preEv_) BF_HIP(hipEventCreateWithFlags(&preEv_, hipEventDisableTiming));
+}
+
+void Recon::setFrameRaw(uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx) {
+    BF_REQUIRE(f < opt_.maxFrames, BF_ERR_CAPACITY, "frame index beyond maxFrames");
+    frames_[f].rawDepth = depthU16;
+    frames_[f].rawColor = rgbx;
+}
+
+void Recon::preprocessFrame(uint32_t f) {
+    FrameRef& fr = frames_[f];
+    BF_REQUIRE(fr.depth && fr.color, BF_ERR_STATE, "preprocessing needs the frame's frame-store slot (bf_recon_set_frame)");
+    const hipStream_t ps = preproc_->stream();
+    // the preprocessing buffers (raw / filtered sensor depth) are read by the previous frame's cache store
+    if (cacheEv_ && cache_ && cache_->stream() != ps) BF_HIP(hipStreamWaitEvent(ps, cacheEv_, 0));
+    preproc_->run(fr.rawDepth, fr.rawColor, const_cast<float*>(fr.depth), const_cast<uint8_t*>(fr.color));
+    BF_HIP(hipEventRecord(preEv_, ps));
+    BF_HIP(hipStreamWaitEvent(sceneStream_, preEv_, 0));
+    // copyToBundling: the cache takes the sensor-size raw depth and colour (as the FriedLiver app does)
+    fr.srcDepth = preproc_->rawDepth();
+    fr.srcColor = fr.rawColor;
+    fr.srcW = preproc_->colorWidth();
+    fr.srcH = preproc_->colorHeight();
+}
+
 // Bundler::storeCachedFrame (Bundler.cpp:278-281) for frame f, on the cache's stream
 void Recon::storeCacheFrame(uint32_t f) {
     FrameRef& fr = frames_[f];
+    if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream()) BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_, 0));
     BF_REQUIRE(cache_->numFrames() == f, BF_ERR_STATE, "attached cache must hold exactly the frames before this one");
     const float* d = fr.srcDepth ? fr.srcDepth : fr.depth;
     const uint8_t* c = fr.srcDepth ? fr.srcColor : fr.color;

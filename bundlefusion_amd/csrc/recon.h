@@ -32,6 +32,7 @@
 #include "../../include/bf/bf.h"
 #include "ba.h"
 #include "cache.h"
+#include "frames.h"
 #include "trajectory.h"
 #include "tsdf.h"
 
@@ -60,6 +61,10 @@ public:
     // per-frame CUDACache::storeFrame inside processFrame (OnlineBundler.cpp:199-204); c is borrowed
     void attachCache(Cache* c);
     void setFrameSource(uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH);
+    // CUDAImageManager::process inside the loop: frame f's raw sensor images are preprocessed into its
+    // frame-store slot when it is processed (the cache then reads the raw sensor depth and colour)
+    void attachPreproc(Preproc* p);
+    void setFrameRaw(uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx);
     // TrajectoryManager::getOptimizedTransforms (TrajectoryManager.h:50-68)
     uint32_t optimizedTrajectory(BFMat4* out, uint32_t cap) const;
     // recordOps: the TrajectoryManager call sequence (bf_recon_queue_trace)
@@ -83,6 +88,7 @@ public:
 private:
     struct Pending {  // one submap's bundling results in flight
         uint32_t submap = 0, numLocal = 0, numKeyframes = 0;
+        uint32_t issueFrame = 0;    // the frame whose processing issued it (resultLag)
         uint64_t job = 0;  // bundling-thread job that enqueues this submap's work (see baPost)
         bool localSolved = false, globalSolved = false;
         bool endSolve = false;      // an end-of-sequence global solve (no local part)
@@ -123,6 +129,8 @@ private:
         const float* srcDepth = nullptr;   // cache source images (setFrameSource; null: the frame store's)
         const uint8_t* srcColor = nullptr;
         uint32_t srcW = 0, srcH = 0;
+        const uint16_t* rawDepth = nullptr;  // sensor images preprocessed into depth / color (attachPreproc)
+        const uint8_t* rawColor = nullptr;
         bool set = false;
         bool tilesReady = false;  // its band-cull depth tiles and dc image are in frameTiles_ / frameDC_
     };
@@ -214,7 +222,10 @@ private:
 
     Cache* cache_ = nullptr;            // attached frame cache (borrowed)
     hipEvent_t cacheEv_ = nullptr;      // the last storeFrame on the cache's stream
+    Preproc* preproc_ = nullptr;        // attached input preprocessing (borrowed)
+    hipEvent_t preEv_ = nullptr;        // the last preprocessing run on its stream
     void storeCacheFrame(uint32_t f);
+    void preprocessFrame(uint32_t f);
 
     // recordOps: TrajectoryManager call trace
     std::vector<BFQueueEvent> qEvents_;

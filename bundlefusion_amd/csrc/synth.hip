@@ -25,6 +25,21 @@ void synth_render_device(const BFSynthScene& sc, const BFMat4& T, const BFDepthC
     BF_LAUNCH_CHECK();
 }
 
+__global__ void k_synth_to_raw(const float* d, const uint32_t* c, uint32_t n, float shift, uint16_t* du, uint32_t* rgbx) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float v = d[i];
+        du[i] = (v > 0.0f && v < INFINITY) ? (uint16_t)fminf(rintf(v * shift), 65535.0f) : (uint16_t)0;
+        rgbx[i] = c[i];
+    }
+}
+void synth_to_raw(const float* depth, const uint8_t* color, uint32_t n, float shift, uint16_t* du, uint8_t* rgbx,
+                  hipStream_t stream) {
+    if (!n) return;
+    k_synth_to_raw<<<std::min(div_up(n, 256u), 4096u), 256, 0, stream>>>(depth, reinterpret_cast<const uint32_t*>(color), n, shift, du,
+                                                                      reinterpret_cast<uint32_t*>(rgbx));
+    BF_LAUNCH_CHECK();
+}
+
 void synth_render_host(const BFSynthScene& sc, const BFMat4& T, const BFDepthCameraParams& cam, uint32_t noiseSeed,
                        uint32_t frame, float* depth, uint8_t* color) {
     for (uint32_t y = 0; y < cam.imageHeight; y++)

@@ -122,6 +122,9 @@ public:
     void raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRayCastParams& rp, float* depth, float4* depth4,
                  float4* normals, float4* colors, float* rayMin, float* rayMax);
     KernelClock& renderClock() { return renderClock_; }
+    // accumulated ray-cast counters (BFRenderStats order after launches / kernelMs): trilinear samples,
+    // voxel loads, hash probes, marched rays, splatted blocks, splat atomics, renders, pixels
+    void renderStats(BFRenderStats& out);
     // CUDAMarchingCubesHashSDF::extractIsoSurface (CUDAMarchingCubesHashSDF.cpp:107-118) over every
     // allocated block: writes min(total, cap) triangles to the device array out in (heap block,
     // voxel, case-table) order, returns that count; *total = triangles before the cap. Synchronizes.
@@ -163,7 +166,8 @@ private:
     int numCUs_;
     unsigned integrateGrid_[2] = {0, 0};
     KernelClock integrateClock_;
-    KernelClock renderClock_;
+    KernelClock renderClock_, splatClock_;
+    DevBuf<unsigned long long> renderStats_;
     DevBuf<uint2> blockMask_;  // per work-list entry of an op batch: which ops may update each z-half
     DevBuf<uint32_t> blockBirth_;  // per heap block: epoch << 8 | (255 - first op) of the batch that allocated it
     DevBuf<uint8_t> candOp_;       // per alloc candidate of a batch: the integrate op that emitted it

@@ -159,6 +159,14 @@ class Recon:
         self._cache = cache
         check(lib().bf_recon_attach_cache(self.h, cache.h if cache is not None else None))
 
+    def attach_preproc(self, pre):
+        """CUDAImageManager::process per processed frame (DepthSensing.cpp:986); pre: io.Preprocessor."""
+        self._preproc = pre
+        check(lib().bf_recon_attach_preproc(self.h, pre.h if pre is not None else None))
+
+    def set_frame_raw(self, f: int, depth_u16_ptr: int, rgbx_ptr: int):
+        check(lib().bf_recon_set_frame_raw(self.h, C.c_uint32(f), C.c_void_p(depth_u16_ptr), C.c_void_p(rgbx_ptr)))
+
     def set_frame_source(self, f: int, depth_ptr: int, color_ptr: int, color_w: int, color_h: int):
         check(lib().bf_recon_set_frame_source(self.h, C.c_uint32(f), C.c_void_p(depth_ptr), C.c_void_p(color_ptr),
                                               C.c_uint32(color_w), C.c_uint32(color_h)))
@@ -242,6 +250,12 @@ class Recon:
         n, total = C.c_uint32(), C.c_uint32()
         check(lib().bf_recon_extract_mesh(self.h, C.byref(mc), out.ptr, C.byref(n), C.byref(total)))
         return n.value, total.value
+
+    def render_stats(self) -> dict:
+        from .abi import BFRenderStats
+        r = BFRenderStats()
+        check(lib().bf_recon_render_stats(self.h, C.byref(r)))
+        return {k: getattr(r, k) for k, _ in BFRenderStats._fields_}
 
     def render_time(self):
         ms = C.c_double()

@@ -26,7 +26,8 @@ def _rodrigues(w):
 
 class SyntheticStream:
     def __init__(self, num_frames: int, width=640, height=480, submap=10, seed=0, drift=(0.05, 0.002),
-                 max_per_pair=25, outliers=0.02, cache_w=80, cache_h=60, cache_source="frames", log=None):
+                 max_per_pair=25, outliers=0.02, cache_w=80, cache_h=60, cache_source="frames", log=None,
+                 raw_input=False):
         t0 = time.perf_counter()
         self.F, self.S = num_frames, submap
         self.log = log or (lambda *a: None)
@@ -49,6 +50,17 @@ class SyntheticStream:
                                         C.c_void_p(self.color.ptr.value + 4 * P * i)))
         check(lib().bf_device_synchronize())
         self.log(f"rendered {num_frames} frames {width}x{height} in {time.perf_counter() - t0:.1f}s")
+        # raw_input: the frames as the sensor delivers them (ushort depth in mm, RGBX), preprocessed inside the
+        # loop into the frame store above (CUDAImageManager::process per frame, Recon.attach_preproc)
+        self.raw_input = raw_input
+        if raw_input:
+            self.depth_u16 = DeviceArray((num_frames, height, width), np.uint16)
+            self.rgbx = DeviceArray((num_frames, height, width, 4), np.uint8)
+            for i in range(num_frames):
+                check(lib().bf_synth_to_raw(C.c_void_p(self.depth.ptr.value + 4 * P * i),
+                                            C.c_void_p(self.color.ptr.value + 4 * P * i), C.c_uint32(P), C.c_float(1000.0),
+                                            C.c_void_p(self.depth_u16.ptr.value + 2 * P * i),
+                                            C.c_void_p(self.rgbx.ptr.value + 4 * P * i)))
 
         # front-end frame-to-frame estimates (stand-in for computeSiftTransformCU): GT motion with a
         # random-walk error per frame, so both the local and the global solve have drift to remove
@@ -131,6 +143,13 @@ class SyntheticStream:
                 recon.set_local_correspondences(s, self.local_corr.ptr.value + 32 * self.local_off[s], self.local_n[s])
         recon.set_global_correspondences(self.global_corr.ptr.value, len(self.global_host), self.global_prefix)
         recon.set_initial_pose(self.gt[0])
+        if self.raw_input:  # CUDAImageManager::process of every frame inside process_frame
+            from .io import Preprocessor, preprocess_options
+            W, H = self.cam.imageWidth, self.cam.imageHeight
+            self.preproc = Preprocessor((W, H), (W, H), (W, H), preprocess_options())
+            for i in range(self.F if frames is None else frames):
+                recon.set_frame_raw(i, self.depth_u16.ptr.value + 2 * W * H * i, self.rgbx.ptr.value + 4 * W * H * i)
+            recon.attach_preproc(self.preproc)
         if self.cache_source == "loop":  # storeFrame of every frame inside process_frame (the frame store is the source)
             recon.attach_cache(self.cache_store)
 

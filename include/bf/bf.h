@@ -254,6 +254,10 @@ int bf_synth_pose(uint32_t frame, float T[16]);
  * noiseSeed != 0 adds the depth noise model and 1 mm quantisation. */
 int bf_synth_render(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam,
                     uint32_t noiseSeed, uint32_t frame, float* d_depth, uint8_t* d_color);
+/* device: a rendered frame as the sensor delivers it (the .sens convention, SensorDataReader.cpp:104-107):
+ * depth ushort = rint(d * depthShift), 0 where d is invalid; colour RGBX bytes (alpha kept) */
+int bf_synth_to_raw(const float* d_depth, const uint8_t* d_color, uint32_t numPixels, float depthShift,
+                    uint16_t* d_depthU16, uint8_t* d_rgbx);
 /* same arithmetic on the host (tests) into host buffers */
 int bf_synth_render_host(const BFSynthScene* scene, const float T[16], const BFDepthCameraParams* cam,
                          uint32_t noiseSeed, uint32_t frame, float* depth, uint8_t* color);
@@ -302,6 +306,10 @@ typedef struct BFReconOptions {
                                     solve useVerification + VerifyTrajectoryCU; a failing submap is invalidated
                                     (OnlineBundler.cpp:145-159, 255-261, 351-360, 399-405) */
     BFVerifyOptions verify;      /* its thresholds (0 = defaults) */
+    uint32_t resultLag;          /* asyncBundling 1/2: 0 = a submap's poses are applied by the first frame that
+                                    finds its solves done (timing-dependent, like the reference's threads);
+                                    L > 0 = they are applied exactly L frames after the submap was issued
+                                    (waiting for them if needed), so the run's op sequence is repeatable */
 } BFReconOptions;
 
 typedef struct BFReconStats {
@@ -374,6 +382,9 @@ int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTrian
                           uint32_t* totalTriangles);
 /* summed device time / count of the renderKernel launches since the first call (enables the clock) */
 int bf_recon_render_time(bf_recon* r, double* ms, uint64_t* launches);
+/* the ray caster's device counters, summed over every render of the loop's scene (raycast
+ * bytes = 96 B per trilinear sample (8 voxels x 12 B) + 52 B of output per pixel) */
+int bf_recon_render_stats(bf_recon* r, BFRenderStats* out);
 /* bf_scene_export_blocks on the loop's scene */
 int bf_recon_export_blocks(bf_recon* r, int32_t* out4, uint32_t cap, uint32_t* n);
 /* debugHash-style dump of the loop's scene (same layout as bf_scene_export) */
@@ -396,6 +407,16 @@ typedef struct bf_cache bf_cache;
 int bf_recon_attach_cache(bf_recon* r, bf_cache* c);
 int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW,
                               uint32_t colorH);
+/* Per-frame input preprocessing inside the loop (DepthSensing.cpp:986: CUDAImageManager::process, then the
+ * frame's integration). With a preprocessor attached and raw sensor images registered for frame f,
+ * bf_recon_process_frame(f) first runs bf_preproc_run(raw depth, raw RGBX -> frame f's frame-store depth and
+ * colour of bf_recon_set_frame) on the preprocessor's stream; the scene stream and the attached cache are
+ * ordered after it by events, and the cache takes the raw sensor depth and colour as its source (as
+ * copyToBundling hands them to the bundler). The preprocessor is borrowed and must outlive the loop; its
+ * output size must be the integration size. */
+typedef struct bf_preproc bf_preproc;
+int bf_recon_attach_preproc(bf_recon* r, bf_preproc* p);
+int bf_recon_set_frame_raw(bf_recon* r, uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx);
 
 /* The end of the sequence (the render loop past the last input frame): OnlineBundler::processInput's
  * past-the-end branch (OnlineBundler.cpp:167-196), process() -> optimizeGlobal with isSequenceDone (:373-408)
@@ -578,7 +599,6 @@ int bf_params_preprocess_options(const bf_params* p, float depthShift, BFPreproc
 /* CUDAImageManager::process (CUDAImageManager.cpp:22-158): ushort depth -> metres, erodeDepthMap x2,
  * gaussFilterDepthMap, nearest resampling of depth and colour to the integration size. All image
  * pointers are device pointers; work is queued on the handle's stream. */
-typedef struct bf_preproc bf_preproc;
 int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_t colorH, uint32_t integrationW,
                       uint32_t integrationH, const BFPreprocessOptions* opt, bf_preproc** out);
 int bf_preproc_destroy(bf_preproc* p);

@@ -150,6 +150,21 @@ typedef struct BFSolveResult {
     uint32_t verifyOk;           /* ... and passed (VerifyTrajectoryCU's d_validOpt) */
 } BFSolveResult;
 
+/* Ray-caster counters summed over renders (bf_recon_render_stats). */
+typedef struct BFRenderStats {
+    uint64_t samples;      /* trilinear SDF samples (traversal, bisection, gradients) */
+    uint64_t voxelLoads;   /* 12-B voxel reads (a sample stops at its first zero-weight corner) */
+    uint64_t hashProbes;   /* hash lookups (a per-ray one-block cache skips repeats) */
+    uint64_t rays;         /* pixels with a splatted interval (marched) */
+    uint64_t splatBlocks;  /* visible blocks rasterised by the interval splat */
+    uint64_t splatAtomics; /* atomic min / max depth updates of the splat */
+    uint64_t renders;      /* renderKernel launches */
+    uint64_t pixels;       /* pixels over those launches */
+    uint64_t timedRenders; /* renders timed by the clocks below (enabled by the first bf_recon_render_time) */
+    double renderMs;       /* summed renderKernel device time of the timed renders */
+    double splatMs;        /* summed interval-splat device time of the timed renders */
+} BFRenderStats;
+
 /* Device-side counters used by the bench to compute algorithmic bytes. */
 typedef struct BFTsdfStats {
     uint64_t pixels;          /* P: pixels read by alloc (valid or not) */

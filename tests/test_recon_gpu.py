@@ -8,6 +8,8 @@
 * The loop's poses beat the front end's dead reckoning against ground truth (local + global BA
   with re-integration actually corrects the trajectory).
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -134,3 +136,55 @@ def test_loop_redoes_timed_out_persistent_pcg():
         np.testing.assert_array_equal(a[3], b[3])
     for a, b in zip(g0, g1):
         np.testing.assert_array_equal(a, b)
+
+
+def test_loop_preprocesses_raw_frames_in_order():
+    """CUDAImageManager::process inside the loop (bf_recon_attach_preproc + bf_recon_set_frame_raw): each raw
+    sensor frame (ushort depth, RGBX) is preprocessed into its frame-store slot when the loop reaches it, on
+    the preprocessor's stream, with the scene stream ordered after it. The loop must then do exactly what a
+    loop over frames preprocessed beforehand does: the same scene calls, trajectory and voxels, bit for bit,
+    in the synchronous and the asynchronous bundling modes."""
+    from bundlefusion_amd.io import Preprocessor, preprocess_options
+    F, W, H = 40, 160, 120
+    results = []
+    for mode in ("in_loop", "before"):
+        for async_ba in (0, 1):
+            st = SyntheticStream(F, width=W, height=H, drift=(0.05, 0.002), outliers=0.0, cache_source="synth",
+                                 raw_input=True)
+            if mode == "before":  # preprocess every frame up front into the frame store
+                pre = Preprocessor((W, H), (W, H), (W, H), preprocess_options())
+                P = W * H
+                for f in range(F):
+                    lib_ = bfa.lib()
+                    bfa.check(lib_.bf_preproc_run(pre.h, C.c_void_p(st.depth_u16.ptr.value + 2 * P * f),
+                                                  C.c_void_p(st.rgbx.ptr.value + 4 * P * f),
+                                                  C.c_void_p(st.depth.ptr.value + 4 * P * f),
+                                                  C.c_void_p(st.color.ptr.value + 4 * P * f)))
+                bfa.check(bfa.lib().bf_preproc_synchronize(pre.h))
+                st.raw_input = False  # attach() then registers no raw frames
+            params = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 16, num_blocks=1 << 15)
+            K = st.K
+            opts = recon_options(F, recordOps=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=st.cache_intrinsics,
+                                 maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2), maxKeyframes=K + 1,
+                                 asyncBundling=async_ba, resultLag=10 if async_ba else 0)
+            rc = Recon(params, st.cam, opts)
+            st.attach(rc)
+            for f in range(F):
+                rc.process_frame(f)
+            rc.finish()
+            rc.synchronize()
+            hash_, heap, hc, vox = rc.export()
+            results.append((mode, async_ba, rc.op_log(), rc.trajectory(F), hash_, heap, hc, vox))
+            rc.close()
+    for async_ba in (0, 1):
+        a = [r for r in results if r[1] == async_ba and r[0] == "in_loop"][0]
+        b = [r for r in results if r[1] == async_ba and r[0] == "before"][0]
+        assert len(a[2]) == len(b[2]) and len(a[2]) > F
+        for x, y in zip(a[2], b[2]):
+            assert x[0] == y[0] and x[1] == y[1]
+            np.testing.assert_array_equal(x[2], y[2])
+            np.testing.assert_array_equal(x[3], y[3])
+        np.testing.assert_array_equal(a[3], b[3])
+        assert a[6] == b[6]
+        np.testing.assert_array_equal(a[5], b[5])
+        assert a[4].tobytes() == b[4].tobytes() and a[7].tobytes() == b[7].tobytes()
