@@ -260,7 +260,9 @@ class BFAppOptions(C.Structure):  # include/bf/bf.h: the FriedLiver application 
                 ("enableTiming", C.c_int32), ("maxFrames", C.c_uint32), ("frontEndDriftRad", C.c_float),
                 ("frontEndDriftM", C.c_float), ("frontEndSeed", C.c_uint32), ("noFrontEndDrift", C.c_int32),
                 ("corrStride", C.c_uint32), ("corrDepthThresh", C.c_float), ("prefetchFrames", C.c_uint32),
-                ("decodeThreads", C.c_uint32), ("numSolveFramesBeforeExit", C.c_int32)]
+                ("decodeThreads", C.c_uint32), ("numSolveFramesBeforeExit", C.c_int32),
+                ("shardCount", C.c_uint32), ("shardIndex", C.c_uint32), ("shardChunk", C.c_float),
+                ("resultLag", C.c_uint32)]
 
 
 class BFAppInfo(C.Structure):

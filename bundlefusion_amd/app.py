@@ -42,7 +42,9 @@ class FriedLiver:
                  record_ops: bool = False, enable_timing: bool = False, max_frames: int = 0,
                  front_end_drift=(math.radians(0.05), 0.002), front_end_seed: int = 1, corr_stride: int = 16,
                  corr_depth_thresh: float = 0.02, prefetch_frames: int = 16, decode_threads: int = 4,
-                 num_solve_frames_before_exit: int = 0):
+                 num_solve_frames_before_exit: int = 0, shard=(1, 0), shard_chunk: float = 0.0, result_lag: int = 0):
+        """shard = (count, index): this rank's TSDF chunk-ownership shard of a multi-GPU run (attach the ranks'
+        communicator with set_comm before the first step)."""
         o = BFAppOptions()
         self._keep = [os.fsencode(sens_file) if sens_file else None, os.fsencode(output_dir) if output_dir else None]
         o.sensFile, o.outputDir = self._keep
@@ -57,6 +59,8 @@ class FriedLiver:
         o.corrStride, o.corrDepthThresh = int(corr_stride), float(corr_depth_thresh)
         o.prefetchFrames, o.decodeThreads = int(prefetch_frames), int(decode_threads)
         o.numSolveFramesBeforeExit = int(num_solve_frames_before_exit)
+        o.shardCount, o.shardIndex = int(shard[0]), int(shard[1])
+        o.shardChunk, o.resultLag = float(shard_chunk), int(result_lag)
         self.h = C.c_void_p()
         check(lib().bf_app_create(os.fsencode(app_params), os.fsencode(bundling_params), C.byref(o), C.byref(self.h)))
         self._info = BFAppInfo()
@@ -104,6 +108,12 @@ class FriedLiver:
         h = C.c_void_p()
         check(lib().bf_app_recon(self.h, C.byref(h)))
         return Recon.borrowed(h, self._info.hashParams, self._info.integrationCamera, owner=self)
+
+    def set_comm(self, comm):
+        """The ranks' RCCL communicator (dist.Comm): round-robin local solves + the global solve's pair-stat
+        all-reduce (bf_recon_set_comm on the app's loop); before the first step."""
+        self._comm = comm
+        self.recon.set_comm(comm)
 
     def front_end_pose(self, f: int) -> np.ndarray:
         T = (C.c_float * 16)()

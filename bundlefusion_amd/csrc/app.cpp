@@ -155,6 +155,7 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
     ro.enableTiming = o.enableTiming;
     ro.recordOps = o.recordOps;
     ro.asyncBundling = o.asyncBundling;
+    ro.resultLag = o.resultLag;
     ro.solver.denseDistThresh = flt(bp, "s_denseDistThresh", 0.15f);
     ro.solver.denseNormalThresh = flt(bp, "s_denseNormalThresh", 0.97f);
     ro.solver.denseColorThresh = flt(bp, "s_denseColorThresh", 0.1f);
@@ -196,7 +197,14 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
     cc.depthSigmaD = co.depthSigmaD;
     cc.depthSigmaR = co.depthSigmaR;
     cache_.reset(new Cache(cc, pre_));  // on the preprocessing stream: it reads that stream's buffers
-    recon_.reset(new Recon(info_.hashParams, nullptr, cam, ro));
+    BFSceneOptions so{};  // multi-GPU: this rank's TSDF chunk-ownership shard
+    so.shardCount = std::max(1u, o.shardCount);
+    so.shardIndex = o.shardIndex;
+    so.shardChunk = o.shardChunk;
+    BF_REQUIRE(so.shardIndex < so.shardCount, BF_ERR_ARG, "shardIndex >= shardCount");
+    shardCount_ = so.shardCount;
+    shardIndex_ = so.shardIndex;
+    recon_.reset(new Recon(info_.hashParams, &so, cam, ro));
     recon_->attachCache(cache_.get());
     const size_t ip = (size_t)iw * ih, dp = (size_t)si.depthWidth * si.depthHeight;
     dDepthU16_.alloc(dp);
@@ -436,9 +444,13 @@ void App::writeOutputs(BFAppResult& r) {
     if (nt) BF_HIP(hipMemcpy(tris.data(), dt.p, sizeof(BFMcTriangle) * nt, hipMemcpyDeviceToHost));
     const std::string stem = stem_of(sensPath_);
     const Mesh m = mesh_from_triangles(tris.data(), nt, nullptr);
-    mesh_save_ply(outDir_ + "/" + stem + ".ply", m);
+    // a TSDF shard meshes its own blocks: one .ply per rank, the trajectory outputs (identical on every
+    // rank) from shard 0 only
+    const std::string part = shardCount_ > 1 ? ".shard" + std::to_string(shardIndex_) + "of" + std::to_string(shardCount_) : "";
+    mesh_save_ply(outDir_ + "/" + stem + part + ".ply", m);
     r.meshVertices = (uint32_t)(m.vertices.size() / 3);
     r.meshFaces = (uint32_t)(m.faces.size() / 3);
+    if (shardIndex_ != 0) return;
     const std::string sensOut = opt_.overwriteSens ? sensPath_ : outDir_ + "/" + stem + ".optimized.sens";
     sens_save_with_trajectory(sensPath_, sensOut, traj.data(), traj.size());
     std::ofstream s(outDir_ + "/processed.txt");

@@ -55,6 +55,7 @@ private:
     uint32_t mcMaxTriangles_ = 3000000;
     uint32_t S_ = 10, L_ = 11;
     uint32_t localMinPerPair_ = 5;
+    uint32_t shardCount_ = 1, shardIndex_ = 0;  // this rank's TSDF shard (BFAppOptions)
     std::vector<BFMat4> sensPose_;      // the .sens trajectory (front end + EntryJ stand-in)
     std::vector<BFMat4> tinc_;
 

@@ -57,9 +57,31 @@ class HostGroup:
         self.dist.broadcast(t, src=0)
         return bytes(t.numpy().tobytes())
 
+    def agree(self, what: str, digest: bytes) -> None:
+        """Every rank must run on the same inputs (replicated bundling, one order of collectives): rank 0's
+        digest is broadcast and any rank holding another fails on every rank."""
+        if self.dist is None:
+            return
+        ref = self.broadcast_bytes(digest if self.rank == 0 else None, len(digest))
+        bad = self.max(0.0 if ref == digest else 1.0)
+        if bad:
+            raise RuntimeError(f"ranks disagree on {what}" + (" (this rank differs from rank 0)" if ref != digest else ""))
+
     def close(self):
         if self.dist is not None and self.dist.is_initialized():
             self.dist.destroy_process_group()
+
+
+def input_digest(paths, head_bytes: int = 1 << 20) -> bytes:
+    """32-byte digest of input files: size and first head_bytes of each (a .sens header and its first
+    frames, parameter files whole)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(str(os.path.getsize(p)).encode())
+        with open(p, "rb") as f:
+            h.update(f.read(head_bytes))
+    return h.digest()
 
 
 class Comm:

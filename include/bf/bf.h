@@ -641,6 +641,17 @@ typedef struct BFAppOptions {
     uint32_t prefetchFrames;    /* decoded frames ahead [16] */
     uint32_t decodeThreads;     /* [4] */
     int32_t numSolveFramesBeforeExit; /* overrides s_numSolveFramesBeforeExit when != 0 (-2: run no past-end phase) */
+    uint32_t shardCount;        /* multi-GPU (one app per GPU, every rank on the same .sens and parameters): the
+                                   TSDF is split into shardCount chunk-ownership shards (BFSceneOptions) and
+                                   this app owns shard shardIndex; 0 / 1: one GPU. Attach the ranks'
+                                   communicator with bf_recon_set_comm(bf_app_recon(...)) before the first step:
+                                   local solves then run round-robin by submap with a broadcast, the global
+                                   solve's pair statistics are all-reduced. The reference's
+                                   only multi-GPU mode is its fixed reconstruction / bundling device split
+                                   (DualGPU.h:108-134) */
+    uint32_t shardIndex;
+    float shardChunk;           /* ownership chunk edge, m (0: 1 m) */
+    uint32_t resultLag;         /* BFReconOptions.resultLag (0: poll) */
 } BFAppOptions;
 typedef struct BFAppInfo {      /* what the app derived from the parameters and the .sens header */
     BFHashParams hashParams;    /* (the 16-byte aligned members first) */

@@ -144,3 +144,44 @@ def test_shard_balance_report_shape():
     r = shard_balance(b, 0.004, [T], cam, (2, 4))
     assert r["blocks"] == 5000 and sum(r["G2"]["stored"]) == 5000 and sum(r["G4"]["stored"]) == 5000
     assert r["G2"]["stored_max_over_mean"] >= 1.0
+
+
+def _agree_worker(rank, world, port, paths, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from bundlefusion_amd.dist import input_digest
+    g = HostGroup(rank, world)
+    try:
+        g.agree("the .sens and parameter files", input_digest(paths[rank]))
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+    g.close()
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_app_ranks_agree_on_their_inputs(tmp_path, same):
+    """bench.py --sens under torchrun: every rank opens the same .sens and parameter files (the replicated
+    bundle adjustment and the collectives' sizes depend on them). The ranks compare input digests over gloo;
+    a rank with a different file fails the job on every rank."""
+    files = []
+    for r in range(2):
+        p = tmp_path / f"rank{r}.sens"
+        p.write_bytes(b"SENS" + bytes(range(256)) * 64 + (b"" if same or r == 0 else b"x"))
+        prm = tmp_path / f"params{r}.txt"
+        prm.write_text("s_SDFVoxelSize = 0.004f;\n")
+        files.append([str(p), str(prm)])
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, files, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if same:
+        assert res == [(0, "ok"), (1, "ok")]
+    else:
+        assert all("ranks disagree" in m for _, m in res)
+        assert "differs from rank 0" in res[1][1] and "differs" not in res[0][1]
