@@ -313,10 +313,12 @@ def roofline_ba(solo):
     b_asm = 2.0 * Np * 32.0 + 160.0 * N
     return {"bound": "latency", "kernel": "k_pcg_persist (all PCG iterations of a GN step in one launch)",
             "us_per_pcg_iter": per_iter_s * 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "alg_bytes_matrix_free": b_mf, "achieved_matrix_free": b_mf / per_iter_s / 1e9,
-            "frac_matrix_free": b_mf / per_iter_s / 1e9 / HBM_PEAK_GBS,
             "bytes_assembled": b_asm, "achieved_assembled": b_asm / per_iter_s / 1e9,
             "frac_assembled": b_asm / per_iter_s / 1e9 / HBM_PEAK_GBS,
+            "matrix_free_equivalent": {"bytes": b_mf, "GBps": b_mf / per_iter_s / 1e9,
+                                       "note": "SURVEY 8(d)'s matrix-free bytes per iteration over the same time: an "
+                                               "equivalent rate only (the assembled path does not move these bytes), "
+                                               "so no fraction of peak"},
             "note": "the assembled normal equations move ~50x fewer bytes per iteration than the matrix-free "
                     "formula: the iteration is bound by its two hand-offs (Ap to the finisher, p back), not HBM"}
 
@@ -565,14 +567,27 @@ def main():
                 break
     # counters are taken only from a profile of this same workload (tools/profile_bench.sh records
     # the workload string of the bench run it profiled and averages over its timed launches)
+    evals_pl = ss["batchEvals"] / launches
+    rmw_pl = ss["batchVoxelsRMW"] / launches
+    traffic_units = None
     if tj.get("workload") == workload and world == 1 and args.rehearse_shards <= 1:
-        traffic = tj.get("bytes_per_launch")
         traffic_src = os.path.relpath(args.traffic, REPO)
+        if "fetch_bytes_per_evaluation" in tj:
+            # the profile's per-unit rates x this run's own per-launch counts (identical to the profiled
+            # run's when the hand-off is repeatable: --result-lag)
+            traffic = tj["fetch_bytes_per_evaluation"] * evals_pl + tj["write_bytes_per_voxel_rmw"] * rmw_pl
+            traffic_units = {"fetch_bytes_per_evaluation": tj["fetch_bytes_per_evaluation"],
+                             "write_bytes_per_voxel_rmw": tj["write_bytes_per_voxel_rmw"],
+                             "profiled_units_per_launch": tj.get("units_per_launch"),
+                             "profiled_bytes_per_launch": tj.get("bytes_per_launch")}
+        else:
+            traffic = tj.get("bytes_per_launch")
         if "valu_insts_per_launch" in tj:  # VALU-issue bound of the same kernel (SQ_INSTS_VALU pass)
             us = per_launch_s * 1e6
-            valu = {"wave_insts_per_launch": tj["valu_insts_per_launch"],
+            vpl = tj["valu_insts_per_evaluation"] * evals_pl if "valu_insts_per_evaluation" in tj else tj["valu_insts_per_launch"]
+            valu = {"wave_insts_per_launch": vpl, "wave_insts_per_evaluation": tj.get("valu_insts_per_evaluation"),
                     "peak_wave_insts_per_us": VALU_PEAK_WAVE_INSTS_PER_US,
-                    "frac": tj["valu_insts_per_launch"] / (us * VALU_PEAK_WAVE_INSTS_PER_US), "source": traffic_src}
+                    "frac": vpl / (us * VALU_PEAK_WAVE_INSTS_PER_US), "source": traffic_src}
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
     solo = global_solve_timing(stream, K - 1)
@@ -624,7 +639,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
+                     "traffic_source": traffic_src, "traffic_units": traffic_units,
                      "hbm_frac_counters": (traffic / per_launch_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
                      "pass_frac": pass_bytes / launches / per_launch_s / 1e9 / HBM_PEAK_GBS,
                      "launches": launches, "avg_launch_us": per_launch_s * 1e6,

@@ -168,7 +168,7 @@ private:
     KernelClock integrateClock_;
     KernelClock renderClock_, splatClock_;
     DevBuf<unsigned long long> renderStats_;
-    DevBuf<uint2> blockMask_;  // per work-list entry of an op batch: which ops may update each z-half
+    DevBuf<uint4> blockMask_;  // per work-list entry of an op batch: which ops may update each z-half (uint2) / quarter
     DevBuf<uint32_t> blockBirth_;  // per heap block: epoch << 8 | (255 - first op) of the batch that allocated it
     DevBuf<uint8_t> candOp_;       // per alloc candidate of a batch: the integrate op that emitted it
     uint32_t batchEpoch_ = 0;

@@ -422,6 +422,71 @@ __device__ uint32_t block_may_update_halves(const HashArgs& A, const BFDepthCame
     return bits;
 }
 
+// block_may_update for the four z-quarters of the block (bit q: voxel z 2q, 2q + 1; BF_APPLY_QMASK): the
+// screen footprint and its depth bounds are the whole block's as in the halves form; a voxel level's
+// camera depth is affine in z, so each quarter's depth range is the corner depths' range at z = 0 shifted
+// by its two levels' offsets (conservative by the slack: the rounding of the shift is far below it).
+__device__ uint32_t block_may_update_quarters(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx,
+                                              int by, int bz, const float2* __restrict__ tiles,
+                                              const float2* __restrict__ tiles2) {
+    const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
+    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
+    float zb0 = INFINITY, zb1 = -INFINITY;  // camera depth of the z = 0 level's 4 corners
+    float xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
+        const f3 p = xform(Tinv, w);
+        if (!(p.z > 1e-3f)) return 15u;  // straddles the camera plane: keep
+        const float rz = __builtin_amdgcn_rcpf(p.z);
+        const float sx = p.x * cam.fx * rz + cam.mx, sy = p.y * cam.fy * rz + cam.my;
+        if (!(k & 4)) { zb0 = fminf(zb0, p.z); zb1 = fmaxf(zb1, p.z); }
+        xlo = fminf(xlo, sx); xhi = fmaxf(xhi, sx);
+        ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
+    }
+    const float dz = Tinv.m[10] * A.voxelSize;  // depth change per voxel level
+    const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
+    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
+    if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) return 0u;
+    const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
+    const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
+    const int tx0 = x0 / DEPTH_TILE, tx1 = x1 / DEPTH_TILE, ty0 = y0 / DEPTH_TILE, ty1 = y1 / DEPTH_TILE;
+    float dlo = INFINITY, dhi = -INFINITY;
+    if (tx1 - tx0 <= 2 && ty1 - ty0 <= 2) {
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float2 t = tiles[min(ty0 + j, ty1) * A.tilesW + min(tx0 + i, tx1)];
+                dlo = fminf(dlo, t.x);
+                dhi = fmaxf(dhi, t.y);
+            }
+    } else {
+        const int cx0 = x0 / DEPTH_TILE2, cx1 = x1 / DEPTH_TILE2, cy0 = y0 / DEPTH_TILE2, cy1 = y1 / DEPTH_TILE2;
+        if (cx1 - cx0 > 2 || cy1 - cy0 > 2) return 15u;  // very close block: keep
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float2 t = tiles2[min(cy0 + j, cy1) * A.tiles2W + min(cx0 + i, cx1)];
+                dlo = fminf(dlo, t.x);
+                dhi = fmaxf(dhi, t.y);
+            }
+    }
+    if (!(dlo <= dhi)) return 0u;
+    const float slack = 0.001f;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float a = dz * (float)(2 * q), b = dz * (float)(2 * q + 1);
+        const float zlo = zb0 + fminf(a, b), zhi = zb1 + fmaxf(a, b);
+        if (!(dlo * (1.0f - A.truncScale) >= zhi + A.truncation + slack) &&
+            !(dhi * (1.0f + A.truncScale) <= zlo - A.truncation - slack))
+            bits |= 1u << q;
+    }
+    return bits;
+}
+
 // isSDFBlockInCameraFrustumApprox (VoxelUtilHashSDF.h:322-326, DepthCameraUtil.h:95-107) with the
 // five IEEE divisions replaced by rcp products. The test is a set of comparisons of monotone
 // quotients against +-1 / 0 / 1, so the fast result is taken when every compared value is farther
@@ -1196,6 +1261,18 @@ constexpr uint32_t DC_DEPTH_KEY = 0xFF800000u;
 #ifndef BF_APPLY_WPE
 #define BF_APPLY_WPE 8
 #endif
+// work-list op masks per z-quarter of a block (two voxel slices) instead of per z-half: the voxel pass
+// then skips an op's slice pair that the band cull rules out (1: uint4 masks, 0: uint2)
+#ifndef BF_APPLY_QMASK
+#define BF_APPLY_QMASK 0
+#endif
+#if BF_APPLY_QMASK
+typedef uint4 OpMask;
+constexpr int MASK_PARTS = 4;
+#else
+typedef uint2 OpMask;
+constexpr int MASK_PARTS = 2;
+#endif
 __device__ __forceinline__ uint32_t dc_depth_word(float d, float maxDist) {
     return (d != -INFINITY && d < maxDist) ? (__float_as_uint(d) ^ DC_DEPTH_KEY) : 0u;
 }
@@ -1240,7 +1317,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
 // releases the batch's alloc dedup-set slots.
 __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
-                                                        uint2* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
+                                                        OpMask* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
                                                         uint32_t binCap) {
     {
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
@@ -1254,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
     // run per lane over its ops, it had every lane of a wave execute it whenever one lane's block
     // passed (the wave's 64 blocks almost always include one), ~3x the VALU of the compacted form
     __shared__ int4 s_bp[256];
-    __shared__ uint32_t s_mask[2][256];  // per z-half of the block (voxel z 0..3 / 4..7)
+    __shared__ uint32_t s_mask[MASK_PARTS][256];  // per z-half (voxel z 0..3 / 4..7) or z-quarter of the block
     __shared__ uint16_t s_q[4][64 * Scene::kMaxOps];  // per wave: lane << 5 | op
     __shared__ float s_tinv[Scene::kMaxOps][12];
     __shared__ const float2* s_tiles[2][Scene::kMaxOps];
@@ -1287,8 +1364,8 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         }
         // queue the wave's (block, op) pairs, then every lane takes one pair per round for the band cull
         s_bp[threadIdx.x] = bp;
-        s_mask[0][threadIdx.x] = 0u;
-        s_mask[1][threadIdx.x] = 0u;
+#pragma unroll
+        for (int q = 0; q < MASK_PARTS; q++) s_mask[q][threadIdx.x] = 0u;
         uint32_t qoff = (uint32_t)__popc(fr), qtot = qoff;
         for (int off = 1; off < 64; off <<= 1) {  // inclusive wave scan of the pair counts
             const uint32_t v = (uint32_t)__shfl_up((int)qoff, off);
@@ -1303,14 +1380,28 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             const int4 b = s_bp[src];
             const BFMat4 Ti = op_mat(s_tinv[k]);
             // the voxel pass applies an op to a block half by half (4 z-slices per round)
+#if BF_APPLY_QMASK
+            const uint32_t hb = block_may_update_quarters(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
+#else
             const uint32_t hb = block_may_update_halves(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
-            if (hb & 1u) atomicOr(&s_mask[0][src], 1u << k);
-            if (hb & 2u) atomicOr(&s_mask[1][src], 1u << k);
+#endif
+#pragma unroll
+            for (int q = 0; q < MASK_PARTS; q++)
+                if ((hb >> q) & 1u) atomicOr(&s_mask[q][src], 1u << k);
         }
         __syncthreads();
-        const uint2 hm = make_uint2(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x]);
+#if BF_APPLY_QMASK
+        const OpMask hm = make_uint4(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x], s_mask[2][threadIdx.x], s_mask[3][threadIdx.x]);
+        const uint32_t mask = hm.x | hm.y | hm.z | hm.w;
+        // op-quarters to apply; in half units (an op over a half costs about one unit either way)
+        const uint32_t cost = (uint32_t)(__popc(hm.x | hm.y) + __popc(hm.z | hm.w));
+        const uint32_t evq = (uint32_t)(__popc(hm.x) + __popc(hm.y) + __popc(hm.z) + __popc(hm.w));
+#else
+        const OpMask hm = make_uint2(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x]);
         const uint32_t mask = hm.x | hm.y;
         const uint32_t cost = (uint32_t)(__popc(hm.x) + __popc(hm.y));  // op-halves to apply
+        const uint32_t evq = 2u * cost;
+#endif
         const bool inb = mask != 0;
         // work list: one bin per cost (op-halves, two per bin), so the voxel pass can hand out the
         // costliest blocks first (entry order inside a bin is free: every block is applied by one wave)
@@ -1339,14 +1430,14 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         scanned += alloc ? 1 : 0;
         vis += keepVis ? 1 : 0;
         band += inb ? 1 : 0;
-        evals += (unsigned long long)cost;
+        evals += (unsigned long long)evq;
         __syncthreads();
     }
     flush_stats2(A.stats, S_SCANNED, scanned, S_VISIBLE, vis);
     __syncthreads();
     flush_stats2(A.stats, S_BAND, band, S_BBLOCKS, band);
     __syncthreads();
-    flush_stats2(A.stats, S_BEVAL, evals * (BF_VOXELS_PER_BLOCK / 2), -1, 0);
+    flush_stats2(A.stats, S_BEVAL, evals * (BF_VOXELS_PER_BLOCK / 4), -1, 0);  // evaluations: 128 voxels per op-quarter
 }
 
 // The batch's voxel pass: one wave per work-list block, lane = (x, y), ZC z-slices per round. For
@@ -1413,7 +1504,7 @@ struct RegVox {
 };
 // One op over the lane's ZR register voxels (see k_apply_ops); deint: the op's direction (wave-
 // uniform; a template split of the op body into two directions measured spills at 64 VGPRs).
-template <int ZR, int ZC>
+template <int ZR, int ZC, int TOFF = 0>
 __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Ti,
                                                 const float* bxy, __amdgpu_buffer_rsrc_t dcRsrc, uint32_t wc, float epsc,
                                                 int bzh, RegVox* rv, uint32_t& touched,
@@ -1472,7 +1563,7 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
             nwav += __builtin_amdgcn_ballot_w64(in) ? 64u : 0u;  // measurement build: update executions x 64 as voxels_rmw
 #endif
             if (!in) continue;
-            touched |= 1u << (z0 + zi);
+            touched |= 1u << (TOFF + z0 + zi);
             RegVox& v = rv[z0 + zi];
             if (deint) batch_deintegrate(v.s, v.w, v.c, sd, cc[zi]);
             else batch_integrate(v.s, v.w, v.c, sd, cc[zi], A.weightMax);
@@ -1493,7 +1584,7 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
 // values are re-read per block instead of kept live (no spills), counters are scalar.
 template <int ZR, int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
-    HashArgs A, BFDepthCameraParams cam, OpTable ops, const uint2* __restrict__ masks, uint32_t binCap) {
+    HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap) {
     static_assert(ZR * 2 == BF_SDF_BLOCK_SIZE, "one op mask per z-half of the block");
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -1511,8 +1602,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t blk = (uint32_t)e.w;
         const uint32_t lane = lane_id_here();
         const int lx = lane & 7, ly = lane >> 3;
-        const uint2 mh = masks[b];
+        const OpMask mh = masks[b];
+#if BF_APPLY_QMASK
+        const uint32_t maskQ[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(mh.x), (uint32_t)__builtin_amdgcn_readfirstlane(mh.y),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(mh.z), (uint32_t)__builtin_amdgcn_readfirstlane(mh.w)};
+        const uint32_t maskH[2] = {maskQ[0] | maskQ[1], maskQ[2] | maskQ[3]};
+#else
         const uint32_t maskH[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(mh.x), (uint32_t)__builtin_amdgcn_readfirstlane(mh.y)};
+#endif
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
         Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK) + lane;
@@ -1544,6 +1641,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav, diag);
                 diagPairs++;
                 diagEmpty += nupd == before;
+#elif BF_APPLY_QMASK
+                {   // the op's slice pairs in this half that the cull kept (wave-uniform)
+                    const bool deint = (ops.deintMask >> k) & 1u;
+                    const uint32_t sel = ((maskQ[h / 2] >> k) & 1u) | (((maskQ[h / 2 + 1] >> k) & 1u) << 1);
+#if BF_APPLY_QMASK == 2  // two pair bodies, each skipped on its own
+                    if (sel & 1u) apply_op_slices<2, 2, 0>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
+                    if (sel & 2u) apply_op_slices<2, 2, 2>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h + 2, rv + 2, touched, nupd, nwav);
+#else
+                    if (sel == 3u) apply_op_slices<ZR, ZC>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
+                    else if (sel == 1u) apply_op_slices<2, 2, 0>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
+                    else apply_op_slices<2, 2, 2>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h + 2, rv + 2, touched, nupd, nwav);
+#endif
+                }
 #else
                 apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
 #endif
@@ -1771,7 +1881,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     blockPos_.alloc(B_);
     visible_.alloc(B_);
     band_.alloc((size_t)kMaxOps * B_);  // op batches: one bin per op count
-    blockMask_.alloc((size_t)kMaxOps * B_);
+    blockMask_.alloc((size_t)kMaxOps * B_ * sizeof(OpMask) / sizeof(uint4) + 1);
     blockBirth_.alloc(B_);
     candOp_.alloc(cfg_.candCapacity);
     ctrl_.alloc(C_COUNT);
@@ -1990,12 +2100,12 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     A.tiles2 = tiles2_.p;
     A.tiles2W = tw2;
     k_compactify_ops<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
-                                                                  blockMask_.p, blockBirth_.p, epoch, B_);
+                                                                  reinterpret_cast<OpMask*>(blockMask_.p), blockBirth_.p, epoch, B_);
     BF_LAUNCH_CHECK();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, blockMask_.p, B_);
+    hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;

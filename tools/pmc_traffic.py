@@ -45,12 +45,22 @@ def main():
     if bench:
         res["workload"] = bench["config"]["workload"]
         res["averaged_over"] = f"last {last} dispatches (the bench's timed region)"
+        # per-unit rates (bench.py scales them by its own run's counts): fetched bytes per voxel-op
+        # evaluation (the gathers and the voxel reads both grow with it), written bytes per voxel
+        # read + written, VALU wave-instructions per evaluation
+        pl = bench["roofline"]["per_launch"]
+        res["units_per_launch"] = {"voxel_op_evaluations": pl["voxel_op_evaluations"], "voxels_rmw": pl["voxels_rmw"],
+                                   "work_list_blocks": pl["work_list_blocks"], "ops": pl["ops"]}
+        res["fetch_bytes_per_evaluation"] = fetch_b / max(1.0, pl["voxel_op_evaluations"])
+        res["write_bytes_per_voxel_rmw"] = write_b / max(1.0, pl["voxels_rmw"])
     if len(argv) > 4:
         v = per_dispatch(argv[4], "SQ_INSTS_VALU", rx)
         if last:
             v = v[-last:]
         res["dispatches_valu"] = len(v)
         res["valu_insts_per_launch"] = sum(v) / max(1, len(v))
+        if bench:
+            res["valu_insts_per_evaluation"] = res["valu_insts_per_launch"] / max(1.0, bench["roofline"]["per_launch"]["voxel_op_evaluations"])
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
