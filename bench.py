@@ -487,8 +487,18 @@ def main():
         # global BA: image-pair normal-equation blocks sharded over the ranks, one RCCL all-reduce
         # per GN iteration; the PCG then runs replicated on every GPU
         from bundlefusion_amd.dist import Comm
-        comm = Comm(group)
-        rc.set_comm(comm)
+        try:
+            comm = Comm(group)
+        except Exception as e:  # keep the job alive: bundling replicated on every rank instead
+            log(f"rank {rank}: RCCL communicator failed ({e!r}); global BA replicated")
+            comm = None
+        # every rank must take the same path (one order of collectives)
+        if group.max(0.0 if comm is not None else 1.0):
+            if comm is not None:
+                comm.close()
+            comm = None
+        if comm is not None:
+            rc.set_comm(comm)
     stream.attach(rc)
     log(f"setup {time.perf_counter() - t_setup:.1f}s: {F} frames, {K} keyframes, "
         f"{len(stream.global_host)} global correspondences")
