@@ -43,7 +43,7 @@ enum CtrlWord {
     K_VERIFY_OK,    // VerifyTrajectoryCU's d_validOpt (1 unless a pair failed)
     K_COUNT,
     K_NCHUNK = K_COUNT, K_NPAIRS_A,
-    K_PCG_ITERS0,  // K_PCG_ITERS before the GN step's PCG (k_pair_init): k_pcg_recover restarts from it
+    K_PCG_ITERS0,  // K_PCG_ITERS before the GN step's PCG (k_pair_init): the timeout recovery (pcg_recover) restarts from it
     K_CTRL_WORDS = 32  // words past K_COUNT are solver-internal (not part of the result)
 };
 static_assert(K_COUNT == Solver::kResultWords, "result words");
@@ -95,7 +95,7 @@ struct BA {
     uint2* aGran;  // [2][maxN][6] {value bits, tag}: k_pcg_persist's Ap hand-off
     uint32_t pairMode, shardCount, shardIndex, pairBound;
     uint32_t earlyOut;  // ENABLE_EARLY_OUT (SolverBundling.cu:7): PCG |p.Ap| < 5e-7 and GN max|delta| < 0.005 exits
-    float* poseBak;     // [maxN][6] rot | trans at the GN step's start (k_pair_init), for k_pcg_recover
+    float* poseBak;     // [maxN][6] rot | trans at the GN step's start (k_pair_init), for the timeout recovery (pcg_recover)
     unsigned long long spinTicks;  // bound of every k_pcg_persist wait (s_memrealtime ticks, 100 MHz)
 };
 
@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(WG) void k_pcg(BA a, float wSparse, int iter, int n
 // preconditioner, then initialises the row as PCGInit does (evalMinusJTFDevice + PCGInit_Kernel1,
 // SolverBundlingEquationsLie.h:63-148, SolverBundling.cu:755-794); the last workgroup sums r.z.
 // Row v (one wave); lane 0 also keeps the row's pose as it was before the GN step (a.poseBak, the
-// state k_pcg_recover restarts from)
+// state pcg_recover restarts from)
 __device__ void pair_init_row(const BA& a, float wSparse, uint32_t v, bool backup) {
     const uint32_t lane = lane_id();
     {
@@ -1237,7 +1237,7 @@ __global__ __launch_bounds__(WG) void k_pair_init(BA a, float wSparse) {
     pair_init_finish(a, sh);
 }
 
-// Ap of row v (one wave), handed to the finisher write-through: k_pcg_pairs and k_pcg_recover
+// Ap of row v (one wave), handed to the finisher write-through: k_pcg_pairs and pcg_recover
 __device__ void pair_row_ap(const BA& a, float wSparse, uint32_t v, unsigned long long* stg) {
     const uint32_t lane = lane_id();
     (void)stg;
@@ -1382,7 +1382,7 @@ constexpr uint32_t PP_SHADOW = 256;       // the workgroup without rows (see the
 constexpr int PP_OV = 4;                  // further entries per lane whose pair refs stay in registers (rows up to 448)
 constexpr uint32_t PP_DONE = 0x80000000u; // flag bit: the PCG loop ended (last iteration or timeout)
 constexpr uint32_t PP_ERR_TIMEOUT = 8u;   // K_ERROR bit 3 (BF_SOLVE_ERR_PCG_TIMEOUT)
-constexpr uint32_t PP_RECOVERED = 16u;    // K_ERROR bit 4 (BF_SOLVE_PCG_RECOVERED): k_pcg_recover redid the step
+constexpr uint32_t PP_RECOVERED = 16u;    // K_ERROR bit 4 (BF_SOLVE_PCG_RECOVERED): pcg_recover redid the step
 
 // The finisher workgroup of k_pcg_persist: R image rows per thread (R = 2: up to 513 images, every
 // vector in registers; R = 8: up to 2 049, p and r in registers, the preconditioner M in LDS (sM,
@@ -1825,8 +1825,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
     }
 }
 
-// After every k_pcg_persist launch, in stream order (one workgroup, returns at once unless the launch
-// timed out): a persistent launch that timed out (a hand-off never arrived, e.g. the grid was not
+// Inside the k_gn_end that follows every k_pcg_persist launch (one workgroup; a uniform test of the
+// error word unless the launch timed out): a persistent launch that timed out (a hand-off never arrived, e.g. the grid was not
 // co-resident) redoes the GN step's PCG here, from the state k_pair_init left: the poses it saved are
 // restored (the timed-out launch may have applied a partial Lie update), the rows are initialised
 // again, and every PCG iteration runs as k_pcg_pairs<RB> + its finisher would, in one workgroup (the
@@ -1834,9 +1834,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // step's result is bit-identical to BFSolverOptions.pcgLaunch = 1. Bit 3 of the result's error word is
 // then cleared and bit 4 set: the solve's result is valid and says that it took this path.
 template <int RB>
-__global__ __launch_bounds__(WG) void k_pcg_recover(BA a, float wSparse, int nLin) {
-    __shared__ float sh[WG];
-    if (!(a.ctrl[K_ERROR] & PP_ERR_TIMEOUT)) return;  // uniform
+__device__ __forceinline__ void pcg_recover(const BA& a, float* sh, float wSparse, int nLin) {
     const uint32_t wave = threadIdx.x >> 6, nw = WG / 64;
     for (uint32_t v = 1 + threadIdx.x; v < a.N; v += WG) {
         const float* b = a.poseBak + (size_t)v * 6;
@@ -2015,10 +2013,17 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
     }
 }
 
-// EvalGNConvergence (SolverBundling.cu:694-749) + the early-out test of solveBundlingStub (:1204-1210)
-__global__ void k_gn_end(BA a, int gnIndex, int nNonLin) {
+// EvalGNConvergence (SolverBundling.cu:694-749) + the early-out test of solveBundlingStub (:1204-1210).
+// After a persistent PCG launch (recoverRB = its finisher's rows per thread) it first redoes a GN step
+// whose launch timed out (pcg_recover; one uniform test otherwise, no launch of its own).
+template <int recoverRB>
+__global__ __launch_bounds__(WG) void k_gn_end(BA a, int gnIndex, int nNonLin, float wSparse, int nLin) {
     __shared__ float sh[WG];
     if (a.ctrl[K_GN_DONE]) return;
+    if (recoverRB && (a.ctrl[K_ERROR] & PP_ERR_TIMEOUT)) {
+        pcg_recover<recoverRB ? recoverRB : 2>(a, sh, wSparse, nLin);
+        __syncthreads();
+    }
     float m = 0.0f;
     for (uint32_t v = 1 + threadIdx.x; v < a.N; v += blockDim.x) {
         if (a.valid[v] == 0) continue;
@@ -2862,6 +2867,7 @@ void Solver::solve(const SolveArgs& s) {
             BF_LAUNCH_CHECK();
             if (comm_ && comm_->size() > 1) comm_->allreduceSum(pstat_.p, (size_t)bound * PSTAT, stream_);
             k_pair_init<<<pairRowGrid, WG, 0, stream_>>>(a, wS);
+            int recoverRB = 0;  // the finisher form of a persistent launch this GN step
             if (s.numImages <= (uint32_t)SMALL_N) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
@@ -2891,9 +2897,7 @@ void Solver::solve(const SolveArgs& s) {
                         BF_HIP(hipEventRecord(pg.ev, stream_));
                         pg.stream = stream_;
                         pcgEpoch_ = (pcgEpoch_ + 1) & 0xFFFFFFu;
-                        // a launch that timed out is redone in one workgroup (no-op otherwise)
-                        if (s.numImages <= 2u * WG + 1u) k_pcg_recover<2><<<1, WG, 0, stream_>>>(a, wS, (int)s.nLin);
-                        else k_pcg_recover<8><<<1, WG, 0, stream_>>>(a, wS, (int)s.nLin);
+                        recoverRB = s.numImages <= 2u * WG + 1u ? 2 : 8;  // k_gn_end redoes a timed-out step
                     }
 #ifdef BF_PCG_TIMING
                     {
@@ -3024,7 +3028,9 @@ void Solver::solve(const SolveArgs& s) {
                 }
             }
             BF_LAUNCH_CHECK();
-            k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
+            if (recoverRB == 2) k_gn_end<2><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
+            else if (recoverRB == 8) k_gn_end<8><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
+            else k_gn_end<0><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
             BF_LAUNCH_CHECK();
             continue;
         }
@@ -3042,7 +3048,7 @@ void Solver::solve(const SolveArgs& s) {
         BF_LAUNCH_CHECK();
         for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
         BF_LAUNCH_CHECK();
-        k_gn_end<<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin);
+        k_gn_end<0><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
         BF_LAUNCH_CHECK();
     }
     if (s.findMaxResidual) {

@@ -189,7 +189,8 @@ Recon::~Recon() {
         if (globalDone_[b]) (void)hipEventDestroy(globalDone_[b]);
     }
     if (cacheEv_) (void)hipEventDestroy(cacheEv_);
-    if (preEv_) (void)hipEventDestroy(preEv_);
+    for (hipEvent_t e : preEv_)
+        if (e) (void)hipEventDestroy(e);
     for (Pending& p : ring_) {
         if (p.done) (void)hipEventDestroy(p.done);
         for (void* q : {(void*)p.localT, (void*)p.globalT, (void*)p.valid, (void*)p.ctrl, (void*)p.localInit,
@@ -291,7 +292,15 @@ void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
 
 // reintegrate() (DepthSensing.cpp:854-902). The frame's fixes are applied as one op batch
 // (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls).
+void Recon::awaitPreproc(uint32_t f) {
+    if (!prePending_[f & 1]) return;
+    BF_HIP(hipStreamWaitEvent(sceneStream_, preEv_[f & 1], 0));
+    prePending_[f & 1] = false;
+}
+
 void Recon::runReintegrate() {
+    // the batch integrates the previous frame (pendingOp_): it reads that frame's preprocessed images
+    if (pendingInt_ && numFrames_ > 0) awaitPreproc(numFrames_ - 1);
     tm_->nextFixes(opt_.maxFrameFixes, ops_);
     traceQueue(2, 0, (uint32_t)ops_.size(), nullptr, &ops_);
     std::vector<VoxelOp>& batch = batch_;
@@ -369,6 +378,7 @@ void Recon::reintegrate() {
 
 void Recon::flushIntegrate() {
     if (!pendingInt_) return;
+    if (numFrames_ > 0) awaitPreproc(numFrames_ - 1);
     pendingInt_ = false;
     scene_->applyOps(&pendingOp_, 1, cam_);  // = integrate(); also fills the frame's tile cache
 }
@@ -867,7 +877,8 @@ void Recon::attachPreproc(Preproc* p) {
     BF_REQUIRE(!p || (p->integrationWidth() == cam_.imageWidth && p->integrationHeight() == cam_.imageHeight), BF_ERR_ARG,
                "preprocessing output size differs from the integration size");
     preproc_ = p;
-    if (p && !preEv_) BF_HIP(hipEventCreateWithFlags(&preEv_, hipEventDisableTiming));
+    for (hipEvent_t& e : preEv_)
+        if (p && !e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
 
 void Recon::setFrameRaw(uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx) {
@@ -883,8 +894,14 @@ void Recon::preprocessFrame(uint32_t f) {
     // the preprocessing buffers (raw / filtered sensor depth) are read by the previous frame's cache store
     if (cacheEv_ && cache_ && cache_->stream() != ps) BF_HIP(hipStreamWaitEvent(ps, cacheEv_, 0));
     preproc_->run(fr.rawDepth, fr.rawColor, const_cast<float*>(fr.depth), const_cast<uint8_t*>(fr.color));
-    BF_HIP(hipEventRecord(preEv_, ps));
-    BF_HIP(hipStreamWaitEvent(sceneStream_, preEv_, 0));
+    // the scene stream first reads frame f in the batch of frame f + 1 (its integration is deferred,
+    // pendingOp_), so it waits there (awaitPreproc), not here: frame f's preprocessing overlaps the
+    // voxel pass of frame f's batch
+    BF_HIP(hipEventRecord(preEv_[f & 1], ps));
+    prePending_[f & 1] = true;
+#ifdef BF_PRE_EARLY_WAIT  // A/B build: the scene stream waits right away (the first form)
+    awaitPreproc(f);
+#endif
     // copyToBundling: the cache takes the sensor-size raw depth and colour (as the FriedLiver app does)
     fr.srcDepth = preproc_->rawDepth();
     fr.srcColor = fr.rawColor;
@@ -895,7 +912,7 @@ void Recon::preprocessFrame(uint32_t f) {
 // Bundler::storeCachedFrame (Bundler.cpp:278-281) for frame f, on the cache's stream
 void Recon::storeCacheFrame(uint32_t f) {
     FrameRef& fr = frames_[f];
-    if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream()) BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_, 0));
+    if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream()) BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_[f & 1], 0));
     BF_REQUIRE(cache_->numFrames() == f, BF_ERR_STATE, "attached cache must hold exactly the frames before this one");
     const float* d = fr.srcDepth ? fr.srcDepth : fr.depth;
     const uint8_t* c = fr.srcDepth ? fr.srcColor : fr.color;

@@ -223,7 +223,9 @@ private:
     Cache* cache_ = nullptr;            // attached frame cache (borrowed)
     hipEvent_t cacheEv_ = nullptr;      // the last storeFrame on the cache's stream
     Preproc* preproc_ = nullptr;        // attached input preprocessing (borrowed)
-    hipEvent_t preEv_ = nullptr;        // the last preprocessing run on its stream
+    hipEvent_t preEv_[2] = {nullptr, nullptr};  // preprocessing of frames of each parity, on its stream
+    bool prePending_[2] = {false, false};        // recorded and not yet awaited by the scene stream
+    void awaitPreproc(uint32_t f);               // the scene stream after frame f's preprocessing
     void storeCacheFrame(uint32_t f);
     void preprocessFrame(uint32_t f);
 

@@ -467,7 +467,7 @@ def test_persistent_pcg_bit_identical(early_out):
 @pytest.mark.parametrize("case", ["k400", "dense72", "wide700"])
 def test_persistent_pcg_timeout_is_redone(case):
     """A persistent PCG launch whose hand-offs time out (forced: every wait bounded by 1 us through
-    BFSolverOptions.pcgSpinLimitUs) must not hand back its partial result. k_pcg_recover redoes the GN
+    BFSolverOptions.pcgSpinLimitUs) must not hand back its partial result. k_gn_end (pcg_recover) redoes the GN
     step from the state k_pair_init saved, with the per-iteration arithmetic: the error word says so
     (BF_SOLVE_PCG_RECOVERED, no fatal bit) and the poses, residual analysis and iteration counts are bit
     for bit those of one launch per PCG iteration (pcgLaunch = 1), on both persistent routes (<= 513 images,

@@ -100,7 +100,7 @@ def test_loop_corrects_drift(loop):
 def test_loop_redoes_timed_out_persistent_pcg():
     """The loop never consumes a timed-out persistent PCG solve. With every wait of the persistent launch
     bounded by 1 us (BFSolverOptions.pcgSpinLimitUs) each global solve above 64 keyframes times out and
-    its GN steps are redone in stream order (k_pcg_recover): the loop counts them (pcgRecoveries) and its
+    its GN steps are redone in stream order (pcg_recover in k_gn_end): the loop counts them (pcgRecoveries) and its
     scene calls, trajectory and submap poses are bit-identical to a loop that runs one launch per PCG
     iteration (pcgLaunch = 1)."""
     F, S = 216, 3  # 72 keyframes: the global solves from keyframe 65 on take the persistent route

@@ -1,14 +1,14 @@
 """In-loop timeline of the persistent global PCG (k_pcg_persist) from a rocprofv3 kernel trace (csv):
 per launch, the delay from the previous BA-stream kernel's end to its start (queueing behind the
 scene stream), its duration, and how much of [start, end] the scene stream's kernels overlapped.
-Usage: python3 tools/persist_gaps.py run_kernel_trace.csv"""
+Usage: python3 tools/persist_gaps.py run_kernel_trace.csv [first_pass] [passes]"""
 import csv
 import sys
 from collections import Counter
 
 
 def short(n):
-    n = n.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]
     return n.split("::")[-1]
 
 
@@ -17,8 +17,12 @@ K = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_
            for r in rows)
 ap = [k for k in K if k[2] == "k_apply_ops"]
 scene = ap[-1][3]
-t0 = ap[-200][0] if len(ap) > 200 else ap[0][0]
-K = [k for k in K if k[0] >= t0]
+# the window: voxel passes [first, first + count) (bench --steps 20 on the 5 000-frame stream: its timed
+# frames are passes 4 800 .. 4 999; the end-of-sequence phase follows)
+first = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(ap) - 200)
+count = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+t0, t1 = ap[first][0], ap[min(len(ap), first + count) - 1][1]
+K = [k for k in K if t0 <= k[0] <= t1]
 per = [k for k in K if k[2] == "k_pcg_persist"]
 if not per:
     sys.exit("no k_pcg_persist in the window")
@@ -60,3 +64,18 @@ for name in ("k_cache_geometry", "k_cache_intensity", "k_depth_u16", "k_erode", 
     m = lambda v: sum(v) / len(v) / 1e3 if v else float("nan")
     print("%s: %d launches, mean us %.1f; overlapping a k_apply_ops: %d (mean %.1f us); alone: %d (mean %.1f us)" %
           (name, len(ck), m([k[1] - k[0] for k in ck]), len(with_ap), m(with_ap), len(alone), m(alone)))
+
+# every BA-stream kernel: the idle time before it (since the previous BA kernel ended), by kernel name
+# (the waits for CU slots held by the scene stream's kernels), and its own duration
+gapby, durby, cnt = Counter(), Counter(), Counter()
+for p, k in zip(bak, bak[1:]):
+    g = k[0] - p[1]
+    if g > 200000:  # > 200 us: the stream was idle (no work queued), not waiting for slots
+        continue
+    gapby[k[2]] += g
+    durby[k[2]] += k[1] - k[0]
+    cnt[k[2]] += 1
+print("BA stream, per kernel name: launches, mean wait before (us), mean duration (us)")
+for n, c in cnt.most_common(14):
+    print("  %-22s %6d  wait %7.1f  dur %7.1f" % (n, c, gapby[n] / c / 1e3, durby[n] / c / 1e3))
+print("BA stream totals in the window: waits %.2f ms, kernels %.2f ms" % (sum(gapby.values()) / 1e6, sum(durby.values()) / 1e6))
