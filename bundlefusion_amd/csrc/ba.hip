@@ -714,9 +714,8 @@ __device__ __forceinline__ void diag_apply(const double* d, const double w[3], c
 // ---- per GN iteration -------------------------------------------------------------------------
 // convertLiePosesToMatricesCU (SolverBundling.cu:1114-1121); also resets the PCG state of this
 // GN iteration. gated: no-op once the GN loop converged on the device.
-__global__ void k_transforms(BA a, float wSparse, int useDense, int gated, int setState) {
-    if (gated && a.ctrl[K_GN_DONE]) return;
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.N; v += gridDim.x * blockDim.x) {
+__device__ __forceinline__ void transforms_rows(const BA& a, uint32_t first, uint32_t stride) {
+    for (uint32_t v = first; v < a.N; v += stride) {
         const m4 T = pose_to_matrix(mk3(a.rot[3 * v], a.rot[3 * v + 1], a.rot[3 * v + 2]),
                                     mk3(a.trans[3 * v], a.trans[3 * v + 1], a.trans[3 * v + 2]));
         const m4 Ti = inverse44(T);
@@ -727,6 +726,10 @@ __global__ void k_transforms(BA a, float wSparse, int useDense, int gated, int s
             ti[r] = make_float4(Ti.e[r * 4], Ti.e[r * 4 + 1], Ti.e[r * 4 + 2], Ti.e[r * 4 + 3]);
         }
     }
+}
+__global__ void k_transforms(BA a, float wSparse, int useDense, int gated, int setState) {
+    if (gated && a.ctrl[K_GN_DONE]) return;
+    transforms_rows(a, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
     if (setState && blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctrl[K_PCG_DONE] = 0;
         a.ctrl[K_TICKET] = 0;
@@ -2017,7 +2020,9 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
 // After a persistent PCG launch (recoverRB = its finisher's rows per thread) it first redoes a GN step
 // whose launch timed out (pcg_recover; one uniform test otherwise, no launch of its own).
 template <int recoverRB>
-__global__ __launch_bounds__(WG) void k_gn_end(BA a, int gnIndex, int nNonLin, float wSparse, int nLin) {
+// nextW > 0: the next GN step is a sparse pair-mode step of weight nextW, whose k_transforms this launch
+// does when the loop goes on (one launch fewer per GN step)
+__global__ __launch_bounds__(WG) void k_gn_end(BA a, int gnIndex, int nNonLin, float wSparse, int nLin, float nextW) {
     __shared__ float sh[WG];
     if (a.ctrl[K_GN_DONE]) return;
     if (recoverRB && (a.ctrl[K_ERROR] & PP_ERR_TIMEOUT)) {
@@ -2038,9 +2043,19 @@ __global__ __launch_bounds__(WG) void k_gn_end(BA a, int gnIndex, int nNonLin, f
         if ((int)threadIdx.x < s) sh[threadIdx.x] = fmaxf(sh[threadIdx.x], sh[threadIdx.x + s]);
         __syncthreads();
     }
+    const bool done = a.earlyOut && gnIndex < nNonLin - 1 && sh[0] < 0.005f;
     if (threadIdx.x == 0) {
         a.ctrl[K_GN_ITERS]++;
-        if (a.earlyOut && gnIndex < nNonLin - 1 && sh[0] < 0.005f) a.ctrl[K_GN_DONE] = 1;
+        if (done) a.ctrl[K_GN_DONE] = 1;
+    }
+    if (nextW > 0.0f && !done) {  // k_transforms(a, nextW, 0, 1, 1) of the next step
+        transforms_rows(a, threadIdx.x, blockDim.x);
+        if (threadIdx.x == 0) {
+            a.ctrl[K_PCG_DONE] = 0;
+            a.ctrl[K_TICKET] = 0;
+            a.ctrl[K_LAST_W] = __float_as_uint(nextW);
+            a.ctrl[K_USE_DENSE] = 0u;
+        }
     }
 }
 
@@ -2847,12 +2862,18 @@ void Solver::solve(const SolveArgs& s) {
     }
     if (pairMode) k_pair_gather<<<(unsigned)numCUs_ * 4, WG, 0, stream_>>>(a);
     const unsigned pairRowGrid = std::max(1u, std::min(div_up(s.numImages, WG / 64), (unsigned)numCUs_ * 4));
+    bool transformsDone = false;
     for (uint32_t it = 0; it < s.nNonLin; it++) {
         const float wS = s.wSparse[it];
         const float wD = s.wDenseDepth ? s.wDenseDepth[it] : 0.0f;
         const float wC = s.wDenseColor ? s.wDenseColor[it] : 0.0f;
         const bool dense = (wD > 0.0f || wC > 0.0f) && s.cache != nullptr;
-        k_transforms<<<div_up(s.numImages, 64), 64, 0, stream_>>>(a, wS, dense ? 1 : 0, 1, 1);
+        // the next sparse pair-mode step's transforms come from this step's k_gn_end
+        const bool nextDense = it + 1 < s.nNonLin && s.cache != nullptr &&
+                               ((s.wDenseDepth && s.wDenseDepth[it + 1] > 0.0f) || (s.wDenseColor && s.wDenseColor[it + 1] > 0.0f));
+        const float nextW = (pairMode && it + 1 < s.nNonLin && !nextDense && s.wSparse[it + 1] > 0.0f) ? s.wSparse[it + 1] : 0.0f;
+        if (!transformsDone) k_transforms<<<div_up(s.numImages, 64), 64, 0, stream_>>>(a, wS, dense ? 1 : 0, 1, 1);
+        transformsDone = nextW > 0.0f;
         if (pairMode) {
             if (dense) {
                 k_dense_reset<<<64, WG, 0, stream_>>>(a);
@@ -3028,9 +3049,9 @@ void Solver::solve(const SolveArgs& s) {
                 }
             }
             BF_LAUNCH_CHECK();
-            if (recoverRB == 2) k_gn_end<2><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
-            else if (recoverRB == 8) k_gn_end<8><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
-            else k_gn_end<0><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
+            if (recoverRB == 2) k_gn_end<2><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin, nextW);
+            else if (recoverRB == 8) k_gn_end<8><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin, nextW);
+            else k_gn_end<0><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin, nextW);
             BF_LAUNCH_CHECK();
             continue;
         }
@@ -3048,8 +3069,9 @@ void Solver::solve(const SolveArgs& s) {
         BF_LAUNCH_CHECK();
         for (uint32_t li = 0; li < s.nLin; li++) k_pcg<<<rowGrid, WG, 0, stream_>>>(a, wS, (int)li, (int)s.nLin);
         BF_LAUNCH_CHECK();
-        k_gn_end<0><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin);
+        k_gn_end<0><<<1, WG, 0, stream_>>>(a, (int)it, (int)s.nNonLin, wS, (int)s.nLin, 0.0f);
         BF_LAUNCH_CHECK();
+        transformsDone = false;
     }
     if (s.findMaxResidual) {
         // T from the final poses (ctrl untouched), then computeMaxResidual with the weightSparse of

@@ -914,6 +914,14 @@ void Recon::storeCacheFrame(uint32_t f) {
     FrameRef& fr = frames_[f];
     if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream()) BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_[f & 1], 0));
     BF_REQUIRE(cache_->numFrames() == f, BF_ERR_STATE, "attached cache must hold exactly the frames before this one");
+    // multi-GPU: a rank solves only its own local submaps (round-robin, issueSubmap), so it builds the cache
+    // frames of those and the keyframes (the dense end solve runs on every rank); other slots stay empty
+    const uint32_t S = opt_.submapSize;
+    if (comm_ && comm_->size() > 1 && f % S != 0 && (f / S) % (uint32_t)comm_->size() != (uint32_t)comm_->rank()) {
+        cache_->increment();
+        fr.cache = BFCachedFrame{};
+        return;
+    }
     const float* d = fr.srcDepth ? fr.srcDepth : fr.depth;
     const uint8_t* c = fr.srcDepth ? fr.srcColor : fr.color;
     const uint32_t w = fr.srcDepth ? fr.srcW : cam_.imageWidth, h = fr.srcDepth ? fr.srcH : cam_.imageHeight;
