@@ -32,6 +32,11 @@ __device__ __forceinline__ uint32_t enc_f(float f) {  // monotone float -> uint3
     const uint32_t b = __float_as_uint(f);
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
 __device__ __forceinline__ float dec_f(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); }
 
 struct RayArgs {
@@ -115,13 +120,17 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
         const uint32_t w = (uint32_t)(x1 - x0 + 1), npx = w * (uint32_t)(y1 - y0 + 1);
         const uint32_t emin = enc_f(dwMin), emax = enc_f(dwMax);
         quads++;
-        atoms += npx * ((minOk ? 1u : 0u) + (maxOk ? 1u : 0u));
+        // ~30 quads cover a pixel: read first and issue the atomic only where it can still change the
+        // value (the targets only decrease / increase, so a stale read can only cause a redundant atomic)
         for (uint32_t k = lane; k < npx; k += 64) {
             const uint32_t idx = (uint32_t)(y0 + (int)(k / w)) * rp.width + (uint32_t)(x0 + (int)(k % w));
-            if (minOk) atomicMin(&smin[idx], emin);
-            if (maxOk) atomicMax(&smax[idx], emax);
+            const uint32_t cmn = minOk ? __builtin_nontemporal_load(&smin[idx]) : 0u;
+            const uint32_t cmx = maxOk ? __builtin_nontemporal_load(&smax[idx]) : 0xFFFFFFFFu;
+            if (minOk && emin < cmn) { atomicMin(&smin[idx], emin); atoms++; }
+            if (maxOk && emax > cmx) { atomicMax(&smax[idx], emax); atoms++; }
         }
     }
+    atoms = wave_sum_u32(atoms);  // per lane above
     if (lane == 0 && quads) {
         atomicAdd(&stats[RS_QUADS], (unsigned long long)quads);
         atomicAdd(&stats[RS_ATOMICS], (unsigned long long)atoms);
@@ -156,11 +165,28 @@ __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 po
     color = *reinterpret_cast<const uint32_t*>(vp->color);
 }
 
+// the voxel of worldPos without loading it: nullptr for a free block (deleteVoxel: sdf 0, weight 0)
+__device__ __forceinline__ const BFVoxel* voxel_ptr(const RayArgs& R, BlockCache& c, f3 pos) {
+    const i3 v = world_to_vvox(pos, R.voxelSize);
+    const i3 b = vvox_to_block(v);
+    if (b.x != c.bx || b.y != c.by || b.z != c.bz) {
+        c.bx = b.x; c.by = b.y; c.bz = b.z;
+        c.ptr = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
+        c.probes++;
+    }
+    if (c.ptr == BF_FREE_ENTRY) return nullptr;
+    int lx = v.x % BF_SDF_BLOCK_SIZE, ly = v.y % BF_SDF_BLOCK_SIZE, lz = v.z % BF_SDF_BLOCK_SIZE;
+    if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
+    if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
+    if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
+    return R.voxels + (size_t)c.ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+}
+
 __device__ __forceinline__ float frac1(float v) { return v - floorf(v); }
 
 // trilinearInterpolationSimpleFastFast (RayCastSDFUtil.h:96-116). On a zero-weight corner it returns
 // false with dist holding the partial sum, which gradientForPoint then uses as the reference does.
-__device__ bool trilinear(const RayArgs& R, BlockCache& c, f3 pos, float& dist, uint32_t& rgb) {
+__device__ __forceinline__ bool trilinear(const RayArgs& R, BlockCache& c, f3 pos, float& dist, uint32_t& rgb) {
     const float oSet = R.voxelSize;
     const f3 posDual = pos - mk3(oSet / 2.0f, oSet / 2.0f, oSet / 2.0f);
     const f3 vv = pos / R.voxelSize;
@@ -168,13 +194,32 @@ __device__ bool trilinear(const RayArgs& R, BlockCache& c, f3 pos, float& dist, 
     const f3 weight = mk3(frac1(vv.x), frac1(vv.y), frac1(vv.z));
     dist = 0.0f;
     f3 colorFloat = mk3(0.0f, 0.0f, 0.0f);
-    const f3 offs[8] = {mk3(0.0f, 0.0f, 0.0f), mk3(oSet, 0.0f, 0.0f), mk3(0.0f, oSet, 0.0f), mk3(0.0f, 0.0f, oSet),
-                        mk3(oSet, oSet, 0.0f), mk3(0.0f, oSet, oSet), mk3(oSet, 0.0f, oSet), mk3(oSet, oSet, oSet)};
+    // corner k's offset (the reference's order: 000, 100, 010, 001, 110, 011, 101, 111), selected per
+    // component rather than read from a table (an offset table was kept in scratch)
+    auto offs = [&](int k) {
+        return mk3((k == 1 || k == 4 || k == 6 || k == 7) ? oSet : 0.0f, (k == 2 || k == 4 || k == 5 || k == 7) ? oSet : 0.0f,
+                   (k == 3 || k == 5 || k == 6 || k == 7) ? oSet : 0.0f);
+    };
+    // the 8 corners' voxels located first (hash probes only where the block changes), then loaded
+    // together: the reference reads them one after another and stops at the first zero weight, which
+    // made each load wait for the previous one; the sums below keep its order and its stop
+    float vs[8], vw[8];
+    uint32_t vc[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        float sdf, w;
-        uint32_t col;
-        get_voxel(R, c, posDual + offs[k], sdf, w, col);
+        const BFVoxel* vp = voxel_ptr(R, c, posDual + offs(k));
+        vs[k] = 0.0f; vw[k] = 0.0f; vc[k] = 0u;
+        if (vp) {
+            vs[k] = vp->sdf;
+            vw[k] = vp->weight;
+            vc[k] = *reinterpret_cast<const uint32_t*>(vp->color);
+            c.loads++;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const float sdf = vs[k], w = vw[k];
+        const uint32_t col = vc[k];
         if (w == 0.0f) return false;
         const f3 vColor = mk3((float)(col & 0xFF), (float)((col >> 8) & 0xFF), (float)((col >> 16) & 0xFF));
         const float a = (k == 1 || k == 4 || k == 6 || k == 7) ? weight.x : 1.0f - weight.x;
@@ -190,7 +235,7 @@ __device__ bool trilinear(const RayArgs& R, BlockCache& c, f3 pos, float& dist, 
 }
 
 // gradientForPoint (RayCastSDFUtil.h:172-194)
-__device__ f3 gradient_for_point(const RayArgs& R, BlockCache& c, f3 pos) {
+__device__ __forceinline__ f3 gradient_for_point(const RayArgs& R, BlockCache& c, f3 pos) {
     const float vs = R.voxelSize;
     const f3 offset = mk3(vs, vs, vs);
     float dp00, d0p0, d00p, d100, d010, d001;
@@ -208,7 +253,7 @@ __device__ f3 gradient_for_point(const RayArgs& R, BlockCache& c, f3 pos) {
 }
 
 // renderKernel (CUDARayCastSDF.cu:17-57) + traverseCoarseGridSimpleSampleAll (RayCastSDFUtil.h:224-290)
-__device__ void render_pixel(const RayArgs& R, const BFRayCastParams& rp, BlockCache& cache, uint32_t x, uint32_t y,
+__device__ __forceinline__ void render_pixel(const RayArgs& R, const BFRayCastParams& rp, BlockCache& cache, uint32_t x, uint32_t y,
                              const uint32_t* __restrict__ smin, const uint32_t* __restrict__ smax, float* d_depth,
                              float4* d_depth4, float4* d_normals, float4* d_colors, float* outMin, float* outMax, bool& rayed) {
     const uint32_t pix = y * rp.width + x;
@@ -284,11 +329,6 @@ __device__ void render_pixel(const RayArgs& R, const BFRayCastParams& rp, BlockC
             rayCurrent += rp.rayIncrement;
         }
     }
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-    return v;
 }
 // stats: [RS_SAMPLES] trilinear samples, [RS_LOADS] voxel loads, [RS_PROBES] hash probes, [RS_RAYS] marched rays
 __global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,

@@ -5,6 +5,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 T=$1; shift
 mkdir -p gpurun_out/$T
-timeout -k 10 700 python -u -m pytest tests/test_ba_gpu.py tests/test_recon_gpu.py tests/test_verify_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" gpurun_out/$T/tests.log | head; tail -30 gpurun_out/$T/tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_ba_gpu.py tests/test_recon_gpu.py tests/test_verify_gpu.py tests/test_raycast_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" gpurun_out/$T/tests.log | head; tail -30 gpurun_out/$T/tests.log; exit 1; }
 tail -1 gpurun_out/$T/tests.log
 bash tools/gpu_lag.sh $T "$@"
