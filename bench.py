@@ -416,7 +416,7 @@ def main():
                     help="feed the rendered float depth straight into the loop instead of raw sensor frames "
                          "(ushort depth, RGBX) preprocessed per frame inside it (CUDAImageManager::process: erode x2, "
                          "bilateral filter, resample; DepthSensing.cpp:986)")
-    ap.add_argument("--result-lag", type=int, default=10,
+    ap.add_argument("--result-lag", type=int, default=20,
                     help="frames after its issue at which a submap's solved poses are applied (waiting if needed): "
                          "the run's op sequence is then repeatable; 0: picked up by polling as soon as done "
                          "(timing-dependent, like the reference's bundling thread)")

@@ -29,7 +29,7 @@ public:
     // (CUDAImageManager.h:223-227): d_depthInputRaw (the two erosion passes end in it) and
     // d_depthInputFiltered (the bilateral filter's output; the raw image when the filter is off)
     const float* rawDepth() const { return a_.p; }
-    const float* filteredDepth() const { return opt_.depthFilter ? b_.p : a_.p; }
+    const float* filteredDepth() const { return filteredOut_ ? filteredOut_ : (opt_.depthFilter ? b_.p : a_.p); }
 
 private:
     uint32_t dw_, dh_, cw_, ch_, iw_, ih_;
@@ -37,6 +37,7 @@ private:
     hipStream_t stream_;
     GaussTable gauss_{};
     DevBuf<float> a_, b_;
+    const float* filteredOut_ = nullptr;  // the last run's filtered image (depthOut when no resampling)
 };
 
 }  // namespace bf

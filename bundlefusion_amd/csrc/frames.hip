@@ -45,13 +45,32 @@ __device__ __forceinline__ void stage_tile(float (*t)[TX + 2 * MAXR], const floa
     }
     __syncthreads();
 }
+// the same from the sensor's ushort depth, converted as k_depth_u16 does (the first erosion's input)
+template <int R>
+__device__ __forceinline__ void stage_tile_u16(float (*t)[TX + 2 * MAXR], const uint16_t* __restrict__ in, int W, int H,
+                                               float shift) {
+    const int x0 = blockIdx.x * TX - R, y0 = blockIdx.y * TY - R;
+    for (int k = threadIdx.x; k < (TX + 2 * R) * (TY + 2 * R); k += blockDim.x) {
+        const int ty = k / (TX + 2 * R), tx = k % (TX + 2 * R);
+        const int x = x0 + tx, y = y0 + ty;
+        float v = 0.0f;
+        if (x >= 0 && x < W && y >= 0 && y < H) {
+            const uint16_t d = in[y * W + x];
+            v = d == 0 ? -INFINITY : (float)d / shift;
+        }
+        t[ty][tx] = v;
+    }
+    __syncthreads();
+}
 
 // erodeDepthMapDevice (CUDAImageUtil.cu:701-739)
+// inU16 != nullptr: the input is the sensor's ushort depth (k_depth_u16 folded into the staging)
 template <int R>
 __global__ __launch_bounds__(256) void k_erode(float* __restrict__ out, const float* __restrict__ in, int W, int H, float dThresh,
-                                               float fracReq) {
+                                               float fracReq, const uint16_t* __restrict__ inU16, float shift) {
     __shared__ float t[TY + 2 * MAXR][TX + 2 * MAXR];
-    stage_tile<R>(t, in, W, H);
+    if (inU16) stage_tile_u16<R>(t, inU16, W, H, shift);
+    else stage_tile<R>(t, in, W, H);
     const int lx = threadIdx.x % TX, ly = threadIdx.x / TX;
     const int x = blockIdx.x * TX + lx, y = blockIdx.y * TY + ly;
     if (x >= W || y >= H) return;
@@ -106,8 +125,9 @@ __global__ __launch_bounds__(256) void k_resample(T* __restrict__ out, uint32_t 
 }
 
 template <int R>
-void launch_erode(float* out, const float* in, int W, int H, float dT, float fr, hipStream_t s) {
-    k_erode<R><<<dim3(div_up(W, TX), div_up(H, TY)), 256, 0, s>>>(out, in, W, H, dT, fr);
+void launch_erode(float* out, const float* in, int W, int H, float dT, float fr, hipStream_t s, const uint16_t* inU16 = nullptr,
+                  float shift = 1.0f) {
+    k_erode<R><<<dim3(div_up(W, TX), div_up(H, TY)), 256, 0, s>>>(out, in, W, H, dT, fr, inU16, shift);
 }
 template <int R>
 void launch_gauss(float* out, const float* in, int W, int H, float sR, const GaussTable& g, hipStream_t s) {
@@ -145,27 +165,34 @@ void Preproc::run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut
     const uint32_t n = dw_ * dh_;
     float* raw = a_.p;
     float* filtered = b_.p;
-    k_depth_u16<<<div_up(n, 256), 256, 0, stream_>>>(depthU16, raw, n, opt_.depthShift);
-    BF_LAUNCH_CHECK();
     const int W = (int)dw_, H = (int)dh_;
-    if (opt_.erode) {
+    if (opt_.erode) {  // the first erosion converts the ushort depth as it stages its tile
         for (int i = 0; i < 2; i++) {
             float* out = (i % 2 == 0) ? filtered : raw;
             const float* in = (i % 2 == 0) ? raw : filtered;
+            const uint16_t* u = i == 0 ? depthU16 : nullptr;
+            const float sh = opt_.depthShift;
             switch (opt_.erodeStructureSize) {
-                case 0: launch_erode<0>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                case 1: launch_erode<1>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                case 2: launch_erode<2>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                case 3: launch_erode<3>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                case 4: launch_erode<4>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                case 5: launch_erode<5>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                case 6: launch_erode<6>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
-                default: launch_erode<7>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_); break;
+                case 0: launch_erode<0>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                case 1: launch_erode<1>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                case 2: launch_erode<2>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                case 3: launch_erode<3>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                case 4: launch_erode<4>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                case 5: launch_erode<5>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                case 6: launch_erode<6>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
+                default: launch_erode<7>(out, in, W, H, opt_.erodeDepthThresh, opt_.erodeFraction, stream_, u, sh); break;
             }
             BF_LAUNCH_CHECK();
         }
+    } else {
+        k_depth_u16<<<div_up(n, 256), 256, 0, stream_>>>(depthU16, raw, n, opt_.depthShift);
+        BF_LAUNCH_CHECK();
     }
     const float* result = raw;
+    // no resampling: the filter writes straight into the output (it is then the filtered image too)
+    const bool direct = dw_ == iw_ && dh_ == ih_ && depthOut != nullptr;
+    if (direct && opt_.depthFilter) filtered = depthOut;
+    filteredOut_ = opt_.depthFilter ? filtered : raw;
     if (opt_.depthFilter) {
         switch (gauss_.radius) {
             case 0: launch_gauss<0>(filtered, raw, W, H, opt_.sigmaR, gauss_, stream_); break;
@@ -180,8 +207,8 @@ void Preproc::run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut
         BF_LAUNCH_CHECK();
         result = filtered;
     }
-    if (dw_ == iw_ && dh_ == ih_) {
-        BF_HIP(hipMemcpyAsync(depthOut, result, sizeof(float) * n, hipMemcpyDeviceToDevice, stream_));
+    if (direct) {
+        if (result != depthOut) BF_HIP(hipMemcpyAsync(depthOut, result, sizeof(float) * n, hipMemcpyDeviceToDevice, stream_));
     } else {
         k_resample<float><<<dim3(div_up(iw_, TX), div_up(ih_, TY)), 256, 0, stream_>>>(depthOut, iw_, ih_, result, dw_, dh_);
         BF_LAUNCH_CHECK();

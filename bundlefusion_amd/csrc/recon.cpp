@@ -893,7 +893,11 @@ void Recon::preprocessFrame(uint32_t f) {
     const hipStream_t ps = preproc_->stream();
     // the preprocessing buffers (raw / filtered sensor depth) are read by the previous frame's cache store
     if (cacheEv_ && cache_ && cache_->stream() != ps) BF_HIP(hipStreamWaitEvent(ps, cacheEv_, 0));
-    preproc_->run(fr.rawDepth, fr.rawColor, const_cast<float*>(fr.depth), const_cast<uint8_t*>(fr.color));
+    // colour at the integration size already: the loop reads the raw colour itself (no copy); the raw
+    // images stay registered for as long as the frame store's
+    const bool colorAsIs = preproc_->colorWidth() == cam_.imageWidth && preproc_->colorHeight() == cam_.imageHeight;
+    preproc_->run(fr.rawDepth, fr.rawColor, const_cast<float*>(fr.depth), colorAsIs ? nullptr : const_cast<uint8_t*>(fr.color));
+    if (colorAsIs) fr.color = fr.rawColor;
     // the scene stream first reads frame f in the batch of frame f + 1 (its integration is deferred,
     // pendingOp_), so it waits there (awaitPreproc), not here: frame f's preprocessing overlaps the
     // voxel pass of frame f's batch

@@ -413,7 +413,8 @@ int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const
  * colour of bf_recon_set_frame) on the preprocessor's stream; the scene stream and the attached cache are
  * ordered after it by events, and the cache takes the raw sensor depth and colour as its source (as
  * copyToBundling hands them to the bundler). The preprocessor is borrowed and must outlive the loop; its
- * output size must be the integration size. */
+ * output size must be the integration size. The raw images must stay valid as long as the frame store's
+ * (a raw colour image of the integration size is integrated from directly, without a copy). */
 typedef struct bf_preproc bf_preproc;
 int bf_recon_attach_preproc(bf_recon* r, bf_preproc* p);
 int bf_recon_set_frame_raw(bf_recon* r, uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx);
