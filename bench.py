@@ -671,6 +671,8 @@ def main():
                  "removed_pairs": st["removedPairs"], "global_solve_ms": st["globalSolveMs"],
                  "local_solve_ms": st["localSolveMs"], "integrate_kernel_ms": st["integrateKernelMs"],
                  "apply_kernel_ms": st["reintegrateKernelMs"],
+                 "host_ms_per_frame": st["hostMs"] / max(1, st["frames"]),
+                 "host_wait_ms_per_frame": st["hostWaitMs"] / max(1, st["frames"]),
                  "heap_free": rc.heap_free_count(),
                  "allocated_blocks_scanned_per_compactify": ss["scanned"] / max(1, ss["integrateOps"])},
     }

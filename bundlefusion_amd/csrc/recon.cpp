@@ -4,6 +4,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <limits>
 #include <unordered_set>
@@ -337,6 +338,7 @@ void Recon::runReintegrate() {
 }
 
 void Recon::processFrame(uint32_t f) {
+    const auto tStart = std::chrono::steady_clock::now();
     BF_REQUIRE(f == numFrames_, BF_ERR_STATE, "frames must be processed in order");
     BF_REQUIRE(f < opt_.maxFrames && frames_[f].set, BF_ERR_STATE, "frame not in the frame store");
     const uint32_t S = opt_.submapSize;
@@ -369,6 +371,7 @@ void Recon::processFrame(uint32_t f) {
     traceQueue(0, f, 1, &T, nullptr);
     numFrames_++;
     st_.frames++;
+    st_.hostMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tStart).count();
 }
 
 void Recon::reintegrate() {
@@ -400,8 +403,10 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     const uint32_t base = s * S;
     if (inflight_.size() == RING) {  // ring full: wait for the oldest result
         Pending& old = ring_[inflight_.front()];
+        const auto tw = std::chrono::steady_clock::now();
         baWaitFor(old.job);
         BF_HIP(hipEventSynchronize(old.done));
+        st_.hostWaitMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
         apply(old);
         inflight_.pop_front();
     }
@@ -728,8 +733,10 @@ void Recon::applyPending(bool block) {
         while (!inflight_.empty()) {
             Pending& P = ring_[inflight_.front()];
             if (numFrames_ < P.issueFrame + opt_.resultLag) break;
+            const auto tw = std::chrono::steady_clock::now();
             baWaitFor(P.job);
             BF_HIP(hipEventSynchronize(P.done));
+            st_.hostWaitMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
             apply(P);
             inflight_.pop_front();
         }

@@ -331,6 +331,8 @@ typedef struct BFReconStats {
     uint64_t endSolves;          /* end-of-sequence global solves (bf_recon_end_solve) */
     uint64_t pcgRecoveries;      /* solves whose persistent PCG timed out and was redone (BF_SOLVE_PCG_RECOVERED);
                                     a solve with a BF_SOLVE_ERR_FATAL bit fails the call with BF_ERR_INTERNAL */
+    double hostMs;               /* host wall time inside bf_recon_process_frame (enqueueing + waits) */
+    double hostWaitMs;           /* ... of it blocked on bundling results (resultLag, a full ring) */
 } BFReconStats;
 
 typedef struct bf_recon bf_recon;

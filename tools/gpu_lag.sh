@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/$1; mkdir -p $O; shift
-summ() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; pl=r['per_launch']; l=d['loop']; print('$2', 'fps %.1f' % d['value'], 'apply_us %.1f' % r['avg_launch_us'], 'evals %.3fM upd %.3fM blocks %.1f' % (pl['voxel_op_evaluations']/1e6, pl['voxel_op_updates']/1e6, pl['work_list_blocks']), 'gn %.3f loop %.3f' % (d['ms_per_gn_iter'], d['global_solve']['ms_per_gn_iter_in_loop']), 'local_ms %.2f global_ms %.2f' % (l['local_solve_ms'], l['global_solve_ms']))"; }
+summ() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; pl=r['per_launch']; l=d['loop']; print('$2', 'host %.0f wait %.0f us' % (1e3*l.get('host_ms_per_frame',0), 1e3*l.get('host_wait_ms_per_frame',0)), 'fps %.1f' % d['value'], 'apply_us %.1f' % r['avg_launch_us'], 'evals %.3fM upd %.3fM blocks %.1f' % (pl['voxel_op_evaluations']/1e6, pl['voxel_op_updates']/1e6, pl['work_list_blocks']), 'gn %.3f loop %.3f' % (d['ms_per_gn_iter'], d['global_solve']['ms_per_gn_iter_in_loop']), 'local_ms %.2f global_ms %.2f' % (l['local_solve_ms'], l['global_solve_ms']))"; }
 i=0
 for v in "$@"; do
   i=$((i+1))
