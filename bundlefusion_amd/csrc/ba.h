@@ -178,6 +178,7 @@ private:
     DevBuf<double> pstat_, dstat_;
     DevBuf<float> apPair_, rzPart_, poseBak_;
     DevBuf<uint2> aGran_;           // k_pcg_persist: Ap rows as {value, tag} granules
+    DevBuf<uint2> fxGran_;          // k_pcg_persist's four-workgroup finisher: its exchanged partials
     uint32_t pcgEpoch_ = 0;          // tag base of the next persistent launch
 };
 

@@ -93,6 +93,7 @@ struct BA {
     double *pstat, *dstat;
     float *apPair, *rzPart;
     uint2* aGran;  // [2][maxN][6] {value bits, tag}: k_pcg_persist's Ap hand-off
+    uint2* fxGran; // [2][8] {block partial, tag}: the four-workgroup finisher's p.Ap / r.z partials
     uint32_t pairMode, shardCount, shardIndex, pairBound;
     uint32_t earlyOut;  // ENABLE_EARLY_OUT (SolverBundling.cu:7): PCG |p.Ap| < 5e-7 and GN max|delta| < 0.005 exits
     float* poseBak;     // [maxN][6] rot | trans at the GN step's start (k_pair_init), for the timeout recovery (pcg_recover)
@@ -939,10 +940,25 @@ __device__ __forceinline__ void pcg_ap(const BA& a, uint32_t v, uint32_t nch, in
 // PCG finisher with each thread's R rows held in registers: all loads issue up front, then the
 // two block reductions, then the stores (z and Ap never go to memory). Same arithmetic as the
 // multi-pass form below.
+// R = 8 (514..2 049 images): the two dot products are summed as FIN_GROUPS block sums of two rows per
+// thread each (rows q = 2g, 2g + 1), added in group order: the order of k_pcg_persist's four-workgroup
+// finisher (pcg_persist_finisher_x4), so the persistent and the per-launch solves agree bit for bit
+constexpr int FIN_GROUPS = 4;
+template <int R>
+__device__ __forceinline__ float grouped_sum(const float* e, float* sh) {
+    if (R != 8) return block_sum(e[0], sh);
+    float t = 0.0f;
+#pragma unroll
+    for (int g = 0; g < FIN_GROUPS; g++) t += block_sum(e[g], sh);
+    return t;
+}
 template <int R, bool WT>
 __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDense, int iter, int nLin, bool& lastOut) {
     f3 pR[R], pT[R], aR[R], aT[R], dR[R], dT[R], rR[R], rT[R], mR[R], mT[R];
-    float d = 0.0f;
+    constexpr int NG = R == 8 ? FIN_GROUPS : 1;
+    float d[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++) d[g] = 0.0f;
 #pragma unroll
     for (int q = 0; q < R; q++) {
         const uint32_t v = 1 + threadIdx.x + q * WG;
@@ -952,13 +968,15 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
             vload_t<WT>(a, V_R, v, rR[q], rT[q]);
             vload_t<WT>(a, V_M, v, mR[q], mT[q]);
             pcg_ap(a, v, nch, useDense, pR[q], pT[q], aR[q], aT[q]);
-            d += dot3(pR[q], aR[q]) + dot3(pT[q], aT[q]);
+            d[NG > 1 ? q / 2 : 0] += dot3(pR[q], aR[q]) + dot3(pT[q], aT[q]);
         }
     }
-    const float pAp = block_sum(d, sh);
+    const float pAp = grouped_sum<R>(d, sh);
     const float rDotzOld = WT ? __uint_as_float(ld_wt(&a.ctrl[K_RDOTZ])) : ctrlf(a.ctrl, K_RDOTZ);
     const float alpha = (pAp > FLOAT_EPSILON) ? rDotzOld / pAp : 0.0f;
-    float b = 0.0f;
+    float b[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++) b[g] = 0.0f;
 #pragma unroll
     for (int q = 0; q < R; q++) {
         if (1 + threadIdx.x + q * WG < a.N) {
@@ -968,10 +986,10 @@ __device__ float pcg_finish_regs(const BA& a, float* sh, uint32_t nch, int useDe
             rT[q] = rT[q] - alpha * aT[q];
             mR[q] = mul3(mR[q], rR[q]);  // z
             mT[q] = mul3(mT[q], rT[q]);
-            b += dot3(mR[q], rR[q]) + dot3(mT[q], rT[q]);
+            b[NG > 1 ? q / 2 : 0] += dot3(mR[q], rR[q]) + dot3(mT[q], rT[q]);
         }
     }
-    const float rDotzNew = block_sum(b, sh);
+    const float rDotzNew = grouped_sum<R>(b, sh);
     const bool last = (iter == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
     const float beta = (rDotzOld > FLOAT_EPSILON) ? rDotzNew / rDotzOld : 0.0f;
 #pragma unroll
@@ -1644,7 +1662,175 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
     }
 }
 
-template <int R>
+// The finisher of wide sparse solves (514..2 017 images) as PP_NF workgroups instead of one with 8 rows per
+// thread (whose serial per-row work and polls were 8 of the 11.7 us of a K = 2 001 iteration,
+// profiles/r8h_pcg_phase_timing.txt): workgroup g owns rows 1 + t + (2g + q) WG, q = 0, 1, in registers (the
+// R = 2 form), and the two dot products go through a hand-off: each workgroup publishes its block partial
+// as a tagged granule, every workgroup adds the PP_NF partials in workgroup order (the grouped order of
+// pcg_finish_regs<8>, so the result equals the per-launch solve's bit for bit). Workgroup 0 sets the
+// flag (p halves carry their iteration's tag; workers re-gather a stale one) and the control words.
+constexpr int PP_NF = FIN_GROUPS;
+constexpr int SH_FX = 64;  // the finisher's LDS slots of the exchanged totals
+__device__ __forceinline__ float fx_exchange(const BA& a, float* sh, int kind, uint32_t g, float S, uint32_t tag,
+                                             unsigned long long t0, bool& ok) {
+    if (threadIdx.x == 0) gran_store(a.fxGran + kind * 8 + g, S, tag);
+    if (threadIdx.x < 64) {
+        const uint32_t l = threadIdx.x;
+        uint64_t x = 0;
+        bool got = l >= (uint32_t)PP_NF;
+        for (;;) {
+            if (!got) {
+                x = gran_load(a.fxGran + kind * 8 + l);
+                got = (uint32_t)(x >> 32) == tag;
+            }
+            if (__all(got)) break;
+            if (pp_timed_out(t0, a.spinTicks)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const bool all = __all(got);
+        float tot = 0.0f;
+#pragma unroll
+        for (int k = 0; k < PP_NF; k++) tot += __shfl(__uint_as_float((uint32_t)x), k);  // workgroup order
+        if (l == 0) {
+            sh[SH_FX + 2 * kind] = tot;
+            sh[SH_FX + 2 * kind + 1] = all ? 1.0f : 0.0f;
+        }
+    }
+    __syncthreads();
+    ok = sh[SH_FX + 2 * kind + 1] != 0.0f;
+    return sh[SH_FX + 2 * kind];
+}
+__device__ __forceinline__ uint32_t fin_row_g(int q, uint32_t g) {
+    uint32_t v = 1 + threadIdx.x + (2 * g + (uint32_t)q) * WG;
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ void pcg_persist_finisher_x4(const BA& a, float* sh, int nLin, uint32_t tagBase, uint32_t* flag, unsigned long long t0,
+                                        uint32_t g) {
+    constexpr int R = 2;
+    f3 pR[R], pT[R], rR[R], rT[R], mR[R], mT[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        const uint32_t v = fin_row_g(q, g);
+        if (v < a.N) {
+            vload(a, V_P, v, pR[q], pT[q]);
+            vload(a, V_R, v, rR[q], rT[q]);
+            vload(a, V_M, v, mR[q], mT[q]);
+        }
+    }
+    float rz = ctrlf(a.ctrl, K_RDOTZ);
+    const __amdgpu_buffer_rsrc_t prs = p_rsrc(a);
+    int it = 0;
+    bool last = false;
+    float lastAlpha = 0.0f;
+    for (;; it++) {
+        const uint32_t tag = tagBase + (uint32_t)it + 1u;
+        const uint2* gp[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = fin_row_g(q, g);
+            gp[q] = a.aGran + (size_t)(v < a.N ? v : 1u) * 6;  // image 1's granules: written every iteration
+        }
+        float x[R][6];
+        const int got = gran_rows<R>(gp, tag, x, t0, a.spinTicks);
+#ifdef BF_PCG_TIMING
+        if (g == 0 && threadIdx.x == 0) g_pcgT[it & 1023][2] = rtc();
+#endif
+        float d = 0.0f;
+#pragma unroll
+        for (int q = 0; q < R; q++)
+            if (fin_row_g(q, g) < a.N) d += dot3(pR[q], mk3(x[q][0], x[q][1], x[q][2])) + dot3(pT[q], mk3(x[q][3], x[q][4], x[q][5]));
+        float S;
+        bool all = true;
+        {   // block_sum's order, with the timeout vote in the same pass
+            const float wsum = wave_sum(d);
+            const bool wok = __all(got > 0);
+            if ((threadIdx.x & 63) == 0) { sh[threadIdx.x >> 6] = wsum; sh[WG / 64 + (threadIdx.x >> 6)] = wok ? 1.0f : 0.0f; }
+            __syncthreads();
+            S = 0.0f;
+            for (uint32_t w = 0; w < WG / 64; w++) { S += sh[w]; all = all && sh[WG / 64 + w] != 0.0f; }
+        }
+        if (!all) break;
+        bool ok;
+        const float pAp = fx_exchange(a, sh, 0, g, S, tag, t0, ok);
+        if (!ok) break;
+#ifdef BF_PCG_TIMING
+        if (g == 0 && threadIdx.x == 0) g_pcgS[it & 1023][0] = rtc();
+#endif
+        const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
+        lastAlpha = alpha;
+        float b = 0.0f;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            if (fin_row_g(q, g) < a.N) {
+                rR[q] = rR[q] - alpha * mk3(x[q][0], x[q][1], x[q][2]);
+                rT[q] = rT[q] - alpha * mk3(x[q][3], x[q][4], x[q][5]);
+                const f3 zR = mul3(mR[q], rR[q]), zT = mul3(mT[q], rT[q]);
+                b += dot3(zR, rR[q]) + dot3(zT, rT[q]);
+            }
+        }
+        float S2;
+        {
+            const float wsum = wave_sum(b);
+            if ((threadIdx.x & 63) == 0) sh[2 * (WG / 64) + (threadIdx.x >> 6)] = wsum;
+            __syncthreads();
+            S2 = 0.0f;
+            for (uint32_t w = 0; w < WG / 64; w++) S2 += sh[2 * (WG / 64) + w];
+        }
+        const float rzNew = fx_exchange(a, sh, 1, g, S2, tag, t0, ok);
+        if (!ok) break;
+#ifdef BF_PCG_TIMING
+        if (g == 0 && threadIdx.x == 0) g_pcgS[it & 1023][1] = rtc();
+#endif
+        last = (it == nLin - 1) || (a.earlyOut && fabsf(pAp) < 5e-7f);
+        const float beta = (rz > FLOAT_EPSILON) ? rzNew / rz : 0.0f;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t v = fin_row_g(q, g);
+            if (v < a.N) {
+                const f3 zR = mul3(mR[q], rR[q]), zT = mul3(mT[q], rT[q]);
+                pR[q] = zR + beta * pR[q];
+                pT[q] = zT + beta * pT[q];
+                if (!last) pstore_tag(prs, v, pR[q], pT[q], tagBase + (uint32_t)it + 2u);  // iteration it + 1's p
+            }
+        }
+        rz = rzNew;
+        if (last) break;
+#ifdef BF_PCG_TIMING
+        if (g == 0 && threadIdx.x == 0) g_pcgS[it & 1023][2] = rtc();
+#endif
+        // the flag only says when to start gathering: the p halves of the other finishers' rows carry
+        // their tag, and a worker re-gathers a stale one
+        if (g == 0 && threadIdx.x < PP_NFLAG) st_wt64(flag + threadIdx.x * PP_FLAG_STRIDE, (uint32_t)(it + 1), __float_as_uint(lastAlpha));
+#ifdef BF_PCG_TIMING
+        if (g == 0 && threadIdx.x == 0) g_pcgT[it & 1023][3] = rtc();
+#endif
+    }
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        const uint32_t v = fin_row_g(q, g);
+        if (v < a.N) {
+            vstore(a, V_R, v, rR[q], rT[q]);
+            vstore(a, V_P, v, pR[q], pT[q]);
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (!last) atomicOr(&a.ctrl[K_ERROR], PP_ERR_TIMEOUT);
+        if (g == 0) {
+            a.ctrl[K_RDOTZ] = __float_as_uint(rz);
+            a.ctrl[K_PCG_ITERS] += (uint32_t)(it + (last ? 1 : 0));
+            a.ctrl[K_PCG_DONE] = 1;
+        }
+    }
+    if (g == 0 && threadIdx.x < 64) {
+        drain_stores();
+        if (threadIdx.x < PP_NFLAG)
+            st_wt64(flag + threadIdx.x * PP_FLAG_STRIDE, PP_DONE | (uint32_t)(it + (last ? 1 : 0)), __float_as_uint(lastAlpha));
+    }
+}
+
+// NF finisher workgroups: 1 (the R-rows-per-thread finisher) or PP_NF (pcg_persist_finisher_x4, R = 2)
+template <int R, int NF = 1>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_pcg_persist(BA a, float wSparse, int nLin, uint32_t epoch) {
     __shared__ float sh[WG];
     __shared__ float sM[R > 2 ? 6 * R * WG : 1];  // the R = 8 finisher's preconditioner (48 KB)
@@ -1655,17 +1841,20 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const unsigned long long t0 = rtc();
     uint32_t* flag = &a.sync[SYNC_FLAGR];
     const uint32_t tagBase = epoch << 8;  // iteration it's Ap granules carry tagBase + it + 1
-    if (blockIdx.x == 0) {
-        pcg_persist_finisher<R>(a, sh, sM, useDense, nLin, tagBase, flag, t0);
+    if (blockIdx.x < NF) {
+        if (NF == 1) pcg_persist_finisher<R>(a, sh, sM, useDense, nLin, tagBase, flag, t0);
+        else pcg_persist_finisher_x4(a, sh, nLin, tagBase, flag, t0, blockIdx.x);
         return;
     }
     const uint32_t* myFlag = flag + ((blockIdx.x * (WG / 64) + (threadIdx.x >> 6)) % PP_NFLAG) * PP_FLAG_STRIDE;
     // ---- workers: one wave per row ----
     // Workgroup PP_SHADOW is dispatched onto the finisher's CU (256 CUs, round-robin) and holds no rows:
     // there, the finisher's granule polls held its rows' gathers up 2.4x (8 us of the 3.4 us others took)
-    const uint32_t wb = blockIdx.x < PP_SHADOW ? blockIdx.x : blockIdx.x - 1;
-    const uint32_t v = 1 + (wb - 1) * (WG / 64) + (threadIdx.x >> 6);
-    const bool hasRow = blockIdx.x != PP_SHADOW && v < a.N;
+    // (the NF workgroups dispatched onto the finishers' CUs hold none)
+    const bool shadow = blockIdx.x >= PP_SHADOW && blockIdx.x < PP_SHADOW + NF;
+    const uint32_t wb = blockIdx.x - NF - (blockIdx.x >= PP_SHADOW + NF ? NF : 0);
+    const uint32_t v = 1 + wb * (WG / 64) + (threadIdx.x >> 6);
+    const bool hasRow = !shadow && v < a.N;
     f3 dlR = mk3(0, 0, 0), dlT = dlR, pvR = dlR, pvT = dlR;  // the row's delta (every lane), the p it gathered
     int e0 = 0, e1 = 0;
     int2 rp[PP_CPL], rq[PP_OV];
@@ -2720,6 +2909,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     dstat_.alloc((size_t)N * DSTAT);
     apPair_.alloc((size_t)N * 8);
     aGran_.alloc((size_t)N * 12);  // [2][N][6]: sparse Ap rows, then the dense off-diagonal products
+    fxGran_.alloc(16);
     rzPart_.alloc(N);
     poseBak_.alloc((size_t)N * 6);
     int dev = 0;
@@ -2729,7 +2919,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     numCUs_ = prop.multiProcessorCount;
     int occP = 0, occP8 = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP, k_pcg_persist<2>, WG, 0));
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP8, k_pcg_persist<8>, WG, 0));
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occP8, k_pcg_persist<2, PP_NF>, WG, 0));
     persistCapacity_ = (unsigned)std::max(std::min(occP, occP8), 0) * (unsigned)numCUs_;
 #ifdef BF_PCG_TIMING
     fprintf(stderr, "k_pcg_persist occupancy: <2> %d, <8> %d workgroups per CU, %d CUs\n", occP, occP8, numCUs_);
@@ -2738,6 +2928,7 @@ Solver::Solver(const SolverConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_
     BF_HIP(hipMemsetAsync(ctrl_.p, 0, ctrl_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(sync_.p, 0, sync_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(aGran_.p, 0, aGran_.bytes(), stream_));  // tag 0 is never awaited
+    BF_HIP(hipMemsetAsync(fxGran_.p, 0, fxGran_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(imgPairN_.p, 0, imgPairN_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(rowCount_.p, 0, rowCount_.bytes(), stream_));
 }
@@ -2800,6 +2991,7 @@ void Solver::solve(const SolveArgs& s) {
     a.pairCorr = pairCorr_.p; a.rowPair = rowPair_.p; a.pstat = pstat_.p; a.dstat = dstat_.p;
     a.apPair = apPair_.p; a.rzPart = rzPart_.p;
     a.aGran = aGran_.p;
+    a.fxGran = fxGran_.p;
     a.shardCount = shardCount_; a.shardIndex = shardIndex_; a.pairBound = 0;
     a.earlyOut = cfg_.earlyOut ? 1u : 0u;
     a.poseBak = poseBak_.p;
@@ -2892,13 +3084,17 @@ void Solver::solve(const SolveArgs& s) {
             if (s.numImages <= (uint32_t)SMALL_N) {
                 if (s.nLin) k_pcg_small<<<1, SMALL_WG, 0, stream_>>>(a, wS, (int)s.nLin);
             } else {
-                unsigned persistGrid = 1u + div_up(s.numImages - 1u, (unsigned)(WG / 64));
-                if (persistGrid > PP_SHADOW) persistGrid++;  // the row-less workgroup on the finisher's CU
                 // one launch for the GN step's PCG loop when its grid is co-resident: up to 513 images
-                // (finisher rows in registers, dense term included) with room to spare, up to 2 049
-                // sparse-only (config 4's 2 001 keyframes) within the occupancy query's capacity
-                const bool small = s.numImages <= 2u * WG + 1u && persistGrid * 2u <= persistCapacity_;
-                const bool wide = !small && !dense && s.numImages <= 8u * WG + 1u && persistGrid <= persistCapacity_;
+                // (one finisher workgroup, rows in registers, dense term included) with room to spare; up
+                // to 2 017 sparse-only (config 4's 2 001 keyframes) with PP_NF finisher workgroups within
+                // the occupancy query's capacity (persistent launches are serialized per device, below)
+                const bool smallN = s.numImages <= 2u * WG + 1u;
+                const unsigned nF = smallN ? 1u : (unsigned)PP_NF;
+                const unsigned nW = div_up(s.numImages - 1u, (unsigned)(WG / 64));
+                unsigned persistGrid = nF + nW;
+                if (persistGrid > PP_SHADOW) persistGrid += nF;  // the row-less workgroups on the finishers' CUs
+                const bool small = smallN && persistGrid * 2u <= persistCapacity_;
+                const bool wide = !smallN && !dense && persistGrid <= persistCapacity_;
                 if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.nLin < 255u && s.numImages >= 2u && (small || wide)) {
 #ifdef BF_PCG_TIMING
                     {
@@ -2913,7 +3109,7 @@ void Solver::solve(const SolveArgs& s) {
                         std::lock_guard<std::mutex> lk(pg.mu);
                         if (pg.ev && pg.stream != stream_) BF_HIP(hipStreamWaitEvent(stream_, pg.ev, 0));
                         if (small) k_pcg_persist<2><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
-                        else k_pcg_persist<8><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
+                        else k_pcg_persist<2, PP_NF><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
                         if (!pg.ev) BF_HIP(hipEventCreateWithFlags(&pg.ev, hipEventDisableTiming));
                         BF_HIP(hipEventRecord(pg.ev, stream_));
                         pg.stream = stream_;
