@@ -176,7 +176,8 @@ int bf_abi_struct_size(const char* name, size_t* out) {
         {"BFAppInfo", sizeof(BFAppInfo)},
         {"BFAppResult", sizeof(BFAppResult)},
         {"BFMcTriangle", sizeof(BFMcTriangle)},
-        {"BFSynthScene", sizeof(BFSynthScene)}};
+        {"BFSynthScene", sizeof(BFSynthScene)},
+        {"BFRenderStats", sizeof(BFRenderStats)}};
     for (const auto& e : kSizes)
         if (std::strcmp(e.n, name) == 0) {
             *out = e.s;

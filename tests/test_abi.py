@@ -53,7 +53,7 @@ def test_struct_sizes_match_the_library():
             continue  # a Python-only helper struct
         assert C.sizeof(cls) == n.value, (name, C.sizeof(cls), n.value)
         checked += 1
-    assert checked >= 20
+    assert checked >= 26  # every BF* struct of the header that the bindings mirror
 
 
 def test_error_path_without_device():
@@ -74,3 +74,13 @@ def test_synthetic_stream_host():
     assert valid.min() >= 0.1 and valid.max() <= 4.0
     # 1 mm quantisation (.sens ushort/1000 convention)
     assert abs(valid * 1000 - (valid * 1000).round()).max() < 1e-2
+
+
+def test_solver_error_bits():
+    """BFSolveResult.error: the recovered-timeout bit is the only non-fatal one (include/bf/types.h)."""
+    assert abi.SOLVE_PCG_RECOVERED == 16 and abi.SOLVE_ERR_PCG_TIMEOUT == 8 and abi.SOLVE_ERR_PAIR_BOUND == 4
+    assert abi.SOLVE_ERR_FATAL & abi.SOLVE_PCG_RECOVERED == 0
+    assert abi.SOLVE_ERR_FATAL & abi.SOLVE_ERR_PCG_TIMEOUT and abi.SOLVE_ERR_FATAL & abi.SOLVE_ERR_PAIR_BOUND
+    text = open(abi.HEADER_PATH.replace("bf.h", "types.h")).read()
+    for name, v in (("BF_SOLVE_ERR_PAIR_BOUND", 4), ("BF_SOLVE_ERR_PCG_TIMEOUT", 8), ("BF_SOLVE_PCG_RECOVERED", 16)):
+        assert f"#define {name} {v}u" in text, name
