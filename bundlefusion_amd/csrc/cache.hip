@@ -45,30 +45,35 @@ struct GeomArgs {
     uchar4* outNU8;
 };
 
-// gaussFilterDepthMapDevice (CUDAImageUtil.cu:759-797) evaluated at one pixel: m (x) outer, n (y) inner
-__device__ float filtered_at(const GeomArgs& A, int x, int y) {
+// gaussFilterDepthMapDevice (CUDAImageUtil.cu:759-797) evaluated at one pixel: m (x) outer, n (y) inner.
+// R = the kernel radius as a template argument (R < 0: no filter), so the taps unroll: their loads
+// issue together and the weights are compile-time offsets into the argument table
+template <int R>
+__device__ __forceinline__ float filtered_at(const GeomArgs& A, int x, int y) {
     const int W = (int)A.iW, H = (int)A.iH;
     const float depthCenter = A.depth[y * W + x];
-    if (!A.useGauss) return depthCenter;
-    const int R = A.g.radius;
-    float sum = 0.0f, sumWeight = 0.0f;
-    if (depthCenter != -INFINITY) {
-        // loops over the offsets (same m-outer / n-inner order), so the weight index is wave-uniform
-        // and the weights come through scalar loads instead of one vector load per tap
-        for (int dm = -R; dm <= R; dm++)
-            for (int dn = -R; dn <= R; dn++) {
-                const int m = x + dm, n = y + dn;
-                if (m >= 0 && n >= 0 && m < W && n < H) {
-                    const float currentDepth = A.depth[n * W + m];
-                    if (currentDepth != -INFINITY && fabsf(depthCenter - currentDepth) < A.sigmaR) {
-                        const float weight = A.g.w[(dn + R) * (2 * R + 1) + (dm + R)];
-                        sumWeight += weight;
-                        sum += weight * currentDepth;
+    if constexpr (R < 0) {
+        return depthCenter;
+    } else {
+        float sum = 0.0f, sumWeight = 0.0f;
+        if (depthCenter != -INFINITY) {
+#pragma unroll
+            for (int dm = -R; dm <= R; dm++)
+#pragma unroll
+                for (int dn = -R; dn <= R; dn++) {
+                    const int m = x + dm, n = y + dn;
+                    if (m >= 0 && n >= 0 && m < W && n < H) {
+                        const float currentDepth = A.depth[n * W + m];
+                        if (currentDepth != -INFINITY && fabsf(depthCenter - currentDepth) < A.sigmaR) {
+                            const float weight = A.g.w[(dn + R) * (2 * R + 1) + (dm + R)];
+                            sumWeight += weight;
+                            sum += weight * currentDepth;
+                        }
                     }
                 }
-            }
+        }
+        return sumWeight > 0.0f ? sum / sumWeight : -INFINITY;
     }
-    return sumWeight > 0.0f ? sum / sumWeight : -INFINITY;
 }
 
 // convertDepthFloatToCameraSpaceFloat4_Kernel (CUDAImageUtil.cu:367-384) at one pixel
@@ -85,6 +90,7 @@ __device__ float4 campos_at(const GeomArgs& A, int x, int y, float depth) {
 // 64 cache pixels per workgroup; wave w evaluates the filtered depth at point w of each pixel's
 // stencil (the sample, then +y, +x, -y, -x), so each thread runs one 5x5 bilateral window; wave 0
 // then forms camera positions, the normal and the outputs from LDS.
+template <int R>
 __global__ __launch_bounds__(GEOM_WG) void k_cache_geometry(GeomArgs A) {
     __shared__ float sd[5][64];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -98,7 +104,7 @@ __global__ __launch_bounds__(GEOM_WG) void k_cache_geometry(GeomArgs A) {
     const int dx[5] = {0, 0, 1, 0, -1}, dy[5] = {0, 1, 0, -1, 0};
     const bool interior = xi > 0 && xi < (int)A.iW - 1 && yi > 0 && yi < (int)A.iH - 1;
     float f = -INFINITY;
-    if (on && (w == 0 || interior)) f = filtered_at(A, xi + dx[w], yi + dy[w]);
+    if (on && (w == 0 || interior)) f = filtered_at<R>(A, xi + dx[w], yi + dy[w]);
     sd[w][lane] = f;
     __syncthreads();
     if (w != 0 || !on) return;
@@ -141,14 +147,13 @@ struct IntArgs {
 // 16x16 cache pixels per workgroup: the resampled intensity of the tile + (R + 1) halo and the
 // Gaussian of the tile + 1 halo are staged in LDS, then the Sobel derivatives of the tile.
 constexpr int IT = 16;
-constexpr int IMAXR = 7;
-constexpr int IH1 = IT + 2 * (IMAXR + 1);  // staged intensity edge
+// R: the Gaussian's radius, R < 0: unfiltered (template argument: the taps unroll, see filtered_at)
+template <int R>
 __global__ __launch_bounds__(256) void k_cache_intensity(IntArgs A) {
-    __shared__ float I[IH1 * IH1];
+    constexpr int h = (R < 0 ? 0 : R) + 1, E = IT + 2 * h;  // staged edge for this radius
+    __shared__ float I[E * E];
     __shared__ float G[(IT + 2) * (IT + 2)];
     const int W = (int)A.oW, H = (int)A.oH;
-    const int R = A.useGauss ? A.g.radius : 0;
-    const int h = R + 1, E = IT + 2 * h;  // staged edge for this radius
     const int x0 = blockIdx.x * IT - h, y0 = blockIdx.y * IT - h;
     // resampleToIntensity_Kernel (CUDAImageUtil.cu:224-241) + convertToIntensity (:197-199)
     const float scaleWidth = (float)(A.cW - 1) / (float)(W - 1);
@@ -172,9 +177,11 @@ __global__ __launch_bounds__(256) void k_cache_intensity(IntArgs A) {
         float out = 0.0f;
         if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
             out = I[(gy - y0) * E + (gx - x0)];
-            if (A.useGauss) {
+            if constexpr (R >= 0) {
                 float sum = 0.0f, sumWeight = 0.0f;
+#pragma unroll
                 for (int dm = -R; dm <= R; dm++)  // offsets: wave-uniform weight index (scalar loads)
+#pragma unroll
                     for (int dq = -R; dq <= R; dq++) {
                         const int m = gx + dm, q = gy + dq;
                         if (m >= 0 && q >= 0 && m < W && q < H) {
@@ -261,7 +268,13 @@ uint32_t Cache::storeFrame(const float* depth, const uint8_t* color, uint32_t co
     g.useGauss = cfg_.depthSigmaD > 0.0f;
     g.g = depthGauss_;
     g.outDepth = depth_.p + o; g.outCampos = campos_.p + o; g.outNormals = normals_.p + o; g.outNU8 = normalsU8_.p + o;
-    k_cache_geometry<<<div_up((uint32_t)hw_, 64u), GEOM_WG, 0, stream_>>>(g);
+    const int rg = g.useGauss ? depthGauss_.radius : -1;
+    switch (rg) {
+#define BF_GEOM(r) case r: k_cache_geometry<r><<<div_up((uint32_t)hw_, 64u), GEOM_WG, 0, stream_>>>(g); break;
+        BF_GEOM(-1) BF_GEOM(0) BF_GEOM(1) BF_GEOM(2) BF_GEOM(3) BF_GEOM(4) BF_GEOM(5) BF_GEOM(6) BF_GEOM(7)
+#undef BF_GEOM
+        default: BF_REQUIRE(false, BF_ERR_ARG, "depth filter radius above 7");
+    }
     BF_LAUNCH_CHECK();
     IntArgs ia{};
     ia.color = reinterpret_cast<const uchar4*>(color);
@@ -270,7 +283,13 @@ uint32_t Cache::storeFrame(const float* depth, const uint8_t* color, uint32_t co
     ia.g = colorGauss_;
     ia.outIntensity = intensity_.p + o;
     ia.outDeriv = deriv_.p + o;
-    k_cache_intensity<<<dim3(div_up(cfg_.width, (uint32_t)IT), div_up(cfg_.height, (uint32_t)IT)), 256, 0, stream_>>>(ia);
+    const dim3 ig(div_up(cfg_.width, (uint32_t)IT), div_up(cfg_.height, (uint32_t)IT));
+    switch (ia.useGauss ? colorGauss_.radius : -1) {
+#define BF_INT(r) case r: k_cache_intensity<r><<<ig, 256, 0, stream_>>>(ia); break;
+        BF_INT(-1) BF_INT(0) BF_INT(1) BF_INT(2) BF_INT(3) BF_INT(4) BF_INT(5) BF_INT(6) BF_INT(7)
+#undef BF_INT
+        default: BF_REQUIRE(false, BF_ERR_ARG, "colour filter radius above 7");
+    }
     BF_LAUNCH_CHECK();
     cur_++;
     return f;

@@ -64,6 +64,27 @@ __device__ __forceinline__ void stage_tile_u16(float (*t)[TX + 2 * MAXR], const 
 }
 
 // erodeDepthMapDevice (CUDAImageUtil.cu:701-739)
+// BOUNDS false: the workgroup's tile and halo lie inside the image, so the reference's per-tap
+// `x + j >= 0 && ...` tests are all true and are left out (the same taps, the same result)
+template <int R, bool BOUNDS>
+__device__ __forceinline__ unsigned int erode_count(const float (*t)[TX + 2 * MAXR], int lx, int ly, int x, int y, int W, int H,
+                                                    float oldDepth, float dThresh) {
+    unsigned int count = 0;
+#pragma unroll
+    for (int i = -R; i <= R; i++)
+#pragma unroll
+        for (int j = -R; j <= R; j++)
+            if (!BOUNDS || (x + j >= 0 && x + j < W && y + i >= 0 && y + i < H)) {
+                const float depth = t[ly + R + i][lx + R + j];
+                if (depth == -INFINITY || depth == 0.0f || fabsf(depth - oldDepth) > dThresh) count++;
+            }
+    return count;
+}
+template <int R>
+__device__ __forceinline__ bool tile_interior(int W, int H) {
+    const int x0 = blockIdx.x * TX - R, y0 = blockIdx.y * TY - R;
+    return x0 >= 0 && y0 >= 0 && x0 + TX + 2 * R <= W && y0 + TY + 2 * R <= H;
+}
 // inU16 != nullptr: the input is the sensor's ushort depth (k_depth_u16 folded into the staging)
 template <int R>
 __global__ __launch_bounds__(256) void k_erode(float* __restrict__ out, const float* __restrict__ in, int W, int H, float dThresh,
@@ -74,19 +95,32 @@ __global__ __launch_bounds__(256) void k_erode(float* __restrict__ out, const fl
     const int lx = threadIdx.x % TX, ly = threadIdx.x / TX;
     const int x = blockIdx.x * TX + lx, y = blockIdx.y * TY + ly;
     if (x >= W || y >= H) return;
-    unsigned int count = 0;
     const float oldDepth = t[ly + R][lx + R];
-    for (int i = -R; i <= R; i++)
-        for (int j = -R; j <= R; j++)
-            if (x + j >= 0 && x + j < W && y + i >= 0 && y + i < H) {
-                const float depth = t[ly + R + i][lx + R + j];
-                if (depth == -INFINITY || depth == 0.0f || fabsf(depth - oldDepth) > dThresh) count++;
-            }
+    const unsigned int count = tile_interior<R>(W, H) ? erode_count<R, false>(t, lx, ly, x, y, W, H, oldDepth, dThresh)
+                                                      : erode_count<R, true>(t, lx, ly, x, y, W, H, oldDepth, dThresh);
     const unsigned int sum = (2 * R + 1) * (2 * R + 1);
     out[y * W + x] = ((float)count / (float)sum >= fracReq) ? -INFINITY : oldDepth;
 }
 
 // gaussFilterDepthMapDevice (CUDAImageUtil.cu:759-797): m (x) outer, n (y) inner, as the reference
+template <int R, bool BOUNDS>
+__device__ __forceinline__ float gauss_at(const float (*t)[TX + 2 * MAXR], int lx, int ly, int x, int y, int W, int H,
+                                          float depthCenter, float sigmaR, const GaussTable& g) {
+    float sum = 0.0f, sumWeight = 0.0f;
+#pragma unroll
+    for (int dm = -R; dm <= R; dm++)
+#pragma unroll
+        for (int dn = -R; dn <= R; dn++)
+            if (!BOUNDS || (x + dm >= 0 && y + dn >= 0 && x + dm < W && y + dn < H)) {
+                const float currentDepth = t[ly + R + dn][lx + R + dm];
+                if (currentDepth != -INFINITY && fabsf(depthCenter - currentDepth) < sigmaR) {
+                    const float weight = g.w[(dn + R) * (2 * R + 1) + (dm + R)];
+                    sumWeight += weight;
+                    sum += weight * currentDepth;
+                }
+            }
+    return sumWeight > 0.0f ? sum / sumWeight : -INFINITY;
+}
 template <int R>
 __global__ __launch_bounds__(256) void k_gauss(float* __restrict__ out, const float* __restrict__ in, int W, int H, float sigmaR,
                                                GaussTable g) {
@@ -95,21 +129,12 @@ __global__ __launch_bounds__(256) void k_gauss(float* __restrict__ out, const fl
     const int lx = threadIdx.x % TX, ly = threadIdx.x / TX;
     const int x = blockIdx.x * TX + lx, y = blockIdx.y * TY + ly;
     if (x >= W || y >= H) return;
-    float sum = 0.0f, sumWeight = 0.0f;
     const float depthCenter = t[ly + R][lx + R];
-    if (depthCenter != -INFINITY) {
-        for (int m = x - R; m <= x + R; m++)
-            for (int n = y - R; n <= y + R; n++)
-                if (m >= 0 && n >= 0 && m < W && n < H) {
-                    const float currentDepth = t[ly + R + (n - y)][lx + R + (m - x)];
-                    if (currentDepth != -INFINITY && fabsf(depthCenter - currentDepth) < sigmaR) {
-                        const float weight = g.w[(n - y + R) * (2 * R + 1) + (m - x + R)];
-                        sumWeight += weight;
-                        sum += weight * currentDepth;
-                    }
-                }
-    }
-    out[y * W + x] = sumWeight > 0.0f ? sum / sumWeight : -INFINITY;
+    float r = -INFINITY;
+    if (depthCenter != -INFINITY)
+        r = tile_interior<R>(W, H) ? gauss_at<R, false>(t, lx, ly, x, y, W, H, depthCenter, sigmaR, g)
+                                   : gauss_at<R, true>(t, lx, ly, x, y, W, H, depthCenter, sigmaR, g);
+    out[y * W + x] = r;
 }
 
 // resampleFloat_Kernel / resampleUCHAR4_Kernel (CUDAImageUtil.cu:93-111, 160-177): nearest sample

@@ -1907,7 +1907,9 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, 256, 0));
     // sharded: one workgroup slot per CU stays free for the bundling streams' launches (Recon::Recon)
-    applyGrid_ = (unsigned)std::max(1, occA - (cfg_.shardCount > 1 ? 1 : 0)) * (unsigned)numCUs_;
+    int freeSlots = cfg_.shardCount > 1 ? 1 : 0;
+    if (const char* e = std::getenv("BF_APPLY_FREE_SLOTS")) freeSlots = std::atoi(e);  // A/B measurements
+    applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
