@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <limits>
 
 namespace bf {
@@ -131,15 +132,27 @@ TrajectoryManager::TrajectoryManager(uint32_t maxFrames, uint32_t topNActive, fl
     for (float& v : ninf.m) v = NEG_INF;
     optimized_.assign(maxFrames, ninf);
     frames_.assign(maxFrames, Frame{FrameType::NotIntegrated_NoTransform, 0xFFFFFFFFu, ninf, 0.0f});
+    integratedPose_.assign(maxFrames, PoseCache{});
+    optimizedPose_.assign(maxFrames, PoseCache{});
     sortOrder_.reserve(maxFrames);
+}
+
+void TrajectoryManager::setIntegrated(uint32_t i, const BFMat4& T) {
+    if (std::memcmp(frames_[i].integrated.m, T.m, sizeof(T.m)) != 0) integratedPose_[i].valid = false;
+    frames_[i].integrated = T;
+}
+
+void TrajectoryManager::setOptimized(uint32_t i, const BFMat4& T) {
+    if (std::memcmp(optimized_[i].m, T.m, sizeof(T.m)) != 0) optimizedPose_[i].valid = false;
+    optimized_[i] = T;
 }
 
 void TrajectoryManager::addFrame(FrameType what, const BFMat4& T, uint32_t idx) {
     Frame& f = frames_.at(idx);
     f.type = what;
     f.frameIdx = idx;
-    f.integrated = T;
-    optimized_[idx] = T;
+    setIntegrated(idx, T);
+    setOptimized(idx, T);
     sortOrder_.push_back(idx);
     numAdded_++;
 }
@@ -147,7 +160,7 @@ void TrajectoryManager::addFrame(FrameType what, const BFMat4& T, uint32_t idx) 
 void TrajectoryManager::updateOptimizedTransforms(const BFMat4* T, uint32_t numFrames) {
     numOptimized_ = numFrames;
     numFrames = std::min(numFrames, numAdded_);
-    for (uint32_t i = 0; i < numFrames; i++) optimized_[i] = T[i];
+    for (uint32_t i = 0; i < numFrames; i++) setOptimized(i, T[i]);
 }
 
 void TrajectoryManager::invalidateFrame(uint32_t i) {
@@ -169,9 +182,19 @@ void TrajectoryManager::generateUpdateLists() {
             f.type = FrameType::NotIntegrated_WithTransform;
             integ_.push_back(i);
         }
+        PoseCache& co = optimizedPose_[i];
+        PoseCache& ci = integratedPose_[i];
+        if (!co.valid) {
+            pose_helper_matrix_to_pose(optimized_[i], co.p);
+            co.valid = true;
+        }
+        if (!ci.valid) {
+            pose_helper_matrix_to_pose(f.integrated, ci.p);
+            ci.valid = true;
+        }
         float po[6], pi[6];
-        pose_helper_matrix_to_pose(optimized_[i], po);
-        pose_helper_matrix_to_pose(f.integrated, pi);
+        std::memcpy(po, co.p, sizeof(po));
+        std::memcpy(pi, ci.p, sizeof(pi));
         for (int k = 0; k < 3; k++) {
             po[k] *= rescale_;
             pi[k] *= rescale_;
@@ -180,15 +203,7 @@ void TrajectoryManager::generateUpdateLists() {
         for (int k = 0; k < 6; k++) d += (pi[k] - po[k]) * (pi[k] - po[k]);
         f.dist = d;
     }
-    auto less = [this](uint32_t a, uint32_t b) {
-        const Frame& l = frames_[a];
-        const Frame& r = frames_[b];
-        if (l.type == FrameType::Integrated && r.type != FrameType::Integrated) return true;
-        if (l.type != FrameType::Integrated) return false;
-        if (r.type != FrameType::Integrated) return false;
-        return l.dist > r.dist;
-    };
-    std::stable_sort(sortOrder_.begin(), sortOrder_.begin() + numFrames, less);
+    sortFrames(numFrames);
     for (uint32_t i = (uint32_t)reint_.size(); i < topN_ && i < numFrames; i++) {
         Frame& f = frames_[sortOrder_[i]];
         if (f.dist > minDist_ && f.type == FrameType::Integrated) {
@@ -198,6 +213,56 @@ void TrajectoryManager::generateUpdateLists() {
             break;
         }
     }
+}
+
+// m_framesSort's sort (TrajectoryManager.cpp:87-100): integrated frames first by decreasing distance,
+// everything else after them; equal keys keep their order (see trajectory.h). The same permutation
+// as std::stable_sort with that comparator, from a radix sort of unique 64-bit keys
+// {not integrated, ~distance bits, position}: the distances are sums of squares, so for the
+// integrated frames (the only ones whose distance is compared) the float order is the bit order
+// unless one is NaN, which takes the comparator sort itself.
+void TrajectoryManager::sortFrames(uint32_t numFrames) {
+    auto less = [this](uint32_t a, uint32_t b) {
+        const Frame& l = frames_[a];
+        const Frame& r = frames_[b];
+        if (l.type == FrameType::Integrated && r.type != FrameType::Integrated) return true;
+        if (l.type != FrameType::Integrated) return false;
+        if (r.type != FrameType::Integrated) return false;
+        return l.dist > r.dist;
+    };
+    if (numFrames == 0) return;
+    bool keyed = numFrames < (1u << 20);
+    sortKeys_.resize(numFrames);
+    for (uint32_t p = 0; p < numFrames && keyed; p++) {
+        const Frame& f = frames_[sortOrder_[p]];
+        uint64_t k = 1ull << 52;
+        if (f.type == FrameType::Integrated) {
+            uint32_t bits;
+            std::memcpy(&bits, &f.dist, 4);
+            if (f.dist != f.dist || (bits >> 31)) keyed = false;  // NaN / negative: not a plain bit order
+            k = (uint64_t)(~bits) << 20;
+        }
+        sortKeys_[p] = k | p;
+    }
+    if (!keyed) {
+        std::stable_sort(sortOrder_.begin(), sortOrder_.begin() + numFrames, less);
+        return;
+    }
+    // LSD radix sort on the 33 bits above the position, 11 bits per pass: each pass is stable and the
+    // keys enter in position order, so equal {class, distance} keep it
+    sortKeys2_.resize(numFrames);
+    uint64_t* a = sortKeys_.data();
+    uint64_t* b = sortKeys2_.data();
+    for (int shift = 20; shift < 53; shift += 11) {
+        uint32_t count[2048 + 1] = {0};
+        for (uint32_t p = 0; p < numFrames; p++) count[((a[p] >> shift) & 2047u) + 1]++;
+        if (count[((a[0] >> shift) & 2047u) + 1] == numFrames) continue;  // one digit value: the order stands
+        for (int d = 0; d < 2048; d++) count[d + 1] += count[d];
+        for (uint32_t p = 0; p < numFrames; p++) b[count[(a[p] >> shift) & 2047u]++] = a[p];
+        std::swap(a, b);
+    }
+    sortTmp_.assign(sortOrder_.begin(), sortOrder_.begin() + numFrames);
+    for (uint32_t p = 0; p < numFrames; p++) sortOrder_[p] = sortTmp_[a[p] & 0xFFFFFu];
 }
 
 void TrajectoryManager::confirmIntegration(uint32_t frameIdx) { frames_[frameIdx].type = FrameType::Integrated; }
@@ -211,7 +276,7 @@ bool TrajectoryManager::topReIntegrate(BFMat4& oldT, BFMat4& newT, uint32_t& fra
         oldT = frames_[i].integrated;
         reint_.pop_front();
         if (newT.m[0] != NEG_INF) {
-            frames_[i].integrated = newT;
+            setIntegrated(i, newT);
             break;
         }
     }
@@ -223,7 +288,7 @@ bool TrajectoryManager::topIntegrate(BFMat4& T, uint32_t& frame) {
     const uint32_t i = integ_.front();
     T = optimized_[i];
     frame = i;
-    frames_[i].integrated = T;
+    setIntegrated(i, T);
     integ_.pop_front();
     return true;
 }

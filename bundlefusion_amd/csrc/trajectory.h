@@ -72,12 +72,25 @@ private:
         float dist;
     };
     void invalidateFrame(uint32_t i);
+    void setIntegrated(uint32_t i, const BFMat4& T);
+    void setOptimized(uint32_t i, const BFMat4& T);
+    void sortFrames(uint32_t numFrames);
 
     std::vector<BFMat4> optimized_;
     std::vector<Frame> frames_;
     std::vector<uint32_t> sortOrder_;  // m_framesSort (frame indices in added order)
     uint32_t numAdded_ = 0, numOptimized_ = 0;
     std::deque<uint32_t> deint_, integ_, reint_;
+    // generateUpdateLists' two MatrixToPose per frame, cached until the transform changes (the
+    // loop calls it every few frames over every frame so far: at 5 000 frames it was most of the
+    // host time per frame); the values are the same calls on the same matrices
+    struct PoseCache {
+        float p[6];
+        bool valid = false;
+    };
+    std::vector<PoseCache> integratedPose_, optimizedPose_;
+    std::vector<uint64_t> sortKeys_, sortKeys2_;
+    std::vector<uint32_t> sortTmp_;
     uint32_t topN_;
     float minDist_;
     float rescale_ = 2.0f;

@@ -129,6 +129,37 @@ def test_queue_matches_oracle(seed):
         assert prod.frame_info(f) == orc.frame_info(f)
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_queue_ties_match_oracle(seed):
+    """Equal non-zero distances in bulk: frames share one of a few poses and get one of a few
+    corrections, so whole groups tie. The product sorts by a radix sort of {class, distance,
+    position} keys and caches MatrixToPose per frame; the order among equal keys must stay the
+    oracle's stable_sort order over the persistent permutation, across many regenerations."""
+    rng = np.random.default_rng(seed)
+    F = 400
+    prod, orc = TrajectoryManager(F, 30), OracleTM(F, 30)
+    base = [pose_mat(rng) for _ in range(3)]
+    corr = [pose_mat(rng, scale_r=s, scale_t=0.01) for s in (1e-3, 1e-2, 3e-2)]
+    traj = np.stack([base[int(rng.integers(3))] for _ in range(F)])
+    for f in range(F):
+        if f % 10 == 0 and f > 0:
+            opt = traj[:f].copy()
+            for g in range(f):
+                if rng.random() < 0.8:
+                    opt[g] = opt[g] @ corr[int(rng.integers(3))]
+            if f % 30 == 0:
+                opt[int(rng.integers(f))] = -np.inf
+            prod.update_optimized(opt)
+            orc.update_optimized(opt)
+        assert_same_ops(prod.next_fixes(10), orc.next_fixes(10))
+        prod.add_frame(0, traj[f], f)
+        orc.add_frame(0, traj[f], f)
+    for _ in range(60):
+        assert_same_ops(prod.next_fixes(10), orc.next_fixes(10))
+    for f in range(F):
+        assert prod.frame_info(f) == orc.frame_info(f)
+
+
 def test_queue_semantics_by_hand():
     """Reference behaviour spelled out: integrated frames whose optimized pose moved are re-integrated
     largest distance first (top 30, dist > 0); -inf frames are de-integrated; a re-validated frame is
