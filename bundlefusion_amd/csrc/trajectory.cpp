@@ -182,8 +182,10 @@ void TrajectoryManager::generateUpdateLists() {
             f.type = FrameType::NotIntegrated_WithTransform;
             integ_.push_back(i);
         }
+        // the distance changes only with one of the two poses, i.e. when a cache was invalidated
         PoseCache& co = optimizedPose_[i];
         PoseCache& ci = integratedPose_[i];
+        if (co.valid && ci.valid) continue;
         if (!co.valid) {
             pose_helper_matrix_to_pose(optimized_[i], co.p);
             co.valid = true;
