@@ -656,6 +656,10 @@ def main():
                      "alg_bytes_per_launch": per_launch_bytes,
                      "alg_bytes_source": "SURVEY 8(d) per-op integrate bytes (8 P + 16 Nv + 24 V) x ops per launch",
                      "alg_bytes_pass_per_launch": pass_bytes / launches,
+                     "note": "frac prices SURVEY 8(d)'s per-op bytes, what the reference's one pass per op moves; "
+                             "the batch reads and writes each voxel once for all of its ops, so frac can pass 1. "
+                             "The pass's own bytes give pass_frac, the PMC counters hbm_frac_counters; the kernel "
+                             "is bound by VALU issue and latency (valu.frac), not by HBM",
                      "achieved_pass": pass_bytes / launches / per_launch_s / 1e9,
                      "per_launch": {"work_list_blocks": ss["batchBlocks"] / launches,
                                     "voxels_rmw": ss["batchVoxelsRMW"] / launches,

@@ -12,7 +12,7 @@
 //    writes depth / campos / normals / uchar4 normals: 5 x 4 800 filter windows (one per thread)
 //    instead of 307 200 full-resolution ones, with the same float expressions in the same order,
 //    so the results are bit-identical to the staged pipeline (checked against the oracle, which stages).
-//  * k_cache_intensity: per 16x16 tile, the resampled intensity (tile + radius + 1 halo) and its
+//  * k_cache_intensity: per 8x8 tile, the resampled intensity (tile + radius + 1 halo) and its
 //    Gaussian (tile + 1 halo) are staged in LDS: resample + convertToIntensity, the Gaussian and
 //    the Sobel derivatives in one launch instead of three.
 #include <hip/hip_runtime.h>
@@ -144,9 +144,9 @@ struct IntArgs {
     float2* outDeriv;
 };
 
-// 16x16 cache pixels per workgroup: the resampled intensity of the tile + (R + 1) halo and the
+// IT x IT cache pixels per workgroup: the resampled intensity of the tile + (R + 1) halo and the
 // Gaussian of the tile + 1 halo are staged in LDS, then the Sobel derivatives of the tile.
-constexpr int IT = 16;
+constexpr int IT = 8;  // 8x8 tiles: 80 workgroups at 80x60 (16x16: 20, each with twice the serial work)
 // R: the Gaussian's radius, R < 0: unfiltered (template argument: the taps unroll, see filtered_at)
 template <int R>
 __global__ __launch_bounds__(256) void k_cache_intensity(IntArgs A) {
@@ -199,6 +199,7 @@ __global__ __launch_bounds__(256) void k_cache_intensity(IntArgs A) {
     }
     __syncthreads();
     // computeIntensityDerivatives_Kernel (CUDAImageUtil.cu:260-296)
+    if (threadIdx.x >= IT * IT) return;
     const int lx = threadIdx.x % IT, ly = threadIdx.x / IT;
     const int x = blockIdx.x * IT + lx, y = blockIdx.y * IT + ly;
     if (x >= W || y >= H) return;
