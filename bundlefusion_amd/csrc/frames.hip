@@ -181,14 +181,17 @@ Preproc::Preproc(uint32_t dw, uint32_t dh, uint32_t cw, uint32_t ch, uint32_t iw
     BF_REQUIRE(o.erodeStructureSize >= 0 && o.erodeStructureSize <= MAXR, BF_ERR_ARG, "erode structure size 0..7");
     BF_REQUIRE(o.depthShift > 0.0f, BF_ERR_ARG, "depthShift");
     if (o.depthFilter) gauss_ = gauss_table(o.sigmaD);
-    a_.alloc((size_t)dw * dh);
+    a_[0].alloc((size_t)dw * dh);
+    a_[1].alloc((size_t)dw * dh);
     b_.alloc((size_t)dw * dh);
 }
 
 // CUDAImageManager::process: raw -> [erode x2 (raw <-> filtered)] -> [gauss | copy] -> resample
-void Preproc::run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut) {
+void Preproc::run(const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut, int slot) {
+    BF_REQUIRE(slot == 0 || slot == 1, BF_ERR_ARG, "preprocessing buffer slot 0 / 1");
     const uint32_t n = dw_ * dh_;
-    float* raw = a_.p;
+    slot_ = slot;
+    float* raw = a_[slot].p;
     float* filtered = b_.p;
     const int W = (int)dw_, H = (int)dh_;
     if (opt_.erode) {  // the first erosion converts the ushort depth as it stages its tile

@@ -189,7 +189,8 @@ Recon::~Recon() {
         if (localDone_[b]) (void)hipEventDestroy(localDone_[b]);
         if (globalDone_[b]) (void)hipEventDestroy(globalDone_[b]);
     }
-    if (cacheEv_) (void)hipEventDestroy(cacheEv_);
+    for (hipEvent_t e : cacheEvF_)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : preEv_)
         if (e) (void)hipEventDestroy(e);
     for (Pending& p : ring_) {
@@ -436,7 +437,8 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     const std::pair<BFEntryJ*, uint32_t> lc = localCorr_[s];
     // everything below only issues work on baStream_ from state fixed at this point: the bundling
     // thread runs it while the frame loop goes on enqueuing scene work
-    baPost([this, s, n, S, slot, haveCache, lc, nk]() { issueSubmap(s, n, S, slot, haveCache, lc, nk); });
+    const hipEvent_t cev = cacheEv_;  // the submap's last cache store (the frame thread re-points cacheEv_)
+    baPost([this, s, n, S, slot, haveCache, lc, nk, cev]() { issueSubmap(s, n, S, slot, haveCache, lc, nk, cev); });
     P.job = lastJob_;
     inflight_.push_back(slot);
     lastSubmapEnqueued_ = s;
@@ -445,7 +447,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
 }
 
 void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache,
-                        std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk) {
+                        std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk, hipEvent_t cev) {
     Pending& P = ring_[slot];
     const uint32_t L = S + 1;
     const int bi = (int)(s & 1u);
@@ -453,7 +455,7 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
     // ---- local solve over frames base .. base+n-1 (first frame fixed), on the local stream ----------
     // set bi was last read by global solve s - 2
     BF_HIP(hipStreamWaitEvent(localStream_, globalDone_[bi], 0));
-    if (cacheEv_) BF_HIP(hipStreamWaitEvent(localStream_, cacheEv_, 0));  // the submap's cache frames
+    if (cev) BF_HIP(hipStreamWaitEvent(localStream_, cev, 0));  // the submap's cache frames
     BF_HIP(hipMemcpyAsync(B.T.p, P.localInit, 64 * n, hipMemcpyHostToDevice, localStream_));
     matrices_to_poses(B.T.p, n, B.rot.p, B.trans, B.valid.p, localStream_);
     // multi-GPU: submap s's local solve runs on rank s % R only (the submaps are independent units,
@@ -867,7 +869,8 @@ void Recon::attachCache(Cache* c) {
     BF_REQUIRE(!c || c->config().width == opt_.cacheWidth && c->config().height == opt_.cacheHeight, BF_ERR_ARG,
                "cache size differs from the loop's cacheWidth x cacheHeight");
     cache_ = c;
-    if (c && !cacheEv_) BF_HIP(hipEventCreateWithFlags(&cacheEv_, hipEventDisableTiming));
+    for (hipEvent_t& e : cacheEvF_)
+        if (c && !e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
 
 void Recon::setFrameSource(uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH) {
@@ -898,12 +901,14 @@ void Recon::preprocessFrame(uint32_t f) {
     FrameRef& fr = frames_[f];
     BF_REQUIRE(fr.depth && fr.color, BF_ERR_STATE, "preprocessing needs the frame's frame-store slot (bf_recon_set_frame)");
     const hipStream_t ps = preproc_->stream();
-    // the preprocessing buffers (raw / filtered sensor depth) are read by the previous frame's cache store
-    if (cacheEv_ && cache_ && cache_->stream() != ps) BF_HIP(hipStreamWaitEvent(ps, cacheEv_, 0));
+    // the raw sensor-depth buffer this run ends in (slot f & 1) was last read by frame f - 2's cache store;
+    // frame f - 1's may still be running (its buffer is the other one)
+    if (cacheEvF_[f & 1] && cache_ && cache_->stream() != ps) BF_HIP(hipStreamWaitEvent(ps, cacheEvF_[f & 1], 0));
     // colour at the integration size already: the loop reads the raw colour itself (no copy); the raw
     // images stay registered for as long as the frame store's
     const bool colorAsIs = preproc_->colorWidth() == cam_.imageWidth && preproc_->colorHeight() == cam_.imageHeight;
-    preproc_->run(fr.rawDepth, fr.rawColor, const_cast<float*>(fr.depth), colorAsIs ? nullptr : const_cast<uint8_t*>(fr.color));
+    preproc_->run(fr.rawDepth, fr.rawColor, const_cast<float*>(fr.depth), colorAsIs ? nullptr : const_cast<uint8_t*>(fr.color),
+                  (int)(f & 1));
     if (colorAsIs) fr.color = fr.rawColor;
     // the scene stream first reads frame f in the batch of frame f + 1 (its integration is deferred,
     // pendingOp_), so it waits there (awaitPreproc), not here: frame f's preprocessing overlaps the
@@ -942,6 +947,7 @@ void Recon::storeCacheFrame(uint32_t f) {
                BF_ERR_ARG, "the attached cache's input size differs from the integration size: set a frame source (bf_recon_set_frame_source)");
     cache_->storeFrame(d, c, w, h);
     fr.cache = cache_->frame(f);
+    cacheEv_ = cacheEvF_[f & 1];
     BF_HIP(hipEventRecord(cacheEv_, cache_->stream()));
 }
 

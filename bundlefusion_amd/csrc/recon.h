@@ -103,7 +103,7 @@ private:
     };
     void endSubmap(uint32_t s, uint32_t numFrames);
     void issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache, std::pair<BFEntryJ*, uint32_t> lc,
-                     uint32_t nk);
+                     uint32_t nk, hipEvent_t cacheEv);
     void issueEndSolve(uint32_t slot, uint32_t nk, uint32_t ncorr, float wDense, hipEvent_t t0, hipEvent_t t1);
     void applyPending(bool block);
     void apply(Pending& p);
@@ -221,7 +221,8 @@ private:
     std::vector<BFFixOp> log_;
 
     Cache* cache_ = nullptr;            // attached frame cache (borrowed)
-    hipEvent_t cacheEv_ = nullptr;      // the last storeFrame on the cache's stream
+    hipEvent_t cacheEv_ = nullptr;      // the last storeFrame on the cache's stream (one of cacheEvF_)
+    hipEvent_t cacheEvF_[2] = {nullptr, nullptr};  // frame f's storeFrame: cacheEvF_[f & 1]
     Preproc* preproc_ = nullptr;        // attached input preprocessing (borrowed)
     hipEvent_t preEv_[2] = {nullptr, nullptr};  // preprocessing of frames of each parity, on its stream
     bool prePending_[2] = {false, false};        // recorded and not yet awaited by the scene stream
