@@ -737,7 +737,7 @@ def main():
                                            "the march is bound by load latency, not bandwidth"},
                       "splat_roofline": {"kernel": "k_splat (ray-interval splat)", "atomics_per_render": atomics,
                                          "atomics_per_us": atomics / max(1e-9, splat_us),
-                                         "note": "per covered pixel and pass a 4-B read, and an atomic min / max only where it lowers / raises the target"},
+                                         "note": "per covered pixel one atomic min (near pass) and one atomic max (far pass), issued without waiting for a return value"},
                       "note": f"compactify + interval splat + renderKernel + computeNormals at {W_}x{H_} from the last pose"}
     # marching cubes over the final scene (StopScanningAndExtractIsoSurfaceMC, reported beside the metric)
     mcp = bfa.mc_params(params.virtualVoxelSize)

@@ -120,17 +120,16 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
         const uint32_t w = (uint32_t)(x1 - x0 + 1), npx = w * (uint32_t)(y1 - y0 + 1);
         const uint32_t emin = enc_f(dwMin), emax = enc_f(dwMax);
         quads++;
-        // ~30 quads cover a pixel: read first and issue the atomic only where it can still change the
-        // value (the targets only decrease / increase, so a stale read can only cause a redundant atomic)
+        // every covered pixel takes an atomic min / max (no return value: the wave does not wait on
+        // them). Reading the target first to skip the atomics that cannot change it cut them 3x
+        // (8.9 -> 2.9 M per render) but put a dependent load in front of each: 143 -> 178 us
+        atoms += npx * ((minOk ? 1u : 0u) + (maxOk ? 1u : 0u));
         for (uint32_t k = lane; k < npx; k += 64) {
             const uint32_t idx = (uint32_t)(y0 + (int)(k / w)) * rp.width + (uint32_t)(x0 + (int)(k % w));
-            const uint32_t cmn = minOk ? __builtin_nontemporal_load(&smin[idx]) : 0u;
-            const uint32_t cmx = maxOk ? __builtin_nontemporal_load(&smax[idx]) : 0xFFFFFFFFu;
-            if (minOk && emin < cmn) { atomicMin(&smin[idx], emin); atoms++; }
-            if (maxOk && emax > cmx) { atomicMax(&smax[idx], emax); atoms++; }
+            if (minOk) atomicMin(&smin[idx], emin);
+            if (maxOk) atomicMax(&smax[idx], emax);
         }
     }
-    atoms = wave_sum_u32(atoms);  // per lane above
     if (lane == 0 && quads) {
         atomicAdd(&stats[RS_QUADS], (unsigned long long)quads);
         atomicAdd(&stats[RS_ATOMICS], (unsigned long long)atoms);
