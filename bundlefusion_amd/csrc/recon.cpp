@@ -5,11 +5,30 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <unordered_set>
 
 namespace bf {
+
+#ifdef BF_HOST_PROFILE  // diagnostic build (tools/build_variant.sh): host time per loop section
+namespace {
+enum HostSec { HS_PRE, HS_CACHE, HS_PENDING, HS_SUBMAP, HS_QUEUE, HS_SCENE, HS_GC, HS_ALL, HS_N };
+const char* kHostSecName[HS_N] = {"preprocess", "cache", "applyPending", "endSubmap", "queue", "applyOps", "gc", "processFrame"};
+double g_hostSec[HS_N];
+uint64_t g_hostFrames;
+struct HostTimer {
+    HostSec s;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    explicit HostTimer(HostSec x) : s(x) {}
+    ~HostTimer() { g_hostSec[s] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count(); }
+};
+}  // namespace
+#define BF_HOST_T(sec) HostTimer bf_host_timer_(sec)
+#else
+#define BF_HOST_T(sec) ((void)0)
+#endif
 
 BFMat4 mat4_mul(const BFMat4& a, const BFMat4& b);  // api.cpp
 
@@ -174,6 +193,13 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
 }
 
 Recon::~Recon() {
+#ifdef BF_HOST_PROFILE
+    if (g_hostFrames) {
+        fprintf(stderr, "host us per frame over %llu frames:", (unsigned long long)g_hostFrames);
+        for (int k = 0; k < HS_N; k++) fprintf(stderr, " %s %.1f", kHostSecName[k], g_hostSec[k] / (double)g_hostFrames);
+        fprintf(stderr, "\n");
+    }
+#endif
     if (baThread_.joinable()) {
         {
             std::lock_guard<std::mutex> lk(baMu_);
@@ -303,7 +329,10 @@ void Recon::awaitPreproc(uint32_t f) {
 void Recon::runReintegrate() {
     // the batch integrates the previous frame (pendingOp_): it reads that frame's preprocessed images
     if (pendingInt_ && numFrames_ > 0) awaitPreproc(numFrames_ - 1);
-    tm_->nextFixes(opt_.maxFrameFixes, ops_);
+    {
+        BF_HOST_T(HS_QUEUE);
+        tm_->nextFixes(opt_.maxFrameFixes, ops_);
+    }
     traceQueue(2, 0, (uint32_t)ops_.size(), nullptr, &ops_);
     std::vector<VoxelOp>& batch = batch_;
     batch.clear();
@@ -332,9 +361,15 @@ void Recon::runReintegrate() {
         }
         st_.fixOps++;
     }
-    for (size_t k = 0; k < batch.size(); k += Scene::kMaxOps)
-        scene_->applyOps(batch.data() + k, (uint32_t)std::min<size_t>(Scene::kMaxOps, batch.size() - k), cam_);
-    scene_->garbageCollect();
+    {
+        BF_HOST_T(HS_SCENE);
+        for (size_t k = 0; k < batch.size(); k += Scene::kMaxOps)
+            scene_->applyOps(batch.data() + k, (uint32_t)std::min<size_t>(Scene::kMaxOps, batch.size() - k), cam_);
+    }
+    {
+        BF_HOST_T(HS_GC);
+        scene_->garbageCollect();
+    }
     logOp(4, 0, nullptr);
 }
 
@@ -347,13 +382,27 @@ void Recon::processFrame(uint32_t f) {
     // CUDAImageManager::process (DepthSensing.cpp:986 -> CUDAImageManager.cpp:22-158): the raw sensor
     // frame into its frame-store slot; the scene stream (which integrates it with the next frame's batch)
     // and the cache (which reads the raw depth) are ordered after it by an event
-    if (preproc_ && frames_[f].rawDepth) preprocessFrame(f);
+#ifdef BF_HOST_PROFILE
+    HostTimer allT(HS_ALL);
+    g_hostFrames++;
+#endif
+    if (preproc_ && frames_[f].rawDepth) {
+        BF_HOST_T(HS_PRE);
+        preprocessFrame(f);
+    }
     // processInput -> storeCachedFrame before anything reads the frame's cache (the submap ending at
     // this frame includes it as its overlap frame)
-    if (cache_) storeCacheFrame(f);
-    applyPending(false);
+    if (cache_) {
+        BF_HOST_T(HS_CACHE);
+        storeCacheFrame(f);
+    }
+    {
+        BF_HOST_T(HS_PENDING);
+        applyPending(false);
+    }
     FrameRef& fr = frames_[f];
     if (f % S == 0 && f > 0) {
+        BF_HOST_T(HS_SUBMAP);
         endSubmap(s - 1, S + 1);
         if (!opt_.asyncBundling) applyPending(true);
         if (!kfSolved_[s]) {  // solver result not back yet: dead-reckon the new keyframe
@@ -857,6 +906,10 @@ BFReconStats Recon::stats() {
 void Recon::resetStats() {
     synchronize();
     st_ = BFReconStats{};
+#ifdef BF_HOST_PROFILE
+    for (double& v : g_hostSec) v = 0.0;
+    g_hostFrames = 0;
+#endif
     scene_->resetStats();
     scene_->integrateClock().reset();
     scene_->applyClock().reset();
