@@ -193,13 +193,6 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
 }
 
 Recon::~Recon() {
-#ifdef BF_HOST_PROFILE
-    if (g_hostFrames) {
-        fprintf(stderr, "host us per frame over %llu frames:", (unsigned long long)g_hostFrames);
-        for (int k = 0; k < HS_N; k++) fprintf(stderr, " %s %.1f", kHostSecName[k], g_hostSec[k] / (double)g_hostFrames);
-        fprintf(stderr, "\n");
-    }
-#endif
     if (baThread_.joinable()) {
         {
             std::lock_guard<std::mutex> lk(baMu_);
@@ -890,6 +883,13 @@ void Recon::synchronize() {
 }
 
 BFReconStats Recon::stats() {
+#ifdef BF_HOST_PROFILE
+    if (g_hostFrames) {
+        fprintf(stderr, "host us per frame (since the last resetStats) over %llu frames:", (unsigned long long)g_hostFrames);
+        for (int k = 0; k < HS_N; k++) fprintf(stderr, " %s %.1f", kHostSecName[k], g_hostSec[k] / (double)g_hostFrames);
+        fprintf(stderr, "\n");
+    }
+#endif
     synchronize();
     BFReconStats s = st_;
     if (opt_.enableTiming) {
