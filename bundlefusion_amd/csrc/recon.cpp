@@ -1,6 +1,8 @@
 // recon.cpp — see recon.h.
 #include "recon.h"
 
+#include "host_pool.h"
+
 #include <cstdlib>
 
 #include <algorithm>
@@ -865,10 +867,12 @@ void Recon::apply(Pending& P) {
     // frames of invalid keyframes (and of invalidated local submaps) get -inf transforms: the queue
     // de-integrates them (invalidateImages + updateTrajectoryCU, OnlineBundler.cpp:317-320, 387-394)
     const uint32_t optimized = P.endSolve ? std::min(optimizedFrames_, numFrames_) : std::min(S * s + std::min(n, S), numFrames_);
-    for (uint32_t g = 0; g < optimized; g++) {
-        const uint32_t k = g / S;
-        complete_[g] = (globalValid_[k] && localKnown_[k]) ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();
-    }
+    HostPool::get().parallel_for(optimized, [this, S](size_t b, size_t e) {  // independent per frame
+        for (size_t g = b; g < e; g++) {
+            const size_t k = g / S;
+            complete_[g] = (globalValid_[k] && localKnown_[k]) ? mat4_mul(globalT_[k], localTraj_[k][g % S]) : ninf_mat();
+        }
+    }, 1024);
     tm_->updateOptimizedTransforms(complete_.data(), optimized);
     traceQueue(1, 0, optimized, complete_.data(), nullptr);
 }

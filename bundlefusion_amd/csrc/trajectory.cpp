@@ -1,6 +1,8 @@
 // trajectory.cpp — see trajectory.h. Host code (the reference's TrajectoryManager is host C++).
 #include "trajectory.h"
 
+#include "host_pool.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -138,12 +140,18 @@ TrajectoryManager::TrajectoryManager(uint32_t maxFrames, uint32_t topNActive, fl
 }
 
 void TrajectoryManager::setIntegrated(uint32_t i, const BFMat4& T) {
-    if (std::memcmp(frames_[i].integrated.m, T.m, sizeof(T.m)) != 0) integratedPose_[i].valid = false;
+    if (std::memcmp(frames_[i].integrated.m, T.m, sizeof(T.m)) != 0 && integratedPose_[i].valid) {
+        integratedPose_[i].valid = false;
+        stalePoses_++;
+    }
     frames_[i].integrated = T;
 }
 
 void TrajectoryManager::setOptimized(uint32_t i, const BFMat4& T) {
-    if (std::memcmp(optimized_[i].m, T.m, sizeof(T.m)) != 0) optimizedPose_[i].valid = false;
+    if (std::memcmp(optimized_[i].m, T.m, sizeof(T.m)) != 0 && optimizedPose_[i].valid) {
+        optimizedPose_[i].valid = false;
+        stalePoses_++;
+    }
     optimized_[i] = T;
 }
 
@@ -172,6 +180,28 @@ void TrajectoryManager::invalidateFrame(uint32_t i) {
 
 void TrajectoryManager::generateUpdateLists() {
     const uint32_t numFrames = std::min(numOptimized_, numAdded_);
+    // the MatrixToPose conversions of the transforms that changed (after a solve: every frame's
+    // optimized one) are independent per frame: on the host pool when there are many, before the
+    // serial pass (new frames' caches start invalid and are converted here too)
+    const size_t minPer = stalePoses_ >= 1024 ? 256 : ~(size_t)0;
+    stalePoses_ = 0;
+    HostPool::get().parallel_for(numFrames, [this](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) {
+            if (optimized_[i].m[0] == NEG_INF) continue;
+            PoseCache& co = optimizedPose_[i];
+            PoseCache& ci = integratedPose_[i];
+            if (!co.valid) {
+                pose_helper_matrix_to_pose(optimized_[i], co.p);
+                co.valid = true;
+                ci.fresh = true;  // the distance must be recomputed below
+            }
+            if (!ci.valid) {
+                pose_helper_matrix_to_pose(frames_[i].integrated, ci.p);
+                ci.valid = true;
+                ci.fresh = true;
+            }
+        }
+    }, minPer);
     for (uint32_t i = 0; i < numFrames; i++) {
         Frame& f = frames_[i];
         if (optimized_[i].m[0] == NEG_INF) {
@@ -185,15 +215,8 @@ void TrajectoryManager::generateUpdateLists() {
         // the distance changes only with one of the two poses, i.e. when a cache was invalidated
         PoseCache& co = optimizedPose_[i];
         PoseCache& ci = integratedPose_[i];
-        if (co.valid && ci.valid) continue;
-        if (!co.valid) {
-            pose_helper_matrix_to_pose(optimized_[i], co.p);
-            co.valid = true;
-        }
-        if (!ci.valid) {
-            pose_helper_matrix_to_pose(f.integrated, ci.p);
-            ci.valid = true;
-        }
+        if (!ci.fresh) continue;
+        ci.fresh = false;
         float po[6], pi[6];
         std::memcpy(po, co.p, sizeof(po));
         std::memcpy(pi, ci.p, sizeof(pi));

@@ -8,6 +8,7 @@
 // order of equal keys unspecified; here equal keys keep ascending frame index (stable sort over
 // the frame-added order), so every shard of a multi-GPU run derives the identical op list.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <deque>
 #include <vector>
@@ -87,8 +88,10 @@ private:
     struct PoseCache {
         float p[6];
         bool valid = false;
+        bool fresh = false;  // (integrated entry) a pose of the frame was converted since its distance was computed
     };
     std::vector<PoseCache> integratedPose_, optimizedPose_;
+    size_t stalePoses_ = 0;  // caches invalidated since the last generateUpdateLists
     std::vector<uint64_t> sortKeys_, sortKeys2_;
     std::vector<uint32_t> sortTmp_;
     uint32_t topN_;
