@@ -160,6 +160,33 @@ def test_queue_ties_match_oracle(seed):
         assert prod.frame_info(f) == orc.frame_info(f)
 
 
+def test_queue_long_stream_matches_oracle():
+    """1 600 frames with every frame's optimized pose changed by each update: the product converts the
+    changed poses on its host pool (more than 1 024 stale poses), the oracle serially; op lists and
+    per-frame distances must agree."""
+    rng = np.random.default_rng(9)
+    F = 1600
+    prod, orc = TrajectoryManager(F), OracleTM(F)
+    ang = rng.uniform(-np.pi, np.pi, F)
+    traj = np.tile(np.eye(4, dtype=np.float32), (F, 1, 1))
+    traj[:, 0, 0], traj[:, 0, 1], traj[:, 1, 0], traj[:, 1, 1] = np.cos(ang), -np.sin(ang), np.sin(ang), np.cos(ang)
+    traj[:, :3, 3] = rng.normal(size=(F, 3))
+    for f in range(F):
+        if f % 10 == 0 and f > 0:
+            a = rng.normal(0, 1e-3, f).astype(np.float32)
+            corr = np.tile(np.eye(4, dtype=np.float32), (f, 1, 1))
+            corr[:, 0, 0], corr[:, 0, 1], corr[:, 1, 0], corr[:, 1, 1] = np.cos(a), -np.sin(a), np.sin(a), np.cos(a)
+            corr[:, :3, 3] = rng.normal(0, 5e-3, (f, 3))
+            opt = np.einsum("nij,njk->nik", traj[:f], corr).astype(np.float32)
+            prod.update_optimized(opt)
+            orc.update_optimized(opt)
+        assert_same_ops(prod.next_fixes(10), orc.next_fixes(10))
+        prod.add_frame(0, traj[f], f)
+        orc.add_frame(0, traj[f], f)
+    for f in range(F):
+        assert prod.frame_info(f) == orc.frame_info(f)
+
+
 def test_queue_semantics_by_hand():
     """Reference behaviour spelled out: integrated frames whose optimized pose moved are re-integrated
     largest distance first (top 30, dist > 0); -inf frames are de-integrated; a re-validated frame is
