@@ -98,7 +98,9 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     // free, Scene::Scene). Measured on one GPU as one rank's share (--rehearse-shards G): +7 % at G = 4,
     // +11 % at G = 8, neutral at G = 2; unsharded it costs 3 % (the scene stream is the bound there),
     // so the streams keep the default priority (profiles/r3n_late_experiments.txt).
-    if (so && so->shardCount > 1) {
+    bool baHigh = so && so->shardCount > 1;
+    if (const char* e = std::getenv("BF_BA_HIGH_PRIORITY")) baHigh = std::atoi(e) != 0;  // A/B measurements
+    if (baHigh) {
         int prLeast = 0, prGreatest = 0;
         BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
         BF_HIP(hipStreamCreateWithPriority(&baStream_, hipStreamNonBlocking, prGreatest));
