@@ -392,8 +392,9 @@ def sens_main(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--frames", type=int, default=5000,
-                    help="stream length (BASELINE north star: 5000 frames); independent of --steps")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="stream length (BASELINE north star: 5000 frames; --preset config5: 10000, config 5's length); "
+                         "independent of --steps")
     ap.add_argument("--steps", type=int, default=50, help="timed submaps (10 frames each) at the stream's tail")
     ap.add_argument("--warmup", type=int, default=5, help="untimed submaps right before the timed ones")
     ap.add_argument("--width", type=int, default=None)
@@ -403,7 +404,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=None)
     ap.add_argument("--preset", choices=["config1", "config5"], default="config1",
                     help="config1: BASELINE north star (640x480, 4 mm, 2^23 buckets, 2^21 blocks); config5: "
-                         "1280x960 depth at 2 mm voxels (2^24 buckets, 2^23 blocks: a heap beyond the "
+                         "1280x960 depth at 2 mm voxels over 10 000 frames (2^24 buckets, 2^23 blocks: a heap beyond the "
                          "reference's 2^22-block int32 voxel index); explicit size flags override")
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="single process: run rank 0's share of a G-way TSDF-sharded job (scene chunk shard 0 "
@@ -438,8 +439,8 @@ def main():
                          "workload equals this run's, else traffic is null. Default: the first "
                          "profiles/apply_pass_pmc*.json whose workload matches")
     args = ap.parse_args()
-    preset = {"config1": dict(width=640, height=480, voxel=0.004, buckets=1 << 23, blocks=1 << 21),
-              "config5": dict(width=1280, height=960, voxel=0.002, buckets=1 << 24, blocks=1 << 23)}[args.preset]
+    preset = {"config1": dict(width=640, height=480, voxel=0.004, buckets=1 << 23, blocks=1 << 21, frames=5000),
+              "config5": dict(width=1280, height=960, voxel=0.002, buckets=1 << 24, blocks=1 << 23, frames=10000)}[args.preset]
     for k, v in preset.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
