@@ -115,6 +115,9 @@ public:
     void resultAsync(uint32_t* pinnedCtrl);
     static SolveResult decodeResult(const uint32_t* ctrl);
     static constexpr uint32_t kResultWords = 19;
+    // image count up to which a persistent global PCG runs with one finisher workgroup (2 rows per
+    // thread): its grid, about N / 4 + 2 workgroups, takes at most a quarter of the device's slots
+    static constexpr uint32_t kSmallPersistImages = 2 * 256 + 1;
     // device-side SBA::removeMaxResidualCUDA after a solve with findMaxResidual
     void removeMaxResidualAsync(BFEntryJ* corr, uint32_t n, int* valid, uint32_t numImages, float thresh);
     // async local verification after a solve with findMaxResidual (its high-residual count decides

@@ -27,6 +27,7 @@ namespace {
 
 constexpr float FLOAT_EPSILON = 0.000001f;  // Source/SolverUtil.h:9
 constexpr int WG = 256;
+static_assert(Solver::kSmallPersistImages == 2 * WG + 1, "the small persistent route (one finisher, 2 rows per thread)");
 constexpr uint32_t TILE = 256;  // correspondences per table-build tile, per 256 images (a.tile)
 // tile size for n images: the [n][nTiles] count matrix stays ~nCorr entries at any image count (a
 // fixed 256 made it 8 x nCorr at 2 001 images: 955 us of strided count writes per solve)

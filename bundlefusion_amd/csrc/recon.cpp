@@ -92,13 +92,19 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     opt_.maxGlobalCorr = or_default(o.maxGlobalCorr, opt_.maxKeyframes * 1000u);
 
     BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
-    // A sharded scene leaves each GPU a fraction of the voxel work and the (replicated) bundling
-    // becomes co-critical: its dependent PCG launches then queue at the highest priority, so they take
-    // CU slots ahead of the scene stream's next workgroups (with one voxel-pass workgroup per CU left
-    // free, Scene::Scene). Measured on one GPU as one rank's share (--rehearse-shards G): +7 % at G = 4,
-    // +11 % at G = 8, neutral at G = 2; unsharded it costs 3 % (the scene stream is the bound there),
-    // so the streams keep the default priority (profiles/r3n_late_experiments.txt).
-    bool baHigh = so && so->shardCount > 1;
+    // Bundling streams at the highest queue priority take CU slots ahead of the scene stream's next
+    // workgroups (priority orders dispatch; it never preempts a running workgroup):
+    // - sharded, each GPU has a fraction of the voxel work and the (replicated) bundling is co-critical:
+    //   +7 % at G = 4, +11 % at G = 8 (one rank's share on one GPU, profiles/r3n_late_experiments.txt);
+    // - unsharded with a global solve that stays on the small persistent route (<= 513 keyframes, a grid
+    //   of at most a quarter of the slots): 1 300 -> 1 362-1 367 frames/s on the bench stream. At normal
+    //   priority each of a solve's dependent launches waits for slots behind the voxel pass, the submap's
+    //   result misses its hand-off frame and the frame loop blocks with less work queued
+    //   (profiles/r8u_ba_priority_ab.txt, r8v_*);
+    // - unsharded with larger global solves (config 4's 2 000 keyframes: the grid needs nearly every
+    //   slot), the priority starves the scene stream instead: 981 -> 921 frames/s, so those keep the
+    //   default priority.
+    bool baHigh = (so && so->shardCount > 1) || opt_.maxKeyframes <= Solver::kSmallPersistImages;
     if (const char* e = std::getenv("BF_BA_HIGH_PRIORITY")) baHigh = std::atoi(e) != 0;  // A/B measurements
     if (baHigh) {
         int prLeast = 0, prGreatest = 0;
