@@ -653,6 +653,27 @@ int bf_comm_create(const uint8_t id[128], int nranks, int rank, bf_comm** out) {
     *out = h;
     BF_CATCH
 }
+int bf_comm_create_loopback(int nranks, int timeoutMs, bf_comm** out) {
+    BF_TRY
+    BF_REQUIRE(out && nranks >= 1, BF_ERR_ARG, "null argument / nranks");
+    auto group = Comm::loopbackGroup(nranks, timeoutMs);
+    std::vector<bf_comm*> made;
+    try {
+        for (int r = 0; r < nranks; r++) {
+            bf_comm* h = new bf_comm();
+            made.push_back(h);
+            h->c = new Comm(group, r);
+        }
+    } catch (...) {
+        for (bf_comm* h : made) {
+            delete h->c;
+            delete h;
+        }
+        throw;
+    }
+    for (int r = 0; r < nranks; r++) out[r] = made[(size_t)r];
+    BF_CATCH
+}
 int bf_comm_destroy(bf_comm* c) {
     BF_TRY
     if (c) {

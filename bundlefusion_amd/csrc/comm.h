@@ -8,14 +8,24 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 
 namespace bf {
+
+struct Loopback;
 
 class Comm {
 public:
     static constexpr size_t kIdBytes = 128;  // NCCL_UNIQUE_ID_BYTES
     static void uniqueId(uint8_t* out);
     Comm(const uint8_t* id, int nranks, int rank);
+    // In-process loopback group (tests): nranks communicators in one process, each rank driven from its
+    // own host thread (ranks may share a GPU). A collective synchronizes the calling rank's stream,
+    // exchanges through host memory behind a barrier (a rank that never arrives fails it after
+    // timeoutMs instead of hanging) and sums in rank order, so the call sites of the multi-rank path
+    // run without one GPU per rank; RCCL itself is not exercised.
+    static std::shared_ptr<Loopback> loopbackGroup(int nranks, int timeoutMs);
+    Comm(std::shared_ptr<Loopback> group, int rank);
     ~Comm();
     int size() const { return nranks_; }
     int rank() const { return rank_; }
@@ -26,6 +36,7 @@ public:
 
 private:
     void* comm_ = nullptr;  // ncclComm_t
+    std::shared_ptr<Loopback> lb_;
     int nranks_ = 1, rank_ = 0;
 };
 

@@ -117,6 +117,29 @@ class Comm:
             self.h = None
 
 
+class LoopbackComm:
+    """One rank of an in-process loopback group (bf_comm_create_loopback): the multi-rank loop's
+    collectives for ranks driven from threads of one process, exchanged through host memory (tests;
+    no RCCL). Same .h / .rank / .world / .close() as Comm."""
+
+    def __init__(self, h, rank: int, world: int):
+        self.h, self.rank, self.world = h, rank, world
+
+    @staticmethod
+    def group(world: int, timeout_ms: int = 120000) -> list["LoopbackComm"]:
+        import ctypes as C
+        from . import check, lib
+        hs = (C.c_void_p * world)()
+        check(lib().bf_comm_create_loopback(C.c_int(world), C.c_int(timeout_ms), hs))
+        return [LoopbackComm(C.c_void_p(hs[r]), r, world) for r in range(world)]
+
+    def close(self):
+        from . import lib
+        if self.h:
+            lib().bf_comm_destroy(self.h)
+            self.h = None
+
+
 def chunk_owner_array(blocks, voxel_size: float, shard_count: int, chunk: float = 1.0):
     """chunk_owner over an int array of block coordinates [n, 3] (same float32 / int32 arithmetic)."""
     import numpy as np

@@ -229,6 +229,11 @@ typedef struct bf_comm bf_comm;
 int bf_comm_unique_id(uint8_t id[128]);
 int bf_comm_create(const uint8_t id[128], int nranks, int rank, bf_comm** out);
 int bf_comm_destroy(bf_comm* c);
+/* In-process loopback group (tests): out[0..nranks-1] are communicators of one group for ranks driven from
+ * their own host threads in this process (they may share a GPU). Collectives synchronize the calling rank's
+ * stream and exchange through host memory behind a barrier that fails after timeoutMs (0: 60 s) if a rank
+ * never arrives; sums run in rank order. Lets the multi-rank loop run on one GPU; RCCL is not involved. */
+int bf_comm_create_loopback(int nranks, int timeoutMs, bf_comm** out);
 /* in-place sum over ranks of n doubles (device pointer); synchronizes (tests) */
 int bf_comm_allreduce_sum_f64(bf_comm* c, double* d, size_t n);
 /* shard the solver's pairs: count shards, this is shard index; comm (count ranks) or NULL (no
