@@ -1,6 +1,6 @@
-"""GPU: the multi-rank reconstruction loop with its communicator, two ranks on one GPU.
+"""GPU: the multi-rank reconstruction loop with its communicator, 2 and 3 ranks on one GPU.
 
-Each rank is a bf_recon with TSDF shard r of 2 and a communicator of one in-process loopback group
+Each rank is a bf_recon with TSDF shard r of G and a communicator of one in-process loopback group
 (bf_comm_create_loopback), driven from its own host thread, as one process per GPU drives its loop. With
 the communicator the ranks take the multi-GPU code paths: local solves round-robin by submap with the
 solved poses broadcast from the owner, the global solve's image-pair statistics built on the owning rank
@@ -25,15 +25,15 @@ from oracle_lib import blocks_of
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 
-@pytest.mark.parametrize("async_bundling,lag", [(0, 0), (1, 20)])
-def test_two_rank_loops_with_communicator_match_the_unsharded_loop(async_bundling, lag):
+@pytest.mark.parametrize("world,async_bundling,lag", [(2, 0, 0), (2, 1, 20), (3, 1, 20)])
+def test_rank_loops_with_communicator_match_the_unsharded_loop(world, async_bundling, lag):
     F, VOX, CHUNK = 80, 0.01, 0.5
-    streams = [SyntheticStream(F, width=160, height=120, cache_source="loop") for _ in range(3)]
+    streams = [SyntheticStream(F, width=160, height=120, cache_source="loop") for _ in range(world + 1)]
     st = streams[0]
     params = bfa.hash_params(voxel_size=VOX, num_buckets=1 << 16, num_blocks=1 << 15)
     K = st.K
     loops = []
-    for (count, index), sti in zip([(1, 0), (2, 0), (2, 1)], streams):
+    for (count, index), sti in zip([(1, 0)] + [(world, r) for r in range(world)], streams):
         opts = recon_options(F, recordOps=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=st.cache_intrinsics,
                              maxGlobalCorr=max(1000, 25 * K * (K - 1) // 2), maxKeyframes=K + 1,
                              asyncBundling=async_bundling, resultLag=lag)
@@ -42,10 +42,10 @@ def test_two_rank_loops_with_communicator_match_the_unsharded_loop(async_bundlin
         rc = Recon(params, st.cam, opts, so)
         sti.attach(rc)
         loops.append(rc)
-    full, r0, r1 = loops
-    comms = LoopbackComm.group(2)
-    r0.set_comm(comms[0])
-    r1.set_comm(comms[1])
+    full, ranks = loops[0], loops[1:]
+    comms = LoopbackComm.group(world)
+    for rc, c in zip(ranks, comms):
+        rc.set_comm(c)
 
     for f in range(F):  # the reference: one loop, no communicator
         full.process_frame(f)
@@ -63,7 +63,7 @@ def test_two_rank_loops_with_communicator_match_the_unsharded_loop(async_bundlin
         except Exception as e:  # noqa: BLE001 — re-raised below with its rank
             errors.append((i, repr(e)))
 
-    threads = [threading.Thread(target=rank, args=(i, rc)) for i, rc in enumerate((r0, r1))]
+    threads = [threading.Thread(target=rank, args=(i, rc)) for i, rc in enumerate(ranks)]
     for t in threads:
         t.start()
     for t in threads:
@@ -73,11 +73,11 @@ def test_two_rank_loops_with_communicator_match_the_unsharded_loop(async_bundlin
 
     keys = ("pastEndFrames", "globalSolves", "localSolved", "denseSolve", "queueDrained")
     assert end_full["denseSolve"] == 1
-    for i in (0, 1):
+    for i in range(world):
         assert [results[i][k] for k in keys] == [end_full[k] for k in keys]
     ref = full.op_log()
     assert sum(1 for k, *_ in ref if k == FIX_DEINTEGRATE) > 0
-    for rc in (r0, r1):
+    for rc in ranks:
         log = rc.op_log()
         assert len(log) == len(ref)
         for (k0, f0, o0, n0), (k1, f1, o1, n1) in zip(ref, log):
@@ -86,19 +86,19 @@ def test_two_rank_loops_with_communicator_match_the_unsharded_loop(async_bundlin
             np.testing.assert_array_equal(n0, n1)
         np.testing.assert_array_equal(rc.trajectory(F), full.trajectory(F))
     # each rank solved only its own local submaps (round-robin), together all of them
-    s_full, s0, s1 = full.stats(), r0.stats(), r1.stats()
-    assert s0["localSolves"] > 0 and s1["localSolves"] > 0
-    assert s0["localSolves"] + s1["localSolves"] == s_full["localSolves"]
-    assert s0["globalSolves"] == s1["globalSolves"] == s_full["globalSolves"]
+    s_full, s_ranks = full.stats(), [rc.stats() for rc in ranks]
+    assert all(s["localSolves"] > 0 for s in s_ranks)
+    assert sum(s["localSolves"] for s in s_ranks) == s_full["localSolves"]
+    assert all(s["globalSolves"] == s_full["globalSolves"] for s in s_ranks)
 
     fh, _, _, fv = full.export()
     fb = blocks_of(fh)
     union = {}
-    for i, rc in enumerate((r0, r1)):
+    for i, rc in enumerate(ranks):
         h, _, _, v = rc.export()
         b = blocks_of(h)
-        assert b and not (set(b) & set(union)), "a block is owned by both ranks"
-        assert np.all(chunk_owner_array(np.array(sorted(b)), VOX, 2, chunk=CHUNK) == i)
+        assert b and not (set(b) & set(union)), "a block is owned by two ranks"
+        assert np.all(chunk_owner_array(np.array(sorted(b)), VOX, world, chunk=CHUNK) == i)
         for k, ptr in b.items():
             union[k] = v[ptr:ptr + 512]
     assert set(union) == set(fb) and len(fb) > 500
