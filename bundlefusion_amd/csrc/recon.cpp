@@ -267,39 +267,52 @@ void Recon::setLocalCorrespondences(uint32_t submap, BFEntryJ* corr, uint32_t n)
 
 void Recon::setGlobalCorrespondences(BFEntryJ* corr, uint32_t n, const uint32_t* prefix, uint32_t numKeyframes) {
     BF_REQUIRE(n <= opt_.maxGlobalCorr, BF_ERR_CAPACITY, "global correspondences exceed maxGlobalCorr");
+    // the app appends each keyframe's correspondences to the same list: the pair bounds then extend
+    // from the new entries alone (no drain of the bundling stream, no copy of the whole list)
+    const bool extends = corr == globalCorr_ && n >= globalCorrN_ && numKeyframes >= globalPrefix_.size() &&
+                         std::equal(globalPrefix_.begin(), globalPrefix_.end(), prefix);
     globalCorr_ = corr;
     globalCorrN_ = n;
     globalPrefix_.assign(prefix, prefix + numKeyframes);
-    if (comm_) computePairBounds();
+    if (comm_) computePairBounds(extends);
 }
 
 void Recon::setComm(Comm* c) {
     BF_REQUIRE(numFrames_ == 0, BF_ERR_STATE, "set the communicator before the first frame");
     comm_ = c;
     global_->setShard(c ? (uint32_t)c->size() : 1u, c ? (uint32_t)c->rank() : 0u, c);
-    if (comm_ && globalCorr_) computePairBounds();
+    if (comm_ && globalCorr_) computePairBounds(false);
 }
 
-// The sharded global solve all-reduces its pair blocks, so the host must know how many there are:
-// count the distinct image pairs of every keyframe prefix once, from a host copy of the list
-// (removals and the per-image cap only ever drop pairs, so these counts bound every later solve).
-void Recon::computePairBounds() {
-    std::vector<BFEntryJ> h(globalCorrN_);
-    baDrain();
-    BF_HIP(hipStreamSynchronize(baStream_));
-    if (globalCorrN_) BF_HIP(hipMemcpy(h.data(), globalCorr_, sizeof(BFEntryJ) * globalCorrN_, hipMemcpyDeviceToHost));
-    std::unordered_set<uint64_t> seen;
-    pairBound_.assign(globalPrefix_.size(), 0);
-    uint32_t e = 0;
-    for (size_t s = 0; s < globalPrefix_.size(); s++) {
+// The sharded global solve all-reduces its pair blocks, so the host must know how many there are, the
+// same count on every rank: the distinct image pairs of every keyframe prefix, counted from the entries
+// as they were handed over (removals and the per-image cap only ever drop pairs, so these counts bound
+// every later solve). append: the list only grew since the last count (the app's per-keyframe appends),
+// so only the new entries are read, which no solve touches yet (a submap's issue captures the list
+// length of its own frame); otherwise everything is recounted after the bundling work drains.
+void Recon::computePairBounds(bool append) {
+    if (!append) {
+        baDrain();
+        BF_HIP(hipStreamSynchronize(baStream_));
+        pairSeen_.clear();
+        pairCountedN_ = 0;
+        pairBound_.clear();
+    }
+    const uint32_t from = std::min(pairCountedN_, globalCorrN_);
+    std::vector<BFEntryJ> h(globalCorrN_ - from);
+    if (!h.empty()) BF_HIP(hipMemcpy(h.data(), globalCorr_ + from, sizeof(BFEntryJ) * h.size(), hipMemcpyDeviceToHost));
+    uint32_t e = from;
+    for (size_t s = pairBound_.size(); s < globalPrefix_.size(); s++) {
         const uint32_t end = std::min(globalPrefix_[s], globalCorrN_);
         for (; e < end; e++) {
-            const uint32_t i = h[e].imgIdx_i, j = h[e].imgIdx_j;
+            const BFEntryJ& c = h[e - from];
+            const uint32_t i = c.imgIdx_i, j = c.imgIdx_j;
             if (i == BF_INVALID_IMAGE || i == j) continue;
-            seen.insert(((uint64_t)std::min(i, j) << 32) | std::max(i, j));
+            pairSeen_.insert(((uint64_t)std::min(i, j) << 32) | std::max(i, j));
         }
-        pairBound_[s] = (uint32_t)seen.size();
+        pairBound_.push_back((uint32_t)pairSeen_.size());
     }
+    pairCountedN_ = e;
 }
 
 void Recon::setInitialPose(const BFMat4& T0) {
@@ -490,7 +503,11 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     // everything below only issues work on baStream_ from state fixed at this point: the bundling
     // thread runs it while the frame loop goes on enqueuing scene work
     const hipEvent_t cev = cacheEv_;  // the submap's last cache store (the frame thread re-points cacheEv_)
-    baPost([this, s, n, S, slot, haveCache, lc, nk, cev]() { issueSubmap(s, n, S, slot, haveCache, lc, nk, cev); });
+    // the global list as of this frame: the frame thread may append keyframes' correspondences (the app)
+    // while a bundling thread issues this submap, so the issue works from these values, not the members
+    GlobalView gv{globalCorr_, globalCorrN_, (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_,
+                  (comm_ && s < pairBound_.size()) ? std::max(pairBound_[s], 1u) : 0u};
+    baPost([this, s, n, S, slot, haveCache, lc, nk, cev, gv]() { issueSubmap(s, n, S, slot, haveCache, lc, nk, cev, gv); });
     P.job = lastJob_;
     inflight_.push_back(slot);
     lastSubmapEnqueued_ = s;
@@ -499,7 +516,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
 }
 
 void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache,
-                        std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk, hipEvent_t cev) {
+                        std::pair<BFEntryJ*, uint32_t> lc, uint32_t nk, hipEvent_t cev, GlobalView gv) {
     Pending& P = ring_[slot];
     const uint32_t L = S + 1;
     const int bi = (int)(s & 1u);
@@ -583,12 +600,12 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
     // 399-405). Keyframe 0 is never invalidated (the reference exits on an invalid first chunk,
     // Bundler.cpp:377-384).
     const int* gate = (verify && s > 0) ? B.gate : nullptr;
-    if (gate && globalCorr_) invalidate_local(gate, s, dGlobalValid_.p, globalCorr_, globalCorrN_, baStream_);
-    const uint32_t ncorr = (s < globalPrefix_.size()) ? globalPrefix_[s] : globalCorrN_;
-    if (nk >= 2 && globalCorr_ && ncorr > 0) {
+    if (gate && gv.corr) invalidate_local(gate, s, dGlobalValid_.p, gv.corr, gv.n, baStream_);
+    const uint32_t ncorr = gv.ncorr;
+    if (nk >= 2 && gv.corr && ncorr > 0) {
         std::vector<float> ws(opt_.globalNonLin, 1.0f), wz(opt_.globalNonLin, 0.0f);  // SBA.cpp:34-39, dense off
         SolveArgs a{};
-        a.corr = globalCorr_;
+        a.corr = gv.corr;
         a.numCorr = ncorr;
         a.valid = dGlobalValid_.p;
         a.numImages = nk;
@@ -602,10 +619,10 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
         a.rebuildJT = true;
         a.findMaxResidual = true;
         a.gate = gate;
-        if (comm_ && s < pairBound_.size()) a.pairBound = std::max(pairBound_[s], 1u);
+        if (gv.pairBound) a.pairBound = gv.pairBound;
         global_->solve(a);
         // removeMaxResidualCUDA with getMaxResidual's (0, <10) exemption, on the device
-        global_->removeMaxResidualAsync(globalCorr_, ncorr, dGlobalValid_.p, nk, opt_.maxResidualThresh);
+        global_->removeMaxResidualAsync(gv.corr, ncorr, dGlobalValid_.p, nk, opt_.maxResidualThresh);
         global_->resultAsync(P.ctrl + Solver::kResultWords);
         P.globalSolved = true;
     }

@@ -27,6 +27,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/bf/bf.h"
@@ -102,8 +103,12 @@ private:
         BFCachedFrame* cacheTable = nullptr; // pinned staging [S+1] (H2D of the local cache table)
     };
     void endSubmap(uint32_t s, uint32_t numFrames);
+    struct GlobalView {  // the global correspondence list as a submap's issue sees it
+        BFEntryJ* corr;
+        uint32_t n, ncorr, pairBound;
+    };
     void issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache, std::pair<BFEntryJ*, uint32_t> lc,
-                     uint32_t nk, hipEvent_t cacheEv);
+                     uint32_t nk, hipEvent_t cacheEv, GlobalView gv);
     void issueEndSolve(uint32_t slot, uint32_t nk, uint32_t ncorr, float wDense, hipEvent_t t0, hipEvent_t t1);
     void applyPending(bool block);
     void apply(Pending& p);
@@ -149,7 +154,9 @@ private:
     std::vector<uint32_t> globalPrefix_;
     Comm* comm_ = nullptr;
     std::vector<uint32_t> pairBound_;  // distinct image pairs among the entries of each keyframe prefix
-    void computePairBounds();
+    std::unordered_set<uint64_t> pairSeen_;  // the pairs counted so far (entries [0, pairCountedN_))
+    uint32_t pairCountedN_ = 0;
+    void computePairBounds(bool append);
 
     std::vector<BFMat4> kf_;            // keyframe poses used for integration (solver or dead reckoning)
     std::vector<char> kfSolved_;        // kf_[k] came from the solver

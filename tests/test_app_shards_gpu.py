@@ -9,12 +9,13 @@ end-of-sequence phase. Outputs: each rank writes the mesh of its own blocks (<st
 alone the trajectory .sens and processed.txt. The multi-process form (one app per GPU, RCCL round-robin local
 solves + pair-stat all-reduce) is bench.py --sens under torchrun; its host plumbing is tests/test_dist.py."""
 import os
+import threading
 
 import numpy as np
 import pytest
 
 from bundlefusion_amd.app import FriedLiver
-from bundlefusion_amd.dist import chunk_owner_array
+from bundlefusion_amd.dist import LoopbackComm, chunk_owner_array
 from bundlefusion_amd.params import NORTH_STAR_APP, write_parameter_files
 from bundlefusion_amd.recon import FIX_DEINTEGRATE
 from bundlefusion_amd.stream import write_synthetic_sens
@@ -27,7 +28,11 @@ CHUNK = 0.5
 APP = dict(NORTH_STAR_APP, s_hashNumBuckets=1 << 20, s_hashNumSDFBlocks=1 << 18)
 
 
-def test_two_shard_apps_partition_the_unsharded_app(tmp_path):
+@pytest.mark.parametrize("with_comm", [False, True])
+def test_two_shard_apps_partition_the_unsharded_app(tmp_path, with_comm):
+    """with_comm: the shard apps also share an in-process loopback communicator (bf_comm_create_loopback)
+    and run from their own threads, so they take the multi-GPU bundling paths (round-robin local solves
+    with the broadcast, the pair-stat all-reduce, own-submap cache frames) and must still match."""
     d = str(tmp_path)
     sens = os.path.join(d, "synthetic.sens")
     write_synthetic_sens(sens, F, 640, 480)
@@ -39,10 +44,35 @@ def test_two_shard_apps_partition_the_unsharded_app(tmp_path):
         outs.append(out)
         apps.append(FriedLiver(pa, pb, output_dir=out, async_bundling=0, record_ops=True, shard=(count, index),
                                shard_chunk=CHUNK))
-    for f in range(F):
-        for a in apps:
-            assert a.step()
-    res = [a.finish() for a in apps]
+    if not with_comm:
+        for f in range(F):
+            for a in apps:
+                assert a.step()
+        res = [a.finish() for a in apps]
+    else:
+        comms = LoopbackComm.group(2)
+        apps[1].set_comm(comms[0])
+        apps[2].set_comm(comms[1])
+        for f in range(F):
+            assert apps[0].step()
+        res = [apps[0].finish(), None, None]
+        errors = []
+
+        def rank(i):
+            try:
+                for f in range(F):
+                    assert apps[i].step()
+                res[i] = apps[i].finish()
+            except Exception as e:  # noqa: BLE001 — reported below with its rank
+                errors.append((i, repr(e)))
+
+        threads = [threading.Thread(target=rank, args=(i,)) for i in (1, 2)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=500)
+        assert not any(t.is_alive() for t in threads), "a rank did not finish"
+        assert not errors, errors
     for k in ("pastEndFrames", "globalSolves", "localSolved", "denseSolve", "queueDrained"):
         assert res[1]["end"][k] == res[2]["end"][k] == res[0]["end"][k], k
     assert res[0]["end"]["denseSolve"] == 1
@@ -86,3 +116,6 @@ def test_two_shard_apps_partition_the_unsharded_app(tmp_path):
     assert res[1]["meshTriangles"] > 0 and res[2]["meshTriangles"] > 0
     for a in apps:
         a.close()
+    if with_comm:
+        for c in comms:
+            c.close()
