@@ -96,15 +96,15 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     // workgroups (priority orders dispatch; it never preempts a running workgroup):
     // - sharded, each GPU has a fraction of the voxel work and the (replicated) bundling is co-critical:
     //   +7 % at G = 4, +11 % at G = 8 (one rank's share on one GPU, profiles/r3n_late_experiments.txt);
-    // - unsharded with a global solve that stays on the small persistent route (<= 513 keyframes, a grid
-    //   of at most a quarter of the slots): 1 300 -> 1 362-1 367 frames/s on the bench stream. At normal
-    //   priority each of a solve's dependent launches waits for slots behind the voxel pass, the submap's
-    //   result misses its hand-off frame and the frame loop blocks with less work queued
-    //   (profiles/r8u_ba_priority_ab.txt, r8v_*);
-    // - unsharded with larger global solves (config 4's 2 000 keyframes: the grid needs nearly every
-    //   slot), the priority starves the scene stream instead: 981 -> 921 frames/s, so those keep the
-    //   default priority.
-    bool baHigh = (so && so->shardCount > 1) || opt_.maxKeyframes <= Solver::kSmallPersistImages;
+    // - unsharded, as long as the global solve's persistent grid (about N / 4 workgroups of the 512 slots
+    //   at 2 per CU) leaves the scene stream a quarter of the device: the bench stream (K = 500) 1 300 ->
+    //   1 362-1 367 frames/s, config 5's stream (K = 1 000) 181.6 -> 183.7. At normal priority each of a
+    //   solve's dependent launches waits for slots behind the voxel pass, the submap's result misses its
+    //   hand-off frame and the frame loop blocks with less work queued (profiles/r8u_*, r8v_*, r9b_*);
+    // - config 4's 2 000 keyframes, whose grid needs nearly every slot, starve the scene stream at high
+    //   priority instead (981 -> 921 frames/s), so solves that large keep the default priority.
+    constexpr uint32_t kHighPriorityMaxKeyframes = 1537;  // grid <= ~3/4 of the slots
+    bool baHigh = (so && so->shardCount > 1) || opt_.maxKeyframes <= kHighPriorityMaxKeyframes;
     if (const char* e = std::getenv("BF_BA_HIGH_PRIORITY")) baHigh = std::atoi(e) != 0;  // A/B measurements
     if (baHigh) {
         int prLeast = 0, prGreatest = 0;
