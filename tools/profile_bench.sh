@@ -12,6 +12,20 @@ OUT=gpurun_out/${TAG}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > $OUT/stats_bench.json 2> $OUT/stats_bench.err || { echo "stats pass failed"; tail -20 $OUT/stats_bench.err; exit 1; }
 python3 tools/prof_summary.py $OUT/stats/run_kernel_stats.csv > $OUT/kernel_stats.txt && head -25 $OUT/kernel_stats.txt
+# the dominant kernel over the bench's timed region only (its last roofline.launches dispatches): the figure
+# the bench line's avg_launch_us (HIP events) must agree with; the stats csv averages the whole stream
+python3 - $OUT/stats/run_kernel_trace.csv $OUT/stats_bench.json > $OUT/apply_timed_region.txt <<'PY'
+import csv, json, sys
+d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+n = int(d["roofline"]["launches"])
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_apply_ops" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+last = rows[-n:]
+us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
+print("k_apply_ops over the timed region (last %d of %d dispatches): avg %.1f us (rocprofv3 kernel trace); "
+      "the profiled bench line's HIP-event average %.1f us" % (len(us), len(rows), sum(us) / max(1, len(us)), d["roofline"]["avg_launch_us"]))
+PY
+cat $OUT/apply_timed_region.txt
 rm -f $OUT/stats/run_kernel_trace.csv  # per-dispatch rows are large; the stats csv is what we keep
 K=${PMC_KERNEL:-k_apply_ops}
 for C in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU; do
