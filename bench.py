@@ -48,6 +48,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 VALU_PEAK_WAVE_INSTS_PER_US = 256 * 4 * 2400 / 2
 
 
+# revision of k_apply_ops' memory behaviour: a PMC profile (profiles/apply_pass_pmc*.json) describes the
+# kernel only for the revision it recorded (2: z-halves no op reaches are not loaded)
+APPLY_PASS_REV = 2
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -365,6 +369,7 @@ def sens_main(args):
     group.barrier()
     dt = group.max(dt)
     st = rc.stats()
+    tm = app.timing()
     res = app.finish()
     out = {"metric": f"frames/s FriedLiver pipeline on {os.path.basename(args.sens)}", "value": done / dt,
            "unit": "frames/s", "n_gpus": world, "steps": done, "warmup": 0, "ms_per_step": dt / max(1, done) * 1e3,
@@ -379,6 +384,21 @@ def sens_main(args):
                                        "globalGnIterations", "globalPcgIterations", "removedPairs", "invalidLocals")},
            "end_phase": {k: res["end"][k] for k in ("pastEndFrames", "globalSolves", "localSolved", "denseSolve",
                                                      "queueDrained", "denseSolveMs")},
+           "host": {"decode_wait_ms_per_frame": tm["decodeWaitSeconds"] * 1e3 / max(1, done),
+                    "upload_preprocess_ms_per_frame": tm["uploadSeconds"] * 1e3 / max(1, done),
+                    "entryj_ms_per_frame": tm["corrSeconds"] * 1e3 / max(1, done),
+                    "loop_ms_per_frame": tm["loopSeconds"] * 1e3 / max(1, done),
+                    "decode_ms_per_frame_per_thread": tm["decodeSeconds"] * 1e3 / max(1, done),
+                    "decode_threads": tm["decodeThreads"],
+                    "upload_GBps": tm["uploadBytes"] / max(1e-9, tm["uploadSeconds"]) / 1e9,
+                    "loop_host_ms_per_frame": st["hostMs"] / max(1, st["frames"]),
+                    "loop_host_wait_ms_per_frame": st["hostWaitMs"] / max(1, st["frames"]),
+                    "note": "host time per frame inside bf_app_step by section (bf_app_timing); decode runs on "
+                            "prefetch threads beside the loop, so only decode_wait is on the critical path"},
+           "gpu": {"scene_kernel_ms_per_frame": (st["reintegrateKernelMs"] + st["integrateKernelMs"]) / max(1, done),
+                   "scene_stream_busy": (st["reintegrateKernelMs"] + st["integrateKernelMs"]) / 1e3 / dt,
+                   "apply_us_per_launch": st["reintegrateKernelMs"] * 1e3 / max(1, st["reintegrateLaunches"]),
+                   "global_ms_per_gn_iter_in_loop": st["globalSolveMs"] / max(1, st["globalGnIterations"])},
            "end_phase_s": res["endSeconds"], "heap_free": res["heapFreeCount"],
            "valid_transforms": [res["numValidTransforms"], res["numTransforms"]], "mesh_triangles": res["meshTriangles"]}
     if rank == 0:
@@ -554,17 +574,19 @@ def main():
     # dominant kernel: k_apply_ops, the op-batch voxel pass that applies a frame's re-integration
     # fixes (<= 10 x de-integrate + integrate) in one read + write per voxel. Per launch, from the
     # device counters of the same launches:
-    #   SURVEY §8(d) per-op bytes of the integrate kernel, summed over the launch's ops:
+    #   the fused pass's own bytes (roofline.achieved / frac): 20 B per work-list block (16 B entry + 4 B op
+    #     mask) + 12 B per voxel of every block z-half the pass loads (a half some op's mask reaches; 256
+    #     voxels) + 12 B per voxel written back + 8 B per pixel per op (the op's {depth, colour} image)
+    #   SURVEY §8(d) per-op bytes of the integrate kernel, summed over the launch's ops (what the reference's
+    #     one pass per op moves; an equivalent rate only, so no fraction of peak):
     #     8 B per pixel per op + 16 B per visible-list block per op + 24 B per in-band voxel update
-    #   the fused pass's own bytes: 20 B per work-list block (16 B entry + 4 B op mask) + 24 B per
-    #     voxel read + written once + 8 B per pixel per op
     launches = max(1, st["reintegrateLaunches"])
     kernel_ms = st["reintegrateKernelMs"]
-    alg_bytes = 8 * P * ss["batchOps"] + 16 * ss["batchBlocks"] * (ss["batchOps"] / launches) + 24 * ss["batchUpdates"]
-    pass_bytes = 20 * ss["batchBlocks"] + 24 * ss["batchVoxelsRMW"] + 8 * P * ss["batchOps"]
-    per_launch_bytes = alg_bytes / launches
+    survey_bytes = 8 * P * ss["batchOps"] + 16 * ss["batchBlocks"] * (ss["batchOps"] / launches) + 24 * ss["batchUpdates"]
+    pass_bytes = (20 * ss["batchBlocks"] + 12 * 256 * ss["batchHalves"] + 12 * ss["batchVoxelsRMW"]
+                  + 8 * P * ss["batchOps"])
     per_launch_s = kernel_ms / 1e3 / launches
-    achieved = per_launch_bytes / per_launch_s / 1e9
+    achieved = pass_bytes / launches / per_launch_s / 1e9
     traffic = None
     valu = None
     traffic_src = None
@@ -573,7 +595,7 @@ def main():
     for c in cands:
         if c and os.path.exists(c):
             tj = json.load(open(c))
-            if tj.get("workload") == workload:
+            if tj.get("workload") == workload and tj.get("pass_rev") == APPLY_PASS_REV:
                 args.traffic = c
                 break
     # counters are taken only from a profile of this same workload (tools/profile_bench.sh records
@@ -581,7 +603,7 @@ def main():
     evals_pl = ss["batchEvals"] / launches
     rmw_pl = ss["batchVoxelsRMW"] / launches
     traffic_units = None
-    if tj.get("workload") == workload and world == 1 and args.rehearse_shards <= 1:
+    if tj.get("workload") == workload and tj.get("pass_rev") == APPLY_PASS_REV and world == 1 and args.rehearse_shards <= 1:
         traffic_src = os.path.relpath(args.traffic, REPO)
         if "fetch_bytes_per_evaluation" in tj:
             # the profile's per-unit rates x this run's own per-launch counts (identical to the profiled
@@ -599,6 +621,9 @@ def main():
             valu = {"wave_insts_per_launch": vpl, "wave_insts_per_evaluation": tj.get("valu_insts_per_evaluation"),
                     "peak_wave_insts_per_us": VALU_PEAK_WAVE_INSTS_PER_US,
                     "frac": vpl / (us * VALU_PEAK_WAVE_INSTS_PER_US), "source": traffic_src}
+    hbm_cnt = traffic / per_launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
+    bound = ("valu-issue/latency" if valu and hbm_cnt is not None and valu["frac"] > hbm_cnt else
+             "latency" if hbm_cnt is None or hbm_cnt < 0.7 else "hbm")
     gn = max(1, st["globalGnIterations"])
     ms_gn_loop = st["globalSolveMs"] / gn
     solo = global_solve_timing(stream, K - 1)
@@ -647,22 +672,26 @@ def main():
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
         "roofline_ba": roofline_ba(solo),
         "global_dense_end_solve": dense_end,
-        "roofline": {"bound": "hbm", "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "roofline": {"bound": bound, "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "traffic_units": traffic_units,
                      "hbm_frac_counters": (traffic / per_launch_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                     "pass_frac": pass_bytes / launches / per_launch_s / 1e9 / HBM_PEAK_GBS,
-                     "launches": launches, "avg_launch_us": per_launch_s * 1e6,
-                     "alg_bytes_per_launch": per_launch_bytes,
-                     "alg_bytes_source": "SURVEY 8(d) per-op integrate bytes (8 P + 16 Nv + 24 V) x ops per launch",
-                     "alg_bytes_pass_per_launch": pass_bytes / launches,
-                     "note": "frac prices SURVEY 8(d)'s per-op bytes, what the reference's one pass per op moves; "
-                             "the batch reads and writes each voxel once for all of its ops, so frac can pass 1. "
-                             "The pass's own bytes give pass_frac, the PMC counters hbm_frac_counters; the kernel "
-                             "is bound by VALU issue and latency (valu.frac), not by HBM",
-                     "achieved_pass": pass_bytes / launches / per_launch_s / 1e9,
+                     "launches": launches, "avg_launch_us": per_launch_s * 1e6, "pass_rev": APPLY_PASS_REV,
+                     "alg_bytes_per_launch": pass_bytes / launches,
+                     "alg_bytes_source": "the fused pass's own bytes: 20 B per work-list block + 12 B per voxel of each "
+                                         "block z-half loaded (256 voxels; halves no op reaches are skipped) + 12 B per "
+                                         "voxel written + 8 B per pixel per op",
+                     "equivalent_GBps": survey_bytes / launches / per_launch_s / 1e9,
+                     "survey_bytes_per_launch": survey_bytes / launches,
+                     "survey_bytes_source": "SURVEY 8(d) per-op integrate bytes (8 P + 16 Nv + 24 V) x ops per launch: "
+                                            "what one reference pass per op would move; the batch reads and writes each "
+                                            "voxel once for all of its ops, so this is an equivalent rate, not a roofline "
+                                            "position",
+                     "note": "frac is the pass's own bytes against HBM peak (traffic / hbm_frac_counters: the PMC bytes "
+                             "of the same launches); bound names the resource that binds: VALU issue and dependency "
+                             "latency (valu.frac above the counters' HBM fraction), not HBM",
                      "per_launch": {"work_list_blocks": ss["batchBlocks"] / launches,
+                                    "halves_loaded": ss["batchHalves"] / launches,
                                     "voxels_rmw": ss["batchVoxelsRMW"] / launches,
                                     "voxel_op_updates": ss["batchUpdates"] / launches,
                                     "voxel_op_evaluations": ss["batchEvals"] / launches,

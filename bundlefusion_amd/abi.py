@@ -90,7 +90,7 @@ class BFTsdfStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "pixels", "candidates", "allocated", "scanned", "visible", "voxelsUpdated",
         "gcBlocks", "gcFreed", "allocOverflow", "integrateOps", "bandBlocks", "voxelsRMW",
-        "batchOps", "batchBlocks", "batchVoxelsRMW", "batchUpdates", "batchEvals")]
+        "batchOps", "batchBlocks", "batchVoxelsRMW", "batchUpdates", "batchEvals", "batchHalves")]
 
 
 class BFSceneOptions(C.Structure):
@@ -280,6 +280,12 @@ class BFAppResult(C.Structure):
                 ("end", BFEndSequenceResult), ("heapFreeCount", C.c_uint32), ("numTransforms", C.c_uint32),
                 ("numValidTransforms", C.c_uint32), ("valid", C.c_int32), ("meshTriangles", C.c_uint32),
                 ("meshVertices", C.c_uint32), ("meshFaces", C.c_uint32)]
+
+
+class BFAppTiming(C.Structure):  # include/bf/bf.h: the app's host time per section (bf_app_timing)
+    _fields_ = [("frames", C.c_uint32), ("decodeThreads", C.c_uint32)] + [
+        (n, C.c_double) for n in ("stepSeconds", "decodeWaitSeconds", "uploadSeconds", "corrSeconds", "loopSeconds",
+                                  "decodeSeconds", "uploadBytes")]
 
 
 class BFReconStats(C.Structure):

@@ -19,7 +19,7 @@ import sys
 import numpy as np
 
 from . import check, lib
-from .abi import BFAppInfo, BFAppOptions, BFAppResult
+from .abi import BFAppInfo, BFAppOptions, BFAppResult, BFAppTiming, BFReconOptions
 
 
 def _struct_dict(s):
@@ -32,6 +32,18 @@ def _struct_dict(s):
             v = list(v)
         out[k] = v
     return out
+
+
+def resolve(app_params: str, bundling_params: str, sens_file: str | None = None, max_frames: int = 0):
+    """Host only: what bf_app_create derives from the two zParameters files and the .sens header
+    (bf_app_resolve; FriedLiver.cpp:228-250) -> (BFAppInfo, BFReconOptions of the loop)."""
+    o = BFAppOptions()
+    keep = os.fsencode(sens_file) if sens_file else None
+    o.sensFile, o.maxFrames = keep, int(max_frames)
+    info, loop = BFAppInfo(), BFReconOptions()
+    check(lib().bf_app_resolve(os.fsencode(app_params), os.fsencode(bundling_params), C.byref(o), C.byref(info),
+                               C.byref(loop)))
+    return info, loop
 
 
 class FriedLiver:
@@ -114,6 +126,12 @@ class FriedLiver:
         all-reduce (bf_recon_set_comm on the app's loop); before the first step."""
         self._comm = comm
         self.recon.set_comm(comm)
+
+    def timing(self) -> dict:
+        """Host time per section of the frame loop so far (decode wait, upload + preprocessing, EntryJ, loop)."""
+        t = BFAppTiming()
+        check(lib().bf_app_timing(self.h, C.byref(t)))
+        return _struct_dict(t)
 
     def front_end_pose(self, f: int) -> np.ndarray:
         T = (C.c_float * 16)()

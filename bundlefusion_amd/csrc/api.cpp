@@ -175,6 +175,7 @@ int bf_abi_struct_size(const char* name, size_t* out) {
         {"BFAppOptions", sizeof(BFAppOptions)},
         {"BFAppInfo", sizeof(BFAppInfo)},
         {"BFAppResult", sizeof(BFAppResult)},
+        {"BFAppTiming", sizeof(BFAppTiming)},
         {"BFMcTriangle", sizeof(BFMcTriangle)},
         {"BFSynthScene", sizeof(BFSynthScene)},
         {"BFRenderStats", sizeof(BFRenderStats)}};
@@ -1016,6 +1017,23 @@ int bf_front_end_tinc(const float prev[16], const float cur[16], uint32_t frame,
     BF_REQUIRE(prev && cur && Tinc, BF_ERR_ARG, "null argument");
     const BFMat4 T = front_end_tinc(prev, cur, frame, seed, driftRad, driftM);
     std::memcpy(Tinc, T.m, 64);
+    BF_CATCH
+}
+int bf_app_resolve(const char* appParams, const char* bundlingParams, const BFAppOptions* o, BFAppInfo* info,
+                   BFReconOptions* loop) {
+    BF_TRY
+    BF_REQUIRE(appParams && bundlingParams && info, BF_ERR_ARG, "null argument");
+    BFAppOptions opt{};
+    if (o) opt = *o;
+    const AppConfig c = load_app_config(appParams, bundlingParams, opt);
+    *info = c.info;
+    if (loop) *loop = c.ro;
+    BF_CATCH
+}
+int bf_app_timing(const bf_app* a, BFAppTiming* out) {
+    BF_TRY
+    BF_REQUIRE(a && out, BF_ERR_ARG, "null argument");
+    *out = a->a->timing();
     BF_CATCH
 }
 int bf_app_front_end_pose(const bf_app* a, uint32_t f, float Tinc[16]) {

@@ -43,34 +43,37 @@ double now_s() {
 
 }  // namespace
 
-App::App(const std::string& appParams, const std::string& bundlingParams, const BFAppOptions& o) : opt_(o) {
+// The parameter half of bf_app_create (FriedLiver.cpp:228-250 + the .sens header): everything the app derives
+// from the two zParameters files and the sensor file, without touching the device (bf_app_resolve).
+AppConfig load_app_config(const std::string& appParams, const std::string& bundlingParams, const BFAppOptions& o) {
+    AppConfig c;
     ParamFile ap, bp;  // FriedLiver.cpp:228-250: two files, two name spaces
     ap.load(appParams);
     bp.load(bundlingParams);
-    sensPath_ = (o.sensFile && *o.sensFile) ? std::string(o.sensFile) : ap.str("s_binaryDumpSensorFile");
-    outDir_ = (o.outputDir && *o.outputDir) ? std::string(o.outputDir) : dir_of(sensPath_);
+    c.sensPath = (o.sensFile && *o.sensFile) ? std::string(o.sensFile) : ap.str("s_binaryDumpSensorFile");
+    c.outDir = (o.outputDir && *o.outputDir) ? std::string(o.outputDir) : dir_of(c.sensPath);
 
     // ---- SensorDataReader::createFirstConnected (SensorDataReader.cpp:38-79) ----------------------------
-    SensReader reader(sensPath_);
+    SensReader reader(c.sensPath);
     const BFSensInfo si = reader.info();
-    BF_REQUIRE(si.depthWidth >= 2 && si.depthHeight >= 2, BF_ERR_IO, "no depth stream in " + sensPath_);
+    BF_REQUIRE(si.depthWidth >= 2 && si.depthHeight >= 2, BF_ERR_IO, "no depth stream in " + c.sensPath);
     BF_REQUIRE(si.colorCompression >= 0 && si.colorCompression <= 2 && si.colorWidth >= 2 && si.colorHeight >= 2, BF_ERR_ARG,
                "the path integrates colour: raw / PNG / JPEG colour stream required");
-    S_ = (uint32_t)num(bp, "s_submapSize", 10);
-    L_ = S_ + 1;
+    c.S = (uint32_t)num(bp, "s_submapSize", 10);
+    c.L = c.S + 1;
     const uint32_t maxNumImages = (uint32_t)num(bp, "s_maxNumImages", 1200);
     uint64_t frames = si.numFrames;
     if (o.maxFrames) frames = std::min<uint64_t>(frames, o.maxFrames);
-    BF_REQUIRE(frames <= (uint64_t)maxNumImages * S_, BF_ERR_CAPACITY,
+    BF_REQUIRE(frames <= (uint64_t)maxNumImages * c.S, BF_ERR_CAPACITY,
                "sens file #frames = " + std::to_string(frames) + ", please change param file to accommodate");
     BF_REQUIRE(frames >= 1, BF_ERR_IO, "empty .sens file");
-    info_.numFrames = (uint32_t)frames;
-    info_.sensorDepthWidth = si.depthWidth;
-    info_.sensorDepthHeight = si.depthHeight;
-    info_.sensorColorWidth = si.colorWidth;
-    info_.sensorColorHeight = si.colorHeight;
-    sensPose_.resize(frames);
-    for (uint64_t f = 0; f < frames; f++) reader.pose(f, sensPose_[f].m);
+    c.info.numFrames = (uint32_t)frames;
+    c.info.sensorDepthWidth = si.depthWidth;
+    c.info.sensorDepthHeight = si.depthHeight;
+    c.info.sensorColorWidth = si.colorWidth;
+    c.info.sensorColorHeight = si.colorHeight;
+    c.sensPose.resize(frames);
+    for (uint64_t f = 0; f < frames; f++) reader.pose(f, c.sensPose[f].m);
 
     // ---- parameters ---------------------------------------------------------------------------------
     const uint32_t iw = (uint32_t)num(ap, "s_integrationWidth", 320), ih = (uint32_t)num(ap, "s_integrationHeight", 240);
@@ -84,28 +87,28 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
     cam.imageHeight = ih;
     cam.sensorDepthWorldMin = flt(ap, "s_renderDepthMin", 0.1f);
     cam.sensorDepthWorldMax = flt(ap, "s_renderDepthMax", 4.0f);
-    info_.integrationCamera = cam;
-    info_.hashParams = hash_params_from(ap);
-    info_.preprocess = preprocess_options_from(bp, si.depthShift);
-    mcThreshFactor_ = flt(ap, "s_SDFMarchingCubeThreshFactor", 10.0f);
-    mcMaxTriangles_ = (uint32_t)num(ap, "s_marchingCubesMaxNumTriangles", 3000000);
-    info_.numSolveFramesBeforeExit = o.numSolveFramesBeforeExit ? o.numSolveFramesBeforeExit
+    c.info.integrationCamera = cam;
+    c.info.hashParams = hash_params_from(ap);
+    c.info.preprocess = preprocess_options_from(bp, si.depthShift);
+    c.mcThreshFactor = flt(ap, "s_SDFMarchingCubeThreshFactor", 10.0f);
+    c.mcMaxTriangles = (uint32_t)num(ap, "s_marchingCubesMaxNumTriangles", 3000000);
+    c.info.numSolveFramesBeforeExit = o.numSolveFramesBeforeExit ? o.numSolveFramesBeforeExit
                                                                : (int32_t)num(ap, "s_numSolveFramesBeforeExit", 30);
 
     // CUDACache (Bundler.cpp:33-38): sensor-size depth input, s_downsampledWidth x Height
-    BFCacheOptions& co = info_.cache;
+    BFCacheOptions& co = c.info.cache;
     co.inputWidth = si.depthWidth;
     co.inputHeight = si.depthHeight;
     co.width = (uint32_t)num(bp, "s_downsampledWidth", 80);
     co.height = (uint32_t)num(bp, "s_downsampledHeight", 60);
-    co.maxFrames = info_.numFrames;
+    co.maxFrames = c.info.numFrames;
     std::memcpy(co.inputIntrinsics, si.depthIntrinsic, 64);
     co.colorSigma = flt(bp, "s_colorDownSigma", 2.5f);
     co.depthSigmaD = flt(bp, "s_depthDownSigmaD", 1.0f);
     co.depthSigmaR = flt(bp, "s_depthDownSigmaR", 0.05f);
 
     // the EntryJ producer (AddCurrToResidualsCU's siftIntrinsicsInv at the sensor depth size)
-    BFCorrOptions& cr = info_.corr;
+    BFCorrOptions& cr = c.info.corr;
     cr.intrinsics[0] = K[0];
     cr.intrinsics[1] = K[5];
     cr.intrinsics[2] = K[2];
@@ -122,56 +125,80 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
     cr.maxDepth = flt(ap, "s_SDFMaxIntegrationDistance", 3.0f);
     cr.depthThresh = o.corrDepthThresh > 0.0f ? o.corrDepthThresh : 0.02f;
 
-    const uint32_t numSubmaps = (info_.numFrames + S_ - 1) / S_;
-    info_.submapSize = S_;
-    info_.maxKeyframes = numSubmaps + 1;
-    info_.maxLocalCorr = cr.maxPerPair * L_ * (L_ - 1) / 2;
-    const uint64_t Kf = info_.maxKeyframes;
-    info_.maxGlobalCorr = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1000, cr.maxPerPair * Kf * (Kf - 1) / 2), 0xFFFFFFFFull);
+    const uint32_t numSubmaps = (c.info.numFrames + c.S - 1) / c.S;
+    c.info.submapSize = c.S;
+    c.info.maxKeyframes = numSubmaps + 1;
+    c.info.maxLocalCorr = cr.maxPerPair * c.L * (c.L - 1) / 2;
+    const uint64_t Kf = c.info.maxKeyframes;
+    c.info.maxGlobalCorr = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1000, cr.maxPerPair * Kf * (Kf - 1) / 2), 0xFFFFFFFFull);
 
-    BFReconOptions ro{};
-    ro.maxFrames = info_.numFrames;
-    ro.submapSize = S_;
-    ro.maxFrameFixes = (uint32_t)num(ap, "s_maxFrameFixes", 10);
-    ro.topNActive = (uint32_t)num(ap, "s_topNActive", 30);
-    ro.minPoseDistSqrt = flt(ap, "s_minPoseDistSqrt", 0.0f);
-    ro.localNonLin = (uint32_t)num(bp, "s_numLocalNonLinIterations", 2);
-    ro.localLin = (uint32_t)num(bp, "s_numLocalLinIterations", 100);
-    ro.globalNonLin = (uint32_t)num(bp, "s_numGlobalNonLinIterations", 3);
-    ro.globalLin = (uint32_t)num(bp, "s_numGlobalLinIterations", 150);
-    ro.maxKeyframes = info_.maxKeyframes;
-    ro.maxLocalCorr = info_.maxLocalCorr;
-    ro.maxGlobalCorr = info_.maxGlobalCorr;
-    ro.maxResidualThresh = flt(bp, "s_optMaxResThresh", 0.08f);
-    ro.useLocalDense = flag(bp, "s_useLocalDense", true) ? 1 : 0;
-    ro.cacheWidth = co.width;
-    ro.cacheHeight = co.height;
+    c.ro.maxFrames = c.info.numFrames;
+    c.ro.submapSize = c.S;
+    c.ro.maxFrameFixes = (uint32_t)num(ap, "s_maxFrameFixes", 10);
+    c.ro.topNActive = (uint32_t)num(ap, "s_topNActive", 30);
+    c.ro.minPoseDistSqrt = flt(ap, "s_minPoseDistSqrt", 0.0f);
+    c.ro.localNonLin = (uint32_t)num(bp, "s_numLocalNonLinIterations", 2);
+    c.ro.localLin = (uint32_t)num(bp, "s_numLocalLinIterations", 100);
+    c.ro.globalNonLin = (uint32_t)num(bp, "s_numGlobalNonLinIterations", 3);
+    c.ro.globalLin = (uint32_t)num(bp, "s_numGlobalLinIterations", 150);
+    c.ro.maxKeyframes = c.info.maxKeyframes;
+    c.ro.maxLocalCorr = c.info.maxLocalCorr;
+    c.ro.maxGlobalCorr = c.info.maxGlobalCorr;
+    c.ro.maxResidualThresh = flt(bp, "s_optMaxResThresh", 0.08f);
+    c.ro.useLocalDense = flag(bp, "s_useLocalDense", true) ? 1 : 0;
+    c.ro.cacheWidth = co.width;
+    c.ro.cacheHeight = co.height;
     // CUDACache::m_intrinsics: the input intrinsics scaled to the cache size (CUDACache.cpp:14-21)
-    info_.cacheIntrinsics[0] = K[0] * ((float)co.width / (float)co.inputWidth);
-    info_.cacheIntrinsics[1] = K[5] * ((float)co.height / (float)co.inputHeight);
-    info_.cacheIntrinsics[2] = K[2] * ((float)(co.width - 1) / (float)(co.inputWidth - 1));
-    info_.cacheIntrinsics[3] = K[6] * ((float)(co.height - 1) / (float)(co.inputHeight - 1));
-    std::memcpy(ro.cacheIntrinsics, info_.cacheIntrinsics, 16);
-    ro.enableTiming = o.enableTiming;
-    ro.recordOps = o.recordOps;
-    ro.asyncBundling = o.asyncBundling;
-    ro.resultLag = o.resultLag;
-    ro.solver.denseDistThresh = flt(bp, "s_denseDistThresh", 0.15f);
-    ro.solver.denseNormalThresh = flt(bp, "s_denseNormalThresh", 0.97f);
-    ro.solver.denseColorThresh = flt(bp, "s_denseColorThresh", 0.1f);
-    ro.solver.denseColorGradientMin = flt(bp, "s_denseColorGradientMin", 0.005f);
-    ro.solver.denseDepthMin = flt(bp, "s_denseDepthMin", 0.5f);
-    ro.solver.denseDepthMax = flt(bp, "s_denseDepthMax", 4.0f);
-    ro.solver.denseOverlapSubsample = (uint32_t)num(bp, "s_denseOverlapCheckSubsampleFactor", 4);
-    ro.disableLocalVerify = flag(bp, "s_useLocalVerify", true) ? 0 : 1;
-    ro.verify.projCorrDistThresh = flt(bp, "s_projCorrDistThres", 0.15f);
-    ro.verify.projCorrNormalThresh = flt(bp, "s_projCorrNormalThres", 0.97f);
-    ro.verify.verifyOptErrThresh = flt(bp, "s_verifyOptErrThresh", 0.05f);
-    ro.verify.verifyOptCorrThresh = flt(bp, "s_verifyOptCorrThresh", 0.001f);
+    c.info.cacheIntrinsics[0] = K[0] * ((float)co.width / (float)co.inputWidth);
+    c.info.cacheIntrinsics[1] = K[5] * ((float)co.height / (float)co.inputHeight);
+    c.info.cacheIntrinsics[2] = K[2] * ((float)(co.width - 1) / (float)(co.inputWidth - 1));
+    c.info.cacheIntrinsics[3] = K[6] * ((float)(co.height - 1) / (float)(co.inputHeight - 1));
+    std::memcpy(c.ro.cacheIntrinsics, c.info.cacheIntrinsics, 16);
+    c.ro.enableTiming = o.enableTiming;
+    c.ro.recordOps = o.recordOps;
+    c.ro.asyncBundling = o.asyncBundling;
+    c.ro.resultLag = o.resultLag;
+    c.ro.solver.denseDistThresh = flt(bp, "s_denseDistThresh", 0.15f);
+    c.ro.solver.denseNormalThresh = flt(bp, "s_denseNormalThresh", 0.97f);
+    c.ro.solver.denseColorThresh = flt(bp, "s_denseColorThresh", 0.1f);
+    c.ro.solver.denseColorGradientMin = flt(bp, "s_denseColorGradientMin", 0.005f);
+    c.ro.solver.denseDepthMin = flt(bp, "s_denseDepthMin", 0.5f);
+    c.ro.solver.denseDepthMax = flt(bp, "s_denseDepthMax", 4.0f);
+    c.ro.solver.denseOverlapSubsample = (uint32_t)num(bp, "s_denseOverlapCheckSubsampleFactor", 4);
+    c.ro.disableLocalVerify = flag(bp, "s_useLocalVerify", true) ? 0 : 1;
+    c.ro.verify.projCorrDistThresh = flt(bp, "s_projCorrDistThres", 0.15f);
+    c.ro.verify.projCorrNormalThresh = flt(bp, "s_projCorrNormalThres", 0.97f);
+    c.ro.verify.verifyOptErrThresh = flt(bp, "s_verifyOptErrThresh", 0.05f);
+    c.ro.verify.verifyOptCorrThresh = flt(bp, "s_verifyOptCorrThresh", 0.001f);
     // the matcher's s_minNumMatchesLocal / Global filter on a pair (5)
     const uint32_t minLocal = (uint32_t)num(bp, "s_minNumMatchesLocal", 5), minGlobal = (uint32_t)num(bp, "s_minNumMatchesGlobal", 5);
     cr.minPerPair = minGlobal;
-    localMinPerPair_ = minLocal;
+    c.localMinPerPair = minLocal;
+
+    return c;
+}
+
+App::App(const std::string& appParams, const std::string& bundlingParams, const BFAppOptions& o) : opt_(o) {
+    AppConfig c = load_app_config(appParams, bundlingParams, o);
+    info_ = c.info;
+    sensPath_ = c.sensPath;
+    outDir_ = c.outDir;
+    sensPose_ = std::move(c.sensPose);
+    S_ = c.S;
+    L_ = c.L;
+    mcThreshFactor_ = c.mcThreshFactor;
+    mcMaxTriangles_ = c.mcMaxTriangles;
+    localMinPerPair_ = c.localMinPerPair;
+    BFReconOptions ro = c.ro;
+    const BFCacheOptions& co = info_.cache;
+    const uint32_t iw = info_.integrationCamera.imageWidth, ih = info_.integrationCamera.imageHeight;
+    const BFDepthCameraParams cam = info_.integrationCamera;
+    const uint32_t numSubmaps = (info_.numFrames + S_ - 1) / S_;
+    BFSensInfo si{};
+    si.depthWidth = info_.sensorDepthWidth;
+    si.depthHeight = info_.sensorDepthHeight;
+    si.colorWidth = info_.sensorColorWidth;
+    si.colorHeight = info_.sensorColorHeight;
 
     // ---- front end (frontend.h) ----------------------------------------------------------------------
     const float dr = o.noFrontEndDrift ? 0.0f : (o.frontEndDriftRad > 0.0f ? o.frontEndDriftRad : 0.05f * 3.14159265f / 180.0f);
@@ -273,6 +300,7 @@ void App::decodeLoop(uint32_t w) {
             s.ready = false;
         }
         std::string e = err;
+        const double t0 = now_s();
         if (e.empty()) {
             try {
                 r->depthU16(f, s.depth);
@@ -281,8 +309,10 @@ void App::decodeLoop(uint32_t w) {
                 e = ex.what();
             }
         }
+        const double dt = now_s() - t0;
         {
             std::lock_guard<std::mutex> lk(mu_);
+            decodeSeconds_ += dt;
             s.error = e;
             s.ready = true;
         }
@@ -307,6 +337,16 @@ void App::releaseFrame(uint32_t f) {
         s.expect += numSlots_;
     }
     cv_.notify_all();
+}
+
+BFAppTiming App::timing() const {
+    BFAppTiming t = tm_;
+    t.decodeThreads = numWorkers_;
+    {
+        std::lock_guard<std::mutex> lk(const_cast<std::mutex&>(mu_));
+        t.decodeSeconds = decodeSeconds_;
+    }
+    return t;
 }
 
 BFMat4 App::frontEndPose(uint32_t f) const {
@@ -368,6 +408,8 @@ bool App::step() {
     const size_t dp = (size_t)info_.sensorDepthWidth * info_.sensorDepthHeight;
     // ---- CUDAImageManager::process ---------------------------------------------------------------------
     Slot& sl = waitFrame(f);
+    const double t1 = now_s();
+    tm_.decodeWaitSeconds += t1 - t0;
     BF_HIP(hipMemcpyAsync(dDepthU16_.p, sl.depth, dp * 2, hipMemcpyHostToDevice, pre_));
     BF_HIP(hipMemcpyAsync(dRgbx_.p, sl.rgbx, dRgbx_.n, hipMemcpyHostToDevice, pre_));
     float* depth = frameDepth_.p + ip * f;
@@ -379,6 +421,9 @@ bool App::step() {
         BF_HIP(hipMemcpyAsync(kfDepth_.p + dp * (f / S_), preproc_->filteredDepth(), dp * 4, hipMemcpyDeviceToDevice, pre_));
     BF_HIP(hipStreamSynchronize(pre_));
     releaseFrame(f);  // the pinned slot has been copied
+    const double t2 = now_s();
+    tm_.uploadSeconds += t2 - t1;
+    tm_.uploadBytes += (double)(dp * 2 + dRgbx_.n);
     // ---- processInput: cache source (stored by the loop on this stream), correspondences ------------
     recon_->setFrame(f, depth, color, nullptr, tinc_[f]);
     recon_->setFrameSource(f, preproc_->rawDepth(), dRgbx_.p, info_.sensorColorWidth, info_.sensorColorHeight);
@@ -387,10 +432,16 @@ bool App::step() {
         localCorrespondences(s, L_);
         keyframeCorrespondences(s);
     }
+    const double t3 = now_s();
+    tm_.corrSeconds += t3 - t2;
     // ---- OnD3D11FrameRender: reintegrate + integrate (+ the submap's solves) -----------------------------
     recon_->processFrame(f);
     next_++;
-    loopSeconds_ += now_s() - t0;
+    const double t4 = now_s();
+    tm_.loopSeconds += t4 - t3;
+    tm_.stepSeconds += t4 - t0;
+    tm_.frames++;
+    loopSeconds_ += t4 - t0;
     return true;
 }
 

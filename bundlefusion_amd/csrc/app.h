@@ -21,6 +21,19 @@
 
 namespace bf {
 
+// What bf_app_create derives from the two parameter files and the .sens header (host only)
+struct AppConfig {
+    BFAppInfo info{};
+    BFReconOptions ro{};
+    std::string sensPath, outDir;
+    float mcThreshFactor = 10.0f;
+    uint32_t mcMaxTriangles = 3000000;
+    uint32_t S = 10, L = 11;
+    uint32_t localMinPerPair = 5;
+    std::vector<BFMat4> sensPose;  // the .sens trajectory
+};
+AppConfig load_app_config(const std::string& appParams, const std::string& bundlingParams, const BFAppOptions& o);
+
 class App {
 public:
     App(const std::string& appParams, const std::string& bundlingParams, const BFAppOptions& o);
@@ -31,6 +44,7 @@ public:
     Recon& recon() { return *recon_; }
     const BFAppInfo& info() const { return info_; }
     BFMat4 frontEndPose(uint32_t f) const;
+    BFAppTiming timing() const;
 
 private:
     struct Slot {  // one decoded frame (pinned host memory)
@@ -86,6 +100,8 @@ private:
     uint32_t next_ = 0;                 // next input frame
     bool finished_ = false;
     double loopSeconds_ = 0.0;
+    BFAppTiming tm_{};                  // host time per section (bf_app_timing)
+    double decodeSeconds_ = 0.0;        // summed over the workers (under mu_)
 };
 
 }  // namespace bf

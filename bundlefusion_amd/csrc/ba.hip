@@ -1671,6 +1671,8 @@ __device__ void pcg_persist_finisher(const BA& a, float* sh, float* sM, int useD
 // pcg_finish_regs<8>, so the result equals the per-launch solve's bit for bit). Workgroup 0 sets the
 // flag (p halves carry their iteration's tag; workers re-gather a stale one) and the control words.
 constexpr int PP_NF = FIN_GROUPS;
+// the rows the wide finishers own, 1 .. 2 PP_NF WG: the host's wide-route bound on numImages (Solver::solve)
+static_assert(2 * PP_NF * WG + 1 == 2049, "wide persistent finishers cover rows 1..2048");
 constexpr int SH_FX = 64;  // the finisher's LDS slots of the exchanged totals
 __device__ __forceinline__ float fx_exchange(const BA& a, float* sh, int kind, uint32_t g, float S, uint32_t tag,
                                              unsigned long long t0, bool& ok) {
@@ -3095,7 +3097,9 @@ void Solver::solve(const SolveArgs& s) {
                 unsigned persistGrid = nF + nW;
                 if (persistGrid > PP_SHADOW) persistGrid += nF;  // the row-less workgroups on the finishers' CUs
                 const bool small = smallN && persistGrid * 2u <= persistCapacity_;
-                const bool wide = !smallN && !dense && persistGrid <= persistCapacity_;
+                // the PP_NF finishers own rows 1 .. 2 * PP_NF * WG: beyond that no finisher would tag a row's p
+                const bool wide = !smallN && !dense && s.numImages <= 2u * (unsigned)PP_NF * WG + 1u &&
+                                  persistGrid <= persistCapacity_;
                 if (BF_PCG_PERSISTENT && cfg_.pcgLaunch == 0 && s.nLin < 255u && s.numImages >= 2u && (small || wide)) {
 #ifdef BF_PCG_TIMING
                     {
@@ -3108,7 +3112,9 @@ void Solver::solve(const SolveArgs& s) {
                         // partly resident persistent grids could each wait on the other's workgroups
                         PersistGate& pg = persist_gate();
                         std::lock_guard<std::mutex> lk(pg.mu);
-                        if (pg.ev && pg.stream != stream_) BF_HIP(hipStreamWaitEvent(stream_, pg.ev, 0));
+                        // always wait, on the same stream too: a destroyed solver's stream handle may be
+                        // reused by a new solver whose launch must still follow the old one (cheap in order)
+                        if (pg.ev) BF_HIP(hipStreamWaitEvent(stream_, pg.ev, 0));
                         if (small) k_pcg_persist<2><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
                         else k_pcg_persist<2, PP_NF><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
                         if (!pg.ev) BF_HIP(hipEventCreateWithFlags(&pg.ev, hipEventDisableTiming));

@@ -25,6 +25,8 @@ public:
     hipStream_t stream() const { return stream_; }
     uint32_t integrationWidth() const { return iw_; }
     uint32_t integrationHeight() const { return ih_; }
+    uint32_t depthWidth() const { return dw_; }
+    uint32_t depthHeight() const { return dh_; }
     uint32_t colorWidth() const { return cw_; }
     uint32_t colorHeight() const { return ch_; }
     // the sensor-size images of the last run that CUDAImageManager::copyToBundling hands the bundler

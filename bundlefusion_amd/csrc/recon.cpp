@@ -86,6 +86,9 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     opt_.cacheHeight = or_default(o.cacheHeight, 60u);
     BF_REQUIRE(opt_.maxFrames > 0, BF_ERR_ARG, "maxFrames");
     const uint32_t S = opt_.submapSize;
+    // a full result ring (RING submaps in flight) hands the oldest result over early, so a lag beyond
+    // RING submaps could not be kept exactly
+    BF_REQUIRE(opt_.resultLag <= RING * S, BF_ERR_ARG, "resultLag exceeds the result ring (8 submaps)");
     const uint32_t maxSubmaps = (opt_.maxFrames + S - 1) / S;
     opt_.maxKeyframes = std::max(or_default(o.maxKeyframes, maxSubmaps + 1), 2u);
     opt_.maxLocalCorr = or_default(o.maxLocalCorr, (S + 1) * S / 2 * 25u);
@@ -950,6 +953,8 @@ void Recon::attachCache(Cache* c) {
     BF_REQUIRE(numFrames_ == 0, BF_ERR_STATE, "attach the cache before the first frame");
     BF_REQUIRE(!c || c->config().width == opt_.cacheWidth && c->config().height == opt_.cacheHeight, BF_ERR_ARG,
                "cache size differs from the loop's cacheWidth x cacheHeight");
+    BF_REQUIRE(!c || !preproc_ || (preproc_->depthWidth() == c->config().inputWidth && preproc_->depthHeight() == c->config().inputHeight),
+               BF_ERR_ARG, "the cache's input size differs from the attached preprocessing's sensor depth size");
     cache_ = c;
     for (hipEvent_t& e : cacheEvF_)
         if (c && !e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -968,6 +973,9 @@ void Recon::attachPreproc(Preproc* p) {
     BF_REQUIRE(numFrames_ == 0, BF_ERR_STATE, "attach the preprocessing before the first frame");
     BF_REQUIRE(!p || (p->integrationWidth() == cam_.imageWidth && p->integrationHeight() == cam_.imageHeight), BF_ERR_ARG,
                "preprocessing output size differs from the integration size");
+    // the cache reads the preprocessing's sensor-size raw depth (k_cache_geometry: inputWidth x inputHeight)
+    BF_REQUIRE(!p || !cache_ || (p->depthWidth() == cache_->config().inputWidth && p->depthHeight() == cache_->config().inputHeight),
+               BF_ERR_ARG, "the attached cache's input size differs from the preprocessing's sensor depth size");
     preproc_ = p;
     for (hipEvent_t& e : preEv_)
         if (p && !e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -92,7 +92,7 @@ struct __attribute__((packed, aligned(4))) Vox3 {
 };
 
 enum StatField { S_PIXELS = 0, S_CAND, S_ALLOC, S_SCANNED, S_VISIBLE, S_VOXELS, S_GCBLOCKS, S_GCFREED, S_OVERFLOW, S_OPS,
-                 S_BAND, S_RMW, S_BOPS, S_BBLOCKS, S_BRMW, S_BUPD, S_BEVAL };
+                 S_BAND, S_RMW, S_BOPS, S_BBLOCKS, S_BRMW, S_BUPD, S_BEVAL, S_BHALF };
 constexpr int DEPTH_TILE = 8;    // 8x8-pixel depth-bound tiles for the band cull
 constexpr int DEPTH_TILE2 = 16;  // coarse level: 16x16 pixels
 constexpr int STAT_SLOTS = 64;
@@ -1580,8 +1580,10 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
 // z-round-outer order re-fetched every op's footprint once per round: 888 -> 856 us per launch at the
 // bench workload); the op's pose and the (x, y) part of its projection are taken once per ZR slices.
 // ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us).
-// The kernel is VALU-issue bound (~95% of the VALU issue rate at the bench workload): lane-derived
-// values are re-read per block instead of kept live (no spills), counters are scalar.
+// The kernel sits at neither roof: 0.42 of the VALU issue peak and 0.34 of HBM by the counters at the bench
+// workload, with the waves' cycles 25 % issuing, 44 % waiting to issue (dependencies) and 31 % waiting on
+// memory (profiles/r9g_apply_sq_pmc.txt): it is dependency / latency bound. Lane-derived values are re-read
+// per block instead of kept live (no spills), counters are scalar.
 template <int ZR, int ZC, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap) {
@@ -1589,7 +1591,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
-    uint32_t updated = 0, rmw = 0;  // per wave and launch: < 2^32
+    uint32_t updated = 0, rmw = 0, halves = 0;  // per wave and launch: < 2^32
 #ifdef BF_APPLY_DIAG
     uint32_t diag[6] = {0, 0, 0, 0, 0, 0}, diagPairs = 0, diagEmpty = 0;
 #endif
@@ -1617,6 +1619,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         uint32_t nupd = 0, nrmw = 0, nwav = 0;
 #pragma unroll
         for (int h = 0; h < BF_SDF_BLOCK_SIZE; h += ZR) {
+            // a half no op reaches is neither read nor written (wave-uniform branch on an SGPR mask)
+            if (maskH[h / ZR] == 0u) continue;
+            halves++;
             RegVox rv[ZR];
             uint32_t pos0 = 0;
 #pragma unroll
@@ -1685,6 +1690,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);
     __syncthreads();
     flush_stats2(A.stats, S_BUPD, lane_id_here() == 0 ? updated : 0u, S_BRMW, rmw);
+    __syncthreads();
+    flush_stats2(A.stats, S_BHALF, lane_id_here() == 0 ? halves : 0u, -1, 0);
 #ifdef BF_APPLY_DIAG
     __syncthreads();
     flush_stats2(A.stats, 20, diag[0], 21, diag[1]);
@@ -2160,7 +2167,7 @@ BFTsdfStats Scene::stats() {
     for (int sl = 0; sl < STAT_SLOTS; sl++)
         for (int f = 0; f < STAT_FIELDS; f++) sum[f] += h[sl * STAT_FIELDS + f];
     BFTsdfStats s;
-    static_assert(sizeof(BFTsdfStats) == 17 * 8 && sizeof(BFTsdfStats) <= STAT_FIELDS * 8, "stats layout");
+    static_assert(sizeof(BFTsdfStats) == 18 * 8 && sizeof(BFTsdfStats) <= STAT_FIELDS * 8, "stats layout");
     std::memcpy(&s, sum, sizeof(s));
     s.pixels += hostPixels_;
 #ifdef BF_APPLY_DIAG

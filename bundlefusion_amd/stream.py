@@ -155,13 +155,18 @@ class SyntheticStream:
 
 
 def write_synthetic_sens(path: str, num_frames: int, width: int = 640, height: int = 480, seed: int = 0,
-                         color_codec: str = "jpeg", jpeg_quality: int = 90, device: bool = True, log=None):
+                         color_codec: str = "jpeg", jpeg_quality: int = 90, device: bool = True, log=None,
+                         threads: int = 8):
     """A `.sens` of the seeded synthetic room (SURVEY.md §8(d) inputs) in the copyroom / apt0 layout: JPEG
     (or PNG / raw) colour, zlib ushort depth in millimetres, the ground-truth camera trajectory, the depth
     camera's intrinsics. Frames are rendered on the GPU (device=True) or with the host renderer, and the
-    colour is compressed with PIL (the image library mLib's SensorData uses for its colour streams)."""
+    colour is compressed with PIL (the image library mLib's SensorData uses for its colour streams). The
+    compression of a frame runs on a thread pool (PIL and zlib release the GIL) while the next ones render;
+    frames are written in order, so the file does not depend on `threads`."""
     import io as _io
     import zlib
+    from collections import deque
+    from concurrent.futures import ThreadPoolExecutor
 
     from .io import SensWriter, sens_info
     f = 577.87 * width / 640.0
@@ -175,8 +180,30 @@ def write_synthetic_sens(path: str, num_frames: int, width: int = 640, height: i
     if device:
         dd = DeviceArray((height, width), np.float32)
         dc = DeviceArray((height, width, 4), np.uint8)
+
+    def compress(d, c):
+        # the renderer quantises to 1 mm (the .sens convention, SensorDataReader.cpp:104-107)
+        du = np.where(np.isfinite(d) & (d > 0), np.rint(d * 1000.0), 0).astype(np.uint16)
+        rgb = np.ascontiguousarray(c[..., :3])
+        if cc == 0:
+            col = rgb.tobytes()
+        else:
+            b = _io.BytesIO()
+            Image.fromarray(rgb).save(b, "JPEG", quality=jpeg_quality) if cc == 2 else Image.fromarray(rgb).save(b, "PNG")
+            col = b.getvalue()
+        return col, zlib.compress(du.tobytes(), 1)
+
     t0 = time.perf_counter()
-    with SensWriter(path, sens_info((width, height), (width, height), K, color_compression=cc)) as w:
+    last = t0
+    pending = deque()
+    with SensWriter(path, sens_info((width, height), (width, height), K, color_compression=cc)) as w, \
+            ThreadPoolExecutor(max(1, threads)) as pool:
+        def drain(limit):
+            while len(pending) > limit:
+                i, T, fut = pending.popleft()
+                col, dep = fut.result()
+                w.add_compressed_frame(T, col, dep, ts=(i, i))
+
         for i in range(num_frames):
             T = synth_pose(i)
             if device:
@@ -186,16 +213,12 @@ def write_synthetic_sens(path: str, num_frames: int, width: int = 640, height: i
             else:
                 from . import synth_render_host
                 d, c = synth_render_host(scene, T, cam, 1, i)
-            # the renderer quantises to 1 mm (the .sens convention, SensorDataReader.cpp:104-107)
-            du = np.where(np.isfinite(d) & (d > 0), np.rint(d * 1000.0), 0).astype(np.uint16)
-            rgb = np.ascontiguousarray(c[..., :3])
-            if cc == 0:
-                col = rgb.tobytes()
-            else:
-                b = _io.BytesIO()
-                Image.fromarray(rgb).save(b, "JPEG", quality=jpeg_quality) if cc == 2 else Image.fromarray(rgb).save(b, "PNG")
-                col = b.getvalue()
-            w.add_compressed_frame(T, col, zlib.compress(du.tobytes(), 1), ts=(i, i))
+            pending.append((i, T, pool.submit(compress, d, c)))
+            drain(4 * max(1, threads))
+            if log and time.perf_counter() - last > 20.0:
+                log(f"  .sens frame {i}")
+                last = time.perf_counter()
+        drain(0)
     if log:
         log(f"wrote {num_frames} frames {width}x{height} ({color_codec}) to {path} in {time.perf_counter() - t0:.1f}s")
     return cam

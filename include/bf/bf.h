@@ -314,7 +314,8 @@ typedef struct BFReconOptions {
     uint32_t resultLag;          /* asyncBundling 1/2: 0 = a submap's poses are applied by the first frame that
                                     finds its solves done (timing-dependent, like the reference's threads);
                                     L > 0 = they are applied exactly L frames after the submap was issued
-                                    (waiting for them if needed), so the run's op sequence is repeatable */
+                                    (waiting for them if needed), so the run's op sequence is repeatable;
+                                    L <= 8 * submapSize (the result ring), else BF_ERR_ARG */
 } BFReconOptions;
 
 typedef struct BFReconStats {
@@ -684,8 +685,25 @@ typedef struct BFAppResult {
     int32_t valid;              /* processed.txt's verdict: heap free >= 800 and >= half the transforms valid */
     uint32_t meshTriangles, meshVertices, meshFaces;
 } BFAppResult;
+/* where the app's frame loop spends its host time (bf_app_timing; cumulative over the steps so far) */
+typedef struct BFAppTiming {
+    uint32_t frames;            /* steps that processed a frame */
+    uint32_t decodeThreads;     /* decode workers */
+    double stepSeconds;         /* wall time inside bf_app_step */
+    double decodeWaitSeconds;   /* ... blocked waiting for the decode workers */
+    double uploadSeconds;       /* ... issuing the H2D copies + preprocessing and waiting for the copies */
+    double corrSeconds;         /* ... producing EntryJ (the SiftGPU stand-in) at submap boundaries */
+    double loopSeconds;         /* ... in the loop's processFrame (re-integration, integrate, solves) */
+    double decodeSeconds;       /* decode work summed over the workers (read + zlib + JPEG/PNG) */
+    double uploadBytes;         /* bytes copied host -> device for the input frames */
+} BFAppTiming;
 int bf_app_create(const char* appParams, const char* bundlingParams, const BFAppOptions* o, bf_app** out);
 int bf_app_destroy(bf_app* a);
+/* Host only (no device): the parameters bf_app_create derives from the two zParameters files and the .sens
+ * header (FriedLiver.cpp:228-250, GlobalAppState / GlobalBundlingState), and the loop options it hands the
+ * loop; the same checks and errors as bf_app_create's parameter stage. loop may be NULL. */
+int bf_app_resolve(const char* appParams, const char* bundlingParams, const BFAppOptions* o, BFAppInfo* info,
+                   BFReconOptions* loop);
 int bf_app_info(const bf_app* a, BFAppInfo* out);
 /* one input frame through the loop; *gotFrame = 0 once the input has ended (nothing done) */
 int bf_app_step(bf_app* a, int* gotFrame);
@@ -695,6 +713,7 @@ int bf_app_finish(bf_app* a, BFAppResult* out);
 int bf_app_run(bf_app* a, BFAppResult* out);
 /* the app's loop (borrowed: do not destroy) for the bf_recon_* queries (op log, submap poses, trajectory) */
 int bf_app_recon(bf_app* a, bf_recon** out);
+int bf_app_timing(const bf_app* a, BFAppTiming* out);
 /* The stand-in front end's frame-to-frame estimate (computeSiftTransformCU's role, OnlineBundler.cu:6-71;
  * bundlefusion_amd/csrc/frontend.h): inv(prev) * cur * a seeded error step (rotation sigma driftRad, translation
  * sigma driftM; both 0: the exact relative motion), identity when a pose is not finite. Host only. */

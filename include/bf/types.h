@@ -186,6 +186,7 @@ typedef struct BFTsdfStats {
     uint64_t batchVoxelsRMW;  /* voxels read + written once by a batch pass */
     uint64_t batchUpdates;    /* voxel-op updates inside the truncation band applied by batch passes */
     uint64_t batchEvals;      /* voxel-op evaluations (projection + band test) of the batch passes */
+    uint64_t batchHalves;     /* block z-halves (256 voxels) a batch pass loaded: those some op's mask reaches */
 } BFTsdfStats;
 
 /* mLib SensorData v4 header (SensorDataReader.cpp:45-60 reads these fields) */

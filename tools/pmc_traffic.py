@@ -44,12 +44,14 @@ def main():
            "correction": "FETCH_SIZE x2 (gfx950 half-count on 128-B requests), KB -> bytes"}
     if bench:
         res["workload"] = bench["config"]["workload"]
+        res["pass_rev"] = bench["roofline"].get("pass_rev")
         res["averaged_over"] = f"last {last} dispatches (the bench's timed region)"
         # per-unit rates (bench.py scales them by its own run's counts): fetched bytes per voxel-op
         # evaluation (the gathers and the voxel reads both grow with it), written bytes per voxel
         # read + written, VALU wave-instructions per evaluation
         pl = bench["roofline"]["per_launch"]
         res["units_per_launch"] = {"voxel_op_evaluations": pl["voxel_op_evaluations"], "voxels_rmw": pl["voxels_rmw"],
+                                   "halves_loaded": pl.get("halves_loaded"),
                                    "work_list_blocks": pl["work_list_blocks"], "ops": pl["ops"]}
         res["fetch_bytes_per_evaluation"] = fetch_b / max(1.0, pl["voxel_op_evaluations"])
         res["write_bytes_per_voxel_rmw"] = write_b / max(1.0, pl["voxels_rmw"])
