@@ -281,12 +281,15 @@ def global_solve_timing(stream, K, reps=3):
     L = bfa.lib()
     timer = C.c_void_p()
     bfa.check(L.bf_timer_create(C.byref(timer)))
+    pcg_ms, pcg_n = C.c_double(), C.c_uint64()
     ms_tot, gn_tot, pcg_tot = 0.0, 0, 0
     for r in range(reps + 1):
         corr.upload(stream.global_host[:n])
         S.matrices_to_poses(dT, K, dr, dt, dv)
         S.synchronize()
         ms = C.c_float()
+        if r == 1 and hasattr(L, "bf_solver_pcg_time"):  # the persistent PCG launches' own device time
+            bfa.check(L.bf_solver_pcg_time(S.h, 1, None, None))
         bfa.check(L.bf_solver_timer_start(S.h, timer))
         S.solve(corr, n, dv, K, 3, 150, [1.0, 1.0, 1.0], rot=dr, trans=dt)
         bfa.check(L.bf_solver_timer_stop(S.h, timer, C.byref(ms)))
@@ -295,13 +298,16 @@ def global_solve_timing(stream, K, reps=3):
             ms_tot += ms.value
             gn_tot += res["gnIterations"]
             pcg_tot += res["pcgIterations"]
+    if hasattr(L, "bf_solver_pcg_time"):
+        bfa.check(L.bf_solver_pcg_time(S.h, 0, C.byref(pcg_ms), C.byref(pcg_n)))
     bfa.check(L.bf_timer_destroy(timer))
     S.close()
     g = stream.global_host[:n]
     ok = (g["i"] < K) & (g["j"] < K)
     pairs = int(np.unique(np.minimum(g["i"][ok], g["j"][ok]).astype(np.int64) * K + np.maximum(g["i"][ok], g["j"][ok])).size)
     return {"ms_per_gn_iter": ms_tot / max(1, gn_tot), "keyframes": K, "correspondences": n, "image_pairs": pairs,
-            "gn_iters": gn_tot / reps, "pcg_iters": pcg_tot / reps, "ms_per_solve": ms_tot / reps}
+            "gn_iters": gn_tot / reps, "pcg_iters": pcg_tot / reps, "ms_per_solve": ms_tot / reps,
+            "pcg_kernel_us_per_iter": pcg_ms.value * 1e3 / max(1, pcg_tot) if pcg_n.value else None}
 
 
 def roofline_ba(solo):
@@ -669,7 +675,13 @@ def main():
                    "fill_global_gn_iters": fill_stats["globalGnIterations"],
                    "note": "whole stream = fill + timed tail, same loop; value is the tail (largest K, largest scene)"},
         "ms_per_gn_iter": solo["ms_per_gn_iter"],
-        "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop),
+        "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop,
+                             pcg_kernel_us_per_iter_in_loop=(st["globalPcgKernelMs"] * 1e3 / max(1, st["globalPcgIterations"])
+                                                             if st["globalPcgLaunches"] else None),
+                             pcg_launches_in_loop=st["globalPcgLaunches"],
+                             note="ms_per_gn_iter*: whole solves (table build, GN steps, per-solve overheads) per GN "
+                                  "iteration; pcg_kernel_us_per_iter*: the persistent PCG launches' own device time per "
+                                  "PCG iteration (dispatch-stamped events), standalone vs inside the loop"),
         "roofline_ba": roofline_ba(solo),
         "global_dense_end_solve": dense_end,
         "roofline": {"bound": bound, "kernel": "k_apply_ops (op-batch voxel pass)", "achieved": achieved,

@@ -296,4 +296,5 @@ class BFReconStats(C.Structure):
         ("integrateKernelMs", C.c_double), ("localSolveMs", C.c_double), ("globalSolveMs", C.c_double),
         ("reintegrateLaunches", C.c_uint64), ("reintegrateKernelMs", C.c_double),
         ("localVerifications", C.c_uint64), ("invalidLocals", C.c_uint64), ("endSolves", C.c_uint64),
-        ("pcgRecoveries", C.c_uint64), ("hostMs", C.c_double), ("hostWaitMs", C.c_double)]
+        ("pcgRecoveries", C.c_uint64), ("hostMs", C.c_double), ("hostWaitMs", C.c_double),
+        ("globalPcgLaunches", C.c_uint64), ("globalPcgKernelMs", C.c_double)]

@@ -595,6 +595,16 @@ int bf_solver_timer_stop(bf_solver* s, bf_timer* t, float* ms) {
     BF_HIP(hipEventElapsedTime(ms, t->a, t->b));
     BF_CATCH
 }
+int bf_solver_pcg_time(bf_solver* s, int enable, double* ms, uint64_t* launches) {
+    BF_TRY
+    BF_REQUIRE(s, BF_ERR_ARG, "null solver");
+    KernelClock& c = s->solver->pcgClock();
+    if (ms) *ms = c.enabled() ? c.totalMs() : 0.0;
+    if (launches) *launches = c.enabled() ? c.launches() : 0;
+    if (enable && !c.enabled()) c.reset();
+    c.enable(enable != 0);
+    BF_CATCH
+}
 int bf_solver_matrices_to_poses(bf_solver* s, const float* T, uint32_t n, float* rot, float* trans, const int* valid) {
     BF_TRY
     BF_REQUIRE(s && T && rot && trans && valid, BF_ERR_ARG, "null argument");

@@ -369,13 +369,16 @@ void App::localCorrespondences(uint32_t s, uint32_t n) {
     BF_HIP(hipMemcpyAsync(depthPtrs_.p, ptrs.data(), sizeof(float*) * n, hipMemcpyHostToDevice, pre_));
     BF_HIP(hipMemcpyAsync(localT_.p, T.data(), 64 * n, hipMemcpyHostToDevice, pre_));
     BF_HIP(hipMemcpyAsync(localTinv_.p, Ti.data(), 64 * n, hipMemcpyHostToDevice, pre_));
-    BF_HIP(hipStreamSynchronize(pre_));
     BFCorrOptions o = info_.corr;
     o.minPerPair = localMinPerPair_;
     BFEntryJ* out = localCorr_.p + (size_t)info_.maxLocalCorr * s;
-    uint32_t total = 0;
+    // every pair (i, cur), cur = 1 .. n-1, i < cur, in the order AddCurrToResidualsCU appends them as each
+    // frame arrives: one launch for the submap on the input stream
+    std::vector<uint2> list;
     for (uint32_t cur = 1; cur < n; cur++)
-        total += corr_from_depth(depthPtrs_.p, localT_.p, localTinv_.p, cur, 0, o, out + total, info_.maxLocalCorr - total, nullptr);
+        for (uint32_t i = 0; i < cur; i++) list.push_back(make_uint2(i, cur));
+    const uint32_t total = corr_from_pairs(depthPtrs_.p, localT_.p, localTinv_.p, list.data(), (uint32_t)list.size(), o, out,
+                                           info_.maxLocalCorr, nullptr, pre_, corrScratch_);
     if (total) recon_->setLocalCorrespondences(s, out, total);
 }
 
@@ -390,9 +393,10 @@ void App::keyframeCorrespondences(uint32_t k) {
         std::vector<const float*> ptrs(k + 1);
         for (uint32_t i = 0; i <= k; i++) ptrs[i] = kfDepth_.p + dp * i;
         BF_HIP(hipMemcpyAsync(depthPtrs_.p, ptrs.data(), sizeof(float*) * (k + 1), hipMemcpyHostToDevice, pre_));
-        BF_HIP(hipStreamSynchronize(pre_));
-        globalN_ += corr_from_depth(depthPtrs_.p, kfT_.p, kfTinv_.p, k, 0, info_.corr, globalCorr_.p + globalN_,
-                                    info_.maxGlobalCorr - globalN_, nullptr);
+        std::vector<uint2> list(k);
+        for (uint32_t i = 0; i < k; i++) list[i] = make_uint2(i, k);
+        globalN_ += corr_from_pairs(depthPtrs_.p, kfT_.p, kfTinv_.p, list.data(), k, info_.corr, globalCorr_.p + globalN_,
+                                    info_.maxGlobalCorr - globalN_, nullptr, pre_, corrScratch_);
     }
     globalPrefix_.push_back(globalN_);
     recon_->setGlobalCorrespondences(globalCorr_.p, globalN_, globalPrefix_.data(), (uint32_t)globalPrefix_.size());

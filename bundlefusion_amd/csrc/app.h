@@ -15,6 +15,7 @@
 
 #include "../../include/bf/bf.h"
 #include "cache.h"
+#include "corr.h"
 #include "frames.h"
 #include "io.h"
 #include "recon.h"
@@ -95,6 +96,7 @@ private:
     DevBuf<float> localT_, localTinv_, kfT_, kfTinv_;
     DevBuf<const float*> depthPtrs_;    // pointer table handed to the EntryJ producer
     DevBuf<BFEntryJ> localCorr_, globalCorr_;
+    CorrScratch corrScratch_;           // the EntryJ producer's buffers (no per-call allocation)
     std::vector<uint32_t> globalPrefix_;
     uint32_t globalN_ = 0;
     uint32_t next_ = 0;                 // next input frame

@@ -135,9 +135,11 @@ public:
     // statistics (see ba.hip, k_pair_stats); synchronizes
     uint32_t exportPairs(double* stats, int* pairAB, uint32_t cap);
     KernelClock& solveClock() { return solveClock_; }  // whole-solve device time (ms/GN-iter)
+    KernelClock& pcgClock() { return pcgClock_; }      // device time of the persistent PCG launches
 
 private:
     KernelClock solveClock_;
+    KernelClock pcgClock_;
     SolverConfig cfg_;
     hipStream_t stream_;
     uint32_t maxCorrPerImage_;

@@ -14,6 +14,8 @@
 #include "ba.h"
 #include "lie.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -3115,8 +3117,19 @@ void Solver::solve(const SolveArgs& s) {
                         // always wait, on the same stream too: a destroyed solver's stream handle may be
                         // reused by a new solver whose launch must still follow the old one (cheap in order)
                         if (pg.ev) BF_HIP(hipStreamWaitEvent(stream_, pg.ev, 0));
-                        if (small) k_pcg_persist<2><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
-                        else k_pcg_persist<2, PP_NF><<<persistGrid, WG, 0, stream_>>>(a, wS, (int)s.nLin, pcgEpoch_);
+                        // dispatch-stamped events (pcgClock): the launch's own device time, for the in-loop
+                        // time per PCG iteration beside the standalone one
+                        hipEvent_t e0 = nullptr, e1 = nullptr;
+                        const bool timed = pcgClock_.enabled();
+                        if (timed) pcgClock_.slot(e0, e1);
+                        if (small)
+                            hipExtLaunchKernelGGL(k_pcg_persist<2>, dim3(persistGrid), dim3(WG), 0, stream_, e0, e1, 0, a, wS,
+                                                  (int)s.nLin, pcgEpoch_);
+                        else
+                            hipExtLaunchKernelGGL((k_pcg_persist<2, PP_NF>), dim3(persistGrid), dim3(WG), 0, stream_, e0, e1, 0, a,
+                                                  wS, (int)s.nLin, pcgEpoch_);
+                        BF_LAUNCH_CHECK();
+                        if (timed) pcgClock_.commit();
                         if (!pg.ev) BF_HIP(hipEventCreateWithFlags(&pg.ev, hipEventDisableTiming));
                         BF_HIP(hipEventRecord(pg.ev, stream_));
                         pg.stream = stream_;

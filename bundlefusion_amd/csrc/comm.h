@@ -20,11 +20,15 @@ public:
     static void uniqueId(uint8_t* out);
     Comm(const uint8_t* id, int nranks, int rank);
     // In-process loopback group (tests): nranks communicators in one process, each rank driven from its
-    // own host thread (ranks may share a GPU). A collective synchronizes the calling rank's stream,
-    // exchanges through host memory behind a barrier (a rank that never arrives fails it after
-    // timeoutMs instead of hanging) and sums in rank order, so the call sites of the multi-rank path
-    // run without one GPU per rank; RCCL itself is not exercised.
-    static std::shared_ptr<Loopback> loopbackGroup(int nranks, int timeoutMs);
+    // own host thread (ranks share a GPU). A collective is a one-workgroup kernel on the caller's stream,
+    // as RCCL's are: it publishes the rank's contribution in a device slot, waits on the device for every
+    // rank's arrival (bounded by timeoutMs: a rank that never arrives makes the next call throw) and sums
+    // in rank order (comm_loopback.hip). Nothing waits on the host, so the call sites see RCCL's
+    // asynchronous, stream-ordered semantics; RCCL itself is not exercised. As with RCCL, a rank's streams
+    // must not share a hardware queue with another rank's (one process per GPU has its own queues; ranks in
+    // one process need GPU_MAX_HW_QUEUES above their stream count, tests/conftest.py). capacityBytes: the
+    // largest collective (0: 16 MiB).
+    static std::shared_ptr<Loopback> loopbackGroup(int nranks, int timeoutMs, size_t capacityBytes = 0);
     Comm(std::shared_ptr<Loopback> group, int rank);
     ~Comm();
     int size() const { return nranks_; }
@@ -35,6 +39,7 @@ public:
     void broadcast(float* buf, size_t n, int root, hipStream_t stream);
 
 private:
+    void loopbackCollective(void* buf, size_t n, size_t elemBytes, int kind, int root, hipStream_t stream);
     void* comm_ = nullptr;  // ncclComm_t
     std::shared_ptr<Loopback> lb_;
     int nranks_ = 1, rank_ = 0;

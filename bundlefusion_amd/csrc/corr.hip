@@ -20,6 +20,9 @@
 #include "../../include/bf/bf.h"
 #include "bf_math.h"
 #include "bf_runtime.h"
+#include "corr.h"
+
+#include <vector>
 
 namespace bf {
 
@@ -48,26 +51,28 @@ struct CorrArgs {
     float minDepth, maxDepth, depthThresh;
     BFEntryJ* slots;    // [pairs][maxPerPair]
     uint32_t* counts;   // [pairs]
+    const uint2* list;  // (i, cur) per pair, or null: pair p = (start + p, cur)
 };
 
 __global__ __launch_bounds__(CORR_WG) void k_corr_pairs(CorrArgs A) {
     __shared__ uint32_t sWave[CORR_WG / 64];
     __shared__ uint32_t sTaken;
     const uint32_t p = blockIdx.x;
-    const uint32_t i = A.start + p;
+    const uint32_t i = A.list ? A.list[p].x : A.start + p;
+    const uint32_t cur = A.list ? A.list[p].y : A.cur;
     if (threadIdx.x == 0) sTaken = 0;
     __syncthreads();
     const uint32_t N = A.gridW * A.gridH;
     const float* di = A.depth[i];
-    const float* dj = A.depth[A.cur];
+    const float* dj = A.depth[cur];
     const float* Ti = A.T + 16 * (size_t)i;
-    const float* Tj = A.Tinv + 16 * (size_t)A.cur;
+    const float* Tj = A.Tinv + 16 * (size_t)cur;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t r = 0; r < N; r += CORR_WG) {
         const uint32_t k = r + threadIdx.x;
         bool ok = false;
         BFEntryJ e{};
-        if (k < N && i != A.cur) {
+        if (k < N && i != cur) {
             const uint32_t g = corr_perm(k, N);
             const uint32_t gx = g % A.gridW, gy = g / A.gridW;
             const uint32_t u = gx * (A.W / A.gridW) + (A.W / A.gridW) / 2, v = gy * (A.H / A.gridH) + (A.H / A.gridH) / 2;
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(CORR_WG) void k_corr_pairs(CorrArgs A) {
                         if (d2 != -INFINITY && d2 >= A.minDepth && d2 <= A.maxDepth && fabsf(d2 - pj.z) <= A.depthThresh) {
                             const f3 q = xform_p(A.kinv, mk3(d2 * (float)uj, d2 * (float)vj, d2 * 1.0f));
                             e.imgIdx_i = i;
-                            e.imgIdx_j = A.cur;
+                            e.imgIdx_j = cur;
                             e.pos_i.x = pi.x; e.pos_i.y = pi.y; e.pos_i.z = pi.z;
                             e.pos_j.x = q.x; e.pos_j.y = q.y; e.pos_j.z = q.z;
                             ok = true;
@@ -149,18 +154,31 @@ __global__ __launch_bounds__(1024) void k_corr_pack(const BFEntryJ* __restrict__
 
 }  // namespace
 
-// host entry (bf_corr_from_depth)
-uint32_t corr_from_depth(const float* const* depth, const float* T, const float* Tinv, uint32_t cur, uint32_t start,
-                         const BFCorrOptions& o, BFEntryJ* out, uint32_t cap, uint32_t* total) {
-    BF_REQUIRE(depth && T && Tinv, BF_ERR_ARG, "null input");
-    BF_REQUIRE(start <= cur, BF_ERR_ARG, "startFrame > curFrame");
-    BF_REQUIRE(o.width > 0 && o.height > 0 && o.stride > 0 && o.stride <= o.width && o.stride <= o.height, BF_ERR_ARG,
-               "image size / stride");
-    BF_REQUIRE(o.maxPerPair > 0 && o.maxPerPair <= MAX_PER_PAIR, BF_ERR_ARG, "maxPerPair 1..64");
-    BF_REQUIRE(out != nullptr || cap == 0, BF_ERR_ARG, "null output");
-    const uint32_t pairs = cur - start;
-    if (total) *total = 0;
-    if (pairs == 0) return 0;
+void CorrScratch::reserve(uint32_t npairs, uint32_t maxPerPair) {
+    const size_t need = (size_t)std::max(npairs, 1u) * maxPerPair;
+    if (slots.n < need) slots.alloc(need + need / 2);
+    if (counts.n < npairs) counts.alloc(npairs + npairs / 2 + 1);
+    if (pairs.n < npairs) pairs.alloc(npairs + npairs / 2 + 1);
+    if (!total.n) total.alloc(1);
+    if (!hostTotal) BF_HIP(hipHostMalloc((void**)&hostTotal, sizeof(uint32_t), hipHostMallocDefault));
+}
+
+namespace {
+uint32_t corr_run(CorrArgs A, uint32_t pairs, const BFCorrOptions& o, BFEntryJ* out, uint32_t cap, uint32_t* total,
+                  hipStream_t s, CorrScratch& sc) {
+    A.slots = sc.slots.p;
+    A.counts = sc.counts.p;
+    k_corr_pairs<<<pairs, CORR_WG, 0, s>>>(A);
+    BF_LAUNCH_CHECK();
+    k_corr_pack<<<1, 1024, 0, s>>>(sc.slots.p, sc.counts.p, pairs, o.maxPerPair, o.minPerPair, out, cap, sc.total.p);
+    BF_LAUNCH_CHECK();
+    BF_HIP(hipMemcpyAsync(sc.hostTotal, sc.total.p, 4, hipMemcpyDeviceToHost, s));
+    BF_HIP(hipStreamSynchronize(s));
+    const uint32_t t = *sc.hostTotal;
+    if (total) *total = t;
+    return t < cap ? t : cap;
+}
+CorrArgs corr_args(const float* const* depth, const float* T, const float* Tinv, const BFCorrOptions& o) {
     CorrArgs A{};
     A.depth = depth;
     A.T = T;
@@ -171,25 +189,56 @@ uint32_t corr_from_depth(const float* const* depth, const float* T, const float*
     A.gridW = o.width / o.stride; A.gridH = o.height / o.stride;
     // candidate permutation: k -> k * 2654435761 mod N is a bijection (the multiplier is a prime > N)
     A.maxPerPair = o.maxPerPair;
-    A.cur = cur; A.start = start;
     A.minDepth = o.minDepth; A.maxDepth = o.maxDepth; A.depthThresh = o.depthThresh;
-    DevBuf<BFEntryJ> slots;
-    DevBuf<uint32_t> counts, tot;
-    slots.alloc((size_t)pairs * o.maxPerPair);
-    counts.alloc(pairs);
-    tot.alloc(1);
-    A.slots = slots.p;
-    A.counts = counts.p;
+    return A;
+}
+void corr_check(const BFCorrOptions& o, const BFEntryJ* out, uint32_t cap) {
+    BF_REQUIRE(o.width > 0 && o.height > 0 && o.stride > 0 && o.stride <= o.width && o.stride <= o.height, BF_ERR_ARG,
+               "image size / stride");
+    BF_REQUIRE(o.maxPerPair > 0 && o.maxPerPair <= MAX_PER_PAIR, BF_ERR_ARG, "maxPerPair 1..64");
+    BF_REQUIRE(out != nullptr || cap == 0, BF_ERR_ARG, "null output");
+}
+}  // namespace
+
+uint32_t corr_from_pairs(const float* const* depth, const float* T, const float* Tinv, const uint2* list, uint32_t npairs,
+                         const BFCorrOptions& o, BFEntryJ* out, uint32_t cap, uint32_t* total, hipStream_t stream,
+                         CorrScratch& sc) {
+    BF_REQUIRE(depth && T && Tinv && list, BF_ERR_ARG, "null input");
+    corr_check(o, out, cap);
+    if (total) *total = 0;
+    if (npairs == 0) return 0;
+    sc.reserve(npairs, o.maxPerPair);
+    BF_HIP(hipMemcpyAsync(sc.pairs.p, list, sizeof(uint2) * npairs, hipMemcpyHostToDevice, stream));
+    CorrArgs A = corr_args(depth, T, Tinv, o);
+    A.list = sc.pairs.p;
+    return corr_run(A, npairs, o, out, cap, total, stream, sc);
+}
+
+// host entry (bf_corr_from_depth): pairs (start .. cur - 1, cur), on its own stream and scratch
+uint32_t corr_from_depth(const float* const* depth, const float* T, const float* Tinv, uint32_t cur, uint32_t start,
+                         const BFCorrOptions& o, BFEntryJ* out, uint32_t cap, uint32_t* total) {
+    BF_REQUIRE(depth && T && Tinv, BF_ERR_ARG, "null input");
+    BF_REQUIRE(start <= cur, BF_ERR_ARG, "startFrame > curFrame");
+    corr_check(o, out, cap);
+    const uint32_t pairs = cur - start;
+    if (total) *total = 0;
+    if (pairs == 0) return 0;
+    CorrScratch sc;
+    sc.reserve(pairs, o.maxPerPair);
+    CorrArgs A = corr_args(depth, T, Tinv, o);
+    A.cur = cur;
+    A.start = start;
     hipStream_t s = nullptr;
-    k_corr_pairs<<<pairs, CORR_WG, 0, s>>>(A);
-    BF_LAUNCH_CHECK();
-    k_corr_pack<<<1, 1024, 0, s>>>(slots.p, counts.p, pairs, o.maxPerPair, o.minPerPair, out, cap, tot.p);
-    BF_LAUNCH_CHECK();
-    uint32_t t = 0;
-    BF_HIP(hipMemcpyAsync(&t, tot.p, 4, hipMemcpyDeviceToHost, s));
-    BF_HIP(hipStreamSynchronize(s));
-    if (total) *total = t;
-    return t < cap ? t : cap;
+    BF_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    uint32_t n = 0;
+    try {
+        n = corr_run(A, pairs, o, out, cap, total, s, sc);
+    } catch (...) {
+        (void)hipStreamDestroy(s);
+        throw;
+    }
+    BF_HIP(hipStreamDestroy(s));
+    return n;
 }
 
 }  // namespace bf

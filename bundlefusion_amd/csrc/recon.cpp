@@ -148,6 +148,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
         scene_->applyClock().enable(true);
         local_->solveClock().enable(true);
         global_->solveClock().enable(true);
+        global_->pcgClock().enable(true);
     }
 
     const uint32_t L = S + 1, K = opt_.maxKeyframes;
@@ -237,6 +238,7 @@ Recon::~Recon() {
     if (sceneStream_) (void)hipStreamDestroy(sceneStream_);
     if (baStream_) (void)hipStreamDestroy(baStream_);
     if (localStream_) (void)hipStreamDestroy(localStream_);
+    if (copyStream_) (void)hipStreamDestroy(copyStream_);
 }
 
 void Recon::setFrame(uint32_t f, const float* depth, const uint8_t* color, const BFCachedFrame* cache, const BFMat4& Tinc) {
@@ -303,7 +305,11 @@ void Recon::computePairBounds(bool append) {
     }
     const uint32_t from = std::min(pairCountedN_, globalCorrN_);
     std::vector<BFEntryJ> h(globalCorrN_ - from);
-    if (!h.empty()) BF_HIP(hipMemcpy(h.data(), globalCorr_ + from, sizeof(BFEntryJ) * h.size(), hipMemcpyDeviceToHost));
+    if (!h.empty()) {  // on a stream of its own: no other stream's work (nor the null stream's device-wide order) waits
+        if (!copyStream_) BF_HIP(hipStreamCreateWithFlags(&copyStream_, hipStreamNonBlocking));
+        BF_HIP(hipMemcpyAsync(h.data(), globalCorr_ + from, sizeof(BFEntryJ) * h.size(), hipMemcpyDeviceToHost, copyStream_));
+        BF_HIP(hipStreamSynchronize(copyStream_));
+    }
     uint32_t e = from;
     for (size_t s = pairBound_.size(); s < globalPrefix_.size(); s++) {
         const uint32_t end = std::min(globalPrefix_[s], globalCorrN_);
@@ -931,6 +937,8 @@ BFReconStats Recon::stats() {
         s.reintegrateLaunches = scene_->applyClock().launches();
         s.localSolveMs = local_->solveClock().totalMs();
         s.globalSolveMs = global_->solveClock().totalMs();
+        s.globalPcgKernelMs = global_->pcgClock().totalMs();
+        s.globalPcgLaunches = global_->pcgClock().launches();
     }
     return s;
 }
@@ -947,6 +955,7 @@ void Recon::resetStats() {
     scene_->applyClock().reset();
     local_->solveClock().reset();
     global_->solveClock().reset();
+    global_->pcgClock().reset();
 }
 
 void Recon::attachCache(Cache* c) {

@@ -121,6 +121,7 @@ private:
     // local solves, which depend only on their submap's frames, so submap s+1's local solve runs while
     // submap s's global solve is still in flight
     hipStream_t sceneStream_ = nullptr, baStream_ = nullptr, localStream_ = nullptr;
+    hipStream_t copyStream_ = nullptr;  // host readbacks of inputs (computePairBounds), created on first use
     std::unique_ptr<Scene> scene_;
     std::unique_ptr<Solver> local_, global_;
     std::unique_ptr<TrajectoryManager> tm_;

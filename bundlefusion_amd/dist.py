@@ -119,14 +119,15 @@ class Comm:
 
 class LoopbackComm:
     """One rank of an in-process loopback group (bf_comm_create_loopback): the multi-rank loop's
-    collectives for ranks driven from threads of one process, exchanged through host memory (tests;
-    no RCCL). Same .h / .rank / .world / .close() as Comm."""
+    collectives for ranks driven from threads of one process sharing one GPU, each a one-workgroup kernel
+    on the caller's stream that waits on the device for every rank (RCCL's asynchronous, stream-ordered
+    semantics; tests, no RCCL). Same .h / .rank / .world / .close() as Comm."""
 
     def __init__(self, h, rank: int, world: int):
         self.h, self.rank, self.world = h, rank, world
 
     @staticmethod
-    def group(world: int, timeout_ms: int = 120000) -> list["LoopbackComm"]:
+    def group(world: int, timeout_ms: int = 30000) -> list["LoopbackComm"]:
         import ctypes as C
         from . import check, lib
         hs = (C.c_void_p * world)()

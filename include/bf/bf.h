@@ -187,6 +187,9 @@ int bf_solver_num_entries_per_row(bf_solver* s, const int** dptr);
 int bf_solver_synchronize(bf_solver* s);
 int bf_solver_timer_start(bf_solver* s, bf_timer* t);
 int bf_solver_timer_stop(bf_solver* s, bf_timer* t, float* ms); /* synchronizes */
+/* device time of the persistent PCG launches (one per GN step, dispatch-stamped events): enable != 0 starts
+ * (or keeps) timing them, enable == 0 stops; *ms / *launches: totals since timing started (synchronizes) */
+int bf_solver_pcg_time(bf_solver* s, int enable, double* ms, uint64_t* launches);
 /* convertMatricesToPosesCU / convertPosesToMatricesCU (SBA.cu:75-119), on the solver's stream */
 int bf_solver_matrices_to_poses(bf_solver* s, const float* T, uint32_t n, float* rot, float* trans, const int* valid);
 int bf_solver_poses_to_matrices(bf_solver* s, const float* rot, const float* trans, uint32_t n, float* T, const int* valid);
@@ -230,9 +233,11 @@ int bf_comm_unique_id(uint8_t id[128]);
 int bf_comm_create(const uint8_t id[128], int nranks, int rank, bf_comm** out);
 int bf_comm_destroy(bf_comm* c);
 /* In-process loopback group (tests): out[0..nranks-1] are communicators of one group for ranks driven from
- * their own host threads in this process (they may share a GPU). Collectives synchronize the calling rank's
- * stream and exchange through host memory behind a barrier that fails after timeoutMs (0: 60 s) if a rank
- * never arrives; sums run in rank order. Lets the multi-rank loop run on one GPU; RCCL is not involved. */
+ * their own host threads in this process, sharing the current GPU. A collective is a one-workgroup kernel
+ * enqueued on the caller's stream (as RCCL's are: asynchronous, stream-ordered, no host wait) that waits on
+ * the device for every rank's contribution and sums in rank order; a rank that never arrives within
+ * timeoutMs (0: 60 s) ends the wait and the next collective call fails. Lets the multi-rank loop run on one
+ * GPU with RCCL's ordering semantics; RCCL is not involved. */
 int bf_comm_create_loopback(int nranks, int timeoutMs, bf_comm** out);
 /* in-place sum over ranks of n doubles (device pointer); synchronizes (tests) */
 int bf_comm_allreduce_sum_f64(bf_comm* c, double* d, size_t n);
@@ -339,6 +344,8 @@ typedef struct BFReconStats {
                                     a solve with a BF_SOLVE_ERR_FATAL bit fails the call with BF_ERR_INTERNAL */
     double hostMs;               /* host wall time inside bf_recon_process_frame (enqueueing + waits) */
     double hostWaitMs;           /* ... of it blocked on bundling results (resultLag, a full ring) */
+    uint64_t globalPcgLaunches;  /* timed persistent PCG launches of the global solves (one per GN step) */
+    double globalPcgKernelMs;    /* their summed device time (dispatch-stamped events) */
 } BFReconStats;
 
 typedef struct bf_recon bf_recon;
