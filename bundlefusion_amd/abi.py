@@ -14,7 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-# BF_HIP_LIB: an alternative build of the same library (A/B timing of kernel variants, tools/gpu_ab.sh)
+# BF_HIP_LIB: an alternative build of the same library (A/B timing of kernel variants: the ab: step of tools/gpu.sh)
 LIB_PATH = os.environ.get("BF_HIP_LIB") or os.path.join(_HERE, "libbf_hip.so")
 HEADER_PATH = os.path.join(REPO, "include", "bf", "bf.h")
 

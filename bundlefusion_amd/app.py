@@ -53,7 +53,7 @@ class FriedLiver:
                  overwrite_sens: bool = False, skip_outputs: bool = False, async_bundling: int = 1,
                  record_ops: bool = False, enable_timing: bool = False, max_frames: int = 0,
                  front_end_drift=(math.radians(0.05), 0.002), front_end_seed: int = 1, corr_stride: int = 16,
-                 corr_depth_thresh: float = 0.02, prefetch_frames: int = 16, decode_threads: int = 4,
+                 corr_depth_thresh: float = 0.02, prefetch_frames: int = 16, decode_threads: int = 8,
                  num_solve_frames_before_exit: int = 0, shard=(1, 0), shard_chunk: float = 0.0, result_lag: int = 0):
         """shard = (count, index): this rank's TSDF chunk-ownership shard of a multi-GPU run (attach the ranks'
         communicator with set_comm before the first step)."""

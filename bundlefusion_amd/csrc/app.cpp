@@ -212,6 +212,7 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
 
     // ---- device state ----------------------------------------------------------------------------------
     BF_HIP(hipStreamCreateWithFlags(&pre_, hipStreamNonBlocking));
+    BF_HIP(hipEventCreateWithFlags(&uploadEv_, hipEventDisableTiming));
     preproc_.reset(new Preproc(si.depthWidth, si.depthHeight, si.colorWidth, si.colorHeight, iw, ih, info_.preprocess, pre_));
     CacheConfig cc{};
     cc.inputWidth = co.inputWidth;
@@ -252,7 +253,8 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
 
     // ---- decode threads (SensorDataReader's RGBDFrameCacheRead, SensorDataReader.cpp:76-77) ---------------
     numSlots_ = std::max(2u, o.prefetchFrames ? o.prefetchFrames : 16u);
-    numWorkers_ = std::max(1u, std::min(numSlots_, o.decodeThreads ? o.decodeThreads : 4u));
+    // decoding (zlib + JPEG at 640x480: ~3 ms per frame and thread) sets the pace below ~8 threads
+    numWorkers_ = std::max(1u, std::min(numSlots_, o.decodeThreads ? o.decodeThreads : 8u));
     slots_.resize(numSlots_);
     for (uint32_t k = 0; k < numSlots_; k++) slots_[k].expect = k;
     for (Slot& s : slots_) {
@@ -270,6 +272,7 @@ App::~App() {
     cv_.notify_all();
     for (std::thread& t : workers_)
         if (t.joinable()) t.join();
+    if (pre_) (void)hipStreamSynchronize(pre_);  // no copy out of a pinned slot still in flight
     recon_.reset();
     cache_.reset();
     preproc_.reset();
@@ -277,6 +280,7 @@ App::~App() {
         if (s.depth) (void)hipHostFree(s.depth);
         if (s.rgbx) (void)hipHostFree(s.rgbx);
     }
+    if (uploadEv_) (void)hipEventDestroy(uploadEv_);
     if (pre_) (void)hipStreamDestroy(pre_);
 }
 
@@ -318,6 +322,13 @@ void App::decodeLoop(uint32_t w) {
         }
         cv_.notify_all();
     }
+}
+
+void App::releaseUploaded() {
+    if (uploaded_ < 0) return;
+    BF_HIP(hipEventSynchronize(uploadEv_));
+    releaseFrame((uint32_t)uploaded_);
+    uploaded_ = -1;
 }
 
 App::Slot& App::waitFrame(uint32_t f) {
@@ -411,6 +422,8 @@ bool App::step() {
     const size_t ip = (size_t)cam.imageWidth * cam.imageHeight;
     const size_t dp = (size_t)info_.sensorDepthWidth * info_.sensorDepthHeight;
     // ---- CUDAImageManager::process ---------------------------------------------------------------------
+    // the previous frame's pinned slot goes back to the decoders once its copies have run (a frame ago)
+    releaseUploaded();
     Slot& sl = waitFrame(f);
     const double t1 = now_s();
     tm_.decodeWaitSeconds += t1 - t0;
@@ -423,8 +436,10 @@ bool App::step() {
     BF_HIP(hipMemcpyAsync(localDepth_.p + dp * (f % L_), preproc_->filteredDepth(), dp * 4, hipMemcpyDeviceToDevice, pre_));
     if (f % S_ == 0)
         BF_HIP(hipMemcpyAsync(kfDepth_.p + dp * (f / S_), preproc_->filteredDepth(), dp * 4, hipMemcpyDeviceToDevice, pre_));
-    BF_HIP(hipStreamSynchronize(pre_));
-    releaseFrame(f);  // the pinned slot has been copied
+    // no host wait: every later reader of the staging buffers (this frame's cache store, the next frame's
+    // copies) is queued on pre_ behind them; the pinned slot is released at the next step
+    BF_HIP(hipEventRecord(uploadEv_, pre_));
+    uploaded_ = (int64_t)f;
     const double t2 = now_s();
     tm_.uploadSeconds += t2 - t1;
     tm_.uploadBytes += (double)(dp * 2 + dRgbx_.n);
@@ -451,6 +466,7 @@ bool App::step() {
 
 BFAppResult App::finish() {
     BF_REQUIRE(!finished_, BF_ERR_STATE, "finish called twice");
+    releaseUploaded();
     BFAppResult r{};
     r.frames = next_;
     if (next_ > 0) {

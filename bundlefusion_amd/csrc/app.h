@@ -59,6 +59,7 @@ private:
     void decodeLoop(uint32_t worker);
     Slot& waitFrame(uint32_t f);
     void releaseFrame(uint32_t f);
+    void releaseUploaded();  // the last uploaded frame's pinned slot, once its copies ran
     void localCorrespondences(uint32_t s, uint32_t n);  // submap s's EntryJ (local indices)
     void keyframeCorrespondences(uint32_t k);           // keyframe k against keyframes 0..k-1
     void writeOutputs(BFAppResult& r);
@@ -84,6 +85,8 @@ private:
 
     // device
     hipStream_t pre_ = nullptr;         // preprocessing + cache stream
+    hipEvent_t uploadEv_ = nullptr;     // after the last frame's H2D copies
+    int64_t uploaded_ = -1;             // that frame (its pinned slot not yet released), or -1
     std::unique_ptr<Preproc> preproc_;
     std::unique_ptr<Cache> cache_;
     std::unique_ptr<Recon> recon_;

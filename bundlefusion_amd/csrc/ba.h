@@ -126,6 +126,8 @@ public:
     const int* verifyFlag() const;
     const int* numEntriesPerRow() const { return rowCount_.p; }  // getVarToCorrNumEntriesPerRow
     hipStream_t stream() const { return stream_; }
+    // moves the solver's later work to another stream (the caller orders it after this one's)
+    void setStream(hipStream_t s) { stream_ = s; }
     const SolverConfig& config() const { return cfg_; }
     size_t deviceBytes() const;
     // sharded global solve: this handle builds the normal-equation blocks of the

@@ -95,29 +95,27 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     opt_.maxGlobalCorr = or_default(o.maxGlobalCorr, opt_.maxKeyframes * 1000u);
 
     BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
-    // Bundling streams at the highest queue priority take CU slots ahead of the scene stream's next
-    // workgroups (priority orders dispatch; it never preempts a running workgroup):
-    // - sharded, each GPU has a fraction of the voxel work and the (replicated) bundling is co-critical:
-    //   +7 % at G = 4, +11 % at G = 8 (one rank's share on one GPU, profiles/r3n_late_experiments.txt);
-    // - unsharded, as long as the global solve's persistent grid (about N / 4 workgroups of the 512 slots
-    //   at 2 per CU) leaves the scene stream a quarter of the device: the bench stream (K = 500) 1 300 ->
-    //   1 362-1 367 frames/s, config 5's stream (K = 1 000) 181.6 -> 183.7. At normal priority each of a
-    //   solve's dependent launches waits for slots behind the voxel pass, the submap's result misses its
-    //   hand-off frame and the frame loop blocks with less work queued (profiles/r8u_*, r8v_*, r9b_*);
-    // - config 4's 2 000 keyframes, whose grid needs nearly every slot, starve the scene stream at high
-    //   priority instead (981 -> 921 frames/s), so solves that large keep the default priority.
-    constexpr uint32_t kHighPriorityMaxKeyframes = 1537;  // grid <= ~3/4 of the slots
-    bool baHigh = (so && so->shardCount > 1) || opt_.maxKeyframes <= kHighPriorityMaxKeyframes;
-    if (const char* e = std::getenv("BF_BA_HIGH_PRIORITY")) baHigh = std::atoi(e) != 0;  // A/B measurements
-    if (baHigh) {
-        int prLeast = 0, prGreatest = 0;
-        BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
-        BF_HIP(hipStreamCreateWithPriority(&baStream_, hipStreamNonBlocking, prGreatest));
-        BF_HIP(hipStreamCreateWithPriority(&localStream_, hipStreamNonBlocking, prGreatest));
-    } else {  // normal priority, as the scene stream (ROCm's "least" priority is below normal)
-        BF_HIP(hipStreamCreateWithFlags(&baStream_, hipStreamNonBlocking));
-        BF_HIP(hipStreamCreateWithFlags(&localStream_, hipStreamNonBlocking));
+    // bundling stream priority: see switchBundlingPriority
+    // The policy is keyed on each solve's own size (switchBundlingPriority at every submap): a run sized for
+    // many keyframes bundles at high priority until its global solve grows past kHighPriorityMaxKeyframes.
+    sharded_ = so && so->shardCount > 1;
+    int prLeast = 0, prGreatest = 0;
+    BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
+    const char* forced = std::getenv("BF_BA_HIGH_PRIORITY");  // A/B measurements: one fixed priority
+    if (forced) priorityPolicy_ = std::atoi(forced) != 0 ? 1 : 0;
+    const bool needHigh = forced ? priorityPolicy_ == 1 : true;
+    const bool needNormal = forced ? priorityPolicy_ == 0 : (!sharded_ && opt_.maxKeyframes > kHighPriorityMaxKeyframes);
+    if (needHigh) {
+        BF_HIP(hipStreamCreateWithPriority(&baStreamHi_, hipStreamNonBlocking, prGreatest));
+        BF_HIP(hipStreamCreateWithPriority(&localStreamHi_, hipStreamNonBlocking, prGreatest));
     }
+    if (needNormal) {  // normal priority, as the scene stream (ROCm's "least" priority is below normal)
+        BF_HIP(hipStreamCreateWithFlags(&baStreamLo_, hipStreamNonBlocking));
+        BF_HIP(hipStreamCreateWithFlags(&localStreamLo_, hipStreamNonBlocking));
+    }
+    baHigh_ = needHigh;
+    baStream_ = baHigh_ ? baStreamHi_ : baStreamLo_;
+    localStream_ = baHigh_ ? localStreamHi_ : localStreamLo_;
     for (int b = 0; b < 2; b++) {
         BF_HIP(hipEventCreateWithFlags(&localDone_[b], hipEventDisableTiming));
         BF_HIP(hipEventCreateWithFlags(&globalDone_[b], hipEventDisableTiming));
@@ -132,7 +130,7 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     }
     scene_.reset(new Scene(sc, sceneStream_));
     tileStride_ = Scene::tileCount(cam_);
-    framePixels_ = (size_t)cam_.imageWidth * cam_.imageHeight;
+    framePixels_ = Scene::dcCount(cam_);
     // the cache costs 8 B per pixel per frame (12.3 GB for 5 000 VGA frames, next to the frame store
     // itself); beyond 32 GB each batch rebuilds its ops' images in the scene's scratch instead
     if (tileStride_ * opt_.maxFrames * sizeof(float2) <= (4ull << 30) &&
@@ -216,8 +214,8 @@ Recon::~Recon() {
         baThread_.join();
     }
     if (sceneStream_) (void)hipStreamSynchronize(sceneStream_);
-    if (baStream_) (void)hipStreamSynchronize(baStream_);
-    if (localStream_) (void)hipStreamSynchronize(localStream_);
+    for (hipStream_t st : {baStreamHi_, baStreamLo_, localStreamHi_, localStreamLo_})
+        if (st) (void)hipStreamSynchronize(st);
     for (int b = 0; b < 2; b++) {
         if (localDone_[b]) (void)hipEventDestroy(localDone_[b]);
         if (globalDone_[b]) (void)hipEventDestroy(globalDone_[b]);
@@ -236,8 +234,8 @@ Recon::~Recon() {
     local_.reset();
     global_.reset();
     if (sceneStream_) (void)hipStreamDestroy(sceneStream_);
-    if (baStream_) (void)hipStreamDestroy(baStream_);
-    if (localStream_) (void)hipStreamDestroy(localStream_);
+    for (hipStream_t st : {baStreamHi_, baStreamLo_, localStreamHi_, localStreamLo_})
+        if (st) (void)hipStreamDestroy(st);
     if (copyStream_) (void)hipStreamDestroy(copyStream_);
 }
 
@@ -507,6 +505,7 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     }
     const uint32_t nk = s + 1;
     BF_REQUIRE(nk + 1 <= opt_.maxKeyframes, BF_ERR_CAPACITY, "keyframes exceed maxKeyframes");
+    switchBundlingPriority(nk);
     P.numKeyframes = nk;
     const std::pair<BFEntryJ*, uint32_t> lc = localCorr_[s];
     // everything below only issues work on baStream_ from state fixed at this point: the bundling
@@ -522,6 +521,41 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     lastSubmapEnqueued_ = s;
     // m_totalNumOptLocalFrames (OnlineBundler.cpp:268): the frames the complete trajectory covers
     optimizedFrames_ = S * s + std::min(n, S);
+}
+
+// Bundling streams at the highest queue priority take CU slots ahead of the scene stream's next workgroups
+// (priority orders dispatch; it never preempts a running workgroup):
+// - sharded, each GPU has a fraction of the voxel work and the (replicated) bundling is co-critical: +7 % at
+//   G = 4, +11 % at G = 8 (one rank's share on one GPU, profiles/r3n_late_experiments.txt);
+// - unsharded, while the global solve's persistent grid (about N / 4 workgroups of the 512 slots at 2 per
+//   CU) leaves the scene stream a quarter of the device: the bench stream (K = 500) 1 300 -> 1 362-1 367
+//   frames/s, config 5's stream (K = 1 000) 181.6 -> 183.7. At normal priority each of a solve's dependent
+//   launches waits for slots behind the voxel pass, the submap's result misses its hand-off frame and the
+//   frame loop blocks with less work queued (profiles/r8u_*, r8v_*, r9b_*);
+// - solves above kHighPriorityMaxKeyframes keyframes (config 4's 2 000), whose grid needs nearly every
+//   slot, starve the scene stream at high priority instead (981 -> 921 frames/s): they run at normal priority.
+// Keyed on the solve being issued (nk keyframes), not on the run's capacity: a run sized for 2 000
+// keyframes bundles at high priority until its solves pass the bound. The switch (once per run: K only
+// grows) orders the new streams after the old ones' work and moves both solvers onto them.
+void Recon::switchBundlingPriority(uint32_t nk) {
+    if (priorityPolicy_ >= 0) return;  // fixed by BF_BA_HIGH_PRIORITY
+    const bool high = sharded_ || nk <= kHighPriorityMaxKeyframes;
+    if (high == baHigh_) return;
+    hipStream_t ba = high ? baStreamHi_ : baStreamLo_, loc = high ? localStreamHi_ : localStreamLo_;
+    if (!ba || !loc) return;  // that priority was not created for this run
+    baDrain();                // a bundling thread has issued everything queued on the old streams
+    hipEvent_t e[2];
+    for (hipEvent_t& x : e) BF_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    BF_HIP(hipEventRecord(e[0], baStream_));
+    BF_HIP(hipEventRecord(e[1], localStream_));
+    for (hipStream_t st : {ba, loc})
+        for (hipEvent_t x : e) BF_HIP(hipStreamWaitEvent(st, x, 0));
+    for (hipEvent_t x : e) BF_HIP(hipEventDestroy(x));
+    baStream_ = ba;
+    localStream_ = loc;
+    global_->setStream(ba);
+    local_->setStream(loc);
+    baHigh_ = high;
 }
 
 void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool haveCache,

@@ -122,6 +122,13 @@ private:
     // submap s's global solve is still in flight
     hipStream_t sceneStream_ = nullptr, baStream_ = nullptr, localStream_ = nullptr;
     hipStream_t copyStream_ = nullptr;  // host readbacks of inputs (computePairBounds), created on first use
+    // bundling streams at the highest and at normal queue priority; baStream_ / localStream_ are the active
+    // pair (switchBundlingPriority, keyed on the size of the solve being issued)
+    hipStream_t baStreamHi_ = nullptr, baStreamLo_ = nullptr, localStreamHi_ = nullptr, localStreamLo_ = nullptr;
+    static constexpr uint32_t kHighPriorityMaxKeyframes = 1537;  // persistent grid <= ~3/4 of the CU slots
+    bool baHigh_ = true, sharded_ = false;
+    int priorityPolicy_ = -1;  // -1: by solve size; 0 / 1: normal / high throughout (BF_BA_HIGH_PRIORITY)
+    void switchBundlingPriority(uint32_t nk);
     std::unique_ptr<Scene> scene_;
     std::unique_ptr<Solver> local_, global_;
     std::unique_ptr<TrajectoryManager> tm_;

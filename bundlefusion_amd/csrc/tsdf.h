@@ -56,7 +56,7 @@ struct VoxelOp {
     const uint8_t* color;
     bool deint;
     // optional per-depth-map cache of the band-cull depth tiles (Scene::tileCount(cam) float2: fine
-    // level, then coarse) and of the interleaved {depth bits, colour} image (W*H uint2, the voxel
+    // level, then coarse) and of the interleaved {depth bits, colour} image (Scene::dcCount(cam) uint2, the voxel
     // pass's gather source); both computed by the batch unless tilesReady (they depend on the frame only)
     float2* tiles = nullptr;
     uint2* dc = nullptr;
@@ -87,6 +87,7 @@ public:
     // reference's garbageCollect after the loop sees it.
     void applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& cam);
     static size_t tileCount(const BFDepthCameraParams& cam);  // float2 per depth map of a VoxelOp tile cache
+    static size_t dcCount(const BFDepthCameraParams& cam);    // uint2 per depth map of a VoxelOp dc image
     KernelClock& applyClock() { return applyClock_; }  // k_apply_ops launches
     void garbageCollect();
     void compactify(const BFMat4& T, const BFDepthCameraParams& cam);

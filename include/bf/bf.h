@@ -655,7 +655,7 @@ typedef struct BFAppOptions {
     uint32_t corrStride;        /* EntryJ producer sampling grid, pixels [16] */
     float corrDepthThresh;      /* depth agreement, m [0.02] */
     uint32_t prefetchFrames;    /* decoded frames ahead [16] */
-    uint32_t decodeThreads;     /* [4] */
+    uint32_t decodeThreads;     /* [8] */
     int32_t numSolveFramesBeforeExit; /* overrides s_numSolveFramesBeforeExit when != 0 (-2: run no past-end phase) */
     uint32_t shardCount;        /* multi-GPU (one app per GPU, every rank on the same .sens and parameters): the
                                    TSDF is split into shardCount chunk-ownership shards (BFSceneOptions) and

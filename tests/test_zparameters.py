@@ -190,3 +190,17 @@ def test_params_py_files_resolve_like_the_reference_settings(sens, tmp_path):
     d.mkdir()
     got = _resolved(*write_parameter_files(str(d), {}, {}, sens=sens), sens)
     assert got == ref
+
+
+def test_resolve_rejects_what_bf_app_create_rejects(sens, tmp_path):
+    """The parameter stage's checks (FriedLiver.cpp / SensorDataReader): a stream longer than s_maxNumImages x
+    s_submapSize, a missing sensor file, a stream without colour."""
+    import bundlefusion_amd as bfa
+    pa, pb = write_parameter_files(str(tmp_path), {}, {"s_maxNumImages": 1, "s_submapSize": 2}, sens=sens)
+    with pytest.raises(bfa.BFError, match="please change param file"):
+        resolve(pa, pb, sens)  # 3 frames > 1 x 2
+    pa, pb = write_parameter_files(str(tmp_path), {}, {}, sens=sens)
+    with pytest.raises(bfa.BFError):
+        resolve(pa, pb, str(tmp_path / "missing.sens"))
+    info, loop = resolve(pa, pb, sens, max_frames=2)  # maxFrames caps the stream
+    assert info.numFrames == 2 and loop.maxFrames == 2

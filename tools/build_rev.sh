@@ -1,7 +1,7 @@
 #!/bin/bash
 # Builds bundlefusion_amd/libbf_hip_<NAME>.so with one source (tsdf.hip by default, or ba, ...) taken
 # from git revision REV (the other objects from the current build): the A/B baseline of a kernel change
-# (BF_HIP_LIB=... tools/gpu_ab.sh). Usage: tools/build_rev.sh REV NAME [SRC]
+# (the ab: step of tools/gpu.sh). Usage: tools/build_rev.sh REV NAME [SRC]
 set -e
 cd "$(dirname "$0")/.."
 REV=$1; NAME=$2; BASE=${3:-tsdf}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Builds bundlefusion_amd/libbf_hip_<NAME>.so: the library with one source (tsdf by default, or ba,
 # ...) compiled under extra defines (kernel variants and measurement builds for an A/B timing run:
-# BF_HIP_LIB=... tools/gpu_ab.sh). Usage: tools/build_variant.sh NAME "-DBF_APPLY_ZC=2 ..." [SRC]
+# the ab: step of tools/gpu.sh). Usage: tools/build_variant.sh NAME "-DBF_APPLY_ZC=2 ..." [SRC]
 # (after `make -C bundlefusion_amd/csrc`)
 set -e
 cd "$(dirname "$0")/.."

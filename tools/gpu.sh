@@ -11,6 +11,8 @@
 #   profile:NAME[:ARGS]    tools/profile_bench.sh TAG/NAME ARGS (kernel stats + FETCH/WRITE/VALU passes)
 #   sqpmc:NAME:KERNEL:CNT[:ARGS]  one --pmc pass of counters CNT (',' separated) over KERNEL's dispatches
 #   sens:N[:ARGS]          write an N-frame synthetic .sens (tools/make_sens.py), then bench.py --sens ARGS
+#   trace:NAME[:ARGS]      kernel trace of the bench (rocprofv3 --kernel-trace): the scene stream's per-frame timeline
+#                          (tools/stream_timeline.py) and the input kernels' overlap with the voxel pass (overlap_attr.py)
 #   py:NAME:SECONDS:ARGS   python ARGS (a tool script) with a SECONDS limit -> NAME.log
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -54,6 +56,11 @@ for step in "$@"; do
            python3 tools/pmc_kernel.py "$(python3 -c "import glob,sys; print(glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True)[0])" $O/sqpmc_$a)" "$b" > $O/sqpmc_$a.txt; cat $O/sqpmc_$a.txt; rm -rf $O/sqpmc_$a ;;
     sens) run make_sens_$a 900 python -u tools/make_sens.py $a /tmp/synthetic_$a.sens
           run sens_$a 1100 python -u bench.py --sens /tmp/synthetic_$a.sens ${b//,/ }; summ $O/sens_$a.log ;;
+    trace) run trace_$a 600 rocprofv3 --kernel-trace -d $O/trace_$a -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${b//,/ }
+           f=$(python3 -c "import glob,sys; print(glob.glob(sys.argv[1] + '/**/*kernel_trace.csv', recursive=True)[0])" $O/trace_$a)
+           n=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]['roofline']['launches'])" $O/trace_$a.log)
+           python3 tools/stream_timeline.py $f $n > $O/timeline_$a.txt; python3 tools/overlap_attr.py $f $n >> $O/timeline_$a.txt
+           cat $O/timeline_$a.txt; rm -rf $O/trace_$a ;;
     py) run $a $b python -u ${c//,/ } ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
