@@ -204,9 +204,13 @@ __device__ __forceinline__ bool trilinear(const RayArgs& R, BlockCache& c, f3 po
     // made each load wait for the previous one; the sums below keep its order and its stop
     float vs[8], vw[8];
     uint32_t vc[8];
+    // corner 000 in a free block: the reference's first corner read has weight 0 and the sample ends
+    // there, so the other corners are not located (no probes in free space)
+    const BFVoxel* v0 = voxel_ptr(R, c, posDual + offs(0));
+    if (!v0) return false;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const BFVoxel* vp = voxel_ptr(R, c, posDual + offs(k));
+        const BFVoxel* vp = k == 0 ? v0 : voxel_ptr(R, c, posDual + offs(k));
         vs[k] = 0.0f; vw[k] = 0.0f; vc[k] = 0u;
         if (vp) {
             vs[k] = vp->sdf;

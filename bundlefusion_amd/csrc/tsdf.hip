@@ -356,7 +356,7 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
 // hold an in-band voxel): the screen footprint and its depth bounds are the whole block's (a superset
 // of each half's pixels: still conservative), the depth range is each half's own, from the corners at
 // z offsets 0, 3 and 4, 7 (only the depth row of the transform for the inner two levels).
-__device__ uint32_t block_may_update_halves(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx,
+__device__ __forceinline__ uint32_t block_may_update_halves(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx,
                                             int by, int bz, const float2* __restrict__ tiles,
                                             const float2* __restrict__ tiles2) {
     const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
@@ -1299,6 +1299,10 @@ constexpr uint32_t DC_DEPTH_KEY = 0xFF800000u;
 #ifndef BF_APPLY_QMASK
 #define BF_APPLY_QMASK 0
 #endif
+// k_compactify_ops' band cull: two (block, op) pairs per lane per round (1) or one (0)
+#ifndef BF_CULL_PAIRS2
+#define BF_CULL_PAIRS2 0
+#endif
 #if BF_APPLY_QMASK
 typedef uint4 OpMask;
 constexpr int MASK_PARTS = 4;
@@ -1420,6 +1424,23 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         qoff -= (uint32_t)__popc(fr);
         for (uint32_t m = fr; m; m &= m - 1) s_q[wv][qoff++] = (uint16_t)((lane << 5) | (uint32_t)__builtin_ctz(m));
         __syncthreads();
+#if BF_CULL_PAIRS2 && !BF_APPLY_QMASK
+        // two pairs per lane per round: their corner projections and tile loads are independent, so one
+        // pair's latency hides behind the other's (a wave walks ~21 rounds of dependent work otherwise)
+        for (uint32_t r = lane; r < qtot; r += 128) {
+            const bool two = r + 64 < qtot;
+            const uint32_t e0 = s_q[wv][r], e1 = s_q[wv][two ? r + 64 : r];
+            const uint32_t src0 = wv * 64 + (e0 >> 5), k0 = e0 & 31u, src1 = wv * 64 + (e1 >> 5), k1 = e1 & 31u;
+            const int4 b0 = s_bp[src0], b1 = s_bp[src1];
+            const uint32_t hb0 = block_may_update_halves(A, cam, op_mat(s_tinv[k0]), b0.x, b0.y, b0.z, s_tiles[0][k0], s_tiles[1][k0]);
+            const uint32_t hb1 = block_may_update_halves(A, cam, op_mat(s_tinv[k1]), b1.x, b1.y, b1.z, s_tiles[0][k1], s_tiles[1][k1]);
+#pragma unroll
+            for (int q = 0; q < MASK_PARTS; q++) {
+                if ((hb0 >> q) & 1u) atomicOr(&s_mask[q][src0], 1u << k0);
+                if (two && ((hb1 >> q) & 1u)) atomicOr(&s_mask[q][src1], 1u << k1);
+            }
+        }
+#else
         for (uint32_t r = lane; r < qtot; r += 64) {
             const uint32_t e = s_q[wv][r], src = wv * 64 + (e >> 5), k = e & 31u;
             const int4 b = s_bp[src];
@@ -1434,6 +1455,7 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             for (int q = 0; q < MASK_PARTS; q++)
                 if ((hb >> q) & 1u) atomicOr(&s_mask[q][src], 1u << k);
         }
+#endif
         __syncthreads();
 #if BF_APPLY_QMASK
         const OpMask hm = make_uint4(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x], s_mask[2][threadIdx.x], s_mask[3][threadIdx.x]);
