@@ -1098,6 +1098,11 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // proj_coord's per-lane bound (|qa| + 2 |t| + 2) 2^-21 for every lane with |t| <= max(W, H) + 2.
 // Lanes beyond that are off-screen for the fast and the exact quotient alike (their distance to the
 // screen exceeds the quotient error), so the pixel decision is the IEEE one everywhere.
+// dc rows padded with one zero pixel (pitch W + 1): the voxel pass clamps pixel coordinates into the pad
+// instead of testing them (BF_DC_PAD 0: pitch W, compare + select per pixel)
+#ifndef BF_DC_PAD
+#define BF_DC_PAD 1
+#endif
 __device__ __forceinline__ bool proj_needs_exact(float t, float epsc) { return !(fabsf(t - rintf(t)) > epsc); }
 // the rounding-step test of a voxel pair as one minimum over its four coordinates (BF_PROJ_MIN4 0: four tests)
 #ifndef BF_PROJ_MIN4
@@ -1282,11 +1287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 // test is then that one comparison, and the clamp of sdf to +-truncation (:458-462) is the identity
 // inside the band.
 constexpr uint32_t DC_DEPTH_KEY = 0xFF800000u;
-// dc rows padded with one zero pixel (pitch W + 1): the voxel pass clamps pixel coordinates into the pad
-// instead of testing them (BF_DC_PAD 0: pitch W, compare + select per pixel)
-#ifndef BF_DC_PAD
-#define BF_DC_PAD 1
-#endif
+
 // k_apply_ops's inner step and occupancy (overridable for A/B builds of kernel variants)
 #ifndef BF_APPLY_ZC
 #define BF_APPLY_ZC 4
