@@ -136,20 +136,39 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
     }
 }
 
-// getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417) with a one-entry per-thread block cache
+// getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417) with a two-entry per-thread block cache: a trilinear
+// sample's corners straddle a block face about a third of the time, and a one-entry cache re-probed the hash
+// as the corners alternated between the two blocks (up to six probes per sample instead of two)
 struct BlockCache {
-    int bx = INT_MIN, by = 0, bz = 0, ptr = BF_FREE_ENTRY;
+    int ax = INT_MIN, ay = 0, az = 0, ap = BF_FREE_ENTRY;  // entry A
+    int bx = INT_MIN, by = 0, bz = 0, bp = BF_FREE_ENTRY;  // entry B
+    bool replaceB = false;  // the entry a miss replaces (the one not used last)
     uint32_t samples = 0, loads = 0, probes = 0;  // render statistics (trilinear samples, voxel loads, hash probes)
+    __device__ __forceinline__ int lookup(const RayArgs& R, i3 b) {
+        if (b.x == ax && b.y == ay && b.z == az) {
+            replaceB = true;
+            return ap;
+        }
+        if (b.x == bx && b.y == by && b.z == bz) {
+            replaceB = false;
+            return bp;
+        }
+        const int p = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
+        probes++;
+        if (replaceB) {
+            bx = b.x; by = b.y; bz = b.z; bp = p;
+        } else {
+            ax = b.x; ay = b.y; az = b.z; ap = p;
+        }
+        replaceB = !replaceB;
+        return p;
+    }
 };
 __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 pos, float& sdf, float& weight, uint32_t& color) {
     const i3 v = world_to_vvox(pos, R.voxelSize);
     const i3 b = vvox_to_block(v);
-    if (b.x != c.bx || b.y != c.by || b.z != c.bz) {
-        c.bx = b.x; c.by = b.y; c.bz = b.z;
-        c.ptr = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
-        c.probes++;
-    }
-    if (c.ptr == BF_FREE_ENTRY) {  // deleteVoxel
+    const int ptr = c.lookup(R, b);
+    if (ptr == BF_FREE_ENTRY) {  // deleteVoxel
         sdf = 0.0f; weight = 0.0f; color = 0u;
         return;
     }
@@ -157,7 +176,7 @@ __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 po
     if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
     if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
     if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
-    const BFVoxel* vp = R.voxels + (size_t)c.ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+    const BFVoxel* vp = R.voxels + (size_t)ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
     c.loads++;
     sdf = vp->sdf;
     weight = vp->weight;
@@ -168,17 +187,13 @@ __device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 po
 __device__ __forceinline__ const BFVoxel* voxel_ptr(const RayArgs& R, BlockCache& c, f3 pos) {
     const i3 v = world_to_vvox(pos, R.voxelSize);
     const i3 b = vvox_to_block(v);
-    if (b.x != c.bx || b.y != c.by || b.z != c.bz) {
-        c.bx = b.x; c.by = b.y; c.bz = b.z;
-        c.ptr = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
-        c.probes++;
-    }
-    if (c.ptr == BF_FREE_ENTRY) return nullptr;
+    const int ptr = c.lookup(R, b);
+    if (ptr == BF_FREE_ENTRY) return nullptr;
     int lx = v.x % BF_SDF_BLOCK_SIZE, ly = v.y % BF_SDF_BLOCK_SIZE, lz = v.z % BF_SDF_BLOCK_SIZE;
     if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
     if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
     if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
-    return R.voxels + (size_t)c.ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+    return R.voxels + (size_t)ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
 }
 
 __device__ __forceinline__ float frac1(float v) { return v - floorf(v); }

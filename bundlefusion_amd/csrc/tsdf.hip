@@ -1098,16 +1098,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // proj_coord's per-lane bound (|qa| + 2 |t| + 2) 2^-21 for every lane with |t| <= max(W, H) + 2.
 // Lanes beyond that are off-screen for the fast and the exact quotient alike (their distance to the
 // screen exceeds the quotient error), so the pixel decision is the IEEE one everywhere.
-// dc rows padded with one zero pixel (pitch W + 1): the voxel pass clamps pixel coordinates into the pad
-// instead of testing them (BF_DC_PAD 0: pitch W, compare + select per pixel)
-#ifndef BF_DC_PAD
-#define BF_DC_PAD 1
-#endif
 __device__ __forceinline__ bool proj_needs_exact(float t, float epsc) { return !(fabsf(t - rintf(t)) > epsc); }
-// the rounding-step test of a voxel pair as one minimum over its four coordinates (BF_PROJ_MIN4 0: four tests)
-#ifndef BF_PROJ_MIN4
-#define BF_PROJ_MIN4 0
-#endif
 // b_r = e[4r] wx + e[4r+1] wy: the (x, y) part of every row, computed once per lane column and op.
 // Outputs the byte offsets of the two voxels' pixels in the op's {depth, colour} image, or
 // 0xFFFFFFFF off-screen (wc = 0 forces every pixel off-screen: an op without colour, :441-448);
@@ -1123,20 +1114,6 @@ __device__ __forceinline__ void voxel_pixel2b(const BFDepthCameraParams& cam, co
     const f2v qx = nx * rz, qy = ny * rz;
     f2v tx = (qx + f2v{cam.mx, cam.mx}) + f2v{0.5f, 0.5f};
     f2v ty = (qy + f2v{cam.my, cam.my}) + f2v{0.5f, 0.5f};
-#if BF_PROJ_MIN4
-    // the four distances to the nearest integer (packed subtractions), then one test of their minimum: a
-    // lane near a rounding step in any coordinate recomputes all four with the IEEE quotients
-    const f2v dx = tx - f2v{rintf(tx.x), rintf(tx.y)}, dy = ty - f2v{rintf(ty.x), rintf(ty.y)};
-    const float dmin = fminf(fminf(fabsf(dx.x), fabsf(dx.y)), fminf(fabsf(dy.x), fabsf(dy.y)));
-    const bool nearStep = !(dmin > epsc);
-    if (__builtin_amdgcn_ballot_w64(nearStep)) {  // ~1e-4 of lanes: the IEEE quotients
-        asm volatile("" ::: "memory");
-        if (nearStep) {
-            tx = f2v{(nx.x / p[2].x + cam.mx) + 0.5f, (nx.y / p[2].y + cam.mx) + 0.5f};
-            ty = f2v{(ny.x / p[2].x + cam.my) + 0.5f, (ny.y / p[2].y + cam.my) + 0.5f};
-        }
-    }
-#else
     const bool nx0 = proj_needs_exact(tx.x, epsc), nx1 = proj_needs_exact(tx.y, epsc);
     const bool ny0 = proj_needs_exact(ty.x, epsc), ny1 = proj_needs_exact(ty.y, epsc);
     if (__builtin_amdgcn_ballot_w64(nx0 | nx1 | ny0 | ny1)) {  // ~1e-4 of lanes: the IEEE quotients
@@ -1146,22 +1123,12 @@ __device__ __forceinline__ void voxel_pixel2b(const BFDepthCameraParams& cam, co
         if (ny0) ty.x = (ny.x / p[2].x + cam.my) + 0.5f;
         if (ny1) ty.y = (ny.y / p[2].y + cam.my) + 0.5f;
     }
-#endif
     const uint32_t ux0 = (uint32_t)f2i(tx.x), ux1 = (uint32_t)f2i(tx.y);
     const uint32_t uy0 = (uint32_t)f2i(ty.x), uy1 = (uint32_t)f2i(ty.y);
-    pz = p[2];
-#if BF_DC_PAD
-    // the dc image has a zero column x = W and ends after row H - 1: an unsigned clamp of each coordinate
-    // (negative ints are huge) sends every off-screen pixel to a zero word, without a compare or branch
-    // (an op without colour has an empty buffer range instead, so wc is unused)
-    const uint32_t P8 = (cam.imageWidth + 1u) * 8u;
-    off0 = __umul24(min(uy0, cam.imageHeight), P8) + (min(ux0, cam.imageWidth) << 3);
-    off1 = __umul24(min(uy1, cam.imageHeight), P8) + (min(ux1, cam.imageWidth) << 3);
-#else
     const uint32_t W8 = cam.imageWidth * 8u;
+    pz = p[2];
     off0 = ((ux0 < wc) & (uy0 < cam.imageHeight)) ? __umul24(uy0, W8) + (ux0 << 3) : 0xFFFFFFFFu;
     off1 = ((ux1 < wc) & (uy1 < cam.imageHeight)) ? __umul24(uy1, W8) + (ux1 << 3) : 0xFFFFFFFFu;
-#endif
 }
 
 // Band test of one voxel for one pose (CUDASceneRepHashSDF.cu:449-466): sdf clamped to +-truncation.
@@ -1300,10 +1267,6 @@ constexpr uint32_t DC_DEPTH_KEY = 0xFF800000u;
 #ifndef BF_APPLY_QMASK
 #define BF_APPLY_QMASK 0
 #endif
-// k_compactify_ops' band cull: two (block, op) pairs per lane per round (1) or one (0)
-#ifndef BF_CULL_PAIRS2
-#define BF_CULL_PAIRS2 0
-#endif
 #if BF_APPLY_QMASK
 typedef uint4 OpMask;
 constexpr int MASK_PARTS = 4;
@@ -1311,7 +1274,6 @@ constexpr int MASK_PARTS = 4;
 typedef uint2 OpMask;
 constexpr int MASK_PARTS = 2;
 #endif
-__host__ __device__ __forceinline__ uint32_t dc_pixels(uint32_t W, uint32_t H) { return BF_DC_PAD ? (W + 1u) * H : W * H; }
 __device__ __forceinline__ uint32_t dc_depth_word(float d, float maxDist) {
     return (d != -INFINITY && d < maxDist) ? (__float_as_uint(d) ^ DC_DEPTH_KEY) : 0u;
 }
@@ -1319,22 +1281,12 @@ __device__ __forceinline__ uint32_t dc_depth_word(float d, float maxDist) {
 // per-op interleaved {depth, colour} image: the voxel pass gathers both values of a pixel with one
 // dwordx2 load from one cache line (two dword gathers from two images before). Ops without colour
 // never gather (their pixels are off-screen to integrateDepthMapKernel, :441-448).
-__device__ __forceinline__ void pack_dc(const OpTable& ops, uint32_t k, uint32_t i0, uint32_t stride, uint32_t W, uint32_t P,
-                                        float maxDist) {
+__device__ __forceinline__ void pack_dc(const OpTable& ops, uint32_t k, uint32_t i0, uint32_t stride, uint32_t P, float maxDist) {
     if (ops.color[k] == nullptr) return;
     const float* __restrict__ d = ops.depth[k];
     const uint32_t* __restrict__ c = ops.color[k];
     uint2* __restrict__ o = ops.dc[k];
-#if BF_DC_PAD
-    // P = (W + 1) H dc pixels; x = W is the zero pad
-    for (uint32_t i = i0; i < P; i += stride) {
-        const uint32_t y = i / (W + 1u), x = i - y * (W + 1u);
-        const uint32_t j = y * W + x;
-        o[i] = x < W ? make_uint2(dc_depth_word(d[j], maxDist), c[j]) : make_uint2(0u, 0u);
-    }
-#else
     for (uint32_t i = i0; i < P; i += stride) o[i] = make_uint2(dc_depth_word(d[i], maxDist), c[i]);
-#endif
 }
 // per-op 8x8-tile depth bounds and dc image (blockIdx.y = op; workgroups [0, tileBlocks) build the
 // tiles, the rest the dc image) + the per-batch counter reset (ops whose frame already has both,
@@ -1354,8 +1306,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
     if (blockIdx.y >= ops.nTile) return;  // a batch whose frames are all cached launches one workgroup
     const uint32_t k = ops.tileIdx[blockIdx.y];
     if (blockIdx.x >= tileBlocks) {
-        pack_dc(ops, k, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W,
-                dc_pixels(W, H), maxDist);
+        pack_dc(ops, k, (blockIdx.x - tileBlocks) * blockDim.x + threadIdx.x, (gridDim.x - tileBlocks) * blockDim.x, W * H, maxDist);
         return;
     }
     depth_tile_wave((blockIdx.x * blockDim.x + threadIdx.x) >> 6, ops.depth[k], W, H, tilesW, tilesH, tiles2W, tiles2H,
@@ -1425,23 +1376,6 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         qoff -= (uint32_t)__popc(fr);
         for (uint32_t m = fr; m; m &= m - 1) s_q[wv][qoff++] = (uint16_t)((lane << 5) | (uint32_t)__builtin_ctz(m));
         __syncthreads();
-#if BF_CULL_PAIRS2 && !BF_APPLY_QMASK
-        // two pairs per lane per round: their corner projections and tile loads are independent, so one
-        // pair's latency hides behind the other's (a wave walks ~21 rounds of dependent work otherwise)
-        for (uint32_t r = lane; r < qtot; r += 128) {
-            const bool two = r + 64 < qtot;
-            const uint32_t e0 = s_q[wv][r], e1 = s_q[wv][two ? r + 64 : r];
-            const uint32_t src0 = wv * 64 + (e0 >> 5), k0 = e0 & 31u, src1 = wv * 64 + (e1 >> 5), k1 = e1 & 31u;
-            const int4 b0 = s_bp[src0], b1 = s_bp[src1];
-            const uint32_t hb0 = block_may_update_halves(A, cam, op_mat(s_tinv[k0]), b0.x, b0.y, b0.z, s_tiles[0][k0], s_tiles[1][k0]);
-            const uint32_t hb1 = block_may_update_halves(A, cam, op_mat(s_tinv[k1]), b1.x, b1.y, b1.z, s_tiles[0][k1], s_tiles[1][k1]);
-#pragma unroll
-            for (int q = 0; q < MASK_PARTS; q++) {
-                if ((hb0 >> q) & 1u) atomicOr(&s_mask[q][src0], 1u << k0);
-                if (two && ((hb1 >> q) & 1u)) atomicOr(&s_mask[q][src1], 1u << k1);
-            }
-        }
-#else
         for (uint32_t r = lane; r < qtot; r += 64) {
             const uint32_t e = s_q[wv][r], src = wv * 64 + (e >> 5), k = e & 31u;
             const int4 b = s_bp[src];
@@ -1456,7 +1390,6 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
             for (int q = 0; q < MASK_PARTS; q++)
                 if ((hb >> q) & 1u) atomicOr(&s_mask[q][src], 1u << k);
         }
-#endif
         __syncthreads();
 #if BF_APPLY_QMASK
         const OpMask hm = make_uint4(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x], s_mask[2][threadIdx.x], s_mask[3][threadIdx.x]);
@@ -1706,11 +1639,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const float bxy[3] = {Ti.m[0] * wx + Ti.m[1] * wy, Ti.m[4] * wx + Ti.m[5] * wy, Ti.m[8] * wx + Ti.m[9] * wy};
                 // the op's {depth, colour} image through a buffer descriptor: 32-bit offsets, and an
                 // off-screen lane's out-of-range offset reads 0 without a branch
-#if BF_DC_PAD
-                const int dcBytes = ops.color[k] != nullptr ? (int)(dc_pixels(cam.imageWidth, cam.imageHeight) * 8u) : 0;
-#else
                 const int dcBytes = (int)(cam.imageWidth * cam.imageHeight * 8u);
-#endif
                 const __amdgpu_buffer_rsrc_t dcRsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ops.dc[k], (short)0, dcBytes, 0x00020000);
                 const uint32_t wc = ops.color[k] != nullptr ? cam.imageWidth : 0u;
 #ifdef BF_APPLY_DIAG
@@ -2128,7 +2057,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     const uint32_t tw = div_up(cam.imageWidth, DEPTH_TILE), th = div_up(cam.imageHeight, DEPTH_TILE);
     const uint32_t tw2 = div_up(cam.imageWidth, DEPTH_TILE2), th2 = div_up(cam.imageHeight, DEPTH_TILE2);
     ensureTiles(tw * th * kMaxOps, tw2 * th2 * kMaxOps);
-    const size_t P = dc_pixels(cam.imageWidth, cam.imageHeight);  // dc image pixels (padded rows)
+    const size_t P = (size_t)cam.imageWidth * cam.imageHeight;
     bool needScratch = false;
     for (uint32_t k = 0; k < n; k++) needScratch |= ops[k].tiles == nullptr;
     if (needScratch && dcCap_ < P * kMaxOps) {
@@ -2205,7 +2134,7 @@ void Scene::garbageCollect() {
     BF_LAUNCH_CHECK();
 }
 
-size_t Scene::dcCount(const BFDepthCameraParams& cam) { return dc_pixels(cam.imageWidth, cam.imageHeight); }
+size_t Scene::dcCount(const BFDepthCameraParams& cam) { return (size_t)cam.imageWidth * cam.imageHeight; }
 
 size_t Scene::tileCount(const BFDepthCameraParams& cam) {
     return (size_t)div_up(cam.imageWidth, DEPTH_TILE) * div_up(cam.imageHeight, DEPTH_TILE) +
