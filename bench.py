@@ -640,6 +640,9 @@ def main():
     t_end = time.perf_counter()
     end = rc.end_sequence(30)
     t_end = time.perf_counter() - t_end
+    # the end phase's re-integration batches run k_apply_ops after the timed region: trace / PMC tools take
+    # the timed region's dispatches as the `launches` before the last `launches_after` ones
+    launches_after = rc.stats()["reintegrateLaunches"] - st["reintegrateLaunches"]
     dres = end["last"]
     dense_end = {"ms": end["denseSolveMs"], "keyframes": K - 1, "dense_pairs": dres["numDensePairs"],
                  "gn_iters": dres["gnIterations"], "pcg_iters": dres["pcgIterations"],
@@ -688,7 +691,8 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "traffic_units": traffic_units,
                      "hbm_frac_counters": (traffic / per_launch_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                     "launches": launches, "avg_launch_us": per_launch_s * 1e6, "pass_rev": APPLY_PASS_REV,
+                     "launches": launches, "launches_after": launches_after,
+                     "avg_launch_us": per_launch_s * 1e6, "pass_rev": APPLY_PASS_REV,
                      "alg_bytes_per_launch": pass_bytes / launches,
                      "alg_bytes_source": "the fused pass's own bytes: 20 B per work-list block + 12 B per voxel of each "
                                          "block z-half loaded (256 voxels; halves no op reaches are skipped) + 12 B per "

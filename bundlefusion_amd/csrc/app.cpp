@@ -440,6 +440,8 @@ bool App::step() {
     // copies) is queued on pre_ behind them; the pinned slot is released at the next step
     BF_HIP(hipEventRecord(uploadEv_, pre_));
     uploaded_ = (int64_t)f;
+    // the frame-store images are written on pre_: the loop's scene stream waits for them
+    recon_->inputsProduced(f, pre_);
     const double t2 = now_s();
     tm_.uploadSeconds += t2 - t1;
     tm_.uploadBytes += (double)(dp * 2 + dRgbx_.n);

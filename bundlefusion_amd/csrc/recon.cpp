@@ -341,14 +341,28 @@ void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
     log_.push_back(e);
 }
 
-// reintegrate() (DepthSensing.cpp:854-902). The frame's fixes are applied as one op batch
-// (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls).
+// frame f's images were produced on stream s (preprocessing): the scene stream waits for that in the batch
+// that first reads them (awaitPreproc)
+void Recon::recordInputs(uint32_t f, hipStream_t s) {
+    hipEvent_t& e = preEv_[f & 1];
+    if (!e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    BF_HIP(hipEventRecord(e, s));
+    prePending_[f & 1] = true;
+}
+
+void Recon::inputsProduced(uint32_t f, hipStream_t s) {
+    BF_REQUIRE(f < opt_.maxFrames, BF_ERR_CAPACITY, "frame index beyond maxFrames");
+    recordInputs(f, s);
+}
+
 void Recon::awaitPreproc(uint32_t f) {
     if (!prePending_[f & 1]) return;
     BF_HIP(hipStreamWaitEvent(sceneStream_, preEv_[f & 1], 0));
     prePending_[f & 1] = false;
 }
 
+// reintegrate() (DepthSensing.cpp:854-902). The frame's fixes are applied as one op batch
+// (Scene::applyOps: voxel results equal the sequential deIntegrate / integrate calls).
 void Recon::runReintegrate() {
     // the batch integrates the previous frame (pendingOp_): it reads that frame's preprocessed images
     if (pendingInt_ && numFrames_ > 0) awaitPreproc(numFrames_ - 1);
@@ -1046,8 +1060,7 @@ void Recon::preprocessFrame(uint32_t f) {
     // the scene stream first reads frame f in the batch of frame f + 1 (its integration is deferred,
     // pendingOp_), so it waits there (awaitPreproc), not here: frame f's preprocessing overlaps the
     // voxel pass of frame f's batch
-    BF_HIP(hipEventRecord(preEv_[f & 1], ps));
-    prePending_[f & 1] = true;
+    recordInputs(f, ps);
 #ifdef BF_PRE_EARLY_WAIT  // A/B build: the scene stream waits right away (the first form)
     awaitPreproc(f);
 #endif

@@ -62,6 +62,9 @@ public:
     // per-frame CUDACache::storeFrame inside processFrame (OnlineBundler.cpp:199-204); c is borrowed
     void attachCache(Cache* c);
     void setFrameSource(uint32_t f, const float* depth, const uint8_t* color, uint32_t colorW, uint32_t colorH);
+    // frame f's frame-store images are being produced on stream s (the FriedLiver app's input stream): the
+    // scene stream waits for that before the batch that first reads them
+    void inputsProduced(uint32_t f, hipStream_t s);
     // CUDAImageManager::process inside the loop: frame f's raw sensor images are preprocessed into its
     // frame-store slot when it is processed (the cache then reads the raw sensor depth and colour)
     void attachPreproc(Preproc* p);
@@ -241,6 +244,7 @@ private:
     Preproc* preproc_ = nullptr;        // attached input preprocessing (borrowed)
     hipEvent_t preEv_[2] = {nullptr, nullptr};  // preprocessing of frames of each parity, on its stream
     bool prePending_[2] = {false, false};        // recorded and not yet awaited by the scene stream
+    void recordInputs(uint32_t f, hipStream_t s);
     void awaitPreproc(uint32_t f);               // the scene stream after frame f's preprocessing
     void storeCacheFrame(uint32_t f);
     void preprocessFrame(uint32_t f);

@@ -8,6 +8,7 @@
 #   bench:NAME[:ARGS]      python bench.py --no-cpu-baseline ARGS            -> bench_NAME.json
 #   fullbench:NAME[:ARGS]  python bench.py ARGS (with the CPU baseline)      -> bench_NAME.json
 #   ab:LIB:NAME[:ARGS]     the bench with BF_HIP_LIB=bundlefusion_amd/libbf_hip_LIB.so (a variant build)
+#   envbench:NAME:VAR=VAL[:ARGS]  the bench with one environment setting (runtime A/B switches)
 #   profile:NAME[:ARGS]    tools/profile_bench.sh TAG/NAME ARGS (kernel stats + FETCH/WRITE/VALU passes)
 #   sqpmc:NAME:KERNEL:CNT[:ARGS]  one --pmc pass of counters CNT (',' separated) over KERNEL's dispatches
 #   sens:N[:ARGS]          write an N-frame synthetic .sens (tools/make_sens.py), then bench.py --sens ARGS
@@ -51,6 +52,7 @@ for step in "$@"; do
     bench) run bench_$a 900 python -u bench.py --no-cpu-baseline ${b//,/ }; cp $O/bench_$a.log $O/bench_$a.json; summ $O/bench_$a.json ;;
     fullbench) run bench_$a 900 python -u bench.py ${b//,/ }; cp $O/bench_$a.log $O/bench_$a.json; summ $O/bench_$a.json ;;
     ab) BF_HIP_LIB=bundlefusion_amd/libbf_hip_$a.so run bench_$b 900 python -u bench.py --no-cpu-baseline ${c//,/ }; summ $O/bench_$b.log ;;
+    envbench) export "$b"; run bench_$a 900 python -u bench.py --no-cpu-baseline ${c//,/ }; unset "${b%%=*}"; summ $O/bench_$a.log ;;
     profile) run profile_$a 1100 bash tools/profile_bench.sh $TAG/$a ${b//,/ } ;;
     sqpmc) run sqpmc_$a 300 rocprofv3 --pmc ${c//,/ } --kernel-include-regex "$b" -d $O/sqpmc_$a -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${d//,/ }
            python3 tools/pmc_kernel.py "$(python3 -c "import glob,sys; print(glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True)[0])" $O/sqpmc_$a)" "$b" > $O/sqpmc_$a.txt; cat $O/sqpmc_$a.txt; rm -rf $O/sqpmc_$a ;;
@@ -58,8 +60,9 @@ for step in "$@"; do
           run sens_$a 1100 python -u bench.py --sens /tmp/synthetic_$a.sens ${b//,/ }; summ $O/sens_$a.log ;;
     trace) run trace_$a 600 rocprofv3 --kernel-trace -d $O/trace_$a -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${b//,/ }
            f=$(python3 -c "import glob,sys; print(glob.glob(sys.argv[1] + '/**/*kernel_trace.csv', recursive=True)[0])" $O/trace_$a)
-           n=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]['roofline']['launches'])" $O/trace_$a.log)
-           python3 tools/stream_timeline.py $f $n > $O/timeline_$a.txt; python3 tools/overlap_attr.py $f $n >> $O/timeline_$a.txt
+           grep '^{"metric' $O/trace_$a.log | tail -1 > $O/trace_$a.json
+           python3 tools/stream_timeline.py $f $O/trace_$a.json > $O/timeline_$a.txt; python3 tools/overlap_attr.py $f $O/trace_$a.json >> $O/timeline_$a.txt
+           python3 tools/trace_tail.py $f $O/trace_$a.json $O/trace_tail_$a.csv.gz
            cat $O/timeline_$a.txt; rm -rf $O/trace_$a ;;
     py) run $a $b python -u ${c//,/ } ;;
     *) echo "unknown step $kind"; exit 2 ;;

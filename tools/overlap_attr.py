@@ -2,16 +2,23 @@
 of the bench's timed region (the last `frames` of them), the mean trace interval, the mean part of it
 that overlaps a k_apply_ops dispatch, and the remainder. A kernel whose interval is mostly covered by
 the voxel pass is waiting for CU slots the pass holds (its own work is its standalone time).
-Usage: overlap_attr.py KERNEL_TRACE.csv FRAMES [kernel substrings...]"""
+The timed region comes from the bench line (tools/timed_region.py).
+Usage: overlap_attr.py KERNEL_TRACE.csv BENCH.json [kernel substrings...]"""
 import bisect
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from timed_region import bench_counts, region_bounds  # noqa: E402
 
 
 def main():
-    path, frames = sys.argv[1], int(sys.argv[2])
+    path = sys.argv[1]
+    frames, after = bench_counts(sys.argv[2])
     names = sys.argv[3:] or ["k_cache_geometry", "k_cache_intensity", "k_gauss", "k_erode"]
     rows = list(csv.DictReader(open(path)))
+    t0, t1 = region_bounds(rows, frames, after)
     iv = lambda r: (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))  # noqa: E731
     apply = sorted(iv(r) for r in rows if "k_apply_ops" in r["Kernel_Name"])
     starts = [a for a, _ in apply]
@@ -28,8 +35,7 @@ def main():
 
     for n in names:
         d = sorted((iv(r) for r in rows if n in r["Kernel_Name"]), key=lambda x: x[0])
-        per = 2 if n == "k_erode" else 1
-        d = d[-frames * per:]
+        d = [x for x in d if t0 <= x[0] <= t1]
         if not d:
             print(f"{n}: no dispatches")
             continue

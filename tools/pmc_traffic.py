@@ -5,11 +5,17 @@ Optionally a third pass (SQ_INSTS_VALU, wave-level VALU instructions) gives the 
 With --bench JSON (the bench line the profiled command printed), only the last
 roofline.launches dispatches (bench.py's timed region) are averaged and the bench's
 config.workload is recorded, so bench.py uses the figures only for that same workload.
+With the bench JSON, the timed region is roofline.launches dispatches before the end phase's
+roofline.launches_after (tools/timed_region.py).
 Usage: pmc_traffic.py FETCH.csv WRITE.csv KERNEL_REGEX OUT.json [VALU.csv] [--bench BENCH.json]"""
 import csv
 import json
+import os
 import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from timed_region import window  # noqa: E402
 from collections import defaultdict
 
 
@@ -32,10 +38,11 @@ def main():
     fetch_csv, write_csv, kernel, out = argv[:4]
     rx = re.compile(kernel)
     last = int(bench["roofline"]["launches"]) if bench else 0
+    after = int(bench["roofline"].get("launches_after", 0)) if bench else 0
     f = per_dispatch(fetch_csv, "FETCH_SIZE", rx)
     w = per_dispatch(write_csv, "WRITE_SIZE", rx)
     if last:
-        f, w = f[-last:], w[-last:]
+        f, w = window(f, last, after), window(w, last, after)
     fetch_b = 2.0 * 1024.0 * sum(f) / max(1, len(f))
     write_b = 1024.0 * sum(w) / max(1, len(w))
     res = {"kernel": kernel, "dispatches_fetch": len(f), "dispatches_write": len(w),
@@ -45,7 +52,7 @@ def main():
     if bench:
         res["workload"] = bench["config"]["workload"]
         res["pass_rev"] = bench["roofline"].get("pass_rev")
-        res["averaged_over"] = f"last {last} dispatches (the bench's timed region)"
+        res["averaged_over"] = f"{last} dispatches before the end phase's last {after} (the bench's timed region)"
         # per-unit rates (bench.py scales them by its own run's counts): fetched bytes per voxel-op
         # evaluation (the gathers and the voxel reads both grow with it), written bytes per voxel
         # read + written, VALU wave-instructions per evaluation
@@ -58,7 +65,7 @@ def main():
     if len(argv) > 4:
         v = per_dispatch(argv[4], "SQ_INSTS_VALU", rx)
         if last:
-            v = v[-last:]
+            v = window(v, last, after)
         res["dispatches_valu"] = len(v)
         res["valu_insts_per_launch"] = sum(v) / max(1, len(v))
         if bench:

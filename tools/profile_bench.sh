@@ -16,14 +16,17 @@ python3 tools/prof_summary.py $OUT/stats/run_kernel_stats.csv > $OUT/kernel_stat
 # the bench line's avg_launch_us (HIP events) must agree with; the stats csv averages the whole stream
 python3 - $OUT/stats/run_kernel_trace.csv $OUT/stats_bench.json > $OUT/apply_timed_region.txt <<'PY'
 import csv, json, sys
+sys.path.insert(0, "tools")
+from timed_region import bench_counts, window
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-n = int(d["roofline"]["launches"])
+n, after = bench_counts(sys.argv[2])
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_apply_ops" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-last = rows[-n:]
+last = window(rows, n, after)
 us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
-print("k_apply_ops over the timed region (last %d of %d dispatches): avg %.1f us (rocprofv3 kernel trace); "
-      "the profiled bench line's HIP-event average %.1f us" % (len(us), len(rows), sum(us) / max(1, len(us)), d["roofline"]["avg_launch_us"]))
+print("k_apply_ops over the timed region (%d of %d dispatches, before the end phase's %d): avg %.1f us (rocprofv3 kernel "
+      "trace); the profiled bench line's HIP-event average %.1f us" % (len(us), len(rows), after, sum(us) / max(1, len(us)),
+                                                                       d["roofline"]["avg_launch_us"]))
 PY
 cat $OUT/apply_timed_region.txt
 rm -f $OUT/stats/run_kernel_trace.csv  # per-dispatch rows are large; the stats csv is what we keep
