@@ -16,6 +16,7 @@
 //  * computeNormals from the camera-space points (or the SDF gradient when useGradients).
 #include "hash_dev.h"
 #include "tsdf.h"
+#include <cstdlib>
 
 #include <cstring>
 
@@ -349,11 +350,17 @@ __device__ __forceinline__ void render_pixel(const RayArgs& R, const BFRayCastPa
     }
 }
 // stats: [RS_SAMPLES] trilinear samples, [RS_LOADS] voxel loads, [RS_PROBES] hash probes, [RS_RAYS] marched rays
-__global__ __launch_bounds__(256) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
+// Pixel shape: each wave marches an 8x8 pixel square (neighbouring rays cross the same blocks and end at
+// similar depths); TPB 256: a workgroup is a 16x16 tile of four such squares, TPB 64: one square per
+// workgroup, so a slot frees as soon as its one wave ends (A/B, BF_RENDER_TPB)
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
                                                 const uint32_t* __restrict__ smax, float* d_depth, float4* d_depth4,
                                                 float4* d_normals, float4* d_colors, float* outMin, float* outMax,
                                                 unsigned long long* stats) {
-    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    constexpr uint32_t TILE = TPB == 256 ? 16u : 8u;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * TILE + (wv & 1u) * 8u + (lane & 7u), y = blockIdx.y * TILE + (wv >> 1) * 8u + (lane >> 3);
     BlockCache cache;
     bool rayed = false;
     if (x < rp.width && y < rp.height)
@@ -436,9 +443,17 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
     R.maxList = cfg_.hp.hashMaxCollisionLinkedListSize;
     R.voxelSize = cfg_.hp.virtualVoxelSize;
     const dim3 g(div_up(rp.width, 16), div_up(rp.height, 16));
+    static const int tpb = [] {
+        const char* e = std::getenv("BF_RENDER_TPB");
+        return e && std::atoi(e) == 64 ? 64 : 256;
+    }();
     if (timed) renderClock_.start(stream_);
-    k_render<<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
-                                     renderStats_.p);
+    if (tpb == 64)
+        k_render<64><<<dim3(div_up(rp.width, 8), div_up(rp.height, 8)), 64, 0, stream_>>>(
+            R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax, renderStats_.p);
+    else
+        k_render<256><<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
+                                              renderStats_.p);
     BF_LAUNCH_CHECK();
     if (timed) renderClock_.stop(stream_);
     if (!rp.useGradients) {

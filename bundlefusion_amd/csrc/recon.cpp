@@ -248,6 +248,7 @@ void Recon::setFrame(uint32_t f, const float* depth, const uint8_t* color, const
     r.Tinc = Tinc;
     r.set = true;
     r.tilesReady = false;
+    r.pre = false;  // a new frame-store slot: its preprocessing (if any) is still to run
 }
 
 VoxelOp Recon::frameOp(uint32_t f, const BFMat4& T, bool deint) {
@@ -344,10 +345,10 @@ void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
 // frame f's images were produced on stream s (preprocessing): the scene stream waits for that in the batch
 // that first reads them (awaitPreproc)
 void Recon::recordInputs(uint32_t f, hipStream_t s) {
-    hipEvent_t& e = preEv_[f & 1];
+    hipEvent_t& e = preEv_[f % kPreSlots];
     if (!e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     BF_HIP(hipEventRecord(e, s));
-    prePending_[f & 1] = true;
+    prePending_[f % kPreSlots] = true;
 }
 
 void Recon::inputsProduced(uint32_t f, hipStream_t s) {
@@ -356,9 +357,9 @@ void Recon::inputsProduced(uint32_t f, hipStream_t s) {
 }
 
 void Recon::awaitPreproc(uint32_t f) {
-    if (!prePending_[f & 1]) return;
-    BF_HIP(hipStreamWaitEvent(sceneStream_, preEv_[f & 1], 0));
-    prePending_[f & 1] = false;
+    if (!prePending_[f % kPreSlots]) return;
+    BF_HIP(hipStreamWaitEvent(sceneStream_, preEv_[f % kPreSlots], 0));
+    prePending_[f % kPreSlots] = false;
 }
 
 // reintegrate() (DepthSensing.cpp:854-902). The frame's fixes are applied as one op batch
@@ -423,7 +424,7 @@ void Recon::processFrame(uint32_t f) {
     HostTimer allT(HS_ALL);
     g_hostFrames++;
 #endif
-    if (preproc_ && frames_[f].rawDepth) {
+    if (preproc_ && frames_[f].rawDepth && !frames_[f].pre) {
         BF_HOST_T(HS_PRE);
         preprocessFrame(f);
     }
@@ -432,6 +433,14 @@ void Recon::processFrame(uint32_t f) {
     if (cache_) {
         BF_HOST_T(HS_CACHE);
         storeCacheFrame(f);
+    }
+    // the next frame's preprocessing, issued now rather than when the loop reaches it: the host may block
+    // below on a bundling result, and the scene stream would then reach the batch that reads frame f + 1
+    // (frame f + 2's) before its input work had even been queued (the frame store slot and the raw buffer
+    // of parity f + 1 are free: frame f - 1's cache store is ordered before it, preprocessFrame)
+    if (preproc_ && f + 1 < opt_.maxFrames && frames_[f + 1].rawDepth && frames_[f + 1].set && !frames_[f + 1].pre) {
+        BF_HOST_T(HS_PRE);
+        preprocessFrame(f + 1);
     }
     {
         BF_HOST_T(HS_PENDING);
@@ -1042,6 +1051,7 @@ void Recon::setFrameRaw(uint32_t f, const uint16_t* depthU16, const uint8_t* rgb
     BF_REQUIRE(f < opt_.maxFrames, BF_ERR_CAPACITY, "frame index beyond maxFrames");
     frames_[f].rawDepth = depthU16;
     frames_[f].rawColor = rgbx;
+    frames_[f].pre = false;
 }
 
 void Recon::preprocessFrame(uint32_t f) {
@@ -1061,6 +1071,7 @@ void Recon::preprocessFrame(uint32_t f) {
     // pendingOp_), so it waits there (awaitPreproc), not here: frame f's preprocessing overlaps the
     // voxel pass of frame f's batch
     recordInputs(f, ps);
+    fr.pre = true;
 #ifdef BF_PRE_EARLY_WAIT  // A/B build: the scene stream waits right away (the first form)
     awaitPreproc(f);
 #endif
@@ -1074,7 +1085,8 @@ void Recon::preprocessFrame(uint32_t f) {
 // Bundler::storeCachedFrame (Bundler.cpp:278-281) for frame f, on the cache's stream
 void Recon::storeCacheFrame(uint32_t f) {
     FrameRef& fr = frames_[f];
-    if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream()) BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_[f & 1], 0));
+    if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream())
+        BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_[f % kPreSlots], 0));
     BF_REQUIRE(cache_->numFrames() == f, BF_ERR_STATE, "attached cache must hold exactly the frames before this one");
     // multi-GPU: a rank solves only its own local submaps (round-robin, issueSubmap), so it builds the cache
     // frames of those and the keyframes (the dense end solve runs on every rank); other slots stay empty

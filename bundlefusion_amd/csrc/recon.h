@@ -146,6 +146,7 @@ private:
         const uint8_t* srcColor = nullptr;
         uint32_t srcW = 0, srcH = 0;
         const uint16_t* rawDepth = nullptr;  // sensor images preprocessed into depth / color (attachPreproc)
+        bool pre = false;                    // preprocessed (the loop runs frame f + 1's ahead, at frame f)
         const uint8_t* rawColor = nullptr;
         bool set = false;
         bool tilesReady = false;  // its band-cull depth tiles and dc image are in frameTiles_ / frameDC_
@@ -242,8 +243,11 @@ private:
     hipEvent_t cacheEv_ = nullptr;      // the last storeFrame on the cache's stream (one of cacheEvF_)
     hipEvent_t cacheEvF_[2] = {nullptr, nullptr};  // frame f's storeFrame: cacheEvF_[f & 1]
     Preproc* preproc_ = nullptr;        // attached input preprocessing (borrowed)
-    hipEvent_t preEv_[2] = {nullptr, nullptr};  // preprocessing of frames of each parity, on its stream
-    bool prePending_[2] = {false, false};        // recorded and not yet awaited by the scene stream
+    // a frame's input production (preprocessing, or the app's input stream) on its stream, per frame f & 3: frame
+    // f + 1 is preprocessed ahead while frame f - 1's record still awaits its batch
+    static constexpr uint32_t kPreSlots = 4;
+    hipEvent_t preEv_[kPreSlots] = {nullptr, nullptr, nullptr, nullptr};
+    bool prePending_[kPreSlots] = {false, false, false, false};  // recorded and not yet awaited by the scene stream
     void recordInputs(uint32_t f, hipStream_t s);
     void awaitPreproc(uint32_t f);               // the scene stream after frame f's preprocessing
     void storeCacheFrame(uint32_t f);

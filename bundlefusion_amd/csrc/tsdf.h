@@ -174,7 +174,7 @@ private:
     DevBuf<uint8_t> candOp_;       // per alloc candidate of a batch: the integrate op that emitted it
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
-    unsigned applyGrid_ = 0;
+    unsigned applyGrid_ = 0, compactifyGrid_ = 0;
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;
 };

@@ -1255,6 +1255,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 // inside the band.
 constexpr uint32_t DC_DEPTH_KEY = 0xFF800000u;
 
+// k_apply_ops's grid: rounds of resident workgroups (Scene::Scene)
+constexpr int kApplyRounds = 4;
 // k_apply_ops's inner step and occupancy (overridable for A/B builds of kernel variants)
 #ifndef BF_APPLY_ZC
 #define BF_APPLY_ZC 4
@@ -1917,7 +1919,18 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     // sharded: one workgroup slot per CU stays free for the bundling streams' launches (Recon::Recon)
     int freeSlots = cfg_.shardCount > 1 ? 1 : 0;
     if (const char* e = std::getenv("BF_APPLY_FREE_SLOTS")) freeSlots = std::atoi(e);  // A/B measurements
-    applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_;
+    // The grid is kApplyRounds rounds of resident workgroups, each wave a 1/kApplyRounds share of the strided
+    // list: the dispatcher hands the later rounds' workgroups to the slots the earlier ones free, so the waves
+    // that drew costly blocks no longer set the pass's end (one resident round: 537 us per launch at the
+    // bench workload; 2 / 4 / 8 rounds: 495 / 480 / 505 us, profiles/r10_apply_rounds_ab.txt), and other
+    // streams' kernels find free slots at every round's end instead of the pass's. BF_APPLY_GRID_MULT: A/B.
+    int mult = kApplyRounds;
+    if (const char* e = std::getenv("BF_APPLY_GRID_MULT")) mult = std::max(1, std::atoi(e));
+    applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_ * (unsigned)mult;
+    // the batch scan: 4 workgroups per CU (its occupancy), BF_COMPACTIFY_GRID_MULT rounds of them (A/B)
+    int cmult = 1;
+    if (const char* e = std::getenv("BF_COMPACTIFY_GRID_MULT")) cmult = std::max(1, std::atoi(e));
+    compactifyGrid_ = (unsigned)numCUs_ * 4u * (unsigned)cmult;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
@@ -2109,7 +2122,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     A.tilesH = th;
     A.tiles2 = tiles2_.p;
     A.tiles2W = tw2;
-    k_compactify_ops<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
+    k_compactify_ops<<<compactifyGrid_, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
                                                                   reinterpret_cast<OpMask*>(blockMask_.p), blockBirth_.p, epoch, B_);
     BF_LAUNCH_CHECK();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

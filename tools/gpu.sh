@@ -8,7 +8,8 @@
 #   bench:NAME[:ARGS]      python bench.py --no-cpu-baseline ARGS            -> bench_NAME.json
 #   fullbench:NAME[:ARGS]  python bench.py ARGS (with the CPU baseline)      -> bench_NAME.json
 #   ab:LIB:NAME[:ARGS]     the bench with BF_HIP_LIB=bundlefusion_amd/libbf_hip_LIB.so (a variant build)
-#   envbench:NAME:VAR=VAL[:ARGS]  the bench with one environment setting (runtime A/B switches)
+#   envbench:NAME:VAR=VAL[+VAR=VAL...][:ARGS]  the bench with environment settings (runtime A/B switches)
+#   env:VAR=VAL[+...] / unenv:VAR[+...]  set / clear environment settings for the steps that follow
 #   profile:NAME[:ARGS]    tools/profile_bench.sh TAG/NAME ARGS (kernel stats + FETCH/WRITE/VALU passes)
 #   sqpmc:NAME:KERNEL:CNT[:ARGS]  one --pmc pass of counters CNT (',' separated) over KERNEL's dispatches
 #   sens:N[:ARGS]          write an N-frame synthetic .sens (tools/make_sens.py), then bench.py --sens ARGS
@@ -52,7 +53,10 @@ for step in "$@"; do
     bench) run bench_$a 900 python -u bench.py --no-cpu-baseline ${b//,/ }; cp $O/bench_$a.log $O/bench_$a.json; summ $O/bench_$a.json ;;
     fullbench) run bench_$a 900 python -u bench.py ${b//,/ }; cp $O/bench_$a.log $O/bench_$a.json; summ $O/bench_$a.json ;;
     ab) BF_HIP_LIB=bundlefusion_amd/libbf_hip_$a.so run bench_$b 900 python -u bench.py --no-cpu-baseline ${c//,/ }; summ $O/bench_$b.log ;;
-    envbench) export "$b"; run bench_$a 900 python -u bench.py --no-cpu-baseline ${c//,/ }; unset "${b%%=*}"; summ $O/bench_$a.log ;;
+    env) IFS=+ read -ra KV <<< "$a"; for x in "${KV[@]}"; do export "$x"; done; echo "[env] $a" ;;
+    unenv) IFS=+ read -ra KV <<< "$a"; for x in "${KV[@]}"; do unset "${x%%=*}"; done; echo "[unenv] $a" ;;
+    envbench) IFS=+ read -ra KV <<< "$b"; for x in "${KV[@]}"; do export "$x"; done
+              run bench_$a 900 python -u bench.py --no-cpu-baseline ${c//,/ }; for x in "${KV[@]}"; do unset "${x%%=*}"; done; summ $O/bench_$a.log ;;
     profile) run profile_$a 1100 bash tools/profile_bench.sh $TAG/$a ${b//,/ } ;;
     sqpmc) run sqpmc_$a 300 rocprofv3 --pmc ${c//,/ } --kernel-include-regex "$b" -d $O/sqpmc_$a -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${d//,/ }
            python3 tools/pmc_kernel.py "$(python3 -c "import glob,sys; print(glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True)[0])" $O/sqpmc_$a)" "$b" > $O/sqpmc_$a.txt; cat $O/sqpmc_$a.txt; rm -rf $O/sqpmc_$a ;;
