@@ -1427,13 +1427,23 @@ int bf_params_preprocess_options(const bf_params* p, float depthShift, BFPreproc
     BF_CATCH
 }
 
+// input preprocessing streams: highest priority unless BF_INPUT_PRIORITY=0 (A/B)
+static int input_stream_priority(int least, int greatest) {
+    const char* e = std::getenv("BF_INPUT_PRIORITY");
+    return (e && std::atoi(e) == 0) ? least : greatest;
+}
+
 int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_t colorH, uint32_t integrationW,
                       uint32_t integrationH, const BFPreprocessOptions* opt, bf_preproc** out) {
     BF_TRY
     BF_REQUIRE(opt && out, BF_ERR_ARG, "null argument");
     *out = nullptr;
     std::unique_ptr<bf_preproc> h(new bf_preproc);
-    BF_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    // the input work is on the frame loop's critical path (the scene stream's next batch waits for it):
+    // its kernels take free slots ahead of the voxel pass's next round and of the bundling launches
+    int prLeast = 0, prGreatest = 0;
+    BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
+    BF_HIP(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, input_stream_priority(prLeast, prGreatest)));
     h->p = new Preproc(depthW, depthH, colorW, colorH, integrationW, integrationH, *opt, h->stream);
     *out = h.release();
     BF_CATCH
