@@ -45,7 +45,25 @@ struct RayArgs {
     const BFVoxel* voxels;
     uint32_t numBuckets, numEntries, maxList;
     float voxelSize;
+    uint32_t ldsTable;  // 1: the workgroup's LDS block table may hold heap indices (numBlocks < 2^24 - 1)
 };
+
+// The workgroup's block table in LDS: the rays of a 16x16 tile cross the same blocks, so a block one ray
+// located is found by its neighbours without a hash probe (a probe is a dependent load from a table of
+// 2^23 buckets in HBM; this is one LDS read). Direct-mapped, one 64-bit word per slot: 39 key bits (block
+// coordinates + 4096, 13 bits each, in [0, 8190]) and 24 bits of heap index (0xFFFFFF: a free block). A
+// 64-bit LDS store is single-copy atomic, so a reader sees an empty slot or a whole entry; the hash does
+// not change during a render, so every entry stays valid. Blocks outside the key range take the probe.
+constexpr int RC_SLOTS = 1024;
+constexpr unsigned long long RC_EMPTY = ~0ull;
+__device__ __forceinline__ bool rc_key(i3 b, unsigned long long& key) {
+    const uint32_t x = (uint32_t)(b.x + 4096), y = (uint32_t)(b.y + 4096), z = (uint32_t)(b.z + 4096);
+    key = ((unsigned long long)x << 26) | ((unsigned long long)y << 13) | (unsigned long long)z;
+    return x <= 8190u && y <= 8190u && z <= 8190u;
+}
+__device__ __forceinline__ uint32_t rc_slot(i3 b) {
+    return ((uint32_t)b.x * 73856093u ^ (uint32_t)b.y * 19349669u ^ (uint32_t)b.z * 83492791u) & (RC_SLOTS - 1);
+}
 
 // cameraToDepthProj (RayCastSDFUtil.h:208-222)
 __device__ __forceinline__ f3 camera_to_depth_proj(const BFRayCastParams& p, f3 pos) {
@@ -145,6 +163,7 @@ struct BlockCache {
     int bx = INT_MIN, by = 0, bz = 0, bp = BF_FREE_ENTRY;  // entry B
     bool replaceB = false;  // the entry a miss replaces (the one not used last)
     uint32_t samples = 0, loads = 0, probes = 0;  // render statistics (trilinear samples, voxel loads, hash probes)
+    unsigned long long* table = nullptr;  // the workgroup's LDS block table (nullptr: probe every miss)
     __device__ __forceinline__ int lookup(const RayArgs& R, i3 b) {
         if (b.x == ax && b.y == ay && b.z == az) {
             replaceB = true;
@@ -154,8 +173,19 @@ struct BlockCache {
             replaceB = false;
             return bp;
         }
-        const int p = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
-        probes++;
+        int p;
+        unsigned long long key;
+        const bool keyed = table && rc_key(b, key);
+        const uint32_t slot = rc_slot(b);
+        const unsigned long long e = keyed ? table[slot] : RC_EMPTY;
+        if (keyed && e != RC_EMPTY && (e >> 24) == key) {
+            const uint32_t q = (uint32_t)e & 0xFFFFFFu;
+            p = q == 0xFFFFFFu ? BF_FREE_ENTRY : (int)q;
+        } else {
+            p = hash_lookup(R.hash, R.numBuckets, R.numEntries, R.maxList, b.x, b.y, b.z);
+            probes++;
+            if (keyed) table[slot] = (key << 24) | (p < 0 ? 0xFFFFFFull : (unsigned long long)(uint32_t)p);
+        }
         if (replaceB) {
             bx = b.x; by = b.y; bz = b.z; bp = p;
         } else {
@@ -353,15 +383,27 @@ __device__ __forceinline__ void render_pixel(const RayArgs& R, const BFRayCastPa
 // Pixel shape: each wave marches an 8x8 pixel square (neighbouring rays cross the same blocks and end at
 // similar depths); TPB 256: a workgroup is a 16x16 tile of four such squares, TPB 64: one square per
 // workgroup, so a slot frees as soon as its one wave ends (A/B, BF_RENDER_TPB)
+#ifndef BF_RENDER_WPE  // A/B builds: waves per SIMD asked of the compiler (0: its own choice, 101 VGPRs -> 4)
+#define BF_RENDER_WPE 0
+#endif
+#if BF_RENDER_WPE
+#define BF_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(BF_RENDER_WPE)))
+#else
+#define BF_RENDER_ATTR
+#endif
 template <int TPB>
-__global__ __launch_bounds__(TPB) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
+__global__ __launch_bounds__(TPB) BF_RENDER_ATTR void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
                                                 const uint32_t* __restrict__ smax, float* d_depth, float4* d_depth4,
                                                 float4* d_normals, float4* d_colors, float* outMin, float* outMax,
                                                 unsigned long long* stats) {
     constexpr uint32_t TILE = TPB == 256 ? 16u : 8u;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * TILE + (wv & 1u) * 8u + (lane & 7u), y = blockIdx.y * TILE + (wv >> 1) * 8u + (lane >> 3);
+    __shared__ unsigned long long s_table[RC_SLOTS];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)RC_SLOTS; i += TPB) s_table[i] = RC_EMPTY;
+    __syncthreads();
     BlockCache cache;
+    if (R.ldsTable) cache.table = s_table;
     bool rayed = false;
     if (x < rp.width && y < rp.height)
         render_pixel(R, rp, cache, x, y, smin, smax, d_depth, d_depth4, d_normals, d_colors, outMin, outMax, rayed);
@@ -442,6 +484,11 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
     R.numEntries = E_;
     R.maxList = cfg_.hp.hashMaxCollisionLinkedListSize;
     R.voxelSize = cfg_.hp.virtualVoxelSize;
+    static const bool ldsTable = [] {
+        const char* e = std::getenv("BF_RENDER_LDS_TABLE");  // A/B: 0 = probe every block-cache miss
+        return !(e && std::atoi(e) == 0);
+    }();
+    R.ldsTable = ldsTable && cfg_.hp.numSDFBlocks < 0xFFFFFFu ? 1u : 0u;
     const dim3 g(div_up(rp.width, 16), div_up(rp.height, 16));
     static const int tpb = [] {
         const char* e = std::getenv("BF_RENDER_TPB");

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <string>
 #include <cstdio>
 #include <cstring>
 #include <limits>
@@ -95,13 +96,15 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     opt_.maxGlobalCorr = or_default(o.maxGlobalCorr, opt_.maxKeyframes * 1000u);
 
     BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
-    // bundling stream priority: see switchBundlingPriority
-    // The policy is keyed on each solve's own size (switchBundlingPriority at every submap): a run sized for
-    // many keyframes bundles at high priority until its global solve grows past kHighPriorityMaxKeyframes.
+    // bundling stream priority: normal (as the scene stream) by default since the voxel pass runs in four
+    // resident rounds (Scene::Scene); BF_BA_HIGH_PRIORITY=1: high throughout, =keyed: round 4's policy keyed
+    // on each solve's size (switchBundlingPriority)
     sharded_ = so && so->shardCount > 1;
     int prLeast = 0, prGreatest = 0;
     BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
-    const char* forced = std::getenv("BF_BA_HIGH_PRIORITY");  // A/B measurements: one fixed priority
+    const char* env = std::getenv("BF_BA_HIGH_PRIORITY");
+    const bool keyed = env && std::string(env) == "keyed";
+    const char* forced = keyed ? nullptr : (env ? env : "0");
     if (forced) priorityPolicy_ = std::atoi(forced) != 0 ? 1 : 0;
     const bool needHigh = forced ? priorityPolicy_ == 1 : true;
     const bool needNormal = forced ? priorityPolicy_ == 0 : (!sharded_ && opt_.maxKeyframes > kHighPriorityMaxKeyframes);
@@ -546,6 +549,10 @@ void Recon::endSubmap(uint32_t s, uint32_t n) {
     optimizedFrames_ = S * s + std::min(n, S);
 }
 
+// Round 5: with the voxel pass in four resident rounds (a slot frees every ~120 us instead of once per pass),
+// the bundling streams run at normal priority by default: the bench stream 1 446-1 458 (high) -> 1 470-1 474
+// frames/s, the G = 8 rehearsal 3 707-3 732 -> 3 812-3 825 (profiles/r10_ba_priority_ab.txt). The keyed
+// policy below (BF_BA_HIGH_PRIORITY=keyed) was round 4's, measured with one resident round:
 // Bundling streams at the highest queue priority take CU slots ahead of the scene stream's next workgroups
 // (priority orders dispatch; it never preempts a running workgroup):
 // - sharded, each GPU has a fraction of the voxel work and the (replicated) bundling is co-critical: +7 % at
