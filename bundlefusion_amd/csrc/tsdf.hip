@@ -1318,7 +1318,15 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
 // list garbageCollect walks), work list = blocks some op may update, with the op bit mask. Also
 // releases the batch's alloc dedup-set slots.
-__global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
+#ifndef BF_COMPACTIFY_WPE  // A/B builds: waves per SIMD asked of the compiler for the batch scan (0: its choice, 4)
+#define BF_COMPACTIFY_WPE 0
+#endif
+#if BF_COMPACTIFY_WPE
+#define BF_COMPACTIFY_ATTR __attribute__((amdgpu_waves_per_eu(BF_COMPACTIFY_WPE)))
+#else
+#define BF_COMPACTIFY_ATTR
+#endif
+__global__ __launch_bounds__(256) BF_COMPACTIFY_ATTR void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
                                                         OpMask* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
                                                         uint32_t binCap) {
@@ -1930,7 +1938,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     // the batch scan: 4 workgroups per CU (its occupancy), BF_COMPACTIFY_GRID_MULT rounds of them (A/B)
     int cmult = 1;
     if (const char* e = std::getenv("BF_COMPACTIFY_GRID_MULT")) cmult = std::max(1, std::atoi(e));
-    compactifyGrid_ = (unsigned)numCUs_ * 4u * (unsigned)cmult;
+    compactifyGrid_ = (unsigned)numCUs_ * (BF_COMPACTIFY_WPE > 4 ? (unsigned)BF_COMPACTIFY_WPE : 4u) * (unsigned)cmult;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
