@@ -46,6 +46,7 @@ struct SceneConfig {
     uint32_t shardCount;     // >1: spatial ownership sharding across GPUs
     uint32_t shardIndex;
     float shardChunk;        // ownership chunk edge in metres (default 1 m, the streaming chunk)
+    uint32_t allocForceDirect = 0;  // test switch (BF_ALLOC_FORCE_DIRECT): every walking tile also takes the alloc walk's congested path
 };
 
 // One voxel op of a batch: integrate (deint = false) or de-integrate one frame at pose T (camera ->

@@ -51,6 +51,7 @@ struct HashArgs {
     uint32_t numBuckets, numEntries, numBlocks, maxList;
     float voxelSize, truncation, truncScale, maxIntegrationDistance, weightMax;
     uint32_t shardCount, shardIndex;
+    uint32_t allocForceDirect;
     float shardChunk;
     // reference streaming bitmask (isSDFBlockStreamedOut, CUDASceneRepHashSDF.cu:152-163)
     const uint32_t* bitMask;
@@ -510,60 +511,121 @@ __device__ __forceinline__ bool block_in_frustum_fast(const BFDepthCameraParams&
 
 // allocKernel, CUDASceneRepHashSDF.cu:165-251: per-pixel DDA over 8^3-block cells. Emits the
 // absent, in-frustum, owned blocks (deduplicated per tile in LDS) into `cand`.
+struct RayWalk {  // one pixel's DDA state (CUDASceneRepHashSDF.cu:196-230)
+    i3 id, idBound;
+    f3 tMax, tDelta, step;
+    bool active;
+};
+__device__ __forceinline__ RayWalk ray_walk_setup(const HashArgs& A, const float* __restrict__ depthImg,
+                                                  const BFDepthCameraParams& cam, const BFMat4& T, uint32_t x, uint32_t y) {
+    RayWalk r;
+    r.active = x < cam.imageWidth && y < cam.imageHeight;
+    const float d = r.active ? depthImg[y * cam.imageWidth + x] : 0.0f;
+    if (d == -INFINITY || d == 0.0f) r.active = false;
+    if (d >= A.maxIntegrationDistance) r.active = false;
+    const float t = A.truncation + A.truncScale * d;
+    const float minDepth = fminf(A.maxIntegrationDistance, d - t);
+    const float maxDepth = fminf(A.maxIntegrationDistance, d + t);
+    if (minDepth >= maxDepth) r.active = false;
+    r.id = {0, 0, 0};
+    r.idBound = {0, 0, 0};
+    r.tMax = mk3(0, 0, 0);
+    r.tDelta = mk3(0, 0, 0);
+    r.step = mk3(0, 0, 0);
+    if (r.active) {
+        const f3 rayMin = xform(T, depth_to_camera(cam, x, y, minDepth));
+        const f3 rayMax = xform(T, depth_to_camera(cam, x, y, maxDepth));
+        const f3 rayDir = normalize3(rayMax - rayMin);
+        r.id = world_to_block(rayMin, A.voxelSize);
+        const i3 idEnd = world_to_block(rayMax, A.voxelSize);
+        r.step = mk3((float)sgn(rayDir.x), (float)sgn(rayDir.y), (float)sgn(rayDir.z));
+        const f3 bp = block_to_world(r.id.x + f2i(fmaxf(0.0f, fminf(r.step.x, 1.0f))), r.id.y + f2i(fmaxf(0.0f, fminf(r.step.y, 1.0f))),
+                                     r.id.z + f2i(fmaxf(0.0f, fminf(r.step.z, 1.0f))), A.voxelSize) -
+                      mk3(1.0f, 1.0f, 1.0f) * (0.5f * A.voxelSize);
+        r.tMax = (bp - rayMin) / rayDir;
+        r.tDelta = (r.step * (float)BF_SDF_BLOCK_SIZE * A.voxelSize) / rayDir;
+        r.idBound.x = f2i((float)idEnd.x + r.step.x);
+        r.idBound.y = f2i((float)idEnd.y + r.step.y);
+        r.idBound.z = f2i((float)idEnd.z + r.step.z);
+        if (rayDir.x == 0.0f) { r.tMax.x = INFINITY; r.tDelta.x = INFINITY; }
+        if (bp.x - rayMin.x == 0.0f) { r.tMax.x = INFINITY; r.tDelta.x = INFINITY; }
+        if (rayDir.y == 0.0f) { r.tMax.y = INFINITY; r.tDelta.y = INFINITY; }
+        if (bp.y - rayMin.y == 0.0f) { r.tMax.y = INFINITY; r.tDelta.y = INFINITY; }
+        if (rayDir.z == 0.0f) { r.tMax.z = INFINITY; r.tDelta.z = INFINITY; }
+        if (bp.z - rayMin.z == 0.0f) { r.tMax.z = INFINITY; r.tDelta.z = INFINITY; }
+        // multi-GPU: the walk visits only blocks inside the box of its first and last block; when no
+        // chunk of that box belongs to this rank, none of its blocks can be emitted, so skip the walk
+        // (chunk indices are monotone in the block coordinate: the box's corners bound them)
+        if (A.shardCount > 1) r.active = segment_may_own(A, r.id, idEnd);
+    }
+    return r;
+}
+__device__ __forceinline__ void ray_walk_advance(RayWalk& r) {  // traverse (CUDASceneRepHashSDF.cu:231-246)
+    if (r.tMax.x < r.tMax.y && r.tMax.x < r.tMax.z) {
+        r.id.x = f2i((float)r.id.x + r.step.x);
+        if (r.id.x == r.idBound.x) r.active = false;
+        r.tMax.x += r.tDelta.x;
+    } else if (r.tMax.z < r.tMax.y) {
+        r.id.z = f2i((float)r.id.z + r.step.z);
+        if (r.id.z == r.idBound.z) r.active = false;
+        r.tMax.z += r.tDelta.z;
+    } else {
+        r.id.y = f2i((float)r.id.y + r.step.y);
+        if (r.id.y == r.idBound.y) r.active = false;
+        r.tMax.y += r.tDelta.y;
+    }
+}
+// the absent, in-frustum, owned, not streamed-out blocks are emitted (allocKernel's per-block tests)
+__device__ __forceinline__ bool alloc_wants(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, i3 b) {
+    return block_in_frustum_fast(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
+           !streamed_out(A, b.x, b.y, b.z) && lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY;
+}
+// A tile whose keys overflowed both the LDS set and its overflow list (never seen at the bench workloads):
+// the tile's walk again, every visited block tested and emitted directly. Blocks phase 2 already emitted
+// come out twice; the global dedup of k_alloc_insert removes them. It runs after phase 2, outside the hot
+// walk loop (the first form tested and emitted an unplaced key inside the loop: 141 SGPR spills there).
+__device__ __forceinline__ unsigned long long alloc_walk_direct(const HashArgs& A, const float* __restrict__ depthImg,
+                                                             const BFDepthCameraParams& cam, const BFMat4& T, const BFMat4& Tinv,
+                                                             unsigned long long* __restrict__ cand, uint32_t candCap,
+                                                             uint8_t* __restrict__ candOp, uint8_t opIdx, uint32_t x, uint32_t y) {
+    RayWalk r = ray_walk_setup(A, depthImg, cam, T, x, y);
+    unsigned long long emitted = 0;
+    for (uint32_t iter = 0; iter < 1024 && r.active; iter++) {
+        const i3 b = r.id;
+        ray_walk_advance(r);
+        if (alloc_wants(A, cam, Tinv, b)) {
+            const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
+            if (k < candCap) {
+                cand[k] = block_key(b.x, b.y, b.z);
+                if (candOp) candOp[k] = opIdx;
+            } else {
+                atomicOr(&A.ctrl[C_ERR], 1u);
+            }
+            emitted++;
+        }
+    }
+    return emitted;
+}
+constexpr int ALLOC_OVF = 256;  // per tile: keys the congested LDS set could not place, tested in phase 2
 __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __restrict__ depthImg,
                                               const BFDepthCameraParams& cam, const BFMat4& T, const BFMat4& Tinv,
                                               unsigned long long* __restrict__ cand, uint32_t candCap,
                                               uint8_t* __restrict__ candOp = nullptr, uint8_t opIdx = 0) {
-    __shared__ unsigned long long set[LDS_SET];
+    __shared__ unsigned long long set[LDS_SET + ALLOC_OVF];  // the set, then the overflow keys
+    __shared__ uint32_t s_novf;
     const uint32_t x = blockIdx.x * ALLOC_TILE + (threadIdx.x % ALLOC_TILE);
     const uint32_t y = blockIdx.y * ALLOC_TILE + (threadIdx.x / ALLOC_TILE);
-    bool active = x < cam.imageWidth && y < cam.imageHeight;
-    float d = active ? depthImg[y * cam.imageWidth + x] : 0.0f;
-    if (d == -INFINITY || d == 0.0f) active = false;
-    if (d >= A.maxIntegrationDistance) active = false;
-    const float t = A.truncation + A.truncScale * d;
-    const float minDepth = fminf(A.maxIntegrationDistance, d - t);
-    const float maxDepth = fminf(A.maxIntegrationDistance, d + t);
-    if (minDepth >= maxDepth) active = false;
-
-    i3 id = {0, 0, 0}, idBound = {0, 0, 0};
-    f3 tMax = mk3(0, 0, 0), tDelta = mk3(0, 0, 0), step = mk3(0, 0, 0);
-    if (active) {
-        const f3 rayMin = xform(T, depth_to_camera(cam, x, y, minDepth));
-        const f3 rayMax = xform(T, depth_to_camera(cam, x, y, maxDepth));
-        const f3 rayDir = normalize3(rayMax - rayMin);
-        id = world_to_block(rayMin, A.voxelSize);
-        const i3 idEnd = world_to_block(rayMax, A.voxelSize);
-        step = mk3((float)sgn(rayDir.x), (float)sgn(rayDir.y), (float)sgn(rayDir.z));
-        const f3 bp = block_to_world(id.x + f2i(fmaxf(0.0f, fminf(step.x, 1.0f))), id.y + f2i(fmaxf(0.0f, fminf(step.y, 1.0f))),
-                                     id.z + f2i(fmaxf(0.0f, fminf(step.z, 1.0f))), A.voxelSize) -
-                      mk3(1.0f, 1.0f, 1.0f) * (0.5f * A.voxelSize);
-        tMax = (bp - rayMin) / rayDir;
-        tDelta = (step * (float)BF_SDF_BLOCK_SIZE * A.voxelSize) / rayDir;
-        idBound.x = f2i((float)idEnd.x + step.x);
-        idBound.y = f2i((float)idEnd.y + step.y);
-        idBound.z = f2i((float)idEnd.z + step.z);
-        if (rayDir.x == 0.0f) { tMax.x = INFINITY; tDelta.x = INFINITY; }
-        if (bp.x - rayMin.x == 0.0f) { tMax.x = INFINITY; tDelta.x = INFINITY; }
-        if (rayDir.y == 0.0f) { tMax.y = INFINITY; tDelta.y = INFINITY; }
-        if (bp.y - rayMin.y == 0.0f) { tMax.y = INFINITY; tDelta.y = INFINITY; }
-        if (rayDir.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
-        if (bp.z - rayMin.z == 0.0f) { tMax.z = INFINITY; tDelta.z = INFINITY; }
-        // multi-GPU: the walk visits only blocks inside the box of its first and last block; when no
-        // chunk of that box belongs to this rank, none of its blocks can be emitted, so skip the walk
-        // (chunk indices are monotone in the block coordinate: the box's corners bound them)
-        if (A.shardCount > 1) active = segment_may_own(A, id, idEnd);
-    }
+    RayWalk r = ray_walk_setup(A, depthImg, cam, T, x, y);
     // a tile none of whose rays walks (no valid depth, or, sharded, no ray near an owned chunk) ends here
-    if (!__syncthreads_or(active ? 1 : 0)) return;
+    if (!__syncthreads_or(r.active ? 1 : 0)) return;
     for (int k = threadIdx.x; k < LDS_SET; k += blockDim.x) set[k] = EMPTY_KEY;
+    if (threadIdx.x == 0) s_novf = 0;
     __syncthreads();
 
     // phase 1: walk the ray's blocks and collect the tile's distinct blocks in the LDS set (compute
     // only, no global memory on the DDA's critical path). The per-block tests (frustum, ownership,
     // streaming mask) depend only on the block, so they run once per distinct block in phase 2
     // instead of once per DDA step: same emitted set, far fewer projections.
-    unsigned long long emitted = 0;
     const uint32_t lane = lane_id();
     // The loop runs while any lane of the wave walks (wave-uniform trip) so that lanes can compare
     // keys: a lane whose left (same pixel row) or upper neighbour pixel reaches the same block in
@@ -572,22 +634,7 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
     // Two DDA steps per trip: both steps' first-probe CAS are issued back to back, so a walk pays one
     // LDS round trip per two blocks (probing past a taken slot, rare, follows per step). Which lane
     // inserts a key and in what order changes nothing: the set ends up holding the same keys, and a
-    // key that finds no slot is tested and emitted directly (the global dedup removes repeats).
-    auto advance = [&]() {  // traverse (CUDASceneRepHashSDF.cu:231-246)
-        if (tMax.x < tMax.y && tMax.x < tMax.z) {
-            id.x = f2i((float)id.x + step.x);
-            if (id.x == idBound.x) active = false;
-            tMax.x += tDelta.x;
-        } else if (tMax.z < tMax.y) {
-            id.z = f2i((float)id.z + step.z);
-            if (id.z == idBound.z) active = false;
-            tMax.z += tDelta.z;
-        } else {
-            id.y = f2i((float)id.y + step.y);
-            if (id.y == idBound.y) active = false;
-            tMax.y += tDelta.y;
-        }
-    };
+    // key that finds no slot goes to the tile's overflow list (phase 2 tests it like the set's keys).
     auto is_dup = [&](unsigned long long myKey) {
         const unsigned long long left = __shfl_up(myKey, 1, ALLOC_TILE), up = __shfl_up(myKey, ALLOC_TILE);
         return ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
@@ -595,75 +642,64 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
     // slot from the low coordinate bits (3 + 4 + 3 = 10 bits = LDS_SET): the blocks one 16x16-pixel
     // tile reaches span a few blocks per axis, so they land in distinct slots without a mixing hash
     auto slot_of = [](i3 b) { return ((uint32_t)b.x & 7u) | (((uint32_t)b.y & 15u) << 3) | (((uint32_t)b.z & 7u) << 7); };
-    auto finish_insert = [&](unsigned long long key, i3 b, uint32_t h) {  // probes 2..16, then the direct path
-        bool placed = false;
+    auto finish_insert = [&](unsigned long long key, uint32_t h) {  // probes 2..16, then the overflow list
         for (int p = 1; p < 16; p++) {
             h = (h + 1) & (LDS_SET - 1);
             const unsigned long long old = atomicCAS(&set[h], EMPTY_KEY, key);
-            if (old == EMPTY_KEY || old == key) { placed = true; break; }
+            if (old == EMPTY_KEY || old == key) return;
         }
-        // congested tile set (rare): test and look the block up right here, emit it if absent
-        // (duplicates are removed by the global dedup in k_alloc_insert)
-        if (!placed && block_in_frustum(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
-            !streamed_out(A, b.x, b.y, b.z) && lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY) {
-            const uint32_t k = atomicAdd(&A.ctrl[C_CAND], 1u);
-            if (k < candCap) {
-                cand[k] = key;
-                if (candOp) candOp[k] = opIdx;
-            }
-            else atomicOr(&A.ctrl[C_ERR], 1u);
-            emitted++;
-        }
+        const uint32_t j = atomicAdd(&s_novf, 1u);
+        if (j < (uint32_t)ALLOC_OVF) set[LDS_SET + j] = key;
     };
     for (uint32_t iter = 0; iter < 512; iter++) {
-        if (!__any(active)) break;
-        const bool actA = active;
-        const i3 idA = id;
-        if (active) advance();
-        const bool actB = active;
-        const i3 idB = id;
-        if (active) advance();
+        if (!__any(r.active)) break;
+        const bool actA = r.active;
+        const i3 idA = r.id;
+        if (r.active) ray_walk_advance(r);
+        const bool actB = r.active;
+        const i3 idB = r.id;
+        if (r.active) ray_walk_advance(r);
         const unsigned long long keyA = actA ? block_key(idA.x, idA.y, idA.z) : EMPTY_KEY;
         const unsigned long long keyB = actB ? block_key(idB.x, idB.y, idB.z) : EMPTY_KEY;
         const bool doA = actA && !is_dup(keyA), doB = actB && !is_dup(keyB);
         const uint32_t hA = slot_of(idA), hB = slot_of(idB);
         const unsigned long long oldA = doA ? atomicCAS(&set[hA], EMPTY_KEY, keyA) : EMPTY_KEY;
         const unsigned long long oldB = doB ? atomicCAS(&set[hB], EMPTY_KEY, keyB) : EMPTY_KEY;
-        if (doA && oldA != EMPTY_KEY && oldA != keyA) finish_insert(keyA, idA, hA);
-        if (doB && oldB != EMPTY_KEY && oldB != keyB) finish_insert(keyB, idB, hB);
+        if (doA && oldA != EMPTY_KEY && oldA != keyA) finish_insert(keyA, hA);
+        if (doB && oldB != EMPTY_KEY && oldB != keyB) finish_insert(keyB, hB);
     }
-    // phase 2: compact the distinct blocks to the front of the set, then every thread checks one of
-    // them against the hash (one round of parallel lookups per 256 distinct blocks — a tile reaches
-    // far fewer — instead of a round per 256 slots, each waiting on its hash loads) and emits the
-    // absent ones
+    // phase 2: compact the distinct blocks to the front of the set, append the overflow keys, then every
+    // thread checks one of them against the hash (one round of parallel lookups per 256 distinct blocks —
+    // a tile reaches far fewer — instead of a round per 256 slots, each waiting on its hash loads) and
+    // emits the absent ones
     __shared__ uint32_t s_nkeys;
     constexpr int SLOTS_PER_THREAD = LDS_SET / 256;
     unsigned long long mine[SLOTS_PER_THREAD];
     __syncthreads();
+    const uint32_t novf = s_novf;
+    const uint32_t nOvfKept = min(novf, (uint32_t)ALLOC_OVF);
+    unsigned long long ovfKey = threadIdx.x < nOvfKept ? set[LDS_SET + threadIdx.x] : EMPTY_KEY;
 #pragma unroll
     for (int j = 0; j < SLOTS_PER_THREAD; j++) mine[j] = set[j * 256 + threadIdx.x];
     if (threadIdx.x == 0) s_nkeys = 0;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < SLOTS_PER_THREAD; j++) {
-        const bool full = mine[j] != EMPTY_KEY;
+    for (int j = 0; j < SLOTS_PER_THREAD + 1; j++) {
+        const unsigned long long key = j < SLOTS_PER_THREAD ? mine[j] : ovfKey;
+        const bool full = key != EMPTY_KEY;
         const unsigned long long m = __ballot(full);
         if (m == 0) continue;
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(&s_nkeys, (uint32_t)__popcll(m));
         base = __shfl(base, 0);
-        if (full) set[base + __popcll(m & lanemask_lt())] = mine[j];
+        if (full) set[base + __popcll(m & lanemask_lt())] = key;
     }
     __syncthreads();
     const uint32_t nkeys = s_nkeys;
+    unsigned long long emitted = 0;
     for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
         const unsigned long long key = k0 + threadIdx.x < nkeys ? set[k0 + threadIdx.x] : EMPTY_KEY;
-        bool want = false;
-        if (key != EMPTY_KEY) {
-            const i3 b = key_block(key);
-            want = block_in_frustum_fast(cam, Tinv, b.x, b.y, b.z, A.voxelSize) && owned(A, b.x, b.y, b.z) &&
-                   !streamed_out(A, b.x, b.y, b.z) && lookup_ptr(A, b.x, b.y, b.z) == BF_FREE_ENTRY;
-        }
+        const bool want = key != EMPTY_KEY && alloc_wants(A, cam, Tinv, key_block(key));
         const unsigned long long m = __ballot(want);
         if (want) {
             const int leader = __ffsll((long long)m) - 1;
@@ -679,6 +715,9 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
             emitted++;
         }
     }
+    // the overflow list itself overflowed: the tile's walk again with direct emission (workgroup-uniform)
+    // (A.allocForceDirect, a test switch: every walking tile also takes the direct path; same candidate set)
+    if (novf > (uint32_t)ALLOC_OVF || A.allocForceDirect) emitted += alloc_walk_direct(A, depthImg, cam, T, Tinv, cand, candCap, candOp, opIdx, x, y);
     // pixels are counted on the host (W x H per walk); candidates are rare in steady state, so the
     // workgroup adds its count only when it emitted some (every workgroup adding to a few counters
     // serialised ~10^5 atomics per frame on them)
@@ -691,7 +730,17 @@ __global__ __launch_bounds__(256) void k_alloc_collect(HashArgs A, const float* 
 }
 // batched: blockIdx.z selects the integrate op of the table (all ops' candidates land in one list;
 // the global dedup of k_alloc_insert removes blocks several ops want)
-__global__ __launch_bounds__(256) void k_alloc_collect_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops,
+// waves per SIMD asked of the compiler for the batched walk: 8 (63 VGPRs, 78 SGPRs with 65 spilled to VGPR lanes)
+// against its own choice of 7 (SGPR-limited): k_alloc_collect_ops 90 -> 86.5 us per frame (gpurun_out/s21)
+#ifndef BF_ALLOC_WPE
+#define BF_ALLOC_WPE 8
+#endif
+#if BF_ALLOC_WPE
+#define BF_ALLOC_ATTR __attribute__((amdgpu_waves_per_eu(BF_ALLOC_WPE)))
+#else
+#define BF_ALLOC_ATTR
+#endif
+__global__ __launch_bounds__(256) BF_ALLOC_ATTR void k_alloc_collect_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops,
                                                            unsigned long long* __restrict__ cand, uint32_t candCap,
                                                            uint8_t* __restrict__ candOp) {
     const uint32_t k = ops.intIdx[blockIdx.z];
@@ -1870,6 +1919,7 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
     a.weightMax = (float)cfg.hp.integrationWeightMax;
     a.shardCount = cfg.shardCount;
     a.shardIndex = cfg.shardIndex;
+    a.allocForceDirect = cfg.allocForceDirect;
     a.shardChunk = cfg.shardChunk > 0 ? cfg.shardChunk : 1.0f;
     a.bitMask = bitMask;
     a.streamExtents = cfg.hp.streamingVoxelExtents;
@@ -1879,6 +1929,7 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
 }
 
 Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
+    if (const char* e = std::getenv("BF_ALLOC_FORCE_DIRECT")) cfg_.allocForceDirect = std::atoi(e) != 0 ? 1u : 0u;
     BF_REQUIRE(cfg.hp.hashNumBuckets > 0 && cfg.hp.numSDFBlocks > 0, BF_ERR_ARG, "empty hash/heap");
     // HashEntry.ptr holds the heap block index inside the scene (voxel address = ptr * 512 in 64 bits):
     // the reference's int32 voxel index (ptr = block * 512, VoxelUtilHashSDF.h:60,609) stops at 2^22

@@ -238,6 +238,41 @@ def test_op_batch_parity(scene, shift):
     assert pair.gpu.errorFlags() == 0
 
 
+def test_op_batch_alloc_congested_path(scene, monkeypatch):
+    """The alloc walk's congested-tile path (a tile whose keys overflow its LDS set and overflow list walks
+    again and emits every block directly; never taken at the bench workloads) forced on for every tile
+    (BF_ALLOC_FORCE_DIRECT, read at scene creation): its candidates duplicate phase 2's, the global dedup
+    removes them, and the scene stays bit-exact with the oracle through single integrations and an op
+    batch."""
+    monkeypatch.setenv("BF_ALLOC_FORCE_DIRECT", "1")
+    cam = small_cam()
+    p = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 17, num_blocks=1 << 16)
+    pair = Pair(p, cam)
+    frames = render_frames(scene, cam, [0, 5, 10, 15])
+    for k in range(3):
+        T, d, c = frames[k]
+        pair.integrate(k, T, d, c)
+        pair.compare()
+    pair.gc()
+    rng = np.random.default_rng(7)
+    ops = []
+    for k in (0, 2):
+        T2 = _perturbed(frames[k][0], rng, 0.02, rot_deg=0.3)
+        ops += [(frames[k][0], k, True), (T2, k, False)]
+    ops.append((frames[3][0], 3, False))
+    dev = []
+    for T, k, deint in ops:
+        dd, cc = pair._upload(k, frames[k][1], frames[k][2])
+        dev.append((T, dd, cc, deint))
+        pair.ora.integrate(T, frames[k][1], frames[k][2], cam, deintegrate=deint)
+    pair.gpu.apply_ops(dev, cam)
+    assert pair.compare() > 1000
+    pair.gc()
+    pair.compare()
+    assert pair.gpu.getHeapFreeCount() == pair.ora.getHeapFreeCount()
+    assert pair.gpu.errorFlags() == 0
+
+
 def test_op_batch_full_resolution(scene):
     """A full 10-fix batch (20 ops) at 640x480 / 4 mm against the oracle."""
     cam = bfa.depth_camera(640, 480)
