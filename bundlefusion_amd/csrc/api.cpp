@@ -922,6 +922,12 @@ int bf_recon_set_frame_raw(bf_recon* r, uint32_t f, const uint16_t* depthU16, co
     r->r->setFrameRaw(f, depthU16, rgbx);
     BF_CATCH
 }
+int bf_recon_frame_ready(bf_recon* r, uint32_t f, void* stream) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null argument");
+    r->r->inputsProduced(f, static_cast<hipStream_t>(stream));
+    BF_CATCH
+}
 int bf_recon_end_sequence(bf_recon* r, const BFEndSequenceOptions* o, BFEndSequenceResult* out) {
     BF_TRY
     BF_REQUIRE(r && o, BF_ERR_ARG, "null argument");
@@ -1467,6 +1473,12 @@ int bf_preproc_synchronize(bf_preproc* p) {
     BF_TRY
     BF_REQUIRE(p, BF_ERR_ARG, "null argument");
     BF_HIP(hipStreamSynchronize(p->stream));
+    BF_CATCH
+}
+int bf_preproc_stream(bf_preproc* p, void** stream) {
+    BF_TRY
+    BF_REQUIRE(p && stream, BF_ERR_ARG, "null argument");
+    *stream = static_cast<void*>(p->stream);
     BF_CATCH
 }
 

@@ -254,3 +254,14 @@ class Preprocessor:
         check(lib().bf_preproc_run(self.h, depth_u16.ptr, rgbx.ptr if rgbx is not None else None, depth_out.ptr,
                                    color_out.ptr if color_out is not None else None))
         check(lib().bf_preproc_synchronize(self.h))
+
+    def run_async(self, depth_u16_ptr: int, rgbx_ptr: int, depth_out_ptr: int, color_out_ptr: int):
+        """bf_preproc_run without the wait: queued on self.stream"""
+        check(lib().bf_preproc_run(self.h, C.c_void_p(depth_u16_ptr), C.c_void_p(rgbx_ptr), C.c_void_p(depth_out_ptr),
+                                   C.c_void_p(color_out_ptr)))
+
+    @property
+    def stream(self) -> int:
+        s = C.c_void_p()
+        check(lib().bf_preproc_stream(self.h, C.byref(s)))
+        return s.value or 0

@@ -167,6 +167,11 @@ class Recon:
     def set_frame_raw(self, f: int, depth_u16_ptr: int, rgbx_ptr: int):
         check(lib().bf_recon_set_frame_raw(self.h, C.c_uint32(f), C.c_void_p(depth_u16_ptr), C.c_void_p(rgbx_ptr)))
 
+    def frame_ready(self, f: int, stream: int):
+        """bf_recon_frame_ready: frame f's frame-store images are being written on `stream` (a hipStream_t);
+        the loop's scene stream waits for that work on the device"""
+        check(lib().bf_recon_frame_ready(self.h, C.c_uint32(f), C.c_void_p(stream)))
+
     def set_frame_source(self, f: int, depth_ptr: int, color_ptr: int, color_w: int, color_h: int):
         check(lib().bf_recon_set_frame_source(self.h, C.c_uint32(f), C.c_void_p(depth_ptr), C.c_void_p(color_ptr),
                                               C.c_uint32(color_w), C.c_uint32(color_h)))

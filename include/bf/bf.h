@@ -433,6 +433,12 @@ int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const
 typedef struct bf_preproc bf_preproc;
 int bf_recon_attach_preproc(bf_recon* r, bf_preproc* p);
 int bf_recon_set_frame_raw(bf_recon* r, uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx);
+/* Frame f's frame-store images (bf_recon_set_frame) are being written by work queued on `stream` (a
+ * hipStream_t; the caller's own upload or preprocessing, CUDAImageManager::process outside the loop): the
+ * loop's scene stream waits for that work on the device, in the batch that first reads the frame, instead
+ * of the caller synchronising before bf_recon_process_frame. Call after queueing the producing work and
+ * before bf_recon_process_frame(f). (The FriedLiver app does this for every frame on its input stream.) */
+int bf_recon_frame_ready(bf_recon* r, uint32_t f, void* stream);
 
 /* The end of the sequence (the render loop past the last input frame): OnlineBundler::processInput's
  * past-the-end branch (OnlineBundler.cpp:167-196), process() -> optimizeGlobal with isSequenceDone (:373-408)
@@ -620,6 +626,7 @@ int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_
 int bf_preproc_destroy(bf_preproc* p);
 int bf_preproc_run(bf_preproc* p, const uint16_t* depthU16, const uint8_t* rgbx, float* depthOut, uint8_t* colorOut);
 int bf_preproc_synchronize(bf_preproc* p);
+int bf_preproc_stream(bf_preproc* p, void** stream);  /* the hipStream_t bf_preproc_run queues on */
 
 /* ---- the FriedLiver application over the path: main() + the render loop --------
  * FriedLiver.cpp:184-320 reads two parameter files (argv[1] zParametersDefault.txt -> GlobalAppState,

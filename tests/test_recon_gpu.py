@@ -143,11 +143,13 @@ def test_loop_preprocesses_raw_frames_in_order():
     sensor frame (ushort depth, RGBX) is preprocessed into its frame-store slot when the loop reaches it, on
     the preprocessor's stream, with the scene stream ordered after it. The loop must then do exactly what a
     loop over frames preprocessed beforehand does: the same scene calls, trajectory and voxels, bit for bit,
-    in the synchronous and the asynchronous bundling modes."""
+    in the synchronous and the asynchronous bundling modes. Mode "ready": each frame preprocessed outside the
+    loop right before it is processed, on the preprocessor's own stream with no host wait, the loop ordered
+    after it by bf_recon_frame_ready alone (the FriedLiver app's input path)."""
     from bundlefusion_amd.io import Preprocessor, preprocess_options
     F, W, H = 40, 160, 120
     results = []
-    for mode in ("in_loop", "before"):
+    for mode in ("in_loop", "before", "ready"):
         for async_ba in (0, 1):
             st = SyntheticStream(F, width=W, height=H, drift=(0.05, 0.002), outliers=0.0, cache_source="synth",
                                  raw_input=True)
@@ -162,6 +164,10 @@ def test_loop_preprocesses_raw_frames_in_order():
                                                   C.c_void_p(st.color.ptr.value + 4 * P * f)))
                 bfa.check(bfa.lib().bf_preproc_synchronize(pre.h))
                 st.raw_input = False  # attach() then registers no raw frames
+            pre_async = None
+            if mode == "ready":  # preprocessed outside the loop, frame by frame, ordered by bf_recon_frame_ready only
+                pre_async = Preprocessor((W, H), (W, H), (W, H), preprocess_options())
+                st.raw_input = False
             params = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 16, num_blocks=1 << 15)
             K = st.K
             opts = recon_options(F, recordOps=1, cacheWidth=80, cacheHeight=60, cacheIntrinsics=st.cache_intrinsics,
@@ -169,15 +175,20 @@ def test_loop_preprocesses_raw_frames_in_order():
                                  asyncBundling=async_ba, resultLag=10 if async_ba else 0)
             rc = Recon(params, st.cam, opts)
             st.attach(rc)
+            P = W * H
             for f in range(F):
+                if pre_async is not None:
+                    pre_async.run_async(st.depth_u16.ptr.value + 2 * P * f, st.rgbx.ptr.value + 4 * P * f,
+                                        st.depth.ptr.value + 4 * P * f, st.color.ptr.value + 4 * P * f)
+                    rc.frame_ready(f, pre_async.stream)
                 rc.process_frame(f)
             rc.finish()
             rc.synchronize()
             hash_, heap, hc, vox = rc.export()
             results.append((mode, async_ba, rc.op_log(), rc.trajectory(F), hash_, heap, hc, vox))
             rc.close()
-    for async_ba in (0, 1):
-        a = [r for r in results if r[1] == async_ba and r[0] == "in_loop"][0]
+    for async_ba, other in ((0, "in_loop"), (1, "in_loop"), (0, "ready"), (1, "ready")):
+        a = [r for r in results if r[1] == async_ba and r[0] == other][0]
         b = [r for r in results if r[1] == async_ba and r[0] == "before"][0]
         assert len(a[2]) == len(b[2]) and len(a[2]) > F
         for x, y in zip(a[2], b[2]):
