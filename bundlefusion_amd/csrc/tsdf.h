@@ -31,11 +31,11 @@ enum Ctrl {
     C_CAND = 2,        // alloc candidates emitted
     C_OVF = 3,         // candidates whose bucket was full (collision-list path)
     C_HIGHWATER = 4,   // 1 + highest heap block index ever handed out
-    C_GC_SIMPLE = 5,   // GC victims deletable without touching a collision list
     C_GC_LIST = 6,     // GC victims that touch a collision list (serial path)
     C_ERR = 7,         // error bits (1: candidate buffer overflow, 2: heap exhausted, 4: dedup set full)
     C_BAND = 8,        // blocks of the visible list that may hold a voxel inside the truncation band
     C_TICKET = 9,      // last-workgroup ticket of k_alloc_insert (self-resetting)
+    C_TICKET_GC = 10,  // last-workgroup ticket of k_gc (self-resetting)
     C_OPBIN = 16,      // op batches: work-list entries per op count (1..kMaxOps -> slots 16..39)
     C_COUNT = 48
 };
@@ -161,7 +161,6 @@ private:
     DevBuf<unsigned long long> candSet_;
     DevBuf<int> candSlot_;
     DevBuf<unsigned long long> ovf_;
-    DevBuf<int4> gcSimple_;
     DevBuf<unsigned long long> gcList_;
     DevBuf<uint32_t> blockCount_;
     uint32_t candSetMask_;

@@ -1764,64 +1764,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
 }
 
-// garbageCollectIdentifyKernel (:584-631) via the per-block nonzero-weight count, plus the
-// classification deleteHashEntryElement (VoxelUtilHashSDF.h:739-826) needs: a victim sitting in
-// its bucket with offset == 0 is deleted without the bucket lock; every other victim touches
-// a collision list and goes to the serial path.
-__global__ __launch_bounds__(256) void k_gc_identify(HashArgs A, int4* simple, unsigned long long* listV) {
-    const uint32_t nvis = A.ctrl[C_VISIBLE];
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nvis; b += gridDim.x * blockDim.x) {
-        const int4 e = A.visible[b];
-        const uint32_t blk = (uint32_t)e.w;
-        if (A.blockCount[blk] != 0) continue;
-        if (A.blockPos[blk].w == 0) continue;  // already freed by an earlier GC on this list
-        const uint32_t h = hash_bucket(e.x, e.y, e.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
-        int slot = -1;
-        uint32_t off = 0;
-        for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
-            int4 a, c;
-            load_entry(A.hash, hp + j, a, c);
-            if (a.x == e.x && a.y == e.y && a.z == e.z && a.w != BF_FREE_ENTRY) { slot = (int)(hp + j); off = (uint32_t)c.x; break; }
-        }
-        if (slot >= 0 && off == 0) {
-            const uint32_t k = atomicAdd(&A.ctrl[C_GC_SIMPLE], 1u);
-            simple[k] = make_int4(slot, e.w, 0, 0);
-        } else {
-            const uint32_t k = atomicAdd(&A.ctrl[C_GC_LIST], 1u);
-            if (k < GC_LIST_CAP) listV[k] = block_key(e.x, e.y, e.z);
-        }
-    }
-}
+__device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV);
 
-// garbageCollectFreeKernel (:648-668), in-bucket deletes: one wave per victim frees the slot,
-// pushes the block onto the heap (appendHeap, VoxelUtilHashSDF.h:541-546) and zeroes its voxels.
-__global__ __launch_bounds__(256) void k_gc_free_simple(HashArgs A, const int4* simple) {
-    const uint32_t n = A.ctrl[C_GC_SIMPLE];
+// One launch for the GC pass: garbageCollectIdentifyKernel (:584-631, via the per-block nonzero-weight
+// count) and garbageCollectFreeKernel (:648-668). A victim sitting in its bucket with offset == 0 (the
+// classification deleteHashEntryElement, VoxelUtilHashSDF.h:739-826, needs) is freed right away by the
+// wave that found it: slot cleared, block pushed onto the heap (appendHeap, :541-546), voxels zeroed by
+// the wave. Another victim's classification reads only its own entry, which such a free never touches,
+// so the identified sets equal the two-kernel form's. Every other victim touches a collision list and is
+// queued for the serial path, which the last workgroup to finish runs (release fence + ticket, acquire on
+// the winner: the identify / free / list kernels were three launches).
+__global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* listV) {
+    const uint32_t nvis = A.ctrl[C_VISIBLE];
     const uint32_t lane = lane_id();
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t k = wave; k < n; k += nwaves) {
-        const int4 v = simple[k];
-        const uint32_t blk = (uint32_t)v.y;
-        if (lane == 0) {
-            int4* e = reinterpret_cast<int4*>(A.hash + v.x);
-            e[0] = make_int4(0, 0, 0, BF_FREE_ENTRY);
-            e[1] = make_int4(0, 0, 0, 0);
-            const uint32_t addr = atomicAdd(&A.ctrl[C_HEAP], 1u);
-            A.heap[addr + 1] = blk;
-            A.blockPos[blk] = make_int4(0, 0, 0, 0);
-            A.blockCount[blk] = 0;
+    uint32_t freed = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < nvis; base += gridDim.x * blockDim.x) {
+        const uint32_t b = base + threadIdx.x;
+        bool simple = false;
+        int slot = -1;
+        uint32_t blk = 0;
+        if (b < nvis) {
+            const int4 e = A.visible[b];
+            blk = (uint32_t)e.w;
+            if (A.blockCount[blk] == 0 && A.blockPos[blk].w != 0) {  // (pos.w == 0: already freed by an earlier GC)
+                const uint32_t h = hash_bucket(e.x, e.y, e.z, A.numBuckets), hp = h * BF_HASH_BUCKET_SIZE;
+                uint32_t off = 0;
+                for (int j = 0; j < BF_HASH_BUCKET_SIZE; j++) {
+                    int4 a, c;
+                    load_entry(A.hash, hp + j, a, c);
+                    if (a.x == e.x && a.y == e.y && a.z == e.z && a.w != BF_FREE_ENTRY) { slot = (int)(hp + j); off = (uint32_t)c.x; break; }
+                }
+                simple = slot >= 0 && off == 0;
+                if (!simple) {
+                    const uint32_t k = atomicAdd(&A.ctrl[C_GC_LIST], 1u);
+                    if (k < GC_LIST_CAP) listV[k] = block_key(e.x, e.y, e.z);
+                }
+            }
         }
-        int4* vz = reinterpret_cast<int4*>(A.voxels + (size_t)blk * BF_VOXELS_PER_BLOCK);
-        for (int q = lane; q < BF_VOXELS_PER_BLOCK * 12 / 16; q += 64) vz[q] = make_int4(0, 0, 0, 0);
+        // the wave frees its simple victims one after another, all lanes zeroing each block's voxels
+        for (unsigned long long m = __ballot(simple); m; m &= m - 1) {
+            const int src = __ffsll((long long)m) - 1;
+            const int vSlot = __shfl(slot, src);
+            const uint32_t vBlk = (uint32_t)__shfl((int)blk, src);
+            if (lane == 0) {
+                int4* e = reinterpret_cast<int4*>(A.hash + vSlot);
+                e[0] = make_int4(0, 0, 0, BF_FREE_ENTRY);
+                e[1] = make_int4(0, 0, 0, 0);
+                const uint32_t addr = atomicAdd(&A.ctrl[C_HEAP], 1u);
+                A.heap[addr + 1] = vBlk;
+                A.blockPos[vBlk] = make_int4(0, 0, 0, 0);
+                A.blockCount[vBlk] = 0;
+            }
+            int4* vz = reinterpret_cast<int4*>(A.voxels + (size_t)vBlk * BF_VOXELS_PER_BLOCK);
+            for (int q = lane; q < BF_VOXELS_PER_BLOCK * 12 / 16; q += 64) vz[q] = make_int4(0, 0, 0, 0);
+            freed++;
+        }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.stats[S_GCFREED], (unsigned long long)n);
+    if (lane == 0 && freed) atomicAdd(&A.stats[S_GCFREED], (unsigned long long)freed);
+    __shared__ bool s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(&A.ctrl[C_TICKET_GC], 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x == 0) {
+        __threadfence();
+        A.ctrl[C_TICKET_GC] = 0;
+        gc_free_list_serial(A, listV);
+    }
 }
 
 // deleteHashEntryElement collision-list cases, serial in ascending block-key order with the
-// reference's per-bucket try-lock semantics (one list delete per bucket per GC pass).
-__global__ void k_gc_free_list(HashArgs A, unsigned long long* listV) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// reference's per-bucket try-lock semantics (one list delete per bucket per GC pass); one thread, after
+// every in-bucket free of the pass
+__device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV) {
     const uint32_t n = min(A.ctrl[C_GC_LIST], GC_LIST_CAP);
     for (uint32_t a = 1; a < n; a++) {  // insertion sort (n is tiny)
         unsigned long long k = listV[a];
@@ -1896,7 +1913,6 @@ __global__ void k_gc_free_list(HashArgs A, unsigned long long* listV) {
     // the pass's last kernel re-arms the victim counters for the next GC (zero after a reset, too),
     // so GC needs no counter-reset launch of its own
     A.stats[S_GCBLOCKS] += A.ctrl[C_VISIBLE];
-    A.ctrl[C_GC_SIMPLE] = 0;
     A.ctrl[C_GC_LIST] = 0;
 }
 
@@ -1959,7 +1975,6 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     candSet_.alloc(setSize);
     candSlot_.alloc(cfg_.candCapacity);
     ovf_.alloc(OVF_CAP);
-    gcSimple_.alloc(B_);
     gcList_.alloc(GC_LIST_CAP);
     blockCount_.alloc(B_);
     hipDeviceProp_t prop;
@@ -2007,7 +2022,7 @@ size_t Scene::deviceBytes() const {
     return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
            blockMask_.bytes() + blockBirth_.bytes() + candOp_.bytes() +
            tiles_.bytes() + tiles2_.bytes() + ctrl_.bytes() +
-           stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() + gcSimple_.bytes() +
+           stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() +
            gcList_.bytes() + blockCount_.bytes();
 }
 
@@ -2197,12 +2212,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)
 void Scene::garbageCollect() {
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    const unsigned grid = (unsigned)numCUs_ * 2;
-    k_gc_identify<<<grid, 256, 0, stream_>>>(A, gcSimple_.p, gcList_.p);
-    BF_LAUNCH_CHECK();
-    k_gc_free_simple<<<grid, 256, 0, stream_>>>(A, gcSimple_.p);
-    BF_LAUNCH_CHECK();
-    k_gc_free_list<<<1, 64, 0, stream_>>>(A, gcList_.p);
+    k_gc<<<(unsigned)numCUs_ * 2, 256, 0, stream_>>>(A, gcList_.p);
     BF_LAUNCH_CHECK();
 }
 

@@ -9,7 +9,7 @@ import sys
 from collections import defaultdict
 
 SCENE = ("k_begin_ops_tiles", "k_alloc_collect_ops", "k_alloc_insert", "k_alloc_birth", "k_compactify_ops", "k_apply_ops",
-         "k_gc_identify", "k_gc_free_simple", "k_gc_free_list", "k_gc_zero")
+         "k_gc")
 INPUT = ("k_erode", "k_gauss", "k_resample", "k_depth_u16", "k_color", "k_cache_", "copyBuffer")
 
 

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from timed_region import bench_counts, region_bounds, region_end_all  # noqa: E402
 
 SCENE = ("k_begin_ops_tiles", "k_alloc_collect_ops", "k_alloc_insert", "k_alloc_birth", "k_compactify_ops",
-         "k_apply_ops", "k_gc_identify", "k_gc_free_simple", "k_gc_free_list", "k_gc_zero")
+         "k_apply_ops", "k_gc")
 
 
 def main():
