@@ -773,7 +773,9 @@ def main():
                                      "hash_probes": (rs1["hashProbes"] - rs0["hashProbes"]) / nr,
                                      "rays": (rs1["rays"] - rs0["rays"]) / nr,
                                      "splat_blocks": (rs1["splatBlocks"] - rs0["splatBlocks"]) / nr,
-                                     "splat_atomics": atomics, "k_splat_us": splat_us},
+                                     "splat_atomics": atomics, "k_splat_us": splat_us,
+                                     "march_lane_efficiency": (rs1["samples"] - rs0["samples"]) /
+                                                              max(1, rs1["waveSamples"] - rs0["waveSamples"])},
                       "roofline": {"bound": "latency", "kernel": "k_render (renderKernel)", "unit": "GB/s",
                                    "alg_bytes_per_render": rbytes, "achieved": rbytes / (k_render_us * 1e-6) / 1e9,
                                    "peak": HBM_PEAK_GBS, "frac": rbytes / (k_render_us * 1e-6) / 1e9 / HBM_PEAK_GBS,

@@ -27,7 +27,7 @@ BFMat4 mat4_inverse(const BFMat4& M);  // api.cpp
 namespace {
 
 const float MINF_F = -__builtin_inff();
-enum RenderStat { RS_SAMPLES = 0, RS_LOADS, RS_PROBES, RS_RAYS, RS_QUADS, RS_ATOMICS, RS_RENDERS, RS_PIXELS };
+enum RenderStat { RS_SAMPLES = 0, RS_LOADS, RS_PROBES, RS_RAYS, RS_QUADS, RS_ATOMICS, RS_RENDERS, RS_PIXELS, RS_WAVESAMPLES, RS_COUNT };
 
 __device__ __forceinline__ uint32_t enc_f(float f) {  // monotone float -> uint32
     const uint32_t b = __float_as_uint(f);
@@ -409,6 +409,8 @@ __global__ __launch_bounds__(TPB) BF_RENDER_ATTR void k_render(RayArgs R, BFRayC
         render_pixel(R, rp, cache, x, y, smin, smax, d_depth, d_depth4, d_normals, d_colors, outMin, outMax, rayed);
     const uint32_t s = wave_sum_u32(cache.samples), l = wave_sum_u32(cache.loads), p = wave_sum_u32(cache.probes);
     const uint32_t r = wave_sum_u32(rayed ? 1u : 0u);
+    uint32_t wmax = cache.samples;  // the wave's longest march
+    for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off));
     if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
         atomicAdd(&stats[RS_RENDERS], 1ull);
         atomicAdd(&stats[RS_PIXELS], (unsigned long long)rp.width * rp.height);
@@ -418,6 +420,7 @@ __global__ __launch_bounds__(TPB) BF_RENDER_ATTR void k_render(RayArgs R, BFRayC
         atomicAdd(&stats[RS_LOADS], (unsigned long long)l);
         atomicAdd(&stats[RS_PROBES], (unsigned long long)p);
         atomicAdd(&stats[RS_RAYS], (unsigned long long)r);
+        atomicAdd(&stats[RS_WAVESAMPLES], 64ull * wmax);
     }
 }
 
@@ -442,11 +445,12 @@ __global__ void k_normals(float4* out, const float4* in, uint32_t W, uint32_t H)
 }  // namespace
 
 void Scene::renderStats(BFRenderStats& out) {
-    uint64_t c[8];
+    uint64_t c[RS_COUNT];
     BF_HIP(hipMemcpyAsync(c, renderStats_.p, sizeof(c), hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
     out.samples = c[RS_SAMPLES]; out.voxelLoads = c[RS_LOADS]; out.hashProbes = c[RS_PROBES]; out.rays = c[RS_RAYS];
     out.splatBlocks = c[RS_QUADS]; out.splatAtomics = c[RS_ATOMICS]; out.renders = c[RS_RENDERS]; out.pixels = c[RS_PIXELS];
+    out.waveSamples = c[RS_WAVESAMPLES];
     out.timedRenders = renderClock_.enabled() ? renderClock_.launches() : 0;
     out.renderMs = renderClock_.enabled() ? renderClock_.totalMs() : 0.0;
     out.splatMs = splatClock_.enabled() ? splatClock_.totalMs() : 0.0;

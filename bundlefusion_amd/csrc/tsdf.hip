@@ -1982,7 +1982,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
-    renderStats_.alloc(8);
+    renderStats_.alloc(16);  // RenderStat counters (raycast.hip)
     BF_HIP(hipMemsetAsync(renderStats_.p, 0, renderStats_.bytes(), stream_));
     // k_integrate walks its block list with a static grid stride: size the grid to exactly the
     // resident workgroups, so every wave gets the same share in one round (no tail round)

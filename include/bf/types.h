@@ -163,6 +163,8 @@ typedef struct BFRenderStats {
     uint64_t timedRenders; /* renders timed by the clocks below (enabled by the first bf_recon_render_time) */
     double renderMs;       /* summed renderKernel device time of the timed renders */
     double splatMs;        /* summed interval-splat device time of the timed renders */
+    uint64_t waveSamples;  /* per renderKernel wave, 64 x its largest per-lane sample count: samples / waveSamples
+                              is the fraction of the wave's march steps its lanes spend on samples */
 } BFRenderStats;
 
 /* Device-side counters used by the bench to compute algorithmic bytes. */
