@@ -2407,6 +2407,7 @@ __global__ __launch_bounds__(WG) void k_dense_build(BA a, float wDepth, float wC
         const m4 t = mul44(Tiinv, Tj);
         const BFCachedFrame fi = a.cache[i], fj = a.cache[j];
         float acc[90];  // [0,21) ii upper, [21,42) jj upper, [42,78) ij (row b of i . col c of j), [78,84) jtr_i, [84,90) jtr_j
+#pragma unroll
         for (int q = 0; q < 90; q++) acc[q] = 0.0f;
         const uint32_t W = a.cw, H = a.ch;
         for (uint32_t src = threadIdx.x; src < W * H; src += blockDim.x) {
@@ -2432,7 +2433,9 @@ __global__ __launch_bounds__(WG) void k_dense_build(BA a, float wDepth, float wC
             const f3 cpt = mk3(ci[0], ci[1], ci[2]), nT = mk3(ni[0], ni[1], ni[2]);
             const float dn = nrmj.x * ni[0] + nrmj.y * ni[1] + nrmj.z * ni[2] + nrmjw * ni[3];
             if (!(dn >= a.normT && length3(s2t - cpt) <= a.distT)) continue;
-            // rows of the two terms; accumulate J^T W J and J^T W r
+            // rows of the two terms; accumulate J^T W J and J^T W r (every loop over acc unrolled: with a
+            // run-time index the 90 accumulators lived in scratch, one memory round trip per update)
+#pragma unroll
             for (int term = 0; term < 2; term++) {
                 float Ji[6] = {0, 0, 0, 0, 0, 0}, Jj[6] = {0, 0, 0, 0, 0, 0};
                 float res = 0.0f, w = 0.0f;
@@ -2461,17 +2464,23 @@ __global__ __launch_bounds__(WG) void k_dense_build(BA a, float wDepth, float wC
                     }
                     w = wColor * pw * fmaxf(0.0f, 1.0f - fabsf(res) / (1.15f * a.colT));
                 }
-                int q = 0;
+#pragma unroll
                 for (int r = 0; r < 6; r++)
-                    for (int c = r; c < 6; c++, q++) {
+#pragma unroll
+                    for (int c = r; c < 6; c++) {
+                        const int q = r * 6 - r * (r - 1) / 2 + (c - r);  // row-major upper triangle
                         acc[q] += Ji[r] * Ji[c] * w;
                         acc[21 + q] += Jj[r] * Jj[c] * w;
                     }
+#pragma unroll
                 for (int r = 0; r < 6; r++)
+#pragma unroll
                     for (int c = 0; c < 6; c++) acc[42 + r * 6 + c] += Ji[r] * Jj[c] * w;
+#pragma unroll
                 for (int r = 0; r < 6; r++) { acc[78 + r] += Ji[r] * res * w; acc[84 + r] += Jj[r] * res * w; }
             }
         }
+#pragma unroll
         for (int q = 0; q < 90; q++) {
             const float s = wave_sum(acc[q]);
             if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;

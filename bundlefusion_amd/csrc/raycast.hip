@@ -165,13 +165,13 @@ struct BlockCache {
     uint32_t samples = 0, loads = 0, probes = 0;  // render statistics (trilinear samples, voxel loads, hash probes)
     unsigned long long* table = nullptr;  // the workgroup's LDS block table (nullptr: probe every miss)
     __device__ __forceinline__ int lookup(const RayArgs& R, i3 b) {
-        if (b.x == ax && b.y == ay && b.z == az) {
-            replaceB = true;
-            return ap;
-        }
-        if (b.x == bx && b.y == by && b.z == bz) {
-            replaceB = false;
-            return bp;
+        // hits and updates as register selects: written as branches on the two entries, the compiler kept the
+        // pair {ap, bp} in scratch and read it back on every hit (a memory round trip per corner lookup)
+        const bool hitA = b.x == ax && b.y == ay && b.z == az;
+        const bool hitB = b.x == bx && b.y == by && b.z == bz;
+        if (hitA || hitB) {
+            replaceB = hitA;
+            return hitA ? ap : bp;
         }
         int p;
         unsigned long long key;
@@ -186,11 +186,9 @@ struct BlockCache {
             probes++;
             if (keyed) table[slot] = (key << 24) | (p < 0 ? 0xFFFFFFull : (unsigned long long)(uint32_t)p);
         }
-        if (replaceB) {
-            bx = b.x; by = b.y; bz = b.z; bp = p;
-        } else {
-            ax = b.x; ay = b.y; az = b.z; ap = p;
-        }
+        const bool toB = replaceB;
+        bx = toB ? b.x : bx; by = toB ? b.y : by; bz = toB ? b.z : bz; bp = toB ? p : bp;
+        ax = toB ? ax : b.x; ay = toB ? ay : b.y; az = toB ? az : b.z; ap = toB ? ap : p;
         replaceB = !replaceB;
         return p;
     }

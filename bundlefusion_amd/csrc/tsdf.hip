@@ -1764,7 +1764,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
 }
 
-__device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV);
+__device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV, uint32_t* locked);
 
 // One launch for the GC pass: garbageCollectIdentifyKernel (:584-631, via the per-block nonzero-weight
 // count) and garbageCollectFreeKernel (:648-668). A victim sitting in its bucket with offset == 0 (the
@@ -1828,17 +1828,18 @@ __global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* list
         s_last = atomicAdd(&A.ctrl[C_TICKET_GC], 1u) == gridDim.x - 1;
     }
     __syncthreads();
+    __shared__ uint32_t s_locked[64];  // the serial path's locked buckets (in LDS: a private array went to scratch)
     if (s_last && threadIdx.x == 0) {
         __threadfence();
         A.ctrl[C_TICKET_GC] = 0;
-        gc_free_list_serial(A, listV);
+        gc_free_list_serial(A, listV, s_locked);
     }
 }
 
 // deleteHashEntryElement collision-list cases, serial in ascending block-key order with the
 // reference's per-bucket try-lock semantics (one list delete per bucket per GC pass); one thread, after
 // every in-bucket free of the pass
-__device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV) {
+__device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV, uint32_t* locked) {
     const uint32_t n = min(A.ctrl[C_GC_LIST], GC_LIST_CAP);
     for (uint32_t a = 1; a < n; a++) {  // insertion sort (n is tiny)
         unsigned long long k = listV[a];
@@ -1846,7 +1847,6 @@ __device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV
         while (b >= 0 && listV[b] > k) { listV[b + 1] = listV[b]; b--; }
         listV[b + 1] = k;
     }
-    uint32_t locked[64];
     uint32_t nlocked = 0;
     auto try_lock = [&](uint32_t h) -> bool {
         for (uint32_t q = 0; q < nlocked; q++)
