@@ -1947,7 +1947,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #endif
                 const double w[3] = {qr.x, qr.y, qr.z}, t[3] = {qt.x, qt.y, qt.z};
                 double bb[6];
-                pair_block_apply(a.pstat + (size_t)rq[c].x * PSTAT, ((uint32_t)rq[c].y & PAIR_A_FLAG) != 0, w, t, bb);
+                // the pair's statistics address formed here, each iteration: hoisted out of the loop it was spilled
+                // (255 VGPRs) and reloaded from scratch every iteration
+                int px = rq[c].x;
+                asm volatile("" : "+v"(px));
+                pair_block_apply(a.pstat + (size_t)px * PSTAT, ((uint32_t)rq[c].y & PAIR_A_FLAG) != 0, w, t, bb);
 #pragma unroll
                 for (int q = 0; q < 6; q++) o[q] += bb[q];
             }
