@@ -2081,6 +2081,9 @@ constexpr int SMALL_N = 64;
 constexpr int SMALL_WG = 1024;
 __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int nLin) {
     __shared__ float sP[SMALL_N][6], sAp[SMALL_N][6];
+    // wave 0's per-row vectors live in LDS between iterations: held in registers by every wave of the 16, one
+    // of them was spilled and reloaded from scratch each iteration
+    __shared__ f3 sV[SMALL_N][6];  // dR, dT, rR, rT, mR, mT
     __shared__ int sLast;
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6, nw = SMALL_WG / 64;
@@ -2088,16 +2091,19 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
     const uint32_t npD = useDense ? a.ctrl[K_NPAIRS] : 0u;
     // wave 0, lane v: row v's vectors (row 0 and rows >= N stay zero)
     const bool own = wave == 0 && lane >= 1 && lane < a.N;
-    f3 dR = mk3(0, 0, 0), dT = dR, rR = dR, rT = dR, mR = dR, mT = dR, pR = dR, pT = dR;
-    if (wave == 0 && lane < a.N) {
+    if (wave == 0) {
+        f3 dR = mk3(0, 0, 0), dT = dR, rR = dR, rT = dR, mR = dR, mT = dR, pR = dR, pT = dR;
         if (own) {
             vload(a, V_DELTA, lane, dR, dT);
             vload(a, V_R, lane, rR, rT);
             vload(a, V_M, lane, mR, mT);
             vload(a, V_P, lane, pR, pT);
         }
-        sP[lane][0] = pR.x; sP[lane][1] = pR.y; sP[lane][2] = pR.z;
-        sP[lane][3] = pT.x; sP[lane][4] = pT.y; sP[lane][5] = pT.z;
+        sV[lane][0] = dR; sV[lane][1] = dT; sV[lane][2] = rR; sV[lane][3] = rT; sV[lane][4] = mR; sV[lane][5] = mT;
+        if (lane < a.N) {
+            sP[lane][0] = pR.x; sP[lane][1] = pR.y; sP[lane][2] = pR.z;
+            sP[lane][3] = pT.x; sP[lane][4] = pT.y; sP[lane][5] = pT.z;
+        }
     }
     float rz = ctrlf(a.ctrl, K_RDOTZ);
     int iters = 0;
@@ -2173,6 +2179,10 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
         if (wave == 0) {
             const f3 aR = own ? mk3(sAp[lane][0], sAp[lane][1], sAp[lane][2]) : mk3(0, 0, 0);
             const f3 aT = own ? mk3(sAp[lane][3], sAp[lane][4], sAp[lane][5]) : mk3(0, 0, 0);
+            f3 pR = own ? mk3(sP[lane][0], sP[lane][1], sP[lane][2]) : mk3(0, 0, 0);
+            f3 pT = own ? mk3(sP[lane][3], sP[lane][4], sP[lane][5]) : mk3(0, 0, 0);
+            f3 dR = sV[lane][0], dT = sV[lane][1], rR = sV[lane][2], rT = sV[lane][3];
+            const f3 mR = sV[lane][4], mT = sV[lane][5];
             const float pAp = wave_sum(dot3(pR, aR) + dot3(pT, aT));
             const float alpha = (pAp > FLOAT_EPSILON) ? rz / pAp : 0.0f;
             dR = dR + alpha * pR;
@@ -2189,6 +2199,7 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
                 sP[lane][0] = pR.x; sP[lane][1] = pR.y; sP[lane][2] = pR.z;
                 sP[lane][3] = pT.x; sP[lane][4] = pT.y; sP[lane][5] = pT.z;
             }
+            sV[lane][0] = dR; sV[lane][1] = dT; sV[lane][2] = rR; sV[lane][3] = rT;
             rz = rzNew;
             if (lane == 0) sLast = last ? 1 : 0;
         }
@@ -2197,9 +2208,10 @@ __global__ __launch_bounds__(SMALL_WG) void k_pcg_small(BA a, float wSparse, int
         if (sLast) break;
     }
     if (own) {
+        const f3 dR = sV[lane][0], dT = sV[lane][1];
         vstore(a, V_DELTA, lane, dR, dT);
-        vstore(a, V_R, lane, rR, rT);
-        vstore(a, V_P, lane, pR, pT);
+        vstore(a, V_R, lane, sV[lane][2], sV[lane][3]);
+        vstore(a, V_P, lane, mk3(sP[lane][0], sP[lane][1], sP[lane][2]), mk3(sP[lane][3], sP[lane][4], sP[lane][5]));
         // computeLieUpdate (LieDerivUtil.h:301-307) on the exiting iteration
         f3 nr, nt;
         lie_update(dR, dT, mk3(a.rot[3 * lane], a.rot[3 * lane + 1], a.rot[3 * lane + 2]),

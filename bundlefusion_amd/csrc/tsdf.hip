@@ -607,6 +607,9 @@ __device__ __forceinline__ unsigned long long alloc_walk_direct(const HashArgs& 
     return emitted;
 }
 constexpr int ALLOC_OVF = 256;  // per tile: keys the congested LDS set could not place, tested in phase 2
+#ifndef BF_ALLOC_PIPE
+#define BF_ALLOC_PIPE 0
+#endif
 __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __restrict__ depthImg,
                                               const BFDepthCameraParams& cam, const BFMat4& T, const BFMat4& Tinv,
                                               unsigned long long* __restrict__ cand, uint32_t candCap,
@@ -651,6 +654,12 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         const uint32_t j = atomicAdd(&s_novf, 1u);
         if (j < (uint32_t)ALLOC_OVF) set[LDS_SET + j] = key;
     };
+#if BF_ALLOC_PIPE
+    // (A/B) the CAS results of a trip are checked in the next one, after its own CAS are issued, so the LDS
+    // round trip overlaps the next two DDA steps; the set ends up with the same keys
+    unsigned long long pKeyA = EMPTY_KEY, pKeyB = EMPTY_KEY, pOldA = EMPTY_KEY, pOldB = EMPTY_KEY;
+    uint32_t pHA = 0, pHB = 0;
+#endif
     for (uint32_t iter = 0; iter < 512; iter++) {
         if (!__any(r.active)) break;
         const bool actA = r.active;
@@ -665,9 +674,20 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         const uint32_t hA = slot_of(idA), hB = slot_of(idB);
         const unsigned long long oldA = doA ? atomicCAS(&set[hA], EMPTY_KEY, keyA) : EMPTY_KEY;
         const unsigned long long oldB = doB ? atomicCAS(&set[hB], EMPTY_KEY, keyB) : EMPTY_KEY;
+#if BF_ALLOC_PIPE
+        if (pKeyA != EMPTY_KEY && pOldA != EMPTY_KEY && pOldA != pKeyA) finish_insert(pKeyA, pHA);
+        if (pKeyB != EMPTY_KEY && pOldB != EMPTY_KEY && pOldB != pKeyB) finish_insert(pKeyB, pHB);
+        pKeyA = doA ? keyA : EMPTY_KEY; pOldA = oldA; pHA = hA;
+        pKeyB = doB ? keyB : EMPTY_KEY; pOldB = oldB; pHB = hB;
+#else
         if (doA && oldA != EMPTY_KEY && oldA != keyA) finish_insert(keyA, hA);
         if (doB && oldB != EMPTY_KEY && oldB != keyB) finish_insert(keyB, hB);
+#endif
     }
+#if BF_ALLOC_PIPE
+    if (pKeyA != EMPTY_KEY && pOldA != EMPTY_KEY && pOldA != pKeyA) finish_insert(pKeyA, pHA);
+    if (pKeyB != EMPTY_KEY && pOldB != EMPTY_KEY && pOldB != pKeyB) finish_insert(pKeyB, pHB);
+#endif
     // phase 2: compact the distinct blocks to the front of the set, append the overflow keys, then every
     // thread checks one of them against the hash (one round of parallel lookups per 256 distinct blocks —
     // a tile reaches far fewer — instead of a round per 256 slots, each waiting on its hash loads) and
