@@ -158,7 +158,7 @@ class BFSolverOptions(C.Structure):
                 ("normalEquations", C.c_int32), ("disableEarlyOut", C.c_int32),
                 ("pcgLaunch", C.c_int32), ("pcgSpinLimitUs", C.c_uint32)]
 
-ABI_VERSION = 2  # include/bf/bf.h BF_ABI_VERSION: the struct layouts above
+ABI_VERSION = 3  # include/bf/bf.h BF_ABI_VERSION: the struct layouts above
 SOLVE_ERR_PAIR_BOUND, SOLVE_ERR_PCG_TIMEOUT, SOLVE_PCG_RECOVERED = 4, 8, 16  # BFSolveResult.error bits
 SOLVE_ERR_FATAL = 0xFFFFFFFF & ~SOLVE_PCG_RECOVERED
 

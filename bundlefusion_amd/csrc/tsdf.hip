@@ -610,6 +610,9 @@ constexpr int ALLOC_OVF = 256;  // per tile: keys the congested LDS set could no
 #ifndef BF_ALLOC_PIPE
 #define BF_ALLOC_PIPE 0
 #endif
+#ifndef BF_ALLOC_DPP
+#define BF_ALLOC_DPP 0
+#endif
 __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __restrict__ depthImg,
                                               const BFDepthCameraParams& cam, const BFMat4& T, const BFMat4& Tinv,
                                               unsigned long long* __restrict__ cand, uint32_t candCap,
@@ -638,10 +641,21 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
     // LDS round trip per two blocks (probing past a taken slot, rare, follows per step). Which lane
     // inserts a key and in what order changes nothing: the set ends up holding the same keys, and a
     // key that finds no slot goes to the tile's overflow list (phase 2 tests it like the set's keys).
+#if BF_ALLOC_DPP
+    // (A/B) the left neighbour only, through DPP row_shr:1 (a wave's 16-lane DPP rows are the tile's pixel
+    // rows): no LDS-queue shuffle, whose wait also waited for the outstanding set CAS
+    auto is_dup = [&](unsigned long long myKey) {
+        const uint32_t lo = (uint32_t)myKey, hi = (uint32_t)(myKey >> 32);
+        const uint32_t llo = (uint32_t)__builtin_amdgcn_update_dpp((int)~lo, (int)lo, 0x111, 0xf, 0xf, false);
+        const uint32_t lhi = (uint32_t)__builtin_amdgcn_update_dpp((int)~hi, (int)hi, 0x111, 0xf, 0xf, false);
+        return llo == lo && lhi == hi;
+    };
+#else
     auto is_dup = [&](unsigned long long myKey) {
         const unsigned long long left = __shfl_up(myKey, 1, ALLOC_TILE), up = __shfl_up(myKey, ALLOC_TILE);
         return ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
     };
+#endif
     // slot from the low coordinate bits (3 + 4 + 3 = 10 bits = LDS_SET): the blocks one 16x16-pixel
     // tile reaches span a few blocks per axis, so they land in distinct slots without a mixing hash
     auto slot_of = [](i3 b) { return ((uint32_t)b.x & 7u) | (((uint32_t)b.y & 15u) << 3) | (((uint32_t)b.z & 7u) << 7); };
@@ -1462,6 +1476,9 @@ __global__ __launch_bounds__(256) BF_COMPACTIFY_ATTR void k_compactify_ops(HashA
             // the voxel pass applies an op to a block half by half (4 z-slices per round)
 #if BF_APPLY_QMASK
             const uint32_t hb = block_may_update_quarters(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
+#elif defined(BF_CULL_DIAG_NOBAND)  // timing diagnostic only (wrong masks): the scan without the band cull
+            const uint32_t hb = 3u;
+            (void)Ti; (void)b;
 #else
             const uint32_t hb = block_may_update_halves(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
 #endif

@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define BF_ABI_VERSION 2  /* 2: BFSolverOptions.pcgSpinLimitUs, BFCorrOptions.minPerPair */
+#define BF_ABI_VERSION 3  /* 2: BFSolverOptions.pcgSpinLimitUs, BFCorrOptions.minPerPair; 3: BFReconStats.globalPcgLaunches /
+                             globalPcgKernelMs, BFTsdfStats.batchHalves, BFRenderStats.waveSamples, BFAppTiming */
 
 /* ---- runtime ------------------------------------------------------------- */
 int bf_abi_version(void);

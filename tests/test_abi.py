@@ -11,7 +11,7 @@ from bundlefusion_amd import abi
 def test_library_exists_and_loads():
     assert os.path.exists(abi.LIB_PATH)
     L = bfa.lib()
-    assert L.bf_abi_version() == 2
+    assert L.bf_abi_version() == 3
 
 
 def test_every_declared_symbol_is_exported():
