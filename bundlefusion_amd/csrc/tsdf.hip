@@ -607,12 +607,6 @@ __device__ __forceinline__ unsigned long long alloc_walk_direct(const HashArgs& 
     return emitted;
 }
 constexpr int ALLOC_OVF = 256;  // per tile: keys the congested LDS set could not place, tested in phase 2
-#ifndef BF_ALLOC_PIPE
-#define BF_ALLOC_PIPE 0
-#endif
-#ifndef BF_ALLOC_DPP
-#define BF_ALLOC_DPP 0
-#endif
 __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __restrict__ depthImg,
                                               const BFDepthCameraParams& cam, const BFMat4& T, const BFMat4& Tinv,
                                               unsigned long long* __restrict__ cand, uint32_t candCap,
@@ -641,21 +635,10 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
     // LDS round trip per two blocks (probing past a taken slot, rare, follows per step). Which lane
     // inserts a key and in what order changes nothing: the set ends up holding the same keys, and a
     // key that finds no slot goes to the tile's overflow list (phase 2 tests it like the set's keys).
-#if BF_ALLOC_DPP
-    // (A/B) the left neighbour only, through DPP row_shr:1 (a wave's 16-lane DPP rows are the tile's pixel
-    // rows): no LDS-queue shuffle, whose wait also waited for the outstanding set CAS
-    auto is_dup = [&](unsigned long long myKey) {
-        const uint32_t lo = (uint32_t)myKey, hi = (uint32_t)(myKey >> 32);
-        const uint32_t llo = (uint32_t)__builtin_amdgcn_update_dpp((int)~lo, (int)lo, 0x111, 0xf, 0xf, false);
-        const uint32_t lhi = (uint32_t)__builtin_amdgcn_update_dpp((int)~hi, (int)hi, 0x111, 0xf, 0xf, false);
-        return llo == lo && lhi == hi;
-    };
-#else
     auto is_dup = [&](unsigned long long myKey) {
         const unsigned long long left = __shfl_up(myKey, 1, ALLOC_TILE), up = __shfl_up(myKey, ALLOC_TILE);
         return ((lane % ALLOC_TILE) != 0 && left == myKey) || (lane >= ALLOC_TILE && up == myKey);
     };
-#endif
     // slot from the low coordinate bits (3 + 4 + 3 = 10 bits = LDS_SET): the blocks one 16x16-pixel
     // tile reaches span a few blocks per axis, so they land in distinct slots without a mixing hash
     auto slot_of = [](i3 b) { return ((uint32_t)b.x & 7u) | (((uint32_t)b.y & 15u) << 3) | (((uint32_t)b.z & 7u) << 7); };
@@ -668,12 +651,6 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         const uint32_t j = atomicAdd(&s_novf, 1u);
         if (j < (uint32_t)ALLOC_OVF) set[LDS_SET + j] = key;
     };
-#if BF_ALLOC_PIPE
-    // (A/B) the CAS results of a trip are checked in the next one, after its own CAS are issued, so the LDS
-    // round trip overlaps the next two DDA steps; the set ends up with the same keys
-    unsigned long long pKeyA = EMPTY_KEY, pKeyB = EMPTY_KEY, pOldA = EMPTY_KEY, pOldB = EMPTY_KEY;
-    uint32_t pHA = 0, pHB = 0;
-#endif
     for (uint32_t iter = 0; iter < 512; iter++) {
         if (!__any(r.active)) break;
         const bool actA = r.active;
@@ -688,20 +665,9 @@ __device__ __forceinline__ void alloc_collect(const HashArgs& A, const float* __
         const uint32_t hA = slot_of(idA), hB = slot_of(idB);
         const unsigned long long oldA = doA ? atomicCAS(&set[hA], EMPTY_KEY, keyA) : EMPTY_KEY;
         const unsigned long long oldB = doB ? atomicCAS(&set[hB], EMPTY_KEY, keyB) : EMPTY_KEY;
-#if BF_ALLOC_PIPE
-        if (pKeyA != EMPTY_KEY && pOldA != EMPTY_KEY && pOldA != pKeyA) finish_insert(pKeyA, pHA);
-        if (pKeyB != EMPTY_KEY && pOldB != EMPTY_KEY && pOldB != pKeyB) finish_insert(pKeyB, pHB);
-        pKeyA = doA ? keyA : EMPTY_KEY; pOldA = oldA; pHA = hA;
-        pKeyB = doB ? keyB : EMPTY_KEY; pOldB = oldB; pHB = hB;
-#else
         if (doA && oldA != EMPTY_KEY && oldA != keyA) finish_insert(keyA, hA);
         if (doB && oldB != EMPTY_KEY && oldB != keyB) finish_insert(keyB, hB);
-#endif
     }
-#if BF_ALLOC_PIPE
-    if (pKeyA != EMPTY_KEY && pOldA != EMPTY_KEY && pOldA != pKeyA) finish_insert(pKeyA, pHA);
-    if (pKeyB != EMPTY_KEY && pOldB != EMPTY_KEY && pOldB != pKeyB) finish_insert(pKeyB, pHB);
-#endif
     // phase 2: compact the distinct blocks to the front of the set, append the overflow keys, then every
     // thread checks one of them against the hash (one round of parallel lookups per 256 distinct blocks —
     // a tile reaches far fewer — instead of a round per 256 slots, each waiting on its hash loads) and
