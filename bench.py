@@ -775,7 +775,9 @@ def main():
                                      "splat_blocks": (rs1["splatBlocks"] - rs0["splatBlocks"]) / nr,
                                      "splat_atomics": atomics, "k_splat_us": splat_us,
                                      "march_lane_efficiency": (rs1["samples"] - rs0["samples"]) /
-                                                              max(1, rs1["waveSamples"] - rs0["waveSamples"])},
+                                                              max(1, rs1["waveSamples"] - rs0["waveSamples"]),
+                                     "long_waves": (rs1["longWaves"] - rs0["longWaves"]) / nr,
+                                     "wave_samples_max": rs1["waveSamplesMax"]},
                       "roofline": {"bound": "latency", "kernel": "k_render (renderKernel)", "unit": "GB/s",
                                    "alg_bytes_per_render": rbytes, "achieved": rbytes / (k_render_us * 1e-6) / 1e9,
                                    "peak": HBM_PEAK_GBS, "frac": rbytes / (k_render_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
@@ -783,9 +785,12 @@ def main():
                                    "note": "SURVEY 8(d): 96 B per trilinear sample + 52 B per pixel; a sample's voxels "
                                            "are dependent loads of one ray (hash probe -> 8 corners -> next step), so "
                                            "the march is bound by load latency, not bandwidth"},
-                      "splat_roofline": {"kernel": "k_splat (ray-interval splat)", "atomics_per_render": atomics,
-                                         "atomics_per_us": atomics / max(1e-9, splat_us),
-                                         "note": "per covered pixel one atomic min (near pass) and one atomic max (far pass), issued without waiting for a return value"},
+                      "splat_roofline": {"kernel": "k_splat_quads + k_splat_tiles (ray-interval splat)",
+                                         "pixel_updates_per_render": atomics,
+                                         "pixel_updates_per_us": atomics / max(1e-9, splat_us),
+                                         "note": "per covered pixel one min (near pass) and one max (far pass), folded in "
+                                                 "registers per 64x20 tile from the block rectangles that overlap it "
+                                                 "(BF_SPLAT_ATOMIC=1: one global atomic each)"},
                       "note": f"compactify + interval splat + renderKernel + computeNormals at {W_}x{H_} from the last pose"}
     # marching cubes over the final scene (StopScanningAndExtractIsoSurfaceMC, reported beside the metric)
     mcp = bfa.mc_params(params.virtualVoxelSize)

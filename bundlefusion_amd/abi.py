@@ -236,7 +236,8 @@ class BFReconOptions(C.Structure):
 class BFRenderStats(C.Structure):  # include/bf/bf.h
     _fields_ = [(n, C.c_uint64) for n in ("samples", "voxelLoads", "hashProbes", "rays", "splatBlocks", "splatAtomics",
                                           "renders", "pixels", "timedRenders")] + [
-        ("renderMs", C.c_double), ("splatMs", C.c_double), ("waveSamples", C.c_uint64)]
+        ("renderMs", C.c_double), ("splatMs", C.c_double), ("waveSamples", C.c_uint64),
+        ("waveSamplesMax", C.c_uint64), ("longWaves", C.c_uint64)]
 
 
 class BFEndSequenceOptions(C.Structure):  # include/bf/bf.h: the render loop past the last frame

@@ -19,6 +19,8 @@
 #include <cstdlib>
 
 #include <cstring>
+#include <cstdio>
+#include <vector>
 
 namespace bf {
 
@@ -27,7 +29,17 @@ BFMat4 mat4_inverse(const BFMat4& M);  // api.cpp
 namespace {
 
 const float MINF_F = -__builtin_inff();
-enum RenderStat { RS_SAMPLES = 0, RS_LOADS, RS_PROBES, RS_RAYS, RS_QUADS, RS_ATOMICS, RS_RENDERS, RS_PIXELS, RS_WAVESAMPLES, RS_COUNT };
+enum RenderStat { RS_SAMPLES = 0, RS_LOADS, RS_PROBES, RS_RAYS, RS_QUADS, RS_ATOMICS, RS_RENDERS, RS_PIXELS, RS_WAVESAMPLES, RS_WAVEMAX, RS_LONGWAVES, RS_COUNT };
+
+static_assert(RS_COUNT <= Scene::kRenderStatFields, "render counters per slot");
+// Counter updates: one workgroup's counters are summed in LDS and added to one of kRenderStatSlots slots
+// (workgroup index mod slots; renderStats sums them). Device-scope atomics on one address serialise: with
+// every wave of k_render adding its 7 counters to the same 7 words (34 k atomics per render) the waves
+// drained through that queue one after another, and the kernel took 320 us for a march whose fastest waves
+// end in 23 us (BF_RENDER_WAVE_LOG, gpurun_out/s36)
+__device__ __forceinline__ unsigned long long* rs_slot(unsigned long long* stats) {
+    return stats + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % (uint32_t)Scene::kRenderStatSlots) * Scene::kRenderStatFields;
+}
 
 __device__ __forceinline__ uint32_t enc_f(float f) {  // monotone float -> uint32
     const uint32_t b = __float_as_uint(f);
@@ -46,6 +58,7 @@ struct RayArgs {
     uint32_t numBuckets, numEntries, maxList;
     float voxelSize;
     uint32_t ldsTable;  // 1: the workgroup's LDS block table may hold heap indices (numBlocks < 2^24 - 1)
+    unsigned long long* waveLog;  // diagnostics (BF_RENDER_WAVE_LOG): per wave {start, end, __smid, longest march}
 };
 
 // The workgroup's block table in LDS: the rays of a 16x16 tile cross the same blocks, so a block one ray
@@ -150,29 +163,193 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
         }
     }
     if (lane == 0 && quads) {
-        atomicAdd(&stats[RS_QUADS], (unsigned long long)quads);
-        atomicAdd(&stats[RS_ATOMICS], (unsigned long long)atoms);
+        atomicAdd(&rs_slot(stats)[RS_QUADS], (unsigned long long)quads);
+        atomicAdd(&rs_slot(stats)[RS_ATOMICS], (unsigned long long)atoms);
     }
 }
 
-// getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417) with a two-entry per-thread block cache: a trilinear
-// sample's corners straddle a block face about a third of the time, and a one-entry cache re-probed the hash
-// as the corners alternated between the two blocks (up to six probes per sample instead of two)
+// The same splat binned by screen tile, without global atomics: k_splat_quads writes each visible block's
+// covered pixel rectangle and encoded depths (one thread per block, rayIntervalSplatKernel's projection and
+// tests as above); k_splat_tiles gives each workgroup a 64x20 pixel tile that scans every rectangle, keeps
+// the ones overlapping its tile in LDS, and folds them into per-pixel min / max held in registers, then writes
+// each pixel once. k_splat issued one atomic min and max per covered pixel (8.9 M per render on the bench
+// scene, ~30 per pixel, all to HBM); here the traffic is the rectangle list read once per tile (from L2) and
+// one store per pixel, and k_splat_clear is not needed. A pass a block does not take carries the clear value
+// (enc(+inf) for min, enc(-inf) for max), which leaves the pixel unchanged, so the result is the same
+// order-independent min / max as the atomics'
+constexpr int ST_W = 64, ST_H = 20, ST_PX = ST_W * ST_H / 256, ST_Q = 16;  // tile, pixels per thread, rectangles per thread per chunk
+__global__ __launch_bounds__(256) void k_splat_quads(const int4* __restrict__ visible, const uint32_t* ctrl, float voxelSize,
+                                                     BFDepthCameraParams cam, BFRayCastParams rp, int4* quads,
+                                                     unsigned long long* stats) {
+    const uint32_t n = ctrl[C_VISIBLE];
+    uint32_t nq = 0, npix = 0;
+    const BFMat4 V = rp.viewMatrix;
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < n; b += gridDim.x * blockDim.x) {
+        int4 out = make_int4(0xFFFF, 0, 0, 0);  // an empty rectangle (x0 > x1)
+        const int4 e = visible[b];
+        if (block_in_frustum(cam, V, e.x, e.y, e.z, voxelSize)) {
+            const f3 wv = block_to_world(e.x, e.y, e.z, voxelSize);
+            const float hv = voxelSize / 2.0f;
+            const f3 MINV = mk3(wv.x - hv, wv.y - hv, wv.z - hv);
+            const float ext = (float)BF_SDF_BLOCK_SIZE * voxelSize;
+            const f3 maxv = mk3(MINV.x + ext, MINV.y + ext, MINV.z + ext);
+            const f3 p000 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, MINV.y, MINV.z)));
+            const f3 p100 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, MINV.y, MINV.z)));
+            const f3 p010 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, maxv.y, MINV.z)));
+            const f3 p001 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, MINV.y, maxv.z)));
+            const f3 p110 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, maxv.y, MINV.z)));
+            const f3 p011 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, maxv.y, maxv.z)));
+            const f3 p101 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, MINV.y, maxv.z)));
+            const f3 p111 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, maxv.y, maxv.z)));
+            const f3 mn = fmin3(fmin3(fmin3(p000, p100), fmin3(p010, p001)), fmin3(fmin3(p110, p011), fmin3(p101, p111)));
+            const f3 mx = fmax3(fmax3(fmax3(p000, p100), fmax3(p010, p001)), fmax3(fmax3(p110, p011), fmax3(p101, p111)));
+            const float dwMin = mn.z * (rp.maxDepth - rp.minDepth) + rp.minDepth;
+            const float dwMax = mx.z * (rp.maxDepth - rp.minDepth) + rp.minDepth;
+            const bool minOk = mn.z < 1.0f, maxOk = mx.z > 0.0f;
+            const float W = (float)rp.width, H = (float)rp.height;
+            const float left = (mn.x + 1.0f) * 0.5f * W, right = (mx.x + 1.0f) * 0.5f * W;
+            const float top = (1.0f - mx.y) * 0.5f * H, bottom = (1.0f - mn.y) * 0.5f * H;
+            if ((minOk || maxOk) && left < right && top < bottom) {
+                const float fx0 = ceilf(left - 0.5f), fx1 = ceilf(right - 0.5f) - 1.0f;
+                const float fy0 = ceilf(top - 0.5f), fy1 = ceilf(bottom - 0.5f) - 1.0f;
+                if (!(fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f)) {
+                    const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
+                    const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
+                    if (x1 >= x0 && y1 >= y0) {
+                        out = make_int4(x0 | (y0 << 16), x1 | (y1 << 16), (int)(minOk ? enc_f(dwMin) : enc_f(__builtin_inff())),
+                                        (int)(maxOk ? enc_f(dwMax) : enc_f(-__builtin_inff())));
+                        nq++;
+                        npix += (uint32_t)(x1 - x0 + 1) * (uint32_t)(y1 - y0 + 1) * ((minOk ? 1u : 0u) + (maxOk ? 1u : 0u));
+                    }
+                }
+            }
+        }
+        quads[b] = out;
+    }
+    __shared__ unsigned long long s_st[2];
+    if (threadIdx.x < 2) s_st[threadIdx.x] = 0;
+    __syncthreads();
+    nq = wave_sum_u32(nq);
+    npix = wave_sum_u32(npix);
+    if ((threadIdx.x & 63) == 0 && nq) {
+        atomicAdd(&s_st[0], (unsigned long long)nq);
+        atomicAdd(&s_st[1], (unsigned long long)npix);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_st[0]) {
+        atomicAdd(&rs_slot(stats)[RS_QUADS], s_st[0]);
+        atomicAdd(&rs_slot(stats)[RS_ATOMICS], s_st[1]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_splat_tiles(const int4* __restrict__ quads, const uint32_t* ctrl, uint32_t W, uint32_t H,
+                                                     uint32_t* smin, uint32_t* smax) {
+    const uint32_t n = ctrl[C_VISIBLE];
+    const int tx0 = (int)blockIdx.x * ST_W, ty0 = (int)blockIdx.y * ST_H;
+    const int tx1 = min(tx0 + ST_W, (int)W) - 1, ty1 = min(ty0 + ST_H, (int)H) - 1;
+    const int px = tx0 + (int)(threadIdx.x & 63), py0 = ty0 + (int)(threadIdx.x >> 6);  // rows py0 + 4 i
+    uint32_t mn[ST_PX], mx[ST_PX];
+#pragma unroll
+    for (int i = 0; i < ST_PX; i++) { mn[i] = enc_f(__builtin_inff()); mx[i] = enc_f(-__builtin_inff()); }
+    __shared__ int4 s_list[256 * ST_Q];
+    __shared__ uint32_t s_cnt;
+    // the next chunk's rectangles are loaded while this chunk's are folded (the scan is L2-latency bound otherwise)
+    // (a load from a clamped index, then a select: `idx < n ? quads[idx] : EMPTY` became a select between a global
+    // and a private address, i.e. flat loads and a scratch copy of EMPTY)
+    int4 q[ST_Q];
+    const uint32_t last = n ? n - 1u : 0u;
+    auto fetch = [&](uint32_t idx) {
+        const int4 v = quads[min(idx, last)];
+        return idx < n ? v : make_int4(0xFFFF, 0, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < ST_Q; i++) q[i] = fetch((uint32_t)i * 256u + threadIdx.x);
+    // the barriers order LDS only: __syncthreads() also waits for every outstanding global load, which made each
+    // chunk wait for the next chunk's prefetch (one L2 round trip per chunk: 133 us per render)
+    auto lds_barrier = [] {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t base = 0; base < n; base += 256u * ST_Q) {
+        if (threadIdx.x == 0) s_cnt = 0;
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < ST_Q; i++) {
+            const int x0 = q[i].x & 0xFFFF, y0 = q[i].x >> 16, x1 = q[i].y & 0xFFFF, y1 = q[i].y >> 16;
+            const bool hit = x0 <= tx1 && x1 >= tx0 && y0 <= ty1 && y1 >= ty0;
+            const unsigned long long m = __ballot(hit);  // one LDS atomic per wave and rectangle slot that has hits
+            if (m) {
+                const uint32_t first = (uint32_t)__builtin_ctzll(m);
+                uint32_t at = 0;
+                if (lane == first) at = atomicAdd(&s_cnt, (uint32_t)__builtin_popcountll(m));
+                at = (uint32_t)__shfl((int)at, (int)first);
+                if (hit) s_list[at + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = q[i];
+            }
+        }
+        const uint32_t next = base + 256u * ST_Q;
+#pragma unroll
+        for (int i = 0; i < ST_Q; i++) q[i] = fetch(next + (uint32_t)i * 256u + threadIdx.x);
+        lds_barrier();
+        const uint32_t c = s_cnt;
+        auto fold = [&](const int4 r) {
+            const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+            if (px < x0 || px > x1) return;
+#pragma unroll
+            for (int i = 0; i < ST_PX; i++) {
+                const int py = py0 + 4 * i;
+                if (py >= y0 && py <= y1) {
+                    mn[i] = min(mn[i], (uint32_t)r.z);
+                    mx[i] = max(mx[i], (uint32_t)r.w);
+                }
+            }
+        };
+        uint32_t e = 0;
+        for (; e + 4u <= c; e += 4u) {  // four list reads in flight per wait
+            const int4 r0 = s_list[e], r1 = s_list[e + 1], r2 = s_list[e + 2], r3 = s_list[e + 3];
+            fold(r0); fold(r1); fold(r2); fold(r3);
+        }
+        for (; e < c; e++) fold(s_list[e]);
+        lds_barrier();  // every wave has read s_cnt and the list before the next chunk resets them
+    }
+    if (px >= (int)W) return;
+#pragma unroll
+    for (int i = 0; i < ST_PX; i++) {
+        const int py = py0 + 4 * i;
+        if (py < (int)H) {
+            smin[(uint32_t)py * W + (uint32_t)px] = mn[i];
+            smax[(uint32_t)py * W + (uint32_t)px] = mx[i];
+        }
+    }
+}
+
+// getVoxel(worldPos) (VoxelUtilHashSDF.h:406-417)'s block lookup with a two-entry per-thread block cache: a
+// trilinear sample's corners straddle a block face about a third of the time, and a one-entry cache re-probed
+// the hash as the corners alternated between the two blocks
+#ifndef BF_RENDER_CACHE
+#define BF_RENDER_CACHE 1  // per-thread register cache entries (A/B builds: 2)
+#endif
 struct BlockCache {
     int ax = INT_MIN, ay = 0, az = 0, ap = BF_FREE_ENTRY;  // entry A
+#if BF_RENDER_CACHE == 2
     int bx = INT_MIN, by = 0, bz = 0, bp = BF_FREE_ENTRY;  // entry B
     bool replaceB = false;  // the entry a miss replaces (the one not used last)
+#endif
     uint32_t samples = 0, loads = 0, probes = 0;  // render statistics (trilinear samples, voxel loads, hash probes)
     unsigned long long* table = nullptr;  // the workgroup's LDS block table (nullptr: probe every miss)
     __device__ __forceinline__ int lookup(const RayArgs& R, i3 b) {
         // hits and updates as register selects: written as branches on the two entries, the compiler kept the
         // pair {ap, bp} in scratch and read it back on every hit (a memory round trip per corner lookup)
         const bool hitA = b.x == ax && b.y == ay && b.z == az;
+#if BF_RENDER_CACHE == 2
         const bool hitB = b.x == bx && b.y == by && b.z == bz;
         if (hitA || hitB) {
             replaceB = hitA;
             return hitA ? ap : bp;
         }
+#else
+        if (hitA) return ap;
+#endif
         int p;
         unsigned long long key;
         const bool keyed = table && rc_key(b, key);
@@ -186,43 +363,20 @@ struct BlockCache {
             probes++;
             if (keyed) table[slot] = (key << 24) | (p < 0 ? 0xFFFFFFull : (unsigned long long)(uint32_t)p);
         }
+#if BF_RENDER_CACHE == 2
         const bool toB = replaceB;
         bx = toB ? b.x : bx; by = toB ? b.y : by; bz = toB ? b.z : bz; bp = toB ? p : bp;
         ax = toB ? ax : b.x; ay = toB ? ay : b.y; az = toB ? az : b.z; ap = toB ? ap : p;
         replaceB = !replaceB;
+#else
+        ax = b.x; ay = b.y; az = b.z; ap = p;
+#endif
         return p;
     }
 };
-__device__ __forceinline__ void get_voxel(const RayArgs& R, BlockCache& c, f3 pos, float& sdf, float& weight, uint32_t& color) {
-    const i3 v = world_to_vvox(pos, R.voxelSize);
-    const i3 b = vvox_to_block(v);
-    const int ptr = c.lookup(R, b);
-    if (ptr == BF_FREE_ENTRY) {  // deleteVoxel
-        sdf = 0.0f; weight = 0.0f; color = 0u;
-        return;
-    }
-    int lx = v.x % BF_SDF_BLOCK_SIZE, ly = v.y % BF_SDF_BLOCK_SIZE, lz = v.z % BF_SDF_BLOCK_SIZE;
-    if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
-    if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
-    if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
-    const BFVoxel* vp = R.voxels + (size_t)ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
-    c.loads++;
-    sdf = vp->sdf;
-    weight = vp->weight;
-    color = *reinterpret_cast<const uint32_t*>(vp->color);
-}
-
-// the voxel of worldPos without loading it: nullptr for a free block (deleteVoxel: sdf 0, weight 0)
-__device__ __forceinline__ const BFVoxel* voxel_ptr(const RayArgs& R, BlockCache& c, f3 pos) {
-    const i3 v = world_to_vvox(pos, R.voxelSize);
-    const i3 b = vvox_to_block(v);
-    const int ptr = c.lookup(R, b);
-    if (ptr == BF_FREE_ENTRY) return nullptr;
-    int lx = v.x % BF_SDF_BLOCK_SIZE, ly = v.y % BF_SDF_BLOCK_SIZE, lz = v.z % BF_SDF_BLOCK_SIZE;
-    if (lx < 0) lx += BF_SDF_BLOCK_SIZE;
-    if (ly < 0) ly += BF_SDF_BLOCK_SIZE;
-    if (lz < 0) lz += BF_SDF_BLOCK_SIZE;
-    return R.voxels + (size_t)ptr * BF_VOXELS_PER_BLOCK + (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
+__device__ __forceinline__ int local_mod(int v) {  // v mod SDF_BLOCK_SIZE in [0, 8) (getVoxel's virtualVoxelPosToLocalSDFBlockIndex)
+    int l = v % BF_SDF_BLOCK_SIZE;
+    return l < 0 ? l + BF_SDF_BLOCK_SIZE : l;
 }
 
 __device__ __forceinline__ float frac1(float v) { return v - floorf(v); }
@@ -243,20 +397,47 @@ __device__ __forceinline__ bool trilinear(const RayArgs& R, BlockCache& c, f3 po
         return mk3((k == 1 || k == 4 || k == 6 || k == 7) ? oSet : 0.0f, (k == 2 || k == 4 || k == 5 || k == 7) ? oSet : 0.0f,
                    (k == 3 || k == 5 || k == 6 || k == 7) ? oSet : 0.0f);
     };
-    // the 8 corners' voxels located first (hash probes only where the block changes), then loaded
-    // together: the reference reads them one after another and stops at the first zero weight, which
-    // made each load wait for the previous one; the sums below keep its order and its stop
+    // the 8 corners' voxels located first (hash probes only where the block changes), then loaded together: the
+    // reference reads them one after another and stops at the first zero weight, which made each load wait for
+    // the previous one; the sums below keep its order and its stop.
+    // Corner k is posDual + offs(k), added per component, so its virtual voxel takes on each axis either corner
+    // 000's coordinate or corner 111's: the sample touches the blocks b0 + {0, 1}^3 on the axes where 000's and
+    // 111's blocks differ (mask sm), one block usually, two across a face. Corner 000's block is located first
+    // (in a free block the reference's first read has weight 0 and the sample ends: no other lookups in free
+    // space); each lane then resolves its own other blocks in a loop, so a wave waits for the largest count on
+    // one lane (one lookup, usually) instead of one lookup round trip per corner any lane missed (up to seven)
+    const i3 v0 = world_to_vvox(posDual + offs(0), R.voxelSize), v7 = world_to_vvox(posDual + offs(7), R.voxelSize);
+    const i3 b0 = vvox_to_block(v0), b7 = vvox_to_block(v7);
+    int pj[8];
+    pj[0] = c.lookup(R, b0);
+    if (pj[0] == BF_FREE_ENTRY) return false;
+    const uint32_t sm = (b7.x != b0.x ? 1u : 0u) | (b7.y != b0.y ? 2u : 0u) | (b7.z != b0.z ? 4u : 0u);
+#pragma unroll
+    for (int j = 1; j < 8; j++) pj[j] = pj[0];
+    uint32_t pend = 0u;  // the nonzero subsets of sm
+#pragma unroll
+    for (uint32_t j = 1; j < 8; j++) pend |= (j & ~sm) == 0u ? 1u << j : 0u;
+    while (pend) {
+        const uint32_t j = (uint32_t)__builtin_ctz(pend);
+        pend &= pend - 1u;
+        const int p = c.lookup(R, i3{(j & 1u) ? b7.x : b0.x, (j & 2u) ? b7.y : b0.y, (j & 4u) ? b7.z : b0.z});
+#pragma unroll
+        for (uint32_t jj = 1; jj < 8; jj++) pj[jj] = (jj & sm) == j ? p : pj[jj];
+    }
+    const int l0x = local_mod(v0.x), l0y = local_mod(v0.y), l0z = local_mod(v0.z);
+    const int l7x = local_mod(v7.x), l7y = local_mod(v7.y), l7z = local_mod(v7.z);
     float vs[8], vw[8];
     uint32_t vc[8];
-    // corner 000 in a free block: the reference's first corner read has weight 0 and the sample ends
-    // there, so the other corners are not located (no probes in free space)
-    const BFVoxel* v0 = voxel_ptr(R, c, posDual + offs(0));
-    if (!v0) return false;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const BFVoxel* vp = k == 0 ? v0 : voxel_ptr(R, c, posDual + offs(k));
+        const bool kx = k == 1 || k == 4 || k == 6 || k == 7, ky = k == 2 || k == 4 || k == 5 || k == 7,
+                   kz = k == 3 || k == 5 || k == 6 || k == 7;
+        const int ptr = pj[(kx ? 1 : 0) | (ky ? 2 : 0) | (kz ? 4 : 0)];
         vs[k] = 0.0f; vw[k] = 0.0f; vc[k] = 0u;
-        if (vp) {
+        if (ptr != BF_FREE_ENTRY) {
+            const int lx = kx ? l7x : l0x, ly = ky ? l7y : l0y, lz = kz ? l7z : l0z;
+            const BFVoxel* vp = R.voxels + (size_t)ptr * BF_VOXELS_PER_BLOCK +
+                                (lz * BF_SDF_BLOCK_SIZE * BF_SDF_BLOCK_SIZE + ly * BF_SDF_BLOCK_SIZE + lx);
             vs[k] = vp->sdf;
             vw[k] = vp->weight;
             vc[k] = *reinterpret_cast<const uint32_t*>(vp->color);
@@ -300,6 +481,7 @@ __device__ __forceinline__ f3 gradient_for_point(const RayArgs& R, BlockCache& c
 }
 
 // renderKernel (CUDARayCastSDF.cu:17-57) + traverseCoarseGridSimpleSampleAll (RayCastSDFUtil.h:224-290)
+template <bool GRAD>
 __device__ __forceinline__ void render_pixel(const RayArgs& R, const BFRayCastParams& rp, BlockCache& cache, uint32_t x, uint32_t y,
                              const uint32_t* __restrict__ smin, const uint32_t* __restrict__ smax, float* d_depth,
                              float4* d_depth4, float4* d_normals, float4* d_colors, float* outMin, float* outMax, bool& rayed) {
@@ -357,7 +539,7 @@ __device__ __forceinline__ void render_pixel(const RayArgs& R, const BFRayCastPa
                         d_depth4[pix] = make_float4(cp.x, cp.y, cp.z, 1.0f);
                         d_colors[pix] = make_float4((float)(rgb2 & 0xFF) / 255.f, (float)((rgb2 >> 8) & 0xFF) / 255.f,
                                                     (float)((rgb2 >> 16) & 0xFF) / 255.f, 1.0f);
-                        if (rp.useGradients) {
+                        if (GRAD) {
                             const f3 iso = worldCamPos + alpha * worldDir;
                             const f3 nrm = -gradient_for_point(R, cache, iso);
                             const f3 n = xform4(rp.viewMatrix, nrm, 0.0f);
@@ -381,22 +563,24 @@ __device__ __forceinline__ void render_pixel(const RayArgs& R, const BFRayCastPa
 // Pixel shape: each wave marches an 8x8 pixel square (neighbouring rays cross the same blocks and end at
 // similar depths); TPB 256: a workgroup is a 16x16 tile of four such squares, TPB 64: one square per
 // workgroup, so a slot frees as soon as its one wave ends (A/B, BF_RENDER_TPB)
-#ifndef BF_RENDER_WPE  // A/B builds: waves per SIMD asked of the compiler (0: its own choice, 101 VGPRs -> 4)
-#define BF_RENDER_WPE 0
+// Occupancy: a render is 4 800 waves. At 4 waves per SIMD (105-121 VGPRs) the 4 096 slots took them in two
+// rounds, each a whole march long (the march is bound by memory latency, not by issue); the kernel without the
+// gradient path fits 96 VGPRs (5 waves per SIMD: every wave of a 640x480 render resident at once) when the
+// per-thread block cache holds one block (the sample's own corners no longer need two: trilinear resolves them
+// per sample) and the two pointers it spills are reloaded once per pixel. useGradients renders take the kernel
+// instantiated with the gradient path (its six extra samples need 17 more VGPRs).
+#ifndef BF_RENDER_WPE  // A/B builds: waves per SIMD asked of the compiler for the kernel without gradients
+#define BF_RENDER_WPE 5
 #endif
-#if BF_RENDER_WPE
-#define BF_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(BF_RENDER_WPE)))
-#else
-#define BF_RENDER_ATTR
-#endif
-template <int TPB>
-__global__ __launch_bounds__(TPB) BF_RENDER_ATTR void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
+template <int TPB, bool GRAD>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GRAD ? 4 : BF_RENDER_WPE))) void k_render(RayArgs R, BFRayCastParams rp, const uint32_t* __restrict__ smin,
                                                 const uint32_t* __restrict__ smax, float* d_depth, float4* d_depth4,
                                                 float4* d_normals, float4* d_colors, float* outMin, float* outMax,
                                                 unsigned long long* stats) {
     constexpr uint32_t TILE = TPB == 256 ? 16u : 8u;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * TILE + (wv & 1u) * 8u + (lane & 7u), y = blockIdx.y * TILE + (wv >> 1) * 8u + (lane >> 3);
+    const long long tStart = R.waveLog ? wall_clock64() : 0;
     __shared__ unsigned long long s_table[RC_SLOTS];
     for (uint32_t i = threadIdx.x; i < (uint32_t)RC_SLOTS; i += TPB) s_table[i] = RC_EMPTY;
     __syncthreads();
@@ -404,21 +588,48 @@ __global__ __launch_bounds__(TPB) BF_RENDER_ATTR void k_render(RayArgs R, BFRayC
     if (R.ldsTable) cache.table = s_table;
     bool rayed = false;
     if (x < rp.width && y < rp.height)
-        render_pixel(R, rp, cache, x, y, smin, smax, d_depth, d_depth4, d_normals, d_colors, outMin, outMax, rayed);
+        render_pixel<GRAD>(R, rp, cache, x, y, smin, smax, d_depth, d_depth4, d_normals, d_colors, outMin, outMax, rayed);
     const uint32_t s = wave_sum_u32(cache.samples), l = wave_sum_u32(cache.loads), p = wave_sum_u32(cache.probes);
     const uint32_t r = wave_sum_u32(rayed ? 1u : 0u);
     uint32_t wmax = cache.samples;  // the wave's longest march
     for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off));
-    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
-        atomicAdd(&stats[RS_RENDERS], 1ull);
-        atomicAdd(&stats[RS_PIXELS], (unsigned long long)rp.width * rp.height);
+    __shared__ unsigned long long s_st[RS_COUNT];
+    if (threadIdx.x < RS_COUNT) s_st[threadIdx.x] = 0;
+    __syncthreads();
+    if (lane == 0) {
+        atomicAdd(&s_st[RS_SAMPLES], (unsigned long long)s);
+        atomicAdd(&s_st[RS_LOADS], (unsigned long long)l);
+        atomicAdd(&s_st[RS_PROBES], (unsigned long long)p);
+        atomicAdd(&s_st[RS_RAYS], (unsigned long long)r);
+        atomicAdd(&s_st[RS_WAVESAMPLES], 64ull * wmax);
+        atomicMax(&s_st[RS_WAVEMAX], (unsigned long long)wmax);
+        if (wmax > 32u) atomicAdd(&s_st[RS_LONGWAVES], 1ull);
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&stats[RS_SAMPLES], (unsigned long long)s);
-        atomicAdd(&stats[RS_LOADS], (unsigned long long)l);
-        atomicAdd(&stats[RS_PROBES], (unsigned long long)p);
-        atomicAdd(&stats[RS_RAYS], (unsigned long long)r);
-        atomicAdd(&stats[RS_WAVESAMPLES], 64ull * wmax);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long* st = rs_slot(stats);
+        if (blockIdx.x == 0 && blockIdx.y == 0) {
+            atomicAdd(&st[RS_RENDERS], 1ull);
+            atomicAdd(&st[RS_PIXELS], (unsigned long long)rp.width * rp.height);
+        }
+        if (s_st[RS_SAMPLES]) {
+            atomicAdd(&st[RS_SAMPLES], s_st[RS_SAMPLES]);
+            atomicAdd(&st[RS_LOADS], s_st[RS_LOADS]);
+            atomicAdd(&st[RS_PROBES], s_st[RS_PROBES]);
+            atomicAdd(&st[RS_WAVESAMPLES], s_st[RS_WAVESAMPLES]);
+            atomicMax(&st[RS_WAVEMAX], s_st[RS_WAVEMAX]);
+        }
+        if (s_st[RS_RAYS]) atomicAdd(&st[RS_RAYS], s_st[RS_RAYS]);
+        if (s_st[RS_LONGWAVES]) atomicAdd(&st[RS_LONGWAVES], s_st[RS_LONGWAVES]);
+    }
+    if (lane == 0) {
+        if (R.waveLog) {
+            unsigned long long* w = R.waveLog + 4ull * ((blockIdx.y * gridDim.x + blockIdx.x) * (TPB / 64u) + wv);
+            w[0] = (unsigned long long)tStart;
+            w[1] = (unsigned long long)wall_clock64();
+            w[2] = __smid();
+            w[3] = wmax;
+        }
     }
 }
 
@@ -443,12 +654,20 @@ __global__ void k_normals(float4* out, const float4* in, uint32_t W, uint32_t H)
 }  // namespace
 
 void Scene::renderStats(BFRenderStats& out) {
-    uint64_t c[RS_COUNT];
-    BF_HIP(hipMemcpyAsync(c, renderStats_.p, sizeof(c), hipMemcpyDeviceToHost, stream_));
+    std::vector<uint64_t> all((size_t)kRenderStatSlots * kRenderStatFields);
+    BF_HIP(hipMemcpyAsync(all.data(), renderStats_.p, all.size() * 8, hipMemcpyDeviceToHost, stream_));
     BF_HIP(hipStreamSynchronize(stream_));
+    uint64_t c[RS_COUNT] = {};
+    for (int sl = 0; sl < kRenderStatSlots; sl++)
+        for (int f = 0; f < RS_COUNT; f++) {
+            const uint64_t v = all[(size_t)sl * kRenderStatFields + f];
+            c[f] = f == RS_WAVEMAX ? std::max(c[f], v) : c[f] + v;
+        }
     out.samples = c[RS_SAMPLES]; out.voxelLoads = c[RS_LOADS]; out.hashProbes = c[RS_PROBES]; out.rays = c[RS_RAYS];
     out.splatBlocks = c[RS_QUADS]; out.splatAtomics = c[RS_ATOMICS]; out.renders = c[RS_RENDERS]; out.pixels = c[RS_PIXELS];
     out.waveSamples = c[RS_WAVESAMPLES];
+    out.waveSamplesMax = c[RS_WAVEMAX];
+    out.longWaves = c[RS_LONGWAVES];
     out.timedRenders = renderClock_.enabled() ? renderClock_.launches() : 0;
     out.renderMs = renderClock_.enabled() ? renderClock_.totalMs() : 0.0;
     out.splatMs = splatClock_.enabled() ? splatClock_.totalMs() : 0.0;
@@ -468,15 +687,32 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
         splatMax_.alloc(P);
         splatCap_ = P;
     }
-    k_splat_clear<<<std::max(1u, std::min(div_up(P, 256), 2048u)), 256, 0, stream_>>>(splatMin_.p, splatMax_.p, (uint32_t)P);
-    BF_LAUNCH_CHECK();
+    static const bool atomicSplat = [] {
+        const char* e = std::getenv("BF_SPLAT_ATOMIC");  // A/B: 1 = one global atomic min / max per covered pixel
+        return e && std::atoi(e) == 1;
+    }();
+    if (atomicSplat) {
+        k_splat_clear<<<std::max(1u, std::min(div_up(P, 256), 2048u)), 256, 0, stream_>>>(splatMin_.p, splatMax_.p, (uint32_t)P);
+        BF_LAUNCH_CHECK();
+    } else if (!splatQuads_.p) {
+        splatQuads_.alloc(B_);
+    }
     const bool timed = renderClock_.enabled();
     if (timed) {
         if (!splatClock_.enabled()) splatClock_.enable(true);
         splatClock_.start(stream_);
     }
-    k_splat<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp, splatMin_.p,
-                                                          splatMax_.p, renderStats_.p);
+    if (atomicSplat) {
+        k_splat<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp, splatMin_.p,
+                                                              splatMax_.p, renderStats_.p);
+    } else {
+        BF_REQUIRE(rp.width <= 0xFFFFu && rp.height <= 0x7FFFu, BF_ERR_ARG, "raycast size (16-bit splat rectangles)");
+        k_splat_quads<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp,
+                                                                    splatQuads_.p, renderStats_.p);
+        BF_LAUNCH_CHECK();
+        k_splat_tiles<<<dim3(div_up(rp.width, ST_W), div_up(rp.height, ST_H)), 256, 0, stream_>>>(splatQuads_.p, ctrl_.p, rp.width,
+                                                                                                  rp.height, splatMin_.p, splatMax_.p);
+    }
     BF_LAUNCH_CHECK();
     if (timed) splatClock_.stop(stream_);
     RayArgs R;
@@ -491,20 +727,43 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
         return !(e && std::atoi(e) == 0);
     }();
     R.ldsTable = ldsTable && cfg_.hp.numSDFBlocks < 0xFFFFFFu ? 1u : 0u;
+    // BF_RENDER_WAVE_LOG=path (diagnostics): every render appends {waves, then per wave start / end wall clock
+    // (100 MHz), __smid, longest per-lane march} to path, synchronising the stream after the render
+    static const char* waveLogPath = std::getenv("BF_RENDER_WAVE_LOG");
+    const size_t nWaves = (size_t)div_up(rp.width, 16) * div_up(rp.height, 16) * 4;  // >= the 8x8 squares of either tile shape
+    R.waveLog = nullptr;
+    if (waveLogPath) {
+        if (waveLog_.n < 4 * nWaves) waveLog_.alloc(4 * nWaves);
+        R.waveLog = waveLog_.p;
+    }
     const dim3 g(div_up(rp.width, 16), div_up(rp.height, 16));
     static const int tpb = [] {
         const char* e = std::getenv("BF_RENDER_TPB");
         return e && std::atoi(e) == 64 ? 64 : 256;
     }();
     if (timed) renderClock_.start(stream_);
-    if (tpb == 64)
-        k_render<64><<<dim3(div_up(rp.width, 8), div_up(rp.height, 8)), 64, 0, stream_>>>(
-            R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax, renderStats_.p);
-    else
-        k_render<256><<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
+    auto launch = [&](auto kern, dim3 grid, unsigned tpbLaunch) {
+        kern<<<grid, tpbLaunch, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
                                               renderStats_.p);
+    };
+    const dim3 g8(div_up(rp.width, 8), div_up(rp.height, 8));
+    if (tpb == 64)
+        rp.useGradients ? launch(k_render<64, true>, g8, 64) : launch(k_render<64, false>, g8, 64);
+    else
+        rp.useGradients ? launch(k_render<256, true>, g, 256) : launch(k_render<256, false>, g, 256);
     BF_LAUNCH_CHECK();
     if (timed) renderClock_.stop(stream_);
+    if (waveLogPath) {
+        std::vector<unsigned long long> h(4 * nWaves);
+        BF_HIP(hipMemcpyAsync(h.data(), waveLog_.p, h.size() * 8, hipMemcpyDeviceToHost, stream_));
+        BF_HIP(hipStreamSynchronize(stream_));
+        if (FILE* f = std::fopen(waveLogPath, "ab")) {
+            const unsigned long long n = nWaves;
+            std::fwrite(&n, 8, 1, f);
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
     if (!rp.useGradients) {
         k_normals<<<g, 256, 0, stream_>>>(normals, depth4, rp.width, rp.height);
         BF_LAUNCH_CHECK();

@@ -66,6 +66,8 @@ struct VoxelOp {
 
 class Scene {
 public:
+    // render counters (raycast.hip): kRenderStatSlots slots of kRenderStatFields, summed by renderStats()
+    static constexpr int kRenderStatSlots = 64, kRenderStatFields = 16;
     // a frame's fixes (<= 10 re-integrations, 2 voxel ops each) + the deferred integration of the
     // previous frame; <= 32 (op bit masks)
     static constexpr uint32_t kMaxOps = 24;
@@ -175,8 +177,11 @@ private:
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
     unsigned applyGrid_ = 0, compactifyGrid_ = 0;
+    int applyXcdShift_ = -1;  // BF_APPLY_XCD_CHUNK (A/B): log2 of the work-list run per XCD, -1 off
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;
+    DevBuf<int4> splatQuads_;
+    DevBuf<unsigned long long> waveLog_;  // BF_RENDER_WAVE_LOG diagnostics (raycast.hip)  // per visible block: covered pixel rectangle + encoded depths (k_splat_quads)
 };
 
 }  // namespace bf

@@ -1647,12 +1647,22 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
 // workload, with the waves' cycles 25 % issuing, 44 % waiting to issue (dependencies) and 31 % waiting on
 // memory (profiles/r9g_apply_sq_pmc.txt): it is dependency / latency bound. Lane-derived values are re-read
 // per block instead of kept live (no spills), counters are scalar.
-template <int ZR, int ZC, int WPE>
+template <int ZR, int ZC, int WPE, bool XCDRUNS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
-    HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap) {
+    HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap, int xcdShift) {
     static_assert(ZR * 2 == BF_SDF_BLOCK_SIZE, "one op mask per z-half of the block");
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    // XCDRUNS (A/B, BF_APPLY_XCD_CHUNK): runs of 2^xcdShift consecutive work-list positions go to one XCD
+    // (workgroup i runs on XCD i mod 8), run j to XCD j mod 8; otherwise consecutive positions go to
+    // consecutive waves, i.e. every XCD's waves spread over the whole list
+    uint32_t v0 = wave, vstep = nwaves, xcd = 0, cmask = 0;
+    if constexpr (XCDRUNS) {
+        v0 = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        vstep = nwaves >> 3;
+        xcd = blockIdx.x & 7u;
+        cmask = (1u << xcdShift) - 1u;
+    }
     const float epsc = (3.0f * (float)(max(cam.imageWidth, cam.imageHeight) + 2u) + fmaxf(fabsf(cam.mx), fabsf(cam.my)) + 3.0f) * 0x1p-21f;
     uint32_t updated = 0, rmw = 0, halves = 0;  // per wave and launch: < 2^32
 #ifdef BF_APPLY_DIAG
@@ -1660,7 +1670,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
     WorkCursor cur = work_begin(A.ctrl, ops.n);
     size_t b;
-    for (uint32_t g = wave; work_slot(A.ctrl, cur, g, binCap, b); g += nwaves) {
+    auto pos = [&](uint32_t v) { return XCDRUNS ? (((v >> xcdShift) << 3 | xcd) << xcdShift) | (v & cmask) : v; };
+    for (uint32_t v = v0; work_slot(A.ctrl, cur, pos(v), binCap, b); v += vstep) {
         const int4 ev = A.band[b];  // wave-uniform: keep the block's coordinates and base in SGPRs
         const int4 e = make_int4(__builtin_amdgcn_readfirstlane(ev.x), __builtin_amdgcn_readfirstlane(ev.y),
                                  __builtin_amdgcn_readfirstlane(ev.z), __builtin_amdgcn_readfirstlane(ev.w));
@@ -1985,7 +1996,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipGetDevice(&dev));
     BF_HIP(hipGetDeviceProperties(&prop, dev));
     numCUs_ = prop.multiProcessorCount;
-    renderStats_.alloc(16);  // RenderStat counters (raycast.hip)
+    renderStats_.alloc((size_t)kRenderStatSlots * kRenderStatFields);  // RenderStat counters (raycast.hip)
     BF_HIP(hipMemsetAsync(renderStats_.p, 0, renderStats_.bytes(), stream_));
     // k_integrate walks its block list with a static grid stride: size the grid to exactly the
     // resident workgroups, so every wave gets the same share in one round (no tail round)
@@ -2004,6 +2015,11 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int mult = kApplyRounds;
     if (const char* e = std::getenv("BF_APPLY_GRID_MULT")) mult = std::max(1, std::atoi(e));
     applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_ * (unsigned)mult;
+    if (const char* e = std::getenv("BF_APPLY_XCD_CHUNK")) {  // A/B: work-list runs per XCD (a power of two)
+        const int c = std::atoi(e);
+        for (int sh = 0; sh < 16; sh++)
+            if (c == (1 << sh)) applyXcdShift_ = sh;
+    }
     // the batch scan: 4 workgroups per CU (its occupancy), BF_COMPACTIFY_GRID_MULT rounds of them (A/B)
     int cmult = 1;
     if (const char* e = std::getenv("BF_COMPACTIFY_GRID_MULT")) cmult = std::max(1, std::atoi(e));
@@ -2205,7 +2221,12 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_);
+    if (applyXcdShift_ >= 0 && applyGrid_ % 8u == 0u)  // workgroup i runs on XCD i mod 8
+        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam,
+                              tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, applyXcdShift_);
+    else
+        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab,
+                              reinterpret_cast<const OpMask*>(blockMask_.p), B_, -1);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;

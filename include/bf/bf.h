@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 #define BF_ABI_VERSION 3  /* 2: BFSolverOptions.pcgSpinLimitUs, BFCorrOptions.minPerPair; 3: BFReconStats.globalPcgLaunches /
-                             globalPcgKernelMs, BFTsdfStats.batchHalves, BFRenderStats.waveSamples, BFAppTiming */
+                             globalPcgKernelMs, BFTsdfStats.batchHalves, BFRenderStats.waveSamples / waveSamplesMax / longWaves, BFAppTiming */
 
 /* ---- runtime ------------------------------------------------------------- */
 int bf_abi_version(void);

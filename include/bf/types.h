@@ -157,7 +157,7 @@ typedef struct BFRenderStats {
     uint64_t hashProbes;   /* hash lookups (a per-ray one-block cache skips repeats) */
     uint64_t rays;         /* pixels with a splatted interval (marched) */
     uint64_t splatBlocks;  /* visible blocks rasterised by the interval splat */
-    uint64_t splatAtomics; /* atomic min / max depth updates of the splat */
+    uint64_t splatAtomics; /* min / max depth updates of the splat (one per covered pixel and pass) */
     uint64_t renders;      /* renderKernel launches */
     uint64_t pixels;       /* pixels over those launches */
     uint64_t timedRenders; /* renders timed by the clocks below (enabled by the first bf_recon_render_time) */
@@ -165,6 +165,8 @@ typedef struct BFRenderStats {
     double splatMs;        /* summed interval-splat device time of the timed renders */
     uint64_t waveSamples;  /* per renderKernel wave, 64 x its largest per-lane sample count: samples / waveSamples
                               is the fraction of the wave's march steps its lanes spend on samples */
+    uint64_t waveSamplesMax; /* the largest per-lane sample count of any renderKernel wave (since the scene's creation) */
+    uint64_t longWaves;    /* renderKernel waves whose largest per-lane sample count exceeds 32 */
 } BFRenderStats;
 
 /* Device-side counters used by the bench to compute algorithmic bytes. */

@@ -16,6 +16,8 @@
 #   trace:NAME[:ARGS]      kernel trace of the bench (rocprofv3 --kernel-trace): the scene stream's per-frame timeline
 #                          (tools/stream_timeline.py) and the input kernels' overlap with the voxel pass (overlap_attr.py)
 #   py:NAME:SECONDS:ARGS   python ARGS (a tool script) with a SECONDS limit -> NAME.log
+#   avail                  the counters rocprofv3 offers on this GPU -> avail.log
+#   kstats:NAME[:ARGS]     rocprofv3 --kernel-trace --stats of the bench -> kstats_NAME.csv (per-kernel summary)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -69,6 +71,10 @@ for step in "$@"; do
            python3 tools/trace_tail.py $f $O/trace_$a.json $O/trace_tail_$a.csv.gz
            cat $O/timeline_$a.txt; rm -rf $O/trace_$a ;;
     py) run $a $b python -u ${c//,/ } ;;
+    avail) run avail 120 rocprofv3 --list-avail ;;
+    kstats) run kstats_$a 600 rocprofv3 --kernel-trace --stats -d $O/kstats_$a -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${b//,/ }
+            cp "$(python3 -c "import glob,sys; print(glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True)[0])" $O/kstats_$a)" $O/kstats_$a.csv
+            rm -rf $O/kstats_$a; cut -d, -f1-8 $O/kstats_$a.csv | head -40 ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
 done
