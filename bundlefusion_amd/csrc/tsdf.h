@@ -37,8 +37,7 @@ enum Ctrl {
     C_TICKET = 9,      // last-workgroup ticket of k_alloc_insert (self-resetting)
     C_TICKET_GC = 10,  // last-workgroup ticket of k_gc (self-resetting)
     C_OPBIN = 16,      // op batches: work-list entries per op count (1..kMaxOps -> slots 16..39)
-    C_TICKET_GC_SUB = 48,  // k_gc's eight group tickets (workgroup index mod 8; self-resetting), ahead of C_TICKET_GC
-    C_COUNT = 56
+    C_COUNT = 48
 };
 
 struct SceneConfig {

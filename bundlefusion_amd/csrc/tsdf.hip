@@ -1837,20 +1837,9 @@ __global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* list
     if (lane == 0 && freed) atomicAdd(&A.stats[S_GCFREED], (unsigned long long)freed);
     __shared__ bool s_last;
     __syncthreads();
-    // two-level ticket: every workgroup takes its group's ticket (workgroup index mod 8), the last of a group
-    // the top one. A ticket word that every workgroup increments serialises them (~11 ns per device-scope
-    // atomic on one address: 5.6 us for k_gc's 512 workgroups); the fences chain each group's release
-    // through its last workgroup to the top ticket's winner
     if (threadIdx.x == 0) {
         __threadfence();
-        const uint32_t grp = blockIdx.x & 7u, ngrp = min(gridDim.x, 8u), inGrp = (gridDim.x - grp + 7u) / 8u;
-        bool last = false;
-        if (atomicAdd(&A.ctrl[C_TICKET_GC_SUB + grp], 1u) == inGrp - 1u) {
-            __threadfence();
-            A.ctrl[C_TICKET_GC_SUB + grp] = 0;
-            last = atomicAdd(&A.ctrl[C_TICKET_GC], 1u) == ngrp - 1u;
-        }
-        s_last = last;
+        s_last = atomicAdd(&A.ctrl[C_TICKET_GC], 1u) == gridDim.x - 1;
     }
     __syncthreads();
     __shared__ uint32_t s_locked[64];  // the serial path's locked buckets (in LDS: a private array went to scratch)
