@@ -177,12 +177,32 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
 // one store per pixel, and k_splat_clear is not needed. A pass a block does not take carries the clear value
 // (enc(+inf) for min, enc(-inf) for max), which leaves the pixel unchanged, so the result is the same
 // order-independent min / max as the atomics'
-constexpr int ST_W = 64, ST_H = 20, ST_PX = ST_W * ST_H / 256, ST_Q = 16;  // tile, pixels per thread, rectangles per thread per chunk
+// 64x8 tiles (2 rows per wave), 8 rectangles per thread per chunk (32 KB of LDS list): 600 workgroups for
+// 640x480, two to three per CU. The fold is issue-bound (~40 instructions per rectangle and wave, 140 ns
+// each with one wave per SIMD: BF_SPLAT_TILE_LOG), so it wants several waves per SIMD and few rows per wave;
+// 64x20 tiles (one workgroup per CU, 5 rows per wave) took 58 us, 64x8 37 us, 64x4 (1 200 workgroups) 38 us
+constexpr int ST_W = 64, ST_H = 8, ST_PX = ST_W * ST_H / 256, ST_Q = 8;  // tile, pixels per thread, rectangles per thread per chunk
+// Tile rows: each rectangle is also listed under every 20-pixel tile row it spans (count in k_splat_quads,
+// exclusive scan in k_splat_rows, fill in k_splat_fill), so a tile scans its own row's rectangles instead of
+// all of them. Renders taller than ST_ROWS tile rows, or whose
+// row lists would exceed their capacity (4 entries per visible block), scan every rectangle.
+constexpr int ST_ROWS = 256;
+enum SplatBin { SB_COUNT = 0, SB_START = ST_ROWS, SB_LEN = 2 * ST_ROWS, SB_CURSOR = 3 * ST_ROWS, SB_TOTAL = 4 * ST_ROWS,
+                SB_OVERFLOW, SB_WORDS };
+__device__ __forceinline__ bool quad_rows(const int4 q, int& r0, int& r1) {  // the tile rows a rectangle spans
+    const int x0 = q.x & 0xFFFF, x1 = q.y & 0xFFFF;
+    r0 = (q.x >> 16) / ST_H;
+    r1 = (q.y >> 16) / ST_H;
+    return x0 <= x1;
+}
 __global__ __launch_bounds__(256) void k_splat_quads(const int4* __restrict__ visible, const uint32_t* ctrl, float voxelSize,
                                                      BFDepthCameraParams cam, BFRayCastParams rp, int4* quads,
-                                                     unsigned long long* stats) {
+                                                     unsigned long long* stats, uint32_t* bin) {
     const uint32_t n = ctrl[C_VISIBLE];
     uint32_t nq = 0, npix = 0;
+    __shared__ uint32_t s_row[ST_ROWS];
+    if (threadIdx.x < ST_ROWS) s_row[threadIdx.x] = 0;
+    __syncthreads();
     const BFMat4 V = rp.viewMatrix;
     for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < n; b += gridDim.x * blockDim.x) {
         int4 out = make_int4(0xFFFF, 0, 0, 0);  // an empty rectangle (x0 > x1)
@@ -225,10 +245,14 @@ __global__ __launch_bounds__(256) void k_splat_quads(const int4* __restrict__ vi
             }
         }
         quads[b] = out;
+        int r0, r1;
+        if (bin && quad_rows(out, r0, r1))
+            for (int r = r0; r <= r1; r++) atomicAdd(&s_row[r], 1u);
     }
     __shared__ unsigned long long s_st[2];
     if (threadIdx.x < 2) s_st[threadIdx.x] = 0;
     __syncthreads();
+    if (bin && threadIdx.x < ST_ROWS && s_row[threadIdx.x]) atomicAdd(&bin[SB_COUNT + threadIdx.x], s_row[threadIdx.x]);
     nq = wave_sum_u32(nq);
     npix = wave_sum_u32(npix);
     if ((threadIdx.x & 63) == 0 && nq) {
@@ -242,12 +266,71 @@ __global__ __launch_bounds__(256) void k_splat_quads(const int4* __restrict__ vi
     }
 }
 
-__global__ __launch_bounds__(256) void k_splat_tiles(const int4* __restrict__ quads, const uint32_t* ctrl, uint32_t W, uint32_t H,
-                                                     uint32_t* smin, uint32_t* smax) {
+// exclusive scan of the row counts (then zeroed for the next render), capacity check
+__global__ __launch_bounds__(ST_ROWS) void k_splat_rows(uint32_t* bin, uint32_t cap) {
+    __shared__ uint32_t s[ST_ROWS];
+    const uint32_t r = threadIdx.x, c = bin[SB_COUNT + r];
+    s[r] = c;
+    __syncthreads();
+    for (uint32_t o = 1; o < (uint32_t)ST_ROWS; o <<= 1) {
+        const uint32_t v = r >= o ? s[r - o] : 0u;
+        __syncthreads();
+        s[r] += v;
+        __syncthreads();
+    }
+    const uint32_t incl = s[r];
+    bin[SB_START + r] = incl - c;
+    bin[SB_CURSOR + r] = incl - c;
+    bin[SB_LEN + r] = c;
+    bin[SB_COUNT + r] = 0;
+    if (r == ST_ROWS - 1) {
+        bin[SB_TOTAL] = incl;
+        bin[SB_OVERFLOW] = incl > cap ? 1u : 0u;
+    }
+}
+// the row lists: a workgroup counts its rectangles per row, takes each row's range with one atomic, and hands
+// the slots out in LDS (same grid as k_splat_quads, so the same rectangles per workgroup)
+__global__ __launch_bounds__(256) void k_splat_fill(const int4* __restrict__ quads, const uint32_t* ctrl, uint32_t* bin,
+                                                    uint32_t* rowIdx, uint32_t cap) {
     const uint32_t n = ctrl[C_VISIBLE];
+    __shared__ uint32_t s_row[ST_ROWS];
+    if (threadIdx.x < ST_ROWS) s_row[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < n; b += gridDim.x * blockDim.x) {
+        int r0, r1;
+        if (quad_rows(quads[b], r0, r1))
+            for (int r = r0; r <= r1; r++) atomicAdd(&s_row[r], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < ST_ROWS && s_row[threadIdx.x]) s_row[threadIdx.x] = atomicAdd(&bin[SB_CURSOR + threadIdx.x], s_row[threadIdx.x]);
+    __syncthreads();
+    if (bin[SB_OVERFLOW]) return;  // the tiles scan every rectangle
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < n; b += gridDim.x * blockDim.x) {
+        int r0, r1;
+        if (quad_rows(quads[b], r0, r1))
+            for (int r = r0; r <= r1; r++) {
+                const uint32_t slot = atomicAdd(&s_row[r], 1u);
+                if (slot < cap) rowIdx[slot] = b;
+            }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_splat_tiles(const int4* __restrict__ quads, const uint32_t* ctrl, uint32_t W, uint32_t H,
+                                                     uint32_t* smin, uint32_t* smax, const uint32_t* __restrict__ bin,
+                                                     const uint32_t* __restrict__ rowIdx, unsigned long long* tileLog) {
+    const long long tStart = tileLog ? wall_clock64() : 0;
+    uint32_t folded = 0;  // diagnostics (BF_SPLAT_TILE_LOG): rectangles folded by this tile
+    // binned: this tile row's rectangles (indices into quads), else every rectangle
+    const bool binned = bin && bin[SB_OVERFLOW] == 0u;
+    const uint32_t n = binned ? bin[SB_LEN + blockIdx.y] : ctrl[C_VISIBLE];
+    const uint32_t* idxs = binned ? rowIdx + bin[SB_START + blockIdx.y] : nullptr;
     const int tx0 = (int)blockIdx.x * ST_W, ty0 = (int)blockIdx.y * ST_H;
     const int tx1 = min(tx0 + ST_W, (int)W) - 1, ty1 = min(ty0 + ST_H, (int)H) - 1;
-    const int px = tx0 + (int)(threadIdx.x & 63), py0 = ty0 + (int)(threadIdx.x >> 6);  // rows py0 + 4 i
+    // a wave owns ST_PX consecutive rows of the tile (rows py0 .. py0 + ST_PX - 1, lane = column): a rectangle's
+    // row range is wave-uniform, so a wave skips the rectangles outside its rows with one uniform test and
+    // tests only the column per lane (interleaved rows made every wave fold every rectangle of the tile)
+    const int px = tx0 + (int)(threadIdx.x & 63);
+    const int py0 = __builtin_amdgcn_readfirstlane(ty0 + ST_PX * (int)(threadIdx.x >> 6));  // scalar: row tests are SALU
     uint32_t mn[ST_PX], mx[ST_PX];
 #pragma unroll
     for (int i = 0; i < ST_PX; i++) { mn[i] = enc_f(__builtin_inff()); mx[i] = enc_f(-__builtin_inff()); }
@@ -259,7 +342,8 @@ __global__ __launch_bounds__(256) void k_splat_tiles(const int4* __restrict__ qu
     int4 q[ST_Q];
     const uint32_t last = n ? n - 1u : 0u;
     auto fetch = [&](uint32_t idx) {
-        const int4 v = quads[min(idx, last)];
+        const uint32_t i = min(idx, last);
+        const int4 v = quads[binned ? (n ? idxs[i] : 0u) : i];
         return idx < n ? v : make_int4(0xFFFF, 0, 0, 0);
     };
 #pragma unroll
@@ -292,15 +376,20 @@ __global__ __launch_bounds__(256) void k_splat_tiles(const int4* __restrict__ qu
         for (int i = 0; i < ST_Q; i++) q[i] = fetch(next + (uint32_t)i * 256u + threadIdx.x);
         lds_barrier();
         const uint32_t c = s_cnt;
+        folded += c;
         auto fold = [&](const int4 r) {
-            const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
-            if (px < x0 || px > x1) return;
+            const int y0 = __builtin_amdgcn_readfirstlane(r.x >> 16), y1 = __builtin_amdgcn_readfirstlane(r.y >> 16);
+            if (y1 < py0 || y0 > py0 + ST_PX - 1) return;  // wave-uniform
+            const int x0 = r.x & 0xFFFF, x1 = r.y & 0xFFFF;
+            const bool inx = px >= x0 && px <= x1;
+            // branch-free: a pixel outside the rectangle takes a value that leaves it unchanged (a branch per row
+            // cost ~8 exec-mask instructions: 137 ns per folded rectangle, BF_SPLAT_TILE_LOG)
+            const uint32_t zmin = inx ? (uint32_t)r.z : 0xFFFFFFFFu, zmax = inx ? (uint32_t)r.w : 0u;
 #pragma unroll
             for (int i = 0; i < ST_PX; i++) {
-                const int py = py0 + 4 * i;
-                if (py >= y0 && py <= y1) {
-                    mn[i] = min(mn[i], (uint32_t)r.z);
-                    mx[i] = max(mx[i], (uint32_t)r.w);
+                if (py0 + i >= y0 && py0 + i <= y1) {  // wave-uniform (scalar branch)
+                    mn[i] = min(mn[i], zmin);
+                    mx[i] = max(mx[i], zmax);
                 }
             }
         };
@@ -312,10 +401,17 @@ __global__ __launch_bounds__(256) void k_splat_tiles(const int4* __restrict__ qu
         for (; e < c; e++) fold(s_list[e]);
         lds_barrier();  // every wave has read s_cnt and the list before the next chunk resets them
     }
+    if (tileLog && threadIdx.x == 0) {
+        unsigned long long* w = tileLog + 4ull * (blockIdx.y * gridDim.x + blockIdx.x);
+        w[0] = (unsigned long long)tStart;
+        w[1] = (unsigned long long)wall_clock64();
+        w[2] = __smid();
+        w[3] = folded | ((unsigned long long)n << 32);
+    }
     if (px >= (int)W) return;
 #pragma unroll
     for (int i = 0; i < ST_PX; i++) {
-        const int py = py0 + 4 * i;
+        const int py = py0 + i;
         if (py < (int)H) {
             smin[(uint32_t)py * W + (uint32_t)px] = mn[i];
             smax[(uint32_t)py * W + (uint32_t)px] = mx[i];
@@ -707,11 +803,42 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
                                                               splatMax_.p, renderStats_.p);
     } else {
         BF_REQUIRE(rp.width <= 0xFFFFu && rp.height <= 0x7FFFu, BF_ERR_ARG, "raycast size (16-bit splat rectangles)");
-        k_splat_quads<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp,
-                                                                    splatQuads_.p, renderStats_.p);
+        const bool rows = div_up(rp.height, ST_H) <= (unsigned)ST_ROWS;
+        const uint32_t rowCap = 4u * B_;
+        if (rows && !splatBin_.p) {
+            splatBin_.alloc(SB_WORDS);
+            BF_HIP(hipMemsetAsync(splatBin_.p, 0, splatBin_.bytes(), stream_));
+            splatRowIdx_.alloc(rowCap);
+        }
+        uint32_t* bin = rows ? splatBin_.p : nullptr;
+        const unsigned qgrid = (unsigned)numCUs_;  // one workgroup per CU: few same-address row-count atomics
+        k_splat_quads<<<qgrid, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp, splatQuads_.p,
+                                                   renderStats_.p, bin);
         BF_LAUNCH_CHECK();
-        k_splat_tiles<<<dim3(div_up(rp.width, ST_W), div_up(rp.height, ST_H)), 256, 0, stream_>>>(splatQuads_.p, ctrl_.p, rp.width,
-                                                                                                  rp.height, splatMin_.p, splatMax_.p);
+        if (rows) {
+            k_splat_rows<<<1, ST_ROWS, 0, stream_>>>(bin, rowCap);
+            BF_LAUNCH_CHECK();
+            k_splat_fill<<<qgrid, 256, 0, stream_>>>(splatQuads_.p, ctrl_.p, bin, splatRowIdx_.p, rowCap);
+            BF_LAUNCH_CHECK();
+        }
+        // BF_SPLAT_TILE_LOG=path (diagnostics): per tile {start, end, __smid, rectangles folded | scanned << 32}
+        static const char* tileLogPath = std::getenv("BF_SPLAT_TILE_LOG");
+        const dim3 tg(div_up(rp.width, ST_W), div_up(rp.height, ST_H));
+        const size_t nTiles = (size_t)tg.x * tg.y;
+        if (tileLogPath && tileLog_.n < 4 * nTiles) tileLog_.alloc(4 * nTiles);
+        k_splat_tiles<<<tg, 256, 0, stream_>>>(splatQuads_.p, ctrl_.p, rp.width, rp.height, splatMin_.p, splatMax_.p, bin,
+                                               splatRowIdx_.p, tileLogPath ? tileLog_.p : nullptr);
+        if (tileLogPath) {
+            std::vector<unsigned long long> h(4 * nTiles);
+            BF_HIP(hipMemcpyAsync(h.data(), tileLog_.p, h.size() * 8, hipMemcpyDeviceToHost, stream_));
+            BF_HIP(hipStreamSynchronize(stream_));
+            if (FILE* f = std::fopen(tileLogPath, "ab")) {
+                const unsigned long long nt = nTiles;
+                std::fwrite(&nt, 8, 1, f);
+                std::fwrite(h.data(), 8, h.size(), f);
+                std::fclose(f);
+            }
+        }
     }
     BF_LAUNCH_CHECK();
     if (timed) splatClock_.stop(stream_);

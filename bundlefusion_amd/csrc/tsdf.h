@@ -177,11 +177,12 @@ private:
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
     unsigned applyGrid_ = 0, compactifyGrid_ = 0;
-    int applyXcdShift_ = -1;  // BF_APPLY_XCD_CHUNK (A/B): log2 of the work-list run per XCD, -1 off
+    int applyXcdShift_ = -1;  // log2 of the voxel pass's work-list run per XCD (-1: plain grid stride; Scene::Scene)
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;
     DevBuf<int4> splatQuads_;
-    DevBuf<unsigned long long> waveLog_;  // BF_RENDER_WAVE_LOG diagnostics (raycast.hip)  // per visible block: covered pixel rectangle + encoded depths (k_splat_quads)
+    DevBuf<uint32_t> splatBin_, splatRowIdx_;  // the splat's tile-row lists (raycast.hip)
+    DevBuf<unsigned long long> waveLog_, tileLog_;  // BF_RENDER_WAVE_LOG / BF_SPLAT_TILE_LOG diagnostics (raycast.hip)  // per visible block: covered pixel rectangle + encoded depths (k_splat_quads)
 };
 
 }  // namespace bf

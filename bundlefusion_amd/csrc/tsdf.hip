@@ -2015,8 +2015,16 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int mult = kApplyRounds;
     if (const char* e = std::getenv("BF_APPLY_GRID_MULT")) mult = std::max(1, std::atoi(e));
     applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_ * (unsigned)mult;
-    if (const char* e = std::getenv("BF_APPLY_XCD_CHUNK")) {  // A/B: work-list runs per XCD (a power of two)
+    // the voxel pass hands out runs of 64 consecutive work-list positions per XCD (k_apply_ops<..., true>): the
+    // list is in heap order, so a run's blocks lie together and one XCD's L2 serves their depth / colour lines.
+    // FETCH per launch at the driver workload: 1.14 GB with 4-position runs (consecutive waves: the plain grid
+    // stride), 1.04 / 0.98 / 0.96 / 0.95 / 0.93 GB with 16 / 64 / 128 / 256 / 1024; time 478 µs up to 64, then
+    // 480 / 485 / 516 µs as the coarser runs unbalance the XCDs (profiles/r10_apply_xcd_runs.txt).
+    // BF_APPLY_XCD_CHUNK (A/B): the run length (a power of two), 0 = the plain grid stride.
+    applyXcdShift_ = 6;
+    if (const char* e = std::getenv("BF_APPLY_XCD_CHUNK")) {
         const int c = std::atoi(e);
+        applyXcdShift_ = -1;
         for (int sh = 0; sh < 16; sh++)
             if (c == (1 << sh)) applyXcdShift_ = sh;
     }
