@@ -1647,8 +1647,8 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
 // workload, with the waves' cycles 25 % issuing, 44 % waiting to issue (dependencies) and 31 % waiting on
 // memory (profiles/r9g_apply_sq_pmc.txt): it is dependency / latency bound. Lane-derived values are re-read
 // per block instead of kept live (no spills), counters are scalar.
-template <int ZR, int ZC, int WPE, bool XCDRUNS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
+template <int ZR, int ZC, int WPE, bool XCDRUNS = false, int TPB = 256>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap, int xcdShift) {
     static_assert(ZR * 2 == BF_SDF_BLOCK_SIZE, "one op mask per z-half of the block");
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -2003,10 +2003,17 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int occ0 = 0, occ1 = 0, occA = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
-    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, 256, 0));
+    // BF_APPLY_TPB=64 (A/B): one-wave workgroups, so a wave's slot is handed on when that wave ends instead of
+    // when the slowest of its workgroup's four ends (the waves of a workgroup draw blocks of different cost)
+    if (const char* e = std::getenv("BF_APPLY_TPB")) applyTpb_ = std::atoi(e) == 64 ? 64 : 256;
+    if (applyTpb_ == 64)
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true, 64>, 64, 0));
+    else
+        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, 256, 0));
     // sharded: one workgroup slot per CU stays free for the bundling streams' launches (Recon::Recon)
     int freeSlots = cfg_.shardCount > 1 ? 1 : 0;
     if (const char* e = std::getenv("BF_APPLY_FREE_SLOTS")) freeSlots = std::atoi(e);  // A/B measurements
+    freeSlots *= 256 / applyTpb_;  // in 256-thread workgroups' worth
     // The grid is kApplyRounds rounds of resident workgroups, each wave a 1/kApplyRounds share of the strided
     // list: the dispatcher hands the later rounds' workgroups to the slots the earlier ones free, so the waves
     // that drew costly blocks no longer set the pass's end (one resident round: 537 us per launch at the
@@ -2229,9 +2236,15 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    if (applyXcdShift_ >= 0 && applyGrid_ % 8u == 0u)  // workgroup i runs on XCD i mod 8
+    if (applyTpb_ == 64 && applyXcdShift_ >= 0 && applyGrid_ % 8u == 0u)
+        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true, 64>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
+                              cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, applyXcdShift_);
+    else if (applyXcdShift_ >= 0 && applyGrid_ % 8u == 0u && applyTpb_ == 256)  // workgroup i runs on XCD i mod 8
         hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam,
                               tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, applyXcdShift_);
+    else if (applyTpb_ == 64)
+        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, false, 64>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
+                              cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, -1);
     else
         hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab,
                               reinterpret_cast<const OpMask*>(blockMask_.p), B_, -1);
