@@ -783,10 +783,7 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
         splatMax_.alloc(P);
         splatCap_ = P;
     }
-    static const bool atomicSplat = [] {
-        const char* e = std::getenv("BF_SPLAT_ATOMIC");  // A/B: 1 = one global atomic min / max per covered pixel
-        return e && std::atoi(e) == 1;
-    }();
+    const bool atomicSplat = splatAtomic_;
     if (atomicSplat) {
         k_splat_clear<<<std::max(1u, std::min(div_up(P, 256), 2048u)), 256, 0, stream_>>>(splatMin_.p, splatMax_.p, (uint32_t)P);
         BF_LAUNCH_CHECK();
@@ -804,7 +801,7 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
     } else {
         BF_REQUIRE(rp.width <= 0xFFFFu && rp.height <= 0x7FFFu, BF_ERR_ARG, "raycast size (16-bit splat rectangles)");
         const bool rows = div_up(rp.height, ST_H) <= (unsigned)ST_ROWS;
-        const uint32_t rowCap = 4u * B_;
+        const uint32_t rowCap = splatRowCap_ ? splatRowCap_ : 4u * B_;
         if (rows && !splatBin_.p) {
             splatBin_.alloc(SB_WORDS);
             BF_HIP(hipMemsetAsync(splatBin_.p, 0, splatBin_.bytes(), stream_));

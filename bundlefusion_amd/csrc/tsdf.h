@@ -183,6 +183,8 @@ private:
     size_t splatCap_ = 0;
     DevBuf<int4> splatQuads_;
     DevBuf<uint32_t> splatBin_, splatRowIdx_;  // the splat's tile-row lists (raycast.hip)
+    bool splatAtomic_ = false;   // BF_SPLAT_ATOMIC=1 (A/B): one global atomic min / max per covered pixel
+    uint32_t splatRowCap_ = 0;   // BF_SPLAT_ROW_CAP (test switch): row-list capacity (0: 4 per visible block)
     DevBuf<unsigned long long> waveLog_, tileLog_;  // BF_RENDER_WAVE_LOG / BF_SPLAT_TILE_LOG diagnostics (raycast.hip)  // per visible block: covered pixel rectangle + encoded depths (k_splat_quads)
 };
 

@@ -2003,6 +2003,9 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int occ0 = 0, occ1 = 0, occA = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
+    // ray-cast switches, read per scene so a test can set them (raycast.hip)
+    if (const char* e = std::getenv("BF_SPLAT_ATOMIC")) splatAtomic_ = std::atoi(e) == 1;
+    if (const char* e = std::getenv("BF_SPLAT_ROW_CAP")) splatRowCap_ = (uint32_t)std::max(1, std::atoi(e));
     // BF_APPLY_TPB=64 (A/B): one-wave workgroups, so a wave's slot is handed on when that wave ends instead of
     // when the slowest of its workgroup's four ends (the waves of a workgroup draw blocks of different cost)
     if (const char* e = std::getenv("BF_APPLY_TPB")) applyTpb_ = std::atoi(e) == 64 ? 64 : 256;

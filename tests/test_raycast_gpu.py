@@ -90,3 +90,22 @@ def test_raycast_empty_and_outside():
     rp = bfa.raycast_params(cam.imageWidth, cam.imageHeight, fx=f, fy=f)
     g = pair.gpu.raycast(bfa.synth_pose(0), cam, rp)
     assert np.all(g[0] == -np.inf) and np.all(g[2] == -np.inf)
+
+
+@pytest.mark.parametrize("env", [{"BF_SPLAT_ATOMIC": "1"}, {"BF_SPLAT_ROW_CAP": "1"}, {}],
+                         ids=["atomic-splat", "row-lists-overflow", "row-lists"])
+def test_splat_paths_give_the_same_intervals(env, monkeypatch):
+    """The three forms of the interval splat agree with the oracle bit for bit: the global-atomic form, the
+    tile-row lists (the default), and the full scan a tile falls back to when the row lists overflow their
+    capacity (forced here with a capacity of one entry)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc, cam, pair, f = build()
+    rp = bfa.raycast_params(cam.imageWidth, cam.imageHeight, fx=f, fy=f)
+    T = bfa.synth_pose(5)
+    g = pair.gpu.raycast(T, cam, rp, want_intervals=True)
+    o = pair.ora.raycast(T, cam, rp, want_intervals=True)
+    compare(g, o)
+    gmin, omin = g[4], o[4]
+    sel = np.isfinite(omin) & (omin >= rp.minDepth) & (omin < rp.maxDepth)
+    np.testing.assert_array_equal(gmin[sel], omin[sel])
