@@ -94,3 +94,27 @@ def test_trace_tail_keeps_the_region(tmp_path):
     kept = list(csv.DictReader(gzip.open(out, "rt")))
     names = [r["Kernel_Name"] for r in kept]
     assert names.count("k_apply_ops") == 20 and "k_pcg_persist" in names
+
+
+def test_wave_log_reads_the_renders(tmp_path):
+    """tools/wave_log.py: the BF_RENDER_WAVE_LOG / BF_SPLAT_TILE_LOG layout ({count, then count x {start, end,
+    __smid, value}} per render, 100 MHz ticks)."""
+    import numpy as np
+    from wave_log import renders
+    recs = []
+    for r in range(2):
+        n = 3 + r
+        w = np.zeros((n, 4), np.uint64)
+        w[:, 0] = 1000 + r * 500
+        w[:, 1] = w[:, 0] + np.arange(1, n + 1) * 100  # 1, 2, 3 .. us
+        w[:, 2] = (np.arange(n) % 8) << 6  # xcc in bits 6+
+        w[:, 3] = 7
+        recs += [np.array([n], np.uint64), w.ravel()]
+    path = tmp_path / "log.bin"
+    np.concatenate(recs).tofile(path)
+    rs = renders(str(path))
+    assert [len(x) for x in rs] == [3, 4]
+    assert int(rs[1][3, 1] - rs[1][3, 0]) == 400
+    out = subprocess.run([sys.executable, os.path.join(TOOLS, "wave_log.py"), str(path)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "2 renders in the log; render -1: 4 waves, span 4.0 us" in out, out
