@@ -177,7 +177,7 @@ private:
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
     unsigned applyGrid_ = 0, compactifyGrid_ = 0;
-    int applyTpb_ = 256;      // k_apply_ops workgroup size (BF_APPLY_TPB=64: A/B)
+    int applyTpb_ = 64;       // k_apply_ops workgroup size (Scene::Scene; BF_APPLY_TPB=256: A/B)
     int applyXcdShift_ = -1;  // log2 of the voxel pass's work-list run per XCD (-1: plain grid stride; Scene::Scene)
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;

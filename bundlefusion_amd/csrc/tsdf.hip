@@ -2006,9 +2006,13 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     // ray-cast switches, read per scene so a test can set them (raycast.hip)
     if (const char* e = std::getenv("BF_SPLAT_ATOMIC")) splatAtomic_ = std::atoi(e) == 1;
     if (const char* e = std::getenv("BF_SPLAT_ROW_CAP")) splatRowCap_ = (uint32_t)std::max(1, std::atoi(e));
-    // BF_APPLY_TPB=64 (A/B): one-wave workgroups, so a wave's slot is handed on when that wave ends instead of
-    // when the slowest of its workgroup's four ends (the waves of a workgroup draw blocks of different cost)
-    if (const char* e = std::getenv("BF_APPLY_TPB")) applyTpb_ = std::atoi(e) == 64 ? 64 : 256;
+    // One-wave workgroups: a wave's slot is handed on when that wave ends instead of when the slowest of its
+    // workgroup's four ends (the waves of a workgroup draw blocks of different cost, and the workgroup's end-of-
+    // pass counter flush waited for all four): k_apply_ops 475-477 -> 466-467 us, 1 484-1 487 -> 1 498-1 499
+    // frames/s at the bench workload, config 4's stream and the G = 8 rehearsal unchanged
+    // (profiles/r10_apply_tpb_ab.txt). BF_APPLY_TPB=256 (A/B): four-wave workgroups.
+    applyTpb_ = 64;
+    if (const char* e = std::getenv("BF_APPLY_TPB")) applyTpb_ = std::atoi(e) == 256 ? 256 : 64;
     if (applyTpb_ == 64)
         BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true, 64>, 64, 0));
     else
