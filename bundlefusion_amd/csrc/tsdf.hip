@@ -1761,11 +1761,28 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
     }
     // updated is the wave's total (scalar), rmw per lane
-    flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);
-    __syncthreads();
-    flush_stats2(A.stats, S_BUPD, lane_id_here() == 0 ? updated : 0u, S_BRMW, rmw);
-    __syncthreads();
-    flush_stats2(A.stats, S_BHALF, lane_id_here() == 0 ? halves : 0u, -1, 0);
+    if constexpr (TPB == 64) {
+        // one wave per workgroup: its sums go straight to the workgroup's counter slot (no LDS stage, no barriers)
+        const unsigned long long rmwW = wave_sum_u64(rmw);
+        if (lane_id_here() == 0) {
+            unsigned long long* st = A.stats + (size_t)(blockIdx.x % STAT_SLOTS) * STAT_FIELDS;
+            if (updated) {
+                atomicAdd(&st[S_VOXELS], (unsigned long long)updated);
+                atomicAdd(&st[S_BUPD], (unsigned long long)updated);
+            }
+            if (rmwW) {
+                atomicAdd(&st[S_RMW], rmwW);
+                atomicAdd(&st[S_BRMW], rmwW);
+            }
+            if (halves) atomicAdd(&st[S_BHALF], (unsigned long long)halves);
+        }
+    } else {
+        flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);
+        __syncthreads();
+        flush_stats2(A.stats, S_BUPD, lane_id_here() == 0 ? updated : 0u, S_BRMW, rmw);
+        __syncthreads();
+        flush_stats2(A.stats, S_BHALF, lane_id_here() == 0 ? halves : 0u, -1, 0);
+    }
 #ifdef BF_APPLY_DIAG
     __syncthreads();
     flush_stats2(A.stats, 20, diag[0], 21, diag[1]);
