@@ -95,13 +95,18 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     opt_.maxLocalCorr = or_default(o.maxLocalCorr, (S + 1) * S / 2 * 25u);
     opt_.maxGlobalCorr = or_default(o.maxGlobalCorr, opt_.maxKeyframes * 1000u);
 
-    BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
     // bundling stream priority: normal (as the scene stream) by default since the voxel pass runs in four
     // resident rounds (Scene::Scene); BF_BA_HIGH_PRIORITY=1: high throughout, =keyed: round 4's policy keyed
     // on each solve's size (switchBundlingPriority)
     sharded_ = so && so->shardCount > 1;
     int prLeast = 0, prGreatest = 0;
     BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
+    // BF_SCENE_HIGH_PRIORITY=1 (A/B): the scene stream at the highest priority (its workgroups dispatched ahead
+    // of the bundling streams' whenever both wait for slots)
+    if (const char* e = std::getenv("BF_SCENE_HIGH_PRIORITY"); e && std::atoi(e) == 1)
+        BF_HIP(hipStreamCreateWithPriority(&sceneStream_, hipStreamNonBlocking, prGreatest));
+    else
+        BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
     const char* env = std::getenv("BF_BA_HIGH_PRIORITY");
     const bool keyed = env && std::string(env) == "keyed";
     const char* forced = keyed ? nullptr : (env ? env : "0");
