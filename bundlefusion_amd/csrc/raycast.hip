@@ -170,11 +170,11 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
 
 // The same splat binned by screen tile, without global atomics: k_splat_quads writes each visible block's
 // covered pixel rectangle and encoded depths (one thread per block, rayIntervalSplatKernel's projection and
-// tests as above); k_splat_tiles gives each workgroup a 64x20 pixel tile that scans every rectangle, keeps
-// the ones overlapping its tile in LDS, and folds them into per-pixel min / max held in registers, then writes
+// tests as above); k_splat_tiles gives each workgroup a 64x8 pixel tile that scans its tile row's rectangles,
+// keeps the ones overlapping its tile in LDS, and folds them into per-pixel min / max held in registers, then writes
 // each pixel once. k_splat issued one atomic min and max per covered pixel (8.9 M per render on the bench
-// scene, ~30 per pixel, all to HBM); here the traffic is the rectangle list read once per tile (from L2) and
-// one store per pixel, and k_splat_clear is not needed. A pass a block does not take carries the clear value
+// scene, ~30 per pixel, all to HBM); here the traffic is the row's rectangle list read once per tile (from L2)
+// and one store per pixel, and k_splat_clear is not needed. A pass a block does not take carries the clear value
 // (enc(+inf) for min, enc(-inf) for max), which leaves the pixel unchanged, so the result is the same
 // order-independent min / max as the atomics'
 // 64x8 tiles (2 rows per wave), 8 rectangles per thread per chunk (32 KB of LDS list): 600 workgroups for
@@ -182,10 +182,10 @@ __global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible,
 // each with one wave per SIMD: BF_SPLAT_TILE_LOG), so it wants several waves per SIMD and few rows per wave;
 // 64x20 tiles (one workgroup per CU, 5 rows per wave) took 58 us, 64x8 37 us, 64x4 (1 200 workgroups) 38 us
 constexpr int ST_W = 64, ST_H = 8, ST_PX = ST_W * ST_H / 256, ST_Q = 8;  // tile, pixels per thread, rectangles per thread per chunk
-// Tile rows: each rectangle is also listed under every 20-pixel tile row it spans (count in k_splat_quads,
+// Tile rows: each rectangle is also listed under every ST_H-pixel tile row it spans (count in k_splat_quads,
 // exclusive scan in k_splat_rows, fill in k_splat_fill), so a tile scans its own row's rectangles instead of
-// all of them. Renders taller than ST_ROWS tile rows, or whose
-// row lists would exceed their capacity (4 entries per visible block), scan every rectangle.
+// all of them. Renders taller than ST_ROWS tile rows, or whose row lists would exceed their capacity
+// (4 entries per visible block), scan every rectangle.
 constexpr int ST_ROWS = 256;
 enum SplatBin { SB_COUNT = 0, SB_START = ST_ROWS, SB_LEN = 2 * ST_ROWS, SB_CURSOR = 3 * ST_ROWS, SB_TOTAL = 4 * ST_ROWS,
                 SB_OVERFLOW, SB_WORDS };
