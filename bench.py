@@ -533,11 +533,22 @@ def main():
     def barrier():
         group.barrier()
 
+    # visualizeFrame's render every frame (DepthSensing.cpp:790-793: compactify + CUDARayCastSDF::render after each
+    # integration), off the metric per SURVEY 8(d) but part of the reference's frame body: the last frames of the
+    # fill (as many as the timed tail, up to 200) run with it, between synchronizations -> frames_per_s_with_render
+    render_frames = min(fill, S * min(args.steps, 20)) if world == 1 else 0
+    render_from = fill - render_frames
+    rp_loop = bfa.raycast_params(args.width, args.height, fx=stream.cam.fx, fy=stream.cam.fy)
+    t_rw = None
     barrier()
     t_fill = time.perf_counter()
     last = t_fill
     prefix_times = {}
     for f in range(fill):
+        if render_frames and f == render_from:
+            rc.synchronize()
+            t_rw = time.perf_counter()
+            rc.set_render(rp_loop)
         rc.process_frame(f)
         if (f + 1) % PREFIX_STEP == 0 and f + 1 <= PREFIX_FRAMES:
             # the prefixes the CPU loop baseline may run (untimed region): synchronized checkpoints
@@ -548,6 +559,9 @@ def main():
             last = time.perf_counter()
     rc.synchronize()
     t_fill = time.perf_counter() - t_fill
+    if t_rw is not None:
+        t_rw = time.perf_counter() - t_rw
+        rc.set_render(None)
     fill_stats = rc.stats()
     rc.reset_stats()
     barrier()
@@ -562,6 +576,8 @@ def main():
     t_fill = group.max(t_fill)
     st = rc.stats()
     ss = rc.scene_stats()
+    # a dropped block would have failed the loop (BF_ERR_CAPACITY); the line states the headroom it had
+    cap = rc.scene_capacity()
     frames = S * args.steps
     P = args.width * args.height
     workload = (f"{frames_total}-frame {args.width}x{args.height} stream, {args.voxel * 1000:.0f} mm voxels, "
@@ -655,7 +671,7 @@ def main():
                          "until the queue drains; untimed, after the timed tail"}
     out = {
         "metric": f"frames/s integrate+global-BA on {args.width}x{args.height} @{args.voxel * 1000:g}mm voxels",
-        "value": frames / dt,
+        "value": frames / dt if cap["errorFlags"] == 0 else None,
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -677,6 +693,21 @@ def main():
                    "fill_frames_per_s": fill / t_fill if fill else None,
                    "fill_global_gn_iters": fill_stats["globalGnIterations"],
                    "note": "whole stream = fill + timed tail, same loop; value is the tail (largest K, largest scene)"},
+        "frames_per_s_with_render": (render_frames / t_rw) if t_rw else None,
+        "render_in_loop": {"frames": render_frames, "frames_window": [render_from, fill], "s": t_rw,
+                           "renders": fill_stats["renders"],
+                           "note": "the fill's last frames with visualizeFrame's render after each frame's batch "
+                                   "(bf_recon_set_render: compactify + splat + renderKernel + computeNormals at "
+                                   f"{args.width}x{args.height}), between synchronizations; the value above is the "
+                                   "next frames without it (the reference renders every frame for display, which "
+                                   "SURVEY 8(d) keeps out of the metric)"} if render_frames else None,
+        "scene_capacity": {"error_flags": cap["errorFlags"], "peak_candidates": cap["peakCandidates"],
+                           "candidate_capacity": cap["candidateCapacity"],
+                           "candidate_headroom": cap["candidateCapacity"] / max(1, cap["peakCandidates"]),
+                           "heap_free": cap["heapFree"], "num_sdf_blocks": cap["numSDFBlocks"],
+                           "high_water": cap["highWater"],
+                           "note": "peak alloc candidates of one batch over the whole stream vs the candidate "
+                                   "buffer; nonzero error_flags (a dropped block) fail the loop and void value"},
         "ms_per_gn_iter": solo["ms_per_gn_iter"],
         "global_solve": dict(solo, ms_per_gn_iter_in_loop=ms_gn_loop,
                              pcg_kernel_us_per_iter_in_loop=(st["globalPcgKernelMs"] * 1e3 / max(1, st["globalPcgIterations"])
@@ -789,8 +820,8 @@ def main():
                                          "pixel_updates_per_render": atomics,
                                          "pixel_updates_per_us": atomics / max(1e-9, splat_us),
                                          "note": "per covered pixel one min (near pass) and one max (far pass), folded in "
-                                                 "registers per 64x20 tile from the block rectangles that overlap it "
-                                                 "(BF_SPLAT_ATOMIC=1: one global atomic each)"},
+                                                 "registers per 64x8 tile from the block rectangles that overlap it "
+                                                 "(no global atomics)"},
                       "note": f"compactify + interval splat + renderKernel + computeNormals at {W_}x{H_} from the last pose"}
     # marching cubes over the final scene (StopScanningAndExtractIsoSurfaceMC, reported beside the metric)
     mcp = bfa.mc_params(params.virtualVoxelSize)

@@ -142,9 +142,11 @@ def depth_camera(width=640, height=480, fx=577.87, fy=577.87, mx=None, my=None, 
 class SceneRepHashSDF:
     """Mirror of CUDASceneRepHashSDF (DepthSensing/CUDASceneRepHashSDF.h:29-423) over bf_scene_*."""
 
-    def __init__(self, params: BFHashParams, candidate_capacity=0, shard_count=1, shard_index=0, shard_chunk=1.0):
+    def __init__(self, params: BFHashParams, candidate_capacity=0, shard_count=1, shard_index=0, shard_chunk=1.0,
+                 test_flags=0, splat_row_cap=0):
         self.params = params
         opts = BFSceneOptions(candidate_capacity, shard_count, shard_index, shard_chunk)
+        opts.testFlags, opts.splatRowCap = test_flags, splat_row_cap
         self.h = C.c_void_p()
         check(lib().bf_scene_create(C.byref(params), C.byref(opts), C.byref(self.h)))
 
@@ -203,6 +205,13 @@ class SceneRepHashSDF:
         n = C.c_uint32()
         check(lib().bf_scene_num_visible(self.h, C.byref(n)))
         return n.value
+
+    def capacity(self) -> dict:
+        """BFSceneCapacity: sticky error bits, peak alloc candidates vs capacity, heap (bf_scene_capacity)."""
+        from .abi import BFSceneCapacity
+        c = BFSceneCapacity()
+        check(lib().bf_scene_capacity(self.h, C.byref(c)))
+        return {k: getattr(c, k) for k, _ in BFSceneCapacity._fields_}
 
     def errorFlags(self) -> int:
         n = C.c_uint32()

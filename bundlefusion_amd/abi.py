@@ -95,7 +95,17 @@ class BFTsdfStats(C.Structure):
 
 class BFSceneOptions(C.Structure):
     _fields_ = [("candidateCapacity", C.c_uint32), ("shardCount", C.c_uint32),
-                ("shardIndex", C.c_uint32), ("shardChunk", C.c_float)]
+                ("shardIndex", C.c_uint32), ("shardChunk", C.c_float),
+                ("applyXcdRun", C.c_uint32), ("applyRounds", C.c_uint32), ("testFlags", C.c_uint32),
+                ("splatRowCap", C.c_uint32)]
+
+
+BF_SCENE_TEST_ALLOC_DIRECT = 1
+
+
+class BFSceneCapacity(C.Structure):  # include/bf/types.h
+    _fields_ = [(n, C.c_uint32) for n in ("errorFlags", "peakCandidates", "candidateCapacity", "heapFree",
+                                          "numSDFBlocks", "highWater")]
 
 
 class BFSynthScene(C.Structure):
@@ -158,7 +168,7 @@ class BFSolverOptions(C.Structure):
                 ("normalEquations", C.c_int32), ("disableEarlyOut", C.c_int32),
                 ("pcgLaunch", C.c_int32), ("pcgSpinLimitUs", C.c_uint32)]
 
-ABI_VERSION = 3  # include/bf/bf.h BF_ABI_VERSION: the struct layouts above
+ABI_VERSION = 4  # include/bf/bf.h BF_ABI_VERSION: the struct layouts above
 SOLVE_ERR_PAIR_BOUND, SOLVE_ERR_PCG_TIMEOUT, SOLVE_PCG_RECOVERED = 4, 8, 16  # BFSolveResult.error bits
 SOLVE_ERR_FATAL = 0xFFFFFFFF & ~SOLVE_PCG_RECOVERED
 
@@ -230,7 +240,7 @@ class BFReconOptions(C.Structure):
                 ("cacheWidth", C.c_uint32), ("cacheHeight", C.c_uint32), ("cacheIntrinsics", C.c_float * 4),
                 ("enableTiming", C.c_int32), ("recordOps", C.c_int32), ("asyncBundling", C.c_int32),
                 ("solver", BFSolverOptions), ("disableLocalVerify", C.c_int32), ("verify", BFVerifyOptions),
-                ("resultLag", C.c_uint32)]
+                ("resultLag", C.c_uint32), ("bundlingPriority", C.c_int32)]
 
 
 class BFRenderStats(C.Structure):  # include/bf/bf.h
@@ -263,7 +273,7 @@ class BFAppOptions(C.Structure):  # include/bf/bf.h: the FriedLiver application 
                 ("corrStride", C.c_uint32), ("corrDepthThresh", C.c_float), ("prefetchFrames", C.c_uint32),
                 ("decodeThreads", C.c_uint32), ("numSolveFramesBeforeExit", C.c_int32),
                 ("shardCount", C.c_uint32), ("shardIndex", C.c_uint32), ("shardChunk", C.c_float),
-                ("resultLag", C.c_uint32)]
+                ("resultLag", C.c_uint32), ("bundlingPriority", C.c_int32)]
 
 
 class BFAppInfo(C.Structure):
@@ -298,4 +308,4 @@ class BFReconStats(C.Structure):
         ("reintegrateLaunches", C.c_uint64), ("reintegrateKernelMs", C.c_double),
         ("localVerifications", C.c_uint64), ("invalidLocals", C.c_uint64), ("endSolves", C.c_uint64),
         ("pcgRecoveries", C.c_uint64), ("hostMs", C.c_double), ("hostWaitMs", C.c_double),
-        ("globalPcgLaunches", C.c_uint64), ("globalPcgKernelMs", C.c_double)]
+        ("globalPcgLaunches", C.c_uint64), ("globalPcgKernelMs", C.c_double), ("renders", C.c_uint64)]

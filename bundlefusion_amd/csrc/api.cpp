@@ -3,6 +3,7 @@
 #include "../../include/bf/bf.h"
 #include "ba.h"
 #include "recon.h"
+#include "host_pool.h"
 #include "trajectory.h"
 #include "bf_runtime.h"
 #include "synth.h"
@@ -157,6 +158,7 @@ int bf_abi_struct_size(const char* name, size_t* out) {
         {"BFFixOp", sizeof(BFFixOp)},
         {"BFSolveResult", sizeof(BFSolveResult)},
         {"BFTsdfStats", sizeof(BFTsdfStats)},
+        {"BFSceneCapacity", sizeof(BFSceneCapacity)},
         {"BFSensInfo", sizeof(BFSensInfo)},
         {"BFPreprocessOptions", sizeof(BFPreprocessOptions)},
         {"BFMarchingCubesParams", sizeof(BFMarchingCubesParams)},
@@ -197,6 +199,12 @@ int bf_device_count(int* count) {
 int bf_set_device(int device) {
     BF_TRY
     BF_HIP(hipSetDevice(device));
+    BF_CATCH
+}
+int bf_set_host_threads(int n) {
+    BF_TRY
+    BF_REQUIRE(n >= 1 && n <= 256, BF_ERR_ARG, "host threads 1..256");
+    HostPool::requested().store(n);
     BF_CATCH
 }
 int bf_device_synchronize(void) {
@@ -262,14 +270,7 @@ int bf_timer_destroy(bf_timer* t) {
 int bf_scene_create(const BFHashParams* params, const BFSceneOptions* opts, bf_scene** out) {
     BF_TRY
     BF_REQUIRE(params && out, BF_ERR_ARG, "null argument");
-    SceneConfig cfg{};
-    cfg.hp = *params;
-    if (opts) {
-        cfg.candCapacity = opts->candidateCapacity;
-        cfg.shardCount = opts->shardCount;
-        cfg.shardIndex = opts->shardIndex;
-        cfg.shardChunk = opts->shardChunk;
-    }
+    const SceneConfig cfg = scene_config(*params, opts);
     bf_scene* s = new bf_scene();
     try {
         BF_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
@@ -357,6 +358,12 @@ int bf_scene_error_flags(bf_scene* s, uint32_t* flags) {
     BF_TRY
     BF_REQUIRE(s && flags, BF_ERR_ARG, "null argument");
     *flags = s->scene->errorFlags();
+    BF_CATCH
+}
+int bf_scene_capacity(bf_scene* s, BFSceneCapacity* out) {
+    BF_TRY
+    BF_REQUIRE(s && out, BF_ERR_ARG, "null argument");
+    *out = s->scene->capacity();
     BF_CATCH
 }
 int bf_scene_get_stats(bf_scene* s, BFTsdfStats* out) {
@@ -701,6 +708,7 @@ int bf_comm_allreduce_sum_f64(bf_comm* c, double* d, size_t n) {
     try {
         c->c->allreduceSum(d, n, st);
         BF_HIP(hipStreamSynchronize(st));
+        c->c->checkError();  // a collective that timed out waiting for a rank leaves no valid sum
     } catch (...) {
         (void)hipStreamDestroy(st);
         throw;
@@ -837,6 +845,12 @@ int bf_recon_heap_free_count(bf_recon* r, uint32_t* count) {
     *count = r->r->scene().heapFreeCount();
     BF_CATCH
 }
+int bf_recon_scene_capacity(bf_recon* r, BFSceneCapacity* out) {
+    BF_TRY
+    BF_REQUIRE(r && out, BF_ERR_ARG, "null argument");
+    *out = r->r->sceneCapacity();
+    BF_CATCH
+}
 int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n) {
     BF_TRY
     BF_REQUIRE(r && T, BF_ERR_ARG, "null argument");
@@ -864,6 +878,19 @@ int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, 
     BF_REQUIRE(r && T && rp, BF_ERR_ARG, "null argument");
     r->r->scene().raycast(to_mat(T), r->r->camera(), *rp, depth, reinterpret_cast<float4*>(depth4),
                           reinterpret_cast<float4*>(normals), reinterpret_cast<float4*>(colors), nullptr, nullptr);
+    BF_CATCH
+}
+int bf_recon_set_render(bf_recon* r, const BFRayCastParams* rp) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null argument");
+    r->r->setRender(rp);
+    BF_CATCH
+}
+int bf_recon_render_output(bf_recon* r, const float** depth, const float** depth4, const float** normals,
+                           const float** colors) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null argument");
+    r->r->renderOutput(depth, depth4, normals, colors);
     BF_CATCH
 }
 int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTriangle* tris, uint32_t* numTriangles,
@@ -1433,12 +1460,6 @@ int bf_params_preprocess_options(const bf_params* p, float depthShift, BFPreproc
     BF_CATCH
 }
 
-// input preprocessing streams: highest priority unless BF_INPUT_PRIORITY=0 (A/B)
-static int input_stream_priority(int least, int greatest) {
-    const char* e = std::getenv("BF_INPUT_PRIORITY");
-    return (e && std::atoi(e) == 0) ? least : greatest;
-}
-
 int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_t colorH, uint32_t integrationW,
                       uint32_t integrationH, const BFPreprocessOptions* opt, bf_preproc** out) {
     BF_TRY
@@ -1449,7 +1470,7 @@ int bf_preproc_create(uint32_t depthW, uint32_t depthH, uint32_t colorW, uint32_
     // its kernels take free slots ahead of the voxel pass's next round and of the bundling launches
     int prLeast = 0, prGreatest = 0;
     BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
-    BF_HIP(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, input_stream_priority(prLeast, prGreatest)));
+    BF_HIP(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prGreatest));
     h->p = new Preproc(depthW, depthH, colorW, colorH, integrationW, integrationH, *opt, h->stream);
     *out = h.release();
     BF_CATCH

@@ -214,8 +214,7 @@ App::App(const std::string& appParams, const std::string& bundlingParams, const 
     {   // the input stream (upload, preprocessing, cache, EntryJ) feeds the loop's next batch: highest priority
         int prLeast = 0, prGreatest = 0;
         BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
-        const char* e = std::getenv("BF_INPUT_PRIORITY");
-        BF_HIP(hipStreamCreateWithPriority(&pre_, hipStreamNonBlocking, (e && std::atoi(e) == 0) ? prLeast : prGreatest));
+        BF_HIP(hipStreamCreateWithPriority(&pre_, hipStreamNonBlocking, prGreatest));
     }
     BF_HIP(hipEventCreateWithFlags(&uploadEv_, hipEventDisableTiming));
     preproc_.reset(new Preproc(si.depthWidth, si.depthHeight, si.colorWidth, si.colorHeight, iw, ih, info_.preprocess, pre_));

@@ -2866,7 +2866,6 @@ SolverConfig make_solver_config(uint32_t maxImages, uint32_t maxCorr, const BFSo
     cfg.normalEquations = o ? o->normalEquations : 0;
     cfg.earlyOut = !(o && o->disableEarlyOut);
     cfg.pcgLaunch = o ? o->pcgLaunch : 0;
-    if (const char* e = std::getenv("BF_PCG_LAUNCH")) cfg.pcgLaunch = std::atoi(e);  // A/B measurements
     cfg.pcgSpinLimitUs = o ? o->pcgSpinLimitUs : 0u;
     return cfg;
 }

@@ -46,6 +46,14 @@ void Comm::allreduceSum(double* buf, size_t n, hipStream_t stream) {
     BF_NCCL(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, static_cast<ncclComm_t>(comm_), stream));
 }
 
+void Comm::checkError() const {
+    if (lb_) return loopbackCheck();
+    if (!comm_) return;
+    ncclResult_t async = ncclSuccess;
+    BF_NCCL(ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &async));
+    BF_REQUIRE(async == ncclSuccess, BF_ERR_INTERNAL, std::string("RCCL communicator error: ") + ncclGetErrorString(async));
+}
+
 void Comm::broadcast(float* buf, size_t n, int root, hipStream_t stream) {
     if (n == 0) return;
     if (lb_) {

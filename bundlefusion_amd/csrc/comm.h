@@ -37,9 +37,14 @@ public:
     void allreduceSum(double* buf, size_t n, hipStream_t stream);
     // root's n floats to every rank, in place, enqueued on stream
     void broadcast(float* buf, size_t n, int root, hipStream_t stream);
+    // after synchronising the streams that carried this communicator's collectives: throws BF_ERR_INTERNAL when
+    // one of them failed (loopback: a wait for a rank timed out, so its sums are not valid; RCCL: the
+    // communicator's asynchronous error)
+    void checkError() const;
 
 private:
     void loopbackCollective(void* buf, size_t n, size_t elemBytes, int kind, int root, hipStream_t stream);
+    void loopbackCheck() const;
     void* comm_ = nullptr;  // ncclComm_t
     std::shared_ptr<Loopback> lb_;
     int nranks_ = 1, rank_ = 0;

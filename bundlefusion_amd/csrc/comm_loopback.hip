@@ -7,9 +7,13 @@
 // counters, one per slot parity, so slots are reused every other collective without a departure barrier
 // (a rank refills parity p only after every rank arrived at the collective in between, hence finished
 // reading p). Every wait is bounded: a rank that never arrives sets the group's error word (host memory)
-// and the collective ends with whatever the slots hold; the next call on the host throws.
+// and the collective ends with whatever the slots hold. Nothing may consume those: the next collective
+// call throws, and so does Comm::checkError, which the callers run after synchronising the streams that
+// carry collectives (bf_comm_allreduce_sum_f64, Recon::apply before a submap's poses are used,
+// Recon::synchronize); a group destroyed with the word set reports it on stderr.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -80,6 +84,8 @@ struct Loopback {
     std::vector<std::pair<uint32_t, size_t>> sizes;  // (collective, bytes) of recent collectives, by seq % 64
     ~Loopback() {
         (void)hipDeviceSynchronize();  // no collective kernel may still use the slots
+        if (err && __atomic_load_n(err, __ATOMIC_ACQUIRE) != 0)
+            fprintf(stderr, "bf loopback communicator: a collective timed out waiting for a rank (results after it are invalid)\n");
         if (err) (void)hipHostFree(err);
     }
 };
@@ -105,11 +111,15 @@ Comm::Comm(std::shared_ptr<Loopback> group, int rank) : lb_(std::move(group)), n
     BF_REQUIRE(lb_ && rank >= 0 && rank < nranks_, BF_ERR_ARG, "loopback rank");
 }
 
-void Comm::loopbackCollective(void* buf, size_t n, size_t elemBytes, int kind, int root, hipStream_t stream) {
-    Loopback& g = *lb_;
-    BF_REQUIRE(__atomic_load_n(g.err, __ATOMIC_ACQUIRE) == 0, BF_ERR_INTERNAL,
+void Comm::loopbackCheck() const {
+    BF_REQUIRE(__atomic_load_n(lb_->err, __ATOMIC_ACQUIRE) == 0, BF_ERR_INTERNAL,
                "loopback communicator: a rank did not reach a collective in time "
                "(ranks issued different collective sequences)");
+}
+
+void Comm::loopbackCollective(void* buf, size_t n, size_t elemBytes, int kind, int root, hipStream_t stream) {
+    Loopback& g = *lb_;
+    loopbackCheck();
     const size_t bytes = n * elemBytes;
     BF_REQUIRE(bytes <= g.slotBytes, BF_ERR_CAPACITY, "loopback collective larger than the group's slot capacity");
     uint32_t s;

@@ -214,7 +214,9 @@ uint32_t corr_from_pairs(const float* const* depth, const float* T, const float*
     return corr_run(A, npairs, o, out, cap, total, stream, sc);
 }
 
-// host entry (bf_corr_from_depth): pairs (start .. cur - 1, cur), on its own stream and scratch
+// host entry (bf_corr_from_depth): pairs (start .. cur - 1, cur), with its own scratch, on the null stream, so
+// it is ordered after the caller's work on the legacy stream (depth, poses, the pointer table) as the reference's
+// AddCurrToResidualsCU on the default stream is; corr_run waits for its count before returning
 uint32_t corr_from_depth(const float* const* depth, const float* T, const float* Tinv, uint32_t cur, uint32_t start,
                          const BFCorrOptions& o, BFEntryJ* out, uint32_t cap, uint32_t* total) {
     BF_REQUIRE(depth && T && Tinv, BF_ERR_ARG, "null input");
@@ -228,17 +230,7 @@ uint32_t corr_from_depth(const float* const* depth, const float* T, const float*
     CorrArgs A = corr_args(depth, T, Tinv, o);
     A.cur = cur;
     A.start = start;
-    hipStream_t s = nullptr;
-    BF_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    uint32_t n = 0;
-    try {
-        n = corr_run(A, pairs, o, out, cap, total, s, sc);
-    } catch (...) {
-        (void)hipStreamDestroy(s);
-        throw;
-    }
-    BF_HIP(hipStreamDestroy(s));
-    return n;
+    return corr_run(A, pairs, o, out, cap, total, nullptr, sc);
 }
 
 }  // namespace bf

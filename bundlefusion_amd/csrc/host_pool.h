@@ -3,7 +3,8 @@
 // 5 000 frames ~0.3 ms each, once per submap, on the frame thread that also issues the GPU work).
 // parallel_for splits [0, n) into contiguous chunks, runs one on the calling thread and waits for the
 // rest; the loop bodies are independent per element, so results do not depend on the split.
-// BF_HOST_THREADS (default 4) sets the thread count including the caller; 1 runs everything inline.
+// bf_set_host_threads (default 4) sets the thread count including the caller before the pool's first use;
+// 1 runs everything inline.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -18,8 +19,13 @@ namespace bf {
 class HostPool {
 public:
     static HostPool& get() {
-        static HostPool* p = new HostPool();  // leaked on purpose: no join ordering at process exit
+        static HostPool* p = new HostPool(requested());  // leaked on purpose: no join ordering at process exit
         return *p;
+    }
+    // threads for the pool, counting the caller (bf_set_host_threads); read once, at the pool's first use
+    static std::atomic<int>& requested() {
+        static std::atomic<int> n{4};
+        return n;
     }
     int threads() const { return (int)workers_.size() + 1; }
 
@@ -49,9 +55,8 @@ public:
     }
 
 private:
-    HostPool() {
-        int n = 4;
-        if (const char* e = std::getenv("BF_HOST_THREADS")) n = std::max(1, std::atoi(e));
+    explicit HostPool(const std::atomic<int>& req) {
+        const int n = std::max(1, req.load());
         for (int i = 1; i < n; i++) workers_.emplace_back([this, i] { loop((size_t)i); });
         for (auto& w : workers_) w.detach();
     }

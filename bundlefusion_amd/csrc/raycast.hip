@@ -98,83 +98,14 @@ __device__ __forceinline__ f3 rc_depth_to_camera(const BFRayCastParams& p, uint3
 __device__ __forceinline__ f3 fmin3(f3 a, f3 b) { return mk3(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
 __device__ __forceinline__ f3 fmax3(f3 a, f3 b) { return mk3(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
 
-__global__ void k_splat_clear(uint32_t* smin, uint32_t* smax, uint32_t n) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        smin[i] = enc_f(__builtin_inff());
-        smax[i] = enc_f(-__builtin_inff());
-    }
-}
-
-// rayIntervalSplatKernel (CUDARayCastSDF.cu:101-190) for both passes + the raster of its quads
-__global__ __launch_bounds__(256) void k_splat(const int4* __restrict__ visible, const uint32_t* ctrl, float voxelSize,
-                                               BFDepthCameraParams cam, BFRayCastParams rp, uint32_t* smin, uint32_t* smax,
-                                               unsigned long long* stats) {
-    const uint32_t n = ctrl[C_VISIBLE];
-    uint32_t quads = 0, atoms = 0;  // per wave (uniform): rasterised blocks, atomic depth updates
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const BFMat4 V = rp.viewMatrix;
-    for (uint32_t b = wave; b < n; b += nwaves) {
-        const int4 e = visible[b];
-        if (!block_in_frustum(cam, V, e.x, e.y, e.z, voxelSize)) continue;  // :107 (isSDFBlockInCameraFrustumApprox)
-        const f3 wv = block_to_world(e.x, e.y, e.z, voxelSize);
-        const float hv = voxelSize / 2.0f;
-        const f3 MINV = mk3(wv.x - hv, wv.y - hv, wv.z - hv);
-        const float ext = (float)BF_SDF_BLOCK_SIZE * voxelSize;
-        const f3 maxv = mk3(MINV.x + ext, MINV.y + ext, MINV.z + ext);
-        const f3 p000 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, MINV.y, MINV.z)));
-        const f3 p100 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, MINV.y, MINV.z)));
-        const f3 p010 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, maxv.y, MINV.z)));
-        const f3 p001 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, MINV.y, maxv.z)));
-        const f3 p110 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, maxv.y, MINV.z)));
-        const f3 p011 = camera_to_depth_proj(rp, xform(V, mk3(MINV.x, maxv.y, maxv.z)));
-        const f3 p101 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, MINV.y, maxv.z)));
-        const f3 p111 = camera_to_depth_proj(rp, xform(V, mk3(maxv.x, maxv.y, maxv.z)));
-        const f3 mn = fmin3(fmin3(fmin3(p000, p100), fmin3(p010, p001)), fmin3(fmin3(p110, p011), fmin3(p101, p111)));
-        const f3 mx = fmax3(fmax3(fmax3(p000, p100), fmax3(p010, p001)), fmax3(fmax3(p110, p011), fmax3(p101, p111)));
-        // depthProjToCameraZ (RayCastSDFUtil.h:196-199)
-        const float dwMin = mn.z * (rp.maxDepth - rp.minDepth) + rp.minDepth;
-        const float dwMax = mx.z * (rp.maxDepth - rp.minDepth) + rp.minDepth;
-        const bool minOk = mn.z < 1.0f;  // LESS vs depth cleared to 1 (NDC z clamped to [0,1])
-        const bool maxOk = mx.z > 0.0f;  // GREATER vs depth cleared to 0
-        if (!minOk && !maxOk) continue;
-        const float W = (float)rp.width, H = (float)rp.height;
-        const float left = (mn.x + 1.0f) * 0.5f * W, right = (mx.x + 1.0f) * 0.5f * W;
-        const float top = (1.0f - mx.y) * 0.5f * H, bottom = (1.0f - mn.y) * 0.5f * H;
-        if (!(left < right) || !(top < bottom)) continue;  // empty or NaN
-        const float fx0 = ceilf(left - 0.5f), fx1 = ceilf(right - 0.5f) - 1.0f;
-        const float fy0 = ceilf(top - 0.5f), fy1 = ceilf(bottom - 0.5f) - 1.0f;
-        if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) continue;
-        const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
-        const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
-        if (x1 < x0 || y1 < y0) continue;
-        const uint32_t w = (uint32_t)(x1 - x0 + 1), npx = w * (uint32_t)(y1 - y0 + 1);
-        const uint32_t emin = enc_f(dwMin), emax = enc_f(dwMax);
-        quads++;
-        // every covered pixel takes an atomic min / max (no return value: the wave does not wait on
-        // them). Reading the target first to skip the atomics that cannot change it cut them 3x
-        // (8.9 -> 2.9 M per render) but put a dependent load in front of each: 143 -> 178 us
-        atoms += npx * ((minOk ? 1u : 0u) + (maxOk ? 1u : 0u));
-        for (uint32_t k = lane; k < npx; k += 64) {
-            const uint32_t idx = (uint32_t)(y0 + (int)(k / w)) * rp.width + (uint32_t)(x0 + (int)(k % w));
-            if (minOk) atomicMin(&smin[idx], emin);
-            if (maxOk) atomicMax(&smax[idx], emax);
-        }
-    }
-    if (lane == 0 && quads) {
-        atomicAdd(&rs_slot(stats)[RS_QUADS], (unsigned long long)quads);
-        atomicAdd(&rs_slot(stats)[RS_ATOMICS], (unsigned long long)atoms);
-    }
-}
-
-// The same splat binned by screen tile, without global atomics: k_splat_quads writes each visible block's
-// covered pixel rectangle and encoded depths (one thread per block, rayIntervalSplatKernel's projection and
-// tests as above); k_splat_tiles gives each workgroup a 64x8 pixel tile that scans its tile row's rectangles,
-// keeps the ones overlapping its tile in LDS, and folds them into per-pixel min / max held in registers, then writes
-// each pixel once. k_splat issued one atomic min and max per covered pixel (8.9 M per render on the bench
-// scene, ~30 per pixel, all to HBM); here the traffic is the row's rectangle list read once per tile (from L2)
-// and one store per pixel, and k_splat_clear is not needed. A pass a block does not take carries the clear value
+// rayIntervalSplatKernel (CUDARayCastSDF.cu:101-190) for both passes + the raster of its quads, binned by screen
+// tile, without global atomics: k_splat_quads writes each visible block's covered pixel rectangle and encoded
+// depths (one thread per block: the 8 corners projected with cameraToDepthProj, min / max NDC depth rectangles);
+// k_splat_tiles gives each workgroup a 64x8 pixel tile that scans its tile row's rectangles, keeps the ones
+// overlapping its tile in LDS, and folds them into per-pixel min / max held in registers, then writes each pixel
+// once. The first form issued one atomic min and max per covered pixel (8.9 M per render on the bench scene, ~30
+// per pixel, all to HBM: 145 us for the splat against 56 us now); here the traffic is the row's rectangle list
+// read once per tile (from L2) and one store per pixel, and no clear pass is needed. A pass a block does not take carries the clear value
 // (enc(+inf) for min, enc(-inf) for max), which leaves the pixel unchanged, so the result is the same
 // order-independent min / max as the atomics'
 // 64x8 tiles (2 rows per wave), 8 rectangles per thread per chunk (32 KB of LDS list): 600 workgroups for
@@ -783,25 +714,16 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
         splatMax_.alloc(P);
         splatCap_ = P;
     }
-    const bool atomicSplat = splatAtomic_;
-    if (atomicSplat) {
-        k_splat_clear<<<std::max(1u, std::min(div_up(P, 256), 2048u)), 256, 0, stream_>>>(splatMin_.p, splatMax_.p, (uint32_t)P);
-        BF_LAUNCH_CHECK();
-    } else if (!splatQuads_.p) {
-        splatQuads_.alloc(B_);
-    }
+    if (!splatQuads_.p) splatQuads_.alloc(B_);
     const bool timed = renderClock_.enabled();
     if (timed) {
         if (!splatClock_.enabled()) splatClock_.enable(true);
         splatClock_.start(stream_);
     }
-    if (atomicSplat) {
-        k_splat<<<(unsigned)numCUs_ * 4, 256, 0, stream_>>>(visible_.p, ctrl_.p, cfg_.hp.virtualVoxelSize, cam, rp, splatMin_.p,
-                                                              splatMax_.p, renderStats_.p);
-    } else {
+    {
         BF_REQUIRE(rp.width <= 0xFFFFu && rp.height <= 0x7FFFu, BF_ERR_ARG, "raycast size (16-bit splat rectangles)");
         const bool rows = div_up(rp.height, ST_H) <= (unsigned)ST_ROWS;
-        const uint32_t rowCap = splatRowCap_ ? splatRowCap_ : 4u * B_;
+        const uint32_t rowCap = cfg_.splatRowCap ? cfg_.splatRowCap : 4u * B_;
         if (rows && !splatBin_.p) {
             splatBin_.alloc(SB_WORDS);
             BF_HIP(hipMemsetAsync(splatBin_.p, 0, splatBin_.bytes(), stream_));
@@ -818,10 +740,13 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
             k_splat_fill<<<qgrid, 256, 0, stream_>>>(splatQuads_.p, ctrl_.p, bin, splatRowIdx_.p, rowCap);
             BF_LAUNCH_CHECK();
         }
-        // BF_SPLAT_TILE_LOG=path (diagnostics): per tile {start, end, __smid, rectangles folded | scanned << 32}
-        static const char* tileLogPath = std::getenv("BF_SPLAT_TILE_LOG");
         const dim3 tg(div_up(rp.width, ST_W), div_up(rp.height, ST_H));
         const size_t nTiles = (size_t)tg.x * tg.y;
+#ifdef BF_RENDER_DIAG  // diagnostics build: BF_SPLAT_TILE_LOG=path, per tile {start, end, __smid, rectangles folded | scanned << 32}
+        static const char* tileLogPath = std::getenv("BF_SPLAT_TILE_LOG");
+#else
+        static const char* tileLogPath = nullptr;
+#endif
         if (tileLogPath && tileLog_.n < 4 * nTiles) tileLog_.alloc(4 * nTiles);
         k_splat_tiles<<<tg, 256, 0, stream_>>>(splatQuads_.p, ctrl_.p, rp.width, rp.height, splatMin_.p, splatMax_.p, bin,
                                                splatRowIdx_.p, tileLogPath ? tileLog_.p : nullptr);
@@ -846,14 +771,13 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
     R.numEntries = E_;
     R.maxList = cfg_.hp.hashMaxCollisionLinkedListSize;
     R.voxelSize = cfg_.hp.virtualVoxelSize;
-    static const bool ldsTable = [] {
-        const char* e = std::getenv("BF_RENDER_LDS_TABLE");  // A/B: 0 = probe every block-cache miss
-        return !(e && std::atoi(e) == 0);
-    }();
-    R.ldsTable = ldsTable && cfg_.hp.numSDFBlocks < 0xFFFFFFu ? 1u : 0u;
-    // BF_RENDER_WAVE_LOG=path (diagnostics): every render appends {waves, then per wave start / end wall clock
-    // (100 MHz), __smid, longest per-lane march} to path, synchronising the stream after the render
+    R.ldsTable = cfg_.hp.numSDFBlocks < 0xFFFFFFu ? 1u : 0u;
+#ifdef BF_RENDER_DIAG  // diagnostics build: BF_RENDER_WAVE_LOG=path, every render appends {waves, then per wave start /
+                       // end wall clock (100 MHz), __smid, longest per-lane march}, synchronising the stream after it
     static const char* waveLogPath = std::getenv("BF_RENDER_WAVE_LOG");
+#else
+    static const char* waveLogPath = nullptr;
+#endif
     const size_t nWaves = (size_t)div_up(rp.width, 16) * div_up(rp.height, 16) * 4;  // >= the 8x8 squares of either tile shape
     R.waveLog = nullptr;
     if (waveLogPath) {
@@ -861,20 +785,12 @@ void Scene::raycast(const BFMat4& T, const BFDepthCameraParams& cam, const BFRay
         R.waveLog = waveLog_.p;
     }
     const dim3 g(div_up(rp.width, 16), div_up(rp.height, 16));
-    static const int tpb = [] {
-        const char* e = std::getenv("BF_RENDER_TPB");
-        return e && std::atoi(e) == 64 ? 64 : 256;
-    }();
     if (timed) renderClock_.start(stream_);
-    auto launch = [&](auto kern, dim3 grid, unsigned tpbLaunch) {
-        kern<<<grid, tpbLaunch, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
-                                              renderStats_.p);
+    auto launch = [&](auto kern) {
+        kern<<<g, 256, 0, stream_>>>(R, rp, splatMin_.p, splatMax_.p, depth, depth4, normals, colors, rayMin, rayMax,
+                                     renderStats_.p);
     };
-    const dim3 g8(div_up(rp.width, 8), div_up(rp.height, 8));
-    if (tpb == 64)
-        rp.useGradients ? launch(k_render<64, true>, g8, 64) : launch(k_render<64, false>, g8, 64);
-    else
-        rp.useGradients ? launch(k_render<256, true>, g, 256) : launch(k_render<256, false>, g, 256);
+    rp.useGradients ? launch(k_render<256, true>) : launch(k_render<256, false>);
     BF_LAUNCH_CHECK();
     if (timed) renderClock_.stop(stream_);
     if (waveLogPath) {

@@ -95,22 +95,18 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
     opt_.maxLocalCorr = or_default(o.maxLocalCorr, (S + 1) * S / 2 * 25u);
     opt_.maxGlobalCorr = or_default(o.maxGlobalCorr, opt_.maxKeyframes * 1000u);
 
-    // bundling stream priority: normal (as the scene stream) by default since the voxel pass runs in four
-    // resident rounds (Scene::Scene); BF_BA_HIGH_PRIORITY=1: high throughout, =keyed: round 4's policy keyed
-    // on each solve's size (switchBundlingPriority)
+    // bundling stream priority (BFReconOptions.bundlingPriority): normal (as the scene stream) by default since
+    // the voxel pass runs in resident rounds (Scene::Scene); 1: high throughout; 2: round 4's policy keyed on each
+    // solve's size (switchBundlingPriority). (The scene stream itself at the highest priority measured slower:
+    // 1 517 -> 1 499-1 502 frames/s at the bench workload, config 4's stream 1 103 -> 1 055.)
     sharded_ = so && so->shardCount > 1;
     int prLeast = 0, prGreatest = 0;
     BF_HIP(hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest));
-    // BF_SCENE_HIGH_PRIORITY=1 (A/B): the scene stream at the highest priority (its workgroups dispatched ahead
-    // of the bundling streams' whenever both wait for slots)
-    if (const char* e = std::getenv("BF_SCENE_HIGH_PRIORITY"); e && std::atoi(e) == 1)
-        BF_HIP(hipStreamCreateWithPriority(&sceneStream_, hipStreamNonBlocking, prGreatest));
-    else
-        BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
-    const char* env = std::getenv("BF_BA_HIGH_PRIORITY");
-    const bool keyed = env && std::string(env) == "keyed";
-    const char* forced = keyed ? nullptr : (env ? env : "0");
-    if (forced) priorityPolicy_ = std::atoi(forced) != 0 ? 1 : 0;
+    BF_HIP(hipStreamCreateWithFlags(&sceneStream_, hipStreamNonBlocking));
+    BF_REQUIRE(o.bundlingPriority >= 0 && o.bundlingPriority <= 2, BF_ERR_ARG, "bundlingPriority 0..2");
+    const bool keyed = o.bundlingPriority == 2;
+    const bool forced = !keyed;
+    if (forced) priorityPolicy_ = o.bundlingPriority;
     const bool needHigh = forced ? priorityPolicy_ == 1 : true;
     const bool needNormal = forced ? priorityPolicy_ == 0 : (!sharded_ && opt_.maxKeyframes > kHighPriorityMaxKeyframes);
     if (needHigh) {
@@ -128,15 +124,8 @@ Recon::Recon(const BFHashParams& hp, const BFSceneOptions* so, const BFDepthCame
         BF_HIP(hipEventCreateWithFlags(&localDone_[b], hipEventDisableTiming));
         BF_HIP(hipEventCreateWithFlags(&globalDone_[b], hipEventDisableTiming));
     }
-    SceneConfig sc{};
-    sc.hp = hp;
-    if (so) {
-        sc.candCapacity = so->candidateCapacity;
-        sc.shardCount = so->shardCount;
-        sc.shardIndex = so->shardIndex;
-        sc.shardChunk = so->shardChunk;
-    }
-    scene_.reset(new Scene(sc, sceneStream_));
+    scene_.reset(new Scene(scene_config(hp, so), sceneStream_));
+    scene_->enableErrorMirror();  // checkScene: the scene's error bits each frame without a synchronization
     tileStride_ = Scene::tileCount(cam_);
     framePixels_ = Scene::dcCount(cam_);
     // the cache costs 8 B per pixel per frame (12.3 GB for 5 000 VGA frames, next to the frame store
@@ -341,6 +330,39 @@ void Recon::setInitialPose(const BFMat4& T0) {
     BF_HIP(hipStreamSynchronize(baStream_));
 }
 
+void Recon::checkScene(bool exact) {
+    const uint32_t e = exact ? scene_->errorFlags() : scene_->mirroredErrorFlags();
+    if (e == 0) return;
+    std::string why;
+    if (e & 1u) why += " alloc candidate buffer overflow (raise BFSceneOptions.candidateCapacity);";
+    if (e & 2u) why += " SDF block heap exhausted (raise s_hashNumSDFBlocks);";
+    if (e & 4u) why += " alloc candidate dedup set congested (raise BFSceneOptions.candidateCapacity);";
+    throw Error(BF_ERR_CAPACITY, "scene capacity exceeded, blocks were dropped (BFSceneCapacity.errorFlags = " +
+                                     std::to_string(e) + "):" + why);
+}
+
+void Recon::setRender(const BFRayCastParams* rp) {
+    render_ = rp != nullptr;
+    if (!rp) return;
+    BF_REQUIRE(rp->width > 0 && rp->height > 0, BF_ERR_ARG, "render size");
+    renderParams_ = *rp;
+    const size_t P = (size_t)rp->width * rp->height;
+    if (rDepth_.n < P) {
+        BF_HIP(hipStreamSynchronize(sceneStream_));  // an earlier render may still write the old images
+        rDepth_.alloc(P);
+        rDepth4_.alloc(P);
+        rNormals_.alloc(P);
+        rColors_.alloc(P);
+    }
+}
+
+void Recon::renderOutput(const float** depth, const float** depth4, const float** normals, const float** colors) const {
+    if (depth) *depth = rDepth_.p;
+    if (depth4) *depth4 = reinterpret_cast<const float*>(rDepth4_.p);
+    if (normals) *normals = reinterpret_cast<const float*>(rNormals_.p);
+    if (colors) *colors = reinterpret_cast<const float*>(rColors_.p);
+}
+
 void Recon::logOp(int kind, uint32_t frame, const BFMat4* T) {
     if (!opt_.recordOps) return;
     BFFixOp e{};
@@ -357,6 +379,7 @@ void Recon::recordInputs(uint32_t f, hipStream_t s) {
     if (!e) BF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     BF_HIP(hipEventRecord(e, s));
     prePending_[f % kPreSlots] = true;
+    preFrame_[f % kPreSlots] = f;
 }
 
 void Recon::inputsProduced(uint32_t f, hipStream_t s) {
@@ -422,6 +445,7 @@ void Recon::runReintegrate() {
 void Recon::processFrame(uint32_t f) {
     const auto tStart = std::chrono::steady_clock::now();
     BF_REQUIRE(f == numFrames_, BF_ERR_STATE, "frames must be processed in order");
+    checkScene(false);  // a block dropped by an earlier frame's batch fails the loop (no silent holes)
     BF_REQUIRE(f < opt_.maxFrames && frames_[f].set, BF_ERR_STATE, "frame not in the frame store");
     const uint32_t S = opt_.submapSize;
     const uint32_t s = f / S;
@@ -464,7 +488,14 @@ void Recon::processFrame(uint32_t f) {
             kf_[s] = mat4_mul(kf_[s - 1], mat4_mul(frames_[f - 1].Tlocal, fr.Tinc));
         }
     }
+    const bool renderNow = render_ && pendingInt_;  // this frame's batch integrates frame f - 1 at pendingOp_.T
+    const BFMat4 renderT = pendingOp_.T;
     runReintegrate();
+    if (renderNow) {  // visualizeFrame (DepthSensing.cpp:790-793) of the frame the batch integrated
+        BF_HOST_T(HS_SCENE);
+        scene_->raycast(renderT, cam_, renderParams_, rDepth_.p, rDepth4_.p, rNormals_.p, rColors_.p, nullptr, nullptr);
+        st_.renders++;
+    }
     fr.Tlocal = (f % S == 0) ? identity() : mat4_mul(frames_[f - 1].Tlocal, fr.Tinc);
     const BFMat4 T = mat4_mul(kf_[s], fr.Tlocal);  // getCurrentIntegrationFrame
     pendingOp_ = frameOp(f, T, false);
@@ -479,6 +510,7 @@ void Recon::processFrame(uint32_t f) {
 }
 
 void Recon::reintegrate() {
+    checkScene(false);
     applyPending(false);
     runReintegrate();
 }
@@ -910,6 +942,9 @@ void Recon::applyPending(bool block) {
 // updateTrajectoryCU (OnlineBundler.cu:73-110) + TrajectoryManager::updateOptimizedTransform
 void Recon::apply(Pending& P) {
     const uint32_t S = opt_.submapSize, s = P.submap, n = P.numLocal, nk = P.numKeyframes;
+    // the submap's solves are done (its event): a collective among them (the local-pose broadcast, the pair-
+    // statistics all-reduces) that failed leaves poses no rank may use
+    if (comm_) comm_->checkError();
     // a solve whose result is not a valid solve is never consumed: the loop fails instead (a timed-out
     // persistent PCG launch is redone on the device and flagged BF_SOLVE_PCG_RECOVERED, which is valid)
     for (int which = 0; which < 2; which++) {
@@ -986,6 +1021,8 @@ void Recon::synchronize() {
     BF_HIP(hipStreamSynchronize(sceneStream_));
     BF_HIP(hipStreamSynchronize(localStream_));
     BF_HIP(hipStreamSynchronize(baStream_));
+    if (comm_) comm_->checkError();
+    checkScene(true);
     applyPending(true);
 }
 
@@ -1097,8 +1134,9 @@ void Recon::preprocessFrame(uint32_t f) {
 // Bundler::storeCachedFrame (Bundler.cpp:278-281) for frame f, on the cache's stream
 void Recon::storeCacheFrame(uint32_t f) {
     FrameRef& fr = frames_[f];
-    if (preproc_ && fr.rawDepth && cache_->stream() != preproc_->stream())
-        BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_[f % kPreSlots], 0));
+    // the frame's inputs were produced on another stream (the loop's preprocessing, or the caller's own work
+    // announced by bf_recon_frame_ready): the cache reads them only after that work (its own stream waits)
+    if (preFrame_[f % kPreSlots] == f) BF_HIP(hipStreamWaitEvent(cache_->stream(), preEv_[f % kPreSlots], 0));
     BF_REQUIRE(cache_->numFrames() == f, BF_ERR_STATE, "attached cache must hold exactly the frames before this one");
     // multi-GPU: a rank solves only its own local submaps (round-robin, issueSubmap), so it builds the cache
     // frames of those and the keyframes (the dense end solve runs on every rank); other slots stay empty

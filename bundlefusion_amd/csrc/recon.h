@@ -86,6 +86,10 @@ public:
         flushIntegrate();
         return *scene_;
     }
+    BFSceneCapacity sceneCapacity() { return scene().capacity(); }
+    // visualizeFrame's render after every frame's integration (bf_recon_set_render); nullptr stops
+    void setRender(const BFRayCastParams* rp);
+    void renderOutput(const float** depth, const float** depth4, const float** normals, const float** colors) const;
     const BFDepthCameraParams& camera() const { return cam_; }
     const std::vector<BFFixOp>& opLog() const { return log_; }
 
@@ -117,6 +121,13 @@ private:
     void apply(Pending& p);
     void runReintegrate();
     void logOp(int kind, uint32_t frame, const BFMat4* T);
+    // fail with BF_ERR_CAPACITY once the scene dropped a block (its sticky error bits): exact = read the device
+    // word (after a synchronization), else the copy the last GC kernel mirrored to the host
+    void checkScene(bool exact);
+    bool render_ = false;  // setRender
+    BFRayCastParams renderParams_{};
+    DevBuf<float> rDepth_;
+    DevBuf<float4> rDepth4_, rNormals_, rColors_;
 
     BFReconOptions opt_;
     BFDepthCameraParams cam_;
@@ -130,7 +141,7 @@ private:
     hipStream_t baStreamHi_ = nullptr, baStreamLo_ = nullptr, localStreamHi_ = nullptr, localStreamLo_ = nullptr;
     static constexpr uint32_t kHighPriorityMaxKeyframes = 1537;  // persistent grid <= ~3/4 of the CU slots
     bool baHigh_ = true, sharded_ = false;
-    int priorityPolicy_ = -1;  // -1: by solve size; 0 / 1: normal / high throughout (BF_BA_HIGH_PRIORITY)
+    int priorityPolicy_ = -1;  // -1: by solve size; 0 / 1: normal / high throughout (BFReconOptions.bundlingPriority)
     void switchBundlingPriority(uint32_t nk);
     std::unique_ptr<Scene> scene_;
     std::unique_ptr<Solver> local_, global_;
@@ -248,6 +259,9 @@ private:
     static constexpr uint32_t kPreSlots = 4;
     hipEvent_t preEv_[kPreSlots] = {nullptr, nullptr, nullptr, nullptr};
     bool prePending_[kPreSlots] = {false, false, false, false};  // recorded and not yet awaited by the scene stream
+    // the frame whose inputs preEv_[slot] marks (the cache store of that frame waits on it, whichever stream
+    // produced the inputs: the loop's preprocessor or a caller's, bf_recon_frame_ready)
+    uint32_t preFrame_[kPreSlots] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     void recordInputs(uint32_t f, hipStream_t s);
     void awaitPreproc(uint32_t f);               // the scene stream after frame f's preprocessing
     void storeCacheFrame(uint32_t f);

@@ -31,6 +31,7 @@ enum Ctrl {
     C_CAND = 2,        // alloc candidates emitted
     C_OVF = 3,         // candidates whose bucket was full (collision-list path)
     C_HIGHWATER = 4,   // 1 + highest heap block index ever handed out
+    C_CANDPEAK = 5,    // largest alloc candidate count of one integrate / batch since the reset (may exceed the capacity)
     C_GC_LIST = 6,     // GC victims that touch a collision list (serial path)
     C_ERR = 7,         // error bits (1: candidate buffer overflow, 2: heap exhausted, 4: dedup set full)
     C_BAND = 8,        // blocks of the visible list that may hold a voxel inside the truncation band
@@ -46,8 +47,16 @@ struct SceneConfig {
     uint32_t shardCount;     // >1: spatial ownership sharding across GPUs
     uint32_t shardIndex;
     float shardChunk;        // ownership chunk edge in metres (default 1 m, the streaming chunk)
-    uint32_t allocForceDirect = 0;  // test switch (BF_ALLOC_FORCE_DIRECT): every walking tile also takes the alloc walk's congested path
+    uint32_t allocForceDirect = 0;  // test switch (BF_SCENE_TEST_ALLOC_DIRECT): every walking tile also takes the alloc walk's congested path
+    uint32_t applyXcdRun = 0;       // voxel pass: work-list positions per XCD run (0: 64)
+    uint32_t applyRounds = 0;       // voxel pass: rounds of resident workgroups (0: kApplyRounds)
+    uint32_t splatRowCap = 0;       // test switch: ray-interval splat row-list capacity (0: 4 per heap block)
 };
+}  // namespace bf
+struct BFSceneOptions;  // include/bf/bf.h
+namespace bf {
+// the scene configuration of a BFSceneOptions (NULL: defaults)
+SceneConfig scene_config(const BFHashParams& hp, const BFSceneOptions* so);
 
 // One voxel op of a batch: integrate (deint = false) or de-integrate one frame at pose T (camera ->
 // world); depth / color are device pointers (float / uchar4 per pixel).
@@ -99,6 +108,12 @@ public:
     uint32_t heapFreeCount();
     uint32_t numVisible();
     uint32_t errorFlags();
+    // capacity state (BFSceneCapacity): sticky error bits, peak candidates against the capacity, heap; synchronizes
+    BFSceneCapacity capacity();
+    // the error bits as of the last garbageCollect, mirrored by k_gc into pinned host memory (no synchronization;
+    // enableErrorMirror first): the loop checks them once per frame without waiting for the scene stream
+    void enableErrorMirror();
+    uint32_t mirroredErrorFlags() const { return errMirror_ ? __atomic_load_n(errMirror_, __ATOMIC_ACQUIRE) : 0u; }
     BFTsdfStats stats();
     void resetStats();
     void exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
@@ -165,6 +180,7 @@ private:
     DevBuf<unsigned long long> ovf_;
     DevBuf<unsigned long long> gcList_;
     DevBuf<uint32_t> blockCount_;
+    uint32_t* errMirror_ = nullptr;  // pinned host word written by k_gc (enableErrorMirror)
     uint32_t candSetMask_;
     int numCUs_;
     unsigned integrateGrid_[2] = {0, 0};
@@ -177,15 +193,12 @@ private:
     uint32_t batchEpoch_ = 0;
     KernelClock applyClock_;
     unsigned applyGrid_ = 0, compactifyGrid_ = 0;
-    int applyTpb_ = 64;       // k_apply_ops workgroup size (Scene::Scene; BF_APPLY_TPB=256: A/B)
-    int applyXcdShift_ = -1;  // log2 of the voxel pass's work-list run per XCD (-1: plain grid stride; Scene::Scene)
+    int applyXcdShift_ = 6;   // log2 of the voxel pass's work-list run per XCD (BFSceneOptions.applyXcdRun)
     DevBuf<uint32_t> splatMin_, splatMax_;  // ordered-int float targets of the interval splat
     size_t splatCap_ = 0;
     DevBuf<int4> splatQuads_;
     DevBuf<uint32_t> splatBin_, splatRowIdx_;  // the splat's tile-row lists (raycast.hip)
-    bool splatAtomic_ = false;   // BF_SPLAT_ATOMIC=1 (A/B): one global atomic min / max per covered pixel
-    uint32_t splatRowCap_ = 0;   // BF_SPLAT_ROW_CAP (test switch): row-list capacity (0: 4 per visible block)
-    DevBuf<unsigned long long> waveLog_, tileLog_;  // BF_RENDER_WAVE_LOG / BF_SPLAT_TILE_LOG diagnostics (raycast.hip)  // per visible block: covered pixel rectangle + encoded depths (k_splat_quads)
+    DevBuf<unsigned long long> waveLog_, tileLog_;  // diagnostics build (BF_RENDER_DIAG): per-wave / per-tile clocks (raycast.hip)
 };
 
 }  // namespace bf

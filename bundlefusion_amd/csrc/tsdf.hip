@@ -14,6 +14,7 @@
 //  * GC reads a per-block count of voxels with (uint)weight != 0, maintained by the
 //    integrate kernel, instead of re-reading 512 voxels per block.
 #include "tsdf.h"
+#include "../../include/bf/bf.h"
 #include "hash_dev.h"
 
 #include <hip/hip_ext.h>
@@ -423,71 +424,6 @@ __device__ __forceinline__ uint32_t block_may_update_halves(const HashArgs& A, c
     return bits;
 }
 
-// block_may_update for the four z-quarters of the block (bit q: voxel z 2q, 2q + 1; BF_APPLY_QMASK): the
-// screen footprint and its depth bounds are the whole block's as in the halves form; a voxel level's
-// camera depth is affine in z, so each quarter's depth range is the corner depths' range at z = 0 shifted
-// by its two levels' offsets (conservative by the slack: the rounding of the shift is far below it).
-__device__ uint32_t block_may_update_quarters(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx,
-                                              int by, int bz, const float2* __restrict__ tiles,
-                                              const float2* __restrict__ tiles2) {
-    const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
-    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
-    float zb0 = INFINITY, zb1 = -INFINITY;  // camera depth of the z = 0 level's 4 corners
-    float xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
-        const f3 p = xform(Tinv, w);
-        if (!(p.z > 1e-3f)) return 15u;  // straddles the camera plane: keep
-        const float rz = __builtin_amdgcn_rcpf(p.z);
-        const float sx = p.x * cam.fx * rz + cam.mx, sy = p.y * cam.fy * rz + cam.my;
-        if (!(k & 4)) { zb0 = fminf(zb0, p.z); zb1 = fmaxf(zb1, p.z); }
-        xlo = fminf(xlo, sx); xhi = fmaxf(xhi, sx);
-        ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
-    }
-    const float dz = Tinv.m[10] * A.voxelSize;  // depth change per voxel level
-    const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
-    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
-    if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) return 0u;
-    const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
-    const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
-    const int tx0 = x0 / DEPTH_TILE, tx1 = x1 / DEPTH_TILE, ty0 = y0 / DEPTH_TILE, ty1 = y1 / DEPTH_TILE;
-    float dlo = INFINITY, dhi = -INFINITY;
-    if (tx1 - tx0 <= 2 && ty1 - ty0 <= 2) {
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-#pragma unroll
-            for (int i = 0; i < 3; i++) {
-                const float2 t = tiles[min(ty0 + j, ty1) * A.tilesW + min(tx0 + i, tx1)];
-                dlo = fminf(dlo, t.x);
-                dhi = fmaxf(dhi, t.y);
-            }
-    } else {
-        const int cx0 = x0 / DEPTH_TILE2, cx1 = x1 / DEPTH_TILE2, cy0 = y0 / DEPTH_TILE2, cy1 = y1 / DEPTH_TILE2;
-        if (cx1 - cx0 > 2 || cy1 - cy0 > 2) return 15u;  // very close block: keep
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-#pragma unroll
-            for (int i = 0; i < 3; i++) {
-                const float2 t = tiles2[min(cy0 + j, cy1) * A.tiles2W + min(cx0 + i, cx1)];
-                dlo = fminf(dlo, t.x);
-                dhi = fmaxf(dhi, t.y);
-            }
-    }
-    if (!(dlo <= dhi)) return 0u;
-    const float slack = 0.001f;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const float a = dz * (float)(2 * q), b = dz * (float)(2 * q + 1);
-        const float zlo = zb0 + fminf(a, b), zhi = zb1 + fmaxf(a, b);
-        if (!(dlo * (1.0f - A.truncScale) >= zhi + A.truncation + slack) &&
-            !(dhi * (1.0f + A.truncScale) <= zlo - A.truncation - slack))
-            bits |= 1u << q;
-    }
-    return bits;
-}
-
 // isSDFBlockInCameraFrustumApprox (VoxelUtilHashSDF.h:322-326, DepthCameraUtil.h:95-107) with the
 // five IEEE divisions replaced by rcp products. The test is a set of comparisons of monotone
 // quotients against +-1 / 0 / 1, so the fast result is taken when every compared value is farther
@@ -853,6 +789,7 @@ __global__ __launch_bounds__(256) void k_alloc_insert(HashArgs A, const unsigned
     if (s_last && threadIdx.x == 0) {
         __threadfence();
         A.ctrl[C_TICKET] = 0;
+        A.ctrl[C_CANDPEAK] = max(A.ctrl[C_CANDPEAK], A.ctrl[C_CAND]);  // candidate demand, against candCap
         if (A.ctrl[C_OVF]) alloc_overflow_serial(A, ovf);
     }
 }
@@ -1313,18 +1250,9 @@ constexpr int kApplyRounds = 4;
 #ifndef BF_APPLY_WPE
 #define BF_APPLY_WPE 8
 #endif
-// work-list op masks per z-quarter of a block (two voxel slices) instead of per z-half: the voxel pass
-// then skips an op's slice pair that the band cull rules out (1: uint4 masks, 0: uint2)
-#ifndef BF_APPLY_QMASK
-#define BF_APPLY_QMASK 0
-#endif
-#if BF_APPLY_QMASK
-typedef uint4 OpMask;
-constexpr int MASK_PARTS = 4;
-#else
+// work-list op mask of a block: which ops may update each z-half (x: voxel z 0..3, y: 4..7)
 typedef uint2 OpMask;
 constexpr int MASK_PARTS = 2;
-#endif
 __device__ __forceinline__ uint32_t dc_depth_word(float d, float maxDist) {
     return (d != -INFINITY && d < maxDist) ? (__float_as_uint(d) ^ DC_DEPTH_KEY) : 0u;
 }
@@ -1367,15 +1295,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
 // list garbageCollect walks), work list = blocks some op may update, with the op bit mask. Also
 // releases the batch's alloc dedup-set slots.
-#ifndef BF_COMPACTIFY_WPE  // A/B builds: waves per SIMD asked of the compiler for the batch scan (0: its choice, 4)
-#define BF_COMPACTIFY_WPE 0
-#endif
-#if BF_COMPACTIFY_WPE
-#define BF_COMPACTIFY_ATTR __attribute__((amdgpu_waves_per_eu(BF_COMPACTIFY_WPE)))
-#else
-#define BF_COMPACTIFY_ATTR
-#endif
-__global__ __launch_bounds__(256) BF_COMPACTIFY_ATTR void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
+__global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
                                                         OpMask* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
                                                         uint32_t binCap) {
@@ -1440,9 +1360,7 @@ __global__ __launch_bounds__(256) BF_COMPACTIFY_ATTR void k_compactify_ops(HashA
             const int4 b = s_bp[src];
             const BFMat4 Ti = op_mat(s_tinv[k]);
             // the voxel pass applies an op to a block half by half (4 z-slices per round)
-#if BF_APPLY_QMASK
-            const uint32_t hb = block_may_update_quarters(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
-#elif defined(BF_CULL_DIAG_NOBAND)  // timing diagnostic only (wrong masks): the scan without the band cull
+#if defined(BF_CULL_DIAG_NOBAND)  // timing diagnostic only (wrong masks): the scan without the band cull
             const uint32_t hb = 3u;
             (void)Ti; (void)b;
 #else
@@ -1453,18 +1371,10 @@ __global__ __launch_bounds__(256) BF_COMPACTIFY_ATTR void k_compactify_ops(HashA
                 if ((hb >> q) & 1u) atomicOr(&s_mask[q][src], 1u << k);
         }
         __syncthreads();
-#if BF_APPLY_QMASK
-        const OpMask hm = make_uint4(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x], s_mask[2][threadIdx.x], s_mask[3][threadIdx.x]);
-        const uint32_t mask = hm.x | hm.y | hm.z | hm.w;
-        // op-quarters to apply; in half units (an op over a half costs about one unit either way)
-        const uint32_t cost = (uint32_t)(__popc(hm.x | hm.y) + __popc(hm.z | hm.w));
-        const uint32_t evq = (uint32_t)(__popc(hm.x) + __popc(hm.y) + __popc(hm.z) + __popc(hm.w));
-#else
         const OpMask hm = make_uint2(s_mask[0][threadIdx.x], s_mask[1][threadIdx.x]);
         const uint32_t mask = hm.x | hm.y;
         const uint32_t cost = (uint32_t)(__popc(hm.x) + __popc(hm.y));  // op-halves to apply
         const uint32_t evq = 2u * cost;
-#endif
         const bool inb = mask != 0;
         // work list: one bin per cost (op-halves, two per bin), so the voxel pass can hand out the
         // costliest blocks first (entry order inside a bin is free: every block is applied by one wave)
@@ -1642,23 +1552,24 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
 // the same pixels, so its gathers follow each other and hit the lines the previous slice fetched (the
 // z-round-outer order re-fetched every op's footprint once per round: 888 -> 856 us per launch at the
 // bench workload); the op's pose and the (x, y) part of its projection are taken once per ZR slices.
-// ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us).
-// The kernel sits at neither roof: 0.42 of the VALU issue peak and 0.34 of HBM by the counters at the bench
-// workload, with the waves' cycles 25 % issuing, 44 % waiting to issue (dependencies) and 31 % waiting on
-// memory (profiles/r9g_apply_sq_pmc.txt): it is dependency / latency bound. Lane-derived values are re-read
-// per block instead of kept live (no spills), counters are scalar.
-template <int ZR, int ZC, int WPE, bool XCDRUNS = false, int TPB = 256>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
+// ZR = 4, ZC = 4 at 8 waves per SIMD (64 VGPRs; measured: ZR 4 / ZC 2 847 us, 7 waves 901 us). One wave
+// per workgroup (a slot is handed on as soon as its wave ends). The kernel sits at neither roof: ~0.5 of the
+// VALU issue peak and 0.36 of HBM by the counters at the driver workload (458-461 us per launch), with the
+// waves' cycles 22 % issuing, 45.5 % waiting to issue (dependencies) and 32.5 % waiting on memory
+// (profiles/r10_apply_sq_pmc.txt): it is dependency / latency bound. Lane-derived values are re-read per
+// block instead of kept live (no spills), counters are scalar.
+template <int ZR, int ZC, int WPE, bool XCDRUNS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap, int xcdShift) {
     static_assert(ZR * 2 == BF_SDF_BLOCK_SIZE, "one op mask per z-half of the block");
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    // XCDRUNS (A/B, BF_APPLY_XCD_CHUNK): runs of 2^xcdShift consecutive work-list positions go to one XCD
-    // (workgroup i runs on XCD i mod 8), run j to XCD j mod 8; otherwise consecutive positions go to
-    // consecutive waves, i.e. every XCD's waves spread over the whole list
+    const uint32_t nwaves = gridDim.x;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x);
+    // XCDRUNS (BFSceneOptions.applyXcdRun): runs of 2^xcdShift consecutive work-list positions go to one XCD
+    // (workgroup i runs on XCD i mod 8), run j to XCD j mod 8; otherwise (a grid that is not a multiple of 8)
+    // consecutive positions go to consecutive waves, i.e. every XCD's waves spread over the whole list
     uint32_t v0 = wave, vstep = nwaves, xcd = 0, cmask = 0;
     if constexpr (XCDRUNS) {
-        v0 = (uint32_t)__builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        v0 = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x >> 3);
         vstep = nwaves >> 3;
         xcd = blockIdx.x & 7u;
         cmask = (1u << xcdShift) - 1u;
@@ -1679,13 +1590,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t lane = lane_id_here();
         const int lx = lane & 7, ly = lane >> 3;
         const OpMask mh = masks[b];
-#if BF_APPLY_QMASK
-        const uint32_t maskQ[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(mh.x), (uint32_t)__builtin_amdgcn_readfirstlane(mh.y),
-                                   (uint32_t)__builtin_amdgcn_readfirstlane(mh.z), (uint32_t)__builtin_amdgcn_readfirstlane(mh.w)};
-        const uint32_t maskH[2] = {maskQ[0] | maskQ[1], maskQ[2] | maskQ[3]};
-#else
         const uint32_t maskH[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(mh.x), (uint32_t)__builtin_amdgcn_readfirstlane(mh.y)};
-#endif
         const int bx = e.x * BF_SDF_BLOCK_SIZE + lx, by = e.y * BF_SDF_BLOCK_SIZE + ly, bz = e.z * BF_SDF_BLOCK_SIZE;
         const float wx = (float)bx * A.voxelSize, wy = (float)by * A.voxelSize;
         Vox3* vp = reinterpret_cast<Vox3*>(A.voxels + (size_t)e.w * BF_VOXELS_PER_BLOCK) + lane;
@@ -1720,19 +1625,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav, diag);
                 diagPairs++;
                 diagEmpty += nupd == before;
-#elif BF_APPLY_QMASK
-                {   // the op's slice pairs in this half that the cull kept (wave-uniform)
-                    const bool deint = (ops.deintMask >> k) & 1u;
-                    const uint32_t sel = ((maskQ[h / 2] >> k) & 1u) | (((maskQ[h / 2 + 1] >> k) & 1u) << 1);
-#if BF_APPLY_QMASK == 2  // two pair bodies, each skipped on its own
-                    if (sel & 1u) apply_op_slices<2, 2, 0>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
-                    if (sel & 2u) apply_op_slices<2, 2, 2>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h + 2, rv + 2, touched, nupd, nwav);
-#else
-                    if (sel == 3u) apply_op_slices<ZR, ZC>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
-                    else if (sel == 1u) apply_op_slices<2, 2, 0>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
-                    else apply_op_slices<2, 2, 2>(deint, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h + 2, rv + 2, touched, nupd, nwav);
-#endif
-                }
 #else
                 apply_op_slices<ZR, ZC>((ops.deintMask >> k) & 1u, A, cam, Ti, bxy, dcRsrc, wc, epsc, bz + h, rv, touched, nupd, nwav);
 #endif
@@ -1760,9 +1652,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         rmw += nrmw;
 #endif
     }
-    // updated is the wave's total (scalar), rmw per lane
-    if constexpr (TPB == 64) {
-        // one wave per workgroup: its sums go straight to the workgroup's counter slot (no LDS stage, no barriers)
+    // updated is the wave's total (scalar), rmw per lane; one wave per workgroup: its sums go straight to the
+    // workgroup's counter slot (no LDS stage, no barriers)
+    {
         const unsigned long long rmwW = wave_sum_u64(rmw);
         if (lane_id_here() == 0) {
             unsigned long long* st = A.stats + (size_t)(blockIdx.x % STAT_SLOTS) * STAT_FIELDS;
@@ -1776,12 +1668,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             if (halves) atomicAdd(&st[S_BHALF], (unsigned long long)halves);
         }
-    } else {
-        flush_stats2(A.stats, S_VOXELS, lane_id_here() == 0 ? updated : 0u, S_RMW, rmw);
-        __syncthreads();
-        flush_stats2(A.stats, S_BUPD, lane_id_here() == 0 ? updated : 0u, S_BRMW, rmw);
-        __syncthreads();
-        flush_stats2(A.stats, S_BHALF, lane_id_here() == 0 ? halves : 0u, -1, 0);
     }
 #ifdef BF_APPLY_DIAG
     __syncthreads();
@@ -1805,7 +1691,7 @@ __device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV
 // so the identified sets equal the two-kernel form's. Every other victim touches a collision list and is
 // queued for the serial path, which the last workgroup to finish runs (release fence + ticket, acquire on
 // the winner: the identify / free / list kernels were three launches).
-__global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* listV) {
+__global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* listV, uint32_t* errMirror) {
     const uint32_t nvis = A.ctrl[C_VISIBLE];
     const uint32_t lane = lane_id();
     uint32_t freed = 0;
@@ -1864,6 +1750,8 @@ __global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* list
         __threadfence();
         A.ctrl[C_TICKET_GC] = 0;
         gc_free_list_serial(A, listV, s_locked);
+        // the scene's sticky error bits, as of this frame's batch, to the host without a synchronization
+        if (errMirror) __hip_atomic_store(errMirror, A.ctrl[C_ERR], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1975,8 +1863,27 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
     return a;
 }
 
+SceneConfig scene_config(const BFHashParams& hp, const BFSceneOptions* so) {
+    SceneConfig c{};
+    c.hp = hp;
+    if (so) {
+        c.candCapacity = so->candidateCapacity;
+        c.shardCount = so->shardCount;
+        c.shardIndex = so->shardIndex;
+        c.shardChunk = so->shardChunk;
+        c.applyXcdRun = so->applyXcdRun;
+        c.applyRounds = so->applyRounds;
+        c.allocForceDirect = (so->testFlags & BF_SCENE_TEST_ALLOC_DIRECT) ? 1u : 0u;
+        c.splatRowCap = so->splatRowCap;
+        BF_REQUIRE((so->testFlags & ~BF_SCENE_TEST_ALLOC_DIRECT) == 0, BF_ERR_ARG, "unknown BFSceneOptions.testFlags bits");
+        BF_REQUIRE(so->applyXcdRun == 0 || ((so->applyXcdRun & (so->applyXcdRun - 1)) == 0 && so->applyXcdRun <= 32768u),
+                   BF_ERR_ARG, "BFSceneOptions.applyXcdRun must be a power of two <= 32768");
+        BF_REQUIRE(so->applyRounds <= 64, BF_ERR_ARG, "BFSceneOptions.applyRounds > 64");
+    }
+    return c;
+}
+
 Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(stream) {
-    if (const char* e = std::getenv("BF_ALLOC_FORCE_DIRECT")) cfg_.allocForceDirect = std::atoi(e) != 0 ? 1u : 0u;
     BF_REQUIRE(cfg.hp.hashNumBuckets > 0 && cfg.hp.numSDFBlocks > 0, BF_ERR_ARG, "empty hash/heap");
     // HashEntry.ptr holds the heap block index inside the scene (voxel address = ptr * 512 in 64 bits):
     // the reference's int32 voxel index (ptr = block * 512, VoxelUtilHashSDF.h:60,609) stops at 2^22
@@ -2020,49 +1927,32 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     int occ0 = 0, occ1 = 0, occA = 0;
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, k_integrate<false, 4>, 256, 0));
     BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_integrate<true, 4>, 256, 0));
-    // ray-cast switches, read per scene so a test can set them (raycast.hip)
-    if (const char* e = std::getenv("BF_SPLAT_ATOMIC")) splatAtomic_ = std::atoi(e) == 1;
-    if (const char* e = std::getenv("BF_SPLAT_ROW_CAP")) splatRowCap_ = (uint32_t)std::max(1, std::atoi(e));
     // One-wave workgroups: a wave's slot is handed on when that wave ends instead of when the slowest of its
     // workgroup's four ends (the waves of a workgroup draw blocks of different cost, and the workgroup's end-of-
     // pass counter flush waited for all four): k_apply_ops 475-477 -> 466-467 us, 1 484-1 487 -> 1 498-1 499
     // frames/s at the bench workload, config 4's stream and the G = 8 rehearsal unchanged
-    // (profiles/r10_apply_tpb_ab.txt). BF_APPLY_TPB=256 (A/B): four-wave workgroups.
-    applyTpb_ = 64;
-    if (const char* e = std::getenv("BF_APPLY_TPB")) applyTpb_ = std::atoi(e) == 256 ? 256 : 64;
-    if (applyTpb_ == 64)
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true, 64>, 64, 0));
-    else
-        BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, 256, 0));
-    // sharded: one workgroup slot per CU stays free for the bundling streams' launches (Recon::Recon)
-    int freeSlots = cfg_.shardCount > 1 ? 1 : 0;
-    if (const char* e = std::getenv("BF_APPLY_FREE_SLOTS")) freeSlots = std::atoi(e);  // A/B measurements
-    freeSlots *= 256 / applyTpb_;  // in 256-thread workgroups' worth
-    // The grid is kApplyRounds rounds of resident workgroups, each wave a 1/kApplyRounds share of the strided
+    // (profiles/r10_apply_tpb_ab.txt).
+    BF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true>, 64, 0));
+    // sharded: one 256-thread workgroup's worth of slots per CU stays free for the bundling streams' launches
+    const int freeSlots = cfg_.shardCount > 1 ? 4 : 0;
+    // The grid is applyRounds (4) rounds of resident workgroups, each wave a 1/applyRounds share of the strided
     // list: the dispatcher hands the later rounds' workgroups to the slots the earlier ones free, so the waves
     // that drew costly blocks no longer set the pass's end (one resident round: 537 us per launch at the
     // bench workload; 2 / 4 / 8 rounds: 495 / 480 / 505 us, profiles/r10_apply_rounds_ab.txt), and other
-    // streams' kernels find free slots at every round's end instead of the pass's. BF_APPLY_GRID_MULT: A/B.
-    int mult = kApplyRounds;
-    if (const char* e = std::getenv("BF_APPLY_GRID_MULT")) mult = std::max(1, std::atoi(e));
-    applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_ * (unsigned)mult;
+    // streams' kernels find free slots at every round's end instead of the pass's.
+    const unsigned rounds = cfg_.applyRounds ? cfg_.applyRounds : (unsigned)kApplyRounds;
+    applyGrid_ = (unsigned)std::max(1, occA - freeSlots) * (unsigned)numCUs_ * rounds;
     // the voxel pass hands out runs of 64 consecutive work-list positions per XCD (k_apply_ops<..., true>): the
     // list is in heap order, so a run's blocks lie together and one XCD's L2 serves their depth / colour lines.
     // FETCH per launch at the driver workload: 1.14 GB with 4-position runs (consecutive waves: the plain grid
     // stride), 1.04 / 0.98 / 0.96 / 0.95 / 0.93 GB with 16 / 64 / 128 / 256 / 1024; time 478 µs up to 64, then
     // 480 / 485 / 516 µs as the coarser runs unbalance the XCDs (profiles/r10_apply_xcd_runs.txt).
-    // BF_APPLY_XCD_CHUNK (A/B): the run length (a power of two), 0 = the plain grid stride.
-    applyXcdShift_ = 6;
-    if (const char* e = std::getenv("BF_APPLY_XCD_CHUNK")) {
-        const int c = std::atoi(e);
-        applyXcdShift_ = -1;
-        for (int sh = 0; sh < 16; sh++)
-            if (c == (1 << sh)) applyXcdShift_ = sh;
-    }
-    // the batch scan: 4 workgroups per CU (its occupancy), BF_COMPACTIFY_GRID_MULT rounds of them (A/B)
-    int cmult = 1;
-    if (const char* e = std::getenv("BF_COMPACTIFY_GRID_MULT")) cmult = std::max(1, std::atoi(e));
-    compactifyGrid_ = (unsigned)numCUs_ * (BF_COMPACTIFY_WPE > 4 ? (unsigned)BF_COMPACTIFY_WPE : 4u) * (unsigned)cmult;
+    const uint32_t run = cfg_.applyXcdRun ? cfg_.applyXcdRun : 64u;
+    applyXcdShift_ = -1;
+    for (int sh = 0; sh < 16; sh++)
+        if (run == (1u << sh)) applyXcdShift_ = sh;
+    // the batch scan: 4 workgroups per CU (its occupancy; 5-6 per CU and 2-3 resident rounds measured no faster)
+    compactifyGrid_ = (unsigned)numCUs_ * 4u;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
@@ -2074,7 +1964,32 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     reset();
 }
 
-Scene::~Scene() {}
+Scene::~Scene() {
+    if (errMirror_) {
+        (void)hipStreamSynchronize(stream_);  // k_gc may still write it
+        (void)hipHostFree(errMirror_);
+    }
+}
+
+void Scene::enableErrorMirror() {
+    if (errMirror_) return;
+    BF_HIP(hipHostMalloc((void**)&errMirror_, sizeof(uint32_t), hipHostMallocCoherent));
+    *errMirror_ = 0;
+}
+
+BFSceneCapacity Scene::capacity() {
+    uint32_t c[C_COUNT];
+    BF_HIP(hipMemcpyAsync(c, ctrl_.p, sizeof(c), hipMemcpyDeviceToHost, stream_));
+    BF_HIP(hipStreamSynchronize(stream_));
+    BFSceneCapacity o{};
+    o.errorFlags = c[C_ERR];
+    o.peakCandidates = c[C_CANDPEAK];
+    o.candidateCapacity = cfg_.candCapacity;
+    o.heapFree = c[C_HEAP] + 1;
+    o.numSDFBlocks = B_;
+    o.highWater = c[C_HIGHWATER];
+    return o;
+}
 
 size_t Scene::deviceBytes() const {
     return hash_.bytes() + heap_.bytes() + voxels_.bytes() + blockPos_.bytes() + visible_.bytes() + band_.bytes() +
@@ -2260,18 +2175,12 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
     if (timed) applyClock_.slot(ev0, ev1);
-    if (applyTpb_ == 64 && applyXcdShift_ >= 0 && applyGrid_ % 8u == 0u)
-        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true, 64>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
+    if (applyGrid_ % 8u == 0u)  // workgroup i runs on XCD i mod 8
+        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
                               cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, applyXcdShift_);
-    else if (applyXcdShift_ >= 0 && applyGrid_ % 8u == 0u && applyTpb_ == 256)  // workgroup i runs on XCD i mod 8
-        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam,
-                              tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, applyXcdShift_);
-    else if (applyTpb_ == 64)
-        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, false, 64>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
-                              cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, -1);
     else
-        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE>, dim3(applyGrid_), dim3(256), 0, stream_, ev0, ev1, 0, A, cam, tab,
-                              reinterpret_cast<const OpMask*>(blockMask_.p), B_, -1);
+        hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, false>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
+                              cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), B_, -1);
     BF_LAUNCH_CHECK();
     if (timed) applyClock_.commit();
     T_ = ops[n - 1].T;
@@ -2281,7 +2190,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)
 void Scene::garbageCollect() {
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_gc<<<(unsigned)numCUs_ * 2, 256, 0, stream_>>>(A, gcList_.p);
+    k_gc<<<(unsigned)numCUs_ * 2, 256, 0, stream_>>>(A, gcList_.p, errMirror_);
     BF_LAUNCH_CHECK();
 }
 

@@ -126,10 +126,26 @@ class LoopbackComm:
     def __init__(self, h, rank: int, world: int):
         self.h, self.rank, self.world = h, rank, world
 
+    # streams one rank of a loop or FriedLiver app keeps busy (scene, bundling, local solve, result copies, input
+    # preprocessing, cache): each needs a hardware queue of its own, or a collective spinning in a queue another
+    # rank shares would hold that rank's arrival behind it (a 30-s stall, then the group's error)
+    STREAMS_PER_RANK = 6
+
     @staticmethod
     def group(world: int, timeout_ms: int = 30000) -> list["LoopbackComm"]:
+        """The ranks' collectives wait on the device for each other, so the process needs at least
+        world x STREAMS_PER_RANK hardware queues (GPU_MAX_HW_QUEUES, read by HIP at its initialisation: set it
+        before the first HIP call, as tests/conftest.py does); fails fast otherwise. A spinning collective also
+        holds one workgroup slot while it waits; another rank's persistent PCG grid that then cannot become
+        resident times out and is redone in stream order, so the loop stays correct."""
         import ctypes as C
+        import os
         from . import check, lib
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        need = world * LoopbackComm.STREAMS_PER_RANK
+        if world > 1 and queues < need:
+            raise RuntimeError(f"loopback group of {world} ranks needs GPU_MAX_HW_QUEUES >= {need} "
+                               f"(is {queues}); set it before HIP initialises")
         hs = (C.c_void_p * world)()
         check(lib().bf_comm_create_loopback(C.c_int(world), C.c_int(timeout_ms), hs))
         return [LoopbackComm(C.c_void_p(hs[r]), r, world) for r in range(world)]

@@ -235,6 +235,23 @@ class Recon:
         check(lib().bf_recon_scene_stats(self.h, C.byref(s)))
         return {k: getattr(s, k) for k, _ in BFTsdfStats._fields_}
 
+    def scene_capacity(self) -> dict:
+        """bf_recon_scene_capacity: the scene's error bits, peak alloc candidates against the capacity, heap."""
+        from .abi import BFSceneCapacity
+        c = BFSceneCapacity()
+        check(lib().bf_recon_scene_capacity(self.h, C.byref(c)))
+        return {k: getattr(c, k) for k, _ in BFSceneCapacity._fields_}
+
+    def set_render(self, rp) -> None:
+        """visualizeFrame's render after every frame's integration (bf_recon_set_render); None stops."""
+        check(lib().bf_recon_set_render(self.h, C.byref(rp) if rp is not None else None))
+
+    def render_output(self):
+        """The loop's last per-frame render: device pointers (depth, depth4, normals, colors)."""
+        p = [C.c_void_p() for _ in range(4)]
+        check(lib().bf_recon_render_output(self.h, *[C.byref(x) for x in p]))
+        return tuple(x.value for x in p)
+
     def heap_free_count(self) -> int:
         c = C.c_uint32()
         check(lib().bf_recon_heap_free_count(self.h, C.byref(c)))

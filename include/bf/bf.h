@@ -23,8 +23,12 @@
 extern "C" {
 #endif
 
-#define BF_ABI_VERSION 3  /* 2: BFSolverOptions.pcgSpinLimitUs, BFCorrOptions.minPerPair; 3: BFReconStats.globalPcgLaunches /
-                             globalPcgKernelMs, BFTsdfStats.batchHalves, BFRenderStats.waveSamples / waveSamplesMax / longWaves, BFAppTiming */
+#define BF_ABI_VERSION 4  /* 2: BFSolverOptions.pcgSpinLimitUs, BFCorrOptions.minPerPair; 3: BFReconStats.globalPcgLaunches /
+                             globalPcgKernelMs, BFTsdfStats.batchHalves, BFRenderStats.waveSamples / waveSamplesMax / longWaves, BFAppTiming;
+                             4: configuration through the ABI only (BFSceneOptions.applyXcdRun / applyRounds / testFlags /
+                             splatRowCap, BFReconOptions.bundlingPriority, bf_set_host_threads; no environment switches),
+                             BFSceneCapacity + bf_scene_capacity / bf_recon_scene_capacity (scene errors fail the loop),
+                             bf_recon_set_render (visualizeFrame's render per frame) */
 
 /* ---- runtime ------------------------------------------------------------- */
 int bf_abi_version(void);
@@ -34,6 +38,9 @@ const char* bf_last_error(void);
 int bf_device_count(int* count);
 int bf_set_device(int device);
 int bf_device_synchronize(void);
+/* threads of the host pool the loop uses for its per-submap loops over every frame, counting the calling thread
+ * (default 4; results do not depend on it); takes effect before the pool's first use */
+int bf_set_host_threads(int n);
 /* device memory helpers (so hosts need no HIP headers) */
 int bf_malloc(void** dptr, size_t bytes);
 int bf_free(void* dptr);
@@ -56,7 +63,13 @@ typedef struct BFSceneOptions {
     uint32_t shardCount;        /* multi-GPU spatial ownership: number of shards (0/1 = off) */
     uint32_t shardIndex;        /* this handle's shard */
     float shardChunk;           /* ownership chunk edge in metres (0 = 1.0) */
+    /* v4: the voxel pass's scheduling (environment switches up to v3); 0 = the measured defaults */
+    uint32_t applyXcdRun;       /* work-list positions handed to one XCD per run, a power of two (0 = 64) */
+    uint32_t applyRounds;       /* grid of the voxel pass in rounds of resident workgroups (0 = 4) */
+    uint32_t testFlags;         /* test switches (0 in production): BF_SCENE_TEST_ALLOC_DIRECT */
+    uint32_t splatRowCap;       /* test switch: capacity of the ray-interval splat's row lists (0 = 4 per heap block) */
 } BFSceneOptions;
+#define BF_SCENE_TEST_ALLOC_DIRECT 1u  /* every walking alloc tile also takes the walk's congested path */
 
 /* ctor + reset (CUDASceneRepHashSDF.h:32-34, :147-155 -> resetCUDA, CUDASceneRepHashSDF.cu:67) */
 int bf_scene_create(const BFHashParams* params, const BFSceneOptions* opts, bf_scene** out);
@@ -102,6 +115,9 @@ int bf_scene_heap_free_count(bf_scene* s, uint32_t* count);
 int bf_scene_num_visible(bf_scene* s, uint32_t* count);
 /* error bits: 1 candidate buffer overflow, 2 heap exhausted, 4 dedup set congested */
 int bf_scene_error_flags(bf_scene* s, uint32_t* flags);
+/* capacity state (types.h BFSceneCapacity): the sticky error bits, the peak alloc candidates of one call against
+ * candidateCapacity, heap free count and high water — synchronizes */
+int bf_scene_capacity(bf_scene* s, BFSceneCapacity* out);
 int bf_scene_get_stats(bf_scene* s, BFTsdfStats* out);
 int bf_scene_reset_stats(bf_scene* s);
 /* debugHash-style dump to HOST memory (CUDASceneRepHashSDF.h:179-314): any pointer may be NULL.
@@ -322,6 +338,10 @@ typedef struct BFReconOptions {
                                     L > 0 = they are applied exactly L frames after the submap was issued
                                     (waiting for them if needed), so the run's op sequence is repeatable;
                                     L <= 8 * submapSize (the result ring), else BF_ERR_ARG */
+    int32_t bundlingPriority;    /* v4. queue priority of the bundling streams: 0 normal, as the scene stream (default:
+                                    the voxel pass runs in resident rounds, so a bundling launch finds slots within a
+                                    round); 1 the highest; 2 keyed on the solve being issued (highest up to 1 537
+                                    keyframes or when sharded, normal above: the round-4 policy) */
 } BFReconOptions;
 
 typedef struct BFReconStats {
@@ -347,6 +367,7 @@ typedef struct BFReconStats {
     double hostWaitMs;           /* ... of it blocked on bundling results (resultLag, a full ring) */
     uint64_t globalPcgLaunches;  /* timed persistent PCG launches of the global solves (one per GN step) */
     double globalPcgKernelMs;    /* their summed device time (dispatch-stamped events) */
+    uint64_t renders;            /* v4: per-frame renders (bf_recon_set_render) */
 } BFReconStats;
 
 typedef struct bf_recon bf_recon;
@@ -386,12 +407,27 @@ int bf_recon_stats(bf_recon* r, BFReconStats* out);
 int bf_recon_scene_stats(bf_recon* r, BFTsdfStats* out);
 int bf_recon_reset_stats(bf_recon* r);  /* zero loop + scene counters and the device clocks */
 int bf_recon_heap_free_count(bf_recon* r, uint32_t* count);
+/* bf_scene_capacity of the loop's scene (waits for the scene stream). The loop checks the scene's error bits
+ * itself: bf_recon_process_frame / _reintegrate fail with BF_ERR_CAPACITY once a frame's batch set one (seen
+ * one or two frames later: the bits reach the host through pinned memory written by the frame's GC kernel, no
+ * synchronization), and bf_recon_synchronize / _finish / _end_sequence check them exactly. */
+int bf_recon_scene_capacity(bf_recon* r, BFSceneCapacity* out);
 /* integrated camera->world transform per frame (HOST float[16*n], -inf rows when not integrated) */
 int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n);
 /* visualizeFrame's render (DepthSensing.cpp:790-793): bf_scene_raycast on the loop's scene with its
  * depth camera; device outputs as bf_scene_raycast */
 int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, float* depth, float* depth4, float* normals,
                      float* colors);
+/* visualizeFrame every frame (DepthSensing.cpp:766-850 -> :790-793): with rp set, each frame's re-integration
+ * batch (which integrates the previous frame) is followed on the scene stream by setLastRigidTransformAndCompactify
+ * + CUDARayCastSDF::render at the pose of the frame that batch integrated (the reference renders each frame right
+ * after integrating it), with the loop's depth camera, into loop-owned device images of rp->width x rp->height;
+ * rp = NULL stops. The render costs the frame loop what it costs the reference's (BFReconStats.renders counts
+ * them). bf_recon_render_output gives the images of the last render (device pointers; read them after
+ * bf_recon_synchronize): depth f32, depth4 / normals / colors float4, as bf_scene_raycast writes them. */
+int bf_recon_set_render(bf_recon* r, const BFRayCastParams* rp);
+int bf_recon_render_output(bf_recon* r, const float** depth, const float** depth4, const float** normals,
+                           const float** colors);
 /* StopScanningAndExtractIsoSurfaceMC (DepthSensing.cpp:335-365) on the loop's scene: waits for the
  * scene stream, then bf_scene_extract_mesh (tris: DEVICE BFMcTriangle[p->maxNumTriangles]) */
 int bf_recon_extract_mesh(bf_recon* r, const BFMarchingCubesParams* p, BFMcTriangle* tris, uint32_t* numTriangles,
@@ -430,7 +466,11 @@ int bf_recon_set_frame_source(bf_recon* r, uint32_t f, const float* depth, const
  * ordered after it by events, and the cache takes the raw sensor depth and colour as its source (as
  * copyToBundling hands them to the bundler). The preprocessor is borrowed and must outlive the loop; its
  * output size must be the integration size. The raw images must stay valid as long as the frame store's
- * (a raw colour image of the integration size is integrated from directly, without a copy). */
+ * (a raw colour image of the integration size is integrated from directly, without a copy).
+ * Look-ahead: bf_recon_process_frame(f) also queues frame f + 1's preprocessing when its raw images are
+ * registered by then, so the raw images of frame f + 1 must hold their data before bf_recon_process_frame(f)
+ * is called whenever bf_recon_set_frame_raw(f + 1) was called before it (register a frame's raw images only
+ * once they are filled, or fill them all up front). */
 typedef struct bf_preproc bf_preproc;
 int bf_recon_attach_preproc(bf_recon* r, bf_preproc* p);
 int bf_recon_set_frame_raw(bf_recon* r, uint32_t f, const uint16_t* depthU16, const uint8_t* rgbx);
@@ -545,7 +585,8 @@ int bf_corr_load(const char* path, BFEntryJ* corr, uint64_t cap, uint64_t* n);
  * fixed order (pair, then a fixed permutation of the grid). depth: DEVICE array of device pointers
  * (float, width x height, -inf invalid); transforms / transformsInv: DEVICE float4x4[...] camera ->
  * world and its inverse. out: DEVICE EntryJ[cap]; *n = matches written (<= cap), *total (may be NULL)
- * = matches found. Synchronizes. */
+ * = matches found. Runs on the null (legacy) stream, so it is ordered after the caller's work there and on
+ * blocking streams; synchronizes. */
 int bf_corr_from_depth(const float* const* depth, const float* transforms, const float* transformsInv, uint32_t curFrame,
                        uint32_t startFrame, const BFCorrOptions* o, BFEntryJ* out, uint32_t cap, uint32_t* n,
                        uint32_t* total);

@@ -193,6 +193,20 @@ typedef struct BFTsdfStats {
     uint64_t batchHalves;     /* block z-halves (256 voxels) a batch pass loaded: those some op's mask reaches */
 } BFTsdfStats;
 
+/* Capacity state of a scene (bf_scene_capacity / bf_recon_scene_capacity). The reference drops allocations
+ * silently when its heap runs out (VoxelUtilHashSDF.h:535-540); here every dropped block sets a sticky error
+ * bit, and the loop (bf_recon_*, bf_app_step) fails with BF_ERR_CAPACITY once one is set. */
+typedef struct BFSceneCapacity {
+    uint32_t errorFlags;         /* since the last reset: 1 alloc candidate buffer overflow, 2 heap exhausted,
+                                    4 candidate dedup set congested (each drops blocks that should exist) */
+    uint32_t peakCandidates;     /* largest alloc candidate count of one integrate / op batch since the reset
+                                    (it may exceed candidateCapacity: the excess is what bit 1 dropped) */
+    uint32_t candidateCapacity;  /* BFSceneOptions.candidateCapacity in effect */
+    uint32_t heapFree;           /* getHeapFreeCount */
+    uint32_t numSDFBlocks;       /* heap size */
+    uint32_t highWater;          /* 1 + highest heap block index ever handed out */
+} BFSceneCapacity;
+
 /* mLib SensorData v4 header (SensorDataReader.cpp:45-60 reads these fields) */
 typedef struct BFSensInfo {
     uint32_t version;              /* 4 */

@@ -11,7 +11,7 @@ from bundlefusion_amd import abi
 def test_library_exists_and_loads():
     assert os.path.exists(abi.LIB_PATH)
     L = bfa.lib()
-    assert L.bf_abi_version() == 3
+    assert L.bf_abi_version() == abi.ABI_VERSION == 4
 
 
 def test_every_declared_symbol_is_exported():
@@ -84,3 +84,36 @@ def test_solver_error_bits():
     text = open(abi.HEADER_PATH.replace("bf.h", "types.h")).read()
     for name, v in (("BF_SOLVE_ERR_PAIR_BOUND", 4), ("BF_SOLVE_ERR_PCG_TIMEOUT", 8), ("BF_SOLVE_PCG_RECOVERED", 16)):
         assert f"#define {name} {v}u" in text, name
+
+
+def test_configuration_is_in_the_abi_not_the_environment():
+    """ABI v4: every production switch is a BFSceneOptions / BFReconOptions / BFSolverOptions field or
+    bf_set_host_threads; the library reads no environment variable outside the diagnostics build
+    (-DBF_RENDER_DIAG: the ray caster's per-wave / per-tile clock logs)."""
+    import glob
+    import re
+    csrc = os.path.join(os.path.dirname(abi.LIB_PATH), "csrc")
+    for path in glob.glob(os.path.join(csrc, "*.*")):
+        text = open(path).read()
+        for m in re.finditer(r"getenv", text):
+            before = text[:m.start()]
+            # the call must sit inside an #ifdef BF_RENDER_DIAG ... #endif block
+            opened = before.rfind("#ifdef BF_RENDER_DIAG")
+            assert opened >= 0 and before.rfind("#endif") < opened, (path, text[max(0, m.start() - 80):m.end() + 40])
+    names = [n for n, _ in abi.BFSceneOptions._fields_]
+    assert names[4:] == ["applyXcdRun", "applyRounds", "testFlags", "splatRowCap"]
+    assert [n for n, _ in abi.BFReconOptions._fields_][-1] == "bundlingPriority"
+
+
+def test_option_checks_without_device():
+    """Invalid v4 options fail with BF_ERR_ARG before any device work."""
+    L = bfa.lib()
+    assert L.bf_set_host_threads(0) != 0 and L.bf_set_host_threads(257) != 0
+    p = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 10, num_blocks=1 << 10)
+    for field, value, msg in (("testFlags", 2, b"testFlags"), ("applyXcdRun", 48, b"applyXcdRun"),
+                              ("applyRounds", 65, b"applyRounds")):
+        so = abi.BFSceneOptions()
+        setattr(so, field, value)
+        h = C.c_void_p()
+        assert L.bf_scene_create(C.byref(p), C.byref(so), C.byref(h)) != 0
+        assert msg in L.bf_last_error()

@@ -121,6 +121,10 @@ def test_app_ran_the_whole_stream(run):
     assert e["queueDrained"] == 1 and e["denseSolve"] == 1 and e["globalSolves"] == 31
     assert res["valid"] == 1 and res["numValidTransforms"] == res["numTransforms"] == F
     assert open(os.path.join(run["dir"], "processed.txt")).readline().strip() == "valid = true"
+    # no block was dropped over the whole run (the loop would have failed with BF_ERR_CAPACITY), with headroom
+    cap = rc.scene_capacity()
+    assert cap["errorFlags"] == 0 and cap["peakCandidates"] < cap["candidateCapacity"] // 2, cap
+    print(f"scene capacity: {cap}")
     print(f"{s['integrations']} integrations, {s['deintegrations']} de-integrations, {s['globalSolves']} global solves "
           f"({s['globalGnIterations']} GN, {s['globalPcgIterations']} PCG iterations), {s['removedPairs']} pair removals; "
           f"end phase: {e['pastEndFrames']} frames, dense solve {e['denseSolveMs']:.1f} ms")

@@ -1,6 +1,6 @@
 """Host logic (CPU): the frame loop's host pool (bundlefusion_amd/csrc/host_pool.h), compiled on its own
 with g++: every index of [0, n) visited exactly once per parallel_for, for many consecutive dispatches
-of varying sizes (the pool's generation hand-off), from one and from two calling threads, at 1-8 threads."""
+of varying sizes (the pool's generation hand-off), from one and from two calling threads, at 1-8 threads (bf_set_host_threads)."""
 import os
 import subprocess
 
@@ -13,6 +13,7 @@ PROG = r"""
 #include "host_pool.h"
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 using namespace bf;
@@ -29,7 +30,8 @@ static int run(int seed) {
     }
     return 0;
 }
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1) HostPool::requested().store(std::atoi(argv[1]));  // bf_set_host_threads
     int r0 = 0, r1 = 0;
     std::thread t([&] { r1 = run(1); });
     r0 = run(0);
@@ -52,7 +54,6 @@ def exe(tmp_path_factory):
 
 @pytest.mark.parametrize("threads", ["1", "2", "4", "8"])
 def test_parallel_for_visits_every_index_once(exe, threads):
-    env = dict(os.environ, BF_HOST_THREADS=threads)
-    r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, threads], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == f"ok {threads} threads"

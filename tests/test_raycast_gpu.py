@@ -14,12 +14,12 @@ from tsdf_compare import Pair, render_frames
 pytestmark = pytest.mark.gpu
 
 
-def build(W=160, H=120, vs=0.01, frames=(0, 3, 6, 9), noise=1):
+def build(W=160, H=120, vs=0.01, frames=(0, 3, 6, 9), noise=1, **scene_opts):
     sc = bfa.synth_scene(0)
     f = 577.87 * W / 640.0
     cam = bfa.depth_camera(W, H, fx=f, fy=f)
     p = bfa.hash_params(voxel_size=vs, num_buckets=1 << 16, num_blocks=1 << 15)
-    pair = Pair(p, cam)
+    pair = Pair(p, cam, **scene_opts)
     for k, (T, d, c) in enumerate(render_frames(sc, cam, list(frames), noise_seed=noise)):
         pair.integrate(k, T, d, c)
     pair.gc()
@@ -92,15 +92,12 @@ def test_raycast_empty_and_outside():
     assert np.all(g[0] == -np.inf) and np.all(g[2] == -np.inf)
 
 
-@pytest.mark.parametrize("env", [{"BF_SPLAT_ATOMIC": "1"}, {"BF_SPLAT_ROW_CAP": "1"}, {}],
-                         ids=["atomic-splat", "row-lists-overflow", "row-lists"])
-def test_splat_paths_give_the_same_intervals(env, monkeypatch):
-    """The three forms of the interval splat agree with the oracle bit for bit: the global-atomic form, the
-    tile-row lists (the default), and the full scan a tile falls back to when the row lists overflow their
-    capacity (forced here with a capacity of one entry)."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    sc, cam, pair, f = build()
+@pytest.mark.parametrize("row_cap", [1, 0], ids=["row-lists-overflow", "row-lists"])
+def test_splat_paths_give_the_same_intervals(row_cap):
+    """Both forms of the tiled interval splat agree with the oracle bit for bit: the tile-row lists (the
+    default), and the full scan a tile falls back to when the row lists overflow their capacity (forced with a
+    capacity of one entry, BFSceneOptions.splatRowCap)."""
+    sc, cam, pair, f = build(splat_row_cap=row_cap)
     rp = bfa.raycast_params(cam.imageWidth, cam.imageHeight, fx=f, fy=f)
     T = bfa.synth_pose(5)
     g = pair.gpu.raycast(T, cam, rp, want_intervals=True)

@@ -111,3 +111,19 @@ def test_rank_loops_with_communicator_match_the_unsharded_loop(world, async_bund
         rc.close()
     for c in comms:
         c.close()
+
+
+def test_loopback_collective_a_rank_skips_fails_loudly():
+    """A collective that one rank never joins must not hand back sums: its wait ends at the group's timeout
+    and the call that synchronises it fails (bf_comm_allreduce_sum_f64 checks the group's error word after
+    the stream), as does every later collective of the group; the ranks that did join get no success either."""
+    comms = LoopbackComm.group(2, timeout_ms=300)
+    try:
+        d = bfa.DeviceArray.from_host(np.arange(8, dtype=np.float64))
+        with pytest.raises(bfa.BFError, match="did not reach a collective"):
+            comms[0].allreduce_sum_f64(d)  # rank 1 never arrives
+        with pytest.raises(bfa.BFError, match="did not reach a collective"):
+            comms[1].allreduce_sum_f64(d)  # the group stays failed
+    finally:
+        for c in comms:
+            c.close()

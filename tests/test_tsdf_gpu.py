@@ -238,16 +238,16 @@ def test_op_batch_parity(scene, shift):
     assert pair.gpu.errorFlags() == 0
 
 
-def test_op_batch_alloc_congested_path(scene, monkeypatch):
+def test_op_batch_alloc_congested_path(scene):
     """The alloc walk's congested-tile path (a tile whose keys overflow its LDS set and overflow list walks
     again and emits every block directly; never taken at the bench workloads) forced on for every tile
-    (BF_ALLOC_FORCE_DIRECT, read at scene creation): its candidates duplicate phase 2's, the global dedup
-    removes them, and the scene stays bit-exact with the oracle through single integrations and an op
+    (BFSceneOptions.testFlags = BF_SCENE_TEST_ALLOC_DIRECT): its candidates duplicate phase 2's, the global
+    dedup removes them, and the scene stays bit-exact with the oracle through single integrations and an op
     batch."""
-    monkeypatch.setenv("BF_ALLOC_FORCE_DIRECT", "1")
+    from bundlefusion_amd.abi import BF_SCENE_TEST_ALLOC_DIRECT
     cam = small_cam()
     p = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 17, num_blocks=1 << 16)
-    pair = Pair(p, cam)
+    pair = Pair(p, cam, test_flags=BF_SCENE_TEST_ALLOC_DIRECT)
     frames = render_frames(scene, cam, [0, 5, 10, 15])
     for k in range(3):
         T, d, c = frames[k]

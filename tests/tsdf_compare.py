@@ -63,9 +63,9 @@ def compare_states(params, gpu: bfa.SceneRepHashSDF, ora: OracleScene, check_vox
 class Pair:
     """HIP scene + oracle scene driven with identical operations."""
 
-    def __init__(self, params, cam):
+    def __init__(self, params, cam, **scene_opts):
         self.params, self.cam = params, cam
-        self.gpu = bfa.SceneRepHashSDF(params)
+        self.gpu = bfa.SceneRepHashSDF(params, **scene_opts)
         self.ora = OracleScene(params)
         self._dev = {}
 
