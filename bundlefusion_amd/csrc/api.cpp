@@ -880,6 +880,19 @@ int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, 
                           reinterpret_cast<float4*>(normals), reinterpret_cast<float4*>(colors), nullptr, nullptr);
     BF_CATCH
 }
+int bf_recon_capture_global_solve(bf_recon* r, uint32_t submap) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null argument");
+    r->r->captureGlobalSolve(submap);
+    BF_CATCH
+}
+int bf_recon_captured_global_solve(bf_recon* r, BFEntryJ* corrIn, BFEntryJ* corrOut, uint32_t cap, uint32_t* nCorr,
+                                   float* poseIn, float* poseOut, int32_t* valid, uint32_t capImages, uint32_t* nImages) {
+    BF_TRY
+    BF_REQUIRE(r, BF_ERR_ARG, "null argument");
+    r->r->capturedGlobalSolve(corrIn, corrOut, cap, nCorr, poseIn, poseOut, valid, capImages, nImages);
+    BF_CATCH
+}
 int bf_recon_set_render(bf_recon* r, const BFRayCastParams* rp) {
     BF_TRY
     BF_REQUIRE(r, BF_ERR_ARG, "null argument");

@@ -341,6 +341,38 @@ void Recon::checkScene(bool exact) {
                                      std::to_string(e) + "):" + why);
 }
 
+void Recon::captureGlobalSolve(uint32_t s) {
+    BF_REQUIRE(numFrames_ <= s * opt_.submapSize, BF_ERR_STATE, "capture a submap's global solve before it is issued");
+    const size_t K = opt_.maxKeyframes;
+    capCorrIn_.alloc(opt_.maxGlobalCorr);
+    capCorrOut_.alloc(opt_.maxGlobalCorr);
+    capPoseIn_.alloc(6 * K);
+    capPoseOut_.alloc(6 * K);
+    capValid_.alloc(K);
+    capSubmap_ = s;
+    capDone_ = false;
+}
+
+void Recon::capturedGlobalSolve(BFEntryJ* corrIn, BFEntryJ* corrOut, uint32_t cap, uint32_t* nCorr, float* poseIn,
+                                float* poseOut, int32_t* valid, uint32_t capImages, uint32_t* nImages) {
+    synchronize();
+    BF_REQUIRE(capDone_, BF_ERR_STATE, "the captured submap's global solve has not run");
+    const size_t K = opt_.maxKeyframes;
+    const uint32_t n = std::min(cap, capN_), k = std::min(capImages, capK_);
+    if (corrIn && n) BF_HIP(hipMemcpy(corrIn, capCorrIn_.p, sizeof(BFEntryJ) * n, hipMemcpyDeviceToHost));
+    if (corrOut && n) BF_HIP(hipMemcpy(corrOut, capCorrOut_.p, sizeof(BFEntryJ) * n, hipMemcpyDeviceToHost));
+    for (int which = 0; which < 2; which++) {  // [rot 3k | trans 3k] per output
+        float* dst = which ? poseOut : poseIn;
+        const float* src = which ? capPoseOut_.p : capPoseIn_.p;
+        if (!dst || !k) continue;
+        BF_HIP(hipMemcpy(dst, src, 12 * (size_t)k, hipMemcpyDeviceToHost));
+        BF_HIP(hipMemcpy(dst + 3 * (size_t)k, src + 3 * K, 12 * (size_t)k, hipMemcpyDeviceToHost));
+    }
+    if (valid && k) BF_HIP(hipMemcpy(valid, capValid_.p, 4 * (size_t)k, hipMemcpyDeviceToHost));
+    if (nCorr) *nCorr = capN_;
+    if (nImages) *nImages = capK_;
+}
+
 void Recon::setRender(const BFRayCastParams* rp) {
     render_ = rp != nullptr;
     if (!rp) return;
@@ -730,7 +762,24 @@ void Recon::issueSubmap(uint32_t s, uint32_t n, uint32_t S, uint32_t slot, bool 
         a.findMaxResidual = true;
         a.gate = gate;
         if (gv.pairBound) a.pairBound = gv.pairBound;
+        const bool capture = s == capSubmap_;
+        if (capture) {  // test hook: the solve's inputs, as it sees them (after invalidate_local)
+            const size_t K = opt_.maxKeyframes;
+            BF_HIP(hipMemcpyAsync(capCorrIn_.p, gv.corr, sizeof(BFEntryJ) * ncorr, hipMemcpyDeviceToDevice, baStream_));
+            BF_HIP(hipMemcpyAsync(capPoseIn_.p, dGlobalRot_.p, 12 * (size_t)nk, hipMemcpyDeviceToDevice, baStream_));
+            BF_HIP(hipMemcpyAsync(capPoseIn_.p + 3 * K, dGlobalTrans_.p, 12 * (size_t)nk, hipMemcpyDeviceToDevice, baStream_));
+            BF_HIP(hipMemcpyAsync(capValid_.p, dGlobalValid_.p, 4 * (size_t)nk, hipMemcpyDeviceToDevice, baStream_));
+        }
         global_->solve(a);
+        if (capture) {  // ... and its outcome, before the max-residual removal
+            const size_t K = opt_.maxKeyframes;
+            BF_HIP(hipMemcpyAsync(capCorrOut_.p, gv.corr, sizeof(BFEntryJ) * ncorr, hipMemcpyDeviceToDevice, baStream_));
+            BF_HIP(hipMemcpyAsync(capPoseOut_.p, dGlobalRot_.p, 12 * (size_t)nk, hipMemcpyDeviceToDevice, baStream_));
+            BF_HIP(hipMemcpyAsync(capPoseOut_.p + 3 * K, dGlobalTrans_.p, 12 * (size_t)nk, hipMemcpyDeviceToDevice, baStream_));
+            capN_ = ncorr;
+            capK_ = nk;
+            capDone_ = true;
+        }
         // removeMaxResidualCUDA with getMaxResidual's (0, <10) exemption, on the device
         global_->removeMaxResidualAsync(gv.corr, ncorr, dGlobalValid_.p, nk, opt_.maxResidualThresh);
         global_->resultAsync(P.ctrl + Solver::kResultWords);

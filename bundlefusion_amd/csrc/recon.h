@@ -87,6 +87,10 @@ public:
         return *scene_;
     }
     BFSceneCapacity sceneCapacity() { return scene().capacity(); }
+    // test hook (bf_recon_capture_global_solve): keep the inputs and the outcome of submap s's in-loop global solve
+    void captureGlobalSolve(uint32_t s);
+    void capturedGlobalSolve(BFEntryJ* corrIn, BFEntryJ* corrOut, uint32_t cap, uint32_t* nCorr, float* poseIn,
+                             float* poseOut, int32_t* valid, uint32_t capImages, uint32_t* nImages);
     // visualizeFrame's render after every frame's integration (bf_recon_set_render); nullptr stops
     void setRender(const BFRayCastParams* rp);
     void renderOutput(const float** depth, const float** depth4, const float** normals, const float** colors) const;
@@ -124,6 +128,12 @@ private:
     // fail with BF_ERR_CAPACITY once the scene dropped a block (its sticky error bits): exact = read the device
     // word (after a synchronization), else the copy the last GC kernel mirrored to the host
     void checkScene(bool exact);
+    uint32_t capSubmap_ = 0xFFFFFFFFu;  // captureGlobalSolve
+    bool capDone_ = false;
+    uint32_t capN_ = 0, capK_ = 0;
+    DevBuf<BFEntryJ> capCorrIn_, capCorrOut_;
+    DevBuf<float> capPoseIn_, capPoseOut_;  // [rot 3K | trans 3K]
+    DevBuf<int> capValid_;
     bool render_ = false;  // setRender
     BFRayCastParams renderParams_{};
     DevBuf<float> rDepth_;

@@ -150,6 +150,12 @@ class LoopbackComm:
         check(lib().bf_comm_create_loopback(C.c_int(world), C.c_int(timeout_ms), hs))
         return [LoopbackComm(C.c_void_p(hs[r]), r, world) for r in range(world)]
 
+    def allreduce_sum_f64(self, d_array) -> None:
+        """In-place sum over the group's ranks (bf_comm_allreduce_sum_f64; synchronizes, checks the group)."""
+        import ctypes as C
+        from . import check, lib
+        check(lib().bf_comm_allreduce_sum_f64(self.h, d_array.ptr, C.c_size_t(d_array.nbytes // 8)))
+
     def close(self):
         from . import lib
         if self.h:

@@ -8,7 +8,7 @@ import ctypes as C
 import numpy as np
 
 from . import check, lib
-from .abi import (BFEndSequenceOptions, BFEndSequenceResult, BFFixOp, BFQueueEvent, BFReconOptions, BFReconStats,
+from .abi import (ENTRYJ_DTYPE, BFEndSequenceOptions, BFEndSequenceResult, BFFixOp, BFQueueEvent, BFReconOptions, BFReconStats,
                   BFSolveResult, BFTsdfStats)
 
 FIX_DEINTEGRATE, FIX_INTEGRATE, FIX_REINTEGRATE, OP_GC = 1, 2, 3, 4
@@ -241,6 +241,25 @@ class Recon:
         c = BFSceneCapacity()
         check(lib().bf_recon_scene_capacity(self.h, C.byref(c)))
         return {k: getattr(c, k) for k, _ in BFSceneCapacity._fields_}
+
+    def capture_global_solve(self, submap: int) -> None:
+        """Test hook: keep the inputs / outcome of submap's in-loop global solve (bf_recon_capture_global_solve)."""
+        check(lib().bf_recon_capture_global_solve(self.h, C.c_uint32(submap)))
+
+    def captured_global_solve(self) -> dict:
+        """{corr_in, corr_out (EntryJ), rot_in, trans_in, rot_out, trans_out [k, 3], valid [k]} of the capture."""
+        n, k = C.c_uint32(), C.c_uint32()
+        check(lib().bf_recon_captured_global_solve(self.h, None, None, 0, C.byref(n), None, None, None, 0, C.byref(k)))
+        ci, co = np.zeros(n.value, ENTRYJ_DTYPE), np.zeros(n.value, ENTRYJ_DTYPE)
+        pi, po = np.zeros(6 * k.value, np.float32), np.zeros(6 * k.value, np.float32)
+        val = np.zeros(k.value, np.int32)
+        check(lib().bf_recon_captured_global_solve(self.h, ci.ctypes.data_as(C.c_void_p), co.ctypes.data_as(C.c_void_p),
+                                                   C.c_uint32(n.value), C.byref(n), pi.ctypes.data_as(C.c_void_p),
+                                                   po.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p),
+                                                   C.c_uint32(k.value), C.byref(k)))
+        K = k.value
+        return dict(corr_in=ci, corr_out=co, rot_in=pi[:3 * K].reshape(K, 3), trans_in=pi[3 * K:].reshape(K, 3),
+                    rot_out=po[:3 * K].reshape(K, 3), trans_out=po[3 * K:].reshape(K, 3), valid=val)
 
     def set_render(self, rp) -> None:
         """visualizeFrame's render after every frame's integration (bf_recon_set_render); None stops."""

@@ -418,6 +418,15 @@ int bf_recon_trajectory(bf_recon* r, float* T, uint32_t n);
  * depth camera; device outputs as bf_scene_raycast */
 int bf_recon_raycast(bf_recon* r, const float T[16], const BFRayCastParams* rp, float* depth, float* depth4, float* normals,
                      float* colors);
+/* Test hook: capture submap `submap`'s in-loop global solve (arm before that submap is issued). The loop
+ * copies, on the bundling stream, the solve's inputs as it sees them (the global EntryJ list prefix after
+ * invalidate_local, the keyframes' se(3) poses, the valid flags) and its outcome before the max-residual
+ * removal (poses, the list with the per-image cap's invalidations). bf_recon_captured_global_solve waits for
+ * it and copies to HOST: corrIn / corrOut EntryJ[min(cap, *nCorr)], poseIn / poseOut float[6 * k] as
+ * [rot 3k | trans 3k] with k = min(capImages, *nImages), valid int32[k]; any output may be NULL. */
+int bf_recon_capture_global_solve(bf_recon* r, uint32_t submap);
+int bf_recon_captured_global_solve(bf_recon* r, BFEntryJ* corrIn, BFEntryJ* corrOut, uint32_t cap, uint32_t* nCorr,
+                                   float* poseIn, float* poseOut, int32_t* valid, uint32_t capImages, uint32_t* nImages);
 /* visualizeFrame every frame (DepthSensing.cpp:766-850 -> :790-793): with rp set, each frame's re-integration
  * batch (which integrates the previous frame) is followed on the scene stream by setLastRigidTransformAndCompactify
  * + CUDARayCastSDF::render at the pose of the frame that batch integrated (the reference renders each frame right
