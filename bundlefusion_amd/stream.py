@@ -81,10 +81,9 @@ class SyntheticStream:
         t1 = time.perf_counter()
         self.cache = []
         self.cache_source = cache_source
+        self._cache_args = (width, height, f, f, self.cam.mx, self.cam.my, num_frames, cache_w, cache_h)
         if cache_source == "loop":
-            from .cache import CUDACache, cache_options
-            self.cache_store = CUDACache(cache_options(width, height, f, f, self.cam.mx, self.cam.my, num_frames,
-                                                       width=cache_w, height=cache_h))
+            self.cache_store = self.loop_cache()
             self.cache = [None] * num_frames
         elif cache_source == "frames":
             from .cache import CUDACache, cache_options
@@ -133,8 +132,15 @@ class SyntheticStream:
         self.global_prefix = np.searchsorted(mx, np.arange(self.K), side="right").astype(np.uint32)
         self.log(f"correspondences: {off} local, {len(g)} global in {time.perf_counter() - t2:.1f}s")
 
-    def attach(self, recon, frames=None):
-        """Register every frame, correspondence list and the initial pose with a Recon."""
+    def loop_cache(self):
+        """A fresh CUDACache for one more loop over this stream (cache_source "loop": each loop builds its own)."""
+        from .cache import CUDACache, cache_options
+        w, h, fx, fy, mx, my, n, cw, ch = self._cache_args
+        return CUDACache(cache_options(w, h, fx, fy, mx, my, n, width=cw, height=ch))
+
+    def attach(self, recon, frames=None, cache_store=None):
+        """Register every frame, correspondence list and the initial pose with a Recon (cache_store: the loop's own
+        cache for cache_source "loop", default the stream's)."""
         P4 = 4 * self.cam.imageWidth * self.cam.imageHeight
         for i in range(self.F if frames is None else frames):
             recon.set_frame(i, self.depth.ptr.value + P4 * i, self.color.ptr.value + P4 * i, self.cache[i], self.tinc[i])
@@ -151,7 +157,7 @@ class SyntheticStream:
                 recon.set_frame_raw(i, self.depth_u16.ptr.value + 2 * W * H * i, self.rgbx.ptr.value + 4 * W * H * i)
             recon.attach_preproc(self.preproc)
         if self.cache_source == "loop":  # storeFrame of every frame inside process_frame (the frame store is the source)
-            recon.attach_cache(self.cache_store)
+            recon.attach_cache(cache_store or self.cache_store)
 
 
 def write_synthetic_sens(path: str, num_frames: int, width: int = 640, height: int = 480, seed: int = 0,

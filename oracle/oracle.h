@@ -25,6 +25,8 @@ typedef struct ORScene ORScene;
 ORScene* or_scene_create(const BFHashParams* params);
 void or_scene_destroy(ORScene* s);
 void or_scene_reset(ORScene* s);
+/* multi-GPU TSDF shard: alloc keeps only the blocks whose chunk (edge `chunk` m) hashes onto `index` of `count` */
+void or_scene_set_shard(ORScene* s, uint32_t count, uint32_t index, float chunk);
 /* integrate (deintegrate=0) / de-integrate (deintegrate=1) one frame with camera->world T.
  * depth: float[W*H] metres (-inf invalid); color: uchar4[W*H] or NULL. */
 void or_scene_integrate(ORScene* s, const float T[16], const float* depth, const uint8_t* color,

@@ -34,6 +34,9 @@ struct Scene {
     m4 T, Tinv;
     BFDepthCameraParams cam;
     BFTsdfStats stats;
+    // multi-GPU TSDF shard (or_scene_set_shard): alloc keeps only the blocks whose chunk this shard owns
+    uint32_t shardCount = 1, shardIndex = 0;
+    float shardChunk = 1.0f;
 };
 
 m4 toM4(const float* p) { m4 m; std::memcpy(m.e, p, 64); return m; }
@@ -71,6 +74,18 @@ f3 virtualVoxelPosToWorld(const Scene& s, i3 p) {  // :308-310
 }
 f3 SDFBlockToWorld(const Scene& s, i3 b) {  // :313-315
     return virtualVoxelPosToWorld(s, {b.x * BF_SDF_BLOCK_SIZE, b.y * BF_SDF_BLOCK_SIZE, b.z * BF_SDF_BLOCK_SIZE});
+}
+// Multi-GPU spatial ownership (the build's sharding; no reference counterpart beyond the
+// d_bitMask hook of allocKernel, CUDASceneRepHashSDF.cu:227): the block's corner chunk, rounded as
+// worldToChunks (:136-150), hashed with computeHashPos onto the shard count.
+bool owned(const Scene& s, i3 b) {
+    if (s.shardCount <= 1) return true;
+    const f3 w = SDFBlockToWorld(s, b) / s.shardChunk;
+    const i3 c = {f2i(w.x + (float)sgn(w.x) * 0.5f), f2i(w.y + (float)sgn(w.y) * 0.5f), f2i(w.z + (float)sgn(w.z) * 0.5f)};
+    int32_t a = (int32_t)((uint32_t)c.x * 73856093u), bb = (int32_t)((uint32_t)c.y * 19349669u), cc = (int32_t)((uint32_t)c.z * 83492791u);
+    int res = (a ^ bb ^ cc) % (int)s.shardCount;
+    if (res < 0) res += (int)s.shardCount;
+    return (uint32_t)res == s.shardIndex;
 }
 i3 worldToSDFBlock(const Scene& s, f3 w) { return virtualVoxelPosToSDFBlock(worldToVirtualVoxelPos(s, w)); }
 
@@ -279,7 +294,7 @@ void allocPixelWalk(const Scene& s, const float* depth, uint32_t x, uint32_t y, 
     if (boundaryPos.z - rayMin.z == 0.0f) { tMax.z = PINF; tDelta.z = PINF; }
     // (the chunk-streaming bitmask test is disabled with streaming, zParametersDefault.txt:100)
     for (uint32_t iter = 0; iter < 1024; iter++) {
-        if (blockInFrustum(s, id)) out.push_back(id);
+        if (blockInFrustum(s, id) && owned(s, id)) out.push_back(id);
         if (tMax.x < tMax.y && tMax.x < tMax.z) {
             id.x = f2i((float)id.x + step.x);
             if (id.x == idBound.x) return;
@@ -458,6 +473,12 @@ ORScene* or_scene_create(const BFHashParams* params) {
 }
 
 void or_scene_destroy(ORScene* o) { delete o; }
+
+void or_scene_set_shard(ORScene* o, uint32_t count, uint32_t index, float chunk) {
+    o->s.shardCount = count ? count : 1;
+    o->s.shardIndex = index;
+    o->s.shardChunk = chunk > 0.0f ? chunk : 1.0f;
+}
 
 // CUDASceneRepHashSDF::reset (.h:147-155) -> resetCUDA (.cu:67-111)
 void or_scene_reset(ORScene* o) {

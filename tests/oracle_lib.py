@@ -115,9 +115,11 @@ def mc_tables():
 class OracleScene:
     """Serial CPU restatement of CUDASceneRepHashSDF (oracle/tsdf.cpp)."""
 
-    def __init__(self, params: abi.BFHashParams):
+    def __init__(self, params: abi.BFHashParams, shard=None):
         self.params = params
         self.h = lib().or_scene_create(C.byref(params))
+        if shard is not None:  # (count, index, chunk): a multi-GPU TSDF shard's ownership
+            lib().or_scene_set_shard(C.c_void_p(self.h), C.c_uint32(shard[0]), C.c_uint32(shard[1]), C.c_float(shard[2]))
 
     def __del__(self):
         if getattr(self, "h", None):

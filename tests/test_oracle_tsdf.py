@@ -261,3 +261,39 @@ def test_deintegrate_colour_shortcut_is_exact():
                 rcs += [np.nextafter(rcs[0], f32(np.inf)), np.nextafter(rcs[0], f32(0))]
             for rc in rcs:
                 np.testing.assert_array_equal(fast(w, rc), r0, err_msg=f"w={wi} rc={rc!r}")
+
+
+def test_oracle_shards_partition_the_scene():
+    """The oracle scene with a multi-GPU shard's ownership (or_scene_set_shard, the restatement the sharded
+    GPU window replays run on): each shard stores exactly the blocks whose 0.25 m chunk it owns
+    (dist.chunk_owner_array, the host mirror of tsdf.hip's owned()), the shards are disjoint, and their union
+    is the unsharded scene with bit-identical voxels."""
+    from bundlefusion_amd.dist import chunk_owner_array
+    scene = bfa.synth_scene(0)
+    cam = bfa.depth_camera(160, 120, fx=577.87 / 4, fy=577.87 / 4)
+    p = bfa.hash_params(voxel_size=0.01, num_buckets=1 << 15, num_blocks=1 << 14)
+    frames = []
+    for f in (0, 8):
+        T = bfa.synth_pose(f)
+        d, c = bfa.synth_render_host(scene, T, cam, 1, f)
+        frames.append((T, d, c))
+    full = OracleScene(p)
+    shards = [OracleScene(p, shard=(2, r, 0.25)) for r in range(2)]
+    for sc in [full] + shards:
+        for T, d, c in frames:
+            sc.integrate(T, d, c, cam)
+        sc.garbageCollect()
+    fh, _, _, fv = full.export()
+    fb = blocks_of(fh)
+    union = {}
+    for r, sc in enumerate(shards):
+        h, heap, hc, v = sc.export()
+        check_hash_invariants(p, h, heap, hc)
+        b = blocks_of(h)
+        assert b and not (set(b) & set(union))
+        assert np.all(chunk_owner_array(np.array(sorted(b)), 0.01, 2, chunk=0.25) == r)
+        for k, ptr in b.items():
+            union[k] = block_voxels(v, ptr)
+    assert set(union) == set(fb) and len(fb) > 200
+    for k, ptr in fb.items():
+        assert block_voxels(fv, ptr).tobytes() == union[k].tobytes(), k
