@@ -3135,6 +3135,12 @@ void Solver::solve(const SolveArgs& s) {
                     }
 #endif
                     if (s.nLin) {
+                        // ranks of a loopback group (one GPU) issue their persistent launches in rank order
+                        struct Turn {
+                            Comm* c;
+                            explicit Turn(Comm* x) : c(x) { if (c) c->orderedLaunchBegin(); }
+                            ~Turn() { if (c) c->orderedLaunchEnd(); }
+                        } turn(comm_ && comm_->size() > 1 ? comm_ : nullptr);
                         // persistent launches of every solver on this device run one at a time: two
                         // partly resident persistent grids could each wait on the other's workgroups
                         PersistGate& pg = persist_gate();

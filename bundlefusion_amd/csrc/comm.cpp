@@ -54,6 +54,13 @@ void Comm::checkError() const {
     BF_REQUIRE(async == ncclSuccess, BF_ERR_INTERNAL, std::string("RCCL communicator error: ") + ncclGetErrorString(async));
 }
 
+void Comm::orderedLaunchBegin() {
+    if (lb_) loopbackTurn(true);
+}
+void Comm::orderedLaunchEnd() {
+    if (lb_) loopbackTurn(false);
+}
+
 void Comm::broadcast(float* buf, size_t n, int root, hipStream_t stream) {
     if (n == 0) return;
     if (lb_) {

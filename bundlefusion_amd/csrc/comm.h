@@ -41,10 +41,18 @@ public:
     // one of them failed (loopback: a wait for a rank timed out, so its sums are not valid; RCCL: the
     // communicator's asynchronous error)
     void checkError() const;
+    // Loopback groups share one GPU: a persistent launch (k_pcg_persist, which needs nearly every CU and is
+    // serialized per device) of one rank must not be queued ahead of another rank's earlier one, or each waits
+    // on a collective the other can only reach after its own launch. The ranks' persistent launches are
+    // therefore issued in rank order per round: begin waits (host) for this rank's turn, end passes it on.
+    // No-ops for RCCL (one process per GPU).
+    void orderedLaunchBegin();
+    void orderedLaunchEnd();
 
 private:
     void loopbackCollective(void* buf, size_t n, size_t elemBytes, int kind, int root, hipStream_t stream);
     void loopbackCheck() const;
+    void loopbackTurn(bool begin);
     void* comm_ = nullptr;  // ncclComm_t
     std::shared_ptr<Loopback> lb_;
     int nranks_ = 1, rank_ = 0;

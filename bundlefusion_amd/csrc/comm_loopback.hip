@@ -13,8 +13,10 @@
 // Recon::synchronize); a group destroyed with the word set reports it on stderr.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <vector>
 
@@ -80,6 +82,9 @@ struct Loopback {
     DevBuf<uint32_t> arrive;      // arrivals ever, per parity
     uint32_t* err = nullptr;      // pinned host word: a wait ran out
     std::mutex mu;
+    std::condition_variable turnCv;            // ordered persistent launches (Comm::orderedLaunchBegin)
+    uint64_t turn = 0;                         // launches issued by the group so far
+    std::vector<uint64_t> launches;            // per rank
     std::vector<uint32_t> seq;                 // next collective of each rank
     std::vector<std::pair<uint32_t, size_t>> sizes;  // (collective, bytes) of recent collectives, by seq % 64
     ~Loopback() {
@@ -102,6 +107,7 @@ std::shared_ptr<Loopback> Comm::loopbackGroup(int nranks, int timeoutMs, size_t 
     BF_HIP(hipHostMalloc((void**)&g->err, sizeof(uint32_t), hipHostMallocCoherent));
     *g->err = 0;
     g->seq.assign((size_t)nranks, 0u);
+    g->launches.assign((size_t)nranks, 0u);
     g->sizes.assign(64, {0xFFFFFFFFu, 0});
     BF_HIP(hipDeviceSynchronize());
     return g;
@@ -115,6 +121,22 @@ void Comm::loopbackCheck() const {
     BF_REQUIRE(__atomic_load_n(lb_->err, __ATOMIC_ACQUIRE) == 0, BF_ERR_INTERNAL,
                "loopback communicator: a rank did not reach a collective in time "
                "(ranks issued different collective sequences)");
+}
+
+void Comm::loopbackTurn(bool begin) {
+    Loopback& g = *lb_;
+    std::unique_lock<std::mutex> lk(g.mu);
+    const uint64_t mine = g.launches[(size_t)rank_] * (uint64_t)nranks_ + (uint64_t)rank_;
+    if (begin) {
+        // bounded like the device-side waits: a rank that stopped issuing launches fails the others
+        const bool ok = g.turnCv.wait_for(lk, std::chrono::microseconds(g.ticks / 100ull), [&] { return g.turn == mine; });
+        BF_REQUIRE(ok, BF_ERR_INTERNAL, "loopback communicator: a rank did not reach its persistent launch in time");
+    } else {
+        g.launches[(size_t)rank_]++;
+        g.turn = mine + 1;
+        lk.unlock();
+        g.turnCv.notify_all();
+    }
 }
 
 void Comm::loopbackCollective(void* buf, size_t n, size_t elemBytes, int kind, int root, hipStream_t stream) {
