@@ -375,9 +375,11 @@ def sens_main(args):
     group.barrier()
     dt = group.max(dt)
     st = rc.stats()
+    cap = rc.scene_capacity()
     tm = app.timing()
     res = app.finish()
-    out = {"metric": f"frames/s FriedLiver pipeline on {os.path.basename(args.sens)}", "value": done / dt,
+    out = {"metric": f"frames/s FriedLiver pipeline on {os.path.basename(args.sens)}",
+           "value": done / dt if cap["errorFlags"] == 0 else None,
            "unit": "frames/s", "n_gpus": world, "steps": done, "warmup": 0, "ms_per_step": dt / max(1, done) * 1e3,
            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
            "data": f"{args.sens} (.sens input; EntryJ from the stand-in producer)",
@@ -405,6 +407,8 @@ def sens_main(args):
                    "scene_stream_busy": (st["reintegrateKernelMs"] + st["integrateKernelMs"]) / 1e3 / dt,
                    "apply_us_per_launch": st["reintegrateKernelMs"] * 1e3 / max(1, st["reintegrateLaunches"]),
                    "global_ms_per_gn_iter_in_loop": st["globalSolveMs"] / max(1, st["globalGnIterations"])},
+           "scene_capacity": {"error_flags": cap["errorFlags"], "peak_candidates": cap["peakCandidates"],
+                              "candidate_capacity": cap["candidateCapacity"], "heap_free": cap["heapFree"]},
            "end_phase_s": res["endSeconds"], "heap_free": res["heapFreeCount"],
            "valid_transforms": [res["numValidTransforms"], res["numTransforms"]], "mesh_triangles": res["meshTriangles"]}
     if rank == 0:

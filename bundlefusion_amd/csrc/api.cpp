@@ -671,10 +671,10 @@ int bf_comm_create(const uint8_t id[128], int nranks, int rank, bf_comm** out) {
     *out = h;
     BF_CATCH
 }
-int bf_comm_create_loopback(int nranks, int timeoutMs, bf_comm** out) {
+int bf_comm_create_loopback(int nranks, int timeoutMs, size_t capacityBytes, bf_comm** out) {
     BF_TRY
     BF_REQUIRE(out && nranks >= 1, BF_ERR_ARG, "null argument / nranks");
-    auto group = Comm::loopbackGroup(nranks, timeoutMs);
+    auto group = Comm::loopbackGroup(nranks, timeoutMs, capacityBytes);
     std::vector<bf_comm*> made;
     try {
         for (int r = 0; r < nranks; r++) {

@@ -132,7 +132,7 @@ class LoopbackComm:
     STREAMS_PER_RANK = 6
 
     @staticmethod
-    def group(world: int, timeout_ms: int = 30000) -> list["LoopbackComm"]:
+    def group(world: int, timeout_ms: int = 30000, capacity_bytes: int = 0) -> list["LoopbackComm"]:
         """The ranks' collectives wait on the device for each other, so the process needs at least
         world x STREAMS_PER_RANK hardware queues (GPU_MAX_HW_QUEUES, read by HIP at its initialisation: set it
         before the first HIP call, as tests/conftest.py does); fails fast otherwise. A spinning collective also
@@ -147,7 +147,7 @@ class LoopbackComm:
             raise RuntimeError(f"loopback group of {world} ranks needs GPU_MAX_HW_QUEUES >= {need} "
                                f"(is {queues}); set it before HIP initialises")
         hs = (C.c_void_p * world)()
-        check(lib().bf_comm_create_loopback(C.c_int(world), C.c_int(timeout_ms), hs))
+        check(lib().bf_comm_create_loopback(C.c_int(world), C.c_int(timeout_ms), C.c_size_t(capacity_bytes), hs))
         return [LoopbackComm(C.c_void_p(hs[r]), r, world) for r in range(world)]
 
     def allreduce_sum_f64(self, d_array) -> None:

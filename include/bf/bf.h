@@ -253,9 +253,10 @@ int bf_comm_destroy(bf_comm* c);
  * their own host threads in this process, sharing the current GPU. A collective is a one-workgroup kernel
  * enqueued on the caller's stream (as RCCL's are: asynchronous, stream-ordered, no host wait) that waits on
  * the device for every rank's contribution and sums in rank order; a rank that never arrives within
- * timeoutMs (0: 60 s) ends the wait and the next collective call fails. Lets the multi-rank loop run on one
- * GPU with RCCL's ordering semantics; RCCL is not involved. */
-int bf_comm_create_loopback(int nranks, int timeoutMs, bf_comm** out);
+ * timeoutMs (0: 60 s) ends the wait and the next collective call fails. capacityBytes: the largest collective
+ * (0: 16 MiB; the global solve's pair statistics are 224 B per image pair, 83 MB at config 4's 2 001 keyframes).
+ * Lets the multi-rank loop run on one GPU with RCCL's ordering semantics; RCCL is not involved. */
+int bf_comm_create_loopback(int nranks, int timeoutMs, size_t capacityBytes, bf_comm** out);
 /* in-place sum over ranks of n doubles (device pointer); synchronizes (tests) */
 int bf_comm_allreduce_sum_f64(bf_comm* c, double* d, size_t n);
 /* shard the solver's pairs: count shards, this is shard index; comm (count ranks) or NULL (no

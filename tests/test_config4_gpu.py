@@ -78,7 +78,7 @@ def run():
         rc = Recon(params, st.cam, opts, so)
         st.attach(rc, cache_store=caches[r])
         loops.append(rc)
-    comms = LoopbackComm.group(WORLD, timeout_ms=120000)
+    comms = LoopbackComm.group(WORLD, timeout_ms=120000, capacity_bytes=128 << 20)  # pair stats: 83 MB at K = 2 001
     for rc, c in zip(loops, comms):
         rc.set_comm(c)
     loops[0].capture_global_solve(CAP_SUBMAP)
