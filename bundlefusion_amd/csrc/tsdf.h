@@ -22,7 +22,6 @@
 #pragma once
 #include "bf_math.h"
 #include "bf_runtime.h"
-#include "scan_order.h"
 
 namespace bf {
 
@@ -115,9 +114,6 @@ public:
     // enableErrorMirror first): the loop checks them once per frame without waiting for the scene stream
     void enableErrorMirror();
     uint32_t mirroredErrorFlags() const { return errMirror_ ? __atomic_load_n(errMirror_, __ATOMIC_ACQUIRE) : 0u; }
-    // the batch scan's visiting order is re-sorted by space every kScanSortEvery batches (scan_order.h), over the
-    // heap slots below the high water the GC kernel last mirrored (needs enableErrorMirror)
-    static constexpr uint32_t kScanSortEvery = 16;
     BFTsdfStats stats();
     void resetStats();
     void exportState(BFHashEntry* hash, uint32_t* heap, uint32_t* heapCounter, BFVoxel* voxels);
@@ -184,9 +180,7 @@ private:
     DevBuf<unsigned long long> ovf_;
     DevBuf<unsigned long long> gcList_;
     DevBuf<uint32_t> blockCount_;
-    uint32_t* errMirror_ = nullptr;  // pinned host words written by k_gc (enableErrorMirror): {error bits, high water}
-    ScanOrder scanOrder_;
-    uint32_t batchesSinceSort_ = 0;
+    uint32_t* errMirror_ = nullptr;  // pinned host word written by k_gc (enableErrorMirror)
     uint32_t candSetMask_;
     int numCUs_;
     unsigned integrateGrid_[2] = {0, 0};

@@ -1325,7 +1325,7 @@ __device__ __forceinline__ bool box_may_touch_frustum(const float* __restrict__ 
 __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
                                                         OpMask* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
-                                                        uint32_t binCap, const uint32_t* __restrict__ order) {
+                                                        uint32_t binCap) {
     {
         const uint32_t n = min(A.ctrl[C_CAND], candCap);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1353,11 +1353,9 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
     const BFMat4 TinvLast = op_mat(ops.tinv[ops.n - 1]);
     unsigned long long scanned = 0, vis = 0, band = 0, evals = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < hw; base += gridDim.x * blockDim.x) {
-        // scan position -> heap slot (scan_order.h: a permutation of [0, hw), allocated blocks sorted by space)
-        const uint32_t j = base + threadIdx.x;
-        const uint32_t i = j < hw ? order[j] : j;
+        const uint32_t i = base + threadIdx.x;
         int4 bp = make_int4(0, 0, 0, 0);
-        if (j < hw) bp = A.blockPos[i];
+        if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
         // the wave's pre-cull: the box of its allocated blocks' centres against every op's frustum, one op per
         // lane; the per-block tests below run only for the ops the box may touch (heap neighbours were mostly
@@ -1803,10 +1801,7 @@ __global__ __launch_bounds__(256) void k_gc(HashArgs A, unsigned long long* list
         A.ctrl[C_TICKET_GC] = 0;
         gc_free_list_serial(A, listV, s_locked);
         // the scene's sticky error bits, as of this frame's batch, to the host without a synchronization
-        if (errMirror) {
-            __hip_atomic_store(errMirror, A.ctrl[C_ERR], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(errMirror + 1, A.ctrl[C_HIGHWATER], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (errMirror) __hip_atomic_store(errMirror, A.ctrl[C_ERR], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2013,7 +2008,6 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
     BF_HIP(hipMemsetAsync(stats_.p, 0, stats_.bytes(), stream_));
-    scanOrder_.init(B_, stream_);
     float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     std::memcpy(T_.m, I, 64);
     std::memcpy(Tinv_.m, I, 64);
@@ -2029,8 +2023,8 @@ Scene::~Scene() {
 
 void Scene::enableErrorMirror() {
     if (errMirror_) return;
-    BF_HIP(hipHostMalloc((void**)&errMirror_, 2 * sizeof(uint32_t), hipHostMallocCoherent));
-    errMirror_[0] = errMirror_[1] = 0;
+    BF_HIP(hipHostMalloc((void**)&errMirror_, sizeof(uint32_t), hipHostMallocCoherent));
+    *errMirror_ = 0;
 }
 
 BFSceneCapacity Scene::capacity() {
@@ -2052,7 +2046,7 @@ size_t Scene::deviceBytes() const {
            blockMask_.bytes() + blockBirth_.bytes() + candOp_.bytes() +
            tiles_.bytes() + tiles2_.bytes() + ctrl_.bytes() +
            stats_.bytes() + cand_.bytes() + candSet_.bytes() + candSlot_.bytes() + ovf_.bytes() +
-           gcList_.bytes() + blockCount_.bytes() + scanOrder_.deviceBytes();
+           gcList_.bytes() + blockCount_.bytes();
 }
 
 // CUDASceneRepHashSDF::reset (.h:147-155) -> resetCUDA (.cu:67-111)
@@ -2064,8 +2058,6 @@ void Scene::reset() {
     BF_LAUNCH_CHECK();
     BF_HIP(hipMemsetAsync(voxels_.p, 0, voxels_.bytes(), stream_));
     cfg_.hp.numOccupiedBlocks = 0;
-    if (scanOrder_.order()) scanOrder_.reset(stream_);  // (constructed after the first reset)
-    batchesSinceSort_ = 0;
 }
 
 void Scene::ensureTiles(size_t fine, size_t coarse) {
@@ -2227,19 +2219,8 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
     A.tilesH = th;
     A.tiles2 = tiles2_.p;
     A.tiles2W = tw2;
-    // the scan visits the blocks in a space-sorted order, re-sorted every kScanSortEvery batches over the slots below the
-    // high water the last GC mirrored (a lower bound of the current one: the order stays a permutation of [0, highWater))
-#ifdef BF_NO_SCAN_SORT  // A/B build: heap order
-    if (false) {
-#else
-    if (errMirror_ && ++batchesSinceSort_ >= kScanSortEvery) {
-#endif
-        batchesSinceSort_ = 0;
-        scanOrder_.sort(blockPos_.p, __atomic_load_n(errMirror_ + 1, __ATOMIC_ACQUIRE), stream_);
-    }
     k_compactify_ops<<<compactifyGrid_, 256, 0, stream_>>>(A, cam, tab, cfg_.candCapacity, candSlot_.p, candSet_.p,
-                                                                  reinterpret_cast<OpMask*>(blockMask_.p), blockBirth_.p, epoch, B_,
-                                                                  scanOrder_.order());
+                                                                  reinterpret_cast<OpMask*>(blockMask_.p), blockBirth_.p, epoch, B_);
     BF_LAUNCH_CHECK();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const bool timed = applyClock_.enabled();
