@@ -1292,33 +1292,6 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
                     maxDist, ops.tiles[k], ops.tiles2[k]);
 }
 
-// Pre-cull of the batch scan: may any block centre inside the world box [lo, hi] pass op k's frustum test
-// (isSDFBlockInCameraFrustumApprox, VoxelUtilHashSDF.h:322-326, DepthCameraUtil.h:95-107)? The test accepts
-// camera-space points with Z in [zmin, zmin + (zmax - zmin) / 0.95] whose pixel u = fx X / Z + mx lies in
-// (W - 1) / 2 (1 -+ 1 / 0.95) and likewise v: for Z > 0 six half-spaces, linear in the world point. The box is
-// rejected only when it lies beyond one of them by a margin (1 mm of X, Y or Z) far above the float error of
-// the exact test, so a rejected op never holds a block of the box: the op masks are unchanged.
-__device__ __forceinline__ bool box_may_touch_frustum(const float* __restrict__ Ti, const BFDepthCameraParams& c, f3 lo, f3 hi) {
-    const float wm1 = (float)c.imageWidth - 1.0f, hm1 = (float)c.imageHeight - 1.0f, inv = 1.0f / 0.95f;
-    const float u0 = 0.5f * wm1 * (1.0f - inv) - c.mx, u1 = 0.5f * wm1 * (1.0f + inv) - c.mx;
-    const float v0 = 0.5f * hm1 * (1.0f - inv) - c.my, v1 = 0.5f * hm1 * (1.0f + inv) - c.my;
-    const float zn = c.sensorDepthWorldMin, zf = zn + (c.sensorDepthWorldMax - zn) * inv;
-    // outside when a X + b Y + e Z + d > 0, (X, Y, Z) = Ti (world point)
-    const float P[6][4] = {{c.fx, 0.0f, -u1, 0.0f}, {-c.fx, 0.0f, u0, 0.0f}, {0.0f, c.fy, -v1, 0.0f},
-                           {0.0f, -c.fy, v0, 0.0f}, {0.0f, 0.0f, -1.0f, zn}, {0.0f, 0.0f, 1.0f, -zf}};
-    bool maybe = true;
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        const float a = P[q][0], b = P[q][1], e = P[q][2];
-        const float g0 = a * Ti[0] + b * Ti[4] + e * Ti[8], g1 = a * Ti[1] + b * Ti[5] + e * Ti[9];
-        const float g2 = a * Ti[2] + b * Ti[6] + e * Ti[10];
-        const float m = a * Ti[3] + b * Ti[7] + e * Ti[11] + P[q][3] + (g0 > 0.0f ? g0 * lo.x : g0 * hi.x) +
-                        (g1 > 0.0f ? g1 * lo.y : g1 * hi.y) + (g2 > 0.0f ? g2 * lo.z : g2 * hi.z);
-        if (m > 1e-3f * (fabsf(a) + fabsf(b) + fabsf(e))) maybe = false;
-    }
-    return maybe;
-}
-
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
 // list garbageCollect walks), work list = blocks some op may update, with the op bit mask. Also
 // releases the batch's alloc dedup-set slots.
@@ -1357,37 +1330,14 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         int4 bp = make_int4(0, 0, 0, 0);
         if (i < hw) bp = A.blockPos[i];
         const bool alloc = bp.w != 0;
-        // the wave's pre-cull: the box of its allocated blocks' centres against every op's frustum, one op per
-        // lane; the per-block tests below run only for the ops the box may touch (heap neighbours were mostly
-        // allocated together, by one frame's tile, so a wave's box is small)
-        uint32_t wops = 0;
-#ifndef BF_COMPACTIFY_NO_PRECULL
-        {
-            int b0x = alloc ? bp.x : INT_MAX, b0y = alloc ? bp.y : INT_MAX, b0z = alloc ? bp.z : INT_MAX;
-            int b1x = alloc ? bp.x : INT_MIN, b1y = alloc ? bp.y : INT_MIN, b1z = alloc ? bp.z : INT_MIN;
-            for (int off = 32; off > 0; off >>= 1) {
-                b0x = min(b0x, __shfl_xor(b0x, off)); b0y = min(b0y, __shfl_xor(b0y, off)); b0z = min(b0z, __shfl_xor(b0z, off));
-                b1x = max(b1x, __shfl_xor(b1x, off)); b1y = max(b1y, __shfl_xor(b1y, off)); b1z = max(b1z, __shfl_xor(b1z, off));
-            }
-            if (b0x != INT_MAX) {
-                const f3 half = mk3(1.0f, 1.0f, 1.0f) * (A.voxelSize * 0.5f * (BF_SDF_BLOCK_SIZE - 1.0f));
-                const f3 lo = block_to_world(b0x, b0y, b0z, A.voxelSize) + half, hi = block_to_world(b1x, b1y, b1z, A.voxelSize) + half;
-                const bool maybe = lane < ops.n && box_may_touch_frustum(s_tinv[lane < ops.n ? lane : 0], cam, lo, hi);
-                wops = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)__ballot(maybe));
-            }
-        }
-#else
-        wops = ops.n >= 32 ? 0xFFFFFFFFu : (1u << ops.n) - 1u;
-#endif
-        const bool keepVis = alloc && ((wops >> (ops.n - 1)) & 1u) && block_in_frustum_fast(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
+        const bool keepVis = alloc && block_in_frustum_fast(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
         uint32_t fr = 0;  // ops whose frustum holds the block
-        if (alloc && wops) {
+        if (alloc) {
             const uint32_t bi = birth[i];
             // a block born in this batch at op j exists for ops j.. only (ops before it see no block)
             const uint32_t first = (bi >> 8) == epoch ? 255u - (bi & 255u) : 0u;
-            // k runs over the wave's ops in every lane (a wave-uniform loop keeps the op's pose in scalar loads)
-            for (uint32_t m = wops; m; m &= m - 1) {
-                const uint32_t k = (uint32_t)__builtin_ctz(m);
+            // k runs over every op in every lane (a wave-uniform loop keeps the op's pose in scalar loads)
+            for (uint32_t k = 0; k < ops.n; k++) {
                 const BFMat4 Ti = op_mat(ops.tinv[k]);
                 if (k >= first && block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize)) fr |= 1u << k;
             }
