@@ -569,3 +569,47 @@ def test_rccl_single_rank_exchange():
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
     comm.close()
+
+
+@pytest.mark.parametrize("K", [200, 600])
+def test_two_rank_sharded_solve_matches_single(K):
+    """The global solve as the multi-GPU loop runs it: two ranks (an in-process loopback group on one GPU, each
+    rank's solver on its own thread) build the normal-equation blocks of their own image pairs and sum them with
+    one all-reduce per GN iteration, then run the PCG replicated. Both ranks must end bit-identical to the
+    single-GPU solve: K = 200 takes the persistent PCG with one finisher workgroup, K = 600 the four-finisher
+    form (above 513 images), which the loop reaches past 5 130 frames."""
+    import threading
+    from bundlefusion_amd.dist import LoopbackComm
+    from bundlefusion_amd.solver import SolverBundling
+    prob = make_problem(K=K, stride=10, max_per_pair=25, outliers=0.02, drift=(0.05, 0.002), seed=5)
+    ref = gpu_solve(prob, 3, 150, [1, 1, 1], mode=bfa.abi.NORMAL_EQ_ASSEMBLED)
+    comms = LoopbackComm.group(2, timeout_ms=60000, capacity_bytes=64 << 20)
+    outs, errors = [None, None], []
+
+    def rank(r):
+        try:
+            S = SolverBundling(K, max(K * 4000, len(prob["corr"])), normal_equations=bfa.abi.NORMAL_EQ_ASSEMBLED)
+            S.set_shard(2, r, comms[r])
+            d_corr = bfa.DeviceArray.from_host(prob["corr"])
+            d_rot, d_trans = bfa.DeviceArray.from_host(prob["rot"]), bfa.DeviceArray.from_host(prob["trans"])
+            S.solve(d_corr, len(prob["corr"]), bfa.DeviceArray.from_host(prob["valid"]), K, 3, 150, [1, 1, 1],
+                    rot=d_rot, trans=d_trans)
+            res = S.result()
+            outs[r] = (d_rot.download(), d_trans.download(), d_corr.download(), res)
+            S.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    for c in comms:
+        c.close()
+    assert not errors, errors
+    for r in range(2):
+        assert outs[r][3]["error"] == 0, outs[r][3]
+        np.testing.assert_array_equal(outs[r][0], ref[0])
+        np.testing.assert_array_equal(outs[r][1], ref[1])
+        np.testing.assert_array_equal(outs[r][2]["i"] == INVALID, ref[2]["i"] == INVALID)

@@ -9,14 +9,15 @@ import time
 
 import numpy as np
 
+# before anything initialises HIP (as tests/conftest.py): one hardware queue per stream of every rank
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import bundlefusion_amd as bfa  # noqa: E402
 from bundlefusion_amd.abi import BFSceneOptions  # noqa: E402
 from bundlefusion_amd.dist import LoopbackComm  # noqa: E402
 from bundlefusion_amd.recon import Recon, recon_options  # noqa: E402
 from bundlefusion_amd.stream import SyntheticStream  # noqa: E402
-
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "24")
 
 
 def main():
