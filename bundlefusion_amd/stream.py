@@ -119,6 +119,7 @@ class SyntheticStream:
             self.local_n.append(len(c))
             off += len(c)
         allloc = np.concatenate(locs) if off else np.zeros(1, ENTRYJ_DTYPE)
+        self.local_host = allloc
         self.local_corr = DeviceArray.from_host(allloc)
         # global keyframe correspondences, ordered by max(i, j) as keyframes arrive
         kf = self.gt[::submap][: self.K]
@@ -138,16 +139,24 @@ class SyntheticStream:
         w, h, fx, fy, mx, my, n, cw, ch = self._cache_args
         return CUDACache(cache_options(w, h, fx, fy, mx, my, n, width=cw, height=ch))
 
-    def attach(self, recon, frames=None, cache_store=None):
+    def attach(self, recon, frames=None, cache_store=None, own_corr=False):
         """Register every frame, correspondence list and the initial pose with a Recon (cache_store: the loop's own
-        cache for cache_source "loop", default the stream's)."""
+        cache for cache_source "loop", default the stream's). own_corr: the loop gets its own device copies of the
+        correspondence lists — the solves invalidate entries in place (per-image cap, max-residual removal), so
+        loops that run side by side (the ranks of a multi-GPU job, each with its own copy on its GPU) must not
+        share them."""
         P4 = 4 * self.cam.imageWidth * self.cam.imageHeight
         for i in range(self.F if frames is None else frames):
             recon.set_frame(i, self.depth.ptr.value + P4 * i, self.color.ptr.value + P4 * i, self.cache[i], self.tinc[i])
+        local_corr, global_corr = self.local_corr, self.global_corr
+        if own_corr:
+            local_corr = DeviceArray.from_host(self.local_host)
+            global_corr = DeviceArray.from_host(self.global_host if len(self.global_host) else np.zeros(1, ENTRYJ_DTYPE))
+            recon._keep = getattr(recon, "_keep", []) + [local_corr, global_corr]  # alive as long as the loop
         for s in range(self.num_submaps):
             if self.local_n[s]:
-                recon.set_local_correspondences(s, self.local_corr.ptr.value + 32 * self.local_off[s], self.local_n[s])
-        recon.set_global_correspondences(self.global_corr.ptr.value, len(self.global_host), self.global_prefix)
+                recon.set_local_correspondences(s, local_corr.ptr.value + 32 * self.local_off[s], self.local_n[s])
+        recon.set_global_correspondences(global_corr.ptr.value, len(self.global_host), self.global_prefix)
         recon.set_initial_pose(self.gt[0])
         if self.raw_input:  # CUDAImageManager::process of every frame inside process_frame
             from .io import Preprocessor, preprocess_options

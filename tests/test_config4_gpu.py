@@ -76,7 +76,7 @@ def run():
         so = BFSceneOptions()
         so.shardCount, so.shardIndex, so.shardChunk = WORLD, r, CHUNK
         rc = Recon(params, st.cam, opts, so)
-        st.attach(rc, cache_store=caches[r])
+        st.attach(rc, cache_store=caches[r], own_corr=True)  # each rank's own lists, as on its own GPU
         loops.append(rc)
     comms = LoopbackComm.group(WORLD, timeout_ms=120000, capacity_bytes=128 << 20)  # pair stats: 83 MB at K = 2 001
     for rc, c in zip(loops, comms):

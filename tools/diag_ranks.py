@@ -37,7 +37,7 @@ def main():
         so = BFSceneOptions()
         so.shardCount, so.shardIndex, so.shardChunk = 2, r, 0.25
         rc = Recon(params, st.cam, opts, so)
-        st.attach(rc, cache_store=caches[r])
+        st.attach(rc, cache_store=caches[r], own_corr=True)
         loops.append(rc)
     comms = LoopbackComm.group(2, timeout_ms=60000, capacity_bytes=128 << 20)
     for rc, c in zip(loops, comms):
