@@ -355,35 +355,55 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
 }
 
 // block_may_update for the two z-halves of the block at once (bit h: half h, voxel z 4h..4h+3, may
-// hold an in-band voxel): the screen footprint and its depth bounds are the whole block's (a superset
-// of each half's pixels: still conservative), the depth range is each half's own, from the corners at
-// z offsets 0, 3 and 4, 7 (only the depth row of the transform for the inner two levels).
-__device__ __forceinline__ uint32_t block_may_update_halves(const HashArgs& A, const BFDepthCameraParams& cam, const BFMat4& Tinv, int bx,
-                                            int by, int bz, const float2* __restrict__ tiles,
-                                            const float2* __restrict__ tiles2) {
+// hold an in-band voxel), from per-op constants (cull_op_consts, 28 floats). The screen footprint and
+// its depth bounds are the whole block's (a superset of each half's pixels: still conservative); the
+// depth range is each half's own. The camera-space corner positions are affine in the corner
+// offsets, so the block's corner voxel is transformed once (fma, the focal lengths folded into the
+// x / y rows) and the other corners are that point plus sums of the three scaled columns; each
+// half's depth range is the corner point's depth plus per-op minima / maxima of the column terms.
+// Float differences against the per-corner transforms are ~1e-6 relative, far inside the one-pixel
+// growth and the 1 mm slack. Against eight full corner transforms plus eight depth rows per (block,
+// op) pair: k_compactify_ops 57.3 -> 48.8 us per batch (profiles/r11_scan_ab.txt).
+constexpr int CULL_CONSTS = 28;
+// q: [0..11] rows fx r0, fy r1, r2 of Tinv; [12..20] columns 0, 1, 2 of those rows times 7 voxels;
+// [21..24] half 0 depth offset min / max, half 1 min / max (over the xy corners and its z levels)
+__host__ __device__ __forceinline__ void cull_op_consts(const float* t, const BFDepthCameraParams& cam, float voxelSize, float* q) {
+    const float ext = voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
+    for (int c = 0; c < 4; c++) {
+        q[c] = cam.fx * t[c];
+        q[4 + c] = cam.fy * t[4 + c];
+        q[8 + c] = t[8 + c];
+    }
+    for (int c = 0; c < 3; c++)
+        for (int r = 0; r < 3; r++) q[12 + 3 * c + r] = ext * q[4 * r + c];
+    const float ab0 = fminf(0.0f, q[14]) + fminf(0.0f, q[17]), ab1 = fmaxf(0.0f, q[14]) + fmaxf(0.0f, q[17]);
+    const float z3 = voxelSize * 3.0f * t[10], z4 = voxelSize * 4.0f * t[10], z7 = voxelSize * 7.0f * t[10];
+    q[21] = ab0 + fminf(0.0f, z3);
+    q[22] = ab1 + fmaxf(0.0f, z3);
+    q[23] = ab0 + fminf(z4, z7);
+    q[24] = ab1 + fmaxf(z4, z7);
+    q[25] = q[26] = q[27] = 0.0f;
+}
+__device__ __forceinline__ uint32_t block_may_update_halves_q(const HashArgs& A, const BFDepthCameraParams& cam, const float* __restrict__ q,
+                                                              int bx, int by, int bz, const float2* __restrict__ tiles,
+                                                              const float2* __restrict__ tiles2) {
     const f3 c0 = block_to_world(bx, by, bz, A.voxelSize);
-    const float ext = A.voxelSize * (float)(BF_SDF_BLOCK_SIZE - 1);
-    float zlo[2] = {INFINITY, INFINITY}, zhi[2] = {-INFINITY, -INFINITY};
+    const float p0x = __builtin_fmaf(q[0], c0.x, __builtin_fmaf(q[1], c0.y, __builtin_fmaf(q[2], c0.z, q[3])));
+    const float p0y = __builtin_fmaf(q[4], c0.x, __builtin_fmaf(q[5], c0.y, __builtin_fmaf(q[6], c0.z, q[7])));
+    const float p0z = __builtin_fmaf(q[8], c0.x, __builtin_fmaf(q[9], c0.y, __builtin_fmaf(q[10], c0.z, q[11])));
+    const float zlo[2] = {p0z + q[21], p0z + q[23]}, zhi[2] = {p0z + q[22], p0z + q[24]};
+    if (!(fminf(zlo[0], zlo[1]) > 1e-3f)) return 3u;  // reaches the camera plane: keep
     float xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, (k & 4) ? ext : 0.0f);
-        const f3 p = xform(Tinv, w);
-        if (!(p.z > 1e-3f)) return 3u;  // straddles the camera plane: keep
-        const float rz = __builtin_amdgcn_rcpf(p.z);
-        const float sx = p.x * cam.fx * rz + cam.mx, sy = p.y * cam.fy * rz + cam.my;
-        const int hh = (k & 4) ? 1 : 0;
-        zlo[hh] = fminf(zlo[hh], p.z); zhi[hh] = fmaxf(zhi[hh], p.z);
+        float px = p0x, py = p0y, pz = p0z;
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            if ((k >> c) & 1) { px += q[12 + 3 * c]; py += q[13 + 3 * c]; pz += q[14 + 3 * c]; }
+        const float rz = __builtin_amdgcn_rcpf(pz);
+        const float sx = __builtin_fmaf(px, rz, cam.mx), sy = __builtin_fmaf(py, rz, cam.my);
         xlo = fminf(xlo, sx); xhi = fmaxf(xhi, sx);
         ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) {  // the inner levels: z offset 3 (half 0) and 4 (half 1)
-        const int hh = (k & 4) ? 1 : 0;
-        const f3 w = c0 + mk3((k & 1) ? ext : 0.0f, (k & 2) ? ext : 0.0f, A.voxelSize * (float)(3 + hh));
-        const float pz = ((Tinv.m[8] * w.x + Tinv.m[9] * w.y) + Tinv.m[10] * w.z) + Tinv.m[11];
-        if (!(pz > 1e-3f)) return 3u;
-        zlo[hh] = fminf(zlo[hh], pz); zhi[hh] = fmaxf(zhi[hh], pz);
     }
     const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
     const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
@@ -1250,6 +1270,11 @@ constexpr int kApplyRounds = 4;
 #ifndef BF_APPLY_WPE
 #define BF_APPLY_WPE 8
 #endif
+// k_compactify_ops: workgroups per CU, its occupancy (5: <= 96 VGPRs; 4 / 6 measured 49.0 / 47.1 us
+// against 44.7, profiles/r11_scan_ab.txt)
+#ifndef BF_SCAN_WPC
+#define BF_SCAN_WPC 5
+#endif
 // work-list op mask of a block: which ops may update each z-half (x: voxel z 0..3, y: 4..7)
 typedef uint2 OpMask;
 constexpr int MASK_PARTS = 2;
@@ -1295,7 +1320,7 @@ __global__ __launch_bounds__(256) void k_begin_ops_tiles(uint32_t* ctrl, unsigne
 // One scan of the allocated pool for the whole batch: `visible` = frustum list of the last op (the
 // list garbageCollect walks), work list = blocks some op may update, with the op bit mask. Also
 // releases the batch's alloc dedup-set slots.
-__global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF_SCAN_WPC))) void k_compactify_ops(HashArgs A, BFDepthCameraParams cam, OpTable ops, uint32_t candCap,
                                                         const int* __restrict__ candSlot, unsigned long long* candSet,
                                                         OpMask* masks, const uint32_t* __restrict__ birth, uint32_t epoch,
                                                         uint32_t binCap) {
@@ -1321,19 +1346,23 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         s_tiles[1][threadIdx.x] = ops.tiles2[threadIdx.x];
     }
     __syncthreads();
+    __shared__ float4 s_cull[Scene::kMaxOps][CULL_CONSTS / 4];
+    if (threadIdx.x < ops.n) cull_op_consts(s_tinv[threadIdx.x], cam, A.voxelSize, reinterpret_cast<float*>(s_cull[threadIdx.x]));
+    __syncthreads();
     const uint32_t hw = A.ctrl[C_HIGHWATER];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    const BFMat4 TinvLast = op_mat(ops.tinv[ops.n - 1]);
     unsigned long long scanned = 0, vis = 0, band = 0, evals = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < hw; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         int4 bp = make_int4(0, 0, 0, 0);
-        if (i < hw) bp = A.blockPos[i];
+        uint32_t bi = 0;
+        if (i < hw) {  // both loads issued together (the birth load waited for the position before)
+            bp = A.blockPos[i];
+            bi = birth[i];
+        }
         const bool alloc = bp.w != 0;
-        const bool keepVis = alloc && block_in_frustum_fast(cam, TinvLast, bp.x, bp.y, bp.z, A.voxelSize);
         uint32_t fr = 0;  // ops whose frustum holds the block
         if (alloc) {
-            const uint32_t bi = birth[i];
             // a block born in this batch at op j exists for ops j.. only (ops before it see no block)
             const uint32_t first = (bi >> 8) == epoch ? 255u - (bi & 255u) : 0u;
             // k runs over every op in every lane (a wave-uniform loop keeps the op's pose in scalar loads)
@@ -1342,6 +1371,8 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
                 if (k >= first && block_in_frustum_fast(cam, Ti, bp.x, bp.y, bp.z, A.voxelSize)) fr |= 1u << k;
             }
         }
+        // the GC's list: the last op's frustum (a block born in the batch exists for the last op)
+        const bool keepVis = (fr >> (ops.n - 1)) & 1u;
         // queue the wave's (block, op) pairs, then every lane takes one pair per round for the band cull
         s_bp[threadIdx.x] = bp;
 #pragma unroll
@@ -1358,13 +1389,15 @@ __global__ __launch_bounds__(256) void k_compactify_ops(HashArgs A, BFDepthCamer
         for (uint32_t r = lane; r < qtot; r += 64) {
             const uint32_t e = s_q[wv][r], src = wv * 64 + (e >> 5), k = e & 31u;
             const int4 b = s_bp[src];
-            const BFMat4 Ti = op_mat(s_tinv[k]);
             // the voxel pass applies an op to a block half by half (4 z-slices per round)
 #if defined(BF_CULL_DIAG_NOBAND)  // timing diagnostic only (wrong masks): the scan without the band cull
             const uint32_t hb = 3u;
-            (void)Ti; (void)b;
+            (void)b;
 #else
-            const uint32_t hb = block_may_update_halves(A, cam, Ti, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
+            float cq[CULL_CONSTS];
+#pragma unroll
+            for (int c = 0; c < CULL_CONSTS / 4; c++) reinterpret_cast<float4*>(cq)[c] = s_cull[k][c];
+            const uint32_t hb = block_may_update_halves_q(A, cam, cq, b.x, b.y, b.z, s_tiles[0][k], s_tiles[1][k]);
 #endif
 #pragma unroll
             for (int q = 0; q < MASK_PARTS; q++)
@@ -1952,7 +1985,7 @@ Scene::Scene(const SceneConfig& cfg, hipStream_t stream) : cfg_(cfg), stream_(st
     for (int sh = 0; sh < 16; sh++)
         if (run == (1u << sh)) applyXcdShift_ = sh;
     // the batch scan: 4 workgroups per CU (its occupancy; 5-6 per CU and 2-3 resident rounds measured no faster)
-    compactifyGrid_ = (unsigned)numCUs_ * 4u;
+    compactifyGrid_ = (unsigned)numCUs_ * (unsigned)BF_SCAN_WPC;
     integrateGrid_[0] = (unsigned)std::max(1, occ0) * (unsigned)numCUs_;
     integrateGrid_[1] = (unsigned)std::max(1, occ1) * (unsigned)numCUs_;
     BF_HIP(hipMemsetAsync(candSet_.p, 0xFF, candSet_.bytes(), stream_));
