@@ -1270,6 +1270,11 @@ constexpr int kApplyRounds = 4;
 #ifndef BF_APPLY_WPE
 #define BF_APPLY_WPE 8
 #endif
+// k_apply_ops: wave priority while a wave projects an op step's voxels and issues its gathers (0: off;
+// see apply_op_slices)
+#ifndef BF_APPLY_PRIO
+#define BF_APPLY_PRIO 1
+#endif
 // k_compactify_ops: workgroups per CU, its occupancy (5: <= 96 VGPRs; 4 / 6 measured 49.0 / 47.1 us
 // against 44.7, profiles/r11_scan_ab.txt)
 #ifndef BF_SCAN_WPC
@@ -1523,6 +1528,13 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
     for (int z0 = 0; z0 < ZR; z0 += ZC) {
         uint32_t pix[ZC], cc[ZC];
         float pz[ZC], d[ZC];
+#if BF_APPLY_PRIO
+        // the projection at a raised priority, back to normal once the step's gathers are issued: among the
+        // SIMD's waves, one that is about to issue loads goes first, so more gathers are in flight while the
+        // others run their updates (458 -> 441 us per launch; the raise over the whole kernel, above the
+        // bundling kernels' waves, or for the update phase instead measured slower, profiles/r11_prio_ab.txt)
+        __builtin_amdgcn_s_setprio(BF_APPLY_PRIO);
+#endif
 #pragma unroll
         for (int zi = 0; zi < ZC; zi += 2) {
             const f2v wz = f2v{(float)(bzh + z0 + zi), (float)(bzh + z0 + zi + 1)} * f2v{A.voxelSize, A.voxelSize};
@@ -1538,6 +1550,9 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
             d[zi] = __uint_as_float(v[0] ^ DC_DEPTH_KEY);
             cc[zi] = v[1];
         }
+#if BF_APPLY_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
 #ifdef BF_APPLY_DIAG
         {  // (slice pair, op) wave-slots with no lane in band, and all of them (counted on lane 0)
             unsigned long long b[ZC];
