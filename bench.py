@@ -458,6 +458,10 @@ def main():
     ap.add_argument("--app-params", default=None, help="with --sens: zParametersDefault.txt-style file (default: the "
                     "reference defaults at the north-star 640x480 / 4 mm, 2^23 buckets, 2^21 blocks)")
     ap.add_argument("--bundling-params", default=None, help="with --sens: zParametersBundlingDefault.txt-style file")
+    ap.add_argument("--apply-xcd-run", type=int, default=0,
+                    help="BFSceneOptions.applyXcdRun: work-list positions per XCD run of the voxel pass (0: the library's 64)")
+    ap.add_argument("--apply-rounds", type=int, default=0,
+                    help="BFSceneOptions.applyRounds: resident rounds of the voxel pass's grid (0: the library's 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-prefix-frames", type=int, default=PREFIX_FRAMES,
                     help="cpu_baseline: frames of the oracle loop prefix (SURVEY.md §8(d): 500)")
@@ -512,6 +516,7 @@ def main():
     so.shardCount, so.shardIndex, so.shardChunk = world, rank, args.shard_chunk
     if world == 1 and args.rehearse_shards > 1:
         so.shardCount, so.shardIndex = args.rehearse_shards, 0
+    so.applyXcdRun, so.applyRounds = args.apply_xcd_run, args.apply_rounds
     rc = Recon(params, stream.cam, opts, so)
     comm = None
     if world > 1 and os.environ.get("BF_BA_SHARD", "1") != "0":
@@ -692,7 +697,9 @@ def main():
                    "parallelism": (f"tsdf-chunk-shard{world}+ba-pair-shard{world}-rccl" if comm is not None
                                    else f"tsdf-chunk-shard{world}+ba-replicated") if world > 1 else
                                   (f"rehearsal: rank 0 of tsdf-chunk-shard{args.rehearse_shards}, ba-replicated"
-                                   if args.rehearse_shards > 1 else "single")},
+                                   if args.rehearse_shards > 1 else "single"),
+                   **({"apply_xcd_run": args.apply_xcd_run} if args.apply_xcd_run else {}),
+                   **({"apply_rounds": args.apply_rounds} if args.apply_rounds else {})},
         "stream": {"frames_per_s_whole_stream": frames_total / (t_fill + dt), "fill_s": t_fill, "timed_s": dt,
                    "fill_frames_per_s": fill / t_fill if fill else None,
                    "fill_global_gn_iters": fill_stats["globalGnIterations"],
