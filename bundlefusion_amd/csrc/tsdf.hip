@@ -1605,7 +1605,8 @@ __device__ __forceinline__ void apply_op_slices(bool deint, const HashArgs& A, c
 // VALU issue peak and 0.36 of HBM by the counters at the driver workload (458-461 us per launch), with the
 // waves' cycles 22 % issuing, 45.5 % waiting to issue (dependencies) and 32.5 % waiting on memory
 // (profiles/r10_apply_sq_pmc.txt): it is dependency / latency bound. Lane-derived values are re-read per
-// block instead of kept live (no spills), counters are scalar.
+// block instead of kept live (no spills), counters are scalar. The op steps' projections run at a raised
+// issue priority (apply_op_slices): 458 -> 441 us.
 template <int ZR, int ZC, int WPE, bool XCDRUNS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_ops(
     HashArgs A, BFDepthCameraParams cam, OpTable ops, const OpMask* __restrict__ masks, uint32_t binCap, int xcdShift) {
