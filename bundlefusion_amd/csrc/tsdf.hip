@@ -292,6 +292,13 @@ __global__ __launch_bounds__(256) void k_begin_op_tiles(uint32_t* ctrl, unsigned
                     tiles, tiles2);
 }
 
+// The screen rectangle of a block's corner projections, grown for the voxel pass's pixel rule: a voxel at
+// screen x takes column (int)(x + 0.5), truncated toward zero, so x in (-1.5, -0.5] lands in column 0. The
+// rectangle [floor(lo - 0.5), floor(hi + RECT_HI)] holds every column a voxel can take; at the left / top edge
+// the bound is that truncation itself (hi just above -1.5 keeps column 0), so it carries 1/64 px for the
+// corner projections' rounding (~1e-4 px): without it a corner computed 7.5e-5 px past -1.5 dropped a half
+// whose corner voxel lands in row 0 (test_app_gpu's end phase, one weight off).
+constexpr float RECT_HI = 1.5f + 0x1p-6f;
 // Conservative test that a block may contain a voxel integrate will update: project the 8 voxel-
 // centre corners (convex hull -> bounding pixel rectangle, grown by one pixel), take the depth
 // bounds of the covered tiles and reject when every depth is too far behind or in front of the
@@ -320,7 +327,7 @@ __device__ bool block_may_update(const HashArgs& A, const BFDepthCameraParams& c
         ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
     }
     const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
-    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
+    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + RECT_HI), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + RECT_HI);
     if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) return false;  // every voxel off-screen
     const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
     const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);
@@ -406,7 +413,7 @@ __device__ __forceinline__ uint32_t block_may_update_halves_q(const HashArgs& A,
         ylo = fminf(ylo, sy); yhi = fmaxf(yhi, sy);
     }
     const float W = (float)cam.imageWidth, H = (float)cam.imageHeight;
-    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + 1.5f), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + 1.5f);
+    const float fx0 = floorf(xlo - 0.5f), fx1 = floorf(xhi + RECT_HI), fy0 = floorf(ylo - 0.5f), fy1 = floorf(yhi + RECT_HI);
     if (fx1 < 0.0f || fy1 < 0.0f || fx0 > W - 1.0f || fy0 > H - 1.0f) return 0u;  // every voxel off-screen
     const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, W - 1.0f);
     const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, H - 1.0f);

@@ -53,7 +53,10 @@ def compare_states(params, gpu: bfa.SceneRepHashSDF, ora: OracleScene, check_vox
         bad_sdf = np.nonzero(gv["sdf"].view(np.uint32) != ov["sdf"].view(np.uint32))[0]
         bad_w = np.nonzero(gv["weight"] != ov["weight"])[0]
         bad_c = np.nonzero(np.any(gv["color"] != ov["color"], axis=1))[0]
-        assert len(bad_w) == 0, f"{len(bad_w)} weights differ"
+        if len(bad_w):
+            det = [(keys[i // 512], int(i % 512), float(gv["weight"][i]), float(ov["weight"][i]), float(gv["sdf"][i]),
+                    float(ov["sdf"][i])) for i in bad_w[:8]]
+            raise AssertionError(f"{len(bad_w)} weights differ; (block, voxel, gpu w, oracle w, gpu sdf, oracle sdf): {det}")
         assert len(bad_c) == 0, f"{len(bad_c)} colours differ"
         assert len(bad_sdf) == 0, (f"{len(bad_sdf)} sdf differ, max |d| = "
                                    f"{np.max(np.abs(gv['sdf'][bad_sdf] - ov['sdf'][bad_sdf]))}")
