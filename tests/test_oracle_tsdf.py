@@ -297,3 +297,35 @@ def test_oracle_shards_partition_the_scene():
     assert set(union) == set(fb) and len(fb) > 200
     for k, ptr in fb.items():
         assert block_voxels(fv, ptr).tobytes() == union[k].tobytes(), k
+
+
+def test_band_cull_rectangle_covers_truncated_pixels():
+    """csrc/tsdf.hip RECT_HI: the band cull's screen rectangle [floor(lo - 0.5), floor(hi + 1.5 + 1/64)] must hold
+    every column the voxel pass (and integrateDepthMapKernel, CUDASceneRepHashSDF.cu:453-457) gives a voxel whose
+    projection lies within the corners' range, with the pixel taken as (int)(x + 0.5), truncated toward zero (so
+    x in (-1.5, -0.5] is column 0), while the corner projections themselves carry rounding of ~1e-4 px. Without the
+    1/64 the left / top edge has no margin: a corner computed 7.5e-5 px below -1.5 dropped column 0 (the round-6
+    end-phase failure, profiles/r11_cull_margin_fix.txt)."""
+    f32 = np.float32
+    rect_hi = f32(1.5) + f32(2.0 ** -6)
+    rng = np.random.default_rng(3)
+    W = 640
+    # corner ranges around both edges; the true voxel projection may exceed the computed hi by the rounding
+    lo = np.concatenate([rng.uniform(-30, 2, 20000), rng.uniform(W - 30, W + 2, 20000)]).astype(f32)
+    hi = (lo + rng.uniform(0, 25, lo.size)).astype(f32)
+    hi[:5000] = f32(-1.5) - rng.uniform(0, 1e-4, 5000).astype(f32)  # the failing case's neighbourhood
+    lo[:5000] = np.minimum(lo[:5000], hi[:5000] - f32(3))
+    err = f32(1e-4)
+    for x in (hi + err, lo - err, (lo + hi) / 2):  # projections of voxels at the extremes / inside
+        x = x.astype(f32)
+        col = np.trunc(x + f32(0.5)).astype(np.int64)  # C float -> int conversion
+        on = (col >= 0) & (col < W)
+        c0 = np.floor(lo - f32(0.5)).astype(np.int64)
+        c1 = np.floor(hi + rect_hi).astype(np.int64)
+        # the cull rejects when c1 < 0 or c0 > W - 1, else it reads columns [max(c0, 0), min(c1, W - 1)]
+        kept = ~((c1 < 0) | (c0 > W - 1))
+        covered = kept & (np.maximum(c0, 0) <= col) & (col <= np.minimum(c1, W - 1))
+        assert np.all(covered[on]), np.nonzero(on & ~covered)[0][:5]
+    # and the old bound, hi + 1.5, misses the failing case
+    x = (f32(-1.5) - f32(7.5e-5) + f32(1e-4)).astype(f32)
+    assert int(np.trunc(x + f32(0.5))) == 0 and np.floor(f32(-1.5) - f32(7.5e-5) + f32(1.5)) < 0
