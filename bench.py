@@ -49,8 +49,9 @@ VALU_PEAK_WAVE_INSTS_PER_US = 256 * 4 * 2400 / 2
 
 
 # revision of k_apply_ops' memory behaviour: a PMC profile (profiles/apply_pass_pmc*.json) describes the
-# kernel only for the revision it recorded (2: z-halves no op reaches are not loaded)
-APPLY_PASS_REV = 2
+# kernel only for the revision it recorded (2: z-halves no op reaches are not loaded; 3: work-list entries
+# through scalar loads one block ahead, issue priority in the op steps)
+APPLY_PASS_REV = 3
 
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
