@@ -1398,6 +1398,9 @@ __global__ __launch_bounds__(WG) void k_pcg_pairs(BA a, float wSparse, int iter,
 // last-workgroup election and two reloads of every vector. Every wait is bounded (2 s of s_memrealtime):
 // a timeout sets result error bit 3 and releases every workgroup. The grid must be co-resident: the
 // host launches it only when the occupancy query admits it with room to spare.
+#ifndef BF_PCG_PRIO
+#define BF_PCG_PRIO 2  // k_pcg_persist's wave priority (0: off)
+#endif
 #ifndef BF_PCG_PERSISTENT
 #define BF_PCG_PERSISTENT 1  // 0: one k_pcg_pairs launch per PCG iteration (A/B builds)
 #endif
@@ -1842,6 +1845,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) void k_
     __shared__ double sD[WG / 64][DSTAT];          // each worker wave's image statistics
     if (a.ctrl[K_GN_DONE] || a.ctrl[K_PCG_DONE]) return;  // uniform over the grid (set by earlier launches)
     const uint32_t lane = lane_id();
+#if BF_PCG_PRIO
+    // above the voxel pass's waves on the same CU (its op steps run at 1): an iteration's critical path is
+    // this kernel's compute between hand-offs, and its waits sleep (s_sleep), so the raise costs the voxel
+    // pass little: in-loop time per PCG iteration 7.67 -> 6.43 us (1.46x -> 1.23x standalone), frame rate
+    // 1 576 -> 1 587 at the driver workload (profiles/r11_prio_ab.txt)
+    __builtin_amdgcn_s_setprio(BF_PCG_PRIO);
+#endif
     const int useDense = (int)a.ctrl[K_USE_DENSE];
     const unsigned long long t0 = rtc();
     uint32_t* flag = &a.sync[SYNC_FLAGR];
