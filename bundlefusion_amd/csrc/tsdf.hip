@@ -2258,7 +2258,11 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
 // CUDASceneRepHashSDF::garbageCollect (.h:110-126)
 void Scene::garbageCollect() {
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
-    k_gc<<<(unsigned)numCUs_ * 2, 256, 0, stream_>>>(A, gcList_.p, errMirror_);
+    // half a workgroup per CU: every workgroup ends with a fence and a same-address ticket atomic, whose
+    // serialisation made 2 per CU cost 21 us a pass against 13.6 at one per two CUs (15.2 at 1, 14.4 at 1/4;
+    // profiles/r11_gc_ab.txt); the visible-list walk itself is ~6.5 us
+    const unsigned gcGrid = std::max(1u, (unsigned)numCUs_ / 2u);
+    k_gc<<<gcGrid, 256, 0, stream_>>>(A, gcList_.p, errMirror_);
     BF_LAUNCH_CHECK();
 }
 
