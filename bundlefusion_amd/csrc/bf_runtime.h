@@ -106,19 +106,29 @@ public:
         head_ = (head_ + 1) % RING;
         pending_++;
     }
+    // sampled timing (period p): slotSampled() hands out the event pair for one launch in p (the events stamp
+    // the dispatch, which costs the stream a little time per launch) and counts every launch; totalMs() then
+    // scales the sampled time to all launches (their mean is the sampled mean) and launches() counts them all
+    void setPeriod(uint32_t p) { period_ = p ? p : 1u; }
+    bool slotSampled(hipEvent_t& a, hipEvent_t& b) {
+        const bool s = (calls_++ % period_) == 0;
+        if (s) slot(a, b);
+        return s;
+    }
     // drains every pending slot (synchronizes on the newest event)
     double totalMs() {
         while (pending_) harvest((head_ + RING - pending_) % RING);
-        return total_;
+        return (calls_ && n_) ? total_ * (double)calls_ / (double)n_ : total_;
     }
     uint64_t launches() {
         totalMs();
-        return n_;
+        return calls_ ? calls_ : n_;
     }
     void reset() {
         totalMs();
         total_ = 0.0;
         n_ = 0;
+        calls_ = 0;
     }
 
 private:
@@ -139,7 +149,8 @@ private:
     std::vector<hipEvent_t> a_, b_;
     size_t head_ = 0, pending_ = 0;
     double total_ = 0.0;
-    uint64_t n_ = 0;
+    uint64_t n_ = 0, calls_ = 0;
+    uint32_t period_ = 1;
     bool on_ = false;
 };
 

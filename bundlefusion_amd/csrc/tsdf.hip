@@ -2240,8 +2240,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
                                                                   reinterpret_cast<OpMask*>(blockMask_.p), blockBirth_.p, epoch, B_);
     BF_LAUNCH_CHECK();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    const bool timed = applyClock_.enabled();
-    if (timed) applyClock_.slot(ev0, ev1);
+    const bool timed = applyClock_.enabled() && applyClock_.slotSampled(ev0, ev1);
     if (applyGrid_ % 8u == 0u)  // workgroup i runs on XCD i mod 8
         hipExtLaunchKernelGGL(k_apply_ops<4, BF_APPLY_ZC, BF_APPLY_WPE, true>, dim3(applyGrid_), dim3(64), 0, stream_, ev0, ev1, 0, A,
                               cam, tab, reinterpret_cast<const OpMask*>(blockMask_.p), static_cast<const int4*>(band_.p), B_,
