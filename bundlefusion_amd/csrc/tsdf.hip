@@ -51,6 +51,9 @@ struct HashArgs {
     unsigned long long* stats;  // [STAT_SLOTS][16] counters, field order of BFTsdfStats
     uint32_t numBuckets, numEntries, numBlocks, maxList;
     float voxelSize, truncation, truncScale, maxIntegrationDistance, weightMax;
+    // RN(1 / x) of the launch-uniform divisors the alloc walk's setup divides by (div_by_uniform), or 0
+    // when x is outside [2^-20, 2^20] (the IEEE division runs); rFx / rFy are set per batch (camera)
+    float rVoxelSize, rFx, rFy;
     uint32_t shardCount, shardIndex;
     uint32_t allocForceDirect;
     float shardChunk;
@@ -474,6 +477,27 @@ __device__ __forceinline__ bool block_in_frustum_fast(const BFDepthCameraParams&
 
 // allocKernel, CUDASceneRepHashSDF.cu:165-251: per-pixel DDA over 8^3-block cells. Emits the
 // absent, in-frustum, owned blocks (deduplicated per tile in LDS) into `cand`.
+// a / b for a launch-uniform divisor b in [2^-20, 2^20] with rb = RN(1 / b) from the host: a * rb, then
+// two residual corrections. The first leaves a faithful quotient; the second, from a faithful quotient with
+// the correctly rounded reciprocal, rounds to nearest (Markstein's theorem) while the residuals are normal,
+// i.e. for 2^-100 <= |a| <= 2^100 or a = 0 — bit-identical to the IEEE division there (tools/check_uniform_div.c:
+// 8.6e9 cases). 5 VALU against ~11 for the division's scale / fmas / fixup sequence.
+__device__ __forceinline__ float div_by_uniform(float a, float b, float rb) {
+    const float q0 = a * rb;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), rb, q0);
+    return __builtin_fmaf(__builtin_fmaf(-b, q1, a), rb, q1);
+}
+// world_to_block (VoxelUtilHashSDF.h:283-299) of a point with the division by the voxel size through
+// div_by_uniform. Below 2^-100 a coordinate's quotient is off by ulps but stays below 2^-60 with the
+// point's sign, so f2i(p + sgn(p) 0.5) is 0 for it as for the IEEE quotient: only |w| > 2^100 (or no
+// usable reciprocal) needs the IEEE path, which the caller runs under a ballot.
+__device__ __forceinline__ i3 world_to_block_rcp(f3 w, float vs, float rvs) {
+    const f3 p = mk3(div_by_uniform(w.x, vs, rvs), div_by_uniform(w.y, vs, rvs), div_by_uniform(w.z, vs, rvs));
+    const f3 q = p + mk3((float)sgn(p.x), (float)sgn(p.y), (float)sgn(p.z)) * 0.5f;
+    i3 v;
+    v.x = f2i(q.x); v.y = f2i(q.y); v.z = f2i(q.z);
+    return vvox_to_block(v);
+}
 struct RayWalk {  // one pixel's DDA state (CUDASceneRepHashSDF.cu:196-230)
     i3 id, idBound;
     f3 tMax, tDelta, step;
@@ -496,11 +520,31 @@ __device__ __forceinline__ RayWalk ray_walk_setup(const HashArgs& A, const float
     r.tDelta = mk3(0, 0, 0);
     r.step = mk3(0, 0, 0);
     if (r.active) {
-        const f3 rayMin = xform(T, depth_to_camera(cam, x, y, minDepth));
-        const f3 rayMax = xform(T, depth_to_camera(cam, x, y, maxDepth));
+        // depth_to_camera's two divisions by fx / fy and world_to_block's six by the voxel size go through
+        // div_by_uniform (bit-identical in the ranges checked below; otherwise the IEEE form, per wave)
+        f3 rayMin, rayMax;
+        i3 idEnd;
+        if (A.rFx != 0.0f) {  // launch-uniform
+            const float cx = div_by_uniform((float)x - cam.mx, cam.fx, A.rFx), cy = div_by_uniform((float)y - cam.my, cam.fy, A.rFy);
+            rayMin = xform(T, mk3(minDepth * cx, minDepth * cy, minDepth));
+            rayMax = xform(T, mk3(maxDepth * cx, maxDepth * cy, maxDepth));
+        } else {
+            rayMin = xform(T, depth_to_camera(cam, x, y, minDepth));
+            rayMax = xform(T, depth_to_camera(cam, x, y, maxDepth));
+        }
+        r.id = world_to_block_rcp(rayMin, A.voxelSize, A.rVoxelSize);
+        idEnd = world_to_block_rcp(rayMax, A.voxelSize, A.rVoxelSize);
+        const float big = fmaxf(fmaxf(fmaxf(fabsf(rayMin.x), fabsf(rayMin.y)), fmaxf(fabsf(rayMin.z), fabsf(rayMax.x))),
+                                fmaxf(fabsf(rayMax.y), fabsf(rayMax.z)));
+        const bool exactNeeded = A.rVoxelSize == 0.0f || big > 0x1p100f;
+        if (__builtin_amdgcn_ballot_w64(exactNeeded)) {
+            asm volatile("" ::: "memory");
+            if (exactNeeded) {
+                r.id = world_to_block(rayMin, A.voxelSize);
+                idEnd = world_to_block(rayMax, A.voxelSize);
+            }
+        }
         const f3 rayDir = normalize3(rayMax - rayMin);
-        r.id = world_to_block(rayMin, A.voxelSize);
-        const i3 idEnd = world_to_block(rayMax, A.voxelSize);
         r.step = mk3((float)sgn(rayDir.x), (float)sgn(rayDir.y), (float)sgn(rayDir.z));
         const f3 bp = block_to_world(r.id.x + f2i(fmaxf(0.0f, fminf(r.step.x, 1.0f))), r.id.y + f2i(fmaxf(0.0f, fminf(r.step.y, 1.0f))),
                                      r.id.z + f2i(fmaxf(0.0f, fminf(r.step.z, 1.0f))), A.voxelSize) -
@@ -1905,6 +1949,17 @@ __device__ void gc_free_list_serial(const HashArgs& A, unsigned long long* listV
 }  // namespace
 
 // ------------------------------------------------------------------------------------
+// RN(1 / x) for the divisors div_by_uniform admits ([2^-20, 2^20]), else 0 (the kernels divide in IEEE)
+// (BF_ALLOC_UNIFORM_DIV=0 builds the IEEE-only walk setup, for A/B and for the fallback's parity)
+#ifndef BF_ALLOC_UNIFORM_DIV
+#define BF_ALLOC_UNIFORM_DIV 1
+#endif
+static float recip_or_zero(float x) { return (BF_ALLOC_UNIFORM_DIV && x >= 0x1p-20f && x <= 0x1p20f) ? 1.0f / x : 0.0f; }
+static void set_camera_recips(HashArgs& a, const BFDepthCameraParams& cam) {
+    const float rx = recip_or_zero(cam.fx), ry = recip_or_zero(cam.fy);
+    a.rFx = (rx != 0.0f && ry != 0.0f) ? rx : 0.0f;
+    a.rFy = (rx != 0.0f && ry != 0.0f) ? ry : 0.0f;
+}
 static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* heap, BFVoxel* vox, int4* bp, uint32_t* bc,
                           int4* vis, uint32_t* ctrl, unsigned long long* st, const uint32_t* bitMask) {
     HashArgs a;
@@ -1915,6 +1970,8 @@ static HashArgs make_args(const SceneConfig& cfg, BFHashEntry* hash, uint32_t* h
     a.numBlocks = cfg.hp.numSDFBlocks;
     a.maxList = cfg.hp.hashMaxCollisionLinkedListSize;
     a.voxelSize = cfg.hp.virtualVoxelSize;
+    a.rVoxelSize = recip_or_zero(cfg.hp.virtualVoxelSize);
+    a.rFx = a.rFy = 0.0f;  // per batch: set_camera_recips
     a.truncation = cfg.hp.truncation;
     a.truncScale = cfg.hp.truncScale;
     a.maxIntegrationDistance = cfg.hp.maxIntegrationDistance;
@@ -2095,6 +2152,7 @@ void Scene::beginOp() {
 
 void Scene::alloc(const float* depth, const BFDepthCameraParams& cam, const uint32_t* bitMask) {
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, bitMask);
+    set_camera_recips(A, cam);
     dim3 g(div_up(cam.imageWidth, ALLOC_TILE), div_up(cam.imageHeight, ALLOC_TILE));
     k_alloc_collect<<<g, 256, 0, stream_>>>(A, depth, cam, T_, Tinv_, cand_.p, cfg_.candCapacity);
     hostPixels_ += (uint64_t)cam.imageWidth * cam.imageHeight;
@@ -2215,6 +2273,7 @@ void Scene::applyOps(const VoxelOp* ops, uint32_t n, const BFDepthCameraParams& 
         ctrl_.p, stats_.p, tab, cam.imageWidth, cam.imageHeight, tw, th, tw2, th2, cfg_.hp.maxIntegrationDistance, tileBlocks);
     BF_LAUNCH_CHECK();
     HashArgs A = make_args(cfg_, hash_.p, heap_.p, voxels_.p, blockPos_.p, blockCount_.p, visible_.p, ctrl_.p, stats_.p, nullptr);
+    set_camera_recips(A, cam);
     if (++batchEpoch_ >= (1u << 24)) {  // birth stamps are epoch << 8: restart the epochs before they wrap
         BF_HIP(hipMemsetAsync(blockBirth_.p, 0, blockBirth_.bytes(), stream_));
         batchEpoch_ = 1;

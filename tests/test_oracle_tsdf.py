@@ -329,3 +329,20 @@ def test_band_cull_rectangle_covers_truncated_pixels():
     # and the old bound, hi + 1.5, misses the failing case
     x = (f32(-1.5) - f32(7.5e-5) + f32(1e-4)).astype(f32)
     assert int(np.trunc(x + f32(0.5))) == 0 and np.floor(f32(-1.5) - f32(7.5e-5) + f32(1.5)) < 0
+
+
+def test_uniform_divisor_division_is_exact(tmp_path):
+    """csrc/tsdf.hip div_by_uniform (the alloc walk's divisions by fx, fy and the voxel size): a * RN(1/b) plus
+    two fma residual corrections equals the IEEE quotient a / b for b in [2^-20, 2^20] and 2^-100 <= |a| <= 2^100,
+    and stays a tiny number of a's sign below that. tools/check_uniform_div.c, reduced sample (2^13 numerators per
+    divisor, 4 113 divisors; the full 2^21 run is the 8.6e9-case sweep DESIGN.md cites)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = os.path.join(os.path.dirname(__file__), "..", "tools", "check_uniform_div.c")
+    exe = str(tmp_path / "check_uniform_div")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", src, "-lm", "-o", exe], check=True)
+    out = subprocess.run([exe, "13"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:]
+    assert " 0 disagreements" in out.stdout
